@@ -1,0 +1,59 @@
+"""ctypes loader for the CPU oracle (oracle/_build/liboracle.so).
+
+Test infrastructure only: used by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product path.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.oracle_rewrite_mem.restype = ctypes.c_int
+        lib.oracle_rewrite_mem.argtypes = [
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+            ctypes.POINTER(ctypes.c_char_p), ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
+        lib.oracle_mix_seed.restype = ctypes.c_uint32
+        lib.oracle_mix_seed.argtypes = [ctypes.c_uint32]
+        lib.oracle_warn_count.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def rewrite(pcap: bytes, args, cache: bytes = None, want_status=False):
+    """Run the oracle over an in-memory pcap.  Returns (rc, output_bytes[, status])."""
+    lib = load()
+    argv = (ctypes.c_char_p * max(1, len(args)))(*[a.encode() for a in args])
+    # worst-case growth: +4 B per record (VLAN add) or fixlen pad up to len
+    cap = len(pcap) * 2 + 1024 + 262144
+    out = ctypes.create_string_buffer(cap)
+    out_len = ctypes.c_size_t(0)
+    err = ctypes.create_string_buffer(1024)
+    inbuf = ctypes.create_string_buffer(pcap, len(pcap))
+    cbuf = ctypes.create_string_buffer(cache, len(cache)) if cache else None
+    npk = max(1, len(pcap) // 16)
+    status = np.zeros(npk, dtype=np.int8)
+    rc = lib.oracle_rewrite_mem(inbuf, len(pcap), cbuf, len(cache) if cache else 0, len(args), argv, out, cap,
+                                ctypes.byref(out_len), status.ctypes.data, npk, err, 1024)
+    data = out.raw[:out_len.value]
+    if rc == -2:
+        raise ValueError("oracle rejected input/options: " + err.value.decode(errors="replace"))
+    if want_status:
+        return rc, data, status
+    return rc, data
+
+
+def mix_seed(seed: int) -> int:
+    return load().oracle_mix_seed(seed)
