@@ -1,0 +1,149 @@
+/*
+ * tcpedit.h -- C-ABI of the MI355X-native libtcpedit (libtcpedit_hip.so).
+ *
+ * Drop-in for the reference's public tcpedit interface (appneta/tcpreplay
+ * 4.5.5, src/tcpedit/tcpedit.h:38-55, parse_args.h, tcpedit_api.h:32-58):
+ * the same entry points, argument meaning and return codes
+ * (TCPEDIT_ERROR -1, TCPEDIT_SOFT_ERROR -2, TCPEDIT_OK 0, TCPEDIT_WARN 1,
+ * tcpedit_types.h:31-34), plus
+ *   - an option surface that replaces the AutoOpts globals tcpedit_post_args()
+ *     reads (tcpedit_set_option / tcpedit_parse_args), and
+ *   - a batch entry point (tcpedit_batch_*) that stages a whole pcap image in
+ *     HBM and runs the per-packet edit for every record on the GPU in one pass.
+ *
+ * Every edit runs in the gfx950 kernels: tcpedit_packet() itself launches the
+ * same kernel on a one-record batch.  There is no CPU edit path.
+ */
+#ifndef TCPEDIT_HIP_H
+#define TCPEDIT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <sys/time.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCPEDIT_SOFT_ERROR -2
+#define TCPEDIT_ERROR -1
+#define TCPEDIT_OK 0
+#define TCPEDIT_WARN 1
+
+#ifndef PCAP_ERRBUF_SIZE
+/* libpcap's record header (pcap/pcap.h); layout-identical when pcap.h is absent */
+struct pcap_pkthdr {
+    struct timeval ts;
+    uint32_t caplen;
+    uint32_t len;
+};
+#endif
+
+#ifndef TCPR_DIR_T_DEFINED
+#define TCPR_DIR_T_DEFINED
+/* src/common/cache.h:76-82 */
+typedef enum tcpr_dir_e { TCPR_DIR_ERROR = -1, TCPR_DIR_NOSEND = 0, TCPR_DIR_C2S = 1, TCPR_DIR_S2C = 2 } tcpr_dir_t;
+#endif
+
+/* tcpedit_types.h:47 */
+typedef enum { BEFORE_PROCESS, AFTER_PROCESS } tcpedit_coder;
+
+typedef struct tcpedit_s tcpedit_t;
+
+/* ---- reference interface: tcpedit.h:38-55 ---------------------------------- */
+int tcpedit_init(tcpedit_t **tcpedit, int dlt);                       /* tcpedit.c:371-403 */
+char *tcpedit_geterr(tcpedit_t *tcpedit);                              /* tcpedit.c:440-445 */
+char *tcpedit_getwarn(tcpedit_t *tcpedit);                             /* tcpedit.c:482-488 */
+int tcpedit_checkerror(tcpedit_t *tcpedit, int rcode, const char *prefix); /* tcpedit.c:516-544 */
+int tcpedit_validate(tcpedit_t *tcpedit);                              /* tcpedit.c:424-434 */
+/* tcpedit.c:46-366 -- edits *pktdata in place (caller's buffer >= MAXPACKET) */
+int tcpedit_packet(tcpedit_t *tcpedit, struct pcap_pkthdr **pkthdr, unsigned char **pktdata, tcpr_dir_t direction);
+int tcpedit_close(tcpedit_t **tcpedit);                                /* tcpedit.c:551-622 */
+int tcpedit_get_output_dlt(tcpedit_t *tcpedit);                        /* tcpedit.c:408-413 */
+const unsigned char *tcpedit_l3data(tcpedit_t *tcpedit, tcpedit_coder code, unsigned char *packet, int pktlen); /* :627 */
+int tcpedit_l3proto(tcpedit_t *tcpedit, tcpedit_coder code, const unsigned char *packet, int pktlen); /* :642 */
+uint64_t tcpedit_get_total_bytes(tcpedit_t *tcpedit);  /* declared tcpedit.h:54-55, never defined there */
+uint64_t tcpedit_get_pkts_edited(tcpedit_t *tcpedit);
+
+/* ---- parse_args.h: derive the per-run tables from the option surface ----- */
+int tcpedit_post_args(tcpedit_t *tcpedit);                             /* parse_args.c:34-254 */
+
+/* ---- option surface (stands in for AutoOpts HAVE_OPT/OPT_ARG, Appendix C) --
+ * name: long option name without dashes ("seed", "enet-vlan", ...), value: the
+ * argument or NULL for flags.  Stacked options (pnat, portmap, enet-subsmac)
+ * accumulate.  Returns 0, or -1 for an unknown/duplicate option. */
+int tcpedit_set_option(tcpedit_t *tcpedit, const char *name, const char *value);
+/* Parses tcpedit/DLT options in argv (long and short forms); arguments it does
+ * not know are left for the caller: their indices are written to unused[] (if
+ * non-NULL) and counted in the return value (>= 0), or -1 on a parse error. */
+int tcpedit_parse_args(tcpedit_t *tcpedit, int argc, char **argv, int *unused);
+
+/* ---- programmatic setters: tcpedit_api.h:32-58 --------------------------- */
+int tcpedit_set_skip_broadcast(tcpedit_t *, int);
+int tcpedit_set_fixcsum(tcpedit_t *, int);
+int tcpedit_set_fixhdrlen(tcpedit_t *, int);
+int tcpedit_set_efcs(tcpedit_t *, int);
+int tcpedit_set_ttl_mode(tcpedit_t *, int);   /* 0 off, 1 set, 2 add, 3 sub */
+int tcpedit_set_ttl_value(tcpedit_t *, uint8_t);
+int tcpedit_set_tos(tcpedit_t *, uint8_t);
+int tcpedit_set_tclass(tcpedit_t *, uint8_t);
+int tcpedit_set_flowlabel(tcpedit_t *, uint32_t);
+int tcpedit_set_seed(tcpedit_t *);            /* tcpedit_api.c:210: seed = random() */
+int tcpedit_set_mtu(tcpedit_t *, int);
+int tcpedit_set_mtu_truncate(tcpedit_t *, int);
+int tcpedit_set_maxpacket(tcpedit_t *, int);
+int tcpedit_set_fixlen(tcpedit_t *, int);     /* 0 off, 1 pad, 2 trunc, 3 del */
+int tcpedit_set_tcp_sequence(tcpedit_t *, uint32_t);
+int tcpedit_set_cidrmap_s2c(tcpedit_t *, char *);
+int tcpedit_set_cidrmap_c2s(tcpedit_t *, char *);
+int tcpedit_set_srcip_map(tcpedit_t *, char *);
+int tcpedit_set_dstip_map(tcpedit_t *, char *);
+int tcpedit_set_port_map(tcpedit_t *, char *);
+
+/* ---- batch entry point: a whole pcap image on the GPU ---------------------
+ * tcpedit_batch_open copies `pcap` (a complete classic pcap file image,
+ * either byte order, us or ns magic) to HBM, builds the record index and the
+ * tiles, and uploads `cache` (a tcpprep cache file image, or NULL) for the
+ * per-record direction.  pkt_base = 0-based number of the image's first record
+ * in the cache (non-zero for a shard of a larger file).  The output of a run
+ * stays in HBM until fetched.  For a shard the image may be a record range with
+ * a copied 24-byte file header in front. */
+typedef struct tcpedit_batch_s tcpedit_batch_t;
+
+typedef struct {
+    uint64_t packets, bytes_in, bytes_out, written, edited, soft_errors, warnings, errors, unsupported;
+    uint64_t out_len;         /* bytes of the output pcap image (header + written records) */
+    int64_t first_error;      /* 0-based record index of the first TCPEDIT_ERROR, or -1 */
+    int64_t first_unsupported;/* 0-based record index of the first unsupported record, or -1 */
+    uint32_t n_tiles;
+    double kernel_ms;         /* device time of the last run (hipEvent) */
+} tcpedit_batch_result_t;
+
+tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *tcpedit, const void *pcap, size_t len, const void *cache,
+                                    size_t cache_len, uint64_t pkt_base);
+int tcpedit_batch_run(tcpedit_t *tcpedit, tcpedit_batch_t *b);     /* TCPEDIT_OK / TCPEDIT_ERROR */
+int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r);
+size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap); /* D2H, returns bytes */
+const uint8_t *tcpedit_batch_status(tcpedit_batch_t *b);           /* per-record TE_ST_* bytes */
+/* times `iters` back-to-back device runs with hipEvents on the run's stream */
+int tcpedit_batch_time(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run);
+void tcpedit_batch_close(tcpedit_batch_t *b);
+/* device pointers, for callers that keep the data in HBM (e.g. a sender) */
+const void *tcpedit_batch_device_output(tcpedit_batch_t *b);
+uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b);
+
+/* Convenience: H2D + run + D2H of a whole pcap image.  *out is malloc'd. */
+int tcpedit_rewrite_pcap(tcpedit_t *tcpedit, const void *in, size_t in_len, const void *cache, size_t cache_len,
+                         void **out, size_t *out_len);
+
+/* Introspection (tests): copy the derived per-run device table (te_dev_cfg_t)
+ * and, if portlut != NULL, the 65536-entry port map.  Returns its size or -1. */
+int tcpedit_get_dev_cfg(tcpedit_t *tcpedit, void *out, size_t len, uint16_t *portlut);
+
+/* select the HIP device used by subsequently initialised contexts */
+int tcpedit_set_device(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,217 @@
+"""tcpreplay_amd -- MI355X-native tcpedit (tcprewrite's per-packet edit engine).
+
+Python mirror of the reference's libtcpedit interface (src/tcpedit/tcpedit.h,
+parse_args.h, tcpedit_api.h) over the C-ABI of the in-tree native library
+tcpreplay_amd/lib/libtcpedit_hip.so.  Every packet edit runs in the gfx950
+kernels; there is no Python or CPU edit path, and importing the native library
+fails loudly when it has not been built.
+"""
+import ctypes
+import os
+
+__all__ = ["TcpEdit", "Batch", "BatchResult", "load", "LIB_PATH", "TCPEDIT_OK", "TCPEDIT_ERROR",
+           "TCPEDIT_SOFT_ERROR", "TCPEDIT_WARN", "ST"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtcpedit_hip.so")
+
+TCPEDIT_SOFT_ERROR, TCPEDIT_ERROR, TCPEDIT_OK, TCPEDIT_WARN = -2, -1, 0, 1
+TCPR_DIR_NOSEND, TCPR_DIR_C2S, TCPR_DIR_S2C = 0, 1, 2
+
+
+class ST:
+    """per-record status bits (te_dev_cfg.h)"""
+    RC_MASK, OK, WARN, SOFT, ERROR = 0x03, 0, 1, 2, 3
+    DROPPED, NOSEND, UNSUPPORTED, WARNED, ZEROCAP = 0x04, 0x08, 0x10, 0x20, 0x40
+
+
+class BatchResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("packets", "bytes_in", "bytes_out", "written", "edited", "soft_errors", "warnings", "errors",
+                 "unsupported", "out_len")] + [
+        ("first_error", ctypes.c_int64), ("first_unsupported", ctypes.c_int64), ("n_tiles", ctypes.c_uint32),
+        ("kernel_ms", ctypes.c_double)]
+
+
+class PcapPkthdr(ctypes.Structure):
+    _fields_ = [("tv_sec", ctypes.c_long), ("tv_usec", ctypes.c_long), ("caplen", ctypes.c_uint32),
+                ("len", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load():
+    """Load the native library (no fallback: a missing build is an error)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C tcpreplay_amd/csrc` "
+                          "(or __graft_entry__.build()); tcpreplay_amd has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, c_int, u64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "tcpedit_init": (c_int, [ctypes.POINTER(vp), c_int]),
+        "tcpedit_geterr": (ctypes.c_char_p, [vp]),
+        "tcpedit_getwarn": (ctypes.c_char_p, [vp]),
+        "tcpedit_checkerror": (c_int, [vp, c_int, ctypes.c_char_p]),
+        "tcpedit_validate": (c_int, [vp]),
+        "tcpedit_packet": (c_int, [vp, ctypes.POINTER(ctypes.POINTER(PcapPkthdr)),
+                                   ctypes.POINTER(ctypes.c_char_p), c_int]),
+        "tcpedit_close": (c_int, [ctypes.POINTER(vp)]),
+        "tcpedit_get_output_dlt": (c_int, [vp]),
+        "tcpedit_l3data": (vp, [vp, c_int, vp, c_int]),
+        "tcpedit_l3proto": (c_int, [vp, c_int, vp, c_int]),
+        "tcpedit_get_total_bytes": (u64, [vp]),
+        "tcpedit_get_pkts_edited": (u64, [vp]),
+        "tcpedit_post_args": (c_int, [vp]),
+        "tcpedit_set_option": (c_int, [vp, ctypes.c_char_p, ctypes.c_char_p]),
+        "tcpedit_parse_args": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int)]),
+        "tcpedit_batch_open": (vp, [vp, vp, sz, vp, sz, u64]),
+        "tcpedit_batch_run": (c_int, [vp, vp]),
+        "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),
+        "tcpedit_batch_output": (sz, [vp, vp, sz]),
+        "tcpedit_batch_status": (ctypes.POINTER(ctypes.c_uint8), [vp]),
+        "tcpedit_batch_time": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
+        "tcpedit_batch_close": (None, [vp]),
+        "tcpedit_batch_device_output": (vp, [vp]),
+        "tcpedit_batch_input_bytes": (u64, [vp]),
+        "tcpedit_rewrite_pcap": (c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
+        "tcpedit_set_device": (c_int, [c_int]),
+        "tcpedit_get_dev_cfg": (c_int, [vp, vp, sz, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _lib = L
+    return L
+
+
+def _buf(data):
+    if data is None:
+        return None, 0
+    b = ctypes.create_string_buffer(bytes(data), len(data))
+    return b, len(data)
+
+
+class TcpEdit:
+    """A tcpedit context: tcpedit_init + option surface + tcpedit_post_args.
+
+    `args` uses tcprewrite's tcpedit/DLT options, e.g. ["--seed=42", "--fixcsum"];
+    "--skip-soft-errors" (a tcprewrite option) is accepted too.
+    """
+
+    def __init__(self, args=(), dlt=1, device=None):
+        L = load()
+        if device is not None:
+            L.tcpedit_set_device(int(device))
+        self._L = L
+        self._ctx = ctypes.c_void_p()
+        rc = L.tcpedit_init(ctypes.byref(self._ctx), dlt)
+        if rc < 0:
+            err = L.tcpedit_geterr(self._ctx).decode() if self._ctx else "init failed"
+            raise RuntimeError(err)
+        args = list(args)
+        argv = (ctypes.c_char_p * max(1, len(args)))(*[a.encode() for a in args])
+        unused = (ctypes.c_int * max(1, len(args)))()
+        n = L.tcpedit_parse_args(self._ctx, len(args), argv, unused)
+        if n < 0:
+            raise ValueError(self.geterr())
+        extra = [args[unused[i]] for i in range(n)]
+        for a in extra:
+            if a == "--skip-soft-errors":
+                L.tcpedit_set_option(self._ctx, b"skip-soft-errors", None)
+            else:
+                raise ValueError(f"unknown option {a}")
+        if L.tcpedit_post_args(self._ctx) < 0:
+            raise ValueError(self.geterr())
+        L.tcpedit_validate(self._ctx)
+
+    def geterr(self):
+        return self._L.tcpedit_geterr(self._ctx).decode(errors="replace")
+
+    def close(self):
+        if self._ctx:
+            self._L.tcpedit_close(ctypes.byref(self._ctx))
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rewrite(self, pcap: bytes, cache: bytes = None, with_status=False):
+        """Whole-file rewrite (tcprewrite semantics).  Returns (rc, out_bytes[, status])."""
+        b = Batch(self, pcap, cache)
+        try:
+            rc = b.run()
+            out = b.output()
+            if with_status:
+                return rc, out, b.status()
+            return rc, out
+        finally:
+            b.close()
+
+    def packet(self, hdr, data: bytearray, direction=TCPR_DIR_C2S):
+        """tcpedit_packet(): edits `data` (bytearray, >= MAXPACKET bytes recommended) in place.
+
+        hdr = dict(ts_sec, ts_usec, caplen, len); returns (rc, new_hdr)."""
+        h = PcapPkthdr(hdr.get("ts_sec", 0), hdr.get("ts_usec", 0), hdr["caplen"], hdr["len"])
+        hp = ctypes.pointer(h)
+        buf = (ctypes.c_char * len(data)).from_buffer(data)
+        dp = ctypes.c_char_p(ctypes.addressof(buf))
+        rc = self._L.tcpedit_packet(self._ctx, ctypes.byref(hp), ctypes.byref(dp), direction)
+        return rc, {"ts_sec": h.tv_sec, "ts_usec": h.tv_usec, "caplen": h.caplen, "len": h.len}
+
+
+class Batch:
+    """A pcap image staged in HBM (tcpedit_batch_open)."""
+
+    def __init__(self, te: TcpEdit, pcap: bytes, cache: bytes = None, pkt_base=0):
+        self._te, self._L = te, te._L
+        self._in, n = _buf(pcap)
+        self._cache, cn = _buf(cache)
+        self._b = self._L.tcpedit_batch_open(te._ctx, self._in, n, self._cache, cn, pkt_base)
+        if not self._b:
+            raise RuntimeError(te.geterr())
+
+    def run(self):
+        return self._L.tcpedit_batch_run(self._te._ctx, self._b)
+
+    def result(self) -> BatchResult:
+        r = BatchResult()
+        self._L.tcpedit_batch_result(self._b, ctypes.byref(r))
+        return r
+
+    def output(self) -> bytes:
+        r = self.result()
+        out = ctypes.create_string_buffer(max(1, r.out_len))
+        n = self._L.tcpedit_batch_output(self._b, out, r.out_len)
+        return out.raw[:n]
+
+    def status(self):
+        import numpy as np
+        r = self.result()
+        p = self._L.tcpedit_batch_status(self._b)
+        if not p:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array(p, shape=(r.packets,)).copy()
+
+    def time(self, iters):
+        ms = ctypes.c_double()
+        if self._L.tcpedit_batch_time(self._te._ctx, self._b, int(iters), ctypes.byref(ms)) < 0:
+            raise RuntimeError(self._te.geterr())
+        return ms.value
+
+    def close(self):
+        if self._b:
+            self._L.tcpedit_batch_close(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,768 @@
+/*
+ * te_api.c -- the C-ABI of libtcpedit_hip: context lifecycle (tcpedit.c:371-652),
+ * the pcap record index / tile builder, and the batch runner that drives the
+ * gfx950 kernel.  Host code only; every packet edit happens on the GPU.
+ */
+#define _GNU_SOURCE
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "te_internal.h"
+
+#define HIPCHK(t, call)                                                                   \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            if (t)                                                                        \
+                te_seterr((t), "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__); \
+            goto fail;                                                                    \
+        }                                                                                 \
+    } while (0)
+
+static int g_device = -1;
+
+int tcpedit_set_device(int device)
+{
+    g_device = device;
+    return hipSetDevice(device) == hipSuccess ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* batch: a pcap image resident in HBM                                       */
+/* ------------------------------------------------------------------------- */
+struct tcpedit_batch_s {
+    tcpedit_t *ctx;
+    /* host side */
+    int swapped, nsec;
+    uint32_t linktype;
+    uint64_t n_pkts, n_tiles, in_len, out_cap, scratch_bytes;
+    uint64_t pkt_base;
+    te_tile_t *tiles;
+    uint16_t *pkt_rel;
+    uint8_t *status;         /* host copy after a run */
+    int status_valid;
+    int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
+    /* device side */
+    uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
+    uint64_t dirbits_len;
+    te_tile_t *d_tiles;
+    uint16_t *d_pkt_rel;
+    uint8_t *d_ws;           /* err[0..1] | err[2], ticket | counters | tile_state[] */
+    uint64_t ws_bytes;
+    hipEvent_t ev0, ev1;
+    /* results */
+    uint64_t counters[TE_CNT__N];
+    uint64_t err[3];
+    double kernel_ms;
+    int ran;
+};
+
+#define WS_ERR 0
+#define WS_ZERO 16
+#define WS_TICKET 24
+#define WS_COUNTERS 32
+#define WS_STATE 128
+
+static uint32_t rd32(const uint8_t *p, int swapped)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return swapped ? __builtin_bswap32(v) : v;
+}
+
+/* Walk the records (what libpcap's pcap_next does for tcprewrite.c:289) and
+ * cut them into tiles whose LDS slots fit TE_SLOT_BYTES. */
+static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, size_t len)
+{
+    if (len < 24) {
+        te_seterr(t, "pcap image too short");
+        return -1;
+    }
+    uint32_t magic;
+    memcpy(&magic, img, 4);
+    switch (magic) {
+    case 0xa1b2c3d4u: b->swapped = 0; b->nsec = 0; break;
+    case 0xd4c3b2a1u: b->swapped = 1; b->nsec = 0; break;
+    case 0xa1b23c4du: b->swapped = 0; b->nsec = 1; break;
+    case 0x4d3cb2a1u: b->swapped = 1; b->nsec = 1; break;
+    default:
+        te_seterr(t, "not a pcap file (magic 0x%08x)", magic);
+        return -1;
+    }
+    b->linktype = rd32(img + 20, b->swapped) & 0x03ffffffu;
+    const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
+    uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
+    b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
+    b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
+    b->n_pkts = b->n_tiles = 0;
+    b->out_cap = 24 + 64;
+    b->scratch_bytes = 0;
+    b->stop_error_pkt = -1;
+    size_t off = 24;
+    te_tile_t cur;
+    memset(&cur, 0, sizeof(cur));
+    uint32_t cur_slots = 0;
+    int open = 0;
+    while (off + 16 <= len) {
+        uint32_t caplen = rd32(img + off + 8, b->swapped), plen = rd32(img + off + 12, b->swapped);
+        if (caplen > 262144u || off + 16 + caplen > len)
+            break; /* libpcap stops at an oversize or truncated record */
+        if (plen > 262144u) {
+            /* tcprewrite.c:296-297 errx()s here: the output keeps earlier records */
+            b->stop_error_pkt = (int64_t)b->n_pkts;
+            break;
+        }
+        uint32_t data = pad && plen > caplen ? plen : caplen;
+        uint32_t g = (uint32_t)(off & 15);
+        uint32_t slot = TE_SLOT_BYTES_OF(g, data);
+        int huge = slot > TE_SLOT_BYTES;
+        if (open && (huge || cur.npkt >= TE_MAX_PKTS || cur_slots + slot > TE_SLOT_BYTES)) {
+            if (b->n_tiles == cap_tiles)
+                b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
+            b->tiles[b->n_tiles++] = cur;
+            open = 0;
+        }
+        if (!open) {
+            memset(&cur, 0, sizeof(cur));
+            cur.span_off = off;
+            cur.first_pkt = (uint32_t)b->n_pkts;
+            cur.scratch_off = TE_NO_SCRATCH;
+            cur_slots = 0;
+            open = 1;
+        }
+        if (b->n_pkts == cap_pk)
+            b->pkt_rel = realloc(b->pkt_rel, sizeof(uint16_t) * (cap_pk *= 2));
+        b->pkt_rel[b->n_pkts++] = (uint16_t)(off - cur.span_off);
+        cur.npkt++;
+        cur.span_len = (uint32_t)(off + 16 + caplen - cur.span_off);
+        cur_slots += slot;
+        b->out_cap += 16 + (uint64_t)data + 4;
+        if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
+            cur.scratch_off = b->scratch_bytes;
+            b->scratch_bytes += (slot + 255) & ~255u;
+            if (b->n_tiles == cap_tiles)
+                b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
+            b->tiles[b->n_tiles++] = cur;
+            open = 0;
+        }
+        off += 16 + caplen;
+        if (b->n_pkts >= 0xffffffffull) {
+            te_seterr(t, "too many records for one batch");
+            return -1;
+        }
+    }
+    if (open) {
+        if (b->n_tiles == cap_tiles)
+            b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
+        b->tiles[b->n_tiles++] = cur;
+    }
+    b->in_len = len;
+    return 0;
+}
+
+static void batch_free_dev(tcpedit_batch_t *b)
+{
+    hipFree(b->d_in);
+    hipFree(b->d_out);
+    hipFree(b->d_status);
+    hipFree(b->d_scratch);
+    hipFree(b->d_dirbits);
+    hipFree(b->d_tiles);
+    hipFree(b->d_pkt_rel);
+    hipFree(b->d_ws);
+    b->d_in = b->d_out = b->d_status = b->d_scratch = b->d_dirbits = b->d_ws = NULL;
+    b->d_tiles = NULL;
+    b->d_pkt_rel = NULL;
+}
+
+void tcpedit_batch_close(tcpedit_batch_t *b)
+{
+    if (!b)
+        return;
+    batch_free_dev(b);
+    if (b->ev0)
+        hipEventDestroy(b->ev0);
+    if (b->ev1)
+        hipEventDestroy(b->ev1);
+    free(b->tiles);
+    free(b->pkt_rel);
+    free(b->status);
+    free(b);
+}
+
+/* tcpprep cache file image -> its data bytes (cache.c:63-140) */
+static int cache_data(tcpedit_t *t, const uint8_t *c, size_t n, const uint8_t **data, uint64_t *dlen)
+{
+    if (n < 24 || memcmp(c, "tcpprep\0", 8) != 0) {
+        te_seterr(t, "not a tcpprep cache file");
+        return -1;
+    }
+    if (strtol((const char *)c + 8, NULL, 10) != 4) {
+        te_seterr(t, "cache file version mismatch");
+        return -1;
+    }
+    uint64_t np = 0;
+    for (int i = 0; i < 8; i++)
+        np = (np << 8) | c[12 + i];
+    uint32_t ppb = ((uint32_t)c[20] << 8) | c[21], clen = ((uint32_t)c[22] << 8) | c[23];
+    if (ppb == 0) {
+        te_seterr(t, "invalid cache header");
+        return -1;
+    }
+    uint64_t sz = np / ppb + (np % ppb ? 1 : 0);
+    if (24 + (uint64_t)clen + sz > n) {
+        te_seterr(t, "Cache data length doesn't match cache header");
+        return -1;
+    }
+    *data = c + 24 + clen;
+    *dlen = sz;
+    return 0;
+}
+
+/* first device use of a context: pick the device and create its stream */
+static int te_dev_ready(tcpedit_t *t)
+{
+    if (t->stream)
+        return 0;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        te_seterr(t, "no HIP device available: libtcpedit_hip edits packets on the GPU only");
+        return -1;
+    }
+    if (t->device >= 0 && hipSetDevice(t->device) != hipSuccess) {
+        te_seterr(t, "hipSetDevice(%d) failed", t->device);
+        return -1;
+    }
+    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+        te_seterr(t, "hipStreamCreate failed");
+        return -1;
+    }
+    return 0;
+}
+
+int te_upload_cfg(tcpedit_t *t)
+{
+    if (te_dev_ready(t) < 0)
+        return -1;
+    if (!t->dev_dirty && t->d_cfg)
+        return 0;
+    if (!t->d_cfg)
+        HIPCHK(t, hipMalloc((void **)&t->d_cfg, sizeof(te_dev_cfg_t)));
+    HIPCHK(t, hipMemcpyAsync(t->d_cfg, &t->cfg, sizeof(te_dev_cfg_t), hipMemcpyHostToDevice, t->stream));
+    if (t->portlut) {
+        if (!t->d_portlut)
+            HIPCHK(t, hipMalloc((void **)&t->d_portlut, 65536 * sizeof(uint16_t)));
+        HIPCHK(t, hipMemcpyAsync(t->d_portlut, t->portlut, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                                 t->stream));
+    }
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    t->dev_dirty = 0;
+    return 0;
+fail:
+    return -1;
+}
+
+tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, const void *cache, size_t cache_len,
+                                    uint64_t pkt_base)
+{
+    if (!t || !pcap)
+        return NULL;
+    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+        return NULL;
+    tcpedit_batch_t *b = calloc(1, sizeof(*b));
+    b->ctx = t;
+    b->pkt_base = pkt_base;
+    if (index_image(t, b, (const uint8_t *)pcap, len) < 0)
+        goto fail;
+    if (b->linktype != (uint32_t)t->dlt) {
+        te_seterr(t, "pcap linktype %u does not match the context DLT %d", b->linktype, t->dlt);
+        goto fail;
+    }
+    if (te_upload_cfg(t) < 0)
+        goto fail;
+    HIPCHK(t, hipMalloc((void **)&b->d_in, len + 64));
+    HIPCHK(t, hipMemcpyAsync(b->d_in, pcap, len, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMalloc((void **)&b->d_out, b->out_cap + 64));
+    HIPCHK(t, hipMalloc((void **)&b->d_status, b->n_pkts + 16));
+    if (b->scratch_bytes)
+        HIPCHK(t, hipMalloc((void **)&b->d_scratch, b->scratch_bytes));
+    HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (b->n_tiles + 1)));
+    HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->n_pkts + 1)));
+    HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
+                             t->stream));
+    b->ws_bytes = WS_STATE + 8 * (b->n_tiles + 1);
+    HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
+    if (cache) {
+        const uint8_t *cd;
+        if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &b->dirbits_len) < 0)
+            goto fail;
+        HIPCHK(t, hipMalloc((void **)&b->d_dirbits, b->dirbits_len + 16));
+        HIPCHK(t, hipMemcpyAsync(b->d_dirbits, cd, b->dirbits_len, hipMemcpyHostToDevice, t->stream));
+    } else if (t->cfg.n_cidrmap1 && t->have[OPT_ENDPOINTS]) {
+        te_seterr(t, "--endpoints requires a tcpprep cache file");
+        goto fail;
+    }
+    HIPCHK(t, hipEventCreate(&b->ev0));
+    HIPCHK(t, hipEventCreate(&b->ev1));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return b;
+fail:
+    tcpedit_batch_close(b);
+    return NULL;
+}
+
+static int launch(tcpedit_batch_t *b, int fixed_dir)
+{
+    tcpedit_t *t = b->ctx;
+    te_launch_t L;
+    memset(&L, 0, sizeof(L));
+    L.cfg = t->d_cfg;
+    L.portlut = t->cfg.has_portmap ? t->d_portlut : NULL;
+    L.dirbits = b->d_dirbits;
+    L.dirbits_len = b->dirbits_len;
+    L.pkt_base = b->pkt_base;
+    L.fixed_dir = fixed_dir;
+    L.in = b->d_in;
+    L.tiles = b->d_tiles;
+    L.pkt_rel = b->d_pkt_rel;
+    L.n_tiles = (uint32_t)b->n_tiles;
+    L.in_swapped = (uint32_t)b->swapped;
+    L.in_nsec = (uint32_t)b->nsec;
+    L.out = b->d_out;
+    L.out_base = 24;
+    L.tile_state = (uint64_t *)(b->d_ws + WS_STATE);
+    L.ticket = (unsigned int *)(b->d_ws + WS_TICKET);
+    L.status = b->d_status;
+    L.counters = (uint64_t *)(b->d_ws + WS_COUNTERS);
+    L.err = (uint64_t *)(b->d_ws + WS_ERR);
+    L.scratch = b->d_scratch;
+    L.zero_region = b->d_ws + WS_ZERO;
+    L.zero_bytes = b->ws_bytes - WS_ZERO;
+    L.grid = 256 * 4;
+    return te_launch_edit(&L, t->stream);
+}
+
+static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
+{
+    float ms = 0;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    static const uint8_t hdr[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                    0xff, 0xff, 0, 0, 1, 0, 0, 0};
+    /* pcap_open_dead(out_dlt, 65535) + pcap_dump_open (tcprewrite.c:124,147) */
+    HIPCHK(t, hipMemcpyAsync(b->d_out, hdr, 24, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipEventRecord(b->ev0, t->stream));
+    if (launch(b, fixed_dir) != 0) {
+        te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return TCPEDIT_ERROR;
+    }
+    HIPCHK(t, hipEventRecord(b->ev1, t->stream));
+    HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + WS_COUNTERS, sizeof(b->counters), hipMemcpyDeviceToHost,
+                             t->stream));
+    HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    HIPCHK(t, hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->kernel_ms = ms;
+    b->ran = 1;
+    b->status_valid = 0;
+    if (b->err[2]) {
+        te_seterr(t, "device look-back timed out (%llu tiles)", (unsigned long long)b->err[2]);
+        return TCPEDIT_ERROR;
+    }
+    t->packetnum += b->counters[TE_CNT_PACKETS];
+    t->total_bytes += b->counters[TE_CNT_BYTES_OUT];
+    t->pkts_edited += b->counters[TE_CNT_EDITED];
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
+const uint8_t *tcpedit_batch_status(tcpedit_batch_t *b)
+{
+    if (!b || !b->ran)
+        return NULL;
+    if (!b->status_valid) {
+        if (!b->status)
+            b->status = malloc(b->n_pkts + 1);
+        if (hipMemcpy(b->status, b->d_status, b->n_pkts, hipMemcpyDeviceToHost) != hipSuccess)
+            return NULL;
+        b->status_valid = 1;
+    }
+    return b->status;
+}
+
+int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    if (!t || !b)
+        return TCPEDIT_ERROR;
+    if (batch_run_dir(t, b, -1) != TCPEDIT_OK)
+        return TCPEDIT_ERROR;
+    if (b->counters[TE_CNT_UNSUPPORTED]) {
+        const uint8_t *st = tcpedit_batch_status(b);
+        int64_t first = -1;
+        for (uint64_t i = 0; st && i < b->n_pkts; i++)
+            if (st[i] & TE_ST_UNSUPPORTED) {
+                first = (int64_t)i;
+                break;
+            }
+        te_seterr(t,
+                  "record %lld: its edit reads bytes past caplen, i.e. the reference's stale static packet "
+                  "buffer (SURVEY Appendix B Q8); not supported by the device path",
+                  (long long)(first + 1 + (int64_t)b->pkt_base));
+        return TCPEDIT_ERROR;
+    }
+    if (b->err[0] != ~0ull || b->stop_error_pkt >= 0) {
+        int64_t e = b->err[0] != ~0ull ? (int64_t)b->err[0] : b->stop_error_pkt;
+        te_seterr(t, "Error rewriting packets: packet %lld", (long long)(e + 1 + (int64_t)b->pkt_base));
+        return TCPEDIT_ERROR;
+    }
+    return TCPEDIT_OK;
+}
+
+int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r)
+{
+    if (!b || !r || !b->ran)
+        return TCPEDIT_ERROR;
+    memset(r, 0, sizeof(*r));
+    r->packets = b->counters[TE_CNT_PACKETS];
+    r->bytes_in = b->counters[TE_CNT_BYTES_IN];
+    r->bytes_out = b->counters[TE_CNT_BYTES_OUT];
+    r->written = b->counters[TE_CNT_WRITTEN];
+    r->edited = b->counters[TE_CNT_EDITED];
+    r->soft_errors = b->counters[TE_CNT_SOFT];
+    r->warnings = b->counters[TE_CNT_WARN];
+    r->errors = b->counters[TE_CNT_ERROR];
+    r->unsupported = b->counters[TE_CNT_UNSUPPORTED];
+    r->first_error = b->err[0] != ~0ull ? (int64_t)b->err[0] : -1;
+    r->first_unsupported = -1;
+    if (r->unsupported) {
+        const uint8_t *st = tcpedit_batch_status(b);
+        for (uint64_t i = 0; st && i < b->n_pkts; i++)
+            if (st[i] & TE_ST_UNSUPPORTED) {
+                r->first_unsupported = (int64_t)i;
+                break;
+            }
+    }
+    /* a hard error truncates the output at the failing record (tcprewrite.c:156-160) */
+    uint64_t end = 24 + b->counters[TE_CNT_BYTES_OUT];
+    if (b->err[0] != ~0ull)
+        end = b->err[1];
+    else if (b->stop_error_pkt >= 0)
+        r->first_error = b->stop_error_pkt;
+    r->out_len = end;
+    r->n_tiles = (uint32_t)b->n_tiles;
+    r->kernel_ms = b->kernel_ms;
+    return TCPEDIT_OK;
+}
+
+size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap)
+{
+    tcpedit_batch_result_t r;
+    if (tcpedit_batch_result(b, &r) != TCPEDIT_OK)
+        return 0;
+    size_t n = r.out_len < cap ? r.out_len : cap;
+    if (hipMemcpy(dst, b->d_out, n, hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return n;
+}
+
+const void *tcpedit_batch_device_output(tcpedit_batch_t *b) { return b ? b->d_out : NULL; }
+uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b) { return b ? b->in_len : 0; }
+
+int tcpedit_batch_time(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms_per_run)
+{
+    hipEvent_t e0, e1;
+    float ms = 0;
+    if (!t || !b || iters <= 0 || te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    HIPCHK(t, hipEventCreate(&e0));
+    HIPCHK(t, hipEventCreate(&e1));
+    HIPCHK(t, hipEventRecord(e0, t->stream));
+    for (int i = 0; i < iters; i++)
+        if (launch(b, -1) != 0) {
+            te_seterr(t, "kernel launch failed");
+            return TCPEDIT_ERROR;
+        }
+    HIPCHK(t, hipEventRecord(e1, t->stream));
+    HIPCHK(t, hipEventSynchronize(e1));
+    HIPCHK(t, hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    *ms_per_run = ms / iters;
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
+int tcpedit_rewrite_pcap(tcpedit_t *t, const void *in, size_t in_len, const void *cache, size_t cache_len, void **out,
+                         size_t *out_len)
+{
+    *out = NULL;
+    *out_len = 0;
+    tcpedit_batch_t *b = tcpedit_batch_open(t, in, in_len, cache, cache_len, 0);
+    if (!b)
+        return TCPEDIT_ERROR;
+    int rc = tcpedit_batch_run(t, b);
+    tcpedit_batch_result_t r;
+    if (tcpedit_batch_result(b, &r) == TCPEDIT_OK && !r.unsupported) {
+        *out = malloc(r.out_len ? r.out_len : 1);
+        *out_len = tcpedit_batch_output(b, *out, r.out_len);
+    }
+    tcpedit_batch_close(b);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* reference interface                                                       */
+/* ------------------------------------------------------------------------- */
+int tcpedit_init(tcpedit_t **out, int dlt)
+{
+    tcpedit_t *t = calloc(1, sizeof(*t));
+    *out = t;
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->dlt = dlt;
+    t->device = g_device;
+    /* defaults until post_args (tcpedit.c:382-394) */
+    t->cfg.mtu = 1500;
+    t->cfg.tos = t->cfg.tclass = t->cfg.flowlabel = -1;
+    t->cfg.vlan_tag = 65535;
+    t->cfg.vlan_pri = t->cfg.vlan_cfi = 255;
+    t->cfg.vlan_proto = 0x8100;
+    t->fuzz_factor = 8;
+    t->dev_dirty = 1;
+    if (dlt != 1) {
+        te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: DLT_EN10MB)", dlt);
+        return TCPEDIT_ERROR;
+    }
+    return TCPEDIT_OK;
+}
+
+int tcpedit_post_args(tcpedit_t *t)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->errstr[0] = 0;
+    return te_derive_cfg(t) < 0 ? TCPEDIT_ERROR : TCPEDIT_OK;
+}
+
+int tcpedit_validate(tcpedit_t *t)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->validated = 1;
+    return TCPEDIT_OK;
+}
+
+char *tcpedit_geterr(tcpedit_t *t) { return t ? t->errstr : NULL; }
+char *tcpedit_getwarn(tcpedit_t *t) { return t ? t->warnstr : NULL; }
+
+int tcpedit_checkerror(tcpedit_t *t, int rcode, const char *prefix)
+{
+    switch (rcode) {
+    case TCPEDIT_OK:
+    case TCPEDIT_ERROR:
+        return rcode;
+    case TCPEDIT_SOFT_ERROR:
+        fprintf(stderr, prefix ? "Error %s: %s\n" : "Error%s: %s\n", prefix ? prefix : "", tcpedit_geterr(t));
+        break;
+    case TCPEDIT_WARN:
+        fprintf(stderr, prefix ? "Warning %s: %s\n" : "Warning%s: %s\n", prefix ? prefix : "", tcpedit_getwarn(t));
+        return TCPEDIT_OK;
+    default:
+        break;
+    }
+    return TCPEDIT_ERROR;
+}
+
+int tcpedit_get_output_dlt(tcpedit_t *t) { return t ? 1 : -1; }
+
+int tcpedit_get_dev_cfg(tcpedit_t *t, void *out, size_t len, uint16_t *portlut)
+{
+    if (!t || !out || len < sizeof(te_dev_cfg_t))
+        return -1;
+    memcpy(out, &t->cfg, sizeof(te_dev_cfg_t));
+    if (portlut) {
+        for (int p = 0; p < 65536; p++)
+            portlut[p] = t->portlut ? t->portlut[p] : (uint16_t)p;
+    }
+    return (int)sizeof(te_dev_cfg_t);
+}
+uint64_t tcpedit_get_total_bytes(tcpedit_t *t) { return t ? t->total_bytes : 0; }
+uint64_t tcpedit_get_pkts_edited(tcpedit_t *t) { return t ? t->pkts_edited : 0; }
+
+/* tcpedit_l3data / tcpedit_l3proto: L2 walk of an (un)edited frame; these are
+ * the DLT plugins' l3 accessors (dlt_en10mb_get_layer3 / _proto), pure header
+ * inspection used by callers such as fragroute (tcprewrite.c:338) */
+static int host_l2(const unsigned char *p, int n, uint16_t *proto)
+{
+    if (n <= 18)
+        return -1;
+    uint32_t off = 14;
+    uint16_t et = (uint16_t)((p[12] << 8) | p[13]);
+    for (int guard = 0; guard < 4096; guard++) {
+        if (et == 0x8100 || et == 0x88A8 || et == 0x9100) {
+            if ((uint32_t)n < off + 4)
+                return -1;
+            et = (uint16_t)((p[off + 2] << 8) | p[off + 3]);
+            off += 4;
+        } else if (et == 0x8847 || et == 0x8848) {
+            int bos = 0;
+            uint32_t lab = off;
+            while (!bos) {
+                if (off + 4 > (uint32_t)n)
+                    return -1;
+                lab = off;
+                bos = (p[off + 2] & 1) != 0;
+                if ((((uint32_t)p[off] << 12) | ((uint32_t)p[off + 1] << 4) | (p[off + 2] >> 4)) == 13)
+                    return -1;
+                off += 4;
+            }
+            if (lab + 5 > (uint32_t)n)
+                return -1;
+            uint8_t nib = p[lab + 4] >> 4;
+            if (nib == 4)
+                et = 0x0800;
+            else if (nib == 6)
+                et = 0x86DD;
+            else if (nib == 0) {
+                if (off + 18 > (uint32_t)n)
+                    return -1;
+                off += 4;
+                et = (uint16_t)((p[off + 12] << 8) | p[off + 13]);
+                off += 14;
+            } else
+                return -1;
+        } else
+            break;
+    }
+    if (et < 1536)
+        return -1;
+    *proto = et;
+    return (int)off;
+}
+
+const unsigned char *tcpedit_l3data(tcpedit_t *t, tcpedit_coder code, unsigned char *packet, int pktlen)
+{
+    (void)t;
+    (void)code;
+    uint16_t pr;
+    int l2 = host_l2(packet, pktlen, &pr);
+    if (l2 < 0 || pktlen <= l2)
+        return NULL;
+    return packet + l2;
+}
+
+int tcpedit_l3proto(tcpedit_t *t, tcpedit_coder code, const unsigned char *packet, int pktlen)
+{
+    (void)t;
+    (void)code;
+    uint16_t pr;
+    if (pktlen < 14 || host_l2(packet, pktlen, &pr) < 0)
+        return -1;
+    return pr;
+}
+
+/* tcpedit_packet (tcpedit.c:46-366): one record through the GPU kernel. */
+int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pktdata, tcpr_dir_t direction)
+{
+    if (!t || !pkthdr || !*pkthdr || !pktdata || !*pktdata)
+        return TCPEDIT_ERROR;
+    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+        return TCPEDIT_ERROR;
+    struct pcap_pkthdr *h = *pkthdr;
+    uint32_t caplen = h->caplen;
+    size_t img_len = 24 + 16 + caplen;
+    uint8_t *img = malloc(img_len);
+    static const uint8_t fh[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                   0x00, 0x00, 0x04, 0, 1, 0, 0, 0};
+    memcpy(img, fh, 24);
+    uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
+    memcpy(img + 24, rh, 16);
+    memcpy(img + 40, *pktdata, caplen);
+    uint8_t saved_skip = t->cfg.skip_soft_errors;
+    t->cfg.skip_soft_errors = 0; /* tcpedit_packet itself never drops */
+    t->dev_dirty |= saved_skip;
+    tcpedit_batch_t *b = tcpedit_batch_open(t, img, img_len, NULL, 0, t->packetnum);
+    free(img);
+    int rc = TCPEDIT_ERROR;
+    if (!b)
+        goto out;
+    if (batch_run_dir(t, b, (int)direction) != TCPEDIT_OK)
+        goto out;
+    const uint8_t *st = tcpedit_batch_status(b);
+    if (!st)
+        goto out;
+    if (st[0] & TE_ST_UNSUPPORTED) {
+        te_seterr(t, "packet %llu: edit reads bytes past caplen (reference stale buffer, SURVEY Q8)",
+                  (unsigned long long)t->packetnum);
+        goto out;
+    }
+    switch (st[0] & TE_ST_RC_MASK) {
+    case TE_ST_RC_ERROR:
+        te_seterr(t, "packet %llu: tcpedit error", (unsigned long long)t->packetnum);
+        rc = TCPEDIT_ERROR;
+        goto out;
+    case TE_ST_RC_SOFT:
+        te_seterr(t, "Packet %llu has no L3+ header or cannot be edited", (unsigned long long)t->packetnum);
+        rc = TCPEDIT_SOFT_ERROR;
+        break;
+    case TE_ST_RC_WARN:
+        rc = TCPEDIT_WARN;
+        break;
+    default:
+        rc = TCPEDIT_OK;
+    }
+    if (st[0] & TE_ST_WARNED) {
+        te_setwarn(t, "packet %llu: checksum not recomputed", (unsigned long long)t->packetnum);
+        fprintf(stderr, "Warning: %s\n", t->warnstr);
+    }
+    {
+        uint8_t rec[16];
+        tcpedit_batch_result_t r;
+        tcpedit_batch_result(b, &r);
+        if (r.out_len >= 24 + 16) {
+            if (hipMemcpy(rec, b->d_out + 24, 16, hipMemcpyDeviceToHost) != hipSuccess)
+                goto out;
+            uint32_t oc, ol;
+            memcpy(&oc, rec + 8, 4);
+            memcpy(&ol, rec + 12, 4);
+            if (oc > 262166u)
+                goto out;
+            if (hipMemcpy(*pktdata, b->d_out + 40, oc, hipMemcpyDeviceToHost) != hipSuccess)
+                goto out;
+            h->caplen = oc;
+            h->len = ol;
+        } else {
+            h->caplen = 0; /* edited down to zero bytes */
+        }
+    }
+out:
+    t->cfg.skip_soft_errors = saved_skip;
+    t->dev_dirty |= saved_skip;
+    tcpedit_batch_close(b);
+    return rc;
+}
+
+int tcpedit_close(tcpedit_t **tp)
+{
+    if (!tp || !*tp)
+        return TCPEDIT_ERROR;
+    tcpedit_t *t = *tp;
+    for (int k = 0; k < OPT__N; k++) {
+        free(t->arg[k]);
+        for (int i = 0; i < t->nstack[k]; i++)
+            free(t->stack[k][i]);
+    }
+    free(t->portlut);
+    hipFree(t->d_cfg);
+    hipFree(t->d_portlut);
+    if (t->stream)
+        hipStreamDestroy(t->stream);
+    free(t);
+    *tp = NULL;
+    return 0;
+}

@@ -1,0 +1,930 @@
+/*
+ * te_args.c -- the tcpedit option surface and its one-time derivation into
+ * the device tables (te_dev_cfg_t + the port-map LUT).
+ *
+ * Restates, on the host, the config half of libtcpedit:
+ *   tcpedit_post_args         src/tcpedit/parse_args.c:34-254
+ *   dlt_en10mb_parse_opts     src/tcpedit/plugins/dlt_en10mb/en10mb.c:226-396
+ *   parse_cidr_map/_endpoints src/common/cidr.c:130-418
+ *   parse_portmap/ports2PORT  src/tcpedit/portmap.c:55-218
+ *   dualmac2hex/mac2hex       src/common/mac.c:33-104
+ *   tcpr_random               src/common/utils.c:436-458
+ * and the AutoOpts constraints of tcpedit_opts.def / en10mb_opts.def.
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <ctype.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+#include "te_internal.h"
+
+const te_optdef_t te_optdefs[OPT__N] = {
+    [OPT_PORTMAP] = {"portmap", 'r', 1, 9999, 1},
+    [OPT_SEED] = {"seed", 's', 1, 1, 0},
+    [OPT_PNAT] = {"pnat", 'N', 1, 2, 1},
+    [OPT_SRCIPMAP] = {"srcipmap", 'S', 1, 1, 0},
+    [OPT_DSTIPMAP] = {"dstipmap", 'D', 1, 1, 0},
+    [OPT_ENDPOINTS] = {"endpoints", 'e', 1, 1, 0},
+    [OPT_TCP_SEQUENCE] = {"tcp-sequence", 0, 1, 1, 0},
+    [OPT_SKIPBROADCAST] = {"skipbroadcast", 'b', 0, 1, 0},
+    [OPT_FIXCSUM] = {"fixcsum", 'C', 0, 1, 0},
+    [OPT_FIXHDRLEN] = {"fixhdrlen", 0, 0, 1, 0},
+    [OPT_MTU] = {"mtu", 'm', 1, 1, 0},
+    [OPT_MTU_TRUNC] = {"mtu-trunc", 0, 0, 1, 0},
+    [OPT_EFCS] = {"efcs", 'E', 0, 1, 0},
+    [OPT_TTL] = {"ttl", 0, 1, 1, 0},
+    [OPT_TOS] = {"tos", 0, 1, 1, 0},
+    [OPT_TCLASS] = {"tclass", 0, 1, 1, 0},
+    [OPT_FLOWLABEL] = {"flowlabel", 0, 1, 1, 0},
+    [OPT_FIXLEN] = {"fixlen", 'F', 1, 1, 0},
+    [OPT_FUZZ_SEED] = {"fuzz-seed", 0, 1, 1, 0},
+    [OPT_FUZZ_FACTOR] = {"fuzz-factor", 0, 1, 1, 0},
+    [OPT_DLT] = {"dlt", 0, 1, 1, 0},
+    [OPT_SKIPL2BROADCAST] = {"skipl2broadcast", 0, 0, 1, 0},
+    [OPT_ENET_DMAC] = {"enet-dmac", 0, 1, 1, 0},
+    [OPT_ENET_SMAC] = {"enet-smac", 0, 1, 1, 0},
+    [OPT_ENET_SUBSMAC] = {"enet-subsmac", 0, 1, 9999, 1},
+    [OPT_ENET_MAC_SEED] = {"enet-mac-seed", 0, 1, 1, 0},
+    [OPT_ENET_MAC_SEED_KEEP_BYTES] = {"enet-mac-seed-keep-bytes", 0, 1, 1, 0},
+    [OPT_ENET_VLAN] = {"enet-vlan", 0, 1, 1, 0},
+    [OPT_ENET_VLAN_TAG] = {"enet-vlan-tag", 0, 1, 1, 0},
+    [OPT_ENET_VLAN_CFI] = {"enet-vlan-cfi", 0, 1, 1, 0},
+    [OPT_ENET_VLAN_PRI] = {"enet-vlan-pri", 0, 1, 1, 0},
+    [OPT_ENET_VLAN_PROTO] = {"enet-vlan-proto", 0, 1, 1, 0},
+    [OPT_SKIP_SOFT_ERRORS] = {"skip-soft-errors", 0, 0, 1, 0},
+    [OPT_USER_DLT] = {"user-dlt", 0, 1, 1, 0},
+    [OPT_USER_DLINK] = {"user-dlink", 0, 1, 2, 1},
+    [OPT_HDLC_CONTROL] = {"hdlc-control", 0, 1, 1, 0},
+    [OPT_HDLC_ADDRESS] = {"hdlc-address", 0, 1, 1, 0},
+};
+
+void te_seterr(tcpedit_t *t, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t->errstr, sizeof(t->errstr), fmt, ap);
+    va_end(ap);
+}
+
+void te_setwarn(tcpedit_t *t, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t->warnstr, sizeof(t->warnstr), fmt, ap);
+    va_end(ap);
+}
+
+/* ISO C rand_r extended to 32 bits (utils.c:436-458) */
+uint32_t te_tcpr_random(uint32_t *seed)
+{
+    uint32_t n = *seed, r;
+    n = n * 1103515245u + 12345u;
+    r = (uint32_t)((int)(n / 65536) % 2048);
+    n = n * 1103515245u + 12345u;
+    r = (r << 10) ^ (uint32_t)((int)(n / 65536) % 1024);
+    n = n * 1103515245u + 12345u;
+    r = (r << 10) ^ (uint32_t)((int)(n / 65536) % 1024);
+    *seed = n;
+    return r;
+}
+
+/* ------------------------------------------------------------------------- */
+/* option store                                                              */
+/* ------------------------------------------------------------------------- */
+static int find_long(const char *name, size_t n)
+{
+    for (int k = 0; k < OPT__N; k++)
+        if (strlen(te_optdefs[k].name) == n && strncmp(te_optdefs[k].name, name, n) == 0)
+            return k;
+    return -1;
+}
+
+static int store(tcpedit_t *t, int k, const char *value)
+{
+    const te_optdef_t *d = &te_optdefs[k];
+    if (d->has_arg && !value) {
+        te_seterr(t, "option --%s requires an argument", d->name);
+        return -1;
+    }
+    if (d->stacked) {
+        if (t->nstack[k] >= d->max || t->nstack[k] >= TE_MAX_STACK) {
+            te_seterr(t, "too many --%s options (max %d)", d->name, d->max);
+            return -1;
+        }
+        t->stack[k][t->nstack[k]++] = strdup(value);
+    } else if (t->have[k]) {
+        te_seterr(t, "option --%s may appear only once", d->name);
+        return -1;
+    }
+    t->have[k] = 1;
+    free(t->arg[k]);
+    t->arg[k] = value ? strdup(value) : NULL;
+    t->post_args_done = 0;
+    return 0;
+}
+
+int tcpedit_set_option(tcpedit_t *t, const char *name, const char *value)
+{
+    if (!t || !name)
+        return -1;
+    while (*name == '-')
+        name++;
+    int k = find_long(name, strlen(name));
+    if (k < 0) {
+        te_seterr(t, "unknown tcpedit option --%s", name);
+        return -1;
+    }
+    return store(t, k, value);
+}
+
+int tcpedit_parse_args(tcpedit_t *t, int argc, char **argv, int *unused)
+{
+    int nun = 0;
+    for (int i = 0; i < argc; i++) {
+        const char *a = argv[i];
+        int k = -1;
+        const char *val = NULL;
+        if (a[0] == '-' && a[1] == '-' && a[2]) {
+            const char *eq = strchr(a + 2, '=');
+            k = find_long(a + 2, eq ? (size_t)(eq - (a + 2)) : strlen(a + 2));
+            if (k >= 0 && te_optdefs[k].has_arg) {
+                if (eq)
+                    val = eq + 1;
+                else if (i + 1 < argc)
+                    val = argv[++i];
+            }
+        } else if (a[0] == '-' && a[1] && !a[2]) {
+            for (int j = 0; j < OPT__N; j++)
+                if (te_optdefs[j].shortopt == a[1])
+                    k = j;
+            if (k >= 0 && te_optdefs[k].has_arg && i + 1 < argc)
+                val = argv[++i];
+        }
+        if (k < 0) {
+            if (unused)
+                unused[nun] = i;
+            nun++;
+            continue;
+        }
+        if (store(t, k, val) < 0)
+            return -1;
+    }
+    return nun;
+}
+
+/* ------------------------------------------------------------------------- */
+/* CIDR parsing (cidr.c:130-418)                                             */
+/* ------------------------------------------------------------------------- */
+static int parse_one_cidr(char *s, te_cidr_t *c)
+{
+    unsigned int o[4];
+    memset(c, 0, sizeof(*c));
+    c->masklen = 99; /* new_cidr() default (cidr.c:103) */
+    for (char *p = s; *p; ++p) {
+        if (*p == '#')
+            *p = ':';
+        else if (*p == ']') {
+            *p = 0;
+            break;
+        }
+    }
+    int n = sscanf(s, "%u.%u.%u.%u/%d", &o[0], &o[1], &o[2], &o[3], &c->masklen);
+    if (n == 4 || n == 5) {
+        if (n == 4)
+            c->masklen = 32;
+        if (c->masklen > 32)
+            return 0;
+        for (int i = 0; i < 4; i++)
+            if (o[i] > 255)
+                return 0;
+        uint8_t b[4] = {(uint8_t)o[0], (uint8_t)o[1], (uint8_t)o[2], (uint8_t)o[3]};
+        memcpy(&c->network, b, 4); /* inet_aton: network byte order */
+        c->family = 4;
+        return 1;
+    }
+    char *slash = strchr(s, '/');
+    if (slash) {
+        *slash = 0;
+        sscanf(slash + 1, "%d", &c->masklen);
+    } else {
+        c->masklen = 128;
+    }
+    if (c->masklen < 0 || c->masklen > 128)
+        return 0;
+    if (*s == '[')
+        s++;
+    if (inet_pton(AF_INET6, s, c->network6) <= 0)
+        return 0;
+    c->family = 6;
+    return 1;
+}
+
+/* mask_cidr6 (cidr.c:223-236): inside a leading "[...]" turn ':' into '#' */
+static void hide_v6_colons(char **p)
+{
+    if (**p == '[') {
+        ++*p;
+        for (char *q = *p; *q && *q != ']'; ++q)
+            if (*q == ':')
+                *q = '#';
+    }
+}
+
+/* one "from:to" element -> pair; returns 1 ok, 0 not a pair, -1 bad CIDR */
+static int parse_pair(char *piece, te_cidrmap_t *m)
+{
+    char *save = NULL, *tok;
+    te_cidr_t tmp[2];
+    int n = 0;
+    hide_v6_colons(&piece);
+    tok = strtok_r(piece, ":", &save);
+    while (tok) {
+        if (n < 2 && !parse_one_cidr(tok, &tmp[n]))
+            return -1;
+        if (n >= 2) { /* extra elements are parsed (and validated) then ignored */
+            te_cidr_t junk;
+            if (!parse_one_cidr(tok, &junk))
+                return -1;
+        }
+        n++;
+        if (save)
+            hide_v6_colons(&save);
+        tok = strtok_r(NULL, ":", &save);
+    }
+    if (n < 2)
+        return 0;
+    m->from = tmp[0];
+    m->to = tmp[1];
+    return 1;
+}
+
+static int parse_cidr_map(tcpedit_t *t, const char *arg, te_cidrmap_t *out, int32_t *nout, const char *what)
+{
+    char *s = strdup(arg), *save = NULL;
+    int n = 0, ok = 1;
+    for (char *piece = strtok_r(s, ",", &save); piece; piece = strtok_r(NULL, ",", &save)) {
+        if (n >= TE_MAX_CIDRMAP) {
+            te_seterr(t, "%s: more than %d CIDR pairs", what, TE_MAX_CIDRMAP);
+            ok = 0;
+            break;
+        }
+        int rc = parse_pair(piece, &out[n]);
+        if (rc < 0) {
+            te_seterr(t, "Unable to parse as a valid CIDR: %s", piece);
+            ok = 0;
+            break;
+        }
+        if (rc == 0) {
+            te_seterr(t, "Unable to parse %s=%s", what, arg);
+            ok = 0;
+            break;
+        }
+        n++;
+    }
+    if (ok && n == 0) {
+        te_seterr(t, "Unable to parse %s=%s", what, arg);
+        ok = 0;
+    }
+    free(s);
+    *nout = n;
+    return ok;
+}
+
+/* parse_endpoints (cidr.c:290-362): -e A:B == -N 0.0.0.0/0:A -N 0.0.0.0/0:B */
+static int parse_endpoints(tcpedit_t *t, const char *arg)
+{
+    char buf[256];
+    char *s = strdup(arg);
+    int ok = 0;
+    if (*s == '[') {
+        char *p = strstr(s, "]:[");
+        if (p) {
+            *p = 0;
+            snprintf(buf, sizeof(buf), "[::/0]:%s]", s);
+            if (parse_cidr_map(t, buf, t->cfg.cidrmap1, &t->cfg.n_cidrmap1, "--endpoints")) {
+                snprintf(buf, sizeof(buf), "[::/0]:%s", p + 2);
+                ok = parse_cidr_map(t, buf, t->cfg.cidrmap2, &t->cfg.n_cidrmap2, "--endpoints");
+            }
+        }
+    } else {
+        char *save = NULL, *a = strtok_r(s, ":", &save), *b = a ? strtok_r(NULL, ":", &save) : NULL;
+        if (a && b) {
+            snprintf(buf, sizeof(buf), "0.0.0.0/0:%s", a);
+            if (parse_cidr_map(t, buf, t->cfg.cidrmap1, &t->cfg.n_cidrmap1, "--endpoints")) {
+                snprintf(buf, sizeof(buf), "0.0.0.0/0:%s", b);
+                ok = parse_cidr_map(t, buf, t->cfg.cidrmap2, &t->cfg.n_cidrmap2, "--endpoints");
+            }
+        }
+    }
+    free(s);
+    return ok;
+}
+
+/* ------------------------------------------------------------------------- */
+/* port map -> first-match LUT (portmap.c:55-260)                            */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    long from, to;
+} pm_ent_t;
+
+static int pm_push(pm_ent_t **v, int *n, int *cap, long from, long to)
+{
+    if (*n == *cap) {
+        *cap = *cap ? *cap * 2 : 64;
+        *v = realloc(*v, sizeof(pm_ent_t) * (size_t)*cap);
+    }
+    (*v)[(*n)++] = (pm_ent_t){from, to};
+    return 1;
+}
+
+static long strict_long(const char *s, int *bad)
+{
+    char *end;
+    long v = strtol(s, &end, 10);
+    *bad = *end != '\0';
+    return v;
+}
+
+/* ports2PORT: one "<ports>:<port>" record; appends its chain (0 = syntax error) */
+static int pm_record(char *rec, pm_ent_t **v, int *n, int *cap)
+{
+    char *save = NULL, *from_s = strtok_r(rec, ":", &save), *to_s = strtok_r(NULL, ":", &save);
+    int bad;
+    if (strtok_r(NULL, ":", &save) || !from_s || !to_s)
+        return 0;
+    if (strchr(from_s, '-') && strchr(from_s, '+'))
+        return 0;
+    long to = strict_long(to_s, &bad);
+    if (bad || to < 0 || to > 65535)
+        return 0;
+    uint16_t to_n = htons((uint16_t)to);
+    if (strchr(from_s, '-')) {
+        char *s2 = NULL, *b = strtok_r(from_s, "-", &s2), *e = strtok_r(NULL, "-", &s2);
+        if (!b || !e)
+            return 0;
+        long lb = strict_long(b, &bad);
+        if (bad)
+            return 0;
+        long le = strtol(e, NULL, 10);
+        if (lb < 0 || lb > 65535 || le < 0 || le > 65535)
+            return 0;
+        for (long i = lb; i <= le; i++)
+            pm_push(v, n, cap, htons((uint16_t)i), to_n);
+        pm_push(v, n, cap, 0, 0); /* the zeroed trailing node (portmap.c:117-124) */
+    } else if (strchr(from_s, '+')) {
+        int start = *n;
+        char *s2 = NULL;
+        char *p = strtok_r(from_s, "+", &s2);
+        long f = strict_long(p, &bad);
+        if (bad)
+            return 0;
+        pm_push(v, n, cap, htons((uint16_t)f), to_n);
+        while ((p = strtok_r(NULL, "+", &s2)) != NULL) {
+            f = strict_long(p, &bad);
+            if (bad || f < 0 || f > 65535) {
+                *n = start;
+                return 0;
+            }
+            pm_push(v, n, cap, htons((uint16_t)f), to_n);
+        }
+    } else {
+        long f = strict_long(from_s, &bad);
+        if (bad || f < 0 || f > 65535)
+            return 0;
+        pm_push(v, n, cap, htons((uint16_t)f), to_n);
+    }
+    return 1;
+}
+
+/* parse_portmap: the first record must parse; later bad records are dropped */
+static int pm_parse(const char *arg, pm_ent_t **v, int *n, int *cap)
+{
+    char *s = strdup(arg), *save = NULL;
+    char *rec = strtok_r(s, ",", &save);
+    int ok = rec && pm_record(rec, v, n, cap);
+    if (ok)
+        while ((rec = strtok_r(NULL, ",", &save)) != NULL)
+            pm_record(rec, v, n, cap);
+    free(s);
+    return ok;
+}
+
+/* ------------------------------------------------------------------------- */
+/* MAC strings (mac.c:33-104)                                                */
+/* ------------------------------------------------------------------------- */
+static void mac_from_str(const char *m, uint8_t *dst)
+{
+    char *end;
+    while (isspace((unsigned char)*m))
+        m++;
+    for (int i = 0; i < 6; i++) {
+        long l = strtol(m, &end, 16);
+        if (end == m || l < 0 || l > 0xff)
+            return;
+        if (!(*end == ':' || (i == 5 && (isspace((unsigned char)*end) || *end == '\0'))))
+            return;
+        dst[i] = (uint8_t)l;
+        m = end + 1;
+    }
+}
+
+static int dual_mac(const char *arg, uint8_t *first, uint8_t *second)
+{
+    int ret = 0;
+    if (strlen(arg) <= 1)
+        return 0;
+    char *s = strdup(arg), *save = NULL;
+    char *a = strtok_r(s, ",", &save);
+    if (a && *a) {
+        mac_from_str(a, first);
+        ret = 1;
+    }
+    char *b = strtok_r(NULL, ",", &save);
+    if (b && *b) {
+        mac_from_str(b, second);
+        ret += 2;
+    }
+    free(s);
+    return ret;
+}
+
+/* ------------------------------------------------------------------------- */
+/* derivation                                                                */
+/* ------------------------------------------------------------------------- */
+static int num_arg(tcpedit_t *t, int k, long lo, long hi, long *out)
+{
+    char *end;
+    long v = strtol(t->arg[k], &end, 0);
+    if (*end != '\0' || end == t->arg[k]) {
+        te_seterr(t, "invalid number for --%s: %s", te_optdefs[k].name, t->arg[k]);
+        return 0;
+    }
+    if (v < lo || v > hi) {
+        te_seterr(t, "--%s value %ld out of range [%ld, %ld]", te_optdefs[k].name, v, lo, hi);
+        return 0;
+    }
+    *out = v;
+    return 1;
+}
+
+static int conflict(tcpedit_t *t, int a, int b)
+{
+    if (t->have[a] && t->have[b]) {
+        te_seterr(t, "--%s cannot be combined with --%s", te_optdefs[a].name, te_optdefs[b].name);
+        return 1;
+    }
+    return 0;
+}
+
+static int requires_(tcpedit_t *t, int a, int b)
+{
+    if (t->have[a] && !t->have[b]) {
+        te_seterr(t, "--%s requires --%s", te_optdefs[a].name, te_optdefs[b].name);
+        return 1;
+    }
+    return 0;
+}
+
+int te_derive_cfg(tcpedit_t *t)
+{
+    te_dev_cfg_t *c = &t->cfg;
+    long v;
+    uint32_t seed = 1, rnd = 0;
+
+    memset(c, 0, sizeof(*c));
+    free(t->portlut);
+    t->portlut = NULL;
+    c->mtu = 1500; /* DEFAULT_MTU (tcpedit.c:382) */
+    c->tos = c->tclass = c->flowlabel = -1;
+    c->vlan_tag = 65535; /* en10mb.c:117-122 */
+    c->vlan_pri = 255;
+    c->vlan_cfi = 255;
+    c->vlan_proto = 0x8100;
+    t->fuzz_seed = 0;
+    t->fuzz_factor = 8;
+
+    /* AutoOpts flags-cant / flags-must (tcpedit_opts.def, en10mb_opts.def) */
+    if (conflict(t, OPT_SEED, OPT_FUZZ_SEED) || conflict(t, OPT_PNAT, OPT_SRCIPMAP) ||
+        conflict(t, OPT_PNAT, OPT_DSTIPMAP) || conflict(t, OPT_ENET_MAC_SEED, OPT_ENET_SMAC) ||
+        conflict(t, OPT_ENET_MAC_SEED, OPT_ENET_DMAC) || conflict(t, OPT_ENET_MAC_SEED, OPT_ENET_SUBSMAC) ||
+        requires_(t, OPT_FUZZ_FACTOR, OPT_FUZZ_SEED) || requires_(t, OPT_ENET_VLAN_TAG, OPT_ENET_VLAN) ||
+        requires_(t, OPT_ENET_VLAN_CFI, OPT_ENET_VLAN) || requires_(t, OPT_ENET_VLAN_PRI, OPT_ENET_VLAN) ||
+        requires_(t, OPT_ENET_MAC_SEED_KEEP_BYTES, OPT_ENET_MAC_SEED))
+        return -1;
+
+    if (t->have[OPT_PNAT]) { /* parse_args.c:42-68 */
+        c->rewrite_ip = 1;
+        if (!parse_cidr_map(t, t->stack[OPT_PNAT][0], c->cidrmap1, &c->n_cidrmap1, "--pnat"))
+            return -1;
+        if (t->nstack[OPT_PNAT] > 1 &&
+            !parse_cidr_map(t, t->stack[OPT_PNAT][1], c->cidrmap2, &c->n_cidrmap2, "--pnat"))
+            return -1;
+    }
+    if (t->have[OPT_SRCIPMAP]) {
+        c->rewrite_ip = 1;
+        if (!parse_cidr_map(t, t->arg[OPT_SRCIPMAP], c->srcipmap, &c->n_srcipmap, "--srcipmap"))
+            return -1;
+    }
+    if (t->have[OPT_DSTIPMAP]) {
+        c->rewrite_ip = 1;
+        if (!parse_cidr_map(t, t->arg[OPT_DSTIPMAP], c->dstipmap, &c->n_dstipmap, "--dstipmap"))
+            return -1;
+    }
+    if (c->n_cidrmap1 && !c->n_cidrmap2) { /* :89-94 one -N serves both directions */
+        memcpy(c->cidrmap2, c->cidrmap1, sizeof(c->cidrmap1));
+        c->n_cidrmap2 = c->n_cidrmap1;
+    }
+    c->fixcsum = t->have[OPT_FIXCSUM] != 0;
+    c->fixhdrlen = t->have[OPT_FIXHDRLEN] != 0;
+    c->efcs = t->have[OPT_EFCS] != 0;
+    if (t->have[OPT_TTL]) { /* :109-131 */
+        const char *a = t->arg[OPT_TTL];
+        c->ttl_mode = strchr(a, '+') ? TE_TTL_ADD : (strchr(a, '-') ? TE_TTL_SUB : TE_TTL_SET);
+        long ttl = strtol(a, NULL, 10);
+        if (ttl < 0)
+            ttl = -ttl;
+        if (ttl > 255) {
+            te_seterr(t, "Invalid --ttl value (must be 0-255): %ld", ttl);
+            return -1;
+        }
+        c->ttl_value = (uint32_t)ttl;
+    }
+    if (t->have[OPT_TOS]) {
+        if (!num_arg(t, OPT_TOS, 0, 255, &v))
+            return -1;
+        c->tos = (int32_t)v;
+    }
+    if (t->have[OPT_TCLASS]) {
+        if (!num_arg(t, OPT_TCLASS, 0, 255, &v))
+            return -1;
+        c->tclass = (int32_t)v;
+    }
+    if (t->have[OPT_FLOWLABEL]) {
+        if (!num_arg(t, OPT_FLOWLABEL, 0, 1048575, &v))
+            return -1;
+        c->flowlabel = (int32_t)v;
+    }
+    if (t->have[OPT_MTU]) {
+        if (!num_arg(t, OPT_MTU, 1, 262144, &v))
+            return -1;
+        c->mtu = (int32_t)v;
+    }
+    c->mtu_truncate = t->have[OPT_MTU_TRUNC] != 0;
+    c->skip_broadcast = t->have[OPT_SKIPBROADCAST] != 0;
+    if (t->have[OPT_FIXLEN]) {
+        const char *a = t->arg[OPT_FIXLEN];
+        if (!strcmp(a, "pad"))
+            c->fixlen = TE_FIXLEN_PAD;
+        else if (!strcmp(a, "trunc"))
+            c->fixlen = TE_FIXLEN_TRUNC;
+        else if (!strcmp(a, "del"))
+            c->fixlen = TE_FIXLEN_DEL;
+        else {
+            te_seterr(t, "Invalid --fixlen=%s", a);
+            return -1;
+        }
+    }
+    if (t->have[OPT_TCP_SEQUENCE]) { /* :180-188 */
+        if (!num_arg(t, OPT_TCP_SEQUENCE, 1, 0xffffffffL, &v))
+            return -1;
+        c->tcp_sequence_enable = 1;
+        seed = (uint32_t)v;
+        for (int i = 0; i < 5; ++i)
+            rnd = te_tcpr_random(&seed);
+        c->tcp_sequence_adjust = rnd;
+    }
+    if (t->have[OPT_PORTMAP]) { /* :191-216 */
+        pm_ent_t *ents = NULL;
+        int n = 0, cap = 0;
+        for (int k = 0; k < t->nstack[OPT_PORTMAP]; k++) {
+            if (!pm_parse(t->stack[OPT_PORTMAP][k], &ents, &n, &cap)) {
+                te_seterr(t, "Unable to parse --portmap=%s", t->stack[OPT_PORTMAP][k]);
+                free(ents);
+                return -1;
+            }
+        }
+        /* map_port() returns the first match in list order: build a LUT whose
+         * index is the port as loaded from the packet (network order bytes) */
+        t->portlut = malloc(65536 * sizeof(uint16_t));
+        uint8_t *set = calloc(65536, 1);
+        for (int p = 0; p < 65536; p++)
+            t->portlut[p] = (uint16_t)p;
+        for (int i = 0; i < n; i++) {
+            uint16_t f = (uint16_t)ents[i].from;
+            if (!set[f]) {
+                set[f] = 1;
+                t->portlut[f] = (uint16_t)ents[i].to;
+            }
+        }
+        free(set);
+        free(ents);
+        c->has_portmap = 1;
+    }
+    if (t->have[OPT_SEED]) { /* :218-238 */
+        c->rewrite_ip = 1;
+        if (!num_arg(t, OPT_SEED, 0x80000000L * -1, 0xffffffffL, &v))
+            return -1;
+        seed = (uint32_t)v;
+    } else if (t->have[OPT_FUZZ_SEED]) {
+        if (!num_arg(t, OPT_FUZZ_SEED, 0, 0xffffffffL, &v))
+            return -1;
+        seed = (uint32_t)v;
+        if (t->have[OPT_FUZZ_FACTOR]) {
+            if (!num_arg(t, OPT_FUZZ_FACTOR, 1, 0xffffffffL, &v))
+                return -1;
+            t->fuzz_factor = (uint32_t)v;
+        }
+    }
+    for (int i = 0; i < 5; ++i)
+        rnd = te_tcpr_random(&seed);
+    if (t->have[OPT_SEED])
+        c->seed = seed;
+    if (t->have[OPT_FUZZ_SEED]) {
+        t->fuzz_seed = seed;
+        te_seterr(t, "--fuzz-seed is not supported by this build yet (SURVEY.md section 8f, rank 4)");
+        return -1;
+    }
+    if (t->have[OPT_ENDPOINTS]) {
+        c->rewrite_ip = 1;
+        if (!parse_endpoints(t, t->arg[OPT_ENDPOINTS])) {
+            if (!t->errstr[0])
+                te_seterr(t, "Unable to parse --endpoints=%s", t->arg[OPT_ENDPOINTS]);
+            return -1;
+        }
+    }
+
+    /* tcpedit_dlt_post_args (dlt_plugins.c:168-204): encoder = --dlt or decoder */
+    if (t->dlt != 1) {
+        te_seterr(t, "input DLT %d: only DLT_EN10MB (1) is supported by this build", t->dlt);
+        return -1;
+    }
+    if (t->have[OPT_DLT] && strcmp(t->arg[OPT_DLT], "en10mb") != 0) {
+        te_seterr(t, "--dlt=%s: only the en10mb encoder is supported by this build (SURVEY.md 8f rank 3)",
+                  t->arg[OPT_DLT]);
+        return -1;
+    }
+    if (t->have[OPT_USER_DLT] || t->have[OPT_USER_DLINK] || t->have[OPT_HDLC_CONTROL] || t->have[OPT_HDLC_ADDRESS]) {
+        te_seterr(t, "user/hdlc DLT plugin options need --dlt=user/hdlc, not supported by this build");
+        return -1;
+    }
+    c->l2_skip_broadcast = t->have[OPT_SKIPL2BROADCAST] != 0;
+
+    /* dlt_en10mb_parse_opts (en10mb.c:226-396) */
+    for (int k = 0; k < t->nstack[OPT_ENET_SUBSMAC]; k++) {
+        const char *in = t->stack[OPT_ENET_SUBSMAC][k];
+        size_t L = strlen(in), nent = L / 36 + 1; /* SUBSMAC_ENTRY_LEN + 1 */
+        for (size_t e = 0; e < nent; e++) {
+            size_t off = e * 36;
+            if (L - off < 35 || c->n_subs >= TE_MAX_SUBS) {
+                te_seterr(t, "Unable to parse --enet-subsmac=%s", in);
+                return -1;
+            }
+            uint8_t *ent = c->subs[c->n_subs];
+            memset(ent, 0, 12);
+            if (dual_mac(in + off, ent, ent + 6) != 3) {
+                te_seterr(t, "Unable to parse --enet-subsmac=%s", in);
+                return -1;
+            }
+            c->n_subs++;
+        }
+    }
+    if (t->have[OPT_ENET_MAC_SEED]) {
+        if (!num_arg(t, OPT_ENET_MAC_SEED, 0x80000000L * -1, 0xffffffffL, &v))
+            return -1;
+        c->random_set = (uint32_t)v;
+        uint32_t st = c->random_set;
+        for (int i = 0; i < 6; i++) { /* six distinct mask bytes */
+            uint8_t m = (uint8_t)te_tcpr_random(&st);
+            int dup = 0;
+            for (int j = 0; j < i; j++)
+                dup |= c->random_mask[j] == m;
+            if (dup)
+                i--;
+            else
+                c->random_mask[i] = m;
+        }
+        c->random_set = st; /* en10mb.c:253-261 leaves the PRNG state in random.set */
+        if (t->have[OPT_ENET_MAC_SEED_KEEP_BYTES]) {
+            if (!num_arg(t, OPT_ENET_MAC_SEED_KEEP_BYTES, 1, 6, &v))
+                return -1;
+            c->random_keep = (int32_t)v;
+        }
+    }
+    if (t->have[OPT_ENET_DMAC]) {
+        int r = dual_mac(t->arg[OPT_ENET_DMAC], c->intf1_dmac, c->intf2_dmac);
+        c->mac_mask |= ((r & 1) ? TE_MASK_DMAC1 : 0) | ((r & 2) ? TE_MASK_DMAC2 : 0);
+    }
+    if (t->have[OPT_ENET_SMAC]) {
+        int r = dual_mac(t->arg[OPT_ENET_SMAC], c->intf1_smac, c->intf2_smac);
+        c->mac_mask |= ((r & 1) ? TE_MASK_SMAC1 : 0) | ((r & 2) ? TE_MASK_SMAC2 : 0);
+    }
+    if (t->have[OPT_ENET_VLAN]) {
+        const char *a = t->arg[OPT_ENET_VLAN];
+        if (!strcmp(a, "add"))
+            c->vlan = TE_VLAN_ADD;
+        else if (!strcmp(a, "del"))
+            c->vlan = TE_VLAN_DEL;
+        else {
+            te_seterr(t, "Invalid --enet-vlan=%s", a);
+            return -1;
+        }
+        if (c->vlan == TE_VLAN_ADD) {
+            if (!t->have[OPT_ENET_VLAN_TAG]) {
+                te_seterr(t, "Must specify a new 802.1 VLAN tag if vlan mode is add");
+                return -1;
+            }
+            if (!num_arg(t, OPT_ENET_VLAN_TAG, 0, 4095, &v))
+                return -1;
+            c->vlan_tag = (uint32_t)v;
+            if (t->have[OPT_ENET_VLAN_PRI]) {
+                if (!num_arg(t, OPT_ENET_VLAN_PRI, 0, 7, &v))
+                    return -1;
+                c->vlan_pri = (uint32_t)v;
+            }
+            if (t->have[OPT_ENET_VLAN_CFI]) {
+                if (!num_arg(t, OPT_ENET_VLAN_CFI, 0, 1, &v))
+                    return -1;
+                c->vlan_cfi = (uint32_t)v;
+            }
+        }
+        if (t->have[OPT_ENET_VLAN_PROTO]) {
+            const char *p = t->arg[OPT_ENET_VLAN_PROTO];
+            if (!strcasecmp(p, "802.1q"))
+                c->vlan_proto = 0x8100;
+            else if (!strcasecmp(p, "802.1ad"))
+                c->vlan_proto = 0x88A8;
+            else {
+                te_seterr(t, "VLAN protocol \"%s\" is invalid", p);
+                return -1;
+            }
+        }
+    }
+    c->skip_soft_errors = t->have[OPT_SKIP_SOFT_ERRORS] != 0;
+    t->post_args_done = 1;
+    t->dev_dirty = 1;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* programmatic setters (tcpedit_api.c:33-353)                               */
+/* ------------------------------------------------------------------------- */
+#define SETFLAG(fn, field)                     \
+    int fn(tcpedit_t *t, int v)                \
+    {                                          \
+        if (!t)                                \
+            return TCPEDIT_ERROR;              \
+        t->cfg.field = v ? 1 : 0;              \
+        t->dev_dirty = 1;                      \
+        return TCPEDIT_OK;                     \
+    }
+SETFLAG(tcpedit_set_skip_broadcast, skip_broadcast)
+SETFLAG(tcpedit_set_fixcsum, fixcsum)
+SETFLAG(tcpedit_set_fixhdrlen, fixhdrlen)
+SETFLAG(tcpedit_set_efcs, efcs)
+SETFLAG(tcpedit_set_mtu_truncate, mtu_truncate)
+
+int tcpedit_set_ttl_mode(tcpedit_t *t, int m)
+{
+    if (!t || m < 0 || m > 3)
+        return TCPEDIT_ERROR;
+    t->cfg.ttl_mode = m;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_ttl_value(tcpedit_t *t, uint8_t v)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.ttl_value = v;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_tos(tcpedit_t *t, uint8_t v)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.tos = v;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_tclass(tcpedit_t *t, uint8_t v)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.tclass = v;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_flowlabel(tcpedit_t *t, uint32_t v)
+{
+    if (!t || v > 1048575)
+        return TCPEDIT_ERROR;
+    t->cfg.flowlabel = (int32_t)v;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_seed(tcpedit_t *t)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.seed = (uint32_t)random();
+    t->cfg.rewrite_ip = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_mtu(tcpedit_t *t, int mtu)
+{
+    if (!t || mtu < 1 || mtu > 262144)
+        return TCPEDIT_ERROR;
+    t->cfg.mtu = mtu;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_maxpacket(tcpedit_t *t, int v)
+{
+    (void)v; /* tcpedit_t.maxpacket is set but never read on the edit path */
+    return t ? TCPEDIT_OK : TCPEDIT_ERROR;
+}
+int tcpedit_set_fixlen(tcpedit_t *t, int v)
+{
+    if (!t || v < 0 || v > 3)
+        return TCPEDIT_ERROR;
+    t->cfg.fixlen = v;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_tcp_sequence(tcpedit_t *t, uint32_t adjust)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.tcp_sequence_enable = 1;
+    t->cfg.tcp_sequence_adjust = adjust;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_cidrmap_s2c(tcpedit_t *t, char *s)
+{
+    if (!t || !s || !parse_cidr_map(t, s, t->cfg.cidrmap2, &t->cfg.n_cidrmap2, "cidrmap"))
+        return TCPEDIT_ERROR;
+    t->cfg.rewrite_ip = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_cidrmap_c2s(tcpedit_t *t, char *s)
+{
+    if (!t || !s || !parse_cidr_map(t, s, t->cfg.cidrmap1, &t->cfg.n_cidrmap1, "cidrmap"))
+        return TCPEDIT_ERROR;
+    t->cfg.rewrite_ip = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_srcip_map(tcpedit_t *t, char *s)
+{
+    if (!t || !s || !parse_cidr_map(t, s, t->cfg.srcipmap, &t->cfg.n_srcipmap, "srcipmap"))
+        return TCPEDIT_ERROR;
+    t->cfg.rewrite_ip = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_dstip_map(tcpedit_t *t, char *s)
+{
+    if (!t || !s || !parse_cidr_map(t, s, t->cfg.dstipmap, &t->cfg.n_dstipmap, "dstipmap"))
+        return TCPEDIT_ERROR;
+    t->cfg.rewrite_ip = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}
+int tcpedit_set_port_map(tcpedit_t *t, char *s)
+{
+    pm_ent_t *ents = NULL;
+    int n = 0, cap = 0;
+    if (!t || !s || !pm_parse(s, &ents, &n, &cap)) {
+        free(ents);
+        return TCPEDIT_ERROR;
+    }
+    if (!t->portlut) {
+        t->portlut = malloc(65536 * sizeof(uint16_t));
+        for (int p = 0; p < 65536; p++)
+            t->portlut[p] = (uint16_t)p;
+    }
+    /* appended records only apply to ports no earlier record matched */
+    uint8_t *set = calloc(65536, 1);
+    for (int p = 0; p < 65536; p++)
+        set[p] = t->portlut[p] != p;
+    for (int i = 0; i < n; i++) {
+        uint16_t f = (uint16_t)ents[i].from;
+        if (!set[f]) {
+            set[f] = 1;
+            t->portlut[f] = (uint16_t)ents[i].to;
+        }
+    }
+    free(set);
+    free(ents);
+    t->cfg.has_portmap = 1;
+    t->dev_dirty = 1;
+    return TCPEDIT_OK;
+}

@@ -1,0 +1,74 @@
+/*
+ * te_internal.h -- host-side state of a tcpedit context (the counterpart of
+ * the reference's tcpedit_t, tcpedit_types.h:91-153, whose per-packet half now
+ * lives in te_dev_cfg_t on the GPU).
+ */
+#ifndef TE_INTERNAL_H
+#define TE_INTERNAL_H
+
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__
+#endif
+#include <hip/hip_runtime_api.h>
+#include <stdbool.h>
+#include <stdint.h>
+#include "../../../include/tcpedit.h"
+#include "te_dev_cfg.h"
+#include "te_kernels.h"
+
+#define TE_ERRSTR_LEN 1024
+#define TE_MAX_STACK 256
+
+/* option ids of the tcpedit + DLT option surface */
+enum {
+    OPT_PORTMAP, OPT_SEED, OPT_PNAT, OPT_SRCIPMAP, OPT_DSTIPMAP, OPT_ENDPOINTS, OPT_TCP_SEQUENCE, OPT_SKIPBROADCAST,
+    OPT_FIXCSUM, OPT_FIXHDRLEN, OPT_MTU, OPT_MTU_TRUNC, OPT_EFCS, OPT_TTL, OPT_TOS, OPT_TCLASS, OPT_FLOWLABEL,
+    OPT_FIXLEN, OPT_FUZZ_SEED, OPT_FUZZ_FACTOR, OPT_DLT, OPT_SKIPL2BROADCAST, OPT_ENET_DMAC, OPT_ENET_SMAC,
+    OPT_ENET_SUBSMAC, OPT_ENET_MAC_SEED, OPT_ENET_MAC_SEED_KEEP_BYTES, OPT_ENET_VLAN, OPT_ENET_VLAN_TAG,
+    OPT_ENET_VLAN_CFI, OPT_ENET_VLAN_PRI, OPT_ENET_VLAN_PROTO, OPT_SKIP_SOFT_ERRORS, OPT_USER_DLT, OPT_USER_DLINK,
+    OPT_HDLC_CONTROL, OPT_HDLC_ADDRESS, OPT__N
+};
+
+typedef struct {
+    const char *name;
+    char shortopt;
+    int has_arg;
+    int max;       /* AutoOpts `max` (stacked options allow many) */
+    int stacked;
+} te_optdef_t;
+
+extern const te_optdef_t te_optdefs[OPT__N];
+
+struct tcpedit_s {
+    int validated;
+    int dlt;                      /* input DLT */
+    int device;
+    /* option store (AutoOpts stand-in) */
+    int have[OPT__N];
+    char *arg[OPT__N];
+    char *stack[OPT__N][TE_MAX_STACK];
+    int nstack[OPT__N];
+    /* derived per-run tables */
+    te_dev_cfg_t cfg;
+    uint16_t *portlut;            /* host copy, 65536 entries, or NULL */
+    uint32_t fuzz_seed, fuzz_factor;
+    int post_args_done;
+    /* runtime (tcpedit_runtime_t, tcpedit_types.h:49-61) */
+    uint64_t packetnum, total_bytes, pkts_edited;
+    char errstr[TE_ERRSTR_LEN];
+    char warnstr[TE_ERRSTR_LEN];
+    /* device side */
+    hipStream_t stream;
+    te_dev_cfg_t *d_cfg;
+    uint16_t *d_portlut;
+    int dev_dirty;                /* cfg changed since last upload */
+    tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */
+};
+
+void te_seterr(tcpedit_t *t, const char *fmt, ...);
+void te_setwarn(tcpedit_t *t, const char *fmt, ...);
+uint32_t te_tcpr_random(uint32_t *seed);
+int te_derive_cfg(tcpedit_t *t); /* tcpedit_post_args body */
+int te_upload_cfg(tcpedit_t *t);
+
+#endif

@@ -1,0 +1,96 @@
+/*
+ * te_dev_cfg.h -- the per-run constant tables the host derives once from the
+ * tcpedit option surface (tcpedit_post_args, src/tcpedit/parse_args.c:34-254,
+ * and dlt_en10mb_parse_opts, src/tcpedit/plugins/dlt_en10mb/en10mb.c:226-396)
+ * and hands to the gfx950 kernels.  Plain C POD: included by the C host code
+ * and by the HIP kernels.  Lists the reference keeps as linked lists (CIDR maps,
+ * --enet-subsmac) become bounded arrays; the port map becomes a 64 K-entry
+ * first-match lookup table held separately in HBM.
+ */
+#ifndef TE_DEV_CFG_H
+#define TE_DEV_CFG_H
+
+#include <stdint.h>
+
+#define TE_MAX_CIDRMAP 16
+#define TE_MAX_SUBS 32
+
+/* tcpr_cidr_t (src/common/cidr.h) */
+typedef struct {
+    int32_t family;  /* 4 or 6 */
+    int32_t masklen;
+    uint32_t network; /* network byte order as inet_aton stores it */
+    uint8_t network6[16];
+} te_cidr_t;
+
+/* tcpr_cidrmap_t: one from->to pair */
+typedef struct {
+    te_cidr_t from, to;
+} te_cidrmap_t;
+
+enum { TE_TTL_OFF = 0, TE_TTL_SET, TE_TTL_ADD, TE_TTL_SUB };       /* tcpedit_types.h:38-43 */
+enum { TE_FIXLEN_OFF = 0, TE_FIXLEN_PAD, TE_FIXLEN_TRUNC, TE_FIXLEN_DEL };
+enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };                  /* en10mb_types.h:50-54 */
+enum { TE_MASK_SMAC1 = 1, TE_MASK_SMAC2 = 2, TE_MASK_DMAC1 = 4, TE_MASK_DMAC2 = 8 };
+enum { TE_DIR_NOSEND = 0, TE_DIR_C2S = 1, TE_DIR_S2C = 2 };          /* cache.h:77-80 */
+
+typedef struct {
+    /* tcpedit_t (tcpedit_types.h:91-153) */
+    uint8_t skip_broadcast, rewrite_ip, fixcsum, efcs;
+    uint8_t mtu_truncate, fixhdrlen, l2_skip_broadcast, skip_soft_errors;
+    int32_t fixlen;
+    int32_t ttl_mode;
+    uint32_t ttl_value;
+    int32_t tos, flowlabel, tclass, mtu;
+    uint32_t tcp_sequence_enable, tcp_sequence_adjust;
+    uint32_t seed;
+    int32_t has_portmap;
+    int32_t n_cidrmap1, n_cidrmap2, n_srcipmap, n_dstipmap;
+    te_cidrmap_t cidrmap1[TE_MAX_CIDRMAP];
+    te_cidrmap_t cidrmap2[TE_MAX_CIDRMAP];
+    te_cidrmap_t srcipmap[TE_MAX_CIDRMAP];
+    te_cidrmap_t dstipmap[TE_MAX_CIDRMAP];
+    /* en10mb_config_t (en10mb_types.h:60-92) */
+    uint8_t intf1_dmac[6], intf1_smac[6], intf2_dmac[6], intf2_smac[6];
+    int32_t n_subs;
+    uint8_t subs[TE_MAX_SUBS][12]; /* target[6], rewrite[6] */
+    uint32_t random_set;
+    int32_t random_keep;
+    uint8_t random_mask[8];
+    int32_t mac_mask;
+    int32_t vlan;
+    uint32_t vlan_tag; /* 65535 = unset */
+    uint32_t vlan_pri; /* 255 = unset */
+    uint32_t vlan_cfi; /* 255 = unset */
+    uint32_t vlan_proto;
+} te_dev_cfg_t;
+
+/* Per-packet status byte written by the device (one per input record). */
+enum {
+    TE_ST_RC_MASK = 0x03, /* low 2 bits: 0 OK, 1 WARN, 2 SOFT_ERROR, 3 ERROR */
+    TE_ST_RC_OK = 0,
+    TE_ST_RC_WARN = 1,
+    TE_ST_RC_SOFT = 2,
+    TE_ST_RC_ERROR = 3,
+    TE_ST_DROPPED = 0x04,     /* soft error suppressed by --skip-soft-errors */
+    TE_ST_NOSEND = 0x08,      /* cache said NOSEND: written unedited */
+    TE_ST_UNSUPPORTED = 0x10, /* output would depend on bytes outside the packet */
+    TE_ST_WARNED = 0x20,      /* a checksum warning was emitted (tcpedit.c:351-353) */
+    TE_ST_ZEROCAP = 0x40,     /* caplen 0 after editing: not written (tcprewrite.c:367) */
+};
+
+/* Counters reduced across tiles (and across GPUs by one RCCL all-reduce). */
+enum {
+    TE_CNT_PACKETS = 0,
+    TE_CNT_BYTES_IN,
+    TE_CNT_BYTES_OUT,
+    TE_CNT_WRITTEN,
+    TE_CNT_EDITED,
+    TE_CNT_SOFT,
+    TE_CNT_WARN,
+    TE_CNT_ERROR,
+    TE_CNT_UNSUPPORTED,
+    TE_CNT__N
+};
+
+#endif

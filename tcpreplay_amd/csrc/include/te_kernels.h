@@ -1,0 +1,69 @@
+/*
+ * te_kernels.h -- the boundary between the C host code and the gfx950 kernels
+ * (plain pointers and sizes only).  Shared by tcpedit_kernels.hip and the host.
+ */
+#ifndef TE_KERNELS_H
+#define TE_KERNELS_H
+
+#include <stdint.h>
+#include "te_dev_cfg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TE_BLOCK 256           /* threads per block = max packets per tile */
+#define TE_MAX_PKTS 256
+#define TE_SLOT_BYTES 36864    /* LDS slot budget per block (4 blocks / CU) */
+#define TE_HEAD 16             /* headroom before each record (VLAN push) */
+#define TE_TAIL_BYTES 16       /* zeroed bytes after each packet's data */
+#define TE_NO_SCRATCH 0xffffffffffffffffull
+
+/* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
+ * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
+#define TE_SLOT_BYTES_OF(g, data) \
+    ((((uint32_t)TE_HEAD + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
+
+/* A tile = a run of consecutive pcap records processed by one block. */
+typedef struct {
+    uint64_t span_off;    /* HBM offset of the first record (its 16-byte header) */
+    uint64_t scratch_off; /* TE_NO_SCRATCH, or the HBM scratch slot of a huge record */
+    uint32_t first_pkt;   /* index of the first record in this run */
+    uint32_t npkt;
+    uint32_t span_len;    /* bytes of records in the tile */
+    uint32_t pad_;
+} te_tile_t;
+
+typedef struct {
+    const te_dev_cfg_t *cfg;  /* device pointer */
+    const uint16_t *portlut;  /* device: 65536-entry first-match port map, or NULL */
+    const uint8_t *dirbits;   /* device: tcpprep cache data, or NULL */
+    uint64_t dirbits_len;
+    uint64_t pkt_base;        /* 0-based packet number of the first record */
+    int32_t fixed_dir;        /* >= 0: direction for every record (tcpedit_packet); -1: cache/C2S */
+    const uint8_t *in;        /* device: input pcap image */
+    const te_tile_t *tiles;   /* device */
+    const uint16_t *pkt_rel;  /* device: record offset relative to its tile */
+    uint32_t n_tiles;
+    uint32_t in_swapped, in_nsec;
+    uint8_t *out;             /* device: output pcap image */
+    uint64_t out_base;        /* offset of the first output record */
+    uint64_t *tile_state;     /* device: n_tiles look-back granules */
+    unsigned int *ticket;     /* device */
+    uint8_t *status;          /* device: one byte per record */
+    uint64_t *counters;       /* device: TE_CNT__N */
+    uint64_t *err;            /* device: [0] first error record, [1] its output offset, [2] timeouts */
+    uint8_t *scratch;         /* device: huge-record slots */
+    void *zero_region;        /* device range zeroed before each launch */
+    uint64_t zero_bytes;
+    int grid;                 /* blocks to launch (persistent, tiles taken by ticket) */
+} te_launch_t;
+
+#ifdef __HIP_PLATFORM_AMD__
+int te_launch_edit(const te_launch_t *L, hipStream_t stream);
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+#endif

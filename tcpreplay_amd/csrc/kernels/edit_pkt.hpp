@@ -1,0 +1,1196 @@
+// edit_pkt.hpp -- per-packet tcpedit logic for gfx950, one packet per lane.
+//
+// Restates the reference's per-packet path (src/tcpedit/tcpedit.c:46-366 and
+// everything it calls, DLT_EN10MB in and out) over a packet "slot": the packet's
+// 16-byte pcap record header followed by its bytes, staged in LDS by the tile
+// kernel (or in an HBM scratch slot for packets larger than a tile), with
+//   * >= 4 bytes of headroom before the record header, so a VLAN push shifts the
+//     (short) L2 head left instead of memmove-ing the whole payload right, and
+//   * TE_TAIL zeroed bytes after the payload, the only bytes past caplen that the
+//     reference may legitimately touch without depending on an earlier packet.
+// Anything the reference would READ past caplen (its static buffer's stale bytes,
+// SURVEY Appendix B Q8) is detected and flagged TE_ST_UNSUPPORTED instead.
+//
+// Byte order: like the reference on x86, multi-byte fields are loaded in host
+// (little-endian) order and all checksum arithmetic runs on those LE values.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "te_dev_cfg.h"
+#include "te_kernels.h"
+
+namespace te {
+
+constexpr int TE_TAIL = TE_TAIL_BYTES;    // zeroed bytes materialised after each packet
+constexpr uint32_t MAX_SNAPLEN = 262144;  // defines.h.in:177
+constexpr uint32_t MAXPACKET = MAX_SNAPLEN + 22;
+
+constexpr int RC_SOFT = -2, RC_ERROR = -1, RC_OK = 0, RC_WARN = 1;  // tcpedit_types.h:31-34
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+
+#define DI __device__ __forceinline__
+
+DI u16 bswap16(u16 v) { return (u16)((v >> 8) | (v << 8)); }
+DI u32 bswap32(u32 v) { return __builtin_bswap32(v); }
+DI u16 ld16(const u8 *p) { return (u16)(p[0] | (p[1] << 8)); }
+DI u32 ld32(const u8 *p) { return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24); }
+DI void st16(u8 *p, u16 v) { p[0] = (u8)v; p[1] = (u8)(v >> 8); }
+DI void st32(u8 *p, u32 v) { p[0] = (u8)v; p[1] = (u8)(v >> 8); p[2] = (u8)(v >> 16); p[3] = (u8)(v >> 24); }
+DI u16 be16(const u8 *p) { return (u16)((p[0] << 8) | p[1]); }  // ntohs(ld16)
+DI u32 be32(const u8 *p) { return bswap32(ld32(p)); }
+
+// ---------------------------------------------------------------------------
+// Per-packet context: what the slot holds and what the reference's
+// tcpeditdlt_t / en10mb_extra_t decode state carries for this packet.
+// ---------------------------------------------------------------------------
+struct Pkt {
+    u8 *d;        // packet data (record header sits at d - 16)
+    u32 caplen;   // current pcap caplen
+    u32 len;      // current pcap len
+    u32 avail;    // bytes materialised from d (>= caplen; the rest of the slot is the zero tail)
+    bool unsupported;
+};
+
+struct Dec {  // tcpeditdlt_t + en10mb_extra_t fields the encode/merge steps read
+    u8 dstaddr[6], srcaddr[6];
+    int proto;           // ctx->proto (network-order ethertype value)
+    int proto_vlan_tag;  // ctx->proto_vlan_tag
+    int l2offset, l2len;
+    int vlan;
+    u32 vlan_offset;
+    u16 vlan_tag, vlan_pri, vlan_cfi, vlan_proto;
+};
+
+// ---------------------------------------------------------------------------
+// L2 chain walk: get_l2len_protocol (src/common/get.c:262-451) for DLT_EN10MB,
+// with parse_vlan (:170-182), parse_mpls (:87-157), parse_metadata (:196-236).
+// Returns 0 and fills protocol/l2len/l2offset/vlan_offset, or -1.
+// ---------------------------------------------------------------------------
+struct L2 {
+    u16 protocol;
+    u32 l2len, l2offset, vlan_offset;
+};
+
+DI int get_l2len_protocol(const u8 *pkt, u32 datalen, L2 &r) {
+    r.protocol = 0;
+    r.l2len = 0;
+    r.l2offset = 0;
+    r.vlan_offset = 0;
+    if (datalen == 0) return -1;
+    u32 l2_net_off = 14;
+    if (datalen <= l2_net_off + 4) return -1;
+    u16 et = be16(pkt + 12);
+    // bounded walk: every step consumes >= 4 bytes of a <= MAXPACKET buffer
+    for (int guard = 0; guard < 65536; ++guard) {
+        if (et == 0x8100 || et == 0x88A8 || et == 0x9100) {
+            if (r.vlan_offset == 0) r.vlan_offset = l2_net_off;
+            if (datalen < l2_net_off + 4) return -1;
+            et = be16(pkt + l2_net_off + 2);
+            l2_net_off += 4;
+        } else if (et == 0x8847 || et == 0x8848) {
+            u32 len = l2_net_off;
+            bool bos = false;
+            const u8 *lab = nullptr;
+            while (!bos) {
+                if ((uint64_t)len + 4 > datalen) return -1;
+                lab = pkt + len;
+                len += 4;
+                u32 entry = be32(lab);
+                bos = (entry & 0x100u) != 0;
+                if ((entry >> 12) == 13) return -1;  // MPLS_LABEL_GACH
+            }
+            if ((u32)(lab + 4 - pkt) + 1 > datalen) return -1;
+            u8 nib = lab[4] >> 4;
+            if (nib == 4) {
+                et = 0x0800;
+            } else if (nib == 6) {
+                et = 0x86DD;
+            } else if (nib == 0) {  // EoMPLS: skip PW control word, inner Ethernet
+                if ((uint64_t)len + 4 + 14 > datalen) return -1;
+                len += 4;
+                r.l2offset = len;
+                et = be16(pkt + len + 12);
+                len += 14;
+            } else {
+                return -1;
+            }
+            l2_net_off = len;
+        } else {
+            break;
+        }
+    }
+    r.l2len = l2_net_off;
+    if (et >= 1536) {
+        r.protocol = et;
+        return 0;
+    }
+    return -1;  // 802.3 length field / unsupported (get.c:367-380)
+}
+
+// get_l2len (get.c:456-470): 0 on failure
+DI int get_l2len(const u8 *pkt, u32 datalen) {
+    L2 r;
+    if (get_l2len_protocol(pkt, datalen, r) == -1) return 0;
+    return (int)r.l2len;
+}
+
+// dlt_en10mb_l2len (en10mb.c:917-943)
+DI int en10mb_l2len(const u8 *pkt, int pktlen) {
+    if (pktlen < 14) return -1;
+    int l2 = get_l2len(pkt, (u32)pktlen);
+    if (l2 > 0) return pktlen < l2 ? -1 : l2;
+    return -1;
+}
+
+// ---------------------------------------------------------------------------
+// L4 locators: get_layer4_v4 (get.c:611-625), get_ipv6_next (:757-800),
+// get_layer4_v6 (:646-750), get_ipv6_l4proto (:806-853).  Offsets are byte
+// offsets from the IP header; `end` is the offset of end_ptr.  -1 = NULL.
+// ---------------------------------------------------------------------------
+DI int l4_v4(const u8 *ip, int end) {
+    int p = (ip[0] & 0x0f) << 2;
+    return p > end ? -1 : p;
+}
+
+DI int ipv6_next(const u8 *ip, int ext, int end) {
+    if (ext + 2 > end) return -1;
+    switch (ip[ext]) {
+        case 59: case 50: return -1;  // NO_NEXT, ESP
+        case 44: return ext + 8 > end ? -1 : ext + 8;  // FRAGMENT: fixed 8 bytes
+        case 41: case 43: case 60: case 0: case 51: {
+            u8 extlen = (u8)(ip[ext + 1] * 4 + 8);  // IPV6_EXTLEN_TO_BYTES truncated to u8 (get.c:781)
+            if (extlen == 0) return -1;
+            return ext + extlen > end ? -1 : ext + extlen;
+        }
+        default: return ext;  // not an extension header: returns itself
+    }
+}
+
+// get_layer4_v6.  Its NH_IPV6 case re-recurses with an unchanged proto until
+// a call returns NULL (get.c:677-680 + :742-743), and every call advances the
+// pointer by >= 40 bytes, so any v6-in-v6 header yields NULL.
+DI int l4_v6(const u8 *ip, int base, int end) {
+    int next = base + 40;
+    if (next > end) return -1;
+    u8 first = ip[base + 6];
+    u8 proto = first;
+    for (int guard = 0; guard < 4096; ++guard) {
+        if (proto == 41) return -1;
+        if (proto == 51 || proto == 43 || proto == 60 || proto == 0 || proto == 44) {
+            int ex = ipv6_next(ip, next, end);
+            if (ex < 0 || ex + 2 > end) return -1;
+            proto = ip[ex];
+            next = ex;
+            continue;
+        }
+        if (proto == 50) return -1;  // ESP
+        if (proto != first) {
+            if (next + 2 > end) return -1;
+            next = next + (ip[next + 1] * 4 + 8);  // not truncated here (get.c:728)
+            if (next > end) return -1;
+        }
+        return next;
+    }
+    return -1;
+}
+
+DI u8 l4proto_v6(const u8 *ip, int end) {
+    int base = 0;
+    for (int depth = 0; depth < 64; ++depth) {
+        int ptr = base + 40;
+        if (ptr > end) return 59;
+        u8 proto = ip[base + 6];
+        bool recurse = false;
+        for (int guard = 0; guard < 4096; ++guard) {
+            if (proto == 59 || proto == 44 || proto == 50) return proto;
+            if (proto == 41) {
+                recurse = true;
+                break;
+            }
+            if (proto == 51 || proto == 43 || proto == 60 || proto == 0) {
+                int ex = ipv6_next(ip, ptr, end);
+                if (ex < 0 || ex + 2 > end) return 59;
+                proto = ip[ex];
+                ptr = ex;
+                continue;
+            }
+            return proto;
+        }
+        if (!recurse) return 59;
+        base = ptr;
+    }
+    return 59;
+}
+
+// ---------------------------------------------------------------------------
+// One's-complement sums (checksum.c:175-196 do_checksum_math semantics).
+// The reference adds little-endian u16 loads relative to the start pointer
+// (odd trailing byte as the low byte) into an int; only that sum's
+// end-around-carry fold is observable, so we accumulate 32-bit words in a u64
+// over aligned loads and fold, byte-swapping when the start is odd.
+// ---------------------------------------------------------------------------
+DI u32 fold16(unsigned long long s) {
+    while (s >> 16) s = (s & 0xffffull) + (s >> 16);
+    return (u32)s;
+}
+
+// sum of `len` bytes at p, weights relative to p (even offset -> low byte).
+DI u32 csum_bytes(const u8 *p, int len) {
+    if (len <= 0) return 0;
+    uintptr_t a = (uintptr_t)p;
+    const u8 *b = p;
+    unsigned long long s = 0;
+    int i = 0;
+    // head: bytes until 4-aligned (absolute weights)
+    while (i < len && ((a + i) & 3)) {
+        s += (u32)b[i] << (8 * ((a + i) & 1));
+        ++i;
+    }
+    const u32 *w = (const u32 *)(b + i);
+    int nw = (len - i) >> 2;
+    for (int k = 0; k < nw; ++k) s += w[k];
+    i += nw << 2;
+    for (; i < len; ++i) s += (u32)b[i] << (8 * ((a + i) & 1));
+    u32 f = fold16(s);
+    if (a & 1) f = ((f >> 8) | (f << 8)) & 0xffff;  // absolute -> relative weights
+    return f;
+}
+
+// CHECKSUM_CARRY (checksum.h:25) applied to a plain non-negative sum
+DI u16 csum_carry(unsigned long long x) { return (u16)(~fold16(x) & 0xffff); }
+
+// ---------------------------------------------------------------------------
+// RFC 1624 incremental updates: incremental_checksum.h:46-118, .c:40-118
+// ---------------------------------------------------------------------------
+DI u16 csum_fold32(u32 sum) {
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum = (sum & 0xffff) + (sum >> 16);
+    return (u16)~sum;
+}
+DI u32 csum_add(u32 c, u32 a) {
+    u32 r = c + a;
+    return r + (r < a);
+}
+DI u16 csum16_add(u16 c, u16 a) {
+    u16 r = (u16)(c + a);
+    return (u16)(r + (r < a));
+}
+DI void csum_replace2(u8 *sp, u16 from, u16 to) {
+    u16 s = ld16(sp);
+    st16(sp, (u16)~csum16_add(csum16_add((u16)~s, (u16)~from), to));
+}
+DI void csum_replace4(u8 *sp, u32 from, u32 to) {
+    u16 s = ld16(sp);
+    st16(sp, csum_fold32(csum_add(csum_add(~(u32)s, ~from), to)));
+}
+DI void csum_replace16(u8 *sp, const u8 *from, const u8 *to) {
+    // csum_partial over {~from[0..3], to[0..3]} (do_csum on an aligned 32-byte array)
+    u32 result = 0, carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u32 w = i < 4 ? ~ld32(from + 4 * i) : ld32(to + 4 * (i - 4));
+        result += carry;
+        result += w;
+        carry = (w > result);
+    }
+    result += carry;
+    result = (result & 0xffff) + (result >> 16);
+    result = (result & 0xffff) + (result >> 16);
+    result = (result & 0xffff) + (result >> 16);
+    u32 wsum = ~(u32)ld16(sp);
+    result += wsum;
+    if (wsum > result) result += 1;
+    st16(sp, csum_fold32(result));
+}
+
+// ---------------------------------------------------------------------------
+// Small predicates
+// ---------------------------------------------------------------------------
+DI bool mcast4(u32 ip_le) { return (bswap32(ip_le) & 0xf0000000u) == 0xe0000000u; }  // edit_packet.c:1204
+DI bool mcast6(const u8 *a) { return a[0] == 0xff; }                                  // :1229
+
+DI bool is_unicast_ethernet(const u8 *e) {  // plugins/ethernet.c:30-57
+    if (e[0] == 0xff && e[1] == 0xff && e[2] == 0xff && e[3] == 0xff && e[4] == 0xff && e[5] == 0xff) return false;
+    if (e[0] == 0x01 && e[1] == 0x00 && e[2] == 0x5e) return false;
+    if (e[0] == 0x33 && e[1] == 0x33) return false;
+    if (e[0] == 0x00 && e[1] == 0x00 && e[2] == 0x50 && e[3] == 0x00 && (e[4] == 0x01 || e[4] == 0x02))
+        return false;  // IPV4_VRRP / IPV6_VRRP (defines.h.in:226-227)
+    return true;
+}
+
+// ip_in_cidr (cidr.c:425-468): 64-bit mask semantics
+DI bool ip_in_cidr(const te_cidr_t &c, u32 ip_le) {
+    if (c.family != 4) return false;
+    if (c.masklen == 0 && c.network == 0) return true;
+    unsigned long long mask = ~0ull << (32 - c.masklen);
+    return (((unsigned long long)bswap32(ip_le)) & mask) == (((unsigned long long)bswap32(c.network)) & mask);
+}
+
+// ip6_in_cidr (cidr.c:478-529)
+DI bool ip6_in_cidr(const te_cidr_t &c, const u8 *a) {
+    if (c.family != 6) return false;
+    if (c.masklen == 0 && (ld32(a) | ld32(a + 4) | ld32(a + 8) | ld32(a + 12)) == 0) return true;
+    u32 j = (u32)c.masklen / 8;
+    for (u32 i = 0; i < j; ++i)
+        if (a[i] != c.network6[i]) return false;
+    u32 k = (u32)c.masklen % 8;
+    if (k == 0) return true;
+    k = ~0u << (8 - k);
+    return (a[j] & k) == (c.network6[j] & k);
+}
+
+// remap_ipv4 (edit_packet.c:713-746); x86 masks a shift by 32 to 0
+DI u32 remap_ipv4(const te_dev_cfg_t &cfg, const te_cidr_t &c, u32 orig) {
+    if (c.family != 4) return 0;
+    if (cfg.skip_broadcast && mcast4(orig)) return orig;
+    u32 mask = 0xffffffffu << ((32 - c.masklen) & 31);
+    u32 network = bswap32(c.network) & mask;
+    mask ^= 0xffffffffu;
+    return bswap32(network ^ (bswap32(orig) & mask));
+}
+
+// remap_ipv6 (edit_packet.c:748-779) incl. its out-of-range write for
+// non-octet masks, with x86's 5-bit shift-count masking.
+// `addr_off` is the address offset from `base`; returns false if the stray
+// write would land outside the materialised slot.
+DI bool remap_ipv6(const te_dev_cfg_t &cfg, const te_cidr_t &c, u8 *addr, int room_after_addr) {
+    if (c.family != 6) return true;
+    if (cfg.skip_broadcast && mcast6(addr)) return true;
+    u32 j = (u32)c.masklen / 8;
+    for (u32 i = 0; i < j; ++i) addr[i] = c.network6[i];
+    u32 k = (u32)c.masklen % 8;
+    if (k == 0) return true;
+    k = ~0u << (8 - k);
+    u32 i = addr[j] & k;
+    if ((int)i >= room_after_addr) return false;
+    u32 s1 = (8u - k) & 31u, s2 = k & 31u;
+    addr[i] = (u8)((c.network6[j] & (0xffu << s1)) | (addr[i] & (0xffu >> s2)));
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Full checksum: do_checksum (checksum.c:34-170).  `ip` = L3 header, `end` =
+// offset of end_ptr.  Reads past the materialised slot mark the packet.
+// ---------------------------------------------------------------------------
+DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
+    if (len <= 0) return RC_ERROR;
+    bool v6 = (ip[0] >> 4) == 6;
+    int ip_hl;
+    if (v6) {
+        proto = l4proto_v6(ip, end);
+        int l4 = l4_v6(ip, 0, end);
+        if (l4 < 0) return RC_WARN;
+        ip_hl = l4;
+        len -= (ip_hl - 40);
+    } else {
+        ip_hl = (ip[0] & 0x0f) << 2;
+    }
+    // bytes this sum reads: [ip + ip_hl, ip + ip_hl + len); past `avail` only
+    // zero padding may be read (fixlen pad); anything else is the reference's
+    // stale static buffer (Q8) which a lane cannot see.
+    const int ipoff = (int)(ip - pk.d);
+    auto readable = [&](int nbytes) -> int {  // the sum's bytes must lie below caplen
+        if (ipoff + ip_hl + nbytes > (int)pk.caplen) pk.unsupported = true;
+        int lim = (int)pk.avail - (ipoff + ip_hl);
+        return nbytes <= lim ? nbytes : (lim < 0 ? 0 : lim);
+    };
+    u8 *l4 = ip + ip_hl;
+    unsigned long long sum = 0;
+    switch (proto) {
+        case 6:
+        case 44: {  // IPPROTO_TCP, IPPROTO_TCP_V6FRAG (tcpr.h:655)
+            if (len < 20) return RC_WARN;
+            if (ipoff + ip_hl + 18 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            st16(l4 + 16, 0);
+            sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
+            sum += bswap16((u16)(6 + len));
+            sum += csum_bytes(l4, readable(len));
+            st16(l4 + 16, csum_carry(sum));
+            break;
+        }
+        case 17: {
+            if (len < 8) return RC_WARN;
+            if (ipoff + ip_hl + 8 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            if (ld16(l4 + 6) == 0) break;
+            st16(l4 + 6, 0);
+            sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
+            sum += bswap16((u16)(17 + len));
+            sum += csum_bytes(l4, readable(len));
+            st16(l4 + 6, csum_carry(sum));
+            break;
+        }
+        case 1: {
+            if (len < 4) return RC_WARN;
+            if (ipoff + ip_hl + 4 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            st16(l4 + 2, 0);
+            if (v6) {
+                // CHECKSUM_CARRY assigns its argument; the interim value lands in
+                // icmp_sum and is summed with the payload (checksum.c:131-135)
+                sum = csum_bytes(ip + 8, 32);
+                u32 f = (u32)((sum >> 16) + (sum & 0xffff));
+                sum = f;
+                st16(l4 + 2, (u16)(~(f + (f >> 16)) & 0xffff));
+            }
+            sum += csum_bytes(l4, readable(len));
+            st16(l4 + 2, csum_carry(sum));
+            break;
+        }
+        case 58: {
+            if (len < 8) return RC_WARN;
+            if (ipoff + ip_hl + 4 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            st16(l4 + 2, 0);
+            if (v6) sum = csum_bytes(ip + 8, 32);
+            sum += bswap16((u16)(58 + len));
+            sum += csum_bytes(l4, readable(len));
+            st16(l4 + 2, csum_carry(sum));
+            break;
+        }
+        default:
+            if (!v6) {
+                st16(ip + 10, 0);
+                st16(ip + 10, csum_carry(csum_bytes(ip, ip_hl)));
+            } else {
+                return RC_WARN;
+            }
+    }
+    return RC_OK;
+}
+
+// fix_ipv4_checksums (edit_packet.c:55-112)
+DI int fix_ipv4_checksums(Pkt &pk, u8 *ip, int l2len) {
+    if (pk.caplen < 20u + (u32)l2len) return RC_WARN;
+    if ((ip[0] >> 4) != 4) return RC_ERROR;
+    int ret1 = 0, ret2;
+    int ip_len = (int)be16(ip + 2);
+    int end = (int)pk.caplen - l2len;
+    if (pk.caplen == pk.len && (be16(ip + 6) & 0x3fff) == 0) {
+        if (ip_len != (int)(pk.caplen - (u32)l2len)) return RC_WARN;
+        ret1 = do_checksum(pk, ip, ip[9], ip_len - ((ip[0] & 0x0f) << 2), end);
+        if (ret1 < 0) return RC_ERROR;
+    }
+    ret2 = do_checksum(pk, ip, 0, ip_len, end);
+    if (ret2 < 0) return RC_ERROR;
+    if (ret1 == RC_WARN || ret2 == RC_WARN) return RC_WARN;
+    return RC_OK;
+}
+
+// ipv6_header_length (edit_packet.c:118-140)
+DI int ipv6_header_length(Pkt &pk, const u8 *ip6, u32 pkt_len, int l2len) {
+    int offset = 40;
+    u8 nh = ip6[6];
+    const int ipoff = (int)(ip6 - pk.d);
+    for (int guard = 0; guard < 65536 && (u32)(2 + offset + l2len) < pkt_len; ++guard) {
+        if (nh != 0 && nh != 43 && nh != 44) return offset;
+        if (ipoff + offset + 2 > (int)pk.avail) { pk.unsupported = true; return offset; }
+        nh = ip6[offset];
+        offset += (ip6[offset + 1] + 1) << 3;
+    }
+    return -1;
+}
+
+// fix_ipv6_checksums (edit_packet.c:142-189)
+DI int fix_ipv6_checksums(Pkt &pk, u8 *ip6, int l2len) {
+    if (pk.caplen < 40u + (u32)l2len) return RC_WARN;
+    if ((ip6[0] >> 4) != 6) return RC_ERROR;
+    int ret = 0;
+    if (pk.caplen == pk.len) {
+        int ip6_len = ipv6_header_length(pk, ip6, pk.len, l2len);
+        if ((int)ld16(ip6 + 4) < ip6_len) return RC_WARN;  // raw network-order compare (:167)
+        ret = do_checksum(pk, ip6, ip6[6], be16(ip6 + 4), (int)pk.caplen - l2len);
+        if (ret < 0) return RC_ERROR;
+    }
+    return ret == RC_WARN ? RC_WARN : RC_OK;
+}
+
+// ipv4_addr_csum_replace (edit_packet.c:259-296)
+DI void ipv4_addr_csum_replace(u8 *ip, u32 old_ip, u32 new_ip, int l3len) {
+    int len = l3len;
+    if (len < 20) return;
+    csum_replace4(ip + 10, old_ip, new_ip);
+    u8 proto = ip[9];
+    int l4;
+    if (proto == 17) {
+        l4 = l4_v4(ip, l3len);
+        len -= ((ip[0] & 0x0f) << 2) + 8;
+    } else if (proto == 6) {
+        l4 = l4_v4(ip, l3len);
+        len -= ((ip[0] & 0x0f) << 2) + 20;
+    } else {
+        return;
+    }
+    if (l4 < 0 || len < 0) return;
+    if ((be16(ip + 6) & 0x1fff) == 0) {
+        if (proto == 6)
+            csum_replace4(ip + l4 + 16, old_ip, new_ip);
+        else if (ld16(ip + l4 + 6))
+            csum_replace4(ip + l4 + 6, old_ip, new_ip);
+    }
+}
+
+// ipv6_addr_csum_replace (edit_packet.c:298-330)
+DI void ipv6_addr_csum_replace(Pkt &pk, u8 *ip6, const u8 *old_ip, const u8 *new_ip, int l3len) {
+    if (l3len < 40) return;
+    u8 proto = l4proto_v6(ip6, l3len);
+    if (proto != 17 && proto != 6 && proto != 58) return;
+    int l4 = l4_v6(ip6, 0, l3len);
+    if (l4 < 0) return;
+    int fld = proto == 6 ? 16 : (proto == 17 ? 6 : 2);
+    if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.caplen) {
+        // the field lies past caplen: the reference reads its static buffer there
+        if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.avail) { pk.unsupported = true; return; }
+        pk.unsupported = true;
+    }
+    if (proto == 17 && ld16(ip6 + l4 + 6) == 0) return;
+    csum_replace16(ip6 + l4 + fld, old_ip, new_ip);
+}
+
+// randomize_ipv4_addr (edit_packet.c:336-357)
+DI u32 randomize_ipv4_addr(const te_dev_cfg_t &cfg, u32 ip) {
+    bool was = mcast4(ip);
+    if (cfg.skip_broadcast && was) return ip;
+    u32 s = bswap32(cfg.seed);
+    u32 r = (ip ^ s) - (ip & s);
+    if (was && !mcast4(r))
+        r = bswap32((bswap32(r) & 0x0fffffffu) | 0xe0000000u);
+    else if (!was && mcast4(r))
+        r = bswap32(bswap32(r) & 0x7fffffffu);
+    return r;
+}
+
+// randomize_ipv6_addr (edit_packet.c:359-379)
+DI void randomize_ipv6_addr(const te_dev_cfg_t &cfg, u8 *a) {
+    bool was = mcast6(a);
+    u32 s = bswap32(cfg.seed);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        u32 p = ld32(a + 4 * i);
+        st32(a + 4 * i, (p ^ s) - (p & s));
+    }
+    if (was && !mcast6(a))
+        a[0] = 0xff;
+    else if (!was && mcast6(a))
+        a[0] = 0xaa;
+}
+
+// rewrite_ports (portmap.c:267-330) with the first-match port map as a 64K LUT
+DI int rewrite_ports(const u16 *lut, u8 proto, u8 *l4, int l4len) {
+    int sumoff;
+    if (proto == 6) {
+        if (l4len < 20) return RC_WARN;
+        sumoff = 16;
+    } else if (proto == 17) {
+        if (l4len < 8) return RC_WARN;
+        sumoff = 6;
+    } else {
+        return 0;
+    }
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {  // destination port first, then source
+        u8 *pp = l4 + (which == 0 ? 2 : 0);
+        u16 oldp = ld16(pp);
+        u16 np = lut[oldp];
+        if (np != oldp) {
+            if (proto == 6 || ld16(l4 + 6)) csum_replace2(l4 + sumoff, oldp, np);
+            st16(pp, np);
+        }
+    }
+    return 0;
+}
+
+// rewrite_seqs (rewrite_sequence.c:37-55)
+DI void rewrite_seqs(Pkt &pk, const te_dev_cfg_t &cfg, u8 *tcp) {
+    int off = (int)(tcp - pk.d);
+    if (off + 18 > (int)pk.caplen) pk.unsupported = true;  // fields read past caplen (stale)
+    if (off + 18 > (int)pk.avail) return;
+    u32 ns = be32(tcp + 4) + cfg.tcp_sequence_adjust;
+    csum_replace4(tcp + 16, ld32(tcp + 4), bswap32(ns));
+    st32(tcp + 4, bswap32(ns));
+    if (!((tcp[13] & 0x02) && !(tcp[13] & 0x10))) {
+        u32 na = be32(tcp + 8) + cfg.tcp_sequence_adjust;
+        csum_replace4(tcp + 16, ld32(tcp + 8), bswap32(na));
+        st32(tcp + 8, bswap32(na));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// rewrite_ipv4l3 / rewrite_ipv6l3 (edit_packet.c:787-1019)
+// ---------------------------------------------------------------------------
+DI void rewrite_ipv4l3(const te_dev_cfg_t &cfg, u8 *ip, int dir, int len) {
+    for (int m = 0; m < cfg.n_srcipmap; ++m) {
+        if (ip_in_cidr(cfg.srcipmap[m].from, ld32(ip + 12))) {
+            u32 o = ld32(ip + 12);
+            st32(ip + 12, remap_ipv4(cfg, cfg.srcipmap[m].to, o));
+            ipv4_addr_csum_replace(ip, o, ld32(ip + 12), len);
+            break;
+        }
+    }
+    for (int m = 0; m < cfg.n_dstipmap; ++m) {
+        if (ip_in_cidr(cfg.dstipmap[m].from, ld32(ip + 16))) {
+            u32 o = ld32(ip + 16);
+            st32(ip + 16, remap_ipv4(cfg, cfg.dstipmap[m].to, o));
+            ipv4_addr_csum_replace(ip, o, ld32(ip + 16), len);
+            break;
+        }
+    }
+    if (cfg.n_cidrmap1 == 0) return;
+    const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
+    const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+    int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+    int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+    int i1 = 0, i2 = 0;
+    bool didsrc = false, diddst = false;
+    for (;;) {
+        if (!diddst && ip_in_cidr(l2[i2].from, ld32(ip + 16))) {
+            u32 o = ld32(ip + 16);
+            st32(ip + 16, remap_ipv4(cfg, l2[i2].to, o));
+            ipv4_addr_csum_replace(ip, o, ld32(ip + 16), len);
+            diddst = true;
+        }
+        if (!didsrc && ip_in_cidr(l1[i1].from, ld32(ip + 12))) {
+            u32 o = ld32(ip + 12);
+            st32(ip + 12, remap_ipv4(cfg, l1[i1].to, o));
+            ipv4_addr_csum_replace(ip, o, ld32(ip + 12), len);
+            didsrc = true;
+        }
+        if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
+            if (i1 + 1 < n1) ++i1;
+            if (i2 + 1 < n2) ++i2;
+        } else {
+            break;
+        }
+    }
+}
+
+DI void rewrite_ipv6_addr_pair(Pkt &pk, const te_dev_cfg_t &cfg, const te_cidr_t &to, u8 *ip6, int aoff, int l3len) {
+    u8 old[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) old[b] = ip6[aoff + b];
+    int room = (int)pk.avail - ((int)(ip6 - pk.d) + aoff);
+    if (!remap_ipv6(cfg, to, ip6 + aoff, room)) pk.unsupported = true;
+    ipv6_addr_csum_replace(pk, ip6, old, ip6 + aoff, l3len);
+}
+
+DI void rewrite_ipv6l3(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip6, int dir, int l3len) {
+    // the ICMPv6-error recursion (:988-1013) is walked iteratively
+    for (int depth = 0; depth < 64; ++depth) {
+        for (int m = 0; m < cfg.n_srcipmap; ++m)
+            if (ip6_in_cidr(cfg.srcipmap[m].from, ip6 + 8)) {
+                rewrite_ipv6_addr_pair(pk, cfg, cfg.srcipmap[m].to, ip6, 8, l3len);
+                break;
+            }
+        for (int m = 0; m < cfg.n_dstipmap; ++m)
+            if (ip6_in_cidr(cfg.dstipmap[m].from, ip6 + 24)) {
+                rewrite_ipv6_addr_pair(pk, cfg, cfg.dstipmap[m].to, ip6, 24, l3len);
+                break;
+            }
+        if (cfg.n_cidrmap1 != 0) {
+            const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
+            const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+            int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+            int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+            int i1 = 0, i2 = 0;
+            bool didsrc = false, diddst = false;
+            for (;;) {
+                if (!diddst && ip6_in_cidr(l2[i2].from, ip6 + 24)) {
+                    rewrite_ipv6_addr_pair(pk, cfg, l2[i2].to, ip6, 24, l3len);
+                    diddst = true;
+                }
+                if (!didsrc && ip6_in_cidr(l1[i1].from, ip6 + 8)) {
+                    rewrite_ipv6_addr_pair(pk, cfg, l1[i1].to, ip6, 8, l3len);
+                    didsrc = true;
+                }
+                if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
+                    if (i1 + 1 < n1) ++i1;
+                    if (i2 + 1 < n2) ++i2;
+                } else {
+                    break;
+                }
+            }
+        }
+        if (l3len <= 0) return;
+        if (l4proto_v6(ip6, l3len) != 58) return;
+        int ic = l4_v6(ip6, 0, l3len);
+        if (ic < 0 || ic + 8 > l3len) return;
+        u8 type = ip6[ic];
+        if (type < 1 || type > 4) return;  // ICMP6_UNREACH..ICMP6_PARAMPROB
+        u8 *emb = ip6 + ic + 8;
+        int emb_len = l3len - (ic + 8);
+        if (!(emb_len >= 40 && (emb[0] >> 4) == 6)) return;
+        ip6 = emb;
+        l3len = emb_len;
+    }
+}
+
+// randomize_iparp (edit_packet.c:1025-1083) / rewrite_iparp (:1093-1198)
+DI bool arp_addrs(Pkt &pk, u8 *arp, u8 **ip1, u8 **ip2) {
+    int base = (int)(arp - pk.d);
+    if (base + 8 > (int)pk.caplen) pk.unsupported = true;  // ARP header read past caplen
+    if (base + 8 > (int)pk.avail) return false;
+    if (be16(arp + 2) != 0x0800) return false;
+    u16 op = be16(arp + 6);
+    if (op != 1 && op != 2) return false;
+    int o1 = 8 + arp[4];
+    int o2 = o1 + arp[5] + arp[4];
+    if (base + o2 + 4 > (int)pk.caplen) pk.unsupported = true;  // address bytes past caplen
+    if (base + o2 + 4 > (int)pk.avail) return false;
+    *ip1 = arp + o1;
+    *ip2 = arp + o2;
+    return true;
+}
+
+DI void rewrite_iparp(Pkt &pk, const te_dev_cfg_t &cfg, u8 *arp, int dir) {
+    const te_cidrmap_t *l1 = nullptr, *l2 = nullptr;
+    int n1 = 0, n2 = 0;
+    if (dir == TE_DIR_C2S) {
+        l1 = cfg.cidrmap1; n1 = cfg.n_cidrmap1; l2 = cfg.cidrmap2; n2 = cfg.n_cidrmap2;
+    } else if (dir == TE_DIR_S2C) {
+        l1 = cfg.cidrmap2; n1 = cfg.n_cidrmap2; l2 = cfg.cidrmap1; n2 = cfg.n_cidrmap1;
+    }
+    if (n1 == 0 || n2 == 0) return;
+    u8 *ip1, *ip2;
+    if (!arp_addrs(pk, arp, &ip1, &ip2)) return;
+    bool request = be16(arp + 6) == 1;
+    int i1 = 0, i2 = 0;
+    bool didsrc = false, diddst = false;
+    for (;;) {
+        u8 *dsta = request ? ip1 : ip2, *srca = request ? ip2 : ip1;
+        if (!diddst && ip_in_cidr(l2[i2].from, ld32(dsta))) {
+            st32(dsta, remap_ipv4(cfg, l2[i2].to, ld32(dsta)));
+            diddst = true;
+        }
+        if (!didsrc && ip_in_cidr(l1[i1].from, ld32(srca))) {
+            st32(srca, remap_ipv4(cfg, l1[i1].to, ld32(srca)));
+            didsrc = true;
+        }
+        if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
+            if (i1 + 1 < n1) ++i1;
+            if (i2 + 1 < n2) ++i2;
+        } else {
+            break;
+        }
+    }
+}
+
+// untrunc_packet (edit_packet.c:526-621).  Returns -1 (error), 0, 1.
+DI int untrunc_packet(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip, u8 *ip6) {
+    if (pk.caplen == pk.len || (ip == nullptr && ip6 == nullptr))
+        if (!cfg.mtu_truncate) return 0;
+    int l2len = en10mb_l2len(pk.d, (int)pk.caplen);  // layer2len() via the encoder (dlt.c:165-172)
+    if (l2len < 0) return -1;
+    int chksum = 1;
+    if (ip) {
+        u16 off = be16(ip + 6);
+        if (off & 0x1fff) {
+            chksum = 0;
+        } else if (ip[9] == 17 && (off & 0x2000)) {
+            int f = (int)(ip - pk.d) + ((ip[0] & 0x0f) << 2) + 6;
+            if (f + 2 > (int)pk.avail) pk.unsupported = true;
+            else st16(pk.d + f, 0);
+            chksum = 0;
+        }
+    }
+    if (cfg.fixlen == TE_FIXLEN_PAD) {
+        if (pk.len > pk.caplen) {
+            // memset(packet + caplen, 0, len - caplen): the tile sized this slot
+            // for max(caplen, len) when --fixlen=pad is set
+            if (pk.len > pk.avail) pk.unsupported = true;
+            for (u32 i = pk.caplen; i < pk.avail && i < pk.len; ++i) pk.d[i] = 0;
+            pk.caplen = pk.len;
+        } else if (pk.len < pk.caplen) {
+            return -1;
+        }
+    } else if (cfg.fixlen == TE_FIXLEN_TRUNC) {
+        if (ip && pk.len != pk.caplen) st16(ip + 2, bswap16((u16)(pk.caplen - (u32)l2len)));
+        pk.len = pk.caplen;
+    } else if (cfg.mtu_truncate) {
+        if (pk.len > (u32)(cfg.mtu + l2len)) {
+            pk.len = pk.caplen = (u32)l2len + (u32)cfg.mtu;
+            if (ip) st16(ip + 2, bswap16((u16)cfg.mtu));
+            else if (ip6) st16(ip6 + 4, bswap16((u16)(cfg.mtu - 40)));
+            else chksum = 0;
+        }
+    } else {
+        return -1;  // "Invalid fixlen value" (TCPEDIT_FIXLEN_DEL lands here)
+    }
+    return chksum;
+}
+
+// ---------------------------------------------------------------------------
+// DLT_EN10MB decode/encode/merge (plugins/dlt_en10mb/en10mb.c:402-887)
+// ---------------------------------------------------------------------------
+DI int en10mb_decode(const u8 *pkt, int pktlen, Dec &s) {
+    L2 r;
+    if (get_l2len_protocol(pkt, (u32)pktlen, r) == -1) return RC_ERROR;
+    if ((u32)pktlen < 14 + r.l2offset) return RC_ERROR;
+    const u8 *eth = pkt + r.l2offset;
+    u16 prot = be16(eth + 12);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        s.dstaddr[i] = eth[i];
+        s.srcaddr[i] = eth[6 + i];
+    }
+    s.proto_vlan_tag = prot;
+    if (r.vlan_offset != 0) {
+        if (r.vlan_offset != r.l2offset + 14) return RC_ERROR;  // VLAN after MPLS
+        if ((u32)pktlen < r.vlan_offset + 4) return RC_ERROR;
+        u16 tci = be16(pkt + r.vlan_offset);
+        s.vlan = 1;
+        s.vlan_offset = r.vlan_offset;
+        s.vlan_proto = be16(pkt + r.vlan_offset + 2);
+        s.vlan_tag = tci & 0x0fff;
+        s.vlan_pri = tci & 0xe000;
+        s.vlan_cfi = tci & 0x1000;
+    } else {
+        s.vlan = 0;
+        s.vlan_offset = r.l2offset + 14;
+        s.vlan_proto = prot;
+    }
+    s.proto = bswap16(prot);
+    s.l2offset = (int)r.l2offset;
+    s.l2len = (int)r.l2len;
+    return RC_OK;
+}
+
+// Returns the new packet length (or RC_ERROR).  May move the packet start
+// (pk.d) by -4 (VLAN push) / +4 (VLAN pop) together with its record header.
+DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int dir) {
+    if (pktlen < 14) return RC_ERROR;
+    if (cfg.vlan == TE_VLAN_ADD && !s.vlan && cfg.vlan_tag == 65535) return RC_ERROR;
+    u32 newl2 = 0, oldl2 = 0;
+    if (cfg.vlan == TE_VLAN_ADD) {
+        oldl2 = s.vlan_offset;
+        newl2 = s.vlan_offset + 4;
+    } else if (cfg.vlan == TE_VLAN_DEL) {
+        if (s.vlan) { oldl2 = s.vlan_offset + 4; newl2 = s.vlan_offset; }
+    } else {
+        if (s.vlan) { oldl2 = s.vlan_offset; newl2 = s.vlan_offset; }
+    }
+    if ((u32)pktlen < newl2 || pktlen + newl2 - s.l2len > MAXPACKET) return RC_ERROR;
+    if (pktlen < s.l2len) return RC_ERROR;
+    if (newl2 > 0 && newl2 != oldl2) {
+        if (pktlen + (newl2 - oldl2) > MAXPACKET) return RC_ERROR;
+        if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;  // checked below in the reference
+        // move the record header + the first oldl2 bytes instead of the tail
+        if (newl2 > oldl2) {  // push 4 bytes at oldl2
+            u8 *src = pk.d - 16, *dst = pk.d - 20;
+            for (u32 i = 0; i < 16 + oldl2; ++i) dst[i] = src[i];
+            pk.d -= 4;
+        } else {  // pop 4 bytes at newl2
+            u8 *src = pk.d - 16, *dst = pk.d - 12;
+            for (int i = (int)(16 + newl2) - 1; i >= 0; --i) dst[i] = src[i];
+            pk.d += 4;
+            pk.avail -= 4;
+        }
+        if (newl2 > oldl2) pk.avail += 4;
+    }
+    pktlen += (int)(newl2 - oldl2);
+    u8 *eth = pk.d + s.l2offset;
+    u8 *dh = eth, *sh = eth + 6;
+    const bool l2skip = cfg.l2_skip_broadcast;
+    if (dir == TE_DIR_C2S || dir == TE_DIR_S2C) {
+        const bool c2s = dir == TE_DIR_C2S;
+        const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
+        const u8 *smac = c2s ? cfg.intf1_smac : cfg.intf2_smac;
+        const u8 *dmac = c2s ? cfg.intf1_dmac : cfg.intf2_dmac;
+        const bool use_s = (cfg.mac_mask & sm) && (!l2skip || is_unicast_ethernet(s.srcaddr));
+        const bool use_d = (cfg.mac_mask & dm) && (!l2skip || is_unicast_ethernet(s.dstaddr));
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            sh[i] = use_s ? smac[i] : s.srcaddr[i];
+            dh[i] = use_d ? dmac[i] : s.dstaddr[i];
+        }
+    } else {
+        return RC_ERROR;
+    }
+    for (int e = 0; e < cfg.n_subs; ++e) {
+        const u8 *t = cfg.subs[e], *rw = cfg.subs[e] + 6;
+        bool md = true, ms = true;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            md &= dh[i] == t[i];
+            ms &= sh[i] == t[i];
+        }
+        if (md)
+            for (int i = 0; i < 6; ++i) dh[i] = rw[i];
+        if (ms)
+            for (int i = 0; i < 6; ++i) sh[i] = rw[i];
+    }
+    if (cfg.random_set) {
+        int us = is_unicast_ethernet(sh), ud = is_unicast_ethernet(dh);
+        for (int i = cfg.random_keep; i < 6; ++i) {
+            int ms = cfg.random_mask[i] * us, md = cfg.random_mask[i] * ud;
+            sh[i] = (u8)((sh[i] ^ ms) - (sh[i] & ms));  // MAC_MASK_APPLY (en10mb.h:29-30)
+            dh[i] = (u8)((dh[i] ^ md) - (dh[i] & md));
+        }
+        if (!cfg.random_keep) {
+            sh[0] &= (u8)~(0x01 * us);
+            dh[0] &= (u8)~(0x01 * ud);
+        }
+    }
+    if (newl2 == 14) st16(eth + 12, (u16)s.proto);
+    if (cfg.vlan == TE_VLAN_ADD || (cfg.vlan == TE_VLAN_OFF && s.vlan)) {
+        u8 *vh = pk.d + s.vlan_offset;  // {tci, tpid}
+        if (cfg.vlan == TE_VLAN_ADD) {
+            st16(pk.d + s.l2offset + 12, bswap16((u16)cfg.vlan_proto));
+            st16(vh + 2, bswap16((u16)s.proto_vlan_tag));
+        }
+        if (cfg.vlan_tag < 65535) st16(vh, bswap16((u16)(cfg.vlan_tag & 0x0fff)));
+        else if (s.vlan) st16(vh, bswap16(s.vlan_tag));
+        if (cfg.vlan_pri < 255) st16(vh, (u16)(ld16(vh) + bswap16((u16)(cfg.vlan_pri << 13))));
+        else if (s.vlan) st16(vh, (u16)(ld16(vh) + bswap16(s.vlan_pri)));
+        if (cfg.vlan_cfi < 255) st16(vh, (u16)(ld16(vh) + bswap16((u16)(cfg.vlan_cfi << 12))));
+        else if (s.vlan) st16(vh, (u16)(ld16(vh) + bswap16(s.vlan_cfi)));
+    } else if (cfg.vlan == TE_VLAN_DEL && newl2 > 0) {
+        st16(eth + 12, bswap16(s.vlan_proto));
+    }
+    return pktlen;
+}
+
+// dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC; the
+// en10mb decoder never sets dst_modified (memcmp of untouched bytes, :614).
+DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) {
+    int pktlen = (int)pk.caplen;
+    int l2len = en10mb_l2len(pk.d, pktlen);
+    if (l2len == -1 || pktlen < l2len) return;
+    u8 *dh = pk.d + s.l2offset;
+    if (ip) {
+        if (pktlen >= 34) {
+            u32 dst = ld32(ip + 16);
+            if (mcast4(dst)) {
+                u32 c = bswap32(dst);
+                dh[0] = 0x01; dh[1] = 0x00; dh[2] = 0x5e;
+                dh[3] = (u8)(c >> 16) & 0x7f; dh[4] = (u8)(c >> 8); dh[5] = (u8)c;
+            }
+        }
+    } else if (ip6) {
+        if (pktlen >= 54) {
+            const u8 *a = ip6 + 24;
+            if (a[0] == 0xff) {
+                dh[0] = 0x33; dh[1] = 0x33; dh[2] = a[12]; dh[3] = a[13]; dh[4] = a[14]; dh[5] = a[15];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// tcpedit_packet (src/tcpedit/tcpedit.c:46-366), minus fuzzing (out of scope).
+// Returns RC_* ; *warned set when the checksum step warned (:351-353).
+// ---------------------------------------------------------------------------
+DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int dir, bool &warned) {
+    warned = false;
+    u8 *ip = nullptr, *ip6 = nullptr;
+    int needtorecalc = 0, retval = 0;
+
+    if (cfg.efcs && pk.len > 4) {  // :78-84
+        if (pk.caplen == pk.len) pk.caplen -= 4;
+        pk.len -= 4;
+    }
+    // l2proto (:96): dlt_en10mb_proto (en10mb.c:741-762), network-order value
+    int l2proto;
+    {
+        if (pk.caplen < 14) return RC_SOFT;
+        L2 r;
+        if (get_l2len_protocol(pk.d, pk.caplen, r) == -1) return RC_SOFT;
+        l2proto = bswap16(r.protocol);
+    }
+    // tcpedit_dlt_process (dlt_plugins.c:210-238)
+    int pktlen;
+    Dec s;
+    if (dir == TE_DIR_NOSEND) {
+        pktlen = (int)pk.caplen;
+        s.l2offset = 0;
+    } else {
+        if (en10mb_decode(pk.d, (int)pk.caplen, s) == RC_ERROR) return RC_SOFT;
+        pktlen = en10mb_encode(pk, cfg, s, (int)pk.caplen, dir);
+        if (pktlen < 0) return RC_SOFT;
+    }
+    int lendiff = pktlen - (int)pk.caplen;  // :111-113
+    pk.caplen += lendiff;
+    pk.len += lendiff;
+
+    int l2len = en10mb_l2len(pk.d, (int)pk.caplen);  // :116
+    if (l2len == -1) return RC_SOFT;
+
+    if (l2proto == 0x0008) {  // htons(ETHERTYPE_IP)  :123-148
+        if (pk.caplen < (u32)l2len + 20) return RC_SOFT;
+        if ((int)pk.caplen <= l2len) return RC_SOFT;  // tcpedit_dlt_l3data_copy (dlt_utils.c:195)
+        ip = pk.d + l2len;
+        if (l4_v4(ip, (int)pk.caplen - l2len) < 0) return RC_SOFT;
+    } else if (l2proto == 0xDD86) {  // htons(ETHERTYPE_IP6)  :149-173
+        if (pk.caplen < (u32)l2len + 40) return RC_SOFT;
+        if ((int)pk.caplen <= l2len) return RC_SOFT;
+        ip6 = pk.d + l2len;
+        if (l4_v6(ip6, 0, (int)pk.caplen - l2len) < 0) return RC_SOFT;
+    }
+
+    int l3len = (int)pk.caplen - l2len;
+    if (ip) {  // :182-206
+        if (cfg.tos > -1) {
+            u16 oldv = ld16(ip);
+            u16 newv = bswap16((u16)((bswap16(oldv) & 0xff00) | (cfg.tos & 0xff)));
+            st16(ip, newv);
+            csum_replace2(ip + 10, oldv, newv);
+        }
+        if (cfg.ttl_mode != TE_TTL_OFF) {  // rewrite_ipv4_ttl (edit_packet.c:627-667)
+            u8 t = ip[8], v = (u8)cfg.ttl_value;
+            bool changed = true;
+            if (cfg.ttl_mode == TE_TTL_SET) {
+                if (t == v) changed = false;
+                else t = v;
+            } else if (cfg.ttl_mode == TE_TTL_ADD) {
+                t = ((int)t + v > 255) ? 255 : (u8)(t + v);
+            } else {
+                t = (t <= v) ? 1 : (u8)(t - v);
+            }
+            if (changed) {
+                u16 oldv = ip[8];
+                ip[8] = t;
+                csum_replace2(ip + 10, oldv, (u16)t);
+                needtorecalc += 1;
+            }
+        }
+        if (cfg.has_portmap) {  // rewrite_ipv4_ports (portmap.c:332-351)
+            if (ip[9] == 6 || ip[9] == 17) {
+                int l4 = l4_v4(ip, l3len);
+                retval = l4 >= 0 ? rewrite_ports(portlut, ip[9], ip + l4, l3len - l4) : RC_WARN;
+            } else {
+                retval = 0;
+            }
+            needtorecalc += retval;
+        }
+        if (cfg.tcp_sequence_enable && ip[9] == 6) {  // rewrite_sequence.c:57-74
+            int l4 = l4_v4(ip, l3len);
+            if (l4 >= 0) rewrite_seqs(pk, cfg, ip + l4);
+        }
+    } else if (ip6) {  // :209-248
+        if (cfg.ttl_mode != TE_TTL_OFF) {  // rewrite_ipv6_hlim (edit_packet.c:673-706)
+            u8 t = ip6[7], v = (u8)cfg.ttl_value;
+            bool changed = true;
+            if (cfg.ttl_mode == TE_TTL_SET) {
+                if (t == v) changed = false;
+                else t = v;
+            } else if (cfg.ttl_mode == TE_TTL_ADD) {
+                t = ((int)t + v > 255) ? 255 : (u8)(t + v);
+            } else {
+                t = (t <= v) ? 1 : (u8)(t - v);
+            }
+            ip6[7] = t;
+            needtorecalc += changed ? 1 : 0;
+        }
+        if (cfg.tclass > -1) {
+            u32 f = (be32(ip6) & 0xf00fffffu) + ((u32)cfg.tclass << 20);
+            st32(ip6, bswap32(f));
+        }
+        if (cfg.flowlabel > -1) {
+            u32 f = (be32(ip6) & 0xfff00000u) + (u32)cfg.flowlabel;
+            st32(ip6, bswap32(f));
+        }
+        if (cfg.has_portmap) {  // rewrite_ipv6_ports (portmap.c:353-372)
+            if (ip6[6] == 6 || ip6[6] == 17) {
+                int l4 = l4_v6(ip6, 0, l3len);
+                retval = l4 >= 0 ? rewrite_ports(portlut, ip6[6], ip6 + l4, l3len - l4) : RC_WARN;
+            } else {
+                retval = 0;
+            }
+            needtorecalc += retval;
+        }
+        if (cfg.tcp_sequence_enable && ip6[6] == 6) {  // rewrite_sequence.c:76-92
+            int l4 = l4_v6(ip6, 0, l3len);
+            if (l4 >= 0) rewrite_seqs(pk, cfg, ip6 + l4);
+        }
+    }
+
+    if (cfg.fixlen || cfg.mtu_truncate) {  // :261-265
+        retval = untrunc_packet(pk, cfg, ip, ip6);
+        if (retval < 0) return RC_ERROR;
+        needtorecalc += retval;
+    }
+
+    l3len = (int)pk.caplen - l2len;
+    if (cfg.rewrite_ip) {  // :268-290
+        if (ip) {
+            rewrite_ipv4l3(cfg, ip, dir, l3len);
+            retval = 0;
+        } else if (ip6) {
+            rewrite_ipv6l3(pk, cfg, ip6, dir, l3len);
+            retval = 0;
+        } else if (l2proto == 0x0608) {
+            rewrite_iparp(pk, cfg, pk.d + l2len, dir);
+        }
+    }
+
+    if (cfg.seed) {  // :293-317
+        if (ip) {  // randomize_ipv4 (edit_packet.c:420-467)
+            if (l3len < (int)(ip[0] & 0x0f) << 2) return RC_ERROR;
+            if (!(cfg.skip_broadcast && mcast4(ld32(ip + 16)))) {
+                u32 o = ld32(ip + 16);
+                st32(ip + 16, randomize_ipv4_addr(cfg, o));
+                ipv4_addr_csum_replace(ip, o, ld32(ip + 16), l3len);
+            }
+            if (!(cfg.skip_broadcast && mcast4(ld32(ip + 12)))) {
+                u32 o = ld32(ip + 12);
+                st32(ip + 12, randomize_ipv4_addr(cfg, o));
+                ipv4_addr_csum_replace(ip, o, ld32(ip + 12), l3len);
+            }
+            retval = 0;
+        } else if (ip6) {  // randomize_ipv6 (edit_packet.c:469-518)
+            if (l3len < 40) return RC_ERROR;
+#pragma unroll
+            for (int which = 0; which < 2; ++which) {
+                int ao = which == 0 ? 24 : 8;
+                if (!(cfg.skip_broadcast && mcast6(ip6 + ao))) {
+                    u8 old[16];
+                    for (int b = 0; b < 16; ++b) old[b] = ip6[ao + b];
+                    randomize_ipv6_addr(cfg, ip6 + ao);
+                    ipv6_addr_csum_replace(pk, ip6, old, ip6 + ao, l3len);
+                }
+            }
+            retval = 0;
+        } else if (l2proto == 0x0608) {  // randomize_iparp (edit_packet.c:1025-1083)
+            if (l3len < 8) return RC_ERROR;
+            int al2 = get_l2len(pk.d, pk.caplen);
+            u8 *ip1, *ip2;
+            if (arp_addrs(pk, pk.d + al2, &ip1, &ip2)) {
+                st32(ip1, randomize_ipv4_addr(cfg, ld32(ip1)));
+                st32(ip2, randomize_ipv4_addr(cfg, ld32(ip2)));
+            }
+        }
+    }
+
+    if (cfg.fixhdrlen) {  // :321-335
+        int changed = 0;
+        if (ip) {  // fix_ipv4_length (edit_packet.c:381-396)
+            if (pk.caplen < (u32)l2len + 20) {
+                changed = -1;
+            } else if ((be16(ip + 6) & 0x3fff) == 0 && (int)be16(ip + 2) != (int)(pk.len - (u32)l2len)) {
+                st16(ip + 2, bswap16((u16)(pk.len - (u32)l2len)));
+                changed = 1;
+            }
+        } else if (ip6) {  // fix_ipv6_length (edit_packet.c:398-413)
+            int want = (int)(pk.len - (u32)l2len - 40);
+            if (pk.caplen < (u32)l2len + 40) {
+                changed = -1;
+            } else if ((int)be16(ip6 + 4) != want) {
+                st16(ip6 + 4, bswap16((u16)want));
+                changed = 1;
+            }
+        }
+        if (changed > 0) needtorecalc |= changed;
+    }
+
+    if (cfg.fixcsum || needtorecalc > 0) {  // :338-354
+        if (ip) retval = fix_ipv4_checksums(pk, ip, l2len);
+        else if (ip6) retval = fix_ipv6_checksums(pk, ip6, l2len);
+        else retval = RC_OK;
+        if (retval < 0) return RC_ERROR;
+        if (retval == RC_WARN) warned = true;
+    }
+
+    en10mb_merge_layer3(pk, s, ip, ip6);  // :356-361
+    return retval;
+}
+
+}  // namespace te

@@ -1,0 +1,229 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference goldens and
+the CPU oracle.  Integer/byte work, so every comparison is bit-exact."""
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+import oracle_lib as O
+import tcpreplay_amd as TA
+from tcpreplay_amd import synth as S
+
+pytestmark = pytest.mark.gpu
+
+C2_ARGS = ["--seed=42", "--fixcsum"]
+C3_ARGS = ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]
+C4_ARGS = ["--endpoints=10.10.0.1:10.10.0.2", "--enet-dmac=00:12:13:14:15:16,00:22:33:44:55:66",
+           "--enet-smac=00:22:33:44:55:66,00:12:13:14:15:16", "--enet-vlan=add", "--enet-vlan-tag=45",
+           "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"]
+C5_ARGS = ["--fixcsum"]
+
+
+def gpu_rewrite(pcap, args, cache=None, with_status=False):
+    te = TA.TcpEdit(args)
+    try:
+        return te.rewrite(pcap, cache, with_status=with_status)
+    finally:
+        te.close()
+
+
+def first_diff(a, b):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i] != b[i]:
+            return i
+    return n
+
+
+def assert_same(out, exp):
+    assert len(out) == len(exp) and out == exp, f"first difference at byte {first_diff(out, exp)}"
+
+
+# ---------------------------------------------------------------- goldens
+@pytest.mark.parametrize("case", G.IN_SCOPE, ids=[c[0] for c in G.IN_SCOPE])
+def test_gpu_matches_reference_golden(built, case):
+    name, inp, cache, args, _ = case
+    rc, out = gpu_rewrite(G.read(inp), args, G.read(cache) if cache else None)
+    assert rc == 0
+    assert_same(out, G.read(name))
+
+
+# ---------------------------------------------------------------- BASELINE configs vs oracle
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
+def test_gpu_matches_oracle_on_baseline_configs(built, cfg):
+    cache = None
+    if cfg == "C2":
+        pcap, args = S.pcap_fixed(100_000, 64, seed=2), C2_ARGS
+    elif cfg == "C3":
+        pcap, args = S.pcap_imix(60_000, seed=3), C3_ARGS
+    elif cfg == "C4":
+        pcap, args = S.pcap_imix(60_000, seed=4), C4_ARGS
+        cache = S.tcpprep_cache(60_000, seed=4, nosend_every=97)
+    else:
+        pcap, args = S.pcap_mixed_v4v6(20_000, 1514, seed=5), C5_ARGS
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    rc, out = gpu_rewrite(pcap, args, cache)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
+
+
+def test_fixcsum_is_idempotent_and_valid(built):
+    pcap = S.pcap_imix(50_000, seed=9)
+    # corrupt every 7th IPv4 header checksum; --fixcsum must restore the original bytes
+    b = bytearray(pcap)
+    for i, off in enumerate(record_offsets(pcap)):
+        if i % 7 == 0:
+            b[off + 16 + 24] ^= 0x5A
+    rc, out = gpu_rewrite(bytes(b), ["--fixcsum"])
+    assert rc == 0
+    assert_same(out, pcap)
+    rc, out2 = gpu_rewrite(out, ["--fixcsum"])
+    assert_same(out2, out)
+
+
+def record_offsets(pcap):
+    offs, off = [], 24
+    while off + 16 <= len(pcap):
+        offs.append(off)
+        off += 16 + struct.unpack_from("<I", pcap, off + 8)[0]
+    return offs
+
+
+# ---------------------------------------------------------------- differential fuzzing vs oracle
+OPTION_POOL = [c[3] for c in G.IN_SCOPE if c[2] is None] + [
+    ["--fixcsum", "--efcs"], ["--seed=7", "--skipbroadcast", "--fixcsum"], ["--ttl=+3", "--tos=7"],
+    ["--enet-vlan=del", "--fixcsum"], ["--fixlen=pad", "--fixcsum"], ["--mtu-trunc", "--mtu=100", "--fixcsum"],
+    ["--srcipmap=0.0.0.0/0:10.1.0.0/16", "--dstipmap=96.0.0.0/8:11.0.0.0/8", "--fixcsum"],
+    ["--pnat=[::/0]:[2001:db8:aaaa::/40]", "--fixcsum"], ["--tclass=12", "--flowlabel=4660", "--ttl=9"],
+    ["--portmap=1-65535:7", "--tcp-sequence=5"], ["--fixhdrlen", "--fixcsum"], ["--skip-soft-errors", "--seed=3"],
+]
+
+
+def mutate(recs, rng):
+    out = []
+    for ts, tu, cl, ln, data in recs:
+        d = bytearray(data)
+        r = rng.random()
+        if r < 0.25 and len(d) > 14:  # random header byte
+            i = rng.randrange(0, min(len(d), 80))
+            d[i] = rng.randrange(256)
+        elif r < 0.32:  # snaplen-truncated capture
+            cl = rng.randrange(0, cl + 1)
+            d = d[:cl]
+        elif r < 0.36:  # len != caplen
+            ln = cl + rng.randrange(0, 100)
+        elif r < 0.42 and len(d) > 14:  # 802.1Q / QinQ / MPLS encapsulations
+            tag = rng.choice([b"\x81\x00", b"\x88\xa8", b"\x91\x00"])
+            d = d[:12] + tag + bytes([rng.randrange(256), rng.randrange(256)]) + d[12:]
+            cl, ln = len(d), ln + 4
+        out.append((ts, tu, cl, ln, bytes(d)))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_gpu_matches_oracle_on_mutated_captures(built, seed):
+    rng = random.Random(seed)
+    recs = mutate(S.records(G.read("test.pcap")), rng)
+    pcap = S.build_pcap(recs)
+    args = OPTION_POOL[seed % len(OPTION_POOL)]
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out, st = gpu_rewrite(pcap, args, with_status=True)
+    if (st & TA.ST.UNSUPPORTED).any():
+        pytest.skip("capture hits the reference's stale-buffer reads (SURVEY Q8); device flags it")
+    assert rc == rc_o
+    assert_same(out, exp)
+
+
+# ---------------------------------------------------------------- per-packet API
+@pytest.mark.parametrize("args", [["--fixcsum"], ["--seed=55"], ["--enet-vlan=add", "--enet-vlan-tag=45"]])
+def test_tcpedit_packet_api(built, args):
+    recs = S.records(G.read("test.pcap"))[:40]
+    _, exp = O.rewrite(S.build_pcap(recs), args)
+    exp_recs = S.records(exp)
+    te = TA.TcpEdit(args)
+    got = []
+    for ts, tu, cl, ln, data in recs:
+        buf = bytearray(262166)
+        buf[:cl] = data
+        rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf)
+        assert rc != TA.TCPEDIT_ERROR
+        got.append((ts, tu, h["caplen"], h["len"], bytes(buf[:h["caplen"]])))
+    te.close()
+    assert got == exp_recs
+
+
+# ---------------------------------------------------------------- edge cases
+def test_empty_capture(built):
+    hdr = G.read("test.pcap")[:24]
+    rc, out = gpu_rewrite(hdr, ["--fixcsum"])
+    rc_o, exp = O.rewrite(hdr, ["--fixcsum"])
+    assert rc == rc_o == 0
+    assert_same(out, exp)
+
+
+def test_hard_error_truncates_output(built):
+    recs = S.records(G.read("test.pcap"))[:10]
+    ts, tu, cl, ln, d = recs[2]
+    d = bytearray(d)
+    assert d[12:14] == b"\x08\x00"
+    d[14] = 0x55  # IP version 5 with ethertype IPv4 -> TCPEDIT_ERROR (edit_packet.c:73-79)
+    recs[2] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    rc, out = gpu_rewrite(pcap, ["--fixcsum"])
+    assert rc_o == -1 and rc == TA.TCPEDIT_ERROR
+    assert_same(out, exp)
+    assert len(S.records(out)) == 2
+
+
+def test_stale_buffer_dependency_is_flagged(built):
+    # IPv6/UDP whose payload length overstates the captured bytes: the reference's
+    # checksum then reads its static buffer past caplen
+    pcap = S.pcap_fixed(4, 200, ipv6=True, proto=17)
+    recs = S.records(pcap)
+    ts, tu, cl, ln, d = recs[3]
+    d = bytearray(d)
+    struct.pack_into(">H", d, 18, 146 + 50)
+    recs[3] = (ts, tu, cl, ln, bytes(d))
+    te = TA.TcpEdit(["--fixcsum"])
+    b = TA.Batch(te, S.build_pcap(recs))
+    assert b.run() == TA.TCPEDIT_ERROR
+    r = b.result()
+    assert r.unsupported == 1 and r.first_unsupported == 3
+    b.close()
+    te.close()
+
+
+@pytest.mark.parametrize("args", [["--fixcsum"], ["--seed=42", "--fixcsum"], ["--enet-vlan=add", "--enet-vlan-tag=3"]])
+def test_huge_records_use_the_hbm_slot_path(built, args):
+    small = S.records(S.pcap_fixed(3, 64, seed=1))
+    big = S.records(S.pcap_fixed(2, 100_000, seed=2)) + S.records(S.pcap_fixed(1, 262_000, seed=3, ipv6=True))
+    recs = [small[0], big[0], small[1], big[1], big[2], small[2]]
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out = gpu_rewrite(pcap, args)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
+
+
+def test_nanosecond_capture_is_written_in_microseconds(built):
+    p = bytearray(G.read("test.pcap"))
+    p[0:4] = struct.pack("<I", 0xA1B23C4D)
+    for off in record_offsets(bytes(p)):
+        us = struct.unpack_from("<I", p, off + 4)[0]
+        struct.pack_into("<I", p, off + 4, us * 1000 + 999)
+    rc, out = gpu_rewrite(bytes(p), ["--fixcsum"])
+    assert rc == 0
+    assert_same(out, G.read("test2.rewrite_fixcsum"))
+
+
+@pytest.mark.slow
+def test_full_size_c2_matches_oracle(built):
+    pcap = S.pcap_fixed(1_000_000, 64, seed=1)
+    rc_o, exp = O.rewrite(pcap, C2_ARGS)
+    rc, out = gpu_rewrite(pcap, C2_ARGS)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
