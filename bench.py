@@ -1,0 +1,194 @@
+"""bench.py -- device-resident tcpedit rewrite throughput on MI355X.
+
+Metric (BASELINE.json): Mpackets/s of the device-resident tcpedit rewrite
+(+ fixcsum), with the GB/s roofline of the kernel.  At N=1 the workload is
+BASELINE configs[1]: `--seed=42 --fixcsum` over 1M x 64 B synthetic UDP
+records.  A "step" is one pass of the whole device pipeline (one kernel:
+parse + edit + checksum + scan + compaction) over that batch, inputs already
+resident in HBM.  With --gpus N (one process per GPU, torch.distributed over
+RCCL) every rank rewrites its own 1M-record shard -- packets are independent,
+so there is no data-path collective, only one all-reduce of the counters per
+job -- and `value` is the aggregate packets/s over the max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # name: (generator, kwargs, tcpedit args, description)
+    "c2": ("pcap_fixed", dict(size=64), ["--seed=42", "--fixcsum"],
+           "--seed=42 --fixcsum on 1M x 64B synthetic UDP pcap (BASELINE configs[1])"),
+    "c3": ("pcap_imix", dict(), ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"],
+           "--pnat + --portmap + --fixcsum on IMIX 64/570/1514 7:4:1 (BASELINE configs[2])"),
+    "c5": ("pcap_mixed_v4v6", dict(size=1514), ["--fixcsum"],
+           "--fixcsum on 1514B mixed IPv4/IPv6 TCP/UDP (BASELINE configs[4])"),
+}
+DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000}
+
+
+def make_pcap(workload, n, seed):
+    from tcpreplay_amd import synth
+    gen, kw, _, _ = WORKLOADS[workload]
+    return getattr(synth, gen)(n, seed=seed, **kw)
+
+
+def run_workload(workload, n, steps, warmup, seed, device, verify=False):
+    import tcpreplay_amd as TA
+    args = WORKLOADS[workload][2]
+    pcap = make_pcap(workload, n, seed)
+    te = TA.TcpEdit(args, device=device)
+    b = TA.Batch(te, pcap)
+    rc = b.run()  # first (untimed) run: also the correctness check below
+    r = b.result()
+    if rc != 0 or r.unsupported or r.errors:
+        raise RuntimeError(f"{workload}: device run failed rc={rc} ({te.geterr()})")
+    if verify:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        rc_o, exp = oracle_lib.rewrite(pcap, args)
+        if b.output() != exp:
+            raise RuntimeError(f"{workload}: device output differs from the oracle")
+    if warmup:
+        b.time(warmup)
+    return te, b, r, pcap
+
+
+def cpu_baseline(pcap, args, n_pkts, budget_s=10.0):
+    """The oracle (C restatement of tcpedit_packet, 1 thread) on the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    oracle_lib.rewrite(pcap, args)  # warm (page-in)
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        oracle_lib.rewrite(pcap, args)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return runs * n_pkts / el / 1e6, runs, el
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
+    ap.add_argument("--extra", default="c3,c5", help="secondary configs measured at N=1 (comma list, '' = none)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="compare the first run with the oracle")
+    opt = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    n = opt.packets or DEFAULT_PACKETS[opt.workload]
+    te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank, device=local,
+                                  verify=opt.verify)
+    alg_bytes = r.bytes_in + r.bytes_out  # sum(16+caplen_in) + sum(16+caplen_out) per launch
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = b.time(opt.steps)  # K back-to-back launches; hipEvents on the launch stream
+    # the job's single counter reduction (RCCL all-reduce over xGMI at N > 1)
+    cnt = torch.tensor([r.packets * opt.steps, r.bytes_in * opt.steps, r.bytes_out * opt.steps,
+                        r.written * opt.steps], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(cnt)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_pkts = int(cnt[0].item())
+
+    value = total_pkts / elapsed / 1e6
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            traffic = tj.get(opt.workload, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    result = {
+        "metric": "Mpackets/s device-resident tcpedit rewrite+fixcsum",
+        "value": round(value, 3),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": opt.steps,
+        "warmup": opt.warmup,
+        "ms_per_step": round(elapsed / opt.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (tcpreplay_amd.synth, seeded per rank)",
+        "config": {"workload": WORKLOADS[opt.workload][3], "packets_per_gpu": n,
+                   "tcpedit_args": WORKLOADS[opt.workload][2], "parallelism": f"shard{world}",
+                   "global_records": n * world},
+        "gbps_algorithmic": round(alg_bytes * opt.steps * world / elapsed / 1e9, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "te_edit_tiles", "kernel_ms": round(kernel_ms, 5),
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    b.close()
+    te.close()
+
+    if rank == 0 and world == 1:
+        extra = {}
+        for wl in [w for w in opt.extra.split(",") if w]:
+            n2 = DEFAULT_PACKETS[wl]
+            te2, b2, r2, _ = run_workload(wl, n2, 0, 3, seed=11, device=0)
+            ms2 = b2.time(max(5, opt.steps // 20))
+            ab = r2.bytes_in + r2.bytes_out
+            extra[wl] = {"workload": WORKLOADS[wl][3], "packets": n2, "kernel_ms": round(ms2, 4),
+                         "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),
+                         "gbps_algorithmic": round(ab / (ms2 * 1e-3) / 1e9, 1),
+                         "frac_hbm_peak": round(ab / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            b2.close()
+            te2.close()
+        if extra:
+            result["extra_configs"] = extra
+        if not opt.no_cpu_baseline:
+            v, runs, el = cpu_baseline(pcap, WORKLOADS[opt.workload][2], n, opt.cpu_seconds)
+            result["cpu_baseline"] = {"value": round(v, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+                                      "sample": f"{runs} passes of the oracle over the same {n}-record workload "
+                                                f"({el:.1f} s, 1 thread, in-memory, no file I/O)"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -44,6 +44,7 @@ struct tcpedit_batch_s {
     uint8_t *status;         /* host copy after a run */
     int status_valid;
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
+    int slot_layout;
     /* device side */
     uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
     uint64_t dirbits_len;
@@ -60,7 +61,7 @@ struct tcpedit_batch_s {
 };
 
 #define WS_ERR 0
-#define WS_ZERO 16
+#define WS_ZERO 0
 #define WS_TICKET 24
 #define WS_COUNTERS 32
 #define WS_STATE 128
@@ -93,6 +94,8 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
     }
     b->linktype = rd32(img + 20, b->swapped) & 0x03ffffffu;
     const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
+    const int slot_mode = pad || t->cfg.vlan == TE_VLAN_ADD;
+    b->slot_layout = slot_mode;
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
     b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
@@ -117,8 +120,15 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
         uint32_t data = pad && plen > caplen ? plen : caplen;
         uint32_t g = (uint32_t)(off & 15);
         uint32_t slot = TE_SLOT_BYTES_OF(g, data);
-        int huge = slot > TE_SLOT_BYTES;
-        if (open && (huge || cur.npkt >= TE_MAX_PKTS || cur_slots + slot > TE_SLOT_BYTES)) {
+        int huge, fits;
+        if (slot_mode) {
+            huge = slot > TE_SLOT_BYTES;
+            fits = open && cur_slots + slot <= TE_SLOT_BYTES;
+        } else {
+            huge = !TE_CONTIG_FITS(g, 16 + caplen);
+            fits = open && TE_CONTIG_FITS(cur.span_off & 15, off + 16 + caplen - cur.span_off);
+        }
+        if (open && (huge || cur.npkt >= TE_MAX_PKTS || !fits)) {
             if (b->n_tiles == cap_tiles)
                 b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
             b->tiles[b->n_tiles++] = cur;
@@ -141,7 +151,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
         b->out_cap += 16 + (uint64_t)data + 4;
         if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
             cur.scratch_off = b->scratch_bytes;
-            b->scratch_bytes += (slot + 255) & ~255u;
+            b->scratch_bytes += (slot + TE_LDS_FRONT + 64 + 255) & ~255u;
             if (b->n_tiles == cap_tiles)
                 b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
             b->tiles[b->n_tiles++] = cur;
@@ -342,6 +352,7 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
     L.zero_region = b->d_ws + WS_ZERO;
     L.zero_bytes = b->ws_bytes - WS_ZERO;
     L.grid = 256 * 4;
+    L.slot_layout = b->slot_layout;
     return te_launch_edit(&L, t->stream);
 }
 
@@ -364,6 +375,8 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
                              t->stream));
     HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    b->err[0] = ~b->err[0]; /* stored complemented (0 = no error -> ~0) */
+    b->err[1] = ~b->err[1];
     HIPCHK(t, hipEventElapsedTime(&ms, b->ev0, b->ev1));
     b->kernel_ms = ms;
     b->ran = 1;

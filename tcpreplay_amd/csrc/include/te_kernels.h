@@ -21,6 +21,12 @@ extern "C" {
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
+#define TE_LDS_FRONT 16        /* front pad of the LDS image (funnel reads never go below 0) */
+
+/* contiguous layout: a tile's span (starting g bytes into its 16-byte chunk)
+ * fits the LDS image when this holds */
+#define TE_CONTIG_FITS(g, span) ((uint32_t)(g) + (uint32_t)(span) + 16u <= (uint32_t)TE_SLOT_BYTES)
+
 #define TE_SLOT_BYTES_OF(g, data) \
     ((((uint32_t)TE_HEAD + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
 
@@ -52,11 +58,12 @@ typedef struct {
     unsigned int *ticket;     /* device */
     uint8_t *status;          /* device: one byte per record */
     uint64_t *counters;       /* device: TE_CNT__N */
-    uint64_t *err;            /* device: [0] first error record, [1] its output offset, [2] timeouts */
+    uint64_t *err;            /* device: [0] ~first error record, [1] ~its output offset, [2] timeouts */
     uint8_t *scratch;         /* device: huge-record slots */
     void *zero_region;        /* device range zeroed before each launch */
     uint64_t zero_bytes;
     int grid;                 /* blocks to launch (persistent, tiles taken by ticket) */
+    int slot_layout;          /* 1: per-record LDS slots (--enet-vlan=add, --fixlen=pad); 0: contiguous */
 } te_launch_t;
 
 #ifdef __HIP_PLATFORM_AMD__

@@ -50,7 +50,8 @@ struct Pkt {
     u8 *d;        // packet data (record header sits at d - 16)
     u32 caplen;   // current pcap caplen
     u32 len;      // current pcap len
-    u32 avail;    // bytes materialised from d (>= caplen; the rest of the slot is the zero tail)
+    u32 phys;     // bytes from d that hold what the reference's buffer holds (its physical extent)
+    u32 avail;    // bytes from d this lane may write (>= phys; slot tail or nothing)
     bool unsupported;
 };
 
@@ -392,9 +393,9 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
     // zero padding may be read (fixlen pad); anything else is the reference's
     // stale static buffer (Q8) which a lane cannot see.
     const int ipoff = (int)(ip - pk.d);
-    auto readable = [&](int nbytes) -> int {  // the sum's bytes must lie below caplen
-        if (ipoff + ip_hl + nbytes > (int)pk.caplen) pk.unsupported = true;
-        int lim = (int)pk.avail - (ipoff + ip_hl);
+    auto readable = [&](int nbytes) -> int {  // bytes past `phys` are the reference's stale buffer
+        int lim = (int)pk.phys - (ipoff + ip_hl);
+        if (nbytes > lim) pk.unsupported = true;
         return nbytes <= lim ? nbytes : (lim < 0 ? 0 : lim);
     };
     u8 *l4 = ip + ip_hl;
@@ -403,7 +404,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         case 6:
         case 44: {  // IPPROTO_TCP, IPPROTO_TCP_V6FRAG (tcpr.h:655)
             if (len < 20) return RC_WARN;
-            if (ipoff + ip_hl + 18 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 18 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
             st16(l4 + 16, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
             sum += bswap16((u16)(6 + len));
@@ -413,7 +414,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 17: {
             if (len < 8) return RC_WARN;
-            if (ipoff + ip_hl + 8 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 8 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
             if (ld16(l4 + 6) == 0) break;
             st16(l4 + 6, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
@@ -424,7 +425,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 1: {
             if (len < 4) return RC_WARN;
-            if (ipoff + ip_hl + 4 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 4 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
             st16(l4 + 2, 0);
             if (v6) {
                 // CHECKSUM_CARRY assigns its argument; the interim value lands in
@@ -440,7 +441,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 58: {
             if (len < 8) return RC_WARN;
-            if (ipoff + ip_hl + 4 > (int)pk.avail) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 4 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
             st16(l4 + 2, 0);
             if (v6) sum = csum_bytes(ip + 8, 32);
             sum += bswap16((u16)(58 + len));
@@ -484,7 +485,7 @@ DI int ipv6_header_length(Pkt &pk, const u8 *ip6, u32 pkt_len, int l2len) {
     const int ipoff = (int)(ip6 - pk.d);
     for (int guard = 0; guard < 65536 && (u32)(2 + offset + l2len) < pkt_len; ++guard) {
         if (nh != 0 && nh != 43 && nh != 44) return offset;
-        if (ipoff + offset + 2 > (int)pk.avail) { pk.unsupported = true; return offset; }
+        if (ipoff + offset + 2 > (int)pk.phys) { pk.unsupported = true; return offset; }
         nh = ip6[offset];
         offset += (ip6[offset + 1] + 1) << 3;
     }
@@ -538,10 +539,9 @@ DI void ipv6_addr_csum_replace(Pkt &pk, u8 *ip6, const u8 *old_ip, const u8 *new
     int l4 = l4_v6(ip6, 0, l3len);
     if (l4 < 0) return;
     int fld = proto == 6 ? 16 : (proto == 17 ? 6 : 2);
-    if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.caplen) {
-        // the field lies past caplen: the reference reads its static buffer there
-        if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.avail) { pk.unsupported = true; return; }
+    if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.phys) {  // past the physical packet: stale bytes
         pk.unsupported = true;
+        return;
     }
     if (proto == 17 && ld16(ip6 + l4 + 6) == 0) return;
     csum_replace16(ip6 + l4 + fld, old_ip, new_ip);
@@ -603,8 +603,10 @@ DI int rewrite_ports(const u16 *lut, u8 proto, u8 *l4, int l4len) {
 // rewrite_seqs (rewrite_sequence.c:37-55)
 DI void rewrite_seqs(Pkt &pk, const te_dev_cfg_t &cfg, u8 *tcp) {
     int off = (int)(tcp - pk.d);
-    if (off + 18 > (int)pk.caplen) pk.unsupported = true;  // fields read past caplen (stale)
-    if (off + 18 > (int)pk.avail) return;
+    if (off + 18 > (int)pk.phys) {  // fields past the physical packet (stale bytes)
+        pk.unsupported = true;
+        return;
+    }
     u32 ns = be32(tcp + 4) + cfg.tcp_sequence_adjust;
     csum_replace4(tcp + 16, ld32(tcp + 4), bswap32(ns));
     st32(tcp + 4, bswap32(ns));
@@ -668,7 +670,7 @@ DI void rewrite_ipv6_addr_pair(Pkt &pk, const te_dev_cfg_t &cfg, const te_cidr_t
     u8 old[16];
 #pragma unroll
     for (int b = 0; b < 16; ++b) old[b] = ip6[aoff + b];
-    int room = (int)pk.avail - ((int)(ip6 - pk.d) + aoff);
+    int room = (int)pk.phys - ((int)(ip6 - pk.d) + aoff);
     if (!remap_ipv6(cfg, to, ip6 + aoff, room)) pk.unsupported = true;
     ipv6_addr_csum_replace(pk, ip6, old, ip6 + aoff, l3len);
 }
@@ -727,15 +729,19 @@ DI void rewrite_ipv6l3(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip6, int dir, int l
 // randomize_iparp (edit_packet.c:1025-1083) / rewrite_iparp (:1093-1198)
 DI bool arp_addrs(Pkt &pk, u8 *arp, u8 **ip1, u8 **ip2) {
     int base = (int)(arp - pk.d);
-    if (base + 8 > (int)pk.caplen) pk.unsupported = true;  // ARP header read past caplen
-    if (base + 8 > (int)pk.avail) return false;
+    if (base + 8 > (int)pk.phys) {  // ARP header past the physical packet
+        pk.unsupported = true;
+        return false;
+    }
     if (be16(arp + 2) != 0x0800) return false;
     u16 op = be16(arp + 6);
     if (op != 1 && op != 2) return false;
     int o1 = 8 + arp[4];
     int o2 = o1 + arp[5] + arp[4];
-    if (base + o2 + 4 > (int)pk.caplen) pk.unsupported = true;  // address bytes past caplen
-    if (base + o2 + 4 > (int)pk.avail) return false;
+    if (base + o2 + 4 > (int)pk.phys) {  // address bytes past the physical packet
+        pk.unsupported = true;
+        return false;
+    }
     *ip1 = arp + o1;
     *ip2 = arp + o2;
     return true;
@@ -787,7 +793,7 @@ DI int untrunc_packet(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip, u8 *ip6) {
             chksum = 0;
         } else if (ip[9] == 17 && (off & 0x2000)) {
             int f = (int)(ip - pk.d) + ((ip[0] & 0x0f) << 2) + 6;
-            if (f + 2 > (int)pk.avail) pk.unsupported = true;
+            if (f + 2 > (int)pk.phys) pk.unsupported = true;
             else st16(pk.d + f, 0);
             chksum = 0;
         }
@@ -798,6 +804,7 @@ DI int untrunc_packet(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip, u8 *ip6) {
             // for max(caplen, len) when --fixlen=pad is set
             if (pk.len > pk.avail) pk.unsupported = true;
             for (u32 i = pk.caplen; i < pk.avail && i < pk.len; ++i) pk.d[i] = 0;
+            if (pk.len > pk.phys) pk.phys = pk.len < pk.avail ? pk.len : pk.avail;
             pk.caplen = pk.len;
         } else if (pk.len < pk.caplen) {
             return -1;
@@ -883,8 +890,12 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
             for (int i = (int)(16 + newl2) - 1; i >= 0; --i) dst[i] = src[i];
             pk.d += 4;
             pk.avail -= 4;
+            pk.phys -= 4;
         }
-        if (newl2 > oldl2) pk.avail += 4;
+        if (newl2 > oldl2) {
+            pk.avail += 4;
+            pk.phys += 4;
+        }
     }
     pktlen += (int)(newl2 - oldl2);
     u8 *eth = pk.d + s.l2offset;

@@ -1,19 +1,22 @@
 // tcpedit_kernels.hip -- gfx950 kernels for the tcpedit rewrite path.
 //
-// One kernel, te_edit_tiles, runs the whole device pipeline of
+// One kernel, te_edit_tiles<LAYOUT>, runs the whole device pipeline of
 // rewrite_packets() (src/tcprewrite.c:260-373) over a pcap image resident in
 // HBM, in a single pass:
-//   1. a block takes the next tile ticket (tiles = runs of consecutive records,
-//      built from the record index so their LDS slots fit the block's budget);
-//   2. the tile's byte span is streamed HBM -> LDS with 16-byte loads, each
-//      record landing in its own slot whose alignment mod 16 equals its HBM
-//      alignment (so every chunk is one aligned 16-byte LDS store);
-//   3. one lane per packet runs tcpedit_packet() in LDS (edit_pkt.hpp);
+//   1. a block takes the next tile ticket (tiles = runs of consecutive records
+//      whose bytes fit the block's LDS budget, built from the record index);
+//   2. the tile's byte span is streamed HBM -> LDS with 16-byte loads:
+//        CONTIG: the span lands as-is (one straight copy; the common case),
+//        SLOT:   each record lands in its own slot with headroom/zeroed room
+//                (needed only by --enet-vlan=add and --fixlen=pad), the slot
+//                aligned like the record so every chunk is one 16-byte store;
+//   3. one lane per packet runs tcpedit_packet() on its LDS bytes (edit_pkt.hpp);
 //   4. a block scan of the output record sizes plus a decoupled look-back over
 //      earlier tiles gives the tile's output offset (no second pass over HBM);
-//   5. the block streams its output records LDS -> HBM as 16-byte chunks.
-// Records too large for a tile are staged in an HBM scratch slot instead
-// (same code, the slot pointer is in the global address space).
+//   5. the block streams its output LDS -> HBM in 16-byte chunks, funnel-
+//      shifting aligned LDS dwords; tiles whose records keep their length (the
+//      common case) are one contiguous LDS -> HBM copy.
+// Records too large for a tile are edited in an HBM scratch slot instead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "edit_pkt.hpp"
@@ -25,6 +28,22 @@ namespace {
 
 constexpr int BLOCK = TE_BLOCK;
 constexpr int NWAVES = BLOCK / 64;
+constexpr int LDS_FRONT = TE_LDS_FRONT;  // front pad so funnel reads never index below 0
+constexpr int MODE_CONTIG = 0, MODE_SLOT = 1;
+
+// explicit global / constant address spaces (device pass only): pointers
+// loaded from the argument struct are otherwise generic and compile to FLAT ops
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TE_AS_GLOBAL __attribute__((address_space(1)))
+#define TE_AS_CONST __attribute__((address_space(4)))
+#else
+#define TE_AS_GLOBAL
+#define TE_AS_CONST
+#endif
+typedef TE_AS_GLOBAL uint8_t g_u8;
+typedef TE_AS_GLOBAL const uint8_t g_cu8;
+typedef TE_AS_GLOBAL const uint4 g_cu4;
+typedef TE_AS_GLOBAL uint4 g_u4;
 
 struct LaunchArgs {
     const te_dev_cfg_t *cfg;
@@ -44,7 +63,7 @@ struct LaunchArgs {
     unsigned int *ticket;            // zeroed per launch
     uint8_t *status;
     unsigned long long *counters;    // TE_CNT__N, zeroed per launch
-    unsigned long long *err;         // [0] first error pkt, [1] its out offset, [2] look-back timeouts
+    unsigned long long *err;         // [0] ~first error pkt, [1] ~its out offset (0 = none), [2] look-back timeouts
     uint8_t *scratch;                // HBM slots for huge tiles
 };
 
@@ -81,8 +100,8 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uin
 // hand-off (cdna_hip_programming.md G16 "R2"), so no fences are needed.
 constexpr unsigned long long F_AGG = 1ull << 62, F_PFX = 2ull << 62, VMASK = (1ull << 62) - 1;
 
-__device__ unsigned long long lookback(unsigned long long *state, uint32_t t, unsigned long long agg,
-                                       unsigned long long *err) {
+__device__ __forceinline__ unsigned long long lookback(unsigned long long *state, uint32_t t, unsigned long long agg,
+                                                       unsigned long long *err) {
     if (t == 0) {
         __hip_atomic_store(&state[0], F_PFX | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
@@ -110,73 +129,112 @@ __device__ unsigned long long lookback(unsigned long long *state, uint32_t t, un
     return excl;
 }
 
-// ---------------------------------------------------------------------------
-// tile body.  S = slot buffer (LDS for normal tiles, HBM scratch for huge).
-// ---------------------------------------------------------------------------
 struct TileShared {
     uint32_t rel[TE_MAX_PKTS + 1];   // record offset in span (+ sentinel)
-    uint32_t rpos[TE_MAX_PKTS];      // LDS/slot position of record start (after editing)
+    uint32_t rpos[TE_MAX_PKTS];      // slot position of the output record start
     uint32_t opfx[TE_MAX_PKTS + 1];  // exclusive output prefix (+ total)
     uint32_t wsum[NWAVES];
     unsigned long long cnt[TE_CNT__N];
     unsigned long long out_excl;
     uint32_t tile_id;
+    uint32_t ident;                  // every record kept its input size (contiguous output)
 };
 
-template <bool HUGE>
-__device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t, uint8_t *S, TileShared &sh) {
+// 16 bytes of the slot buffer starting at byte `base` (any alignment): five
+// aligned dword reads and four byte-funnel shifts.
+template <typename P>
+__device__ __forceinline__ uint4 read16(P S, uint32_t base) {
+    const uint32_t a = base & ~3u, sh = base & 3u;
+    const uint32_t *w = (const uint32_t *)(S + a);
+    uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    if (sh == 0) return make_uint4(w0, w1, w2, w3);
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+__device__ __forceinline__ uint32_t sel_bytes(uint32_t x, uint32_t y, int b0, int b1, int k) {
+    // bytes [b0,b1) of dword k (bytes 4k..4k+3) from y, the rest from x
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int b = 4 * k + i;
+        if (b >= b0 && b < b1) m |= 0xffu << (8 * i);
+    }
+    return (x & ~m) | (y & m);
+}
+
+// ---------------------------------------------------------------------------
+// tile body.  S = slot buffer (LDS, or HBM scratch for a huge record).
+// ---------------------------------------------------------------------------
+template <int MODE, typename P>
+__device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t, P S,
+                                          TileShared &sh, const te_dev_cfg_t &cfg) {
     const int tid = threadIdx.x;
     const uint32_t npkt = tile.npkt;
-    const uint64_t G0 = tile.span_off;  // global offset of the span
-    const bool pad = a.cfg->fixlen == TE_FIXLEN_PAD;
+    const uint64_t G0 = tile.span_off;  // HBM offset of the span
+    const uint64_t A0 = G0 & ~15ull;    // first aligned chunk
     const bool swp = a.in_swapped != 0;
+    g_cu8 *gin = (g_cu8 *)a.in;
 
-    // ---- slot layout: sizes from the record index ----
-    uint32_t my_rel = 0, my_cap = 0, my_slot = 0;
+    // ---- record positions ----
+    uint32_t my_rel = 0, my_cap = 0, my_slot = 0, r0 = 0, slot_end = 0;
     if (tid < (int)npkt) {
         my_rel = a.pkt_rel[tile.first_pkt + tid];
         uint32_t nxt = (tid + 1 < (int)npkt) ? a.pkt_rel[tile.first_pkt + tid + 1] : tile.span_len;
         my_cap = nxt - my_rel - 16;
-        uint32_t data = my_cap;
-        if (pad) {
-            uint32_t plen = ld_hdr32(a.in + G0 + my_rel + 12, swp);
-            if (plen > data) data = plen;
-        }
-        uint32_t g = (uint32_t)((G0 + my_rel) & 15);
-        my_slot = TE_SLOT_BYTES_OF(g, data);
         sh.rel[tid] = my_rel;
     }
     if (tid == 0) sh.rel[npkt] = tile.span_len;
-    uint32_t total_slot;
-    uint32_t slot_base = block_exscan(my_slot, sh.wsum, total_slot);
-    (void)total_slot;
-    uint32_t r0 = 0;  // record start in S (before editing)
-    if (tid < (int)npkt) {
-        r0 = slot_base + TE_HEAD + (uint32_t)((G0 + my_rel) & 15);
-        sh.rpos[tid] = r0;
+    if constexpr (MODE == MODE_SLOT) {
+        if (tid < (int)npkt) {
+            uint32_t data = my_cap;
+            if (cfg.fixlen == TE_FIXLEN_PAD) {
+                const g_cu8 *lp = gin + G0 + my_rel + 12;
+                uint32_t plen = (uint32_t)lp[0] | ((uint32_t)lp[1] << 8) | ((uint32_t)lp[2] << 16) |
+                                ((uint32_t)lp[3] << 24);
+                if (swp) plen = bswap32(plen);
+                if (plen > data) data = plen;
+            }
+            my_slot = TE_SLOT_BYTES_OF((uint32_t)((G0 + my_rel) & 15), data);
+        }
+        uint32_t total_slot;
+        uint32_t slot_base = LDS_FRONT + block_exscan(my_slot, sh.wsum, total_slot);
+        if (tid < (int)npkt) {
+            r0 = slot_base + TE_HEAD + (uint32_t)((G0 + my_rel) & 15);
+            slot_end = slot_base + my_slot;
+            sh.rpos[tid] = r0;
+        }
+    } else {
+        if (tid < (int)npkt) {
+            r0 = LDS_FRONT + (uint32_t)(G0 - A0) + my_rel;
+            slot_end = r0 + 16 + my_cap;
+            sh.rpos[tid] = r0;
+        }
     }
     __syncthreads();
 
-    // ---- stream the span into the slots: aligned 16-byte chunks ----
+    // ---- stream the span into LDS: aligned 16-byte chunks ----
     {
-        const uint64_t A0 = G0 & ~15ull;
         const uint64_t Aend = G0 + tile.span_len;
         const uint32_t nchunks = (uint32_t)((Aend - A0 + 15) >> 4);
         for (uint32_t c = tid; c < nchunks; c += BLOCK) {
             const uint64_t A = A0 + ((uint64_t)c << 4);
-            const uint4 v = *reinterpret_cast<const uint4 *>(a.in + A);
-            // first record whose start is <= A (binary search on rel)
-            int64_t rA = (int64_t)A - (int64_t)G0;
-            int lo = 0, hi = (int)npkt - 1;
-            while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
-                if ((int64_t)sh.rel[mid] <= rA) lo = mid;
-                else hi = mid - 1;
-            }
-            for (int p = lo; p < (int)npkt && (int64_t)sh.rel[p] < rA + 16; ++p) {
-                if ((int64_t)sh.rel[p + 1] <= rA) continue;  // record ends before chunk
-                const int64_t dst = (int64_t)sh.rpos[p] + (rA - (int64_t)sh.rel[p]);
-                *reinterpret_cast<uint4 *>(S + dst) = v;
+            const uint4 v = *(g_cu4 *)(gin + A);
+            if constexpr (MODE == MODE_CONTIG) {
+                *(uint4 *)(S + LDS_FRONT + (c << 4)) = v;
+            } else {
+                int64_t rA = (int64_t)A - (int64_t)G0;
+                int lo = 0, hi = (int)npkt - 1;
+                while (lo < hi) {
+                    int mid = (lo + hi + 1) >> 1;
+                    if ((int64_t)sh.rel[mid] <= rA) lo = mid;
+                    else hi = mid - 1;
+                }
+                for (int p = lo; p < (int)npkt && (int64_t)sh.rel[p] < rA + 16; ++p) {
+                    if ((int64_t)sh.rel[p + 1] <= rA) continue;
+                    const int64_t dst = (int64_t)sh.rpos[p] + (rA - (int64_t)sh.rel[p]);
+                    *(uint4 *)(S + dst) = v;
+                }
             }
         }
     }
@@ -185,12 +243,11 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
     // ---- one lane per packet ----
     uint32_t out_sz = 0;
     uint8_t st = 0;
-    unsigned long long c_in = 0, c_out = 0;
+    unsigned long long c_in = 0;
     if (tid < (int)npkt) {
-        uint8_t *rec = S + r0;
-        uint32_t slot_end = slot_base + my_slot;
-        // zero the tail (chunk stores spilled up to 15 foreign bytes into it)
-        for (uint32_t i = r0 + 16 + my_cap; i < slot_end; ++i) S[i] = 0;
+        uint8_t *rec = (uint8_t *)(S + r0);
+        if constexpr (MODE == MODE_SLOT)  // zero the room after the data (chunk stores spilled into it)
+            for (uint32_t i = r0 + 16 + my_cap; i < slot_end; ++i) S[i] = 0;
         uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp);
         uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
         if (a.in_nsec) ts_frac /= 1000;  // libpcap opens at us precision
@@ -210,6 +267,7 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
         pk.d = rec + 16;
         pk.caplen = caplen;
         pk.len = len;
+        pk.phys = my_cap;
         pk.avail = slot_end - (r0 + 16);
         pk.unsupported = false;
         int rc = RC_OK;
@@ -217,7 +275,7 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
         if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
             st |= TE_ST_NOSEND;
         } else {
-            rc = tcpedit_packet(pk, *a.cfg, a.portlut, dir, warned);
+            rc = tcpedit_packet(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned);
         }
         if (pk.unsupported) st |= TE_ST_UNSUPPORTED;
         if (warned) st |= TE_ST_WARNED;
@@ -227,7 +285,7 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
             write = false;
         } else if (rc == RC_SOFT) {
             st |= TE_ST_RC_SOFT;
-            if (a.cfg->skip_soft_errors) {
+            if (cfg.skip_soft_errors) {
                 st |= TE_ST_DROPPED;
                 write = false;
             }
@@ -239,38 +297,45 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
             write = false;
         }
         uint8_t *orec = pk.d - 16;
-        st32(orec, ts_sec);
-        st32(orec + 4, ts_frac);
-        st32(orec + 8, pk.caplen);
-        st32(orec + 12, pk.len);
-        sh.rpos[tid] = (uint32_t)(orec - S);
+        if (swp || a.in_nsec || pk.d != rec + 16) {
+            st32(orec, ts_sec);
+            st32(orec + 4, ts_frac);
+        }
+        if (swp || pk.caplen != caplen || pk.len != len || pk.d != rec + 16) {
+            st32(orec + 8, pk.caplen);
+            st32(orec + 12, pk.len);
+        }
+        sh.rpos[tid] = (uint32_t)(orec - (uint8_t *)S);
         if (write) out_sz = 16 + pk.caplen;
-        c_out = out_sz;
-        a.status[tile.first_pkt + tid] = st;
+        ((g_u8 *)a.status)[tile.first_pkt + tid] = st;
     }
 
     // ---- tile output offsets ----
     uint32_t tile_total;
+    const bool keep = tid >= (int)npkt || (out_sz == 16 + my_cap && sh.rpos[tid] == r0);
     uint32_t opos = block_exscan(out_sz, sh.wsum, tile_total);
     if (tid < (int)npkt) sh.opfx[tid] = opos;
-    if (tid == 0) sh.opfx[npkt] = tile_total;
+    if (tid == 0) {
+        sh.opfx[npkt] = tile_total;
+        sh.ident = 1;
+    }
+    if (tid < TE_CNT__N) sh.cnt[tid] = 0;
+    __syncthreads();
+    if (!keep) sh.ident = 0;  // benign race: every writer stores 0
 
     // counters: wave reduce then LDS atomics
     {
-        unsigned long long v[TE_CNT__N] = {0};
-        if (tid < (int)npkt) {
-            v[TE_CNT_PACKETS] = 1;
-            v[TE_CNT_BYTES_IN] = c_in;
-            v[TE_CNT_BYTES_OUT] = c_out;
-            v[TE_CNT_WRITTEN] = out_sz ? 1 : 0;
-            v[TE_CNT_EDITED] = (!(st & TE_ST_NOSEND) && (st & TE_ST_RC_MASK) <= TE_ST_RC_WARN) ? 1 : 0;
-            v[TE_CNT_SOFT] = (st & TE_ST_RC_MASK) == TE_ST_RC_SOFT;
-            v[TE_CNT_WARN] = (st & TE_ST_WARNED) ? 1 : 0;
-            v[TE_CNT_ERROR] = (st & TE_ST_RC_MASK) == TE_ST_RC_ERROR;
-            v[TE_CNT_UNSUPPORTED] = (st & TE_ST_UNSUPPORTED) ? 1 : 0;
-        }
-        if (tid < TE_CNT__N) sh.cnt[tid] = 0;
-        __syncthreads();
+        unsigned long long v[TE_CNT__N];
+        const bool on = tid < (int)npkt;
+        v[TE_CNT_PACKETS] = on;
+        v[TE_CNT_BYTES_IN] = c_in;
+        v[TE_CNT_BYTES_OUT] = out_sz;
+        v[TE_CNT_WRITTEN] = out_sz ? 1 : 0;
+        v[TE_CNT_EDITED] = on && !(st & TE_ST_NOSEND) && (st & TE_ST_RC_MASK) <= TE_ST_RC_WARN;
+        v[TE_CNT_SOFT] = on && (st & TE_ST_RC_MASK) == TE_ST_RC_SOFT;
+        v[TE_CNT_WARN] = (st & TE_ST_WARNED) ? 1 : 0;
+        v[TE_CNT_ERROR] = on && (st & TE_ST_RC_MASK) == TE_ST_RC_ERROR;
+        v[TE_CNT_UNSUPPORTED] = (st & TE_ST_UNSUPPORTED) ? 1 : 0;
 #pragma unroll
         for (int k = 0; k < TE_CNT__N; ++k) {
             unsigned long long x = v[k];
@@ -284,8 +349,9 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
     if (tid < TE_CNT__N && sh.cnt[tid]) atomicAdd(&a.counters[tid], sh.cnt[tid]);
     const unsigned long long E = sh.out_excl;
     if (tid < (int)npkt && (st & TE_ST_RC_MASK) == TE_ST_RC_ERROR) {
-        atomicMin(&a.err[0], (unsigned long long)(tile.first_pkt + tid));
-        atomicMin(&a.err[1], E + opos);
+        // zero-initialised words hold ~value: atomicMax(~x) == ~min(x)
+        atomicMax(&a.err[0], ~(unsigned long long)(tile.first_pkt + tid));
+        atomicMax(&a.err[1], ~(a.out_base + E + opos));
     }
 
     // ---- stream the output records: aligned 16-byte chunks ----
@@ -294,42 +360,48 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
     const uint64_t Ge = Gs + tile_total;
     const uint64_t C0 = Gs & ~15ull;
     const uint32_t nchunks = (uint32_t)((Ge - C0 + 15) >> 4);
+    const bool ident = MODE == MODE_CONTIG && sh.ident != 0;
+    const uint32_t src0 = sh.rpos[0];  // ident: output byte q is slot byte src0 + q
+    g_u8 *gout = (g_u8 *)a.out;
     for (uint32_t c = tid; c < nchunks; c += BLOCK) {
         const uint64_t C = C0 + ((uint64_t)c << 4);
         const int64_t q0 = (int64_t)C - (int64_t)Gs;  // tile-relative output offset of the chunk
         const int b0 = q0 < 0 ? (int)(-q0) : 0;
         const int b1 = (C + 16 > Ge) ? (int)(Ge - C) : 16;
-        // packet holding byte q0+b0
-        const int64_t qf = q0 + b0;
-        int lo = 0, hi = (int)npkt - 1;
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if ((int64_t)sh.opfx[mid] <= qf) lo = mid;
-            else hi = mid - 1;
-        }
-        // gather the chunk's bytes from the records' slots (unrolled: registers only)
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int p = lo;
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {
-            if (b >= b0 && b < b1) {
-                const int64_t q = q0 + b;
-                while ((int64_t)sh.opfx[p + 1] <= q) ++p;
-                const uint32_t x = (uint32_t)S[sh.rpos[p] + (uint32_t)(q - (int64_t)sh.opfx[p])] << (8 * (b & 3));
-                if (b < 4) w0 |= x;
-                else if (b < 8) w1 |= x;
-                else if (b < 12) w2 |= x;
-                else w3 |= x;
+        uint4 v;
+        if (ident) {
+            v = read16(S, (uint32_t)((int64_t)src0 + q0));
+        } else {
+            // records overlapping the chunk: binary search the first, then walk
+            const int64_t qf = q0 + b0;
+            int lo = 0, hi = (int)npkt - 1;
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if ((int64_t)sh.opfx[mid] <= qf) lo = mid;
+                else hi = mid - 1;
+            }
+            v = make_uint4(0, 0, 0, 0);
+            for (int p = lo; p < (int)npkt && (int64_t)sh.opfx[p] < q0 + b1; ++p) {
+                const int64_t s0 = sh.opfx[p], s1 = sh.opfx[p + 1];
+                if (s1 <= q0 + b0) continue;
+                int pb0 = (int)((s0 - q0) > b0 ? (s0 - q0) : b0);
+                int pb1 = (int)((s1 - q0) < b1 ? (s1 - q0) : b1);
+                if (pb0 >= pb1) continue;
+                const uint4 w = read16(S, (uint32_t)((int64_t)sh.rpos[p] + (q0 - s0)));
+                v.x = sel_bytes(v.x, w.x, pb0, pb1, 0);
+                v.y = sel_bytes(v.y, w.y, pb0, pb1, 1);
+                v.z = sel_bytes(v.z, w.z, pb0, pb1, 2);
+                v.w = sel_bytes(v.w, w.w, pb0, pb1, 3);
             }
         }
-        uint8_t *dst = a.out + C;
+        g_u8 *dst = gout + C;
         if (b0 == 0 && b1 == 16) {
-            *reinterpret_cast<uint4 *>(dst) = make_uint4(w0, w1, w2, w3);
+            *(g_u4 *)dst = v;
         } else {
 #pragma unroll
             for (int b = 0; b < 16; ++b) {
                 if (b >= b0 && b < b1) {
-                    const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : (b < 12 ? w2 : w3));
+                    const uint32_t w = b < 4 ? v.x : (b < 8 ? v.y : (b < 12 ? v.z : v.w));
                     dst[b] = (uint8_t)(w >> (8 * (b & 3)));
                 }
             }
@@ -337,19 +409,39 @@ __device__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) te_edit_tiles(LaunchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES];
+// records larger than a tile: same body over an HBM scratch slot, kept out of
+// line and reading its arguments straight from the kernarg segment
+__device__ __attribute__((noinline)) void huge_tile(uint32_t t, const te_dev_cfg_t &cfg) {
+    const LaunchArgs &a = *(const LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    __shared__ TileShared hsh;
+    const te_tile_t tile = a.tiles[t];
+    tile_body<MODE_SLOT>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK, 3) te_edit_tiles(LaunchArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
+    __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
+    {
+        constexpr int NV = (int)((sizeof(te_dev_cfg_t) + 15) / 16);
+        static_assert(sizeof(te_dev_cfg_t) % 4 == 0, "cfg copy");
+        const uint32_t *src = (const uint32_t *)a.cfg;
+        uint32_t *dst = (uint32_t *)&cfg;
+        for (int i = threadIdx.x; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
+        (void)NV;
+    }
     for (;;) {
         if (threadIdx.x == 0) sh.tile_id = atomicAdd(a.ticket, 1u);
         __syncthreads();
         const uint32_t t = sh.tile_id;
+        __syncthreads();
         if (t >= a.n_tiles) return;
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
-            tile_body<false>(a, tile, t, slots, sh);
+            tile_body<MODE>(a, tile, t, slots, sh, cfg);
         else
-            tile_body<true>(a, tile, t, a.scratch + tile.scratch_off, sh);
+            huge_tile(t, cfg);
         __syncthreads();
     }
 }
@@ -381,15 +473,16 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.counters = (unsigned long long *)L->counters;
     a.err = (unsigned long long *)L->err;
     a.scratch = L->scratch;
-    if (L->n_tiles == 0) return 0;
+    // one memset per launch: error words, ticket, counters, look-back granules
     hipError_t e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);
     if (e != hipSuccess) return -1;
-    // err[0], err[1] start at ~0 (atomicMin targets)
-    e = hipMemsetAsync(L->err, 0xff, 2 * sizeof(uint64_t), stream);
-    if (e != hipSuccess) return -1;
+    if (L->n_tiles == 0) return 0;
     int grid = L->grid > 0 ? L->grid : 1;
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
-    hipLaunchKernelGGL(te_edit_tiles, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (L->slot_layout)
+        hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    else
+        hipLaunchKernelGGL(te_edit_tiles<MODE_CONTIG>, dim3(grid), dim3(BLOCK), 0, stream, a);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
 }
