@@ -13,7 +13,7 @@ __all__ = ["TcpEdit", "Batch", "BatchResult", "load", "LIB_PATH", "TCPEDIT_OK", 
            "TCPEDIT_SOFT_ERROR", "TCPEDIT_WARN", "ST"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtcpedit_hip.so")
+LIB_PATH = os.environ.get("TCPEDIT_HIP_LIB") or os.path.join(HERE, "lib", "libtcpedit_hip.so")
 
 TCPEDIT_SOFT_ERROR, TCPEDIT_ERROR, TCPEDIT_OK, TCPEDIT_WARN = -2, -1, 0, 1
 TCPR_DIR_NOSEND, TCPR_DIR_C2S, TCPR_DIR_S2C = 0, 1, 2

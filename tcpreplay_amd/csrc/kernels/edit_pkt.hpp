@@ -14,7 +14,13 @@
 // Byte order: like the reference on x86, multi-byte fields are loaded in host
 // (little-endian) order and all checksum arithmetic runs on those LE values.
 #pragma once
+#ifdef TE_HOST_EMU  // host build of the same logic, for debugging harnesses only
+#include <stdint.h>
+#define __device__
+#define __forceinline__ inline
+#else
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 #include "te_dev_cfg.h"
 #include "te_kernels.h"
@@ -858,6 +864,14 @@ DI int en10mb_decode(const u8 *pkt, int pktlen, Dec &s) {
     s.proto = bswap16(prot);
     s.l2offset = (int)r.l2offset;
     s.l2len = (int)r.l2len;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Optimisation barrier.  Without it the gfx950 backend (ROCm 7.2, -O1..-O3)
+    // re-materialises l2offset as 0 in en10mb_encode for EoMPLS frames whose
+    // inner Ethernet carries an 802.1Q tag (test.pcap records 142/150/157/170/
+    // 174-179), writing the inner MACs over the outer ones; the host build of
+    // this same code is correct.  Pinning the decoded offsets in VGPRs costs nothing.
+    asm volatile("" : "+v"(s.l2offset), "+v"(s.vlan_offset), "+v"(s.l2len));
+#endif
     return RC_OK;
 }
 

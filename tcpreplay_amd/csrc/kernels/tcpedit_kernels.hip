@@ -410,16 +410,23 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
 }
 
 // records larger than a tile: same body over an HBM scratch slot, kept out of
-// line and reading its arguments straight from the kernarg segment
-__device__ __attribute__((noinline)) void huge_tile(uint32_t t, const te_dev_cfg_t &cfg) {
-    const LaunchArgs &a = *(const LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+// line.  The arguments are read through the kernel's kernarg segment, whose
+// address the kernel passes in: the kernarg-pointer builtin is only defined in
+// a kernel entry (a callee gets null), and taking &a in the kernel would copy
+// the arguments to scratch for every tile.
+__device__ __attribute__((noinline)) void huge_tile(const TE_AS_CONST LaunchArgs *ka, uint32_t t,
+                                                    const te_dev_cfg_t &cfg) {
+    const LaunchArgs &a = *(const LaunchArgs *)ka;
     __shared__ TileShared hsh;
     const te_tile_t tile = a.tiles[t];
     tile_body<MODE_SLOT>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
 }
 
+#ifndef TE_MIN_WAVES
+#define TE_MIN_WAVES 3
+#endif
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK, 3) te_edit_tiles(LaunchArgs a) {
+__global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
@@ -441,7 +448,7 @@ __global__ void __launch_bounds__(BLOCK, 3) te_edit_tiles(LaunchArgs a) {
         if (tile.scratch_off == TE_NO_SCRATCH)
             tile_body<MODE>(a, tile, t, slots, sh, cfg);
         else
-            huge_tile(t, cfg);
+            huge_tile((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
         __syncthreads();
     }
 }
