@@ -45,6 +45,7 @@ struct tcpedit_batch_s {
     int status_valid;
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
     int slot_layout;
+    int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
     /* device side */
     uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
     uint64_t dirbits_len;
@@ -103,6 +104,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
     b->out_cap = 24 + 64;
     b->scratch_bytes = 0;
     b->stop_error_pkt = -1;
+    b->has_zero_cap = 0;
     size_t off = 24;
     te_tile_t cur;
     memset(&cur, 0, sizeof(cur));
@@ -117,6 +119,8 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
             b->stop_error_pkt = (int64_t)b->n_pkts;
             break;
         }
+        if (caplen == 0)
+            b->has_zero_cap = 1;
         uint32_t data = pad && plen > caplen ? plen : caplen;
         uint32_t g = (uint32_t)(off & 15);
         uint32_t slot = TE_SLOT_BYTES_OF(g, data);
@@ -351,8 +355,15 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
     L.scratch = b->d_scratch;
     L.zero_region = b->d_ws + WS_ZERO;
     L.zero_bytes = b->ws_bytes - WS_ZERO;
-    L.grid = 256 * 4;
+    L.grid = 0; /* resident blocks (CUs x occupancy) */
     L.slot_layout = b->slot_layout;
+    /* size-preserving config: no edit step can change a record's length or drop
+       it (efcs, VLAN add/del, fixlen, MTU truncation, skipped soft errors, and
+       zero-length records are the only ways), so outputs sit at input offsets */
+    const te_dev_cfg_t *c = &t->cfg;
+    L.static_off = !b->slot_layout && !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF &&
+                   !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap;
+    L.rec0 = 24;
     return te_launch_edit(&L, t->stream);
 }
 

@@ -64,6 +64,9 @@ typedef struct {
     uint64_t zero_bytes;
     int grid;                 /* blocks to launch (persistent, tiles taken by ticket) */
     int slot_layout;          /* 1: per-record LDS slots (--enet-vlan=add, --fixlen=pad); 0: contiguous */
+    int static_off;           /* 1: no record can change size or be dropped, so every output
+                                 record sits at its input offset: no scan, no look-back */
+    uint64_t rec0;            /* input offset of the first record (static_off: out = in - rec0 + out_base) */
 } te_launch_t;
 
 #ifdef __HIP_PLATFORM_AMD__

@@ -65,6 +65,8 @@ struct LaunchArgs {
     unsigned long long *counters;    // TE_CNT__N, zeroed per launch
     unsigned long long *err;         // [0] ~first error pkt, [1] ~its out offset (0 = none), [2] look-back timeouts
     uint8_t *scratch;                // HBM slots for huge tiles
+    uint64_t rec0;                   // static_off: input offset of the first record
+    uint32_t static_off;             // output offsets == input offsets (size-preserving config)
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -95,37 +97,50 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uin
     return base + x - v;
 }
 
-// ---- decoupled look-back (single lane).  Granule = {flag:2 | value:62}
-// stored/polled as one relaxed agent-scope 8-byte atomic: the value IS the
-// hand-off (cdna_hip_programming.md G16 "R2"), so no fences are needed.
+// ---- decoupled look-back, one wave.  Granule = {flag:2 | value:62} stored/
+// polled as one relaxed agent-scope 8-byte atomic: the value IS the hand-off
+// (cdna_hip_programming.md G16 "R2"), so no fences are needed.  Each round
+// polls the 64 nearest unresolved predecessors at once (lane k = tile j-k):
+// one cross-XCD round trip per 64 tiles of depth instead of one per tile.
+// Called by all 64 lanes of wave 0; returns the exclusive prefix on every lane.
 constexpr unsigned long long F_AGG = 1ull << 62, F_PFX = 2ull << 62, VMASK = (1ull << 62) - 1;
 
 __device__ __forceinline__ unsigned long long lookback(unsigned long long *state, uint32_t t, unsigned long long agg,
                                                        unsigned long long *err) {
+    const int lane = threadIdx.x & 63;
     if (t == 0) {
-        __hip_atomic_store(&state[0], F_PFX | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&state[0], F_PFX | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    __hip_atomic_store(&state[t], F_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(&state[t], F_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long excl = 0;
-    int64_t j = (int64_t)t - 1;
+    int64_t j = (int64_t)t - 1;  // nearest unresolved predecessor
     unsigned spins = 0;
     while (j >= 0) {
-        unsigned long long g = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long f = g & ~VMASK;
-        if (f == 0) {
-            if (++spins > (1u << 26)) {  // bounded spin: report and give up
-                atomicAdd(&err[2], 1ull);
+        const int64_t idx = j - lane;
+        unsigned long long g = F_PFX;  // before tile 0: prefix 0
+        if (idx >= 0) g = __hip_atomic_load(&state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long f = g & ~VMASK;
+        const unsigned long long pm = __ballot(f == F_PFX), zm = __ballot(f == 0);
+        const int first_p = pm ? __builtin_ctzll(pm) : 64;
+        const int first_z = zm ? __builtin_ctzll(zm) : 64;
+        const int take = first_z < first_p ? first_z : (first_p < 64 ? first_p + 1 : 64);
+        unsigned long long v = lane < take ? (g & VMASK) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (first_p < first_z) break;  // reached an inclusive prefix
+        j -= take;
+        if (first_z < 64) {  // a predecessor has not published yet
+            if (++spins > (1u << 24)) {  // bounded spin: report and give up
+                if (lane == 0) atomicAdd(&err[2], 1ull);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            continue;
         }
-        excl += g & VMASK;
-        if (f == F_PFX) break;
-        --j;
     }
-    __hip_atomic_store(&state[t], F_PFX | ((excl + agg) & VMASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&state[t], F_PFX | ((excl + agg) & VMASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 
@@ -311,17 +326,28 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     }
 
     // ---- tile output offsets ----
-    uint32_t tile_total;
-    const bool keep = tid >= (int)npkt || (out_sz == 16 + my_cap && sh.rpos[tid] == r0);
-    uint32_t opos = block_exscan(out_sz, sh.wsum, tile_total);
-    if (tid < (int)npkt) sh.opfx[tid] = opos;
-    if (tid == 0) {
-        sh.opfx[npkt] = tile_total;
-        sh.ident = 1;
+    // static_off: sizes are preserved, so output offsets are the input offsets
+    // (no scan, no look-back); otherwise block scan + decoupled look-back.
+    const bool stat = a.static_off != 0;
+    uint32_t tile_total, opos;
+    bool keep = true;
+    if (MODE == MODE_CONTIG && stat) {
+        opos = my_rel;
+        tile_total = tile.span_len;
+        if (tid < TE_CNT__N) sh.cnt[tid] = 0;
+        __syncthreads();
+    } else {
+        keep = tid >= (int)npkt || (out_sz == 16 + my_cap && sh.rpos[tid] == r0);
+        opos = block_exscan(out_sz, sh.wsum, tile_total);
+        if (tid < (int)npkt) sh.opfx[tid] = opos;
+        if (tid == 0) {
+            sh.opfx[npkt] = tile_total;
+            sh.ident = 1;
+        }
+        if (tid < TE_CNT__N) sh.cnt[tid] = 0;
+        __syncthreads();
+        if (!keep) sh.ident = 0;  // benign race: every writer stores 0
     }
-    if (tid < TE_CNT__N) sh.cnt[tid] = 0;
-    __syncthreads();
-    if (!keep) sh.ident = 0;  // benign race: every writer stores 0
 
     // counters: wave reduce then LDS atomics
     {
@@ -344,7 +370,12 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             if ((tid & 63) == 0 && x) atomicAdd(&sh.cnt[k], x);
         }
     }
-    if (tid == 0) sh.out_excl = lookback(a.tile_state, t, tile_total, a.err);
+    if (stat) {
+        if (tid == 0) sh.out_excl = tile.span_off - a.rec0;
+    } else if (tid < 64) {
+        const unsigned long long e = lookback(a.tile_state, t, tile_total, a.err);
+        if (tid == 0) sh.out_excl = e;
+    }
     __syncthreads();
     if (tid < TE_CNT__N && sh.cnt[tid]) atomicAdd(&a.counters[tid], sh.cnt[tid]);
     const unsigned long long E = sh.out_excl;
@@ -360,7 +391,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     const uint64_t Ge = Gs + tile_total;
     const uint64_t C0 = Gs & ~15ull;
     const uint32_t nchunks = (uint32_t)((Ge - C0 + 15) >> 4);
-    const bool ident = MODE == MODE_CONTIG && sh.ident != 0;
+    const bool ident = MODE == MODE_CONTIG && (stat || sh.ident != 0);
     const uint32_t src0 = sh.rpos[0];  // ident: output byte q is slot byte src0 + q
     g_u8 *gout = (g_u8 *)a.out;
     for (uint32_t c = tid; c < nchunks; c += BLOCK) {
@@ -455,6 +486,23 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
 
 }  // namespace
 
+// persistent grid = the blocks that are resident at once (CUs x occupancy)
+static int resident_blocks(int slot_layout) {
+    static int cached[2] = {0, 0};
+    int &c = cached[slot_layout ? 1 : 0];
+    if (c) return c;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 256;
+    hipError_t e = slot_layout
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_edit_tiles<MODE_SLOT>, BLOCK, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_edit_tiles<MODE_CONTIG>, BLOCK, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    c = cus * per_cu;
+    return c;
+}
+
 // ---------------------------------------------------------------------------
 // C-ABI launch wrapper (called from the C host code, no torch types)
 // ---------------------------------------------------------------------------
@@ -480,11 +528,13 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.counters = (unsigned long long *)L->counters;
     a.err = (unsigned long long *)L->err;
     a.scratch = L->scratch;
+    a.rec0 = L->rec0;
+    a.static_off = (uint32_t)L->static_off;
     // one memset per launch: error words, ticket, counters, look-back granules
     hipError_t e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);
     if (e != hipSuccess) return -1;
     if (L->n_tiles == 0) return 0;
-    int grid = L->grid > 0 ? L->grid : 1;
+    int grid = L->grid > 0 ? L->grid : resident_blocks(L->slot_layout);
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
     if (L->slot_layout)
         hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
