@@ -143,6 +143,16 @@ int tcpedit_get_dev_cfg(tcpedit_t *tcpedit, void *out, size_t len, uint16_t *por
 /* select the HIP device used by subsequently initialised contexts */
 int tcpedit_set_device(int device);
 
+/* Multi-GPU sharding: cut a pcap image into `n`
+ * contiguous runs of whole records balanced by bytes, the way libpcap would
+ * walk it (a truncated/oversize record ends the walk; the tail stays in the
+ * last shard).  On return off[0..n] are record-boundary byte offsets
+ * (off[0] = 24, off[n] = end of the walk) and pkt_base[0..n-1] the global
+ * 0-based number of each shard's first record, which a shard passes to
+ * tcpedit_batch_open so tcpprep cache lookups stay global.  Host-only (no
+ * device calls).  Returns the total record count, or -1 on a bad image. */
+int64_t tcpedit_pcap_shards(const void *pcap, size_t len, int n, uint64_t *off, uint64_t *pkt_base);
+
 #ifdef __cplusplus
 }
 #endif

@@ -790,3 +790,46 @@ int tcpedit_close(tcpedit_t **tp)
     *tp = NULL;
     return 0;
 }
+
+int64_t tcpedit_pcap_shards(const void *pcap, size_t len, int n, uint64_t *off, uint64_t *pkt_base)
+{
+    const uint8_t *img = pcap;
+    if (!img || len < 24 || n < 1 || !off || !pkt_base)
+        return -1;
+    uint32_t magic;
+    memcpy(&magic, img, 4);
+    int swapped;
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du)
+        swapped = 0;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u)
+        swapped = 1;
+    else
+        return -1;
+    /* pass 1: where libpcap's walk ends */
+    size_t end = 24;
+    uint64_t total = 0;
+    while (end + 16 <= len) {
+        uint32_t caplen = rd32(img + end + 8, swapped);
+        if (caplen > 262144u || end + 16 + caplen > len)
+            break;
+        end += 16 + caplen;
+        total++;
+    }
+    /* pass 2: cut at the first record boundary at or past k/n of the bytes */
+    const uint64_t bytes = end - 24;
+    size_t o = 24;
+    uint64_t pk = 0;
+    off[0] = 24;
+    pkt_base[0] = 0;
+    for (int k = 1; k < n; k++) {
+        const uint64_t target = 24 + bytes * (uint64_t)k / (uint64_t)n;
+        while (o < target && o < end) {
+            o += 16 + rd32(img + o + 8, swapped);
+            pk++;
+        }
+        off[k] = o;
+        pkt_base[k] = pk;
+    }
+    off[n] = end;
+    return (int64_t)total;
+}

@@ -1,0 +1,161 @@
+"""Multi-GPU path (tcpreplay_amd.dist): shard planning, segment placement, the
+counter all-reduce and hard-error truncation, with world_size-2 gloo process
+groups on CPU.  Each rank's shard is edited by the oracle (test infrastructure)
+so the host-side shard/merge logic is checked without a GPU; the GPU variant
+runs two ranks on cuda:0 through the C-ABI."""
+import os
+import socket
+import struct
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import golden_cases as G
+import oracle_lib as O
+from tcpreplay_amd import dist as D
+from tcpreplay_amd import synth as S
+
+C4_ARGS = ["--endpoints=10.10.0.1:10.10.0.2", "--enet-dmac=00:12:13:14:15:16,00:22:33:44:55:66",
+           "--enet-smac=00:22:33:44:55:66,00:12:13:14:15:16", "--enet-vlan=add", "--enet-vlan-tag=45",
+           "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"]
+
+
+def slice_cache(cache: bytes, first: int, count: int) -> bytes:
+    """tcpprep v04 cache (cache.h:63-72) restricted to packets [first, first+count), repacked."""
+    clen = struct.unpack(">H", cache[22:24])[0]
+    data = np.frombuffer(cache[24 + clen:], np.uint8)
+    bits = np.stack([(data >> (2 * k)) & 3 for k in range(4)], axis=1).reshape(-1)
+    sub = bits[first:first + count]
+    sub = np.concatenate([sub, np.zeros((-len(sub)) % 4, np.uint8)]).reshape(-1, 4)
+    packed = (sub[:, 0] | (sub[:, 1] << 2) | (sub[:, 2] << 4) | (sub[:, 3] << 6)).astype(np.uint8)
+    return cache[:8] + cache[8:12] + struct.pack(">Q", count) + cache[20:24 + clen] + packed.tobytes()
+
+
+def oracle_editor_for(pcap, world):
+    p = D.plan(pcap, world)
+
+    def editor(image, args, cache, pkt_base):
+        k = p.pkt_base.index(pkt_base) if p.pkt_base.count(pkt_base) == 1 else \
+            next(i for i in range(world) if p.pkt_base[i] == pkt_base and p.image(pcap, i) == image)
+        sub = slice_cache(cache, pkt_base, p.count(k)) if cache else None
+        rc, out = O.rewrite(image, args, sub)
+        return D.ShardResult(rc, out, [p.count(k)] + [0] * (len(D.COUNTER_NAMES) - 1))
+    return editor
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, pcap, args, cache, out_path, use_gpu, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        editor = None if use_gpu else oracle_editor_for(pcap, world)
+        rc, counters, seg, off = D.rewrite_distributed(pcap, args, cache, out_path, editor=editor, device=0)
+        q.put((rank, rc, counters))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_world(pcap, args, cache=None, world=2, use_gpu=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out_path = os.path.join(d, "out.pcap")
+        procs = [ctx.Process(target=_worker, args=(r, world, port, pcap, args, cache, out_path, use_gpu, q))
+                 for r in range(world)]
+        for pr in procs:
+            pr.start()
+        for pr in procs:
+            pr.join(300)
+            assert pr.exitcode == 0
+        res = sorted(q.get() for _ in range(world))
+        return open(out_path, "rb").read(), res
+
+
+# ---------------------------------------------------------------- planner
+def test_plan_is_byte_balanced_and_covers_every_record(built):
+    pcap = S.pcap_imix(10_000, seed=3)
+    for n in (1, 2, 3, 8):
+        p = D.plan(pcap, n)
+        assert p.offsets[0] == 24 and p.offsets[-1] == len(pcap) and p.total == 10_000
+        assert sum(p.count(k) for k in range(n)) == 10_000
+        for k in range(1, n):  # each cut is the first record boundary at/after k/n of the bytes
+            target = 24 + (len(pcap) - 24) * k // n
+            assert target <= p.offsets[k] < target + 1514 + 16
+        recs = S.records(pcap)
+        for k in range(n):
+            assert len(S.records(p.image(pcap, k))) == p.count(k)
+            assert S.records(p.image(pcap, k))[:1] == recs[p.pkt_base[k]:p.pkt_base[k] + 1]
+
+
+def test_plan_stops_where_libpcap_stops(built):
+    pcap = S.pcap_fixed(100, 64, seed=1)
+    trunc = pcap[:-10]  # last record truncated: the walk ends before it
+    p = D.plan(trunc, 4)
+    assert p.total == 99 and p.offsets[-1] == 24 + 99 * 80
+
+
+def test_slice_cache_matches_global_lookup(built):
+    cache = S.tcpprep_cache(1000, seed=2, nosend_every=7)
+    sub = slice_cache(cache, 333, 400)
+    for i in (0, 1, 2, 3, 4, 399):
+        g = 333 + i
+
+        def bits(c, n):
+            clen = struct.unpack(">H", c[22:24])[0]
+            return (c[24 + clen + n // 4] >> (2 * (n % 4))) & 3
+        assert bits(sub, i) == bits(cache, g)
+
+
+# ---------------------------------------------------------------- gloo world_size 2 (oracle-edited shards)
+@pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix"])
+def test_two_rank_rewrite_equals_single_process(built, case):
+    if case == "fixcsum":
+        pcap, args, cache = G.read("test.pcap"), ["--fixcsum"], None
+    elif case == "c4_cache":
+        pcap, args, cache = G.read("test.pcap"), C4_ARGS[:1] + ["--enet-vlan=add", "--enet-vlan-tag=45",
+                                                                 "--fixcsum"], G.read("test.auto_router")
+    else:
+        pcap, args, cache = S.pcap_imix(5000, seed=4), ["--seed=42", "--fixcsum"], None
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    out, res = run_world(pcap, args, cache)
+    assert all(r[1] == 0 for r in res) and rc_o == 0
+    assert out == exp
+    assert res[0][2]["packets"] == res[1][2]["packets"] == D.plan(pcap, 2).total
+
+
+@pytest.mark.parametrize("bad_shard", [0, 1])
+def test_hard_error_truncates_at_first_failing_record(built, bad_shard):
+    recs = S.records(S.pcap_fixed(40, 64, seed=5))
+    k = 5 if bad_shard == 0 else 30
+    ts, tu, cl, ln, d = recs[k]
+    d = bytearray(d)
+    d[14] = 0x55  # IPv4 ethertype with IP version 5 -> TCPEDIT_ERROR (edit_packet.c:73-79)
+    recs[k] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    out, res = run_world(pcap, ["--fixcsum"])
+    assert rc_o == -1 and all(r[1] == -1 for r in res)
+    assert out == exp and len(S.records(out)) == k
+
+
+# ---------------------------------------------------------------- the device path, two ranks on one GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c4_cache", "c3_imix"])
+def test_two_rank_gpu_rewrite_equals_oracle(built, case):
+    if case == "c4_cache":
+        pcap, args, cache = G.read("test.pcap"), C4_ARGS, G.read("test.auto_router")
+    else:
+        pcap, cache = S.pcap_imix(20_000, seed=6), None
+        args = ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    out, res = run_world(pcap, args, cache, use_gpu=True)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
