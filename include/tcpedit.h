@@ -117,6 +117,8 @@ typedef struct {
     int64_t first_unsupported;/* 0-based record index of the first unsupported record, or -1 */
     uint32_t n_tiles;
     double kernel_ms;         /* device time of the last run (hipEvent) */
+    uint32_t fast_lane;       /* 1: the register-resident fast lane ran (size-preserving config) */
+    uint32_t generic_tiles;   /* tiles the generic lane edited (all of them without the fast lane) */
 } tcpedit_batch_result_t;
 
 tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *tcpedit, const void *pcap, size_t len, const void *cache,

@@ -46,12 +46,18 @@ struct tcpedit_batch_s {
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
     int slot_layout;
     int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
+    int fast_tiles;          /* tiles were cut for the fast lane (TE_FK_TILE_BYTES budget) */
+    uint64_t launches;       /* parity selects the fast lane's tile-list count */
+    int last_fast;           /* the last launch ran the fast lane ... */
+    uint32_t last_listed;    /* ... and left this many tiles to the generic kernel */
     /* device side */
     uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
     uint64_t dirbits_len;
     te_tile_t *d_tiles;
     uint16_t *d_pkt_rel;
-    uint8_t *d_ws;           /* err[0..1] | err[2], ticket | counters | tile_state[] */
+    uint8_t *d_ws;           /* err[0..2] | ticket, done | counters | tile_state[] | list count */
+    uint32_t *d_tile_list;   /* fast lane: tiles left to the generic kernel */
+    uint64_t *d_fk_part;     /* fast lane: per-block counters */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
     /* results */
@@ -66,6 +72,37 @@ struct tcpedit_batch_s {
 #define WS_TICKET 24
 #define WS_COUNTERS 32
 #define WS_STATE 128
+#define WS_LIST_CNT(n_tiles) (WS_STATE + 8 * ((n_tiles) + 1))
+
+/* no edit step can change a record's length or drop it: efcs, VLAN add/del,
+ * fixlen, MTU truncation and skipped soft errors are the only ways (plus
+ * zero-length records, checked per batch) */
+static int static_capable(const te_dev_cfg_t *c)
+{
+    return !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate &&
+           !c->skip_soft_errors;
+}
+
+/* options the register-resident fast lane carries (fast_lane.hpp); anything
+ * else keeps every packet on the generic lane */
+static int fast_capable(const te_dev_cfg_t *c)
+{
+    return static_capable(c) && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 && c->tclass < 0 &&
+           c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+}
+
+/* IPv6 rewrites with a non-octet target mask keep the reference's stray write
+ * (SURVEY Q9): those packets stay on the generic lane */
+static int fast_v6_ok(const te_dev_cfg_t *c)
+{
+    const te_cidrmap_t *lists[4] = {c->cidrmap1, c->cidrmap2, c->srcipmap, c->dstipmap};
+    const int n[4] = {c->n_cidrmap1, c->n_cidrmap2, c->n_srcipmap, c->n_dstipmap};
+    for (int l = 0; l < 4; l++)
+        for (int i = 0; i < n[l]; i++)
+            if (lists[l][i].to.family == 6 && lists[l][i].to.masklen % 8)
+                return 0;
+    return 1;
+}
 
 static uint32_t rd32(const uint8_t *p, int swapped)
 {
@@ -97,6 +134,8 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
     const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
     const int slot_mode = pad || t->cfg.vlan == TE_VLAN_ADD;
     b->slot_layout = slot_mode;
+    b->fast_tiles = !slot_mode && fast_capable(&t->cfg);
+    const uint32_t budget = b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
     b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
@@ -129,8 +168,8 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
             huge = slot > TE_SLOT_BYTES;
             fits = open && cur_slots + slot <= TE_SLOT_BYTES;
         } else {
-            huge = !TE_CONTIG_FITS(g, 16 + caplen);
-            fits = open && TE_CONTIG_FITS(cur.span_off & 15, off + 16 + caplen - cur.span_off);
+            huge = !TE_CONTIG_FITS_IN(g, 16 + caplen, budget);
+            fits = open && TE_CONTIG_FITS_IN(cur.span_off & 15, off + 16 + caplen - cur.span_off, budget);
         }
         if (open && (huge || cur.npkt >= TE_MAX_PKTS || !fits)) {
             if (b->n_tiles == cap_tiles)
@@ -186,6 +225,10 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_tiles);
     hipFree(b->d_pkt_rel);
     hipFree(b->d_ws);
+    hipFree(b->d_tile_list);
+    hipFree(b->d_fk_part);
+    b->d_tile_list = NULL;
+    b->d_fk_part = NULL;
     b->d_in = b->d_out = b->d_status = b->d_scratch = b->d_dirbits = b->d_ws = NULL;
     b->d_tiles = NULL;
     b->d_pkt_rel = NULL;
@@ -307,8 +350,14 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->n_pkts + 1)));
     HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
                              t->stream));
-    b->ws_bytes = WS_STATE + 8 * (b->n_tiles + 1);
+    b->ws_bytes = WS_LIST_CNT(b->n_tiles) + 64;
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
+    HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream)); /* the list count starts at 0 */
+    if (b->fast_tiles) {
+        const int fg = te_fast_grid();
+        HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->n_tiles + 1)));
+        HIPCHK(t, hipMalloc((void **)&b->d_fk_part, sizeof(uint64_t) * TE_CNT__N * (size_t)(fg > 0 ? fg : 1)));
+    }
     if (cache) {
         const uint8_t *cd;
         if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &b->dirbits_len) < 0)
@@ -326,6 +375,13 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
 fail:
     tcpedit_batch_close(b);
     return NULL;
+}
+
+/* TCPEDIT_HIP_NO_FAST=1 keeps every packet on the generic lane (A/B checks) */
+static int fast_lane_off(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_NO_FAST");
+    return e && *e && *e != '0';
 }
 
 static int launch(tcpedit_batch_t *b, int fixed_dir)
@@ -361,9 +417,16 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
        it (efcs, VLAN add/del, fixlen, MTU truncation, skipped soft errors, and
        zero-length records are the only ways), so outputs sit at input offsets */
     const te_dev_cfg_t *c = &t->cfg;
-    L.static_off = !b->slot_layout && !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF &&
-                   !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap;
+    L.static_off = !b->slot_layout && static_capable(c) && !b->has_zero_cap;
     L.rec0 = 24;
+    L.fast = L.static_off && b->fast_tiles && fast_capable(c) && !fast_lane_off();
+    L.fast_v6 = fast_v6_ok(c);
+    L.tile_list = b->d_tile_list;
+    L.list_cnt = (uint32_t *)(b->d_ws + WS_LIST_CNT(b->n_tiles));
+    L.fk_part = b->d_fk_part;
+    L.parity = (uint32_t)(b->launches++ & 1);
+    b->last_fast = L.fast;
+    L.ws_zero = (uint64_t *)(b->d_ws + WS_ZERO);
     return te_launch_edit(&L, t->stream);
 }
 
@@ -385,6 +448,9 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
     HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + WS_COUNTERS, sizeof(b->counters), hipMemcpyDeviceToHost,
                              t->stream));
     HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
+    if (b->last_fast)
+        HIPCHK(t, hipMemcpyAsync(&b->last_listed, b->d_ws + WS_LIST_CNT(b->n_tiles) + 4 * ((b->launches - 1) & 1),
+                                 sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
     b->err[0] = ~b->err[0]; /* stored complemented (0 = no error -> ~0) */
     b->err[1] = ~b->err[1];
@@ -479,6 +545,8 @@ int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r)
     r->out_len = end;
     r->n_tiles = (uint32_t)b->n_tiles;
     r->kernel_ms = b->kernel_ms;
+    r->fast_lane = (uint32_t)b->last_fast;
+    r->generic_tiles = b->last_fast ? b->last_listed : (uint32_t)b->n_tiles;
     return TCPEDIT_OK;
 }
 

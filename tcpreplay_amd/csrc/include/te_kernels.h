@@ -18,6 +18,7 @@ extern "C" {
 #define TE_HEAD 16             /* headroom before each record (VLAN push) */
 #define TE_TAIL_BYTES 16       /* zeroed bytes after each packet's data */
 #define TE_NO_SCRATCH 0xffffffffffffffffull
+#define TE_FK_TILE_BYTES 16384 /* tile budget when the fast lane runs (more blocks per CU) */
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
@@ -25,7 +26,8 @@ extern "C" {
 
 /* contiguous layout: a tile's span (starting g bytes into its 16-byte chunk)
  * fits the LDS image when this holds */
-#define TE_CONTIG_FITS(g, span) ((uint32_t)(g) + (uint32_t)(span) + 16u <= (uint32_t)TE_SLOT_BYTES)
+#define TE_CONTIG_FITS_IN(g, span, budget) ((uint32_t)(g) + (uint32_t)(span) + 16u <= (uint32_t)(budget))
+#define TE_CONTIG_FITS(g, span) TE_CONTIG_FITS_IN(g, span, TE_SLOT_BYTES)
 
 #define TE_SLOT_BYTES_OF(g, data) \
     ((((uint32_t)TE_HEAD + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
@@ -67,7 +69,20 @@ typedef struct {
     int static_off;           /* 1: no record can change size or be dropped, so every output
                                  record sits at its input offset: no scan, no look-back */
     uint64_t rec0;            /* input offset of the first record (static_off: out = in - rec0 + out_base) */
+    /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
+       every tile it can, appends the rest to tile_list, and the generic kernel then redoes
+       only the listed tiles */
+    int fast;
+    int fast_v6;              /* IPv6 packets may take the fast lane (no non-octet v6 CIDR maps) */
+    uint32_t *tile_list;      /* device: n_tiles entries */
+    uint32_t *list_cnt;       /* device: 2 counts; launch parity p appends to [p] and zeroes [p^1] */
+    uint32_t parity;
+    uint64_t *fk_part;        /* device: te_fast_grid() x TE_CNT__N per-block counters */
+    uint64_t *ws_zero;        /* device: 16 words (err, ticket, counters) the fast kernel zeroes */
 } te_launch_t;
+
+/* blocks of te_fast_tiles resident on the current device (the fk_part rows needed) */
+int te_fast_grid(void);
 
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(const te_launch_t *L, hipStream_t stream);

@@ -285,20 +285,15 @@ DI u16 csum16_add(u16 c, u16 a) {
     u16 r = (u16)(c + a);
     return (u16)(r + (r < a));
 }
-DI void csum_replace2(u8 *sp, u16 from, u16 to) {
-    u16 s = ld16(sp);
-    st16(sp, (u16)~csum16_add(csum16_add((u16)~s, (u16)~from), to));
-}
-DI void csum_replace4(u8 *sp, u32 from, u32 to) {
-    u16 s = ld16(sp);
-    st16(sp, csum_fold32(csum_add(csum_add(~(u32)s, ~from), to)));
-}
-DI void csum_replace16(u8 *sp, const u8 *from, const u8 *to) {
+// value forms (shared with the register-resident fast lane)
+DI u16 csum_replace2_v(u16 s, u16 from, u16 to) { return (u16)~csum16_add(csum16_add((u16)~s, (u16)~from), to); }
+DI u16 csum_replace4_v(u16 s, u32 from, u32 to) { return csum_fold32(csum_add(csum_add(~(u32)s, ~from), to)); }
+DI u16 csum_replace16_v(u16 s, const u32 *from, const u32 *to) {
     // csum_partial over {~from[0..3], to[0..3]} (do_csum on an aligned 32-byte array)
     u32 result = 0, carry = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        u32 w = i < 4 ? ~ld32(from + 4 * i) : ld32(to + 4 * (i - 4));
+        u32 w = i < 4 ? ~from[i] : to[i - 4];
         result += carry;
         result += w;
         carry = (w > result);
@@ -307,10 +302,21 @@ DI void csum_replace16(u8 *sp, const u8 *from, const u8 *to) {
     result = (result & 0xffff) + (result >> 16);
     result = (result & 0xffff) + (result >> 16);
     result = (result & 0xffff) + (result >> 16);
-    u32 wsum = ~(u32)ld16(sp);
+    u32 wsum = ~(u32)s;
     result += wsum;
     if (wsum > result) result += 1;
-    st16(sp, csum_fold32(result));
+    return csum_fold32(result);
+}
+DI void csum_replace2(u8 *sp, u16 from, u16 to) { st16(sp, csum_replace2_v(ld16(sp), from, to)); }
+DI void csum_replace4(u8 *sp, u32 from, u32 to) { st16(sp, csum_replace4_v(ld16(sp), from, to)); }
+DI void csum_replace16(u8 *sp, const u8 *from, const u8 *to) {
+    u32 f[4], t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[i] = ld32(from + 4 * i);
+        t[i] = ld32(to + 4 * i);
+    }
+    st16(sp, csum_replace16_v(ld16(sp), f, t));
 }
 
 // ---------------------------------------------------------------------------

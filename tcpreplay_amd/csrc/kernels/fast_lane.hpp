@@ -1,0 +1,404 @@
+// fast_lane.hpp -- register-resident tcpedit_packet for the dominant header shapes.
+//
+// One lane edits one packet whose headers are plain Ethernet II + IPv4 (IHL 5,
+// not a fragment, ip_len == caplen - 14) or IPv6 (TCP/UDP directly after the
+// fixed header, payload length == caplen - 54), TCP or UDP, caplen == len.
+// With a 14-byte Ethernet header every IP/L4 field sits at a packet offset
+// that is 2 mod 4, so the lane loads an 80-byte window aligned to packet offset
+// -2 into 20 VGPRs:  H[i] = little-endian dword of packet bytes [4i-2, 4i+2).
+// Every address, port and checksum word is then a whole dword or half-dword
+// at a compile-time index, and every one's-complement word of the headers is a
+// 16-bit half of some H[i] (relative offsets 4i-2 and 4i are even).
+//
+// The edits are the reference's, step for step, in tcpedit_packet's order
+// (tcpedit.c:46-366): en10mb MAC rewrite (en10mb.c:479-736), port map
+// (portmap.c:239-372), srcip/dstip/pnat/endpoint maps (edit_packet.c:787-1019),
+// seed randomisation (:336-518), full checksums (:55-189, checksum.c:34-170),
+// multicast destination MAC (en10mb.c:847-887).  They reuse edit_pkt.hpp's value
+// helpers (randomize_ipv4_addr, remap_ipv4, ip_in_cidr, csum_replace*_v), so the
+// two lanes share their arithmetic.  Only the UDP checksum field is carried
+// through the incremental updates: with --fixcsum every other checksum is
+// recomputed from scratch, but a UDP field the updates leave at 0 is NOT
+// recomputed (checksum.c:115), so its incremental value decides.
+//
+// Whatever is not one of these shapes, or needs an option the fast lane does
+// not carry (the host clears te_fast_cfg_t.ok), is deferred to the generic lane.
+#pragma once
+#include "edit_pkt.hpp"
+
+namespace te {
+namespace fl {
+
+constexpr int NW = 20;            // window dwords
+constexpr int WEND = 4 * NW - 2;  // 78: first packet byte past the window
+
+DI u32 lo16(u32 x) { return x & 0xffffu; }
+DI u32 hi16(u32 x) { return x >> 16; }
+DI u32 with_lo16(u32 x, u32 v) { return (x & 0xffff0000u) | (v & 0xffffu); }
+DI u32 with_hi16(u32 x, u32 v) { return (x & 0xffffu) | (v << 16); }
+DI u32 wsum(u32 x) { return (x & 0xffffu) + (x >> 16); }  // its two LE 16-bit words
+DI u32 swap16(u32 x) {
+    x &= 0xffffu;  // (u16) truncation first, as bswap16((u16)...)
+    return ((x >> 8) | (x << 8)) & 0xffffu;
+}
+DI u32 bs16(u32 x) { return swap16(x); }
+
+// mask of bytes [lo, hi) of a dword (lo, hi clamped to [0, 4])
+DI u32 bmask(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    const u32 mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+    const u32 ml = lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+    return mh & ~ml;
+}
+
+DI u32 sel4(const u32 *a, u32 k) { return k == 0 ? a[0] : (k == 1 ? a[1] : (k == 2 ? a[2] : a[3])); }
+
+// ip6_in_cidr (cidr.c:478-529) on an address held as 4 LE dwords
+DI bool ip6_in_cidr_w(const te_cidr_t &c, const u32 *a) {
+    if (c.family != 6) return false;
+    if (c.masklen == 0 && (a[0] | a[1] | a[2] | a[3]) == 0) return true;
+    const int j = c.masklen / 8;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ok &= ((a[k] ^ ld32(c.network6 + 4 * k)) & bmask(0, j - 4 * k)) == 0;
+    if (!ok) return false;
+    const int r = c.masklen % 8;
+    if (r == 0) return true;
+    const u32 km = (0xffu << (8 - r)) & 0xffu;
+    const u32 ab = (sel4(a, (u32)j >> 2) >> (8 * (j & 3))) & 0xffu;
+    return (ab & km) == (c.network6[j] & km);
+}
+
+// remap_ipv6 (edit_packet.c:748-779) for octet masks (the host keeps the
+// non-octet out-of-range write of SURVEY Q9 on the generic lane)
+DI void remap_ipv6_w(const te_dev_cfg_t &cfg, const te_cidr_t &c, u32 *a) {
+    if (c.family != 6) return;
+    if (cfg.skip_broadcast && (a[0] & 0xffu) == 0xffu) return;
+    const int j = c.masklen / 8;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u32 m = bmask(0, j - 4 * k);
+        a[k] = (a[k] & ~m) | (ld32(c.network6 + 4 * k) & m);
+    }
+}
+
+// randomize_ipv6_addr (edit_packet.c:359-379)
+DI void randomize_ipv6_w(const te_dev_cfg_t &cfg, u32 *a) {
+    const bool was = (a[0] & 0xffu) == 0xffu;
+    const u32 s = bswap32(cfg.seed);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = (a[i] ^ s) - (a[i] & s);
+    const bool now = (a[0] & 0xffu) == 0xffu;
+    if (was && !now) a[0] = (a[0] & ~0xffu) | 0xffu;
+    else if (!was && now) a[0] = (a[0] & ~0xffu) | 0xaau;
+}
+
+// is_unicast_ethernet (plugins/ethernet.c:30-57) on a MAC in the low 48 bits
+DI bool unicast48(unsigned long long m) {
+    if ((m & 0xffffffffffffull) == 0xffffffffffffull) return false;
+    if ((m & 0xffffffull) == 0x5e0001ull) return false;  // 01:00:5e
+    if ((m & 0xffffull) == 0x3333ull) return false;      // 33:33
+    if ((m & 0xffffffffull) == 0x00500000ull && (((m >> 32) & 0xff) == 1 || ((m >> 32) & 0xff) == 2))
+        return false;  // 00:00:50:00:01/02 (defines.h.in:226-227)
+    return true;
+}
+DI unsigned long long mac48(const u8 *m) {
+    return (unsigned long long)ld32(m) | ((unsigned long long)ld16(m + 4) << 32);
+}
+
+// what phase B needs to finish a packet after the block's chunk-prefix pass
+struct State {
+    u32 l4sum;  // unfolded one's-complement sum so far (pseudo header + L4 bytes inside the window)
+    u32 end;    // caplen: L4 bytes run to here
+    bool v6, tcp, do_l4, tail;
+};
+
+// ---------------------------------------------------------------------------
+// Phase A: classify, edit, IPv4 header checksum, in-window L4 sum.
+// Returns false to defer the packet to the generic lane (H untouched then).
+// ---------------------------------------------------------------------------
+DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &cfg, bool v6_ok,
+                const TE_AS_GLOBAL uint16_t *lut, State &st) {
+    if (caplen != len || (dir != TE_DIR_C2S && dir != TE_DIR_S2C)) return false;
+    const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
+    bool v6;
+    u32 proto, l4len;
+    if (et == 0x0008u) {  // ETHERTYPE_IP
+        if ((H[4] & 0xffu) != 0x45u) return false;
+        const u32 ip_len = bs16(hi16(H[4]));
+        if (ip_len != caplen - 14) return false;                 // Q4 warning path: generic
+        if ((bs16(hi16(H[5])) & 0x3fffu) != 0) return false;      // fragments: generic
+        proto = (H[6] >> 8) & 0xffu;
+        l4len = ip_len - 20;
+        v6 = false;
+    } else if (et == 0xDD86u) {  // ETHERTYPE_IP6
+        if (!v6_ok || ((H[4] >> 4) & 0xfu) != 6u) return false;
+        proto = (H[5] >> 16) & 0xffu;
+        const u32 plen_raw = lo16(H[5]);
+        l4len = bs16(plen_raw);
+        if (caplen < 54 || l4len != caplen - 54) return false;
+        if (caplen > 56 && plen_raw < 40) return false;  // raw network-order compare (edit_packet.c:167)
+        v6 = true;
+    } else {
+        return false;
+    }
+    bool tcp;
+    if (proto == 6) {
+        if (l4len < 20) return false;
+        tcp = true;
+    } else if (proto == 17) {
+        if (l4len < 8) return false;
+        tcp = false;
+    } else {
+        return false;
+    }
+
+    // ---- en10mb_encode: MAC rewrite (no VLAN, subsmac or mac-seed here) ----
+    if (cfg.mac_mask) {
+        const bool c2s = dir == TE_DIR_C2S;
+        const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
+        unsigned long long dmac = (unsigned long long)hi16(H[0]) | ((unsigned long long)H[1] << 16);
+        unsigned long long smac = (unsigned long long)H[2] | ((unsigned long long)lo16(H[3]) << 32);
+        const bool use_s = (cfg.mac_mask & sm) && (!cfg.l2_skip_broadcast || unicast48(smac));
+        const bool use_d = (cfg.mac_mask & dm) && (!cfg.l2_skip_broadcast || unicast48(dmac));
+        if (use_s) smac = mac48(c2s ? cfg.intf1_smac : cfg.intf2_smac);
+        if (use_d) dmac = mac48(c2s ? cfg.intf1_dmac : cfg.intf2_dmac);
+        H[0] = with_hi16(H[0], (u32)dmac);
+        H[1] = (u32)(dmac >> 16);
+        H[2] = (u32)smac;
+        H[3] = with_lo16(H[3], (u32)(smac >> 32));
+    }
+
+    // L4 header (20 bytes) at packet offset 34 (v4) or 54 (v6)
+    // bitwise selects, not `v6 ? H[14+i] : H[9+i]`: the compiler folds the
+    // latter into one dynamically indexed access, which moves H to scratch
+    const u32 m6 = v6 ? 0xffffffffu : 0u;
+    u32 L[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) L[i] = (H[14 + i] & m6) | (H[9 + i] & ~m6);
+    u32 ucs = hi16(L[1]);  // UDP checksum field (L4 + 6), raw LE
+    const bool udp_live = !tcp;
+
+    // ---- port map (rewrite_ports, portmap.c:267-330): destination, then source ----
+    if (cfg.has_portmap) {
+        u32 oldp = hi16(L[0]), np = lut[oldp];
+        if (np != oldp) {
+            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)oldp, (u16)np);
+            L[0] = with_hi16(L[0], np);
+        }
+        oldp = lo16(L[0]);
+        np = lut[oldp];
+        if (np != oldp) {
+            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)oldp, (u16)np);
+            L[0] = with_lo16(L[0], np);
+        }
+    }
+
+    if (!v6) {
+        u32 src = H[7], dst = H[8];
+        // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is carried
+#define FL_V4_UPD(o, n) \
+    if (udp_live && ucs) ucs = csum_replace4_v((u16)ucs, (o), (n))
+        if (cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
+            for (int m = 0; m < cfg.n_srcipmap; ++m)
+                if (ip_in_cidr(cfg.srcipmap[m].from, src)) {
+                    const u32 o = src;
+                    src = remap_ipv4(cfg, cfg.srcipmap[m].to, o);
+                    FL_V4_UPD(o, src);
+                    break;
+                }
+            for (int m = 0; m < cfg.n_dstipmap; ++m)
+                if (ip_in_cidr(cfg.dstipmap[m].from, dst)) {
+                    const u32 o = dst;
+                    dst = remap_ipv4(cfg, cfg.dstipmap[m].to, o);
+                    FL_V4_UPD(o, dst);
+                    break;
+                }
+            if (cfg.n_cidrmap1 != 0) {
+                const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
+                const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+                const int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+                const int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+                int i1 = 0, i2 = 0;
+                bool didsrc = false, diddst = false;
+                for (;;) {
+                    if (!diddst && ip_in_cidr(l2[i2].from, dst)) {
+                        const u32 o = dst;
+                        dst = remap_ipv4(cfg, l2[i2].to, o);
+                        FL_V4_UPD(o, dst);
+                        diddst = true;
+                    }
+                    if (!didsrc && ip_in_cidr(l1[i1].from, src)) {
+                        const u32 o = src;
+                        src = remap_ipv4(cfg, l1[i1].to, o);
+                        FL_V4_UPD(o, src);
+                        didsrc = true;
+                    }
+                    if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
+                        if (i1 + 1 < n1) ++i1;
+                        if (i2 + 1 < n2) ++i2;
+                    } else {
+                        break;
+                    }
+                }
+            }
+        }
+        if (cfg.seed) {  // randomize_ipv4 (edit_packet.c:420-467): destination, then source
+            if (!(cfg.skip_broadcast && mcast4(dst))) {
+                const u32 o = dst;
+                dst = randomize_ipv4_addr(cfg, o);
+                FL_V4_UPD(o, dst);
+            }
+            if (!(cfg.skip_broadcast && mcast4(src))) {
+                const u32 o = src;
+                src = randomize_ipv4_addr(cfg, o);
+                FL_V4_UPD(o, src);
+            }
+        }
+#undef FL_V4_UPD
+        H[7] = src;
+        H[8] = dst;
+    } else {
+        u32 src[4] = {H[6], H[7], H[8], H[9]}, dst[4] = {H[10], H[11], H[12], H[13]};
+        // ipv6_addr_csum_replace (edit_packet.c:298-330): only the UDP field is carried
+#define FL_V6_UPD(o, n) \
+    if (udp_live && ucs) ucs = csum_replace16_v((u16)ucs, (o), (n))
+        if (cfg.rewrite_ip) {  // rewrite_ipv6l3 (edit_packet.c:884-1019); TCP/UDP: no ICMPv6 recursion
+            for (int m = 0; m < cfg.n_srcipmap; ++m)
+                if (ip6_in_cidr_w(cfg.srcipmap[m].from, src)) {
+                    const u32 o[4] = {src[0], src[1], src[2], src[3]};
+                    remap_ipv6_w(cfg, cfg.srcipmap[m].to, src);
+                    FL_V6_UPD(o, src);
+                    break;
+                }
+            for (int m = 0; m < cfg.n_dstipmap; ++m)
+                if (ip6_in_cidr_w(cfg.dstipmap[m].from, dst)) {
+                    const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
+                    remap_ipv6_w(cfg, cfg.dstipmap[m].to, dst);
+                    FL_V6_UPD(o, dst);
+                    break;
+                }
+            if (cfg.n_cidrmap1 != 0) {
+                const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
+                const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+                const int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+                const int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+                int i1 = 0, i2 = 0;
+                bool didsrc = false, diddst = false;
+                for (;;) {
+                    if (!diddst && ip6_in_cidr_w(l2[i2].from, dst)) {
+                        const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
+                        remap_ipv6_w(cfg, l2[i2].to, dst);
+                        FL_V6_UPD(o, dst);
+                        diddst = true;
+                    }
+                    if (!didsrc && ip6_in_cidr_w(l1[i1].from, src)) {
+                        const u32 o[4] = {src[0], src[1], src[2], src[3]};
+                        remap_ipv6_w(cfg, l1[i1].to, src);
+                        FL_V6_UPD(o, src);
+                        didsrc = true;
+                    }
+                    if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
+                        if (i1 + 1 < n1) ++i1;
+                        if (i2 + 1 < n2) ++i2;
+                    } else {
+                        break;
+                    }
+                }
+            }
+        }
+        if (cfg.seed) {  // randomize_ipv6 (edit_packet.c:469-518): destination, then source
+            if (!(cfg.skip_broadcast && (dst[0] & 0xffu) == 0xffu)) {
+                const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
+                randomize_ipv6_w(cfg, dst);
+                FL_V6_UPD(o, dst);
+            }
+            if (!(cfg.skip_broadcast && (src[0] & 0xffu) == 0xffu)) {
+                const u32 o[4] = {src[0], src[1], src[2], src[3]};
+                randomize_ipv6_w(cfg, src);
+                FL_V6_UPD(o, src);
+            }
+        }
+#undef FL_V6_UPD
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            H[6 + i] = src[i];
+            H[10 + i] = dst[i];
+        }
+    }
+
+    // ---- fix_ipv4/ipv6_checksums (edit_packet.c:55-189) -> do_checksum (checksum.c:34-170) ----
+    // caplen == len, not a fragment, lengths consistent: the L4 sum always runs,
+    // except on a UDP field that is (still) 0 (checksum.c:115).
+    const bool do_l4 = tcp || ucs != 0;
+    if (do_l4) {
+        if (tcp) L[4] = with_lo16(L[4], 0);  // th_sum (L4 + 16)
+        else ucs = 0;                         // uh_sum (L4 + 6)
+    }
+    L[1] = with_hi16(L[1], ucs);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        H[14 + i] = (L[i] & m6) | (H[14 + i] & ~m6);
+        H[9 + i] = (L[i] & ~m6) | (H[9 + i] & m6);
+    }
+    u32 sum = 0;
+    if (do_l4) {
+        // pseudo header: csum_bytes(ip+12, 8) / csum_bytes(ip6+8, 32) + htons(proto + len)
+        if (!v6) {
+            sum = wsum(H[7]) + wsum(H[8]);
+        } else {
+#pragma unroll
+            for (int i = 6; i < 14; ++i) sum += wsum(H[i]);
+        }
+        sum += bs16((tcp ? 6u : 17u) + l4len);
+        // L4 bytes [L4S, min(caplen, WEND)) inside the window
+        const int base = v6 ? 14 : 9;
+#pragma unroll
+        for (int i = 9; i < NW; ++i) {
+            const u32 m = i >= base ? bmask(0, (int)caplen - (4 * i - 2)) : 0u;
+            sum += wsum(H[i] & m);
+        }
+    }
+    if (!v6) {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
+        H[6] = with_hi16(H[6], 0);
+        u32 hs = wsum(H[4]) + wsum(H[5]) + wsum(H[6]) + wsum(H[7]) + wsum(H[8]);
+        H[6] = with_hi16(H[6], (~fold16(hs)) & 0xffffu);
+    }
+
+    // ---- dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC ----
+    if (!v6) {
+        const u32 d = H[8];
+        if (mcast4(d)) {
+            H[0] = with_hi16(H[0], 0x0001u);                                         // 01:00
+            H[1] = 0x5eu | (((d >> 8) & 0x7fu) << 8) | (((d >> 16) & 0xffu) << 16) | ((d >> 24) << 24);
+        }
+    } else if ((H[10] & 0xffu) == 0xffu) {
+        H[0] = with_hi16(H[0], 0x3333u);
+        H[1] = H[13];
+    }
+
+    st.l4sum = sum;
+    st.end = caplen;
+    st.v6 = v6;
+    st.tcp = tcp;
+    st.do_l4 = do_l4;
+    st.tail = do_l4 && caplen > (u32)WEND;
+    return true;
+}
+
+// Phase B: add the L4 bytes past the window (one's-complement sum `tail`,
+// already in the packet's relative byte pairing) and store the checksum.
+DI void phase_b(u32 (&H)[NW], const State &st, u32 tail) {
+    if (!st.do_l4) return;
+    const u32 c = (~fold16((unsigned long long)st.l4sum + tail)) & 0xffffu;  // CHECKSUM_CARRY
+    // explicit per-index selects (a ternary on the index would move H to scratch)
+    const bool t6 = st.tcp && st.v6, t4 = st.tcp && !st.v6, u6 = !st.tcp && st.v6, u4 = !st.tcp && !st.v6;
+    H[18] = t6 ? with_lo16(H[18], c) : H[18];  // 54 + 16
+    H[13] = t4 ? with_lo16(H[13], c) : H[13];  // 34 + 16
+    H[15] = u6 ? with_hi16(H[15], c) : H[15];  // 54 + 6
+    H[10] = u4 ? with_hi16(H[10], c) : H[10];  // 34 + 6
+}
+
+}  // namespace fl
+}  // namespace te

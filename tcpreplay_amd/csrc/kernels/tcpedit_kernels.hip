@@ -44,6 +44,9 @@ typedef TE_AS_GLOBAL uint8_t g_u8;
 typedef TE_AS_GLOBAL const uint8_t g_cu8;
 typedef TE_AS_GLOBAL const uint4 g_cu4;
 typedef TE_AS_GLOBAL uint4 g_u4;
+}  // namespace
+#include "fast_lane.hpp"
+namespace {
 
 struct LaunchArgs {
     const te_dev_cfg_t *cfg;
@@ -67,6 +70,12 @@ struct LaunchArgs {
     uint8_t *scratch;                // HBM slots for huge tiles
     uint64_t rec0;                   // static_off: input offset of the first record
     uint32_t static_off;             // output offsets == input offsets (size-preserving config)
+    // after te_fast_tiles: only the listed tiles are edited here, and the last
+    // block folds the fast kernel's per-block counters into `counters`
+    const uint32_t *tile_list;
+    const uint32_t *list_cnt;        // this launch's count
+    const unsigned long long *fk_part;
+    uint32_t fk_grid;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -232,12 +241,28 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     {
         const uint64_t Aend = G0 + tile.span_len;
         const uint32_t nchunks = (uint32_t)((Aend - A0 + 15) >> 4);
-        for (uint32_t c = tid; c < nchunks; c += BLOCK) {
+        if constexpr (MODE == MODE_CONTIG) {
+            // every chunk a lane owns is in flight before the first LDS store: one HBM
+            // round trip per tile instead of one per chunk
+            constexpr int K = 5;  // 16-byte chunks per lane per batch
+            for (uint32_t c0 = tid; c0 < nchunks; c0 += K * BLOCK) {
+                uint4 v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {  // unconditional (clamped) loads keep v[] in VGPRs
+                    const uint32_t c = min(c0 + k * BLOCK, nchunks - 1);
+                    v[k] = *(g_cu4 *)(gin + A0 + ((uint64_t)c << 4));
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const uint32_t c = c0 + k * BLOCK;
+                    if (c < nchunks) *(uint4 *)(S + LDS_FRONT + (c << 4)) = v[k];
+                }
+            }
+        }
+        for (uint32_t c = tid; MODE != MODE_CONTIG && c < nchunks; c += BLOCK) {
             const uint64_t A = A0 + ((uint64_t)c << 4);
             const uint4 v = *(g_cu4 *)(gin + A);
-            if constexpr (MODE == MODE_CONTIG) {
-                *(uint4 *)(S + LDS_FRONT + (c << 4)) = v;
-            } else {
+            {
                 int64_t rA = (int64_t)A - (int64_t)G0;
                 int lo = 0, hi = (int)npkt - 1;
                 while (lo < hi) {
@@ -469,12 +494,38 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         for (int i = threadIdx.x; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
         (void)NV;
     }
+    const bool listed = a.tile_list != nullptr;
+    const uint32_t n_work = listed ? *(const volatile uint32_t *)a.list_cnt : a.n_tiles;
+    if (a.fk_part && blockIdx.x == 0) {  // fold the fast kernel's per-block counters (all 256 lanes)
+        unsigned long long v[TE_CNT__N];
+#pragma unroll
+        for (int k = 0; k < TE_CNT__N; ++k) v[k] = 0;
+#pragma unroll 4
+        for (uint32_t b = threadIdx.x; b < a.fk_grid; b += BLOCK) {
+            const unsigned long long *row = a.fk_part + (size_t)b * TE_CNT__N;
+#pragma unroll
+            for (int k = 0; k < TE_CNT__N; ++k) v[k] += row[k];
+        }
+        if (threadIdx.x < TE_CNT__N) sh.cnt[threadIdx.x] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < TE_CNT__N; ++k) {
+            unsigned long long x = v[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&sh.cnt[k], x);
+        }
+        __syncthreads();
+        if (threadIdx.x < TE_CNT__N && sh.cnt[threadIdx.x]) atomicAdd(&a.counters[threadIdx.x], sh.cnt[threadIdx.x]);
+    }
+    if (n_work == 0) return;
     for (;;) {
         if (threadIdx.x == 0) sh.tile_id = atomicAdd(a.ticket, 1u);
         __syncthreads();
-        const uint32_t t = sh.tile_id;
+        uint32_t t = sh.tile_id;
         __syncthreads();
-        if (t >= a.n_tiles) return;
+        if (t >= n_work) break;
+        if (listed) t = a.tile_list[t];
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
             tile_body<MODE>(a, tile, t, slots, sh, cfg);
@@ -484,21 +535,293 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
     }
 }
 
+// ===========================================================================
+// te_fast_tiles: the register-resident fast lane (fast_lane.hpp) over tiles of
+// a size-preserving run (static offsets).  Lean on purpose -- few VGPRs and a
+// small LDS image, so many blocks per CU hide HBM latency.  A tile holding any
+// packet the fast lane does not carry (or a huge record) is not written here:
+// its id goes to tile_list and the generic kernel, launched next, redoes the
+// whole tile (its results for the fast-lane packets are the same bytes).
+// ===========================================================================
+#ifndef TE_FK_MIN_BLOCKS
+#define TE_FK_MIN_BLOCKS 4
+#endif
+constexpr int FK_LDS = TE_FK_TILE_BYTES + LDS_FRONT + 128;  // + window overrun past the span
+constexpr int FK_NCH = (TE_FK_TILE_BYTES + LDS_FRONT + 15) / 16 + 2;
+constexpr int FK_Q = (FK_NCH + BLOCK - 1) / BLOCK;
+
+struct FastArgs {
+    const te_dev_cfg_t *cfg;
+    const uint16_t *portlut;
+    const uint8_t *dirbits;
+    uint64_t dirbits_len;
+    uint64_t pkt_base;
+    const uint8_t *in;
+    const te_tile_t *tiles;
+    const uint16_t *pkt_rel;
+    uint8_t *out;
+    uint8_t *status;
+    uint32_t *tile_list;
+    uint32_t *list_cnt;  // this launch's count; list_cnt_next is zeroed for the next launch
+    uint32_t *list_cnt_next;
+    unsigned long long *fk_part;
+    unsigned long long *ws_zero;
+    uint64_t out_base, rec0;
+    uint32_t n_tiles;
+    int32_t fixed_dir;
+    uint32_t in_swapped, in_nsec, v6_ok;
+};
+
+// one's-complement sum of the LE 16-bit words (absolute pairing) of bytes [b0, b1) of chunk c
+__device__ __forceinline__ uint32_t chunk_part(const uint8_t *S, uint32_t c, int b0, int b1) {
+    const uint4 v = *(const uint4 *)(S + 16 * c);
+    return fl::wsum(v.x & fl::bmask(b0, b1)) + fl::wsum(v.y & fl::bmask(b0 - 4, b1 - 4)) +
+           fl::wsum(v.z & fl::bmask(b0 - 8, b1 - 8)) + fl::wsum(v.w & fl::bmask(b0 - 12, b1 - 12));
+}
+
+// folded sum of LDS bytes [x, y) (x < y, absolute pairing) from the chunk prefix P
+__device__ __forceinline__ uint32_t lds_range_sum(const uint8_t *S, const uint32_t *P, uint32_t x, uint32_t y) {
+    const uint32_t cx = x >> 4, cy = y >> 4;
+    unsigned long long sum;
+    if (cx == cy) {
+        sum = chunk_part(S, cx, (int)(x & 15), (int)(y & 15));
+    } else {
+        sum = chunk_part(S, cx, (int)(x & 15), 16);
+        sum += P[cy] - P[cx + 1];
+        if (y & 15) sum += chunk_part(S, cy, 0, (int)(y & 15));
+    }
+    return fold16(sum);
+}
+
+__global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[FK_LDS];
+    __shared__ __attribute__((aligned(16))) uint32_t P[FK_NCH + 1];
+    __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
+    __shared__ uint32_t wsums[NWAVES];
+    const int tid = threadIdx.x;
+    {
+        const uint32_t *src = (const uint32_t *)a.cfg;
+        uint32_t *dst = (uint32_t *)&cfg;
+        for (int i = tid; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
+    }
+    if (blockIdx.x == 0) {
+        if (tid < 16) a.ws_zero[tid] = 0;  // the generic kernel's err/ticket/counters
+        if (tid == 16) *a.list_cnt_next = 0;
+    }
+    const bool swp = a.in_swapped != 0;
+    const bool explicit_dir = a.fixed_dir >= 0;
+    g_cu8 *gin = (g_cu8 *)a.in;
+    g_u8 *gout = (g_u8 *)a.out;
+    const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
+    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
+    __syncthreads();
+
+    te_tile_t next;
+    if (blockIdx.x < a.n_tiles) next = a.tiles[blockIdx.x];
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x) {
+        const te_tile_t tile = next;
+        if (t + gridDim.x < a.n_tiles) next = a.tiles[t + gridDim.x];  // descriptor one tile ahead
+        if (tile.scratch_off != TE_NO_SCRATCH) {  // huge record: generic lane
+            if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+            continue;
+        }
+        const uint32_t npkt = tile.npkt;
+        const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull;
+        const uint32_t my_rel = tid < (int)npkt ? a.pkt_rel[tile.first_pkt + tid] : 0u;
+        // ---- span HBM -> LDS (16-byte chunks) ----
+        const uint32_t img = LDS_FRONT + (uint32_t)(G0 - A0) + tile.span_len;  // LDS bytes in use
+        {
+            constexpr int K = (TE_FK_TILE_BYTES / 16 + BLOCK - 1) / BLOCK + 1;  // all in flight at once
+            const uint32_t nchunks = (uint32_t)((G0 + tile.span_len - A0 + 15) >> 4);
+            uint4 v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {  // unconditional (clamped) loads keep v[] in VGPRs
+                const uint32_t c = min(tid + k * BLOCK, nchunks - 1);
+                v[k] = *(g_cu4 *)(gin + A0 + ((uint64_t)c << 4));
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = tid + k * BLOCK;
+                if (c < nchunks) *(uint4 *)(S + LDS_FRONT + (c << 4)) = v[k];
+            }
+        }
+        __syncthreads();
+
+        // ---- phase A: one lane per packet ----
+        const uint32_t r0 = LDS_FRONT + (uint32_t)(G0 - A0) + my_rel;  // record header in S
+        const uint32_t p = r0 + 16;                                    // packet data in S
+        uint32_t H[fl::NW];
+        uint32_t d0 = 0, caplen = 0, len = 0;
+        fl::State st;
+        st.do_l4 = st.tail = false;
+        bool ok = true, nosend = false;
+        if (tid < (int)npkt) {
+            caplen = ld_hdr32(S + r0 + 8, swp);
+            len = ld_hdr32(S + r0 + 12, swp);
+            const uint64_t pktno = a.pkt_base + tile.first_pkt + tid;
+            int dir = TE_DIR_C2S;
+            if (explicit_dir) {
+                dir = a.fixed_dir;
+            } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354)
+                const uint64_t idx = pktno >> 2;
+                const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+                const uint8_t b = idx < a.dirbits_len ? a.dirbits[idx] : 0;
+                dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+            }
+            if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
+                nosend = true;
+            } else {
+                const uint32_t wa = p - 2, A = wa & ~3u, sh = wa & 3u;
+                uint32_t d[fl::NW + 1];
+#pragma unroll
+                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A + 4 * j);
+#pragma unroll
+                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                d0 = d[0];
+                ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
+            }
+        }
+        if (__syncthreads_or(!ok)) {  // a packet for the generic lane: it redoes this tile
+            if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+            continue;
+        }
+
+        // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
+        if (__syncthreads_or(st.tail)) {
+            const uint32_t nch = (img + 15) >> 4;
+            for (uint32_t c = tid; c < nch; c += BLOCK) {
+                const uint4 v = *(const uint4 *)(S + 16 * c);
+                P[c] = fl::wsum(v.x) + fl::wsum(v.y) + fl::wsum(v.z) + fl::wsum(v.w);
+            }
+            __syncthreads();
+            uint32_t loc[FK_Q], tot = 0;
+#pragma unroll
+            for (int k = 0; k < FK_Q; ++k) {
+                const uint32_t c = (uint32_t)tid * FK_Q + k;
+                const uint32_t v = c < nch ? P[c] : 0u;
+                loc[k] = tot;
+                tot += v;
+            }
+            uint32_t total;
+            const uint32_t base = block_exscan(tot, wsums, total);
+#pragma unroll
+            for (int k = 0; k < FK_Q; ++k) {
+                const uint32_t c = (uint32_t)tid * FK_Q + k;
+                if (c < nch) P[c] = base + loc[k];
+            }
+            if (tid == 0) P[nch] = total;
+            __syncthreads();
+        }
+
+        // ---- phase B + write-back ----
+        if (tid < (int)npkt) {
+            if (!nosend) {
+                uint32_t tail = 0;
+                if (st.tail) {
+                    tail = lds_range_sum(S, P, p + fl::WEND, p + st.end);
+                    if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
+                }
+                fl::phase_b(H, st, tail);
+                const uint32_t wa = p - 2, A = wa & ~3u, sh = wa & 3u;
+#pragma unroll
+                for (int j = 0; j < fl::NW; ++j) {
+                    const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
+                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
+                    const int rel = (int)(A + 4 * j) - (int)p;  // packet offset of the dword's first byte
+                    uint8_t *q = S + A + 4 * j;
+                    if (rel + 4 <= (int)caplen) {
+                        *(uint32_t *)q = v;
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 3; ++b)
+                            if (rel + b < (int)caplen) q[b] = (uint8_t)(v >> (8 * b));
+                    }
+                }
+            }
+            if (swp || a.in_nsec) {  // header in host order, microseconds
+                uint8_t *rec = S + r0;
+                uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp);
+                if (a.in_nsec) ts_frac /= 1000;
+                st32(rec, ts_sec);
+                st32(rec + 4, ts_frac);
+                st32(rec + 8, caplen);
+                st32(rec + 12, len);
+            }
+            ((g_u8 *)a.status)[tile.first_pkt + tid] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
+        }
+        const uint32_t n_nosend = __syncthreads_count(nosend);
+
+        // ---- span LDS -> HBM at its input offset (16-byte chunks) ----
+        {
+            const uint64_t Gs = a.out_base + (G0 - a.rec0), Ge = Gs + tile.span_len, C0 = Gs & ~15ull;
+            const uint32_t nchunks = (uint32_t)((Ge - C0 + 15) >> 4);
+            const uint32_t src0 = LDS_FRONT + (uint32_t)(G0 - A0);
+            for (uint32_t c = tid; c < nchunks; c += BLOCK) {
+                const uint64_t C = C0 + ((uint64_t)c << 4);
+                const int64_t q0 = (int64_t)C - (int64_t)Gs;
+                const int b0 = q0 < 0 ? (int)(-q0) : 0;
+                const int b1 = (C + 16 > Ge) ? (int)(Ge - C) : 16;
+                const uint4 v = read16(S, (uint32_t)((int64_t)src0 + q0));
+                g_u8 *dst = gout + C;
+                if (b0 == 0 && b1 == 16) {
+                    *(g_u4 *)dst = v;
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) {
+                        if (b >= b0 && b < b1) {
+                            const uint32_t w = b < 4 ? v.x : (b < 8 ? v.y : (b < 12 ? v.z : v.w));
+                            dst[b] = (uint8_t)(w >> (8 * (b & 3)));
+                        }
+                    }
+                }
+            }
+        }
+        c_pkts += npkt;
+        c_bytes += tile.span_len;
+        c_edited += npkt - n_nosend;
+        __syncthreads();
+    }
+    if (tid < TE_CNT__N) {
+        unsigned long long v = 0;
+        if (tid == TE_CNT_PACKETS || tid == TE_CNT_WRITTEN) v = c_pkts;
+        else if (tid == TE_CNT_BYTES_IN || tid == TE_CNT_BYTES_OUT) v = c_bytes;
+        else if (tid == TE_CNT_EDITED) v = c_edited;
+        a.fk_part[(size_t)blockIdx.x * TE_CNT__N + tid] = v;
+    }
+}
+
 }  // namespace
 
 // persistent grid = the blocks that are resident at once (CUs x occupancy)
+static int cu_count() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return cus;
+}
+
 static int resident_blocks(int slot_layout) {
     static int cached[2] = {0, 0};
     int &c = cached[slot_layout ? 1 : 0];
     if (c) return c;
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 256;
+    int cus = cu_count(), per_cu = 0;
+    if (!cus) return 256;
     hipError_t e = slot_layout
                        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_edit_tiles<MODE_SLOT>, BLOCK, 0)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_edit_tiles<MODE_CONTIG>, BLOCK, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    c = cus * per_cu;
+    return c;
+}
+
+extern "C" int te_fast_grid(void) {
+    static int c = 0;
+    if (c) return c;
+    int cus = cu_count(), per_cu = 0;
+    if (!cus) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_fast_tiles, BLOCK, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
     c = cus * per_cu;
     return c;
 }
@@ -530,10 +853,52 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.scratch = L->scratch;
     a.rec0 = L->rec0;
     a.static_off = (uint32_t)L->static_off;
-    // one memset per launch: error words, ticket, counters, look-back granules
-    hipError_t e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);
-    if (e != hipSuccess) return -1;
-    if (L->n_tiles == 0) return 0;
+    a.tile_list = nullptr;
+    a.list_cnt = nullptr;
+    a.fk_part = nullptr;
+    a.fk_grid = 0;
+    hipError_t e;
+    const bool fast = L->fast && L->static_off && !L->slot_layout && L->n_tiles > 0;
+    if (fast) {
+        // the fast kernel zeroes the generic kernel's words itself: no memset launch
+        FastArgs f;
+        f.cfg = L->cfg;
+        f.portlut = L->portlut;
+        f.dirbits = L->dirbits;
+        f.dirbits_len = L->dirbits_len;
+        f.pkt_base = L->pkt_base;
+        f.in = L->in;
+        f.tiles = L->tiles;
+        f.pkt_rel = L->pkt_rel;
+        f.out = L->out;
+        f.status = L->status;
+        f.tile_list = L->tile_list;
+        f.list_cnt = L->list_cnt + (L->parity & 1);
+        f.list_cnt_next = L->list_cnt + ((L->parity & 1) ^ 1);
+        f.fk_part = (unsigned long long *)L->fk_part;
+        f.ws_zero = (unsigned long long *)L->ws_zero;
+        f.out_base = L->out_base;
+        f.rec0 = L->rec0;
+        f.n_tiles = L->n_tiles;
+        f.fixed_dir = L->fixed_dir;
+        f.in_swapped = L->in_swapped;
+        f.in_nsec = L->in_nsec;
+        f.v6_ok = (uint32_t)L->fast_v6;
+        int fgrid = te_fast_grid();
+        if (fgrid < 1) return -1;
+        if ((uint32_t)fgrid > L->n_tiles) fgrid = (int)L->n_tiles;
+        hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(BLOCK), 0, stream, f);
+        if (hipGetLastError() != hipSuccess) return -1;
+        a.tile_list = L->tile_list;
+        a.list_cnt = L->list_cnt + (L->parity & 1);
+        a.fk_part = (const unsigned long long *)L->fk_part;
+        a.fk_grid = (uint32_t)fgrid;
+    } else {
+        // one memset per launch: error words, ticket, counters, look-back granules
+        e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);
+        if (e != hipSuccess) return -1;
+        if (L->n_tiles == 0) return 0;
+    }
     int grid = L->grid > 0 ? L->grid : resident_blocks(L->slot_layout);
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
     if (L->slot_layout)
