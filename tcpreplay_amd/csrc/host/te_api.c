@@ -57,7 +57,7 @@ struct tcpedit_batch_s {
     uint16_t *d_pkt_rel;
     uint8_t *d_ws;           /* err[0..2] | ticket, done | counters | tile_state[] | list count */
     uint32_t *d_tile_list;   /* fast lane: tiles left to the generic kernel */
-    uint64_t *d_fk_part;     /* fast lane: per-block counters */
+    uint32_t last_cnt_off;   /* workspace offset of the last launch's counter set */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
     /* results */
@@ -70,8 +70,9 @@ struct tcpedit_batch_s {
 #define WS_ERR 0
 #define WS_ZERO 0
 #define WS_TICKET 24
-#define WS_COUNTERS 32
-#define WS_STATE 128
+#define WS_COUNTERS 32   /* counter set 0 (TE_CNT__N words) */
+#define WS_COUNTERS1 128 /* counter set 1: the fast lane alternates sets by launch parity */
+#define WS_STATE 256
 #define WS_LIST_CNT(n_tiles) (WS_STATE + 8 * ((n_tiles) + 1))
 
 /* no edit step can change a record's length or drop it: efcs, VLAN add/del,
@@ -136,6 +137,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
     b->slot_layout = slot_mode;
     b->fast_tiles = !slot_mode && fast_capable(&t->cfg);
     const uint32_t budget = b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
+    const uint32_t max_pkts = b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
     b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
@@ -171,7 +173,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
             huge = !TE_CONTIG_FITS_IN(g, 16 + caplen, budget);
             fits = open && TE_CONTIG_FITS_IN(cur.span_off & 15, off + 16 + caplen - cur.span_off, budget);
         }
-        if (open && (huge || cur.npkt >= TE_MAX_PKTS || !fits)) {
+        if (open && (huge || cur.npkt >= max_pkts || !fits)) {
             if (b->n_tiles == cap_tiles)
                 b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
             b->tiles[b->n_tiles++] = cur;
@@ -226,9 +228,7 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_pkt_rel);
     hipFree(b->d_ws);
     hipFree(b->d_tile_list);
-    hipFree(b->d_fk_part);
     b->d_tile_list = NULL;
-    b->d_fk_part = NULL;
     b->d_in = b->d_out = b->d_status = b->d_scratch = b->d_dirbits = b->d_ws = NULL;
     b->d_tiles = NULL;
     b->d_pkt_rel = NULL;
@@ -353,11 +353,8 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     b->ws_bytes = WS_LIST_CNT(b->n_tiles) + 64;
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
     HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream)); /* the list count starts at 0 */
-    if (b->fast_tiles) {
-        const int fg = te_fast_grid();
+    if (b->fast_tiles)
         HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->n_tiles + 1)));
-        HIPCHK(t, hipMalloc((void **)&b->d_fk_part, sizeof(uint64_t) * TE_CNT__N * (size_t)(fg > 0 ? fg : 1)));
-    }
     if (cache) {
         const uint8_t *cd;
         if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &b->dirbits_len) < 0)
@@ -423,9 +420,11 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
     L.fast_v6 = fast_v6_ok(c);
     L.tile_list = b->d_tile_list;
     L.list_cnt = (uint32_t *)(b->d_ws + WS_LIST_CNT(b->n_tiles));
-    L.fk_part = b->d_fk_part;
     L.parity = (uint32_t)(b->launches++ & 1);
     b->last_fast = L.fast;
+    b->last_cnt_off = L.fast && L.parity ? WS_COUNTERS1 : WS_COUNTERS;
+    L.counters = (uint64_t *)(b->d_ws + b->last_cnt_off);
+    L.counters_next = (uint64_t *)(b->d_ws + (b->last_cnt_off == WS_COUNTERS ? WS_COUNTERS1 : WS_COUNTERS));
     L.ws_zero = (uint64_t *)(b->d_ws + WS_ZERO);
     return te_launch_edit(&L, t->stream);
 }
@@ -445,7 +444,7 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         return TCPEDIT_ERROR;
     }
     HIPCHK(t, hipEventRecord(b->ev1, t->stream));
-    HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + WS_COUNTERS, sizeof(b->counters), hipMemcpyDeviceToHost,
+    HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters), hipMemcpyDeviceToHost,
                              t->stream));
     HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
     if (b->last_fast)

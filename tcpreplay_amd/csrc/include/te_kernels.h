@@ -18,7 +18,12 @@ extern "C" {
 #define TE_HEAD 16             /* headroom before each record (VLAN push) */
 #define TE_TAIL_BYTES 16       /* zeroed bytes after each packet's data */
 #define TE_NO_SCRATCH 0xffffffffffffffffull
-#define TE_FK_TILE_BYTES 16384 /* tile budget when the fast lane runs (more blocks per CU) */
+#ifndef TE_FK_TILE_BYTES
+#define TE_FK_TILE_BYTES 24576 /* tile budget when the fast lane runs */
+#endif
+#ifndef TE_FK_BLOCK
+#define TE_FK_BLOCK 256        /* threads per fast-lane block = max records per fast-lane tile */
+#endif
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
@@ -77,11 +82,11 @@ typedef struct {
     uint32_t *tile_list;      /* device: n_tiles entries */
     uint32_t *list_cnt;       /* device: 2 counts; launch parity p appends to [p] and zeroes [p^1] */
     uint32_t parity;
-    uint64_t *fk_part;        /* device: te_fast_grid() x TE_CNT__N per-block counters */
-    uint64_t *ws_zero;        /* device: 16 words (err, ticket, counters) the fast kernel zeroes */
+    uint64_t *counters_next;  /* fast lane: the other parity's counter set, zeroed for the next launch */
+    uint64_t *ws_zero;        /* device: 4 words (err, ticket) the fast kernel zeroes */
 } te_launch_t;
 
-/* blocks of te_fast_tiles resident on the current device (the fk_part rows needed) */
+/* blocks of te_fast_tiles resident on the current device */
 int te_fast_grid(void);
 
 #ifdef __HIP_PLATFORM_AMD__

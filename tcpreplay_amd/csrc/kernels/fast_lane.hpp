@@ -111,6 +111,7 @@ DI unsigned long long mac48(const u8 *m) {
 struct State {
     u32 l4sum;  // unfolded one's-complement sum so far (pseudo header + L4 bytes inside the window)
     u32 end;    // caplen: L4 bytes run to here
+    u32 dirty;  // bit i: H[i] may differ from the packet bytes (written back)
     bool v6, tcp, do_l4, tail;
 };
 
@@ -154,6 +155,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
         return false;
     }
 
+    u32 dirty = 0;
     // ---- en10mb_encode: MAC rewrite (no VLAN, subsmac or mac-seed here) ----
     if (cfg.mac_mask) {
         const bool c2s = dir == TE_DIR_C2S;
@@ -168,6 +170,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
         H[1] = (u32)(dmac >> 16);
         H[2] = (u32)smac;
         H[3] = with_lo16(H[3], (u32)(smac >> 32));
+        dirty |= 0xfu;
     }
 
     // L4 header (20 bytes) at packet offset 34 (v4) or 54 (v6)
@@ -259,6 +262,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
 #undef FL_V4_UPD
         H[7] = src;
         H[8] = dst;
+        if (cfg.rewrite_ip || cfg.seed) dirty |= (1u << 7) | (1u << 8);
     } else {
         u32 src[4] = {H[6], H[7], H[8], H[9]}, dst[4] = {H[10], H[11], H[12], H[13]};
         // ipv6_addr_csum_replace (edit_packet.c:298-330): only the UDP field is carried
@@ -326,6 +330,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
             H[6 + i] = src[i];
             H[10 + i] = dst[i];
         }
+        if (cfg.rewrite_ip || cfg.seed) dirty |= 0xffu << 6;
     }
 
     // ---- fix_ipv4/ipv6_checksums (edit_packet.c:55-189) -> do_checksum (checksum.c:34-170) ----
@@ -341,6 +346,10 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     for (int i = 0; i < 5; ++i) {
         H[14 + i] = (L[i] & m6) | (H[14 + i] & ~m6);
         H[9 + i] = (L[i] & ~m6) | (H[9 + i] & m6);
+    }
+    {
+        const int base = v6 ? 14 : 9;  // ports (port map), UDP csum (L4+6), TCP csum (L4+16)
+        dirty |= ((cfg.has_portmap ? 1u : 0u) | (tcp ? 0x10u : 0x2u)) << base;
     }
     u32 sum = 0;
     if (do_l4) {
@@ -364,6 +373,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
         H[6] = with_hi16(H[6], 0);
         u32 hs = wsum(H[4]) + wsum(H[5]) + wsum(H[6]) + wsum(H[7]) + wsum(H[8]);
         H[6] = with_hi16(H[6], (~fold16(hs)) & 0xffffu);
+        dirty |= 1u << 6;
     }
 
     // ---- dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC ----
@@ -372,14 +382,17 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
         if (mcast4(d)) {
             H[0] = with_hi16(H[0], 0x0001u);                                         // 01:00
             H[1] = 0x5eu | (((d >> 8) & 0x7fu) << 8) | (((d >> 16) & 0xffu) << 16) | ((d >> 24) << 24);
+            dirty |= 3u;
         }
     } else if ((H[10] & 0xffu) == 0xffu) {
         H[0] = with_hi16(H[0], 0x3333u);
         H[1] = H[13];
+        dirty |= 3u;
     }
 
     st.l4sum = sum;
     st.end = caplen;
+    st.dirty = dirty;
     st.v6 = v6;
     st.tcp = tcp;
     st.do_l4 = do_l4;

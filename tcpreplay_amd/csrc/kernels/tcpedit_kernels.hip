@@ -74,8 +74,7 @@ struct LaunchArgs {
     // block folds the fast kernel's per-block counters into `counters`
     const uint32_t *tile_list;
     const uint32_t *list_cnt;        // this launch's count
-    const unsigned long long *fk_part;
-    uint32_t fk_grid;
+    unsigned long long *counters_next;  // zeroed here for the next launch (fast lane parity)
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -83,7 +82,11 @@ __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
     return swapped ? bswap32(v) : v;
 }
 
-// ---- block-wide exclusive scan of a u32 (BLOCK threads) ----
+// unsigned min (HIP's min() of mixed int/unsigned arguments resolves to the double overload)
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// ---- block-wide exclusive scan of a u32 (NT threads) ----
+template <int NT = BLOCK>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t &total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t x = v;
@@ -96,7 +99,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uin
     __syncthreads();
     uint32_t base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < NWAVES; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         uint32_t s = wsum[w];
         if (w < wid) base += s;
         tot += s;
@@ -249,7 +252,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
                 uint4 v[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {  // unconditional (clamped) loads keep v[] in VGPRs
-                    const uint32_t c = min(c0 + k * BLOCK, nchunks - 1);
+                    const uint32_t c = umin32(c0 + k * BLOCK, nchunks - 1u);
                     v[k] = *(g_cu4 *)(gin + A0 + ((uint64_t)c << 4));
                 }
 #pragma unroll
@@ -486,39 +489,16 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
+    const bool listed = a.tile_list != nullptr;
+    if (a.counters_next && blockIdx.x == 0 && threadIdx.x < TE_CNT__N) a.counters_next[threadIdx.x] = 0;
+    const uint32_t n_work = listed ? *(const volatile uint32_t *)a.list_cnt : a.n_tiles;
+    if (n_work == 0) return;  // after the fast lane, usually nothing is left
     {
-        constexpr int NV = (int)((sizeof(te_dev_cfg_t) + 15) / 16);
         static_assert(sizeof(te_dev_cfg_t) % 4 == 0, "cfg copy");
         const uint32_t *src = (const uint32_t *)a.cfg;
         uint32_t *dst = (uint32_t *)&cfg;
         for (int i = threadIdx.x; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
-        (void)NV;
     }
-    const bool listed = a.tile_list != nullptr;
-    const uint32_t n_work = listed ? *(const volatile uint32_t *)a.list_cnt : a.n_tiles;
-    if (a.fk_part && blockIdx.x == 0) {  // fold the fast kernel's per-block counters (all 256 lanes)
-        unsigned long long v[TE_CNT__N];
-#pragma unroll
-        for (int k = 0; k < TE_CNT__N; ++k) v[k] = 0;
-#pragma unroll 4
-        for (uint32_t b = threadIdx.x; b < a.fk_grid; b += BLOCK) {
-            const unsigned long long *row = a.fk_part + (size_t)b * TE_CNT__N;
-#pragma unroll
-            for (int k = 0; k < TE_CNT__N; ++k) v[k] += row[k];
-        }
-        if (threadIdx.x < TE_CNT__N) sh.cnt[threadIdx.x] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < TE_CNT__N; ++k) {
-            unsigned long long x = v[k];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&sh.cnt[k], x);
-        }
-        __syncthreads();
-        if (threadIdx.x < TE_CNT__N && sh.cnt[threadIdx.x]) atomicAdd(&a.counters[threadIdx.x], sh.cnt[threadIdx.x]);
-    }
-    if (n_work == 0) return;
     for (;;) {
         if (threadIdx.x == 0) sh.tile_id = atomicAdd(a.ticket, 1u);
         __syncthreads();
@@ -543,12 +523,16 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
 // its id goes to tile_list and the generic kernel, launched next, redoes the
 // whole tile (its results for the fast-lane packets are the same bytes).
 // ===========================================================================
-#ifndef TE_FK_MIN_BLOCKS
-#define TE_FK_MIN_BLOCKS 4
+#ifndef TE_FK_PREFETCH
+#define TE_FK_PREFETCH 1  // load tile k+1 into registers while tile k is edited
 #endif
+#ifndef TE_FK_MIN_BLOCKS
+#define TE_FK_MIN_BLOCKS 3  // waves per SIMD (the second launch-bounds argument on this toolchain)
+#endif
+constexpr int FKB = TE_FK_BLOCK;                              // threads per fast-lane block
 constexpr int FK_LDS = TE_FK_TILE_BYTES + LDS_FRONT + 128;  // + window overrun past the span
 constexpr int FK_NCH = (TE_FK_TILE_BYTES + LDS_FRONT + 15) / 16 + 2;
-constexpr int FK_Q = (FK_NCH + BLOCK - 1) / BLOCK;
+constexpr int FK_Q = (FK_NCH + FKB - 1) / FKB;
 
 struct FastArgs {
     const te_dev_cfg_t *cfg;
@@ -564,7 +548,7 @@ struct FastArgs {
     uint32_t *tile_list;
     uint32_t *list_cnt;  // this launch's count; list_cnt_next is zeroed for the next launch
     uint32_t *list_cnt_next;
-    unsigned long long *fk_part;
+    unsigned long long *counters;  // this launch's counter set (zeroed by the previous launch)
     unsigned long long *ws_zero;
     uint64_t out_base, rec0;
     uint32_t n_tiles;
@@ -593,20 +577,20 @@ __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t *S, const uint32
     return fold16(sum);
 }
 
-__global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs a) {
+__global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t S[FK_LDS];
     __shared__ __attribute__((aligned(16))) uint32_t P[FK_NCH + 1];
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
-    __shared__ uint32_t wsums[NWAVES];
+    __shared__ uint32_t wsums[FKB / 64];
     const int tid = threadIdx.x;
     {
         const uint32_t *src = (const uint32_t *)a.cfg;
         uint32_t *dst = (uint32_t *)&cfg;
-        for (int i = tid; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
+        for (int i = tid; i < (int)(sizeof(te_dev_cfg_t) / 4); i += FKB) dst[i] = src[i];
     }
     if (blockIdx.x == 0) {
-        if (tid < 16) a.ws_zero[tid] = 0;  // the generic kernel's err/ticket/counters
-        if (tid == 16) *a.list_cnt_next = 0;
+        if (tid < 4) a.ws_zero[tid] = 0;  // the generic kernel's err words and ticket
+        if (tid == 4) *a.list_cnt_next = 0;
     }
     const bool swp = a.in_swapped != 0;
     const bool explicit_dir = a.fixed_dir >= 0;
@@ -616,44 +600,76 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
     unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
     __syncthreads();
 
-    te_tile_t next;
-    if (blockIdx.x < a.n_tiles) next = a.tiles[blockIdx.x];
-    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x) {
-        const te_tile_t tile = next;
-        if (t + gridDim.x < a.n_tiles) next = a.tiles[t + gridDim.x];  // descriptor one tile ahead
-        if (tile.scratch_off != TE_NO_SCRATCH) {  // huge record: generic lane
-            if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
-            continue;
-        }
+    constexpr int K = (TE_FK_TILE_BYTES / 16 + FKB - 1) / FKB + 1;  // 16-byte chunks per lane per tile
+    static_assert(K <= 8, "FK_EACH covers 8 chunk registers");
+    // this tile's chunks in flight, in named registers (an array indexed in a loop that
+    // the compiler may re-roll ends up in scratch)
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+#define FK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define FK_LD(k)                                                        \
+    if constexpr (k < K) {                                              \
+        const uint32_t c = umin32((uint32_t)tid + k * FKB, nc_ - 1u);   \
+        v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));              \
+    }
+#define FK_ISSUE(tl)                                                                     \
+    if ((tl).scratch_off == TE_NO_SCRATCH) {                                             \
+        const uint64_t a0_ = (tl).span_off & ~15ull;                                     \
+        const uint32_t nc_ = (uint32_t)(((tl).span_off + (tl).span_len - a0_ + 15) >> 4); \
+        FK_EACH(FK_LD)                                                                   \
+    }
+#define FK_ST(k)                                                                              \
+    if constexpr (k < K) { /* branch-free: lanes past the span write a dummy slot */         \
+        const uint32_t c = (uint32_t)tid + k * FKB;                                           \
+        *(uint4 *)(S + (c < nchunks ? LDS_FRONT + (c << 4) : FK_LDS - 16)) = v##k;            \
+    }
+    const uint32_t G = gridDim.x;
+    te_tile_t cur, nxt;
+    if (blockIdx.x < a.n_tiles) {
+        cur = a.tiles[blockIdx.x];
+        FK_ISSUE(cur);
+    }
+    if (blockIdx.x + G < a.n_tiles) nxt = a.tiles[blockIdx.x + G];
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += G) {
+        const te_tile_t tile = cur;
+        const bool huge = tile.scratch_off != TE_NO_SCRATCH;
         const uint32_t npkt = tile.npkt;
         const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull;
-        const uint32_t my_rel = tid < (int)npkt ? a.pkt_rel[tile.first_pkt + tid] : 0u;
-        // ---- span HBM -> LDS (16-byte chunks) ----
+        const uint32_t my_rel = (!huge && tid < (int)npkt) ? a.pkt_rel[tile.first_pkt + tid] : 0u;
         const uint32_t img = LDS_FRONT + (uint32_t)(G0 - A0) + tile.span_len;  // LDS bytes in use
-        {
-            constexpr int K = (TE_FK_TILE_BYTES / 16 + BLOCK - 1) / BLOCK + 1;  // all in flight at once
+        if (!huge) {  // ---- span -> LDS ----
             const uint32_t nchunks = (uint32_t)((G0 + tile.span_len - A0 + 15) >> 4);
-            uint4 v[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {  // unconditional (clamped) loads keep v[] in VGPRs
-                const uint32_t c = min(tid + k * BLOCK, nchunks - 1);
-                v[k] = *(g_cu4 *)(gin + A0 + ((uint64_t)c << 4));
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const uint32_t c = tid + k * BLOCK;
-                if (c < nchunks) *(uint4 *)(S + LDS_FRONT + (c << 4)) = v[k];
-            }
+            FK_EACH(FK_ST)
         }
         __syncthreads();
+#if TE_FK_PREFETCH
+        // the next tile's loads fly while this one is edited and stored
+        cur = nxt;
+        if (t + G < a.n_tiles) FK_ISSUE(cur);
+        if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+#endif
+        if (huge) {  // a record larger than a tile: generic lane
+            if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+#if !TE_FK_PREFETCH
+            cur = nxt;
+            if (t + G < a.n_tiles) FK_ISSUE(cur);
+            if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+#endif
+            continue;
+        }
+#if !TE_FK_PREFETCH
+        cur = nxt;
+        if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+#endif
 
         // ---- phase A: one lane per packet ----
         const uint32_t r0 = LDS_FRONT + (uint32_t)(G0 - A0) + my_rel;  // record header in S
         const uint32_t p = r0 + 16;                                    // packet data in S
+        const uint32_t wa = p - 2;                                     // window start (packet offset -2)
         uint32_t H[fl::NW];
         uint32_t d0 = 0, caplen = 0, len = 0;
         fl::State st;
         st.do_l4 = st.tail = false;
+        st.dirty = 0;
         bool ok = true, nosend = false;
         if (tid < (int)npkt) {
             caplen = ld_hdr32(S + r0 + 8, swp);
@@ -671,25 +687,38 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
             if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
                 nosend = true;
             } else {
-                const uint32_t wa = p - 2, A = wa & ~3u, sh = wa & 3u;
-                uint32_t d[fl::NW + 1];
+                // 8-byte aligned ds_read_b64 pairs (half the bank conflicts of dword reads), then
+                // a dword select and a byte funnel shift align the window to packet offset -2
+                const uint32_t A8 = wa & ~7u, s8 = wa & 7u, sh = s8 & 3u;
+                uint32_t d[fl::NW + 2];
 #pragma unroll
-                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A + 4 * j);
+                for (int j = 0; j < fl::NW + 2; j += 2) {
+                    const uint2 q = *(const uint2 *)(S + A8 + 4 * j);
+                    d[j] = q.x;
+                    d[j + 1] = q.y;
+                }
+                const uint32_t mh = s8 >= 4 ? 0xffffffffu : 0u;  // bitwise select: an index ternary
+                uint32_t e[fl::NW + 1];                             // would move d[] to scratch
 #pragma unroll
-                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-                d0 = d[0];
+                for (int j = 0; j <= fl::NW; ++j) e[j] = (d[j + 1] & mh) | (d[j] & ~mh);
+#pragma unroll
+                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
+                d0 = e[0];
                 ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
             }
         }
         if (__syncthreads_or(!ok)) {  // a packet for the generic lane: it redoes this tile
             if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+#if !TE_FK_PREFETCH
+            if (t + G < a.n_tiles) FK_ISSUE(cur);
+#endif
             continue;
         }
 
         // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
         if (__syncthreads_or(st.tail)) {
             const uint32_t nch = (img + 15) >> 4;
-            for (uint32_t c = tid; c < nch; c += BLOCK) {
+            for (uint32_t c = tid; c < nch; c += FKB) {
                 const uint4 v = *(const uint4 *)(S + 16 * c);
                 P[c] = fl::wsum(v.x) + fl::wsum(v.y) + fl::wsum(v.z) + fl::wsum(v.w);
             }
@@ -703,7 +732,7 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
                 tot += v;
             }
             uint32_t total;
-            const uint32_t base = block_exscan(tot, wsums, total);
+            const uint32_t base = block_exscan<FKB>(tot, wsums, total);
 #pragma unroll
             for (int k = 0; k < FK_Q; ++k) {
                 const uint32_t c = (uint32_t)tid * FK_Q + k;
@@ -713,7 +742,7 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
             __syncthreads();
         }
 
-        // ---- phase B + write-back ----
+        // ---- phase B + write-back of the dwords phase A touched ----
         if (tid < (int)npkt) {
             if (!nosend) {
                 uint32_t tail = 0;
@@ -722,9 +751,12 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
                     if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
                 }
                 fl::phase_b(H, st, tail);
-                const uint32_t wa = p - 2, A = wa & ~3u, sh = wa & 3u;
+                const uint32_t A = wa & ~3u, sh = wa & 3u;
+                // LDS dword j holds window bytes from H[j-1] and H[j] (from H[j] alone when aligned)
+                const uint32_t need = st.dirty | (sh ? (st.dirty << 1) : 0u);
 #pragma unroll
                 for (int j = 0; j < fl::NW; ++j) {
+                    if (!((need >> j) & 1u)) continue;
                     const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
                     const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
                     const int rel = (int)(A + 4 * j) - (int)p;  // packet offset of the dword's first byte
@@ -751,17 +783,17 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
         }
         const uint32_t n_nosend = __syncthreads_count(nosend);
 
-        // ---- span LDS -> HBM at its input offset (16-byte chunks) ----
+        // ---- span LDS -> HBM at its input offset: output chunk C is LDS chunk
+        //      C - G0 + LDS_FRONT + (G0 - A0), i.e. 16-byte aligned on both sides ----
         {
             const uint64_t Gs = a.out_base + (G0 - a.rec0), Ge = Gs + tile.span_len, C0 = Gs & ~15ull;
             const uint32_t nchunks = (uint32_t)((Ge - C0 + 15) >> 4);
-            const uint32_t src0 = LDS_FRONT + (uint32_t)(G0 - A0);
-            for (uint32_t c = tid; c < nchunks; c += BLOCK) {
+            const int64_t lds_of_out = (int64_t)(LDS_FRONT + (uint32_t)(G0 - A0)) - (int64_t)Gs;
+            for (uint32_t c = tid; c < nchunks; c += FKB) {
                 const uint64_t C = C0 + ((uint64_t)c << 4);
-                const int64_t q0 = (int64_t)C - (int64_t)Gs;
-                const int b0 = q0 < 0 ? (int)(-q0) : 0;
+                const int b0 = C < Gs ? (int)(Gs - C) : 0;
                 const int b1 = (C + 16 > Ge) ? (int)(Ge - C) : 16;
-                const uint4 v = read16(S, (uint32_t)((int64_t)src0 + q0));
+                const uint4 v = *(const uint4 *)(S + (int64_t)C + lds_of_out);
                 g_u8 *dst = gout + C;
                 if (b0 == 0 && b1 == 16) {
                     *(g_u4 *)dst = v;
@@ -779,14 +811,21 @@ __global__ void __launch_bounds__(BLOCK, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArg
         c_pkts += npkt;
         c_bytes += tile.span_len;
         c_edited += npkt - n_nosend;
+#if !TE_FK_PREFETCH
+        if (t + G < a.n_tiles) FK_ISSUE(cur);
+#endif
         __syncthreads();
     }
-    if (tid < TE_CNT__N) {
+#undef FK_ISSUE
+#undef FK_LD
+#undef FK_ST
+#undef FK_EACH
+    if (tid < TE_CNT__N) {  // fire-and-forget adds of the block's totals
         unsigned long long v = 0;
         if (tid == TE_CNT_PACKETS || tid == TE_CNT_WRITTEN) v = c_pkts;
         else if (tid == TE_CNT_BYTES_IN || tid == TE_CNT_BYTES_OUT) v = c_bytes;
         else if (tid == TE_CNT_EDITED) v = c_edited;
-        a.fk_part[(size_t)blockIdx.x * TE_CNT__N + tid] = v;
+        if (v) atomicAdd(&a.counters[tid], v);
     }
 }
 
@@ -820,7 +859,7 @@ extern "C" int te_fast_grid(void) {
     if (c) return c;
     int cus = cu_count(), per_cu = 0;
     if (!cus) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_fast_tiles, BLOCK, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_fast_tiles, FKB, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     c = cus * per_cu;
     return c;
@@ -855,8 +894,7 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.static_off = (uint32_t)L->static_off;
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
-    a.fk_part = nullptr;
-    a.fk_grid = 0;
+    a.counters_next = nullptr;
     hipError_t e;
     const bool fast = L->fast && L->static_off && !L->slot_layout && L->n_tiles > 0;
     if (fast) {
@@ -875,7 +913,7 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
         f.tile_list = L->tile_list;
         f.list_cnt = L->list_cnt + (L->parity & 1);
         f.list_cnt_next = L->list_cnt + ((L->parity & 1) ^ 1);
-        f.fk_part = (unsigned long long *)L->fk_part;
+        f.counters = (unsigned long long *)L->counters;
         f.ws_zero = (unsigned long long *)L->ws_zero;
         f.out_base = L->out_base;
         f.rec0 = L->rec0;
@@ -887,12 +925,11 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
         int fgrid = te_fast_grid();
         if (fgrid < 1) return -1;
         if ((uint32_t)fgrid > L->n_tiles) fgrid = (int)L->n_tiles;
-        hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(BLOCK), 0, stream, f);
+        hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
         if (hipGetLastError() != hipSuccess) return -1;
         a.tile_list = L->tile_list;
         a.list_cnt = L->list_cnt + (L->parity & 1);
-        a.fk_part = (const unsigned long long *)L->fk_part;
-        a.fk_grid = (uint32_t)fgrid;
+        a.counters_next = (unsigned long long *)L->counters_next;
     } else {
         // one memset per launch: error words, ticket, counters, look-back granules
         e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);

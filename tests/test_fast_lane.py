@@ -103,14 +103,15 @@ def test_fast_and_generic_lanes_agree(built):
 
 def test_fast_lane_huge_and_jumbo_records(built):
     rng_recs = F.mixed(200, seed=5, near_miss=0.0)
-    big = S.records(S.pcap_fixed(2, 9000, seed=2)) + S.records(S.pcap_fixed(1, 20000, seed=3, ipv6=True, proto=6))
-    recs = rng_recs[:50] + big[:1] + rng_recs[50:120] + big[1:] + rng_recs[120:]
+    big = (S.records(S.pcap_fixed(2, 9000, seed=2)) + S.records(S.pcap_fixed(1, 20000, seed=3, ipv6=True, proto=6))
+           + S.records(S.pcap_fixed(1, 40000, seed=4, ipv6=True, proto=17)))  # > any fast-lane tile
+    recs = rng_recs[:50] + big[:1] + rng_recs[50:120] + big[1:3] + rng_recs[120:] + big[3:]
     pcap = S.build_pcap(recs)
     for args in (["--fixcsum"], ["--seed=3", "--fixcsum"]):
         rc_o, exp = O.rewrite(pcap, args)
         rc, out, r = run(pcap, args)
-        assert r.fast_lane == 1 and r.generic_tiles >= 1  # the >16 KiB record goes to the generic lane
         assert rc == rc_o == 0 and out == exp
+        assert r.fast_lane == 1 and r.generic_tiles >= 1  # the 40000-byte record takes the generic lane
 
 
 def test_fast_lane_with_tcpprep_cache_directions(built):

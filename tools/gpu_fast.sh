@@ -9,7 +9,7 @@ case $rc in 0|1) ;; *) exit $rc ;; esac
 timeout -k 10 600 python -m pytest tests -x -q -m gpu -k "not full_size" > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/gpu_tests.log; echo "GPU EXIT $rc"
 case $rc in 0|1) ;; *) exit $rc ;; esac
-for v in default fk3 fk5 nofast; do
+for v in b256t16p3 b128t12p3 b256t24p3 b256t32p3 b128t8p3 b256t16n4 b128t12n4; do
   if [ $v = default ]; then unset TCPEDIT_HIP_LIB TCPEDIT_HIP_NO_FAST
   elif [ $v = nofast ]; then unset TCPEDIT_HIP_LIB; export TCPEDIT_HIP_NO_FAST=1
   else export TCPEDIT_HIP_LIB=$PWD/tcpreplay_amd/lib/var/libtcpedit_hip_$v.so; unset TCPEDIT_HIP_NO_FAST; fi
