@@ -129,6 +129,10 @@ size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap); /* D2H, 
 const uint8_t *tcpedit_batch_status(tcpedit_batch_t *b);           /* per-record TE_ST_* bytes */
 /* times `iters` back-to-back device runs with hipEvents on the run's stream */
 int tcpedit_batch_time(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run);
+/* ... and the mean duration of the edit kernel alone (the fast-lane kernel when it runs),
+ * from a hipEvent pair around that kernel in every run */
+int tcpedit_batch_time_kernels(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run,
+                               double *ms_kernel);
 void tcpedit_batch_close(tcpedit_batch_t *b);
 /* device pointers, for callers that keep the data in HBM (e.g. a sender) */
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b);

@@ -74,6 +74,8 @@ def load():
         "tcpedit_batch_output": (sz, [vp, vp, sz]),
         "tcpedit_batch_status": (ctypes.POINTER(ctypes.c_uint8), [vp]),
         "tcpedit_batch_time": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
+        "tcpedit_batch_time_kernels": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_close": (None, [vp]),
         "tcpedit_batch_device_output": (vp, [vp]),
         "tcpedit_batch_input_bytes": (u64, [vp]),
@@ -204,6 +206,14 @@ class Batch:
         if self._L.tcpedit_batch_time(self._te._ctx, self._b, int(iters), ctypes.byref(ms)) < 0:
             raise RuntimeError(self._te.geterr())
         return ms.value
+
+    def time_kernels(self, iters):
+        """(ms per run of the whole device pipeline, ms of the edit kernel alone) over `iters` runs"""
+        ms, kms = ctypes.c_double(), ctypes.c_double()
+        if self._L.tcpedit_batch_time_kernels(self._te._ctx, self._b, int(iters), ctypes.byref(ms),
+                                              ctypes.byref(kms)) < 0:
+            raise RuntimeError(self._te.geterr())
+        return ms.value, kms.value
 
     def close(self):
         if self._b:

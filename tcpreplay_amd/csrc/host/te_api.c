@@ -50,6 +50,8 @@ struct tcpedit_batch_s {
     uint64_t launches;       /* parity selects the fast lane's tile-list count */
     int last_fast;           /* the last launch ran the fast lane ... */
     uint32_t last_listed;    /* ... and left this many tiles to the generic kernel */
+    hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
+    int kev_n;
     /* device side */
     uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
     uint64_t dirbits_len;
@@ -243,6 +245,9 @@ void tcpedit_batch_close(tcpedit_batch_t *b)
         hipEventDestroy(b->ev0);
     if (b->ev1)
         hipEventDestroy(b->ev1);
+    for (int i = 0; i < b->kev_n; i++)
+        hipEventDestroy(b->kev[i]);
+    free(b->kev);
     free(b->tiles);
     free(b->pkt_rel);
     free(b->status);
@@ -381,7 +386,13 @@ static int fast_lane_off(void)
     return e && *e && *e != '0';
 }
 
+static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1);
 static int launch(tcpedit_batch_t *b, int fixed_dir)
+{
+    return launch_ev(b, fixed_dir, NULL, NULL);
+}
+
+static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1)
 {
     tcpedit_t *t = b->ctx;
     te_launch_t L;
@@ -426,6 +437,8 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
     L.counters = (uint64_t *)(b->d_ws + b->last_cnt_off);
     L.counters_next = (uint64_t *)(b->d_ws + (b->last_cnt_off == WS_COUNTERS ? WS_COUNTERS1 : WS_COUNTERS));
     L.ws_zero = (uint64_t *)(b->d_ws + WS_ZERO);
+    L.ev_k0 = k0;
+    L.ev_k1 = k1;
     return te_launch_edit(&L, t->stream);
 }
 
@@ -586,6 +599,51 @@ int tcpedit_batch_time(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms_p
     return TCPEDIT_OK;
 fail:
     return TCPEDIT_ERROR;
+}
+
+int tcpedit_batch_time_kernels(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms_per_run, double *ms_kernel)
+{
+    hipEvent_t e0 = NULL, e1 = NULL;
+    float ms = 0;
+    int rc = TCPEDIT_ERROR;
+    if (!t || !b || iters <= 0 || te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (b->kev_n < 2 * iters) { /* grow the pool (kept for later calls: no creation in timed runs) */
+        hipEvent_t *k = realloc(b->kev, sizeof(hipEvent_t) * 2 * (size_t)iters);
+        if (!k)
+            return TCPEDIT_ERROR;
+        b->kev = k;
+        while (b->kev_n < 2 * iters) {
+            HIPCHK(t, hipEventCreate(&b->kev[b->kev_n]));
+            b->kev_n++;
+        }
+    }
+    HIPCHK(t, hipEventCreate(&e0));
+    HIPCHK(t, hipEventCreate(&e1));
+    HIPCHK(t, hipEventRecord(e0, t->stream));
+    for (int i = 0; i < iters; i++)
+        if (launch_ev(b, -1, b->kev[2 * i], b->kev[2 * i + 1]) != 0) {
+            te_seterr(t, "kernel launch failed");
+            goto fail;
+        }
+    HIPCHK(t, hipEventRecord(e1, t->stream));
+    HIPCHK(t, hipEventSynchronize(e1));
+    HIPCHK(t, hipEventElapsedTime(&ms, e0, e1));
+    *ms_per_run = ms / iters;
+    double ksum = 0;
+    for (int i = 0; i < iters; i++) {
+        float k = 0;
+        HIPCHK(t, hipEventElapsedTime(&k, b->kev[2 * i], b->kev[2 * i + 1]));
+        ksum += k;
+    }
+    *ms_kernel = ksum / iters;
+    rc = TCPEDIT_OK;
+fail:
+    if (e0)
+        hipEventDestroy(e0);
+    if (e1)
+        hipEventDestroy(e1);
+    return rc;
 }
 
 int tcpedit_rewrite_pcap(tcpedit_t *t, const void *in, size_t in_len, const void *cache, size_t cache_len, void **out,

@@ -84,6 +84,7 @@ typedef struct {
     uint32_t parity;
     uint64_t *counters_next;  /* fast lane: the other parity's counter set, zeroed for the next launch */
     uint64_t *ws_zero;        /* device: 4 words (err, ticket) the fast kernel zeroes */
+    void *ev_k0, *ev_k1;      /* optional hipEvent_t pair recorded around the dominant edit kernel */
 } te_launch_t;
 
 /* blocks of te_fast_tiles resident on the current device */

@@ -534,6 +534,19 @@ constexpr int FK_LDS = TE_FK_TILE_BYTES + LDS_FRONT + 128;  // + window overrun 
 constexpr int FK_NCH = (TE_FK_TILE_BYTES + LDS_FRONT + 15) / 16 + 2;
 constexpr int FK_Q = (FK_NCH + FKB - 1) / FKB;
 
+// TE_FK_STAMPS builds (diagnostics only): s_memtime per phase, summed per block,
+// printed by a few blocks at exit
+#if TE_FK_STAMPS
+#define FK_STAMP(i)                                     \
+    {                                                   \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        ph[i] += now_ - last_;                          \
+        last_ = now_;                                   \
+    }
+#else
+#define FK_STAMP(i)
+#endif
+
 struct FastArgs {
     const te_dev_cfg_t *cfg;
     const uint16_t *portlut;
@@ -582,6 +595,10 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
     __shared__ __attribute__((aligned(16))) uint32_t P[FK_NCH + 1];
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
     __shared__ uint32_t wsums[FKB / 64];
+    // per tile: bit 0 some packet deferred, bit 1 some packet needs the chunk prefix.  Two
+    // slots by iteration parity: the other slot is cleared only after the fill barrier, when
+    // every thread has read it (a deferred tile leaves the loop without an end barrier)
+    __shared__ uint32_t tflags[2];
     const int tid = threadIdx.x;
     {
         const uint32_t *src = (const uint32_t *)a.cfg;
@@ -611,11 +628,16 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
         const uint32_t c = umin32((uint32_t)tid + k * FKB, nc_ - 1u);   \
         v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));              \
     }
-#define FK_ISSUE(tl)                                                                     \
-    if ((tl).scratch_off == TE_NO_SCRATCH) {                                             \
-        const uint64_t a0_ = (tl).span_off & ~15ull;                                     \
-        const uint32_t nc_ = (uint32_t)(((tl).span_off + (tl).span_len - a0_ + 15) >> 4); \
-        FK_EACH(FK_LD)                                                                   \
+// unconditional (a huge tile loads its first chunk K times): the vector-memory
+// count is then the same on every path and the waits stay partial
+#define FK_ISSUE(tl)                                                                              \
+    {                                                                                             \
+        const uint64_t a0_ = (tl).span_off & ~15ull;                                              \
+        const uint32_t nc_ = (tl).scratch_off == TE_NO_SCRATCH                                    \
+                                 ? (uint32_t)(((tl).span_off + (tl).span_len - a0_ + 15) >> 4)   \
+                                 : 1u;                                                            \
+        FK_EACH(FK_LD)                                                                            \
+        rel_next = pkt_rel[(tl).first_pkt + umin32((uint32_t)tid, (tl).npkt - 1u)];                \
     }
 #define FK_ST(k)                                                                              \
     if constexpr (k < K) { /* branch-free: lanes past the span write a dummy slot */         \
@@ -623,44 +645,58 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
         *(uint4 *)(S + (c < nchunks ? LDS_FRONT + (c << 4) : FK_LDS - 16)) = v##k;            \
     }
     const uint32_t G = gridDim.x;
+    // descriptors through the constant address space: scalar loads (lgkmcnt), so
+    // fetching one never waits on the vector loads in flight
+    const TE_AS_CONST te_tile_t *tiles = (const TE_AS_CONST te_tile_t *)a.tiles;
+    const TE_AS_CONST uint16_t *pkt_rel = (const TE_AS_CONST uint16_t *)a.pkt_rel;
     te_tile_t cur, nxt;
+    uint32_t rel_next = 0;  // this lane's record offset in the tile whose chunks are in flight
     if (blockIdx.x < a.n_tiles) {
-        cur = a.tiles[blockIdx.x];
+        cur = tiles[blockIdx.x];
         FK_ISSUE(cur);
     }
-    if (blockIdx.x + G < a.n_tiles) nxt = a.tiles[blockIdx.x + G];
-    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += G) {
+    if (blockIdx.x + G < a.n_tiles) nxt = tiles[blockIdx.x + G];
+#if TE_FK_STAMPS
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
+#endif
+    if (tid == 0) tflags[0] = tflags[1] = 0;
+    __syncthreads();
+    uint32_t slot = 0;
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += G, slot ^= 1u) {
+        FK_STAMP(0)  // loop overhead / previous iteration tail
         const te_tile_t tile = cur;
         const bool huge = tile.scratch_off != TE_NO_SCRATCH;
         const uint32_t npkt = tile.npkt;
         const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull;
-        const uint32_t my_rel = (!huge && tid < (int)npkt) ? a.pkt_rel[tile.first_pkt + tid] : 0u;
+        const uint32_t my_rel = rel_next;
         const uint32_t img = LDS_FRONT + (uint32_t)(G0 - A0) + tile.span_len;  // LDS bytes in use
-        if (!huge) {  // ---- span -> LDS ----
-            const uint32_t nchunks = (uint32_t)((G0 + tile.span_len - A0 + 15) >> 4);
+        {  // ---- span -> LDS (also for a huge tile: harmless, and keeps the waits partial) ----
+            const uint32_t nchunks = huge ? 0u : (uint32_t)((G0 + tile.span_len - A0 + 15) >> 4);
             FK_EACH(FK_ST)
         }
         __syncthreads();
+        if (tid == 0) tflags[slot ^ 1u] = 0;
 #if TE_FK_PREFETCH
         // the next tile's loads fly while this one is edited and stored
         cur = nxt;
         if (t + G < a.n_tiles) FK_ISSUE(cur);
-        if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+        if (t + 2 * G < a.n_tiles) nxt = tiles[t + 2 * G];
 #endif
         if (huge) {  // a record larger than a tile: generic lane
             if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
 #if !TE_FK_PREFETCH
             cur = nxt;
             if (t + G < a.n_tiles) FK_ISSUE(cur);
-            if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+            if (t + 2 * G < a.n_tiles) nxt = tiles[t + 2 * G];
 #endif
             continue;
         }
 #if !TE_FK_PREFETCH
         cur = nxt;
-        if (t + 2 * G < a.n_tiles) nxt = a.tiles[t + 2 * G];
+        if (t + 2 * G < a.n_tiles) nxt = tiles[t + 2 * G];
 #endif
 
+        FK_STAMP(1)  // fill LDS (waits for the prefetched chunks) + barrier + next prefetch issue
         // ---- phase A: one lane per packet ----
         const uint32_t r0 = LDS_FRONT + (uint32_t)(G0 - A0) + my_rel;  // record header in S
         const uint32_t p = r0 + 16;                                    // packet data in S
@@ -672,8 +708,17 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
         st.dirty = 0;
         bool ok = true, nosend = false;
         if (tid < (int)npkt) {
-            caplen = ld_hdr32(S + r0 + 8, swp);
-            len = ld_hdr32(S + r0 + 12, swp);
+            {  // caplen, len: three aligned dword reads + funnel shifts (not eight byte reads)
+                const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
+                const uint32_t w0 = *(const uint32_t *)(S + ha), w1 = *(const uint32_t *)(S + ha + 4),
+                               w2 = *(const uint32_t *)(S + ha + 8);
+                caplen = __builtin_amdgcn_alignbyte(w1, w0, hs);
+                len = __builtin_amdgcn_alignbyte(w2, w1, hs);
+                if (swp) {
+                    caplen = bswap32(caplen);
+                    len = bswap32(len);
+                }
+            }
             const uint64_t pktno = a.pkt_base + tile.first_pkt + tid;
             int dir = TE_DIR_C2S;
             if (explicit_dir) {
@@ -707,7 +752,14 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
                 ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
             }
         }
-        if (__syncthreads_or(!ok)) {  // a packet for the generic lane: it redoes this tile
+        {
+            const uint32_t f = (ok ? 0u : 1u) | (st.tail ? 2u : 0u);
+            if (f) atomicOr(&tflags[slot], f);
+        }
+        __syncthreads();
+        const uint32_t tf = tflags[slot];
+        FK_STAMP(2)  // phase A + its barrier
+        if (tf & 1u) {  // a packet for the generic lane: it redoes this tile
             if (tid == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
 #if !TE_FK_PREFETCH
             if (t + G < a.n_tiles) FK_ISSUE(cur);
@@ -716,7 +768,7 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
         }
 
         // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
-        if (__syncthreads_or(st.tail)) {
+        if (tf & 2u) {
             const uint32_t nch = (img + 15) >> 4;
             for (uint32_t c = tid; c < nch; c += FKB) {
                 const uint4 v = *(const uint4 *)(S + 16 * c);
@@ -742,6 +794,7 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
             __syncthreads();
         }
 
+        FK_STAMP(3)  // chunk prefix
         // ---- phase B + write-back of the dwords phase A touched ----
         if (tid < (int)npkt) {
             if (!nosend) {
@@ -782,6 +835,7 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
             ((g_u8 *)a.status)[tile.first_pkt + tid] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
         }
         const uint32_t n_nosend = __syncthreads_count(nosend);
+        FK_STAMP(4)  // phase B + write-back + status + barrier
 
         // ---- span LDS -> HBM at its input offset: output chunk C is LDS chunk
         //      C - G0 + LDS_FRONT + (G0 - A0), i.e. 16-byte aligned on both sides ----
@@ -789,28 +843,44 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
             const uint64_t Gs = a.out_base + (G0 - a.rec0), Ge = Gs + tile.span_len, C0 = Gs & ~15ull;
             const uint32_t nchunks = (uint32_t)((Ge - C0 + 15) >> 4);
             const int64_t lds_of_out = (int64_t)(LDS_FRONT + (uint32_t)(G0 - A0)) - (int64_t)Gs;
-            for (uint32_t c = tid; c < nchunks; c += FKB) {
-                const uint64_t C = C0 + ((uint64_t)c << 4);
-                const int b0 = C < Gs ? (int)(Gs - C) : 0;
-                const int b1 = (C + 16 > Ge) ? (int)(Ge - C) : 16;
-                const uint4 v = *(const uint4 *)(S + (int64_t)C + lds_of_out);
-                g_u8 *dst = gout + C;
-                if (b0 == 0 && b1 == 16) {
-                    *(g_u4 *)dst = v;
-                } else {
+            // all LDS reads first (one LDS latency), then the stores
+            constexpr int KS = (TE_FK_TILE_BYTES / 16 + 2 + FKB - 1) / FKB;
+            uint4 w[KS];
 #pragma unroll
-                    for (int b = 0; b < 16; ++b) {
-                        if (b >= b0 && b < b1) {
-                            const uint32_t w = b < 4 ? v.x : (b < 8 ? v.y : (b < 12 ? v.z : v.w));
-                            dst[b] = (uint8_t)(w >> (8 * (b & 3)));
+            for (int k = 0; k < KS; ++k) {
+                const uint32_t c = umin32((uint32_t)tid + k * FKB, nchunks - 1u);
+                w[k] = *(const uint4 *)(S + (int64_t)(C0 + ((uint64_t)c << 4)) + lds_of_out);
+            }
+#pragma unroll
+            for (int k = 0; k < KS; ++k) {
+                const uint32_t c = (uint32_t)tid + k * FKB;
+                if (c < nchunks) {
+                    const uint64_t C = C0 + ((uint64_t)c << 4);
+                    const int b0 = C < Gs ? (int)(Gs - C) : 0;
+                    const int b1 = (C + 16 > Ge) ? (int)(Ge - C) : 16;
+                    const uint4 v = w[k];
+                    g_u8 *dst = gout + C;
+                    if (b0 == 0 && b1 == 16) {
+                        *(g_u4 *)dst = v;
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 16; ++b) {
+                            if (b >= b0 && b < b1) {
+                                const uint32_t x = b < 4 ? v.x : (b < 8 ? v.y : (b < 12 ? v.z : v.w));
+                                dst[b] = (uint8_t)(x >> (8 * (b & 3)));
+                            }
                         }
                     }
                 }
             }
         }
+        FK_STAMP(5)  // stores issued
         c_pkts += npkt;
         c_bytes += tile.span_len;
         c_edited += npkt - n_nosend;
+#if TE_FK_STAMPS
+        ++ntl;
+#endif
 #if !TE_FK_PREFETCH
         if (t + G < a.n_tiles) FK_ISSUE(cur);
 #endif
@@ -820,6 +890,11 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #undef FK_LD
 #undef FK_ST
 #undef FK_EACH
+#if TE_FK_STAMPS
+    if (tid == 0 && (blockIdx.x == 0 || blockIdx.x == 1 || blockIdx.x == 137 || blockIdx.x == gridDim.x - 1))
+        printf("stamps block %u tiles %llu: top %llu fill %llu phaseA %llu prefix %llu phaseB %llu store %llu\n",
+               blockIdx.x, ntl, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+#endif
     if (tid < TE_CNT__N) {  // fire-and-forget adds of the block's totals
         unsigned long long v = 0;
         if (tid == TE_CNT_PACKETS || tid == TE_CNT_WRITTEN) v = c_pkts;
@@ -925,7 +1000,9 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
         int fgrid = te_fast_grid();
         if (fgrid < 1) return -1;
         if ((uint32_t)fgrid > L->n_tiles) fgrid = (int)L->n_tiles;
+        if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
         hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
+        if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
         if (hipGetLastError() != hipSuccess) return -1;
         a.tile_list = L->tile_list;
         a.list_cnt = L->list_cnt + (L->parity & 1);
@@ -938,10 +1015,13 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     }
     int grid = L->grid > 0 ? L->grid : resident_blocks(L->slot_layout);
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
+    const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
+    if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
     if (L->slot_layout)
         hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
     else
         hipLaunchKernelGGL(te_edit_tiles<MODE_CONTIG>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    if (ev && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
 }

@@ -15,7 +15,12 @@ import statistics
 import sys
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-KERNEL = "te_edit_tiles"
+KERNEL = None  # the kernel with the largest total time in the trace stats
+
+
+def dominant_kernel(stats):
+    rows = [r for r in csv.DictReader(open(stats)) if r["Name"].startswith("te_")]
+    return max(rows, key=lambda r: float(r["TotalDurationNs"]))["Name"]
 
 
 def counter(path, name):
@@ -29,7 +34,9 @@ def main():
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
+    global KERNEL
     stats = os.path.join(src, f"prof_{rnd}_{wl}", "run_kernel_stats.csv")
+    KERNEL = dominant_kernel(stats)
     shutil.copy(stats, os.path.join(dst, f"{rnd}_{wl}_kernel_stats.csv"))
     fetch = counter(os.path.join(src, f"pmc_fetch_{rnd}_{wl}", "run_counter_collection.csv"), "FETCH_SIZE")
     write = counter(os.path.join(src, f"pmc_write_{rnd}_{wl}", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -37,7 +44,7 @@ def main():
     traffic = int(round((2 * f_kib + w_kib) * 1024))
     avg_ns = None
     for r in csv.DictReader(open(stats)):
-        if r["Name"].startswith(KERNEL):
+        if r["Name"] == KERNEL:
             avg_ns = float(r["AverageNs"])
     tj_path = os.path.join(dst, "traffic.json")
     tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
