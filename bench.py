@@ -164,7 +164,7 @@ def main():
         "gbps_algorithmic": round(alg_bytes * opt.steps * world / elapsed / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "te_fast_tiles" if r.fast_lane else "te_edit_tiles",
+                     "kernel": TA.FAST_KERNELS.get(r.fast_kind, "te_edit_tiles"),
                      "kernel_ms": round(kernel_ms, 5), "pipeline_ms": round(pipeline_ms, 5),
                      "alg_bytes_per_launch": alg_bytes},
     }

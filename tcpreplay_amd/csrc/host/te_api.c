@@ -46,10 +46,13 @@ struct tcpedit_batch_s {
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
     int slot_layout;
     int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
-    int fast_tiles;          /* tiles were cut for the fast lane (TE_FK_TILE_BYTES budget) */
+    int fast_tiles;          /* tiles were cut for the fast lane ... */
+    int fast_kind;           /* ... of this kind (TE_FAST_BLOCK / TE_FAST_WAVE budgets) */
     uint64_t launches;       /* parity selects the fast lane's tile-list count */
     int last_fast;           /* the last launch ran the fast lane ... */
     uint32_t last_listed;    /* ... and left this many tiles to the generic kernel */
+    int gen_hint_ok;         /* last_listed came from a run under config generation gen_hint_gen: */
+    uint32_t gen_hint_gen;   /* the generic kernel after the fast lane then launches that many blocks */
     hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
     int kev_n;
     /* device side */
@@ -76,6 +79,7 @@ struct tcpedit_batch_s {
 #define WS_COUNTERS1 128 /* counter set 1: the fast lane alternates sets by launch parity */
 #define WS_STATE 256
 #define WS_LIST_CNT(n_tiles) (WS_STATE + 8 * ((n_tiles) + 1))
+#define WS_SLOTS(n_tiles) ((WS_LIST_CNT(n_tiles) + 8 + 15) & ~(uint64_t)15) /* wave lane: 32 B per block */
 
 /* no edit step can change a record's length or drop it: efcs, VLAN add/del,
  * fixlen, MTU truncation and skipped soft errors are the only ways (plus
@@ -105,6 +109,14 @@ static int fast_v6_ok(const te_dev_cfg_t *c)
             if (lists[l][i].to.family == 6 && lists[l][i].to.masklen % 8)
                 return 0;
     return 1;
+}
+
+/* TCPEDIT_HIP_FAST_KIND=block selects te_fast_tiles (one block per tile) for A/B
+ * checks; the default is te_wave_tiles (one wave per tile) */
+static int fast_kind_pref(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_FAST_KIND");
+    return e && strcmp(e, "block") == 0 ? TE_FAST_BLOCK : TE_FAST_WAVE;
 }
 
 static uint32_t rd32(const uint8_t *p, int swapped)
@@ -138,8 +150,10 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
     const int slot_mode = pad || t->cfg.vlan == TE_VLAN_ADD;
     b->slot_layout = slot_mode;
     b->fast_tiles = !slot_mode && fast_capable(&t->cfg);
-    const uint32_t budget = b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
-    const uint32_t max_pkts = b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
+    b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
+    const int wave = b->fast_kind == TE_FAST_WAVE;
+    const uint32_t budget = wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
+    const uint32_t max_pkts = wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
     b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
@@ -175,7 +189,12 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
             huge = !TE_CONTIG_FITS_IN(g, 16 + caplen, budget);
             fits = open && TE_CONTIG_FITS_IN(cur.span_off & 15, off + 16 + caplen - cur.span_off, budget);
         }
-        if (open && (huge || cur.npkt >= max_pkts || !fits)) {
+        /* wave lane: a record too large for a wave image but not for the generic kernel's
+           LDS slot is a tile of its own, left to the generic kernel (no HBM scratch) */
+        const int solo = huge && wave && TE_CONTIG_FITS(g, 16 + caplen);
+        if (solo)
+            huge = 0;
+        if (open && (huge || solo || cur.npkt >= max_pkts || !fits)) {
             if (b->n_tiles == cap_tiles)
                 b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
             b->tiles[b->n_tiles++] = cur;
@@ -199,6 +218,12 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *img, siz
         if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
             cur.scratch_off = b->scratch_bytes;
             b->scratch_bytes += (slot + TE_LDS_FRONT + 64 + 255) & ~255u;
+            if (b->n_tiles == cap_tiles)
+                b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
+            b->tiles[b->n_tiles++] = cur;
+            open = 0;
+        } else if (solo) {
+            cur.flags |= TE_TILE_SOLO;
             if (b->n_tiles == cap_tiles)
                 b->tiles = realloc(b->tiles, sizeof(te_tile_t) * (cap_tiles *= 2));
             b->tiles[b->n_tiles++] = cur;
@@ -321,6 +346,7 @@ int te_upload_cfg(tcpedit_t *t)
     }
     HIPCHK(t, hipStreamSynchronize(t->stream));
     t->dev_dirty = 0;
+    t->cfg_gen++;
     return 0;
 fail:
     return -1;
@@ -355,7 +381,9 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->n_pkts + 1)));
     HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
                              t->stream));
-    b->ws_bytes = WS_LIST_CNT(b->n_tiles) + 64;
+    b->ws_bytes = WS_SLOTS(b->n_tiles) + 64;
+    if (b->fast_kind == TE_FAST_WAVE)
+        b->ws_bytes += 32 * (uint64_t)te_wave_grid();
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
     HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream)); /* the list count starts at 0 */
     if (b->fast_tiles)
@@ -429,6 +457,10 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.rec0 = 24;
     L.fast = L.static_off && b->fast_tiles && fast_capable(c) && !fast_lane_off();
     L.fast_v6 = fast_v6_ok(c);
+    L.fast_kind = b->fast_kind;
+    L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
+    if (L.fast && b->gen_hint_ok && b->gen_hint_gen == t->cfg_gen)
+        L.grid = b->last_listed ? (int)b->last_listed : 1; /* the generic kernel's grid after the fast lane */
     L.tile_list = b->d_tile_list;
     L.list_cnt = (uint32_t *)(b->d_ws + WS_LIST_CNT(b->n_tiles));
     L.parity = (uint32_t)(b->launches++ & 1);
@@ -464,6 +496,10 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(&b->last_listed, b->d_ws + WS_LIST_CNT(b->n_tiles) + 4 * ((b->launches - 1) & 1),
                                  sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    if (b->last_fast) { /* same batch + same config lists the same tiles next time */
+        b->gen_hint_ok = 1;
+        b->gen_hint_gen = t->cfg_gen;
+    }
     b->err[0] = ~b->err[0]; /* stored complemented (0 = no error -> ~0) */
     b->err[1] = ~b->err[1];
     HIPCHK(t, hipEventElapsedTime(&ms, b->ev0, b->ev1));
@@ -559,6 +595,7 @@ int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r)
     r->kernel_ms = b->kernel_ms;
     r->fast_lane = (uint32_t)b->last_fast;
     r->generic_tiles = b->last_fast ? b->last_listed : (uint32_t)b->n_tiles;
+    r->fast_kind = b->last_fast ? (uint32_t)b->fast_kind : 0;
     return TCPEDIT_OK;
 }
 

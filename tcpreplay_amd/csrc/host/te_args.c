@@ -489,6 +489,23 @@ static int requires_(tcpedit_t *t, int a, int b)
     return 0;
 }
 
+/* the LUT's non-identity entries, for the wave lane's LDS lookup (te_dev_cfg.h n_pm) */
+static void pm_sparse(tcpedit_t *t)
+{
+    te_dev_cfg_t *c = &t->cfg;
+    c->n_pm = 0;
+    for (int p = 0; t->portlut && p < 65536; p++) {
+        if (t->portlut[p] == p)
+            continue;
+        if (c->n_pm == TE_MAX_PM) {
+            c->n_pm = -1;
+            return;
+        }
+        c->pm_from[c->n_pm] = (uint16_t)p;
+        c->pm_to[c->n_pm++] = t->portlut[p];
+    }
+}
+
 int te_derive_cfg(tcpedit_t *t)
 {
     te_dev_cfg_t *c = &t->cfg;
@@ -623,6 +640,7 @@ int te_derive_cfg(tcpedit_t *t)
         free(set);
         free(ents);
         c->has_portmap = 1;
+        pm_sparse(t);
     }
     if (t->have[OPT_SEED]) { /* :218-238 */
         c->rewrite_ip = 1;
@@ -925,6 +943,7 @@ int tcpedit_set_port_map(tcpedit_t *t, char *s)
     free(set);
     free(ents);
     t->cfg.has_portmap = 1;
+    pm_sparse(t);
     t->dev_dirty = 1;
     return TCPEDIT_OK;
 }

@@ -62,6 +62,7 @@ struct tcpedit_s {
     te_dev_cfg_t *d_cfg;
     uint16_t *d_portlut;
     int dev_dirty;                /* cfg changed since last upload */
+    uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */
 };
 

@@ -14,6 +14,7 @@
 
 #define TE_MAX_CIDRMAP 16
 #define TE_MAX_SUBS 32
+#define TE_MAX_PM 64
 
 /* tcpr_cidr_t (src/common/cidr.h) */
 typedef struct {
@@ -63,6 +64,12 @@ typedef struct {
     uint32_t vlan_pri; /* 255 = unset */
     uint32_t vlan_cfi; /* 255 = unset */
     uint32_t vlan_proto;
+    /* the port map's non-identity LUT entries (index and value are the raw little-endian
+     * u16 of the network-order port), so the wave lane looks ports up in LDS; -1 when
+     * there are more than TE_MAX_PM of them (then the 64 Ki-entry LUT in HBM) */
+    int32_t n_pm;
+    uint16_t pm_from[TE_MAX_PM];
+    uint16_t pm_to[TE_MAX_PM];
 } te_dev_cfg_t;
 
 /* Per-packet status byte written by the device (one per input record). */

@@ -24,6 +24,16 @@ extern "C" {
 #ifndef TE_FK_BLOCK
 #define TE_FK_BLOCK 256        /* threads per fast-lane block = max records per fast-lane tile */
 #endif
+#ifndef TE_WK_TILE_BYTES
+#define TE_WK_TILE_BYTES 6144  /* wave-lane tile budget (one wave = one tile of <= 64 records) */
+#endif
+#ifndef TE_WK_BLOCK
+#define TE_WK_BLOCK 256        /* threads per wave-lane block (its waves share only the cfg copy) */
+#endif
+#define TE_WK_PKTS 64          /* records per wave-lane tile: one per lane */
+#define TE_TILE_SOLO 1u        /* te_tile_t.flags: a record too large for a wave-lane image */
+#define TE_FAST_BLOCK 1        /* fast-lane kinds: te_fast_tiles (one block per tile) ... */
+#define TE_FAST_WAVE 2         /* ... or te_wave_tiles (one wave per tile) */
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
@@ -44,7 +54,7 @@ typedef struct {
     uint32_t first_pkt;   /* index of the first record in this run */
     uint32_t npkt;
     uint32_t span_len;    /* bytes of records in the tile */
-    uint32_t pad_;
+    uint32_t flags;       /* TE_TILE_* */
 } te_tile_t;
 
 typedef struct {
@@ -78,6 +88,9 @@ typedef struct {
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
        only the listed tiles */
     int fast;
+    int fast_kind;            /* TE_FAST_BLOCK or TE_FAST_WAVE (how the tiles were cut) */
+    uint64_t *slots;          /* device: wave lane's per-block {packets, bytes, edited, -}, summed by
+                                 the generic kernel's block 0 into this launch's counters */
     int fast_v6;              /* IPv6 packets may take the fast lane (no non-octet v6 CIDR maps) */
     uint32_t *tile_list;      /* device: n_tiles entries */
     uint32_t *list_cnt;       /* device: 2 counts; launch parity p appends to [p] and zeroes [p^1] */
@@ -87,8 +100,9 @@ typedef struct {
     void *ev_k0, *ev_k1;      /* optional hipEvent_t pair recorded around the dominant edit kernel */
 } te_launch_t;
 
-/* blocks of te_fast_tiles resident on the current device */
+/* blocks of te_fast_tiles / te_wave_tiles resident on the current device */
 int te_fast_grid(void);
+int te_wave_grid(void);
 
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(const te_launch_t *L, hipStream_t stream);

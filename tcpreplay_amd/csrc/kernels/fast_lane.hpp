@@ -185,16 +185,30 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
 
     // ---- port map (rewrite_ports, portmap.c:267-330): destination, then source ----
     if (cfg.has_portmap) {
-        u32 oldp = hi16(L[0]), np = lut[oldp];
-        if (np != oldp) {
-            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)oldp, (u16)np);
-            L[0] = with_hi16(L[0], np);
+        const u32 od = hi16(L[0]), os = lo16(L[0]);
+        u32 nd = od, ns = os;
+        if (cfg.n_pm >= 0) {
+            // the map's few non-identity entries, from LDS (unique keys: at most one hit
+            // each).  A LUT load from HBM would wait behind the next tile's loads in flight.
+            for (int i = 0; i < cfg.n_pm; ++i) {
+                const u32 f = cfg.pm_from[i], to = cfg.pm_to[i];
+                nd = f == od ? to : nd;
+                ns = f == os ? to : ns;
+            }
+        } else {
+            nd = lut[od];
+            ns = lut[os];
+            // consume the loads here, so their wait stays on this path (a wait after the
+            // merge would also drain the next tile's loads on the LDS path)
+            asm volatile("" : "+v"(nd), "+v"(ns));
         }
-        oldp = lo16(L[0]);
-        np = lut[oldp];
-        if (np != oldp) {
-            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)oldp, (u16)np);
-            L[0] = with_lo16(L[0], np);
+        if (nd != od) {
+            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)od, (u16)nd);
+            L[0] = with_hi16(L[0], nd);
+        }
+        if (ns != os) {
+            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)os, (u16)ns);
+            L[0] = with_lo16(L[0], ns);
         }
     }
 

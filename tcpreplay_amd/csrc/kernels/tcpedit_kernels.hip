@@ -75,6 +75,10 @@ struct LaunchArgs {
     const uint32_t *tile_list;
     const uint32_t *list_cnt;        // this launch's count
     unsigned long long *counters_next;  // zeroed here for the next launch (fast lane parity)
+    // after te_wave_tiles: its per-block {packets, bytes, edited} totals, which block 0
+    // adds to `counters` (one atomic per counter instead of one per wave-lane block)
+    const unsigned long long *fast_slots;
+    uint32_t n_fast_slots;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -491,6 +495,31 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
     const bool listed = a.tile_list != nullptr;
     if (a.counters_next && blockIdx.x == 0 && threadIdx.x < TE_CNT__N) a.counters_next[threadIdx.x] = 0;
+    if (a.fast_slots && blockIdx.x == 0 && threadIdx.x < 64) {  // fold the wave lane's block totals
+        unsigned long long s0 = 0, s1 = 0, s2 = 0;
+        for (uint32_t i = threadIdx.x; i < a.n_fast_slots; i += 64) {
+            s0 += a.fast_slots[4 * i];
+            s1 += a.fast_slots[4 * i + 1];
+            s2 += a.fast_slots[4 * i + 2];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s0 += __shfl_xor(s0, o, 64);
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+        }
+        if (threadIdx.x == 0) {  // size-preserving: every record written, bytes out == bytes in
+            if (s0) {
+                atomicAdd(&a.counters[TE_CNT_PACKETS], s0);
+                atomicAdd(&a.counters[TE_CNT_WRITTEN], s0);
+            }
+            if (s1) {
+                atomicAdd(&a.counters[TE_CNT_BYTES_IN], s1);
+                atomicAdd(&a.counters[TE_CNT_BYTES_OUT], s1);
+            }
+            if (s2) atomicAdd(&a.counters[TE_CNT_EDITED], s2);
+        }
+    }
     const uint32_t n_work = listed ? *(const volatile uint32_t *)a.list_cnt : a.n_tiles;
     if (n_work == 0) return;  // after the fast lane, usually nothing is left
     {
@@ -562,6 +591,7 @@ struct FastArgs {
     uint32_t *list_cnt;  // this launch's count; list_cnt_next is zeroed for the next launch
     uint32_t *list_cnt_next;
     unsigned long long *counters;  // this launch's counter set (zeroed by the previous launch)
+    unsigned long long *slots;     // te_wave_tiles: per-block totals (4 words a block)
     unsigned long long *ws_zero;
     uint64_t out_base, rec0;
     uint32_t n_tiles;
@@ -904,6 +934,328 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
     }
 }
 
+// ===========================================================================
+// te_wave_tiles: the fast lane with one WAVE per tile -- at most 64
+// consecutive records whose span (plus the next record's header) fits
+// TE_WK_TILE_BYTES.  The waves of a block share only the cfg copy.  Each owns
+// an LDS image and a chunk-prefix array, streams its own span in, edits and
+// stores it, and never meets a workgroup barrier inside the tile loop: one
+// wave's LDS accesses are performed in order, so its write -> read hand-offs
+// need none.  Tiles are dealt statically (wave w of the grid takes w, w + W,
+// w + 2W, ...), and the next tile's span is in flight in registers while the
+// current one is edited and stored.
+//
+// Output (static offsets: output byte q sits at input byte q + out_base -
+// rec0, a multiple of 16): a tile stores the 16-byte chunks that START inside
+// its span, and its leading bytes (span start to the next 16-byte boundary)
+// one byte per lane.  Its last chunk carries at most 15 bytes of the next
+// tile, all inside that tile's first record header, which both waves compute
+// alike (for big-endian / nanosecond input the image then holds that whole
+// header and converts it too).  So no chunk needs bytes of two waves merged.
+// A tile the lane cannot finish (a deferred packet, or a record larger than
+// the image) stores nothing and is listed; the generic kernel, next on the
+// stream, writes its whole span byte-exactly.
+//
+// Every path that writes the next span into LDS has issued the same stores
+// since that span's loads (lanes past the span repeat a chunk or byte of it
+// instead of skipping the store), so the compiler's wait there can be partial:
+// it waits for the loads, not for this tile's stores.
+// ===========================================================================
+#ifndef TE_WK_MIN_BLOCKS
+#define TE_WK_MIN_BLOCKS 3  // blocks per CU (= waves per SIMD at 256 threads); 4 spills
+#endif
+#ifndef TE_WK_LANE_OPAQUE
+#define TE_WK_LANE_OPAQUE 1
+#endif
+constexpr int WKB = TE_WK_BLOCK;
+constexpr int WK_NW = WKB / 64;                          // waves (tiles in flight) per block
+constexpr int WK_KL = TE_WK_TILE_BYTES / 16 / 64;        // 16-byte chunks per lane per tile
+static_assert(TE_WK_TILE_BYTES % 1024 == 0 && WK_KL <= 8, "whole chunks per lane, <= 8 chunk registers");
+constexpr int WK_IMG = LDS_FRONT + TE_WK_TILE_BYTES + 128;  // image + phase-A window overrun
+constexpr int WK_NCH = TE_WK_TILE_BYTES / 16 + 2;           // chunk prefix (+ total)
+static_assert(WK_IMG % 16 == 0, "16-byte aligned wave images");
+
+__device__ __forceinline__ bool wk_solo(const te_tile_t &tl) {
+    return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH;
+}
+
+// big-endian / nanosecond input: a record header in host order and microseconds
+__device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
+    const uint32_t ts_sec = ld_hdr32(rec, swp), cl = ld_hdr32(rec + 8, swp), ln = ld_hdr32(rec + 12, swp);
+    uint32_t ts_frac = ld_hdr32(rec + 4, swp);
+    if (nsec) ts_frac /= 1000;
+    st32(rec, ts_sec);
+    st32(rec + 4, ts_frac);
+    st32(rec + 8, cl);
+    st32(rec + 12, ln);
+}
+
+__global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
+    __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
+    __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
+    __shared__ unsigned long long red[WK_NW][3];
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+    {
+        const uint32_t *src = (const uint32_t *)a.cfg;
+        uint32_t *dst = (uint32_t *)&cfg;
+        for (int i = tid; i < (int)(sizeof(te_dev_cfg_t) / 4); i += WKB) dst[i] = src[i];
+    }
+    if (blockIdx.x == 0) {
+        if (tid < 4) a.ws_zero[tid] = 0;  // the generic kernel's err words and ticket
+        if (tid == 4) *a.list_cnt_next = 0;
+    }
+    uint8_t *S = SB[wid];
+    uint32_t *P = PB[wid];
+    const bool swp = a.in_swapped != 0, nsec = a.in_nsec != 0, conv = swp || nsec;
+    const bool explicit_dir = a.fixed_dir >= 0;
+    const uint32_t extra = conv ? 16u : 0u;  // the next record's header rides along (conversion)
+    g_cu8 *gin = (g_cu8 *)a.in;
+    g_u8 *gout = (g_u8 *)a.out + ((int64_t)a.out_base - (int64_t)a.rec0);
+    const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
+    const TE_AS_CONST te_tile_t *tiles = (const TE_AS_CONST te_tile_t *)a.tiles;
+    const TE_AS_CONST uint16_t *pkt_rel = (const TE_AS_CONST uint16_t *)a.pkt_rel;
+    __syncthreads();
+
+    // the next tile's chunks in flight, in named registers
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+#define WK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define WK_LD(k)                                                           \
+    if constexpr (k < WK_KL) {                                             \
+        const uint32_t c = umin32((uint32_t)lane + k * 64u, nc_ - 1u);     \
+        v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));                 \
+    }
+#define WK_ISSUE(tl)                                                                                        \
+    {                                                                                                       \
+        const uint64_t a0_ = (tl).span_off & ~15ull;                                                        \
+        const uint32_t nc_ =                                                                                \
+            wk_solo(tl) ? 1u : (uint32_t)(((tl).span_off + (tl).span_len + extra - a0_ + 15) >> 4);         \
+        WK_EACH(WK_LD)                                                                                      \
+        const uint32_t k_ = (tl).first_pkt + umin32((uint32_t)lane, (tl).npkt - 1u);                       \
+        rel_next = pkt_rel[k_];                                                                             \
+        if (a.dirbits) { /* this lane's tcpprep cache byte, in flight with the span (no consumer */        \
+            const uint64_t ix_ = (a.pkt_base + k_) >> 2; /* here: its wait would drain the span) */        \
+            dirb_next = a.dirbits[ix_ < a.dirbits_len ? ix_ : 0];                                           \
+            dirv_next = ix_ < a.dirbits_len;                                                                \
+        }                                                                                                   \
+    }
+// the whole image, unconditionally: chunks past the span land past it (never read as data)
+#define WK_ST(k) \
+    if constexpr (k < WK_KL) *(uint4 *)(S + LDS_FRONT + (((uint32_t)lane + k * 64u) << 4)) = v##k;
+    const uint32_t W = gridDim.x * WK_NW;
+    const uint32_t w0 = blockIdx.x * WK_NW + wid;
+    te_tile_t cur, nxt;
+    uint32_t rel_next = 0;  // this lane's record offset in the tile whose chunks are in flight
+    uint32_t dirb_next = 0; // ... and its tcpprep cache byte
+    bool dirv_next = false; // (which exists: idx < dirbits_len)
+    if (w0 < a.n_tiles) {
+        cur = tiles[w0];
+        WK_ISSUE(cur);
+        WK_EACH(WK_ST)
+    }
+    if (w0 + W < a.n_tiles) nxt = tiles[w0 + W];
+    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
+    for (uint32_t t = w0; t < a.n_tiles; t += W) {
+#if TE_WK_LANE_OPAQUE
+        // lane-derived addresses are recomputed per tile instead of being hoisted out of
+        // the loop and kept (or spilled) across it
+        asm volatile("" : "+v"(lane));
+#endif
+        const te_tile_t tile = cur;
+        const uint32_t my_rel = rel_next, my_dirb = dirb_next;
+        const bool my_dirv = dirv_next;
+        const bool more = t + W < a.n_tiles;
+        cur = nxt;
+#if !TE_WK_ISSUE_LATE
+        if (more) WK_ISSUE(cur);  // in flight while this tile is edited and stored
+#endif
+        if (t + 2 * W < a.n_tiles) nxt = tiles[t + 2 * W];
+        const uint32_t npkt = tile.npkt;
+        const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
+        const uint32_t g0 = (uint32_t)(G0 - A0);
+        if (wk_solo(tile)) {  // a record larger than the image: the generic lane
+            if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+#if TE_WK_ISSUE_LATE
+            if (more) WK_ISSUE(cur);
+#endif
+            if (more) WK_EACH(WK_ST)
+            continue;
+        }
+
+        // ---- phase A: one lane per packet ----
+        const uint32_t r0 = LDS_FRONT + g0 + my_rel;  // record header in S
+        const uint32_t p = r0 + 16;                   // packet data in S
+        const uint32_t wa = p - 2;                    // window start (packet offset -2)
+        const bool on = lane < (int)npkt;
+        uint32_t H[fl::NW];
+        uint32_t d0 = 0, caplen = 0, len = 0;
+        fl::State st;
+        st.do_l4 = st.tail = false;
+        st.dirty = 0;
+        bool ok = true, nosend = false;
+        if (on) {
+            {  // caplen, len: three aligned dword reads + funnel shifts
+                const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
+                const uint32_t q0 = *(const uint32_t *)(S + ha), q1 = *(const uint32_t *)(S + ha + 4),
+                               q2 = *(const uint32_t *)(S + ha + 8);
+                caplen = __builtin_amdgcn_alignbyte(q1, q0, hs);
+                len = __builtin_amdgcn_alignbyte(q2, q1, hs);
+                if (swp) {
+                    caplen = bswap32(caplen);
+                    len = bswap32(len);
+                }
+            }
+            const uint64_t pktno = a.pkt_base + tile.first_pkt + lane;
+            int dir = TE_DIR_C2S;
+            if (explicit_dir) {
+                dir = a.fixed_dir;
+            } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354), byte loaded with the span
+                const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+                const uint32_t b = my_dirv ? my_dirb : 0u;
+                dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+            }
+            if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
+                nosend = true;
+            } else {
+                const uint32_t A8 = wa & ~7u, s8 = wa & 7u, sh = s8 & 3u;
+                uint32_t d[fl::NW + 2];
+#pragma unroll
+                for (int j = 0; j < fl::NW + 2; j += 2) {
+                    const uint2 q = *(const uint2 *)(S + A8 + 4 * j);
+                    d[j] = q.x;
+                    d[j + 1] = q.y;
+                }
+                const uint32_t mh = s8 >= 4 ? 0xffffffffu : 0u;
+                uint32_t e[fl::NW + 1];
+#pragma unroll
+                for (int j = 0; j <= fl::NW; ++j) e[j] = (d[j + 1] & mh) | (d[j] & ~mh);
+#pragma unroll
+                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
+                d0 = e[0];
+#if TE_WK_CFG_OPAQUE
+                // cfg fields are re-read from LDS per tile, not hoisted into registers
+                typedef __attribute__((address_space(3))) const te_dev_cfg_t lds_cfg_t;
+                lds_cfg_t *cp = (lds_cfg_t *)&cfg;
+                asm volatile("" : "+v"(cp));
+                ok = fl::phase_a(H, caplen, len, dir, *(const te_dev_cfg_t *)cp, a.v6_ok != 0, lut, st);
+#else
+                ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
+#endif
+            }
+        }
+#if TE_WK_ISSUE_LATE
+        if (more) WK_ISSUE(cur);  // in flight while this tile is finished and stored
+#endif
+        if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
+            if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+            if (more) WK_EACH(WK_ST)
+            continue;
+        }
+
+        // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
+        if (__ballot(st.tail)) {
+            const uint32_t nch = (LDS_FRONT + g0 + tile.span_len + 15) >> 4;  // <= 64 * WK_KL
+            uint32_t loc[WK_KL], tot = 0;
+#pragma unroll
+            for (int q = 0; q < WK_KL; ++q) {  // lane owns chunks [lane * KL, lane * KL + KL)
+                const uint32_t c = (uint32_t)lane * WK_KL + q;
+                uint32_t s = 0;
+                if (c < nch) {
+                    const uint4 v = *(const uint4 *)(S + 16 * c);
+                    s = fl::wsum(v.x) + fl::wsum(v.y) + fl::wsum(v.z) + fl::wsum(v.w);
+                }
+                loc[q] = tot;
+                tot += s;
+            }
+            uint32_t incl = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t base = incl - tot;
+#pragma unroll
+            for (int q = 0; q < WK_KL; ++q) {
+                const uint32_t c = (uint32_t)lane * WK_KL + q;
+                if (c < nch) P[c] = base + loc[q];
+            }
+            if (lane == 63) P[nch] = incl;
+        }
+
+        // ---- phase B + write-back of the dwords phase A touched ----
+        if (on) {
+            if (!nosend) {
+                uint32_t tail = 0;
+                if (st.tail) {
+                    tail = lds_range_sum(S, P, p + fl::WEND, p + st.end);
+                    if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
+                }
+                fl::phase_b(H, st, tail);
+                const uint32_t A = wa & ~3u, sh = wa & 3u;
+                const uint32_t need = st.dirty | (sh ? (st.dirty << 1) : 0u);
+#pragma unroll
+                for (int j = 0; j < fl::NW; ++j) {
+                    if (!((need >> j) & 1u)) continue;
+                    const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
+                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
+                    const int rel = (int)(A + 4 * j) - (int)p;
+                    uint8_t *q = S + A + 4 * j;
+                    if (rel + 4 <= (int)caplen) {
+                        *(uint32_t *)q = v;
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 3; ++b)
+                            if (rel + b < (int)caplen) q[b] = (uint8_t)(v >> (8 * b));
+                    }
+                }
+            }
+            if (conv) conv_hdr(S + r0, swp, nsec);
+            ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
+        }
+        if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
+
+        // ---- store: the chunks that start in the span, then the leading bytes ----
+        {
+            const uint64_t C0 = (G0 + 15) & ~15ull;
+            const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
+            const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
+            uint4 w[WK_KL];
+#pragma unroll
+            for (int k = 0; k < WK_KL; ++k)
+                w[k] = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
+#pragma unroll
+            for (int k = 0; k < WK_KL; ++k)  // lanes past the span repeat its last chunk (same bytes)
+                *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w[k];
+            const uint32_t nlead = (uint32_t)(C0 - G0);
+            const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
+            gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
+        }
+        if (more) WK_EACH(WK_ST)
+        const uint32_t n_nosend = (uint32_t)__popcll(__ballot(nosend));
+        c_pkts += npkt;
+        c_bytes += tile.span_len;
+        c_edited += npkt - n_nosend;
+    }
+#undef WK_ISSUE
+#undef WK_LD
+#undef WK_ST
+#undef WK_EACH
+    if (lane == 0) {
+        red[wid][0] = c_pkts;
+        red[wid][1] = c_bytes;
+        red[wid][2] = c_edited;
+    }
+    __syncthreads();
+    if (tid < 3) {  // this block's totals; the generic kernel's block 0 adds them up
+        unsigned long long s = 0;
+#pragma unroll
+        for (int w = 0; w < WK_NW; ++w) s += red[w][tid];
+        a.slots[4 * blockIdx.x + tid] = s;
+    }
+}
+
 }  // namespace
 
 // persistent grid = the blocks that are resident at once (CUs x occupancy)
@@ -940,6 +1292,17 @@ extern "C" int te_fast_grid(void) {
     return c;
 }
 
+extern "C" int te_wave_grid(void) {
+    static int c = 0;
+    if (c) return c;
+    int cus = cu_count(), per_cu = 0;
+    if (!cus) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles, WKB, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    c = cus * per_cu;
+    return c;
+}
+
 // ---------------------------------------------------------------------------
 // C-ABI launch wrapper (called from the C host code, no torch types)
 // ---------------------------------------------------------------------------
@@ -970,6 +1333,8 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
+    a.fast_slots = nullptr;
+    a.n_fast_slots = 0;
     hipError_t e;
     const bool fast = L->fast && L->static_off && !L->slot_layout && L->n_tiles > 0;
     if (fast) {
@@ -997,23 +1362,38 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
         f.in_swapped = L->in_swapped;
         f.in_nsec = L->in_nsec;
         f.v6_ok = (uint32_t)L->fast_v6;
-        int fgrid = te_fast_grid();
+        f.slots = (unsigned long long *)L->slots;
+        const bool wave = L->fast_kind == TE_FAST_WAVE;
+        int fgrid = wave ? te_wave_grid() : te_fast_grid();
         if (fgrid < 1) return -1;
-        if ((uint32_t)fgrid > L->n_tiles) fgrid = (int)L->n_tiles;
+        const uint32_t need = wave ? (L->n_tiles + WK_NW - 1) / WK_NW : L->n_tiles;
+        if ((uint32_t)fgrid > need) fgrid = (int)need;
+        if (wave && (!L->slots || ((L->out_base - L->rec0) & 15)))
+            return -1;  // the wave lane stores whole 16-byte chunks at input offsets + a multiple of 16
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
-        hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
+        if (wave)
+            hipLaunchKernelGGL(te_wave_tiles, dim3(fgrid), dim3(WKB), 0, stream, f);
+        else
+            hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
         if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
         if (hipGetLastError() != hipSuccess) return -1;
         a.tile_list = L->tile_list;
         a.list_cnt = L->list_cnt + (L->parity & 1);
         a.counters_next = (unsigned long long *)L->counters_next;
+        if (wave) {
+            a.fast_slots = (const unsigned long long *)L->slots;
+            a.n_fast_slots = (uint32_t)fgrid;
+        }
     } else {
         // one memset per launch: error words, ticket, counters, look-back granules
         e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);
         if (e != hipSuccess) return -1;
         if (L->n_tiles == 0) return 0;
     }
-    int grid = L->grid > 0 ? L->grid : resident_blocks(L->slot_layout);
+    // after the fast lane the host may pass a smaller grid (the tiles the previous run of
+    // this batch listed): the loop below takes tickets, so any grid >= 1 edits every tile
+    const int res = resident_blocks(L->slot_layout);
+    int grid = L->grid > 0 && L->grid < res ? L->grid : res;
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
