@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--extra", default="c3,c5", help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
     ap.add_argument("--verify", action="store_true", help="compare the first run with the oracle")
     opt = ap.parse_args()
 
@@ -188,20 +189,21 @@ def main():
             te2.close()
         if extra:
             result["extra_configs"] = extra
-        # PCIe-inclusive rate (never `value`): host pcap bytes -> H2D -> index upload
-        # -> kernel -> D2H -> host bytes, through tcpedit_rewrite_pcap's batch path
-        te3 = TA.TcpEdit(WORKLOADS[opt.workload][2], device=0)
-        e2e = []
-        for _ in range(3):
-            t1 = time.perf_counter()
-            rc3, _out = te3.rewrite(pcap)
-            e2e.append(time.perf_counter() - t1)
-        te3.close()
-        e2e_s = sorted(e2e)[1]
-        result["end_to_end"] = {"mpkt_s": round(n / e2e_s / 1e6, 2), "ms": round(e2e_s * 1e3, 3),
-                                "gbps_in": round(len(pcap) / e2e_s / 1e9, 2),
-                                "path": "host bytes -> hipMemcpy H2D -> kernel -> D2H -> host bytes "
-                                        "(median of 3, includes device allocation and record indexing)"}
+        if not opt.no_e2e:
+            # PCIe-inclusive rate (never `value`): host pcap bytes -> H2D -> index upload
+            # -> kernel -> D2H -> host bytes, through tcpedit_rewrite_pcap's batch path
+            te3 = TA.TcpEdit(WORKLOADS[opt.workload][2], device=0)
+            e2e = []
+            for _ in range(3):
+                t1 = time.perf_counter()
+                rc3, _out = te3.rewrite(pcap)
+                e2e.append(time.perf_counter() - t1)
+            te3.close()
+            e2e_s = sorted(e2e)[1]
+            result["end_to_end"] = {"mpkt_s": round(n / e2e_s / 1e6, 2), "ms": round(e2e_s * 1e3, 3),
+                                    "gbps_in": round(len(pcap) / e2e_s / 1e9, 2),
+                                    "path": "host bytes -> hipMemcpy H2D -> kernel -> D2H -> host bytes "
+                                            "(median of 3, includes device allocation and record indexing)"}
         if not opt.no_cpu_baseline:
             v, runs, el = cpu_baseline(pcap, WORKLOADS[opt.workload][2], n, opt.cpu_seconds)
             result["cpu_baseline"] = {"value": round(v, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",

@@ -52,7 +52,10 @@ struct tcpedit_batch_s {
     int last_fast;           /* the last launch ran the fast lane ... */
     uint32_t last_listed;    /* ... and left this many tiles to the generic kernel */
     int gen_hint_ok;         /* last_listed came from a run under config generation gen_hint_gen: */
-    uint32_t gen_hint_gen;   /* the generic kernel after the fast lane then launches that many blocks */
+    uint32_t gen_hint_gen;   /* the generic pass after the wave lane then runs on that many blocks, or not at all */
+    int last_skipped;        /* the last launch left the generic pass out */
+    int last_fgrid;          /* blocks of the last wave-lane launch (slots it wrote) */
+    uint64_t *slots_host;    /* their {packets, bytes, edited, -} totals, read back after a run */
     hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
     int kev_n;
     /* device side */
@@ -273,6 +276,7 @@ void tcpedit_batch_close(tcpedit_batch_t *b)
     for (int i = 0; i < b->kev_n; i++)
         hipEventDestroy(b->kev[i]);
     free(b->kev);
+    free(b->slots_host);
     free(b->tiles);
     free(b->pkt_rel);
     free(b->status);
@@ -414,13 +418,15 @@ static int fast_lane_off(void)
     return e && *e && *e != '0';
 }
 
-static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1);
+static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1, int generic_only);
 static int launch(tcpedit_batch_t *b, int fixed_dir)
 {
-    return launch_ev(b, fixed_dir, NULL, NULL);
+    return launch_ev(b, fixed_dir, NULL, NULL, 0);
 }
 
-static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1)
+/* generic_only: the generic pass over what the last (wave-lane) launch listed, under
+ * that launch's parity -- for a run whose generic pass was left out by the hint */
+static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1, int generic_only)
 {
     tcpedit_t *t = b->ctx;
     te_launch_t L;
@@ -463,7 +469,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.grid = b->last_listed ? (int)b->last_listed : 1; /* the generic kernel's grid after the fast lane */
     L.tile_list = b->d_tile_list;
     L.list_cnt = (uint32_t *)(b->d_ws + WS_LIST_CNT(b->n_tiles));
-    L.parity = (uint32_t)(b->launches++ & 1);
+    L.parity = (uint32_t)(generic_only ? (b->launches - 1) & 1 : b->launches++ & 1);
     b->last_fast = L.fast;
     b->last_cnt_off = L.fast && L.parity ? WS_COUNTERS1 : WS_COUNTERS;
     L.counters = (uint64_t *)(b->d_ws + b->last_cnt_off);
@@ -471,7 +477,19 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.ws_zero = (uint64_t *)(b->d_ws + WS_ZERO);
     L.ev_k0 = k0;
     L.ev_k1 = k1;
-    return te_launch_edit(&L, t->stream);
+    L.generic_only = generic_only;
+    /* wave lane: this batch's previous run under this config listed nothing, so the
+       generic pass is left out (batch_run_dir runs it after all if a run does list) */
+    L.skip_generic = !generic_only && L.fast && b->fast_kind == TE_FAST_WAVE && b->gen_hint_ok &&
+                     b->gen_hint_gen == t->cfg_gen && b->last_listed == 0;
+    if (generic_only)
+        L.grid = b->last_listed ? (int)b->last_listed : 1;
+    const int rc = te_launch_edit(&L, t->stream);
+    if (!generic_only) {
+        b->last_skipped = L.skip_generic;
+        b->last_fgrid = L.fast && b->fast_kind == TE_FAST_WAVE ? L.out_fgrid : 0;
+    }
+    return rc;
 }
 
 static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
@@ -495,7 +513,34 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
     if (b->last_fast)
         HIPCHK(t, hipMemcpyAsync(&b->last_listed, b->d_ws + WS_LIST_CNT(b->n_tiles) + 4 * ((b->launches - 1) & 1),
                                  sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+    if (b->last_fgrid) {
+        if (!b->slots_host)
+            b->slots_host = malloc(32 * (size_t)te_wave_grid());
+        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
+                                 hipMemcpyDeviceToHost, t->stream));
+    }
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    if (b->last_fast && b->last_skipped && b->last_listed) {
+        /* the hint was wrong (it cannot be for the same image and config): run the
+           generic pass now and read the counters and error words again */
+        if (launch_ev(b, fixed_dir, NULL, NULL, 1) != 0) {
+            te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return TCPEDIT_ERROR;
+        }
+        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+        b->last_skipped = 0;
+    }
+    for (int i = 0; i < b->last_fgrid; i++) { /* the wave lane's per-block totals */
+        const uint64_t *v = b->slots_host + 4 * (size_t)i;
+        b->counters[TE_CNT_PACKETS] += v[0];
+        b->counters[TE_CNT_WRITTEN] += v[0];
+        b->counters[TE_CNT_BYTES_IN] += v[1];
+        b->counters[TE_CNT_BYTES_OUT] += v[1];
+        b->counters[TE_CNT_EDITED] += v[2];
+    }
     if (b->last_fast) { /* same batch + same config lists the same tiles next time */
         b->gen_hint_ok = 1;
         b->gen_hint_gen = t->cfg_gen;
@@ -659,7 +704,7 @@ int tcpedit_batch_time_kernels(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
     HIPCHK(t, hipEventCreate(&e1));
     HIPCHK(t, hipEventRecord(e0, t->stream));
     for (int i = 0; i < iters; i++)
-        if (launch_ev(b, -1, b->kev[2 * i], b->kev[2 * i + 1]) != 0) {
+        if (launch_ev(b, -1, b->kev[2 * i], b->kev[2 * i + 1], 0) != 0) {
             te_seterr(t, "kernel launch failed");
             goto fail;
         }

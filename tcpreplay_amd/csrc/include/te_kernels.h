@@ -89,8 +89,11 @@ typedef struct {
        only the listed tiles */
     int fast;
     int fast_kind;            /* TE_FAST_BLOCK or TE_FAST_WAVE (how the tiles were cut) */
-    uint64_t *slots;          /* device: wave lane's per-block {packets, bytes, edited, -}, summed by
-                                 the generic kernel's block 0 into this launch's counters */
+    uint64_t *slots;          /* device: wave lane's per-block {packets, bytes, edited, -}; the host
+                                 adds them to this launch's counters */
+    int skip_generic;         /* wave lane: leave out the generic pass (no tile will be listed) */
+    int generic_only;         /* run only the generic pass over the tiles the last fast launch listed */
+    int out_fgrid;            /* set by te_launch_edit: blocks of the fast-lane launch (slots written) */
     int fast_v6;              /* IPv6 packets may take the fast lane (no non-octet v6 CIDR maps) */
     uint32_t *tile_list;      /* device: n_tiles entries */
     uint32_t *list_cnt;       /* device: 2 counts; launch parity p appends to [p] and zeroes [p^1] */
@@ -105,7 +108,7 @@ int te_fast_grid(void);
 int te_wave_grid(void);
 
 #ifdef __HIP_PLATFORM_AMD__
-int te_launch_edit(const te_launch_t *L, hipStream_t stream);
+int te_launch_edit(te_launch_t *L, hipStream_t stream);
 #endif
 
 #ifdef __cplusplus

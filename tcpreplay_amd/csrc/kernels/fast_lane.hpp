@@ -375,13 +375,18 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
             for (int i = 6; i < 14; ++i) sum += wsum(H[i]);
         }
         sum += bs16((tcp ? 6u : 17u) + l4len);
-        // L4 bytes [L4S, min(caplen, WEND)) inside the window
-        const int base = v6 ? 14 : 9;
+        // L4 bytes [L4S, min(caplen, WEND)) inside the window, summed as whole dwords: a
+        // dword's 32-bit value folds to the same one's-complement sum as its two 16-bit
+        // halves (2^16 == 1 mod 0xffff), and 11 of them stay far below 2^48
+        unsigned long long s64 = 0;
 #pragma unroll
         for (int i = 9; i < NW; ++i) {
-            const u32 m = i >= base ? bmask(0, (int)caplen - (4 * i - 2)) : 0u;
-            sum += wsum(H[i] & m);
+            const int rem = (int)caplen - (4 * i - 2);  // packet bytes in dword i
+            const int r = rem < 0 ? 0 : (rem > 4 ? 4 : rem);
+            const u32 keep = r == 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
+            s64 += H[i] & ((i >= 14 || !v6) ? keep : 0u);
         }
+        sum += (u32)((s64 & 0xffffull) + (s64 >> 16));  // < 2^16 + 2^20
     }
     if (!v6) {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
         H[6] = with_hi16(H[6], 0);

@@ -75,10 +75,6 @@ struct LaunchArgs {
     const uint32_t *tile_list;
     const uint32_t *list_cnt;        // this launch's count
     unsigned long long *counters_next;  // zeroed here for the next launch (fast lane parity)
-    // after te_wave_tiles: its per-block {packets, bytes, edited} totals, which block 0
-    // adds to `counters` (one atomic per counter instead of one per wave-lane block)
-    const unsigned long long *fast_slots;
-    uint32_t n_fast_slots;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -495,31 +491,6 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
     const bool listed = a.tile_list != nullptr;
     if (a.counters_next && blockIdx.x == 0 && threadIdx.x < TE_CNT__N) a.counters_next[threadIdx.x] = 0;
-    if (a.fast_slots && blockIdx.x == 0 && threadIdx.x < 64) {  // fold the wave lane's block totals
-        unsigned long long s0 = 0, s1 = 0, s2 = 0;
-        for (uint32_t i = threadIdx.x; i < a.n_fast_slots; i += 64) {
-            s0 += a.fast_slots[4 * i];
-            s1 += a.fast_slots[4 * i + 1];
-            s2 += a.fast_slots[4 * i + 2];
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            s0 += __shfl_xor(s0, o, 64);
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-        }
-        if (threadIdx.x == 0) {  // size-preserving: every record written, bytes out == bytes in
-            if (s0) {
-                atomicAdd(&a.counters[TE_CNT_PACKETS], s0);
-                atomicAdd(&a.counters[TE_CNT_WRITTEN], s0);
-            }
-            if (s1) {
-                atomicAdd(&a.counters[TE_CNT_BYTES_IN], s1);
-                atomicAdd(&a.counters[TE_CNT_BYTES_OUT], s1);
-            }
-            if (s2) atomicAdd(&a.counters[TE_CNT_EDITED], s2);
-        }
-    }
     const uint32_t n_work = listed ? *(const volatile uint32_t *)a.list_cnt : a.n_tiles;
     if (n_work == 0) return;  // after the fast lane, usually nothing is left
     {
@@ -591,7 +562,8 @@ struct FastArgs {
     uint32_t *list_cnt;  // this launch's count; list_cnt_next is zeroed for the next launch
     uint32_t *list_cnt_next;
     unsigned long long *counters;  // this launch's counter set (zeroed by the previous launch)
-    unsigned long long *slots;     // te_wave_tiles: per-block totals (4 words a block)
+    unsigned long long *slots;     // te_wave_tiles: per-block totals (4 words a block), summed by the host
+    unsigned long long *counters_next;  // te_wave_tiles: the other parity's counter set, zeroed for the next launch
     unsigned long long *ws_zero;
     uint64_t out_base, rec0;
     uint32_t n_tiles;
@@ -962,7 +934,7 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 // it waits for the loads, not for this tile's stores.
 // ===========================================================================
 #ifndef TE_WK_MIN_BLOCKS
-#define TE_WK_MIN_BLOCKS 3  // blocks per CU (= waves per SIMD at 256 threads); 4 spills
+#define TE_WK_MIN_BLOCKS 4  // blocks per CU (= waves per SIMD at 256 threads): 128 VGPRs
 #endif
 #ifndef TE_WK_LANE_OPAQUE
 #define TE_WK_LANE_OPAQUE 1
@@ -974,6 +946,21 @@ static_assert(TE_WK_TILE_BYTES % 1024 == 0 && WK_KL <= 8, "whole chunks per lane
 constexpr int WK_IMG = LDS_FRONT + TE_WK_TILE_BYTES + 128;  // image + phase-A window overrun
 constexpr int WK_NCH = TE_WK_TILE_BYTES / 16 + 2;           // chunk prefix (+ total)
 static_assert(WK_IMG % 16 == 0, "16-byte aligned wave images");
+
+// TE_WK_STAMPS builds (diagnostics only): s_memtime per phase, summed per wave,
+// printed by a few waves at exit
+#if TE_WK_STAMPS
+#define WK_STAMP(i)                                                        \
+    {                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        ph[i] += now_ - last_;                                             \
+        last_ = now_;                                                      \
+    }
+#else
+#define WK_STAMP(i)
+#endif
 
 __device__ __forceinline__ bool wk_solo(const te_tile_t &tl) {
     return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH;
@@ -1006,6 +993,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     if (blockIdx.x == 0) {
         if (tid < 4) a.ws_zero[tid] = 0;  // the generic kernel's err words and ticket
         if (tid == 4) *a.list_cnt_next = 0;
+        if (tid >= 8 && tid < 8 + TE_CNT__N) a.counters_next[tid - 8] = 0;  // (the generic pass may not run)
     }
     uint8_t *S = SB[wid];
     uint32_t *P = PB[wid];
@@ -1057,6 +1045,9 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     }
     if (w0 + W < a.n_tiles) nxt = tiles[w0 + W];
     unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
+#if TE_WK_STAMPS
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
+#endif
     for (uint32_t t = w0; t < a.n_tiles; t += W) {
 #if TE_WK_LANE_OPAQUE
         // lane-derived addresses are recomputed per tile instead of being hoisted out of
@@ -1072,6 +1063,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
         if (more) WK_ISSUE(cur);  // in flight while this tile is edited and stored
 #endif
         if (t + 2 * W < a.n_tiles) nxt = tiles[t + 2 * W];
+        WK_STAMP(0)  // loop top + next tile's loads issued
         const uint32_t npkt = tile.npkt;
         const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
         const uint32_t g0 = (uint32_t)(G0 - A0);
@@ -1119,21 +1111,15 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
                 nosend = true;
             } else {
-                const uint32_t A8 = wa & ~7u, s8 = wa & 7u, sh = s8 & 3u;
-                uint32_t d[fl::NW + 2];
+                // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
+                // the window to packet offset -2; each H[i] can take d[i]'s register
+                const uint32_t A4 = wa & ~3u, sh = wa & 3u;
+                uint32_t d[fl::NW + 1];
 #pragma unroll
-                for (int j = 0; j < fl::NW + 2; j += 2) {
-                    const uint2 q = *(const uint2 *)(S + A8 + 4 * j);
-                    d[j] = q.x;
-                    d[j + 1] = q.y;
-                }
-                const uint32_t mh = s8 >= 4 ? 0xffffffffu : 0u;
-                uint32_t e[fl::NW + 1];
+                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
 #pragma unroll
-                for (int j = 0; j <= fl::NW; ++j) e[j] = (d[j + 1] & mh) | (d[j] & ~mh);
-#pragma unroll
-                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
-                d0 = e[0];
+                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                d0 = d[0];
 #if TE_WK_CFG_OPAQUE
                 // cfg fields are re-read from LDS per tile, not hoisted into registers
                 typedef __attribute__((address_space(3))) const te_dev_cfg_t lds_cfg_t;
@@ -1154,6 +1140,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             continue;
         }
 
+        WK_STAMP(1)  // phase A
         // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
         if (__ballot(st.tail)) {
             const uint32_t nch = (LDS_FRONT + g0 + tile.span_len + 15) >> 4;  // <= 64 * WK_KL
@@ -1184,6 +1171,15 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             if (lane == 63) P[nch] = incl;
         }
 
+        WK_STAMP(2)  // chunk prefix
+        // LDS dwords any lane writes back, as one wave-uniform mask: the per-dword tests
+        // below are scalar branches.  A lane that did not change such a dword rewrites
+        // it with its own packet's bytes (never past caplen), which is harmless.
+        uint32_t todo = 0;
+        if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) todo |= __shfl_xor(todo, o, 64);
+        todo = __builtin_amdgcn_readfirstlane(todo);
         // ---- phase B + write-back of the dwords phase A touched ----
         if (on) {
             if (!nosend) {
@@ -1194,10 +1190,9 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
                 }
                 fl::phase_b(H, st, tail);
                 const uint32_t A = wa & ~3u, sh = wa & 3u;
-                const uint32_t need = st.dirty | (sh ? (st.dirty << 1) : 0u);
 #pragma unroll
                 for (int j = 0; j < fl::NW; ++j) {
-                    if (!((need >> j) & 1u)) continue;
+                    if (!((todo >> j) & 1u)) continue;
                     const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
                     const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
                     const int rel = (int)(A + 4 * j) - (int)p;
@@ -1216,6 +1211,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
         }
         if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
 
+        WK_STAMP(3)  // phase B
         // ---- store: the chunks that start in the span, then the leading bytes ----
         {
             const uint64_t C0 = (G0 + 15) & ~15ull;
@@ -1232,7 +1228,12 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
             gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
         }
+        WK_STAMP(4)  // stores issued
         if (more) WK_EACH(WK_ST)
+        WK_STAMP(5)  // next span -> LDS (waits for its loads)
+#if TE_WK_STAMPS
+        ++ntl;
+#endif
         const uint32_t n_nosend = (uint32_t)__popcll(__ballot(nosend));
         c_pkts += npkt;
         c_bytes += tile.span_len;
@@ -1242,6 +1243,11 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
 #undef WK_LD
 #undef WK_ST
 #undef WK_EACH
+#if TE_WK_STAMPS
+    if (lane == 0 && wid == 0 && (blockIdx.x % 128) == 0)
+        printf("wstamps block %u tiles %llu: top %llu phaseA %llu prefix %llu phaseB %llu store %llu fill %llu\n",
+               blockIdx.x, ntl, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+#endif
     if (lane == 0) {
         red[wid][0] = c_pkts;
         red[wid][1] = c_bytes;
@@ -1306,7 +1312,7 @@ extern "C" int te_wave_grid(void) {
 // ---------------------------------------------------------------------------
 // C-ABI launch wrapper (called from the C host code, no torch types)
 // ---------------------------------------------------------------------------
-extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
+extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     a.cfg = L->cfg;
     a.portlut = L->portlut;
@@ -1333,11 +1339,9 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
-    a.fast_slots = nullptr;
-    a.n_fast_slots = 0;
     hipError_t e;
     const bool fast = L->fast && L->static_off && !L->slot_layout && L->n_tiles > 0;
-    if (fast) {
+    if (fast && !L->generic_only) {
         // the fast kernel zeroes the generic kernel's words itself: no memset launch
         FastArgs f;
         f.cfg = L->cfg;
@@ -1363,6 +1367,7 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
         f.in_nsec = L->in_nsec;
         f.v6_ok = (uint32_t)L->fast_v6;
         f.slots = (unsigned long long *)L->slots;
+        f.counters_next = (unsigned long long *)L->counters_next;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
         int fgrid = wave ? te_wave_grid() : te_fast_grid();
         if (fgrid < 1) return -1;
@@ -1377,13 +1382,15 @@ extern "C" int te_launch_edit(const te_launch_t *L, hipStream_t stream) {
             hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
         if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
         if (hipGetLastError() != hipSuccess) return -1;
+        L->out_fgrid = fgrid;
+        // after the wave lane the host leaves the generic pass out when this batch's
+        // previous run listed no tile (and runs it, generic_only, if a run ever does)
+        if (L->skip_generic) return 0;
+    }
+    if (fast) {  // the generic kernel redoes only the tiles the fast lane listed
         a.tile_list = L->tile_list;
         a.list_cnt = L->list_cnt + (L->parity & 1);
         a.counters_next = (unsigned long long *)L->counters_next;
-        if (wave) {
-            a.fast_slots = (const unsigned long long *)L->slots;
-            a.n_fast_slots = (uint32_t)fgrid;
-        }
     } else {
         // one memset per launch: error words, ticket, counters, look-back granules
         e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);

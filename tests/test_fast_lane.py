@@ -149,3 +149,29 @@ def test_fast_lane_baseline_configs(built):
         rc, out, r = run(pcap, args)
         assert r.fast_lane == 1 and r.generic_tiles == 0
         assert rc == rc_o == 0 and out == exp
+
+
+@pytest.mark.parametrize("near_miss", [0.0, 0.3])
+def test_repeat_runs_keep_output_and_counters(built, near_miss):
+    """Runs after the first reuse its plan (the generic pass is left out when nothing was
+    listed): output, counters and status must not change from run to run."""
+    pcap = F.build(F.mixed(3000, seed=21, near_miss=near_miss))
+    args = ["--seed=8", "--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=80:8080", "--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args)
+    te = TA.TcpEdit(args)
+    b = TA.Batch(te, pcap)
+    try:
+        seen = []
+        for k in range(4):
+            if k == 2:
+                b.time(3)  # timed runs in between
+            assert b.run() == rc_o
+            r = b.result()
+            seen.append((b.output(), r.packets, r.bytes_in, r.bytes_out, r.written, r.edited, r.generic_tiles,
+                         b.status().tobytes()))
+        assert seen[0][0] == exp
+        assert all(s == seen[0] for s in seen[1:])
+        assert (seen[0][6] == 0) == (near_miss == 0.0)
+    finally:
+        b.close()
+        te.close()
