@@ -143,6 +143,18 @@ uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b);
 int tcpedit_rewrite_pcap(tcpedit_t *tcpedit, const void *in, size_t in_len, const void *cache, size_t cache_len,
                          void **out, size_t *out_len);
 
+/* Pipelined whole-image rewrite into a caller buffer of out_cap >= tcpedit_output_bound()
+ * bytes: the image is cut into chunks of whole records (about chunk_bytes each, 0 = 16 MiB),
+ * and chunk k's edit overlaps chunk k+1's H2D and chunk k-1's D2H copy.  The buffers are
+ * page-locked for the call.  Same output bytes and return codes as tcpedit_rewrite_pcap. */
+int tcpedit_rewrite_pcap_pipelined(tcpedit_t *tcpedit, const void *in, size_t in_len, const void *cache,
+                                   size_t cache_len, void *out, size_t out_cap, size_t *out_len, size_t chunk_bytes);
+/* worst-case output image size of `in` under the context's options (host-only walk) */
+size_t tcpedit_output_bound(tcpedit_t *tcpedit, const void *in, size_t in_len);
+/* page-locked host buffers (a capture read straight into one needs no per-call locking) */
+void *tcpedit_host_alloc(size_t bytes);
+void tcpedit_host_free(void *p);
+
 /* Introspection (tests): copy the derived per-run device table (te_dev_cfg_t)
  * and, if portlut != NULL, the 65536-entry port map.  Returns its size or -1. */
 int tcpedit_get_dev_cfg(tcpedit_t *tcpedit, void *out, size_t len, uint16_t *portlut);

@@ -83,6 +83,10 @@ def load():
         "tcpedit_batch_device_output": (vp, [vp]),
         "tcpedit_batch_input_bytes": (u64, [vp]),
         "tcpedit_rewrite_pcap": (c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
+        "tcpedit_rewrite_pcap_pipelined": (c_int, [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), sz]),
+        "tcpedit_output_bound": (sz, [vp, vp, sz]),
+        "tcpedit_host_alloc": (vp, [sz]),
+        "tcpedit_host_free": (None, [vp]),
         "tcpedit_set_device": (c_int, [c_int]),
         "tcpedit_get_dev_cfg": (c_int, [vp, vp, sz, vp]),
     }
@@ -91,6 +95,32 @@ def load():
         f.restype, f.argtypes = res, args
     _lib = L
     return L
+
+
+class PinnedBuffer:
+    """Page-locked host memory from the library (tcpedit_host_alloc); `.view` is a
+    writable memoryview of it.  A capture read into one crosses PCIe by DMA without the
+    per-call page locking of an ordinary buffer."""
+
+    def __init__(self, nbytes):
+        self._L = load()
+        self.nbytes = int(nbytes)
+        self._p = self._L.tcpedit_host_alloc(max(1, self.nbytes))
+        if not self._p:
+            raise MemoryError(f"tcpedit_host_alloc({nbytes}) failed")
+        self.view = memoryview((ctypes.c_char * self.nbytes).from_address(self._p)).cast("B")
+
+    def close(self):
+        if self._p:
+            self.view.release()
+            self._L.tcpedit_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _buf(data):
@@ -158,6 +188,31 @@ class TcpEdit:
             return rc, out
         finally:
             b.close()
+
+    def output_bound(self, pcap):
+        """worst-case output size of `pcap` under this context's options"""
+        src = pcap if isinstance(pcap, (bytearray, memoryview)) else bytearray(pcap)
+        return self._L.tcpedit_output_bound(self._ctx, (ctypes.c_char * len(src)).from_buffer(src), len(src))
+
+    def rewrite_pipelined(self, pcap, cache: bytes = None, chunk_bytes=0, out=None):
+        """Whole-file rewrite through the chunked H2D | edit | D2H pipeline.  `pcap` may be
+        bytes or any writable buffer; `out` an optional preallocated bytearray (reused across
+        calls).  Returns (rc, output as a memoryview of `out` or bytes)."""
+        L = self._L
+        src = pcap if isinstance(pcap, (bytearray, memoryview)) else bytearray(pcap)
+        n = len(src)
+        inp = (ctypes.c_char * n).from_buffer(src)
+        own = out is None  # a caller's `out` is checked against the output by the library
+        if own:
+            out = bytearray(max(L.tcpedit_output_bound(self._ctx, inp, n), 24))
+        ob = (ctypes.c_char * len(out)).from_buffer(out)
+        cb, cn = _buf(cache)
+        olen = ctypes.c_size_t(0)
+        rc = L.tcpedit_rewrite_pcap_pipelined(self._ctx, inp, n, cb, cn, ob, len(out), ctypes.byref(olen),
+                                              int(chunk_bytes))
+        if own:
+            return rc, bytes(memoryview(out)[:olen.value])
+        return rc, memoryview(out)[:olen.value]
 
     def packet(self, hdr, data: bytearray, direction=TCPR_DIR_C2S):
         """tcpedit_packet(): edits `data` (bytearray, >= MAXPACKET bytes recommended) in place.

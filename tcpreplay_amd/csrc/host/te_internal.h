@@ -64,6 +64,8 @@ struct tcpedit_s {
     int dev_dirty;                /* cfg changed since last upload */
     uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */
+    struct te_pipe_s *pipe;       /* tcpedit_rewrite_pcap_pipelined's slots and streams (kept) */
+    int pipe_err;                 /* that call hit a hard error */
 };
 
 void te_seterr(tcpedit_t *t, const char *fmt, ...);
@@ -71,5 +73,7 @@ void te_setwarn(tcpedit_t *t, const char *fmt, ...);
 uint32_t te_tcpr_random(uint32_t *seed);
 int te_derive_cfg(tcpedit_t *t); /* tcpedit_post_args body */
 int te_upload_cfg(tcpedit_t *t);
+typedef struct te_pipe_s te_pipe_t;
+void te_pipe_free(tcpedit_t *t);
 
 #endif

@@ -8,6 +8,10 @@
  * Same options: -i/--infile, -o/--outfile, -c/--cachefile, --skip-soft-errors
  * and the tcpedit/en10mb option surface (tcpedit_opts.def, en10mb_opts.def).
  * Output: classic pcap, us timestamps, snaplen 65535 (tcprewrite.c:124).
+ *
+ * --pipeline[=MiB] reads the capture straight into page-locked memory and runs
+ * the chunked H2D | edit | D2H pipeline (tcpedit_rewrite_pcap_pipelined) instead:
+ * the same output bytes, without the per-record checksum warnings.
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -26,8 +30,11 @@ static void usage(void)
             "    --tcp-sequence --skipbroadcast/-b --fixcsum/-C --fixhdrlen --mtu/-m --mtu-trunc --efcs/-E\n"
             "    --ttl --tos --tclass --flowlabel --fixlen/-F --dlt --skipl2broadcast --enet-dmac --enet-smac\n"
             "    --enet-subsmac --enet-mac-seed --enet-mac-seed-keep-bytes --enet-vlan --enet-vlan-tag\n"
-            "    --enet-vlan-cfi --enet-vlan-pri --enet-vlan-proto\n");
+            "    --enet-vlan-cfi --enet-vlan-pri --enet-vlan-proto\n"
+            "  --pipeline[=MiB]: chunked H2D | edit | D2H from page-locked buffers (no per-record warnings)\n");
 }
+
+static int g_pinned; /* read into page-locked memory (--pipeline) */
 
 static void *slurp(const char *path, size_t *len)
 {
@@ -37,10 +44,13 @@ static void *slurp(const char *path, size_t *len)
     fseek(f, 0, SEEK_END);
     long n = ftell(f);
     fseek(f, 0, SEEK_SET);
-    void *buf = malloc(n > 0 ? (size_t)n : 1);
-    if (n > 0 && fread(buf, 1, (size_t)n, f) != (size_t)n) {
+    void *buf = g_pinned ? tcpedit_host_alloc(n > 0 ? (size_t)n : 1) : malloc(n > 0 ? (size_t)n : 1);
+    if (!buf || (n > 0 && fread(buf, 1, (size_t)n, f) != (size_t)n)) {
         fclose(f);
-        free(buf);
+        if (g_pinned)
+            tcpedit_host_free(buf);
+        else
+            free(buf);
         return NULL;
     }
     fclose(f);
@@ -55,12 +65,17 @@ int main(int argc, char **argv)
     int *unused = calloc((size_t)argc + 1, sizeof(int));
     tcpedit_t *te = NULL;
 
+    size_t pipe_mib = 0;
     /* the reference reads the input DLT first (pcap_datalink(pin), tcprewrite.c:80) */
     for (int i = 1; i < argc; i++) {
         if ((!strcmp(argv[i], "-i") || !strcmp(argv[i], "--infile")) && i + 1 < argc)
             infile = argv[++i];
         else if (!strncmp(argv[i], "--infile=", 9))
             infile = argv[i] + 9;
+        else if (!strcmp(argv[i], "--pipeline"))
+            g_pinned = 1;
+        else if (!strncmp(argv[i], "--pipeline=", 11))
+            g_pinned = 1, pipe_mib = strtoul(argv[i] + 11, NULL, 10);
     }
     if (!infile) {
         usage();
@@ -106,6 +121,7 @@ int main(int argc, char **argv)
             cachefile = a + 12;
         } else if (!strcmp(a, "--skip-soft-errors")) {
             skip_soft = 1;
+        } else if (!strcmp(a, "--pipeline") || !strncmp(a, "--pipeline=", 11)) {
         } else {
             fprintf(stderr, "tcprewrite: unknown argument %s\n", a);
             usage();
@@ -137,6 +153,28 @@ int main(int argc, char **argv)
         return 255;
     }
 
+    if (g_pinned) { /* page-locked capture -> chunked pipeline -> page-locked output -> file */
+        const size_t cap = tcpedit_output_bound(te, in, in_len);
+        uint8_t *pout = tcpedit_host_alloc(cap > 24 ? cap : 24);
+        size_t olen = 0;
+        int prc = pout ? tcpedit_rewrite_pcap_pipelined(te, in, in_len, cache, cache_len, pout, cap, &olen,
+                                                         pipe_mib << 20)
+                       : TCPEDIT_ERROR;
+        FILE *f = fopen(outfile, "wb");
+        if (!f || fwrite(pout, 1, olen, f) != olen) {
+            fprintf(stderr, "Unable to write output pcap file: %s\n", outfile);
+            return 255;
+        }
+        fclose(f);
+        if (prc != 0)
+            fprintf(stderr, "Error rewriting packets: %s\n", tcpedit_geterr(te));
+        tcpedit_host_free(pout);
+        tcpedit_host_free(in);
+        tcpedit_host_free(cache);
+        tcpedit_close(&te);
+        free(unused);
+        return prc != 0 ? 255 : 0;
+    }
     tcpedit_batch_t *b = tcpedit_batch_open(te, in, in_len, cache, cache_len, 0);
     if (!b) {
         fprintf(stderr, "tcprewrite: %s\n", tcpedit_geterr(te));

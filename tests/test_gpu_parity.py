@@ -227,3 +227,90 @@ def test_full_size_c2_matches_oracle(built):
     rc, out = gpu_rewrite(pcap, C2_ARGS)
     assert rc == rc_o == 0
     assert_same(out, exp)
+
+
+# ---------------------------------------------------------------- pipelined whole-file path
+def pipe_rewrite(pcap, args, cache=None, chunk=1 << 20):
+    te = TA.TcpEdit(args)
+    try:
+        return te.rewrite_pipelined(pcap, cache, chunk_bytes=chunk)
+    finally:
+        te.close()
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
+def test_pipelined_matches_oracle_on_baseline_configs(built, cfg):
+    """Several 1 MiB chunks per capture: record boundaries, cache lookups (pkt_base) and
+    output placement across chunks."""
+    cache = None
+    if cfg == "C2":
+        pcap, args = S.pcap_fixed(60_000, 64, seed=12), C2_ARGS
+    elif cfg == "C3":
+        pcap, args = S.pcap_imix(20_000, seed=13), C3_ARGS
+    elif cfg == "C4":
+        pcap, args = S.pcap_imix(20_000, seed=14), C4_ARGS
+        cache = S.tcpprep_cache(20_000, seed=14, nosend_every=97)
+    else:
+        pcap, args = S.pcap_mixed_v4v6(4_000, 1514, seed=15), C5_ARGS
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    rc, out = pipe_rewrite(pcap, args, cache)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
+
+
+@pytest.mark.parametrize("case", G.IN_SCOPE[:6], ids=[c[0] for c in G.IN_SCOPE[:6]])
+def test_pipelined_matches_reference_golden(built, case):
+    name, inp, cache, args, _ = case
+    rc, out = pipe_rewrite(G.read(inp), args, G.read(cache) if cache else None)
+    assert rc == 0
+    assert_same(out, G.read(name))
+
+
+def test_pipelined_context_reuse_and_edge_cases(built):
+    args = ["--seed=5", "--fixcsum"]
+    te = TA.TcpEdit(args)
+    try:
+        # the empty capture, then a capture ending in a truncated record, then a big one
+        empty = S.build_pcap([])
+        rc, out = te.rewrite_pipelined(empty, chunk_bytes=1 << 20)
+        assert rc == 0 and out == O.rewrite(empty, args)[1]
+        big = S.pcap_imix(30_000, seed=16)
+        cut = big[: len(big) - 700]  # the last record is cut short: libpcap stops before it
+        for img in (cut, big, big):
+            rc_o, exp = O.rewrite(img, args)
+            rc, out = te.rewrite_pipelined(img, chunk_bytes=1 << 20)
+            assert rc == rc_o == 0
+            assert_same(out, exp)
+        # the same slots with the default chunk size
+        rc, out = te.rewrite_pipelined(big)
+        assert rc == 0 and out == O.rewrite(big, args)[1]
+    finally:
+        te.close()
+
+
+def test_pipelined_hard_error_truncates_in_a_later_chunk(built):
+    recs = S.records(S.pcap_fixed(40_000, 64, seed=17))
+    ts, tu, cl, ln, d = recs[30_000]
+    recs[30_000] = (ts, tu, cl, 300_000, d)  # len > MAX_SNAPLEN: tcprewrite.c:296-297 errx()
+    pcap = S.build_pcap(recs)
+    args = ["--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out = pipe_rewrite(pcap, args)
+    assert rc == rc_o == -1
+    assert_same(out, exp)
+
+
+@pytest.mark.parametrize("mode", [[], ["--pipeline=1"]])
+def test_tcprewrite_tool_file_to_file(built, tmp_path, mode):
+    """bin/tcprewrite, batch and pipelined modes, against the reference's own goldens
+    (config 1: --fixcsum; the tcpprep-cache endpoint/VLAN chain)."""
+    import subprocess
+    tool = os.path.join(os.path.dirname(TA.LIB_PATH), "..", "bin", "tcprewrite")
+    for name in ("test2.rewrite_fixcsum", "test2.rewrite_endpoint"):
+        case = next(c for c in G.CASES if c[0] == name)
+        out = tmp_path / f"{name}.out"
+        cmd = [tool, "-i", os.path.join(G.GOLDEN_DIR, case[1]), "-o", str(out)] + case[3] + mode
+        if case[2]:
+            cmd += ["-c", os.path.join(G.GOLDEN_DIR, case[2])]
+        subprocess.run(cmd, check=True, capture_output=True, timeout=60)
+        assert_same(out.read_bytes(), G.read(name))
