@@ -322,7 +322,8 @@ DI void csum_replace16(u8 *sp, const u8 *from, const u8 *to) {
 // ---------------------------------------------------------------------------
 // Small predicates
 // ---------------------------------------------------------------------------
-DI bool mcast4(u32 ip_le) { return (bswap32(ip_le) & 0xf0000000u) == 0xe0000000u; }  // edit_packet.c:1204
+// edit_packet.c:1204 (ntohl(ip) & 0xf0000000) == 0xe0000000, on the first octet = the low byte
+DI bool mcast4(u32 ip_le) { return (ip_le & 0xf0u) == 0xe0u; }
 DI bool mcast6(const u8 *a) { return a[0] == 0xff; }                                  // :1229
 
 DI bool is_unicast_ethernet(const u8 *e) {  // plugins/ethernet.c:30-57
@@ -565,11 +566,11 @@ DI u32 randomize_ipv4_addr(const te_dev_cfg_t &cfg, u32 ip) {
     if (cfg.skip_broadcast && was) return ip;
     u32 s = bswap32(cfg.seed);
     u32 r = (ip ^ s) - (ip & s);
-    if (was && !mcast4(r))
-        r = bswap32((bswap32(r) & 0x0fffffffu) | 0xe0000000u);
-    else if (!was && mcast4(r))
-        r = bswap32(bswap32(r) & 0x7fffffffu);
-    return r;
+    // htonl((ntohl(r) & 0x0fffffff) | 0xe0000000) and htonl(ntohl(r) & 0x7fffffff),
+    // on the first octet (the low byte of the little-endian value)
+    const bool now = mcast4(r);
+    const u32 r1 = (r & 0xffffff0fu) | 0xe0u, r2 = r & 0xffffff7fu;
+    return (was && !now) ? r1 : ((!was && now) ? r2 : r);
 }
 
 // randomize_ipv6_addr (edit_packet.c:359-379)

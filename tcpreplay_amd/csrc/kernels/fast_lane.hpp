@@ -42,6 +42,12 @@ DI u32 swap16(u32 x) {
     return ((x >> 8) | (x << 8)) & 0xffffu;
 }
 DI u32 bs16(u32 x) { return swap16(x); }
+// end-around-carry fold of a sum below 2^32 to 16 bits: two steps always suffice
+// (fold16's data-dependent loop, unrolled for this range)
+DI u32 fold32(u32 x) {
+    x = (x & 0xffffu) + (x >> 16);
+    return (x & 0xffffu) + (x >> 16);
+}
 
 // mask of bytes [lo, hi) of a dword (lo, hi clamped to [0, 4])
 DI u32 bmask(int lo, int hi) {
@@ -215,8 +221,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     if (!v6) {
         u32 src = H[7], dst = H[8];
         // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is carried
-#define FL_V4_UPD(o, n) \
-    if (udp_live && ucs) ucs = csum_replace4_v((u16)ucs, (o), (n))
+#define FL_V4_UPD(o, n) ucs = (udp_live && ucs) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs
         if (cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
             for (int m = 0; m < cfg.n_srcipmap; ++m)
                 if (ip_in_cidr(cfg.srcipmap[m].from, src)) {
@@ -262,14 +267,16 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
             }
         }
         if (cfg.seed) {  // randomize_ipv4 (edit_packet.c:420-467): destination, then source
-            if (!(cfg.skip_broadcast && mcast4(dst))) {
+            // branch-free: a skipped address maps to itself, and the update of an
+            // unchanged address leaves the checksum field as it is
+            {
                 const u32 o = dst;
-                dst = randomize_ipv4_addr(cfg, o);
+                dst = (cfg.skip_broadcast && mcast4(o)) ? o : randomize_ipv4_addr(cfg, o);
                 FL_V4_UPD(o, dst);
             }
-            if (!(cfg.skip_broadcast && mcast4(src))) {
+            {
                 const u32 o = src;
-                src = randomize_ipv4_addr(cfg, o);
+                src = (cfg.skip_broadcast && mcast4(o)) ? o : randomize_ipv4_addr(cfg, o);
                 FL_V4_UPD(o, src);
             }
         }
@@ -391,7 +398,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     if (!v6) {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
         H[6] = with_hi16(H[6], 0);
         u32 hs = wsum(H[4]) + wsum(H[5]) + wsum(H[6]) + wsum(H[7]) + wsum(H[8]);
-        H[6] = with_hi16(H[6], (~fold16(hs)) & 0xffffu);
+        H[6] = with_hi16(H[6], (~fold32(hs)) & 0xffffu);
         dirty |= 1u << 6;
     }
 
@@ -423,7 +430,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
 // already in the packet's relative byte pairing) and store the checksum.
 DI void phase_b(u32 (&H)[NW], const State &st, u32 tail) {
     if (!st.do_l4) return;
-    const u32 c = (~fold16((unsigned long long)st.l4sum + tail)) & 0xffffu;  // CHECKSUM_CARRY
+    const u32 c = (~fold32(st.l4sum + tail)) & 0xffffu;  // CHECKSUM_CARRY (l4sum < 2^21, tail < 2^16)
     // explicit per-index selects (a ternary on the index would move H to scratch)
     const bool t6 = st.tcp && st.v6, t4 = st.tcp && !st.v6, u6 = !st.tcp && st.v6, u4 = !st.tcp && !st.v6;
     H[18] = t6 ? with_lo16(H[18], c) : H[18];  // 54 + 16

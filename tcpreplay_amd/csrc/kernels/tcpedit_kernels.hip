@@ -1190,16 +1190,24 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
                 }
                 fl::phase_b(H, st, tail);
                 const uint32_t A = wa & ~3u, sh = wa & 3u;
+                uint32_t part = 0;  // dwords that straddle caplen: written bytewise below
 #pragma unroll
                 for (int j = 0; j < fl::NW; ++j) {
                     if (!((todo >> j) & 1u)) continue;
                     const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
                     const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
-                    const int rel = (int)(A + 4 * j) - (int)p;
-                    uint8_t *q = S + A + 4 * j;
-                    if (rel + 4 <= (int)caplen) {
-                        *(uint32_t *)q = v;
-                    } else {
+                    const int rel = (int)(A + 4 * j) - (int)p;  // packet offset of the dword's first byte
+                    if (rel + 4 <= (int)caplen) *(uint32_t *)(S + A + 4 * j) = v;
+                    else if (rel < (int)caplen) part |= 1u << j;
+                }
+                if (part) {  // rare: a touched dword past the last whole one of a short packet
+#pragma unroll
+                    for (int j = 0; j < fl::NW; ++j) {
+                        if (!((part >> j) & 1u)) continue;
+                        const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
+                        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
+                        const int rel = (int)(A + 4 * j) - (int)p;
+                        uint8_t *q = S + A + 4 * j;
 #pragma unroll
                         for (int b = 0; b < 3; ++b)
                             if (rel + b < (int)caplen) q[b] = (uint8_t)(v >> (8 * b));

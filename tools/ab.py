@@ -16,7 +16,12 @@ CASES = {
     "c3": (lambda: S.pcap_imix(1_000_000, seed=1),
            ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]),
     "c5": (lambda: S.pcap_mixed_v4v6(250_000, 1514, seed=1), ["--fixcsum"]),
+    "c4": (lambda: S.pcap_imix(1_000_000, seed=1),
+           ["--endpoints=10.10.0.1:10.10.0.2", "--enet-dmac=00:12:13:14:15:16,00:22:33:44:55:66",
+            "--enet-smac=00:22:33:44:55:66,00:12:13:14:15:16", "--enet-vlan=add", "--enet-vlan-tag=45",
+            "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"]),
 }
+CACHES = {"c4": lambda: S.tcpprep_cache(1_000_000, seed=1)}
 
 
 def main():
@@ -24,9 +29,10 @@ def main():
     for name in (sys.argv[1:] or list(CASES)):
         gen, args = CASES[name]
         pcap = gen()
-        _, exp = O.rewrite(pcap, args)
+        cache = CACHES[name]() if name in CACHES else None
+        _, exp = O.rewrite(pcap, args, cache)
         te = TA.TcpEdit(args)
-        b = TA.Batch(te, pcap)
+        b = TA.Batch(te, pcap, cache)
         rc = b.run()
         r = b.result()
         ok = rc == 0 and b.output() == exp
