@@ -462,6 +462,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     te_launch_t L;
     memset(&L, 0, sizeof(L));
     L.cfg = t->d_cfg;
+    L.cfg_host = &t->cfg;
     L.portlut = t->cfg.has_portmap ? t->d_portlut : NULL;
     L.dirbits = b->d_dirbits;
     L.dirbits_len = b->dirbits_len;

@@ -34,6 +34,13 @@ extern "C" {
 #define TE_TILE_SOLO 1u        /* te_tile_t.flags: a record too large for a wave-lane image */
 #define TE_FAST_BLOCK 1        /* fast-lane kinds: te_fast_tiles (one block per tile) ... */
 #define TE_FAST_WAVE 2         /* ... or te_wave_tiles (one wave per tile) */
+/* option groups of the fast lane: a te_wave_tiles instance compiles in the groups of
+   its mask, and te_launch_edit launches the smallest instance covering the config */
+#define TE_FF_MAC 1u     /* --enet-dmac / --enet-smac */
+#define TE_FF_PORTMAP 2u /* --portmap */
+#define TE_FF_RWIP 4u    /* --srcipmap / --dstipmap / --pnat / --endpoints */
+#define TE_FF_SEED 8u    /* --seed */
+#define TE_FF_ALL 15u
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
@@ -59,6 +66,7 @@ typedef struct {
 
 typedef struct {
     const te_dev_cfg_t *cfg;  /* device pointer */
+    const te_dev_cfg_t *cfg_host; /* the same config on the host (instance choice, scalar knobs) */
     const uint16_t *portlut;  /* device: 65536-entry first-match port map, or NULL */
     const uint8_t *dirbits;   /* device: tcpprep cache data, or NULL */
     uint64_t dirbits_len;

@@ -560,17 +560,19 @@ DI void ipv6_addr_csum_replace(Pkt &pk, u8 *ip6, const u8 *old_ip, const u8 *new
     csum_replace16(ip6 + l4 + fld, old_ip, new_ip);
 }
 
-// randomize_ipv4_addr (edit_packet.c:336-357)
-DI u32 randomize_ipv4_addr(const te_dev_cfg_t &cfg, u32 ip) {
-    bool was = mcast4(ip);
-    if (cfg.skip_broadcast && was) return ip;
-    u32 s = bswap32(cfg.seed);
-    u32 r = (ip ^ s) - (ip & s);
+// randomize_ipv4_addr (edit_packet.c:336-357) without the skip test; s = bswap32(seed)
+DI u32 randomize_ipv4_sw(u32 s, u32 ip) {
+    const bool was = mcast4(ip);
+    const u32 r = (ip ^ s) - (ip & s);
     // htonl((ntohl(r) & 0x0fffffff) | 0xe0000000) and htonl(ntohl(r) & 0x7fffffff),
     // on the first octet (the low byte of the little-endian value)
     const bool now = mcast4(r);
     const u32 r1 = (r & 0xffffff0fu) | 0xe0u, r2 = r & 0xffffff7fu;
     return (was && !now) ? r1 : ((!was && now) ? r2 : r);
+}
+DI u32 randomize_ipv4_addr(const te_dev_cfg_t &cfg, u32 ip) {
+    if (cfg.skip_broadcast && mcast4(ip)) return ip;
+    return randomize_ipv4_sw(bswap32(cfg.seed), ip);
 }
 
 // randomize_ipv6_addr (edit_packet.c:359-379)

@@ -89,10 +89,9 @@ DI void remap_ipv6_w(const te_dev_cfg_t &cfg, const te_cidr_t &c, u32 *a) {
     }
 }
 
-// randomize_ipv6_addr (edit_packet.c:359-379)
-DI void randomize_ipv6_w(const te_dev_cfg_t &cfg, u32 *a) {
+// randomize_ipv6_addr (edit_packet.c:359-379); s = bswap32(seed)
+DI void randomize_ipv6_w(u32 s, u32 *a) {
     const bool was = (a[0] & 0xffu) == 0xffu;
-    const u32 s = bswap32(cfg.seed);
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = (a[i] ^ s) - (a[i] & s);
     const bool now = (a[0] & 0xffu) == 0xffu;
@@ -113,6 +112,21 @@ DI unsigned long long mac48(const u8 *m) {
     return (unsigned long long)ld32(m) | ((unsigned long long)ld16(m + 4) << 32);
 }
 
+// Feature instances: F (TE_FF_* bits) names the option groups a kernel
+// instance compiles in; a group left out is dead code, not a runtime branch on
+// an LDS cfg field.  The host launches the smallest instance whose F covers the
+// config (te_launch_edit).
+constexpr u32 F_MAC = TE_FF_MAC, F_PORTMAP = TE_FF_PORTMAP, F_RWIP = TE_FF_RWIP, F_SEED = TE_FF_SEED;
+
+// the scalar options phase A reads per packet, held in SGPRs (kernel arguments)
+// instead of being re-read from the LDS cfg copy on every tile
+struct Knobs {
+    u32 seed_sw;      // bswap32(cfg.seed), as randomize_ipv4/6 use it
+    bool seed;        // cfg.seed != 0
+    bool skip_bcast;  // cfg.skip_broadcast
+};
+DI Knobs knobs_of(const te_dev_cfg_t &cfg) { return Knobs{bswap32(cfg.seed), cfg.seed != 0, cfg.skip_broadcast != 0}; }
+
 // what phase B needs to finish a packet after the block's chunk-prefix pass
 struct State {
     u32 l4sum;  // unfolded one's-complement sum so far (pseudo header + L4 bytes inside the window)
@@ -125,7 +139,8 @@ struct State {
 // Phase A: classify, edit, IPv4 header checksum, in-window L4 sum.
 // Returns false to defer the packet to the generic lane (H untouched then).
 // ---------------------------------------------------------------------------
-DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &cfg, bool v6_ok,
+template <u32 F>
+DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &cfg, const Knobs &kn, bool v6_ok,
                 const TE_AS_GLOBAL uint16_t *lut, State &st) {
     if (caplen != len || (dir != TE_DIR_C2S && dir != TE_DIR_S2C)) return false;
     const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
@@ -163,7 +178,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
 
     u32 dirty = 0;
     // ---- en10mb_encode: MAC rewrite (no VLAN, subsmac or mac-seed here) ----
-    if (cfg.mac_mask) {
+    if ((F & F_MAC) && cfg.mac_mask) {
         const bool c2s = dir == TE_DIR_C2S;
         const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
         unsigned long long dmac = (unsigned long long)hi16(H[0]) | ((unsigned long long)H[1] << 16);
@@ -190,7 +205,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     const bool udp_live = !tcp;
 
     // ---- port map (rewrite_ports, portmap.c:267-330): destination, then source ----
-    if (cfg.has_portmap) {
+    if ((F & F_PORTMAP) && cfg.has_portmap) {
         const u32 od = hi16(L[0]), os = lo16(L[0]);
         u32 nd = od, ns = os;
         if (cfg.n_pm >= 0) {
@@ -222,7 +237,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
         u32 src = H[7], dst = H[8];
         // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is carried
 #define FL_V4_UPD(o, n) ucs = (udp_live && ucs) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs
-        if (cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
+        if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
             for (int m = 0; m < cfg.n_srcipmap; ++m)
                 if (ip_in_cidr(cfg.srcipmap[m].from, src)) {
                     const u32 o = src;
@@ -266,30 +281,30 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
                 }
             }
         }
-        if (cfg.seed) {  // randomize_ipv4 (edit_packet.c:420-467): destination, then source
+        if ((F & F_SEED) && kn.seed) {  // randomize_ipv4 (edit_packet.c:420-467): destination, then source
             // branch-free: a skipped address maps to itself, and the update of an
             // unchanged address leaves the checksum field as it is
             {
                 const u32 o = dst;
-                dst = (cfg.skip_broadcast && mcast4(o)) ? o : randomize_ipv4_addr(cfg, o);
+                dst = (kn.skip_bcast && mcast4(o)) ? o : randomize_ipv4_sw(kn.seed_sw, o);
                 FL_V4_UPD(o, dst);
             }
             {
                 const u32 o = src;
-                src = (cfg.skip_broadcast && mcast4(o)) ? o : randomize_ipv4_addr(cfg, o);
+                src = (kn.skip_bcast && mcast4(o)) ? o : randomize_ipv4_sw(kn.seed_sw, o);
                 FL_V4_UPD(o, src);
             }
         }
 #undef FL_V4_UPD
         H[7] = src;
         H[8] = dst;
-        if (cfg.rewrite_ip || cfg.seed) dirty |= (1u << 7) | (1u << 8);
+        if (((F & F_RWIP) && cfg.rewrite_ip) || ((F & F_SEED) && kn.seed)) dirty |= (1u << 7) | (1u << 8);
     } else {
         u32 src[4] = {H[6], H[7], H[8], H[9]}, dst[4] = {H[10], H[11], H[12], H[13]};
         // ipv6_addr_csum_replace (edit_packet.c:298-330): only the UDP field is carried
 #define FL_V6_UPD(o, n) \
     if (udp_live && ucs) ucs = csum_replace16_v((u16)ucs, (o), (n))
-        if (cfg.rewrite_ip) {  // rewrite_ipv6l3 (edit_packet.c:884-1019); TCP/UDP: no ICMPv6 recursion
+        if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv6l3 (edit_packet.c:884-1019); TCP/UDP: no ICMPv6 recursion
             for (int m = 0; m < cfg.n_srcipmap; ++m)
                 if (ip6_in_cidr_w(cfg.srcipmap[m].from, src)) {
                     const u32 o[4] = {src[0], src[1], src[2], src[3]};
@@ -333,15 +348,15 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
                 }
             }
         }
-        if (cfg.seed) {  // randomize_ipv6 (edit_packet.c:469-518): destination, then source
-            if (!(cfg.skip_broadcast && (dst[0] & 0xffu) == 0xffu)) {
+        if ((F & F_SEED) && kn.seed) {  // randomize_ipv6 (edit_packet.c:469-518): destination, then source
+            if (!(kn.skip_bcast && (dst[0] & 0xffu) == 0xffu)) {
                 const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
-                randomize_ipv6_w(cfg, dst);
+                randomize_ipv6_w(kn.seed_sw, dst);
                 FL_V6_UPD(o, dst);
             }
-            if (!(cfg.skip_broadcast && (src[0] & 0xffu) == 0xffu)) {
+            if (!(kn.skip_bcast && (src[0] & 0xffu) == 0xffu)) {
                 const u32 o[4] = {src[0], src[1], src[2], src[3]};
-                randomize_ipv6_w(cfg, src);
+                randomize_ipv6_w(kn.seed_sw, src);
                 FL_V6_UPD(o, src);
             }
         }
@@ -351,7 +366,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
             H[6 + i] = src[i];
             H[10 + i] = dst[i];
         }
-        if (cfg.rewrite_ip || cfg.seed) dirty |= 0xffu << 6;
+        if (((F & F_RWIP) && cfg.rewrite_ip) || ((F & F_SEED) && kn.seed)) dirty |= 0xffu << 6;
     }
 
     // ---- fix_ipv4/ipv6_checksums (edit_packet.c:55-189) -> do_checksum (checksum.c:34-170) ----
@@ -370,7 +385,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     }
     {
         const int base = v6 ? 14 : 9;  // ports (port map), UDP csum (L4+6), TCP csum (L4+16)
-        dirty |= ((cfg.has_portmap ? 1u : 0u) | (tcp ? 0x10u : 0x2u)) << base;
+        dirty |= ((((F & F_PORTMAP) && cfg.has_portmap) ? 1u : 0u) | (tcp ? 0x10u : 0x2u)) << base;
     }
     u32 sum = 0;
     if (do_l4) {

@@ -569,6 +569,7 @@ struct FastArgs {
     uint32_t n_tiles;
     int32_t fixed_dir;
     uint32_t in_swapped, in_nsec, v6_ok;
+    uint32_t seed_sw, seed_on, skip_bcast;  // te_wave_tiles' phase-A knobs (fl::Knobs), in SGPRs
 };
 
 // one's-complement sum of the LE 16-bit words (absolute pairing) of bytes [b0, b1) of chunk c
@@ -751,7 +752,7 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #pragma unroll
                 for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
                 d0 = e[0];
-                ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
+                ok = fl::phase_a<TE_FF_ALL>(H, caplen, len, dir, cfg, fl::knobs_of(cfg), a.v6_ok != 0, lut, st);
             }
         }
         {
@@ -962,6 +963,18 @@ static_assert(WK_IMG % 16 == 0, "16-byte aligned wave images");
 #define WK_STAMP(i)
 #endif
 
+// OR over the wave's 64 lanes, in VALU: DPP row shifts leave each 16-lane row's OR in
+// its lane 15, and four readlanes combine the rows (__shfl_xor would be six dependent
+// ds_bpermute round trips through the LDS pipe)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 15) | __builtin_amdgcn_readlane((int)v, 31) |
+                      __builtin_amdgcn_readlane((int)v, 47) | __builtin_amdgcn_readlane((int)v, 63));
+}
+
 __device__ __forceinline__ bool wk_solo(const te_tile_t &tl) {
     return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH;
 }
@@ -977,6 +990,7 @@ __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     st32(rec + 12, ln);
 }
 
+template <uint32_t F>
 __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
     __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
@@ -1005,6 +1019,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
     const TE_AS_CONST te_tile_t *tiles = (const TE_AS_CONST te_tile_t *)a.tiles;
     const TE_AS_CONST uint16_t *pkt_rel = (const TE_AS_CONST uint16_t *)a.pkt_rel;
+    const fl::Knobs kn{a.seed_sw, a.seed_on != 0, a.skip_bcast != 0};
     __syncthreads();
 
     // the next tile's chunks in flight, in named registers
@@ -1081,55 +1096,60 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
         const uint32_t p = r0 + 16;                   // packet data in S
         const uint32_t wa = p - 2;                    // window start (packet offset -2)
         const bool on = lane < (int)npkt;
-        uint32_t H[fl::NW];
-        uint32_t d0 = 0, caplen = 0, len = 0;
+        // every lane reads a header and a window (lanes past npkt: the tile's last
+        // record's), so H has one definition and no lane-dependent merge copies
+        uint32_t caplen, len;
+        {  // caplen, len: three aligned dword reads + funnel shifts
+            const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
+            const uint32_t q0 = *(const uint32_t *)(S + ha), q1 = *(const uint32_t *)(S + ha + 4),
+                           q2 = *(const uint32_t *)(S + ha + 8);
+            caplen = __builtin_amdgcn_alignbyte(q1, q0, hs);
+            len = __builtin_amdgcn_alignbyte(q2, q1, hs);
+            if (swp) {
+                caplen = bswap32(caplen);
+                len = bswap32(len);
+            }
+        }
+        // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
+        // the window to packet offset -2; each H[i] can take d[i]'s register
+        uint32_t H[fl::NW], d0;
+        {
+            const uint32_t A4 = wa & ~3u, sh = wa & 3u;
+            uint32_t d[fl::NW + 1];
+#pragma unroll
+            for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
+#pragma unroll
+            for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+            d0 = d[0];
+        }
+        int dir = TE_DIR_C2S;
+        if (explicit_dir) {
+            dir = a.fixed_dir;
+        } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354), byte loaded with the span
+            const uint64_t pktno = a.pkt_base + tile.first_pkt + lane;
+            const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+            const uint32_t b = my_dirv ? my_dirb : 0u;
+            dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+        }
+#if TE_WK_EXP == 1  // diagnostics only: the skeleton without the edit (output = input)
+        dir = TE_DIR_NOSEND;
+#endif
+        // tcprewrite.c:314-315: a record the cache says not to send is written unedited
+        bool nosend = on && dir == TE_DIR_NOSEND && !explicit_dir;
         fl::State st;
         st.do_l4 = st.tail = false;
         st.dirty = 0;
-        bool ok = true, nosend = false;
-        if (on) {
-            {  // caplen, len: three aligned dword reads + funnel shifts
-                const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
-                const uint32_t q0 = *(const uint32_t *)(S + ha), q1 = *(const uint32_t *)(S + ha + 4),
-                               q2 = *(const uint32_t *)(S + ha + 8);
-                caplen = __builtin_amdgcn_alignbyte(q1, q0, hs);
-                len = __builtin_amdgcn_alignbyte(q2, q1, hs);
-                if (swp) {
-                    caplen = bswap32(caplen);
-                    len = bswap32(len);
-                }
-            }
-            const uint64_t pktno = a.pkt_base + tile.first_pkt + lane;
-            int dir = TE_DIR_C2S;
-            if (explicit_dir) {
-                dir = a.fixed_dir;
-            } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354), byte loaded with the span
-                const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
-                const uint32_t b = my_dirv ? my_dirb : 0u;
-                dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
-            }
-            if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
-                nosend = true;
-            } else {
-                // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
-                // the window to packet offset -2; each H[i] can take d[i]'s register
-                const uint32_t A4 = wa & ~3u, sh = wa & 3u;
-                uint32_t d[fl::NW + 1];
+        bool ok = true;
+        if (on && !nosend) {
+#if TE_WK_EXP == 2  // diagnostics only: window reads, no edit
+            uint32_t x = 0;
 #pragma unroll
-                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
-#pragma unroll
-                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-                d0 = d[0];
-#if TE_WK_CFG_OPAQUE
-                // cfg fields are re-read from LDS per tile, not hoisted into registers
-                typedef __attribute__((address_space(3))) const te_dev_cfg_t lds_cfg_t;
-                lds_cfg_t *cp = (lds_cfg_t *)&cfg;
-                asm volatile("" : "+v"(cp));
-                ok = fl::phase_a(H, caplen, len, dir, *(const te_dev_cfg_t *)cp, a.v6_ok != 0, lut, st);
+            for (int i = 0; i < fl::NW; ++i) x ^= H[i];
+            ok = x != 0x9e3779b9u;
+            nosend = true;
 #else
-                ok = fl::phase_a(H, caplen, len, dir, cfg, a.v6_ok != 0, lut, st);
+            ok = fl::phase_a<F>(H, caplen, len, dir, cfg, kn, a.v6_ok != 0, lut, st);
 #endif
-            }
         }
 #if TE_WK_ISSUE_LATE
         if (more) WK_ISSUE(cur);  // in flight while this tile is finished and stored
@@ -1177,9 +1197,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
         // it with its own packet's bytes (never past caplen), which is harmless.
         uint32_t todo = 0;
         if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) todo |= __shfl_xor(todo, o, 64);
-        todo = __builtin_amdgcn_readfirstlane(todo);
+        todo = wave_or(todo);
         // ---- phase B + write-back of the dwords phase A touched ----
         if (on) {
             if (!nosend) {
@@ -1306,12 +1324,29 @@ extern "C" int te_fast_grid(void) {
     return c;
 }
 
+// the te_wave_tiles instances built (TE_FF_* masks), smallest first: a launch takes
+// the first whose mask covers the config's option groups
+#define TE_WAVE_INSTANCES(X) X(0u) X(TE_FF_SEED) X(TE_FF_PORTMAP | TE_FF_RWIP) X(TE_FF_ALL)
+static const struct {
+    uint32_t feat;
+    const void *fn;
+} wave_inst[] = {
+#define TE_WI(f) {f, (const void *)te_wave_tiles<f>},
+    TE_WAVE_INSTANCES(TE_WI)
+#undef TE_WI
+};
+
+static uint32_t fast_feat(const te_dev_cfg_t *c) {
+    return (c->mac_mask ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
+           (c->rewrite_ip ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u);
+}
+
 extern "C" int te_wave_grid(void) {
     static int c = 0;
     if (c) return c;
     int cus = cu_count(), per_cu = 0;
     if (!cus) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles, WKB, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL>, WKB, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     c = cus * per_cu;
     return c;
@@ -1376,6 +1411,14 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.v6_ok = (uint32_t)L->fast_v6;
         f.slots = (unsigned long long *)L->slots;
         f.counters_next = (unsigned long long *)L->counters_next;
+        const te_dev_cfg_t *ch = L->cfg_host;
+        if (!ch) return -1;
+        f.seed_sw = __builtin_bswap32(ch->seed);
+        f.seed_on = ch->seed != 0;
+        f.skip_bcast = ch->skip_broadcast != 0;
+        const void *wfn = nullptr;
+        for (const auto &wi : wave_inst)
+            if (!wfn && (fast_feat(ch) & ~wi.feat) == 0) wfn = wi.fn;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
         int fgrid = wave ? te_wave_grid() : te_fast_grid();
         if (fgrid < 1) return -1;
@@ -1385,7 +1428,10 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             return -1;  // the wave lane stores whole 16-byte chunks at input offsets + a multiple of 16
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
         if (wave)
-            hipLaunchKernelGGL(te_wave_tiles, dim3(fgrid), dim3(WKB), 0, stream, f);
+        {
+            void *args[] = {&f};
+            if (hipLaunchKernel(wfn, dim3(fgrid), dim3(WKB), args, 0, stream) != hipSuccess) return -1;
+        }
         else
             hipLaunchKernelGGL(te_fast_tiles, dim3(fgrid), dim3(FKB), 0, stream, f);
         if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
