@@ -37,6 +37,8 @@ DI u32 hi16(u32 x) { return x >> 16; }
 DI u32 with_lo16(u32 x, u32 v) { return (x & 0xffff0000u) | (v & 0xffffu); }
 DI u32 with_hi16(u32 x, u32 v) { return (x & 0xffffu) | (v << 16); }
 DI u32 wsum(u32 x) { return (x & 0xffffu) + (x >> 16); }  // its two LE 16-bit words
+// acc + the two LE 16-bit words of x, in one v_sad_u16 (|x.lo - 0| + |x.hi - 0| + acc)
+DI u32 wsum_acc(u32 x, u32 acc) { return __builtin_amdgcn_sad_u16(x, 0u, acc); }
 DI u32 swap16(u32 x) {
     x &= 0xffffu;  // (u16) truncation first, as bswap16((u16)...)
     return ((x >> 8) | (x << 8)) & 0xffffu;
@@ -139,9 +141,13 @@ struct State {
 // Phase A: classify, edit, IPv4 header checksum, in-window L4 sum.
 // Returns false to defer the packet to the generic lane (H untouched then).
 // ---------------------------------------------------------------------------
+// `part`: the window's one partly valid dword (packet bytes [4k - 2, caplen) with
+// k = (caplen + 2) / 4 < NW, the rest zeroed; 0 when there is none), which the
+// caller reads from the unedited image.  It is always L4 payload: a packet on
+// this lane has its whole L4 header inside caplen, and the header dwords are whole.
 template <u32 F>
-DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &cfg, const Knobs &kn, bool v6_ok,
-                const TE_AS_GLOBAL uint16_t *lut, State &st) {
+DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_dev_cfg_t &cfg, const Knobs &kn,
+                bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st) {
     if (caplen != len || (dir != TE_DIR_C2S && dir != TE_DIR_S2C)) return false;
     const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
     bool v6;
@@ -391,28 +397,27 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
     if (do_l4) {
         // pseudo header: csum_bytes(ip+12, 8) / csum_bytes(ip6+8, 32) + htons(proto + len)
         if (!v6) {
-            sum = wsum(H[7]) + wsum(H[8]);
+            sum = wsum_acc(H[8], wsum_acc(H[7], 0u));
         } else {
 #pragma unroll
-            for (int i = 6; i < 14; ++i) sum += wsum(H[i]);
+            for (int i = 6; i < 14; ++i) sum = wsum_acc(H[i], sum);
         }
         sum += bs16((tcp ? 6u : 17u) + l4len);
-        // L4 bytes [L4S, min(caplen, WEND)) inside the window, summed as whole dwords: a
-        // dword's 32-bit value folds to the same one's-complement sum as its two 16-bit
-        // halves (2^16 == 1 mod 0xffff), and 11 of them stay far below 2^48
-        unsigned long long s64 = 0;
+        // L4 bytes [L4S, min(caplen, WEND)) inside the window: the whole dwords
+        // (4i + 2 <= caplen) and the partly valid one.  Relative offsets 4i - 2 are
+        // even, so each dword's halves are packet-pairing 16-bit words.
 #pragma unroll
         for (int i = 9; i < NW; ++i) {
-            const int rem = (int)caplen - (4 * i - 2);  // packet bytes in dword i
-            const int r = rem < 0 ? 0 : (rem > 4 ? 4 : rem);
-            const u32 keep = r == 4 ? 0xffffffffu : ((1u << (8 * r)) - 1u);
-            s64 += H[i] & ((i >= 14 || !v6) ? keep : 0u);
+            const bool whole = caplen >= (u32)(4 * i + 2) && (i >= 14 || !v6);
+            sum = wsum_acc(whole ? H[i] : 0u, sum);
         }
-        sum += (u32)((s64 & 0xffffull) + (s64 >> 16));  // < 2^16 + 2^20
+        sum = wsum_acc(part, sum);  // < 2^16 * 32 overall
     }
     if (!v6) {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
         H[6] = with_hi16(H[6], 0);
-        u32 hs = wsum(H[4]) + wsum(H[5]) + wsum(H[6]) + wsum(H[7]) + wsum(H[8]);
+        u32 hs = 0;
+#pragma unroll
+        for (int i = 4; i < 9; ++i) hs = wsum_acc(H[i], hs);
         H[6] = with_hi16(H[6], (~fold32(hs)) & 0xffffu);
         dirty |= 1u << 6;
     }
@@ -445,7 +450,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, int dir, const te_dev_cfg_t &
 // already in the packet's relative byte pairing) and store the checksum.
 DI void phase_b(u32 (&H)[NW], const State &st, u32 tail) {
     if (!st.do_l4) return;
-    const u32 c = (~fold32(st.l4sum + tail)) & 0xffffu;  // CHECKSUM_CARRY (l4sum < 2^21, tail < 2^16)
+    const u32 c = (~fold32(st.l4sum + tail)) & 0xffffu;  // CHECKSUM_CARRY (l4sum < 2^22, tail < 2^16)
     // explicit per-index selects (a ternary on the index would move H to scratch)
     const bool t6 = st.tcp && st.v6, t4 = st.tcp && !st.v6, u6 = !st.tcp && st.v6, u4 = !st.tcp && !st.v6;
     H[18] = t6 ? with_lo16(H[18], c) : H[18];  // 54 + 16

@@ -572,6 +572,17 @@ struct FastArgs {
     uint32_t seed_sw, seed_on, skip_bcast;  // te_wave_tiles' phase-A knobs (fl::Knobs), in SGPRs
 };
 
+// the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
+// (caplen + 2) / 4, read from the unedited image at window start wa (packet offset -2);
+// 0 when caplen + 2 is a multiple of 4 or the dword lies past the window
+__device__ __forceinline__ uint32_t window_part(const uint8_t *S, uint32_t wa, uint32_t caplen) {
+    const uint32_t t = caplen + 2, k = t >> 2, nb = t & 3u;
+    const uint32_t q = (wa & ~3u) + 4u * umin32(k, fl::NW - 1);
+    const uint32_t e0 = *(const uint32_t *)(S + q), e1 = *(const uint32_t *)(S + q + 4);
+    const uint32_t keep = (nb != 0 && k < (uint32_t)fl::NW) ? ((1u << (8 * nb)) - 1u) : 0u;
+    return __builtin_amdgcn_alignbyte(e1, e0, wa & 3u) & keep;
+}
+
 // one's-complement sum of the LE 16-bit words (absolute pairing) of bytes [b0, b1) of chunk c
 __device__ __forceinline__ uint32_t chunk_part(const uint8_t *S, uint32_t c, int b0, int b1) {
     const uint4 v = *(const uint4 *)(S + 16 * c);
@@ -752,7 +763,8 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #pragma unroll
                 for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
                 d0 = e[0];
-                ok = fl::phase_a<TE_FF_ALL>(H, caplen, len, dir, cfg, fl::knobs_of(cfg), a.v6_ok != 0, lut, st);
+                ok = fl::phase_a<TE_FF_ALL>(H, caplen, len, window_part(S, wa, caplen), dir, cfg, fl::knobs_of(cfg),
+                                            a.v6_ok != 0, lut, st);
             }
         }
         {
@@ -936,6 +948,9 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 // ===========================================================================
 #ifndef TE_WK_MIN_BLOCKS
 #define TE_WK_MIN_BLOCKS 4  // blocks per CU (= waves per SIMD at 256 threads): 128 VGPRs
+#endif
+#ifndef TE_WK_STORE_BARRIER
+#define TE_WK_STORE_BARRIER 1
 #endif
 #ifndef TE_WK_LANE_OPAQUE
 #define TE_WK_LANE_OPAQUE 1
@@ -1122,6 +1137,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
             d0 = d[0];
         }
+        const uint32_t part = window_part(S, wa, caplen);
         int dir = TE_DIR_C2S;
         if (explicit_dir) {
             dir = a.fixed_dir;
@@ -1148,7 +1164,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             ok = x != 0x9e3779b9u;
             nosend = true;
 #else
-            ok = fl::phase_a<F>(H, caplen, len, dir, cfg, kn, a.v6_ok != 0, lut, st);
+            ok = fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
 #endif
         }
 #if TE_WK_ISSUE_LATE
@@ -1198,6 +1214,8 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
         uint32_t todo = 0;
         if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
         todo = wave_or(todo);
+        // every written dword ends by packet offset 78 <= caplen + 16: no per-dword test
+        const bool wide = !__ballot(on && !nosend && caplen < (uint32_t)fl::WEND - 16);
         // ---- phase B + write-back of the dwords phase A touched ----
         if (on) {
             if (!nosend) {
@@ -1207,29 +1225,18 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
                     if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
                 }
                 fl::phase_b(H, st, tail);
+                // A dword is written whole when it ends within 16 bytes past caplen: past
+                // caplen lie the next record's pcap header bytes, which no lane edits before
+                // conv_hdr (after this loop), so their original bytes go back unchanged.  A
+                // dword further out would overlap the next record's packet bytes, which its
+                // own lane may be rewriting in this same loop.
                 const uint32_t A = wa & ~3u, sh = wa & 3u;
-                uint32_t part = 0;  // dwords that straddle caplen: written bytewise below
 #pragma unroll
                 for (int j = 0; j < fl::NW; ++j) {
                     if (!((todo >> j) & 1u)) continue;
                     const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
                     const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
-                    const int rel = (int)(A + 4 * j) - (int)p;  // packet offset of the dword's first byte
-                    if (rel + 4 <= (int)caplen) *(uint32_t *)(S + A + 4 * j) = v;
-                    else if (rel < (int)caplen) part |= 1u << j;
-                }
-                if (part) {  // rare: a touched dword past the last whole one of a short packet
-#pragma unroll
-                    for (int j = 0; j < fl::NW; ++j) {
-                        if (!((part >> j) & 1u)) continue;
-                        const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
-                        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
-                        const int rel = (int)(A + 4 * j) - (int)p;
-                        uint8_t *q = S + A + 4 * j;
-#pragma unroll
-                        for (int b = 0; b < 3; ++b)
-                            if (rel + b < (int)caplen) q[b] = (uint8_t)(v >> (8 * b));
-                    }
+                    if (wide || A + 4 * j + 4 <= p + caplen + 16) *(uint32_t *)(S + A + 4 * j) = v;
                 }
             }
             if (conv) conv_hdr(S + r0, swp, nsec);
@@ -1243,13 +1250,21 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             const uint64_t C0 = (G0 + 15) & ~15ull;
             const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
             const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
-            uint4 w[WK_KL];
-#pragma unroll
-            for (int k = 0; k < WK_KL; ++k)
-                w[k] = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
-#pragma unroll
-            for (int k = 0; k < WK_KL; ++k)  // lanes past the span repeat its last chunk (same bytes)
-                *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w[k];
+            // named registers, all reads in flight before the first store (left to itself the
+            // scheduler reuses one register quad and waits out each read's LDS latency in turn)
+            uint4 w0, w1, w2, w3, w4, w5, w6, w7;
+#define WK_RD(k) \
+    if constexpr (k < WK_KL) w##k = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
+#define WK_WR(k)                                                                                   \
+    if constexpr (k < WK_KL)                                                                       \
+        *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w##k;
+            WK_EACH(WK_RD)
+#if TE_WK_STORE_BARRIER
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            WK_EACH(WK_WR)  // lanes past the span repeat its last chunk (same bytes)
+#undef WK_RD
+#undef WK_WR
             const uint32_t nlead = (uint32_t)(C0 - G0);
             const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
             gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
