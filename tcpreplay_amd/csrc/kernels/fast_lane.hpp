@@ -60,35 +60,31 @@ DI u32 bmask(int lo, int hi) {
     return mh & ~ml;
 }
 
-DI u32 sel4(const u32 *a, u32 k) { return k == 0 ? a[0] : (k == 1 ? a[1] : (k == 2 ? a[2] : a[3])); }
+// a[min(k, 3)] by masks: a ternary chain on a lane-varying k becomes a dynamically
+// indexed stack array
+DI u32 sel4(const u32 *a, u32 k) {
+    return (a[0] & (0u - (u32)(k == 0))) | (a[1] & (0u - (u32)(k == 1))) | (a[2] & (0u - (u32)(k == 2))) |
+           (a[3] & (0u - (u32)(k >= 3)));
+}
 
-// ip6_in_cidr (cidr.c:478-529) on an address held as 4 LE dwords
+// ip6_in_cidr (cidr.c:478-529) on an address held as 4 LE dwords, as one expression
+// (a /0 mask matches every address there, zero or not)
 DI bool ip6_in_cidr_w(const te_cidr_t &c, const u32 *a) {
-    if (c.family != 6) return false;
-    if (c.masklen == 0 && (a[0] | a[1] | a[2] | a[3]) == 0) return true;
-    const int j = c.masklen / 8;
+    const int j = c.masklen / 8, r = c.masklen % 8;
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < 4; ++k) ok &= ((a[k] ^ ld32(c.network6 + 4 * k)) & bmask(0, j - 4 * k)) == 0;
-    if (!ok) return false;
-    const int r = c.masklen % 8;
-    if (r == 0) return true;
     const u32 km = (0xffu << (8 - r)) & 0xffu;
     const u32 ab = (sel4(a, (u32)j >> 2) >> (8 * (j & 3))) & 0xffu;
-    return (ab & km) == (c.network6[j] & km);
+    const bool last = r == 0 || (ab & km) == (c.network6[j & 15] & km);
+    return (c.family == 6) & ok & last;
 }
 
-// remap_ipv6 (edit_packet.c:748-779) for octet masks (the host keeps the
-// non-octet out-of-range write of SURVEY Q9 on the generic lane)
-DI void remap_ipv6_w(const te_dev_cfg_t &cfg, const te_cidr_t &c, u32 *a) {
-    if (c.family != 6) return;
-    if (cfg.skip_broadcast && (a[0] & 0xffu) == 0xffu) return;
-    const int j = c.masklen / 8;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const u32 m = bmask(0, j - 4 * k);
-        a[k] = (a[k] & ~m) | (ld32(c.network6 + 4 * k) & m);
-    }
+// ip_in_cidr (cidr.c:425-468) as one expression (64-bit mask semantics)
+DI bool ip_in_cidr_f(const te_cidr_t &c, u32 ip_le) {
+    const unsigned long long mask = ~0ull << (32 - c.masklen);
+    const bool in = (((unsigned long long)bswap32(ip_le)) & mask) == (((unsigned long long)bswap32(c.network)) & mask);
+    return (c.family == 4) & (in | ((c.masklen == 0) & (c.network == 0)));
 }
 
 // randomize_ipv6_addr (edit_packet.c:359-379); s = bswap32(seed)
@@ -129,6 +125,27 @@ struct Knobs {
 };
 DI Knobs knobs_of(const te_dev_cfg_t &cfg) { return Knobs{bswap32(cfg.seed), cfg.seed != 0, cfg.skip_broadcast != 0}; }
 
+// remap_ipv6 (edit_packet.c:748-779) for octet masks (the host keeps the
+// non-octet out-of-range write of SURVEY Q9 on the generic lane)
+DI void remap_ipv6_w(const Knobs &kn, const te_cidr_t &c, u32 *a) {
+    const bool skip = (c.family != 6) | (kn.skip_bcast & ((a[0] & 0xffu) == 0xffu));
+    const int j = c.masklen / 8;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u32 m = skip ? 0u : bmask(0, j - 4 * k);
+        a[k] = (a[k] & ~m) | (ld32(c.network6 + 4 * k) & m);
+    }
+}
+
+// remap_ipv4 (edit_packet.c:713-746) as one expression; x86 masks a shift by 32 to 0
+DI u32 remap_ipv4_f(const Knobs &kn, const te_cidr_t &c, u32 orig) {
+    u32 mask = 0xffffffffu << ((32 - c.masklen) & 31);
+    const u32 network = bswap32(c.network) & mask;
+    mask ^= 0xffffffffu;
+    const u32 r = bswap32(network ^ (bswap32(orig) & mask));
+    return c.family != 4 ? 0u : ((kn.skip_bcast && mcast4(orig)) ? orig : r);
+}
+
 // what phase B needs to finish a packet after the block's chunk-prefix pass
 struct State {
     u32 l4sum;  // unfolded one's-complement sum so far (pseudo header + L4 bytes inside the window)
@@ -139,60 +156,51 @@ struct State {
 
 // ---------------------------------------------------------------------------
 // Phase A: classify, edit, IPv4 header checksum, in-window L4 sum.
-// Returns false to defer the packet to the generic lane (H untouched then).
-// ---------------------------------------------------------------------------
+// Returns false to defer the packet to the generic lane.
+//
+// The body has no lane-divergent control flow.  Every lane runs the same
+// instructions and takes its results by selects; the option blocks and the
+// IPv4 / IPv6 address blocks branch only on wave-uniform conditions (cfg fields,
+// ballots).  A lane whose packet is deferred or not edited computes values that
+// are never used: its tile goes to the generic lane, or its H is not written
+// back.  (Divergent branches around edits of H made the compiler copy the whole
+// window between register sets at every merge.)
+//
 // `part`: the window's one partly valid dword (packet bytes [4k - 2, caplen) with
 // k = (caplen + 2) / 4 < NW, the rest zeroed; 0 when there is none), which the
 // caller reads from the unedited image.  It is always L4 payload: a packet on
 // this lane has its whole L4 header inside caplen, and the header dwords are whole.
+// ---------------------------------------------------------------------------
 template <u32 F>
 DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_dev_cfg_t &cfg, const Knobs &kn,
                 bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st) {
-    if (caplen != len || (dir != TE_DIR_C2S && dir != TE_DIR_S2C)) return false;
+    // ---- classify: Ethernet II + IPv4 (IHL 5, no fragment, ip_len == caplen - 14) or
+    // IPv6 (payload length == caplen - 54), then TCP or UDP with a whole header ----
     const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
-    bool v6;
-    u32 proto, l4len;
-    if (et == 0x0008u) {  // ETHERTYPE_IP
-        if ((H[4] & 0xffu) != 0x45u) return false;
-        const u32 ip_len = bs16(hi16(H[4]));
-        if (ip_len != caplen - 14) return false;                 // Q4 warning path: generic
-        if ((bs16(hi16(H[5])) & 0x3fffu) != 0) return false;      // fragments: generic
-        proto = (H[6] >> 8) & 0xffu;
-        l4len = ip_len - 20;
-        v6 = false;
-    } else if (et == 0xDD86u) {  // ETHERTYPE_IP6
-        if (!v6_ok || ((H[4] >> 4) & 0xfu) != 6u) return false;
-        proto = (H[5] >> 16) & 0xffu;
-        const u32 plen_raw = lo16(H[5]);
-        l4len = bs16(plen_raw);
-        if (caplen < 54 || l4len != caplen - 54) return false;
-        if (caplen > 56 && plen_raw < 40) return false;  // raw network-order compare (edit_packet.c:167)
-        v6 = true;
-    } else {
-        return false;
-    }
-    bool tcp;
-    if (proto == 6) {
-        if (l4len < 20) return false;
-        tcp = true;
-    } else if (proto == 17) {
-        if (l4len < 8) return false;
-        tcp = false;
-    } else {
-        return false;
-    }
+    const u32 ip_len = bs16(hi16(H[4]));
+    const bool ok4 = (et == 0x0008u) & ((H[4] & 0xffu) == 0x45u) & (ip_len == caplen - 14) &  // Q4 warning path
+                     (ip_len >= 20) & ((bs16(hi16(H[5])) & 0x3fffu) == 0);                    // and fragments: generic
+    const u32 plen_raw = lo16(H[5]), l4len6 = bs16(plen_raw);
+    const bool v6 = et == 0xDD86u;  // ETHERTYPE_IP6
+    const bool ok6 = v6 & v6_ok & (((H[4] >> 4) & 0xfu) == 6u) & (caplen >= 54) & (l4len6 == caplen - 54) &
+                     !((caplen > 56) & (plen_raw < 40));  // raw network-order compare (edit_packet.c:167)
+    const u32 proto = v6 ? (H[5] >> 16) & 0xffu : (H[6] >> 8) & 0xffu;
+    const u32 l4len = v6 ? l4len6 : ip_len - 20;
+    const bool tcp = proto == 6;
+    const bool ok = (caplen == len) & ((dir == TE_DIR_C2S) | (dir == TE_DIR_S2C)) & (ok4 | ok6) &
+                    (tcp ? l4len >= 20 : ((proto == 17) & (l4len >= 8)));
+    const bool c2s = dir == TE_DIR_C2S;
 
     u32 dirty = 0;
     // ---- en10mb_encode: MAC rewrite (no VLAN, subsmac or mac-seed here) ----
     if ((F & F_MAC) && cfg.mac_mask) {
-        const bool c2s = dir == TE_DIR_C2S;
         const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
         unsigned long long dmac = (unsigned long long)hi16(H[0]) | ((unsigned long long)H[1] << 16);
         unsigned long long smac = (unsigned long long)H[2] | ((unsigned long long)lo16(H[3]) << 32);
         const bool use_s = (cfg.mac_mask & sm) && (!cfg.l2_skip_broadcast || unicast48(smac));
         const bool use_d = (cfg.mac_mask & dm) && (!cfg.l2_skip_broadcast || unicast48(dmac));
-        if (use_s) smac = mac48(c2s ? cfg.intf1_smac : cfg.intf2_smac);
-        if (use_d) dmac = mac48(c2s ? cfg.intf1_dmac : cfg.intf2_dmac);
+        smac = use_s ? mac48(c2s ? cfg.intf1_smac : cfg.intf2_smac) : smac;
+        dmac = use_d ? mac48(c2s ? cfg.intf1_dmac : cfg.intf2_dmac) : dmac;
         H[0] = with_hi16(H[0], (u32)dmac);
         H[1] = (u32)(dmac >> 16);
         H[2] = (u32)smac;
@@ -229,211 +237,211 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
             // merge would also drain the next tile's loads on the LDS path)
             asm volatile("" : "+v"(nd), "+v"(ns));
         }
-        if (nd != od) {
-            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)od, (u16)nd);
-            L[0] = with_hi16(L[0], nd);
-        }
-        if (ns != os) {
-            if (udp_live && ucs) ucs = csum_replace2_v((u16)ucs, (u16)os, (u16)ns);
-            L[0] = with_lo16(L[0], ns);
-        }
+        ucs = ((nd != od) & udp_live & (ucs != 0)) ? (u32)csum_replace2_v((u16)ucs, (u16)od, (u16)nd) : ucs;
+        L[0] = with_hi16(L[0], nd);
+        ucs = ((ns != os) & udp_live & (ucs != 0)) ? (u32)csum_replace2_v((u16)ucs, (u16)os, (u16)ns) : ucs;
+        L[0] = with_lo16(L[0], ns);
     }
 
-    if (!v6) {
+    constexpr bool kAddr = (F & (F_RWIP | F_SEED)) != 0;
+    const bool edit_addr = kAddr && (((F & F_RWIP) && cfg.rewrite_ip) || ((F & F_SEED) && kn.seed));
+    if (edit_addr && __ballot(!v6)) {
         u32 src = H[7], dst = H[8];
-        // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is carried
-#define FL_V4_UPD(o, n) ucs = (udp_live && ucs) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs
+        // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is
+        // carried, and only on an IPv4 lane whose address was replaced
+#define FL_V4_UPD(c, o, n) \
+    ucs = ((c) & !v6 & udp_live & (ucs != 0)) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs
         if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
-            for (int m = 0; m < cfg.n_srcipmap; ++m)
-                if (ip_in_cidr(cfg.srcipmap[m].from, src)) {
-                    const u32 o = src;
-                    src = remap_ipv4(cfg, cfg.srcipmap[m].to, o);
-                    FL_V4_UPD(o, src);
-                    break;
-                }
-            for (int m = 0; m < cfg.n_dstipmap; ++m)
-                if (ip_in_cidr(cfg.dstipmap[m].from, dst)) {
-                    const u32 o = dst;
-                    dst = remap_ipv4(cfg, cfg.dstipmap[m].to, o);
-                    FL_V4_UPD(o, dst);
-                    break;
-                }
+            bool done = false;  // the first matching entry of each list
+            for (int m = 0; m < cfg.n_srcipmap; ++m) {
+                const bool hit = !done & ip_in_cidr_f(cfg.srcipmap[m].from, src);
+                const u32 o = src, n = remap_ipv4_f(kn, cfg.srcipmap[m].to, o);
+                src = hit ? n : o;
+                FL_V4_UPD(hit, o, n);
+                done |= hit;
+            }
+            done = false;
+            for (int m = 0; m < cfg.n_dstipmap; ++m) {
+                const bool hit = !done & ip_in_cidr_f(cfg.dstipmap[m].from, dst);
+                const u32 o = dst, n = remap_ipv4_f(kn, cfg.dstipmap[m].to, o);
+                dst = hit ? n : o;
+                FL_V4_UPD(hit, o, n);
+                done |= hit;
+            }
             if (cfg.n_cidrmap1 != 0) {
-                const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
-                const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
-                const int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
-                const int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
-                int i1 = 0, i2 = 0;
-                bool didsrc = false, diddst = false;
-                for (;;) {
-                    if (!diddst && ip_in_cidr(l2[i2].from, dst)) {
-                        const u32 o = dst;
-                        dst = remap_ipv4(cfg, l2[i2].to, o);
-                        FL_V4_UPD(o, dst);
-                        diddst = true;
+                // the reference walks both lists in step, each index stopping at its list's
+                // end, until both addresses matched or both lists ran out: max(n1, n2) steps
+                const int n1 = c2s ? cfg.n_cidrmap1 : cfg.n_cidrmap2, n2 = c2s ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+                const int steps = cfg.n_cidrmap1 > cfg.n_cidrmap2 ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+                bool diddst = false, didsrc = false;
+                for (int k = 0; k < steps; ++k) {
+                    const int i1 = k < n1 - 1 ? k : (n1 > 0 ? n1 - 1 : 0);
+                    const int i2 = k < n2 - 1 ? k : (n2 > 0 ? n2 - 1 : 0);
+                    const te_cidrmap_t &e2 = c2s ? cfg.cidrmap2[i2] : cfg.cidrmap1[i2];
+                    const te_cidrmap_t &e1 = c2s ? cfg.cidrmap1[i1] : cfg.cidrmap2[i1];
+                    const bool hd = !diddst & ip_in_cidr_f(e2.from, dst);
+                    {
+                        const u32 o = dst, n = remap_ipv4_f(kn, e2.to, o);
+                        dst = hd ? n : o;
+                        FL_V4_UPD(hd, o, n);
                     }
-                    if (!didsrc && ip_in_cidr(l1[i1].from, src)) {
-                        const u32 o = src;
-                        src = remap_ipv4(cfg, l1[i1].to, o);
-                        FL_V4_UPD(o, src);
-                        didsrc = true;
+                    diddst |= hd;
+                    const bool hs = !didsrc & ip_in_cidr_f(e1.from, src);
+                    {
+                        const u32 o = src, n = remap_ipv4_f(kn, e1.to, o);
+                        src = hs ? n : o;
+                        FL_V4_UPD(hs, o, n);
                     }
-                    if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
-                        if (i1 + 1 < n1) ++i1;
-                        if (i2 + 1 < n2) ++i2;
-                    } else {
-                        break;
-                    }
+                    didsrc |= hs;
                 }
             }
         }
         if ((F & F_SEED) && kn.seed) {  // randomize_ipv4 (edit_packet.c:420-467): destination, then source
-            // branch-free: a skipped address maps to itself, and the update of an
-            // unchanged address leaves the checksum field as it is
+            // a skipped address maps to itself, and the update of an unchanged address
+            // leaves the checksum field as it is
             {
                 const u32 o = dst;
                 dst = (kn.skip_bcast && mcast4(o)) ? o : randomize_ipv4_sw(kn.seed_sw, o);
-                FL_V4_UPD(o, dst);
+                FL_V4_UPD(true, o, dst);
             }
             {
                 const u32 o = src;
                 src = (kn.skip_bcast && mcast4(o)) ? o : randomize_ipv4_sw(kn.seed_sw, o);
-                FL_V4_UPD(o, src);
+                FL_V4_UPD(true, o, src);
             }
         }
 #undef FL_V4_UPD
-        H[7] = src;
-        H[8] = dst;
-        if (((F & F_RWIP) && cfg.rewrite_ip) || ((F & F_SEED) && kn.seed)) dirty |= (1u << 7) | (1u << 8);
-    } else {
+        H[7] = v6 ? H[7] : src;
+        H[8] = v6 ? H[8] : dst;
+        dirty |= v6 ? 0u : (1u << 7) | (1u << 8);
+    }
+    if (edit_addr && __ballot(v6)) {
         u32 src[4] = {H[6], H[7], H[8], H[9]}, dst[4] = {H[10], H[11], H[12], H[13]};
         // ipv6_addr_csum_replace (edit_packet.c:298-330): only the UDP field is carried
-#define FL_V6_UPD(o, n) \
-    if (udp_live && ucs) ucs = csum_replace16_v((u16)ucs, (o), (n))
+#define FL_V6_UPD(c, o, n) \
+    ucs = ((c) & v6 & udp_live & (ucs != 0)) ? (u32)csum_replace16_v((u16)ucs, (o), (n)) : ucs
+#define FL_V6_SET(a, c, n)                                 \
+    _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) a[q_] = (c) ? n[q_] : a[q_];
         if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv6l3 (edit_packet.c:884-1019); TCP/UDP: no ICMPv6 recursion
-            for (int m = 0; m < cfg.n_srcipmap; ++m)
-                if (ip6_in_cidr_w(cfg.srcipmap[m].from, src)) {
-                    const u32 o[4] = {src[0], src[1], src[2], src[3]};
-                    remap_ipv6_w(cfg, cfg.srcipmap[m].to, src);
-                    FL_V6_UPD(o, src);
-                    break;
-                }
-            for (int m = 0; m < cfg.n_dstipmap; ++m)
-                if (ip6_in_cidr_w(cfg.dstipmap[m].from, dst)) {
-                    const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
-                    remap_ipv6_w(cfg, cfg.dstipmap[m].to, dst);
-                    FL_V6_UPD(o, dst);
-                    break;
-                }
+            bool done = false;
+            for (int m = 0; m < cfg.n_srcipmap; ++m) {
+                const bool hit = !done & ip6_in_cidr_w(cfg.srcipmap[m].from, src);
+                u32 n[4] = {src[0], src[1], src[2], src[3]};
+                remap_ipv6_w(kn, cfg.srcipmap[m].to, n);
+                FL_V6_UPD(hit, src, n);
+                FL_V6_SET(src, hit, n);
+                done |= hit;
+            }
+            done = false;
+            for (int m = 0; m < cfg.n_dstipmap; ++m) {
+                const bool hit = !done & ip6_in_cidr_w(cfg.dstipmap[m].from, dst);
+                u32 n[4] = {dst[0], dst[1], dst[2], dst[3]};
+                remap_ipv6_w(kn, cfg.dstipmap[m].to, n);
+                FL_V6_UPD(hit, dst, n);
+                FL_V6_SET(dst, hit, n);
+                done |= hit;
+            }
             if (cfg.n_cidrmap1 != 0) {
-                const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
-                const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
-                const int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
-                const int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
-                int i1 = 0, i2 = 0;
-                bool didsrc = false, diddst = false;
-                for (;;) {
-                    if (!diddst && ip6_in_cidr_w(l2[i2].from, dst)) {
-                        const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
-                        remap_ipv6_w(cfg, l2[i2].to, dst);
-                        FL_V6_UPD(o, dst);
-                        diddst = true;
+                const int n1 = c2s ? cfg.n_cidrmap1 : cfg.n_cidrmap2, n2 = c2s ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
+                const int steps = cfg.n_cidrmap1 > cfg.n_cidrmap2 ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
+                bool diddst = false, didsrc = false;
+                for (int k = 0; k < steps; ++k) {
+                    const int i1 = k < n1 - 1 ? k : (n1 > 0 ? n1 - 1 : 0);
+                    const int i2 = k < n2 - 1 ? k : (n2 > 0 ? n2 - 1 : 0);
+                    const te_cidrmap_t &e2 = c2s ? cfg.cidrmap2[i2] : cfg.cidrmap1[i2];
+                    const te_cidrmap_t &e1 = c2s ? cfg.cidrmap1[i1] : cfg.cidrmap2[i1];
+                    const bool hd = !diddst & ip6_in_cidr_w(e2.from, dst);
+                    {
+                        u32 n[4] = {dst[0], dst[1], dst[2], dst[3]};
+                        remap_ipv6_w(kn, e2.to, n);
+                        FL_V6_UPD(hd, dst, n);
+                        FL_V6_SET(dst, hd, n);
                     }
-                    if (!didsrc && ip6_in_cidr_w(l1[i1].from, src)) {
-                        const u32 o[4] = {src[0], src[1], src[2], src[3]};
-                        remap_ipv6_w(cfg, l1[i1].to, src);
-                        FL_V6_UPD(o, src);
-                        didsrc = true;
+                    diddst |= hd;
+                    const bool hs = !didsrc & ip6_in_cidr_w(e1.from, src);
+                    {
+                        u32 n[4] = {src[0], src[1], src[2], src[3]};
+                        remap_ipv6_w(kn, e1.to, n);
+                        FL_V6_UPD(hs, src, n);
+                        FL_V6_SET(src, hs, n);
                     }
-                    if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
-                        if (i1 + 1 < n1) ++i1;
-                        if (i2 + 1 < n2) ++i2;
-                    } else {
-                        break;
-                    }
+                    didsrc |= hs;
                 }
             }
         }
         if ((F & F_SEED) && kn.seed) {  // randomize_ipv6 (edit_packet.c:469-518): destination, then source
-            if (!(kn.skip_bcast && (dst[0] & 0xffu) == 0xffu)) {
-                const u32 o[4] = {dst[0], dst[1], dst[2], dst[3]};
-                randomize_ipv6_w(kn.seed_sw, dst);
-                FL_V6_UPD(o, dst);
+            {
+                const bool skip = kn.skip_bcast && (dst[0] & 0xffu) == 0xffu;
+                u32 n[4] = {dst[0], dst[1], dst[2], dst[3]};
+                randomize_ipv6_w(kn.seed_sw, n);
+                FL_V6_UPD(!skip, dst, n);
+                FL_V6_SET(dst, !skip, n);
             }
-            if (!(kn.skip_bcast && (src[0] & 0xffu) == 0xffu)) {
-                const u32 o[4] = {src[0], src[1], src[2], src[3]};
-                randomize_ipv6_w(kn.seed_sw, src);
-                FL_V6_UPD(o, src);
+            {
+                const bool skip = kn.skip_bcast && (src[0] & 0xffu) == 0xffu;
+                u32 n[4] = {src[0], src[1], src[2], src[3]};
+                randomize_ipv6_w(kn.seed_sw, n);
+                FL_V6_UPD(!skip, src, n);
+                FL_V6_SET(src, !skip, n);
             }
         }
+#undef FL_V6_SET
 #undef FL_V6_UPD
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            H[6 + i] = src[i];
-            H[10 + i] = dst[i];
+            H[6 + i] = v6 ? src[i] : H[6 + i];
+            H[10 + i] = v6 ? dst[i] : H[10 + i];
         }
-        if (((F & F_RWIP) && cfg.rewrite_ip) || ((F & F_SEED) && kn.seed)) dirty |= 0xffu << 6;
+        dirty |= v6 ? 0xffu << 6 : 0u;
     }
 
     // ---- fix_ipv4/ipv6_checksums (edit_packet.c:55-189) -> do_checksum (checksum.c:34-170) ----
     // caplen == len, not a fragment, lengths consistent: the L4 sum always runs,
     // except on a UDP field that is (still) 0 (checksum.c:115).
     const bool do_l4 = tcp || ucs != 0;
-    if (do_l4) {
-        if (tcp) L[4] = with_lo16(L[4], 0);  // th_sum (L4 + 16)
-        else ucs = 0;                         // uh_sum (L4 + 6)
-    }
+    L[4] = (do_l4 && tcp) ? with_lo16(L[4], 0) : L[4];  // th_sum (L4 + 16)
+    ucs = (do_l4 && !tcp) ? 0u : ucs;                     // uh_sum (L4 + 6)
     L[1] = with_hi16(L[1], ucs);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         H[14 + i] = (L[i] & m6) | (H[14 + i] & ~m6);
         H[9 + i] = (L[i] & ~m6) | (H[9 + i] & m6);
     }
-    {
-        const int base = v6 ? 14 : 9;  // ports (port map), UDP csum (L4+6), TCP csum (L4+16)
-        dirty |= ((((F & F_PORTMAP) && cfg.has_portmap) ? 1u : 0u) | (tcp ? 0x10u : 0x2u)) << base;
+    // ports (port map), UDP csum (L4+6), TCP csum (L4+16)
+    dirty |= ((((F & F_PORTMAP) && cfg.has_portmap) ? 1u : 0u) | (tcp ? 0x10u : 0x2u)) << (v6 ? 14 : 9);
+    // pseudo header: csum_bytes(ip+12, 8) / csum_bytes(ip6+8, 32) + htons(proto + len)
+    u32 sum = wsum_acc(H[8], wsum_acc(H[7], 0u));
+    if (__ballot(v6)) {
+        u32 s6 = 0;
+#pragma unroll
+        for (int i = 6; i < 14; ++i) s6 = wsum_acc(H[i], s6);
+        sum = v6 ? s6 : sum;
     }
-    u32 sum = 0;
-    if (do_l4) {
-        // pseudo header: csum_bytes(ip+12, 8) / csum_bytes(ip6+8, 32) + htons(proto + len)
-        if (!v6) {
-            sum = wsum_acc(H[8], wsum_acc(H[7], 0u));
-        } else {
+    sum += bs16((tcp ? 6u : 17u) + l4len);
+    // L4 bytes [L4S, min(caplen, WEND)) inside the window: the whole dwords
+    // (4i + 2 <= caplen) and the partly valid one.  Relative offsets 4i - 2 are
+    // even, so each dword's halves are packet-pairing 16-bit words.
 #pragma unroll
-            for (int i = 6; i < 14; ++i) sum = wsum_acc(H[i], sum);
-        }
-        sum += bs16((tcp ? 6u : 17u) + l4len);
-        // L4 bytes [L4S, min(caplen, WEND)) inside the window: the whole dwords
-        // (4i + 2 <= caplen) and the partly valid one.  Relative offsets 4i - 2 are
-        // even, so each dword's halves are packet-pairing 16-bit words.
-#pragma unroll
-        for (int i = 9; i < NW; ++i) {
-            const bool whole = caplen >= (u32)(4 * i + 2) && (i >= 14 || !v6);
-            sum = wsum_acc(whole ? H[i] : 0u, sum);
-        }
-        sum = wsum_acc(part, sum);  // < 2^16 * 32 overall
+    for (int i = 9; i < NW; ++i) {
+        const bool whole = caplen >= (u32)(4 * i + 2) && (i >= 14 || !v6);
+        sum = wsum_acc(whole ? H[i] : 0u, sum);
     }
-    if (!v6) {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
-        H[6] = with_hi16(H[6], 0);
-        u32 hs = 0;
-#pragma unroll
-        for (int i = 4; i < 9; ++i) hs = wsum_acc(H[i], hs);
-        H[6] = with_hi16(H[6], (~fold32(hs)) & 0xffffu);
-        dirty |= 1u << 6;
+    sum = wsum_acc(part, sum);  // < 2^16 * 32 overall
+    {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
+        const u32 h6 = with_hi16(H[6], 0);
+        const u32 hs = wsum_acc(H[8], wsum_acc(H[7], wsum_acc(h6, wsum_acc(H[5], wsum_acc(H[4], 0u)))));
+        H[6] = v6 ? H[6] : with_hi16(h6, (~fold32(hs)) & 0xffffu);
+        dirty |= v6 ? 0u : 1u << 6;
     }
 
     // ---- dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC ----
-    if (!v6) {
+    {
         const u32 d = H[8];
-        if (mcast4(d)) {
-            H[0] = with_hi16(H[0], 0x0001u);                                         // 01:00
-            H[1] = 0x5eu | (((d >> 8) & 0x7fu) << 8) | (((d >> 16) & 0xffu) << 16) | ((d >> 24) << 24);
-            dirty |= 3u;
-        }
-    } else if ((H[10] & 0xffu) == 0xffu) {
-        H[0] = with_hi16(H[0], 0x3333u);
-        H[1] = H[13];
-        dirty |= 3u;
+        const bool mc4 = !v6 && mcast4(d), mc6 = v6 && (H[10] & 0xffu) == 0xffu;
+        const u32 h1_4 = 0x5eu | (((d >> 8) & 0x7fu) << 8) | (((d >> 16) & 0xffu) << 16) | ((d >> 24) << 24);
+        H[0] = mc4 ? with_hi16(H[0], 0x0001u) : (mc6 ? with_hi16(H[0], 0x3333u) : H[0]);  // 01:00 / 33:33
+        H[1] = mc4 ? h1_4 : (mc6 ? H[13] : H[1]);
+        dirty |= (mc4 || mc6) ? 3u : 0u;
     }
 
     st.l4sum = sum;
@@ -443,7 +451,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     st.tcp = tcp;
     st.do_l4 = do_l4;
     st.tail = do_l4 && caplen > (u32)WEND;
-    return true;
+    return ok;
 }
 
 // Phase B: add the L4 bytes past the window (one's-complement sum `tail`,

@@ -1005,7 +1005,7 @@ __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     st32(rec + 12, ln);
 }
 
-template <uint32_t F>
+template <uint32_t F, int DEPTH>
 __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
     __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
@@ -1037,252 +1037,274 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     const fl::Knobs kn{a.seed_sw, a.seed_on != 0, a.skip_bcast != 0};
     __syncthreads();
 
-    // the next tile's chunks in flight, in named registers
-    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+    // a tile in flight: its descriptor, its chunks in named registers, and this lane's
+    // record offset and tcpprep cache byte
+    struct Span {
+        te_tile_t tl;
+        uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+        uint32_t rel, dirb;
+        bool dirv;  // (the cache byte exists: idx < dirbits_len)
+    };
 #define WK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
-#define WK_LD(k)                                                           \
-    if constexpr (k < WK_KL) {                                             \
-        const uint32_t c = umin32((uint32_t)lane + k * 64u, nc_ - 1u);     \
-        v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));                 \
-    }
-#define WK_ISSUE(tl)                                                                                        \
-    {                                                                                                       \
-        const uint64_t a0_ = (tl).span_off & ~15ull;                                                        \
-        const uint32_t nc_ =                                                                                \
-            wk_solo(tl) ? 1u : (uint32_t)(((tl).span_off + (tl).span_len + extra - a0_ + 15) >> 4);         \
-        WK_EACH(WK_LD)                                                                                      \
-        const uint32_t k_ = (tl).first_pkt + umin32((uint32_t)lane, (tl).npkt - 1u);                       \
-        rel_next = pkt_rel[k_];                                                                             \
-        if (a.dirbits) { /* this lane's tcpprep cache byte, in flight with the span (no consumer */        \
-            const uint64_t ix_ = (a.pkt_base + k_) >> 2; /* here: its wait would drain the span) */        \
-            dirb_next = a.dirbits[ix_ < a.dirbits_len ? ix_ : 0];                                           \
-            dirv_next = ix_ < a.dirbits_len;                                                                \
-        }                                                                                                   \
-    }
-// the whole image, unconditionally: chunks past the span land past it (never read as data)
-#define WK_ST(k) \
-    if constexpr (k < WK_KL) *(uint4 *)(S + LDS_FRONT + (((uint32_t)lane + k * 64u) << 4)) = v##k;
     const uint32_t W = gridDim.x * WK_NW;
     const uint32_t w0 = blockIdx.x * WK_NW + wid;
-    te_tile_t cur, nxt;
-    uint32_t rel_next = 0;  // this lane's record offset in the tile whose chunks are in flight
-    uint32_t dirb_next = 0; // ... and its tcpprep cache byte
-    bool dirv_next = false; // (which exists: idx < dirbits_len)
-    if (w0 < a.n_tiles) {
-        cur = tiles[w0];
-        WK_ISSUE(cur);
-        WK_EACH(WK_ST)
-    }
-    if (w0 + W < a.n_tiles) nxt = tiles[w0 + W];
+    const uint32_t n_tiles = a.n_tiles;
     unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
 #if TE_WK_STAMPS
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
 #endif
-    for (uint32_t t = w0; t < a.n_tiles; t += W) {
+
+    // loads of a tile's span (its chunks, record offsets and cache bytes) into R
+    auto issue = [&](Span &R, const te_tile_t &tl) __attribute__((always_inline)) {
+        R.tl = tl;
+        const uint64_t a0_ = tl.span_off & ~15ull;
+        const uint32_t nc_ = wk_solo(tl) ? 1u : (uint32_t)((tl.span_off + tl.span_len + extra - a0_ + 15) >> 4);
+#define WK_LD(k)                                                           \
+    if constexpr (k < WK_KL) {                                             \
+        const uint32_t c = umin32((uint32_t)lane + k * 64u, nc_ - 1u);     \
+        R.v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));               \
+    }
+        WK_EACH(WK_LD)
+#undef WK_LD
+        const uint32_t k_ = tl.first_pkt + umin32((uint32_t)lane, tl.npkt - 1u);
+        R.rel = pkt_rel[k_];
+        if (a.dirbits) {  // in flight with the span (no consumer here: its wait would drain the span)
+            const uint64_t ix_ = (a.pkt_base + k_) >> 2;
+            R.dirb = a.dirbits[ix_ < a.dirbits_len ? ix_ : 0];
+            R.dirv = ix_ < a.dirbits_len;
+        } else {
+            R.dirb = 0;
+            R.dirv = false;
+        }
+    };
+    // R's chunks -> the LDS image, the whole image unconditionally: chunks past the span
+    // land past it (never read as data).  Waits for R's loads only.
+    auto fill = [&](const Span &R) __attribute__((always_inline)) {
+#define WK_ST(k) \
+    if constexpr (k < WK_KL) *(uint4 *)(S + LDS_FRONT + (((uint32_t)lane + k * 64u) << 4)) = R.v##k;
+        WK_EACH(WK_ST)
+#undef WK_ST
+    };
+    // edit and store tile t, whose span is in the LDS image; a tile the lane cannot
+    // finish is listed for the generic lane and stores nothing
+    auto edit = [&](const uint32_t t, const te_tile_t &tile, const uint32_t my_rel, const uint32_t my_dirb,
+                    const bool my_dirv) __attribute__((always_inline)) {
+            const uint32_t npkt = tile.npkt;
+            const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
+            const uint32_t g0 = (uint32_t)(G0 - A0);
+            if (wk_solo(tile)) {  // a record larger than the image: the generic lane
+                if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                return;
+            }
+
+            // ---- phase A: one lane per packet ----
+            const uint32_t r0 = LDS_FRONT + g0 + my_rel;  // record header in S
+            const uint32_t p = r0 + 16;                   // packet data in S
+            const uint32_t wa = p - 2;                    // window start (packet offset -2)
+            const bool on = lane < (int)npkt;
+            // every lane reads a header and a window (lanes past npkt: the tile's last
+            // record's), so H has one definition and no lane-dependent merge copies
+            uint32_t caplen, len;
+            {  // caplen, len: three aligned dword reads + funnel shifts
+                const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
+                const uint32_t q0 = *(const uint32_t *)(S + ha), q1 = *(const uint32_t *)(S + ha + 4),
+                               q2 = *(const uint32_t *)(S + ha + 8);
+                caplen = __builtin_amdgcn_alignbyte(q1, q0, hs);
+                len = __builtin_amdgcn_alignbyte(q2, q1, hs);
+                if (swp) {
+                    caplen = bswap32(caplen);
+                    len = bswap32(len);
+                }
+            }
+            // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
+            // the window to packet offset -2; each H[i] can take d[i]'s register
+            uint32_t H[fl::NW], d0;
+            {
+                const uint32_t A4 = wa & ~3u, sh = wa & 3u;
+                uint32_t d[fl::NW + 1];
+#pragma unroll
+                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
+#pragma unroll
+                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                d0 = d[0];
+            }
+            const uint32_t part = window_part(S, wa, caplen);
+            int dir = TE_DIR_C2S;
+            if (explicit_dir) {
+                dir = a.fixed_dir;
+            } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354), byte loaded with the span
+                const uint64_t pktno = a.pkt_base + tile.first_pkt + lane;
+                const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+                const uint32_t b = my_dirv ? my_dirb : 0u;
+                dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+            }
+#if TE_WK_EXP == 1  // diagnostics only: the skeleton without the edit (output = input)
+            dir = TE_DIR_NOSEND;
+#endif
+            // tcprewrite.c:314-315: a record the cache says not to send is written unedited
+            bool nosend = on && dir == TE_DIR_NOSEND && !explicit_dir;
+            fl::State st;
+            st.do_l4 = st.tail = false;
+            st.dirty = 0;
+            // phase A runs on every lane (it has no divergent branches); only lanes that edit
+            // a packet keep its verdict and state
+            const bool edit = on && !nosend;
+#if TE_WK_EXP == 2  // diagnostics only: window reads, no edit
+            bool ok = true;
+            {
+                uint32_t x = 0;
+#pragma unroll
+                for (int i = 0; i < fl::NW; ++i) x ^= H[i];
+                ok = x != 0x9e3779b9u;
+                nosend = true;
+            }
+#else
+            bool ok = fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
+            ok = ok || !edit;
+            st.tail = st.tail && edit;
+#endif
+            if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
+                if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                return;
+            }
+
+            WK_STAMP(1)  // phase A
+            // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
+            if (__ballot(st.tail)) {
+                const uint32_t nch = (LDS_FRONT + g0 + tile.span_len + 15) >> 4;  // <= 64 * WK_KL
+                uint32_t loc[WK_KL], tot = 0;
+#pragma unroll
+                for (int q = 0; q < WK_KL; ++q) {  // lane owns chunks [lane * KL, lane * KL + KL)
+                    const uint32_t c = (uint32_t)lane * WK_KL + q;
+                    uint32_t s = 0;
+                    if (c < nch) {
+                        const uint4 v = *(const uint4 *)(S + 16 * c);
+                        s = fl::wsum(v.x) + fl::wsum(v.y) + fl::wsum(v.z) + fl::wsum(v.w);
+                    }
+                    loc[q] = tot;
+                    tot += s;
+                }
+                uint32_t incl = tot;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const uint32_t base = incl - tot;
+#pragma unroll
+                for (int q = 0; q < WK_KL; ++q) {
+                    const uint32_t c = (uint32_t)lane * WK_KL + q;
+                    if (c < nch) P[c] = base + loc[q];
+                }
+                if (lane == 63) P[nch] = incl;
+            }
+
+            WK_STAMP(2)  // chunk prefix
+            // LDS dwords any lane writes back, as one wave-uniform mask: the per-dword tests
+            // below are scalar branches.  A lane that did not change such a dword rewrites
+            // it with its own packet's bytes (never past caplen), which is harmless.
+            uint32_t todo = 0;
+            if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
+            todo = wave_or(todo);
+            // every written dword ends by packet offset 78 <= caplen + 16: no per-dword test
+            const bool wide = !__ballot(on && !nosend && caplen < (uint32_t)fl::WEND - 16);
+            // ---- phase B + write-back of the dwords phase A touched ----
+            if (on) {
+                if (!nosend) {
+                    uint32_t tail = 0;
+                    if (st.tail) {
+                        tail = lds_range_sum(S, P, p + fl::WEND, p + st.end);
+                        if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
+                    }
+                    fl::phase_b(H, st, tail);
+                    // A dword is written whole when it ends within 16 bytes past caplen: past
+                    // caplen lie the next record's pcap header bytes, which no lane edits before
+                    // conv_hdr (after this loop), so their original bytes go back unchanged.  A
+                    // dword further out would overlap the next record's packet bytes, which its
+                    // own lane may be rewriting in this same loop.
+                    const uint32_t A = wa & ~3u, sh = wa & 3u;
+#pragma unroll
+                    for (int j = 0; j < fl::NW; ++j) {
+                        if (!((todo >> j) & 1u)) continue;
+                        const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
+                        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
+                        if (wide || A + 4 * j + 4 <= p + caplen + 16) *(uint32_t *)(S + A + 4 * j) = v;
+                    }
+                }
+                if (conv) conv_hdr(S + r0, swp, nsec);
+                ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
+            }
+            if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
+
+            WK_STAMP(3)  // phase B
+            // ---- store: the chunks that start in the span, then the leading bytes ----
+            {
+                const uint64_t C0 = (G0 + 15) & ~15ull;
+                const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
+                const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
+                // named registers, all reads in flight before the first store (left to itself the
+                // scheduler reuses one register quad and waits out each read's LDS latency in turn)
+                uint4 w0, w1, w2, w3, w4, w5, w6, w7;
+#define WK_RD(k) \
+        if constexpr (k < WK_KL) w##k = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
+#define WK_WR(k)                                                                                   \
+        if constexpr (k < WK_KL)                                                                       \
+            *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w##k;
+                WK_EACH(WK_RD)
+#if TE_WK_STORE_BARRIER
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                WK_EACH(WK_WR)  // lanes past the span repeat its last chunk (same bytes)
+#undef WK_RD
+#undef WK_WR
+                const uint32_t nlead = (uint32_t)(C0 - G0);
+                const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
+                gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
+            }
+#if TE_WK_STAMPS
+            ++ntl;
+#endif
+            const uint32_t n_nosend = (uint32_t)__popcll(__ballot(nosend));
+            c_pkts += npkt;
+            c_bytes += tile.span_len;
+            c_edited += npkt - n_nosend;
+    };
+    // one tile with DEPTH spans in flight.  Rf holds tile t's descriptor and per-lane
+    // values (its chunks are in LDS already) and is reloaded with tile t + DEPTH * W;
+    // Rn (DEPTH 2: tile t + W, in flight; DEPTH 1: Rf itself) goes to LDS after the store.
+    te_tile_t dpre;  // descriptor of the next tile to issue
+    auto step = [&](const uint32_t t, Span &Rf, Span &Rn) __attribute__((always_inline)) {
 #if TE_WK_LANE_OPAQUE
         // lane-derived addresses are recomputed per tile instead of being hoisted out of
         // the loop and kept (or spilled) across it
         asm volatile("" : "+v"(lane));
 #endif
-        const te_tile_t tile = cur;
-        const uint32_t my_rel = rel_next, my_dirb = dirb_next;
-        const bool my_dirv = dirv_next;
-        const bool more = t + W < a.n_tiles;
-        cur = nxt;
-#if !TE_WK_ISSUE_LATE
-        if (more) WK_ISSUE(cur);  // in flight while this tile is edited and stored
-#endif
-        if (t + 2 * W < a.n_tiles) nxt = tiles[t + 2 * W];
-        WK_STAMP(0)  // loop top + next tile's loads issued
-        const uint32_t npkt = tile.npkt;
-        const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
-        const uint32_t g0 = (uint32_t)(G0 - A0);
-        if (wk_solo(tile)) {  // a record larger than the image: the generic lane
-            if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
-#if TE_WK_ISSUE_LATE
-            if (more) WK_ISSUE(cur);
-#endif
-            if (more) WK_EACH(WK_ST)
-            continue;
-        }
-
-        // ---- phase A: one lane per packet ----
-        const uint32_t r0 = LDS_FRONT + g0 + my_rel;  // record header in S
-        const uint32_t p = r0 + 16;                   // packet data in S
-        const uint32_t wa = p - 2;                    // window start (packet offset -2)
-        const bool on = lane < (int)npkt;
-        // every lane reads a header and a window (lanes past npkt: the tile's last
-        // record's), so H has one definition and no lane-dependent merge copies
-        uint32_t caplen, len;
-        {  // caplen, len: three aligned dword reads + funnel shifts
-            const uint32_t h8 = r0 + 8, ha = h8 & ~3u, hs = h8 & 3u;
-            const uint32_t q0 = *(const uint32_t *)(S + ha), q1 = *(const uint32_t *)(S + ha + 4),
-                           q2 = *(const uint32_t *)(S + ha + 8);
-            caplen = __builtin_amdgcn_alignbyte(q1, q0, hs);
-            len = __builtin_amdgcn_alignbyte(q2, q1, hs);
-            if (swp) {
-                caplen = bswap32(caplen);
-                len = bswap32(len);
-            }
-        }
-        // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
-        // the window to packet offset -2; each H[i] can take d[i]'s register
-        uint32_t H[fl::NW], d0;
-        {
-            const uint32_t A4 = wa & ~3u, sh = wa & 3u;
-            uint32_t d[fl::NW + 1];
-#pragma unroll
-            for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
-#pragma unroll
-            for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-            d0 = d[0];
-        }
-        const uint32_t part = window_part(S, wa, caplen);
-        int dir = TE_DIR_C2S;
-        if (explicit_dir) {
-            dir = a.fixed_dir;
-        } else if (a.dirbits) {  // check_cache (src/common/cache.c:321-354), byte loaded with the span
-            const uint64_t pktno = a.pkt_base + tile.first_pkt + lane;
-            const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
-            const uint32_t b = my_dirv ? my_dirb : 0u;
-            dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
-        }
-#if TE_WK_EXP == 1  // diagnostics only: the skeleton without the edit (output = input)
-        dir = TE_DIR_NOSEND;
-#endif
-        // tcprewrite.c:314-315: a record the cache says not to send is written unedited
-        bool nosend = on && dir == TE_DIR_NOSEND && !explicit_dir;
-        fl::State st;
-        st.do_l4 = st.tail = false;
-        st.dirty = 0;
-        bool ok = true;
-        if (on && !nosend) {
-#if TE_WK_EXP == 2  // diagnostics only: window reads, no edit
-            uint32_t x = 0;
-#pragma unroll
-            for (int i = 0; i < fl::NW; ++i) x ^= H[i];
-            ok = x != 0x9e3779b9u;
-            nosend = true;
-#else
-            ok = fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
-#endif
-        }
-#if TE_WK_ISSUE_LATE
-        if (more) WK_ISSUE(cur);  // in flight while this tile is finished and stored
-#endif
-        if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
-            if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
-            if (more) WK_EACH(WK_ST)
-            continue;
-        }
-
-        WK_STAMP(1)  // phase A
-        // ---- chunk prefix for L4 bytes past the windows (large packets only) ----
-        if (__ballot(st.tail)) {
-            const uint32_t nch = (LDS_FRONT + g0 + tile.span_len + 15) >> 4;  // <= 64 * WK_KL
-            uint32_t loc[WK_KL], tot = 0;
-#pragma unroll
-            for (int q = 0; q < WK_KL; ++q) {  // lane owns chunks [lane * KL, lane * KL + KL)
-                const uint32_t c = (uint32_t)lane * WK_KL + q;
-                uint32_t s = 0;
-                if (c < nch) {
-                    const uint4 v = *(const uint4 *)(S + 16 * c);
-                    s = fl::wsum(v.x) + fl::wsum(v.y) + fl::wsum(v.z) + fl::wsum(v.w);
-                }
-                loc[q] = tot;
-                tot += s;
-            }
-            uint32_t incl = tot;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
-            }
-            const uint32_t base = incl - tot;
-#pragma unroll
-            for (int q = 0; q < WK_KL; ++q) {
-                const uint32_t c = (uint32_t)lane * WK_KL + q;
-                if (c < nch) P[c] = base + loc[q];
-            }
-            if (lane == 63) P[nch] = incl;
-        }
-
-        WK_STAMP(2)  // chunk prefix
-        // LDS dwords any lane writes back, as one wave-uniform mask: the per-dword tests
-        // below are scalar branches.  A lane that did not change such a dword rewrites
-        // it with its own packet's bytes (never past caplen), which is harmless.
-        uint32_t todo = 0;
-        if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
-        todo = wave_or(todo);
-        // every written dword ends by packet offset 78 <= caplen + 16: no per-dword test
-        const bool wide = !__ballot(on && !nosend && caplen < (uint32_t)fl::WEND - 16);
-        // ---- phase B + write-back of the dwords phase A touched ----
-        if (on) {
-            if (!nosend) {
-                uint32_t tail = 0;
-                if (st.tail) {
-                    tail = lds_range_sum(S, P, p + fl::WEND, p + st.end);
-                    if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
-                }
-                fl::phase_b(H, st, tail);
-                // A dword is written whole when it ends within 16 bytes past caplen: past
-                // caplen lie the next record's pcap header bytes, which no lane edits before
-                // conv_hdr (after this loop), so their original bytes go back unchanged.  A
-                // dword further out would overlap the next record's packet bytes, which its
-                // own lane may be rewriting in this same loop.
-                const uint32_t A = wa & ~3u, sh = wa & 3u;
-#pragma unroll
-                for (int j = 0; j < fl::NW; ++j) {
-                    if (!((todo >> j) & 1u)) continue;
-                    const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
-                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
-                    if (wide || A + 4 * j + 4 <= p + caplen + 16) *(uint32_t *)(S + A + 4 * j) = v;
-                }
-            }
-            if (conv) conv_hdr(S + r0, swp, nsec);
-            ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
-        }
-        if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
-
-        WK_STAMP(3)  // phase B
-        // ---- store: the chunks that start in the span, then the leading bytes ----
-        {
-            const uint64_t C0 = (G0 + 15) & ~15ull;
-            const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
-            const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
-            // named registers, all reads in flight before the first store (left to itself the
-            // scheduler reuses one register quad and waits out each read's LDS latency in turn)
-            uint4 w0, w1, w2, w3, w4, w5, w6, w7;
-#define WK_RD(k) \
-    if constexpr (k < WK_KL) w##k = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
-#define WK_WR(k)                                                                                   \
-    if constexpr (k < WK_KL)                                                                       \
-        *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w##k;
-            WK_EACH(WK_RD)
-#if TE_WK_STORE_BARRIER
-            __builtin_amdgcn_sched_barrier(0);
-#endif
-            WK_EACH(WK_WR)  // lanes past the span repeat its last chunk (same bytes)
-#undef WK_RD
-#undef WK_WR
-            const uint32_t nlead = (uint32_t)(C0 - G0);
-            const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
-            gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
-        }
+        const te_tile_t tile = Rf.tl;
+        const uint32_t my_rel = Rf.rel, my_dirb = Rf.dirb;
+        const bool my_dirv = Rf.dirv;
+        if (t + DEPTH * W < n_tiles) issue(Rf, dpre);  // in flight while this tile is edited and stored
+        if (t + (DEPTH + 1) * W < n_tiles) dpre = tiles[t + (DEPTH + 1) * W];
+        WK_STAMP(0)  // loop top + loads issued
+        edit(t, tile, my_rel, my_dirb, my_dirv);
         WK_STAMP(4)  // stores issued
-        if (more) WK_EACH(WK_ST)
+        if (t + W < n_tiles) fill(Rn);
         WK_STAMP(5)  // next span -> LDS (waits for its loads)
-#if TE_WK_STAMPS
-        ++ntl;
-#endif
-        const uint32_t n_nosend = (uint32_t)__popcll(__ballot(nosend));
-        c_pkts += npkt;
-        c_bytes += tile.span_len;
-        c_edited += npkt - n_nosend;
+    };
+
+    Span RA, RB;
+    if (w0 < n_tiles) issue(RA, tiles[w0]);
+    if (DEPTH == 2 && w0 + W < n_tiles) issue(RB, tiles[w0 + W]);
+    if (w0 < n_tiles) fill(RA);
+    if (w0 + DEPTH * W < n_tiles) dpre = tiles[w0 + DEPTH * W];
+    if constexpr (DEPTH == 1) {
+        for (uint32_t t = w0; t < n_tiles; t += W) step(t, RA, RA);
+    } else {
+        for (uint32_t t = w0; t < n_tiles; t += 2 * W) {
+            step(t, RA, RB);
+            if (t + W >= n_tiles) break;
+            step(t + W, RB, RA);
+        }
     }
-#undef WK_ISSUE
-#undef WK_LD
-#undef WK_ST
 #undef WK_EACH
 #if TE_WK_STAMPS
     if (lane == 0 && wid == 0 && (blockIdx.x % 128) == 0)
@@ -1341,12 +1363,19 @@ extern "C" int te_fast_grid(void) {
 
 // the te_wave_tiles instances built (TE_FF_* masks), smallest first: a launch takes
 // the first whose mask covers the config's option groups
-#define TE_WAVE_INSTANCES(X) X(0u) X(TE_FF_SEED) X(TE_FF_PORTMAP | TE_FF_RWIP) X(TE_FF_ALL)
+// TE_WK_DEPTH_LEAN=2 gives the lean instances two spans in flight per wave (their
+// registers allow it at 4 waves per SIMD).  Measured on MI355X: C2 -0.6 %, C5 +2.5 %
+// time, so one span is the default.
+#ifndef TE_WK_DEPTH_LEAN
+#define TE_WK_DEPTH_LEAN 1
+#endif
+#define TE_WAVE_INSTANCES(X) \
+    X(0u, TE_WK_DEPTH_LEAN) X(TE_FF_SEED, TE_WK_DEPTH_LEAN) X(TE_FF_PORTMAP | TE_FF_RWIP, 1) X(TE_FF_ALL, 1)
 static const struct {
     uint32_t feat;
     const void *fn;
 } wave_inst[] = {
-#define TE_WI(f) {f, (const void *)te_wave_tiles<f>},
+#define TE_WI(f, d) {f, (const void *)te_wave_tiles<f, d>},
     TE_WAVE_INSTANCES(TE_WI)
 #undef TE_WI
 };
@@ -1361,7 +1390,7 @@ extern "C" int te_wave_grid(void) {
     if (c) return c;
     int cus = cu_count(), per_cu = 0;
     if (!cus) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL>, WKB, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL, 1>, WKB, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     c = cus * per_cu;
     return c;
