@@ -46,6 +46,11 @@ struct tcpedit_batch_s {
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
     int slot_layout;
     int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
+    int grow_off;            /* a run found a record that broke static_grow placement ... */
+    uint32_t grow_off_gen;   /* ... under this cfg_gen: place by scan from then on */
+    int last_grow;           /* the last launch placed records by static_grow */
+    int grow_never;          /* pipelined chunk slots: no rerun on a violation, so always scan */
+    uint32_t grow_bad;       /* its violation word, read back */
     int fast_tiles;          /* tiles were cut for the fast lane ... */
     int fast_kind;           /* ... of this kind (TE_FAST_BLOCK / TE_FAST_WAVE budgets) */
     uint64_t launches;       /* parity selects the fast lane's tile-list count */
@@ -82,6 +87,7 @@ struct tcpedit_batch_s {
 #define WS_ERR 0
 #define WS_ZERO 0
 #define WS_TICKET 24
+#define WS_GROW_BAD 28   /* u32: a record broke static_grow placement (zeroed with the error words) */
 #define WS_COUNTERS 32   /* counter set 0 (TE_CNT__N words) */
 #define WS_COUNTERS1 128 /* counter set 1: the fast lane alternates sets by launch parity */
 #define WS_STATE 256
@@ -105,6 +111,16 @@ static int fast_capable(const te_dev_cfg_t *c)
            c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
 
+/* VLAN add as the only size change, on the wave lane (static +4 placement): the other
+ * fast-lane conditions, and a tag to push (an untagged frame without one is an error) */
+static int fast_capable_grow(const te_dev_cfg_t *c)
+{
+    return c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
+           !c->mtu_truncate && !c->skip_soft_errors && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 &&
+           c->tclass < 0 && c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 &&
+           !c->random_set;
+}
+
 /* IPv6 rewrites with a non-octet target mask keep the reference's stray write
  * (SURVEY Q9): those packets stay on the generic lane */
 static int fast_v6_ok(const te_dev_cfg_t *c)
@@ -116,6 +132,13 @@ static int fast_v6_ok(const te_dev_cfg_t *c)
             if (lists[l][i].to.family == 6 && lists[l][i].to.masklen % 8)
                 return 0;
     return 1;
+}
+
+/* TCPEDIT_HIP_NO_GROW=1 places VLAN-add outputs by scan + look-back (A/B checks) */
+static int grow_off_env(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_NO_GROW");
+    return e && *e && strcmp(e, "0") != 0;
 }
 
 /* TCPEDIT_HIP_FAST_KIND=block selects te_fast_tiles (one block per tile) for A/B
@@ -156,7 +179,11 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
     const int slot_mode = pad || t->cfg.vlan == TE_VLAN_ADD;
     b->slot_layout = slot_mode;
-    b->fast_tiles = !slot_mode && fast_capable(&t->cfg);
+    /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
+       are cut to the wave image (their per-record slots then fit the generic kernel's) */
+    const int grow_fast = !pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
+                          fast_kind_pref() == TE_FAST_WAVE;
+    b->fast_tiles = (!slot_mode && fast_capable(&t->cfg)) || grow_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
     const int wave = b->fast_kind == TE_FAST_WAVE;
     const uint32_t budget = wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
@@ -213,7 +240,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         uint32_t g = (uint32_t)(off & 15);
         uint32_t slot = TE_SLOT_BYTES_OF(g, data);
         int huge, fits;
-        if (slot_mode) {
+        if (slot_mode && !grow_fast) {
             huge = slot > TE_SLOT_BYTES;
             fits = open && cur_slots + slot <= TE_SLOT_BYTES;
         } else {
@@ -222,7 +249,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         }
         /* wave lane: a record too large for a wave image but not for the generic kernel's
            LDS slot is a tile of its own, left to the generic kernel (no HBM scratch) */
-        const int solo = huge && wave && TE_CONTIG_FITS(g, 16 + caplen);
+        const int solo = huge && wave && (slot_mode ? slot <= TE_SLOT_BYTES : TE_CONTIG_FITS(g, 16 + caplen));
         if (solo)
             huge = 0;
         if (open && (huge || solo || cur.npkt >= max_pkts || !fits)) {
@@ -492,7 +519,15 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     const te_dev_cfg_t *c = &t->cfg;
     L.static_off = !b->slot_layout && static_capable(c) && !b->has_zero_cap;
     L.rec0 = 24;
-    L.fast = L.static_off && b->fast_tiles && fast_capable(c) && !fast_lane_off();
+    /* VLAN add as the only size change: every record grows by 4 bytes or is a hard error
+       (dlt_en10mb_encode, en10mb.c:520-575), so outputs sit at input offset + 4 x index */
+    L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
+                    !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap &&
+                    !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env();
+    L.grow_bad = (uint32_t *)(b->d_ws + WS_GROW_BAD);
+    b->last_grow = L.static_grow;
+    L.fast = b->fast_tiles && !fast_lane_off() &&
+             ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)));
     L.fast_v6 = fast_v6_ok(c);
     L.fast_kind = b->fast_kind;
     L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
@@ -550,7 +585,26 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
                                  hipMemcpyDeviceToHost, t->stream));
     }
+    if (b->last_grow)
+        HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    if (b->last_grow && b->grow_bad) {
+        /* a record did not grow by exactly 4 bytes: place this batch by scan + look-back
+           from now on, and run it again that way */
+        b->grow_off = 1;
+        b->grow_off_gen = t->cfg_gen;
+        b->grow_bad = 0;
+        if (launch(b, fixed_dir) != 0) {
+            te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return TCPEDIT_ERROR;
+        }
+        HIPCHK(t, hipEventRecord(b->ev1, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+    }
     if (b->last_fast && b->last_skipped && b->last_listed) {
         /* the hint was wrong (it cannot be for the same image and config): run the
            generic pass now and read the counters and error words again */
@@ -569,7 +623,7 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
-        b->counters[TE_CNT_BYTES_OUT] += v[1];
+        b->counters[TE_CNT_BYTES_OUT] += v[1] + (b->last_grow ? 4 * v[0] : 0); /* + the pushed tags */
         b->counters[TE_CNT_EDITED] += v[2];
     }
     if (b->last_fast) { /* same batch + same config lists the same tiles next time */
@@ -862,6 +916,7 @@ static tcpedit_batch_t *pipe_slot_open(tcpedit_t *t, size_t chunk)
     tcpedit_batch_t *b = calloc(1, sizeof(*b));
     b->ctx = t;
     b->idx_pinned = 1;
+    b->grow_never = 1;
     b->idx_cap_pkts = chunk / 16 + 2; /* a record is at least its 16-byte header */
     b->idx_cap_tiles = b->idx_cap_pkts;
     HIPCHK(t, hipHostMalloc((void **)&b->tiles, sizeof(te_tile_t) * b->idx_cap_tiles, 0));

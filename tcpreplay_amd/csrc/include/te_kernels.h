@@ -92,6 +92,11 @@ typedef struct {
     int static_off;           /* 1: no record can change size or be dropped, so every output
                                  record sits at its input offset: no scan, no look-back */
     uint64_t rec0;            /* input offset of the first record (static_off: out = in - rec0 + out_base) */
+    int static_grow;          /* 1: every record grows by exactly 4 bytes (VLAN add and no other size
+                                 change), so record i (0-based in the launch) sits at its input offset
+                                 + 4 i: no scan, no look-back.  A record that breaks this (and is not a
+                                 hard error, which truncates the output there) sets *grow_bad */
+    uint32_t *grow_bad;       /* device word, zeroed with the error words */
     /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
        only the listed tiles */

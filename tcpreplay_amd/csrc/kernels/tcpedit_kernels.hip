@@ -70,6 +70,8 @@ struct LaunchArgs {
     uint8_t *scratch;                // HBM slots for huge tiles
     uint64_t rec0;                   // static_off: input offset of the first record
     uint32_t static_off;             // output offsets == input offsets (size-preserving config)
+    uint32_t static_grow;            // output offset = input offset + 4 x record index (VLAN add)
+    uint32_t *grow_bad;              // set when a record breaks static_grow's placement
     // after te_fast_tiles: only the listed tiles are edited here, and the last
     // block folds the fast kernel's per-block counters into `counters`
     const uint32_t *tile_list;
@@ -356,12 +358,27 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     // ---- tile output offsets ----
     // static_off: sizes are preserved, so output offsets are the input offsets
     // (no scan, no look-back); otherwise block scan + decoupled look-back.
-    const bool stat = a.static_off != 0;
+    const bool stat = a.static_off != 0, grow = a.static_grow != 0;
     uint32_t tile_total, opos;
     bool keep = true;
     if (MODE == MODE_CONTIG && stat) {
         opos = my_rel;
         tile_total = tile.span_len;
+        if (tid < TE_CNT__N) sh.cnt[tid] = 0;
+        __syncthreads();
+    } else if (grow) {
+        // every record before this one grew by 4 bytes (or the output ends at an earlier
+        // hard error): static placement, checked record by record
+        opos = my_rel + 4u * (uint32_t)tid;
+        tile_total = tile.span_len + 4u * npkt;
+        if (tid < (int)npkt) {
+            sh.opfx[tid] = opos;
+            if ((st & TE_ST_RC_MASK) != TE_ST_RC_ERROR && out_sz != 16 + my_cap + 4) atomicOr(a.grow_bad, 1u);
+        }
+        if (tid == 0) {
+            sh.opfx[npkt] = tile_total;
+            sh.ident = 0;
+        }
         if (tid < TE_CNT__N) sh.cnt[tid] = 0;
         __syncthreads();
     } else {
@@ -398,8 +415,8 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             if ((tid & 63) == 0 && x) atomicAdd(&sh.cnt[k], x);
         }
     }
-    if (stat) {
-        if (tid == 0) sh.out_excl = tile.span_off - a.rec0;
+    if (stat || grow) {
+        if (tid == 0) sh.out_excl = tile.span_off - a.rec0 + (grow ? 4ull * tile.first_pkt : 0ull);
     } else if (tid < 64) {
         const unsigned long long e = lookback(a.tile_state, t, tile_total, a.err);
         if (tid == 0) sh.out_excl = e;
@@ -570,6 +587,7 @@ struct FastArgs {
     int32_t fixed_dir;
     uint32_t in_swapped, in_nsec, v6_ok;
     uint32_t seed_sw, seed_on, skip_bcast;  // te_wave_tiles' phase-A knobs (fl::Knobs), in SGPRs
+    uint32_t vlan_tag_word;                 // GROW: the 4 pushed bytes {TPID, TCI} as a LE dword
 };
 
 // the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
@@ -991,7 +1009,99 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 }
 
 __device__ __forceinline__ bool wk_solo(const te_tile_t &tl) {
-    return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH;
+    // (the last test: a span the image cannot hold never reaches the lane, whatever the cut)
+    return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH ||
+           (uint32_t)(tl.span_off & 15) + tl.span_len + 16u > (uint32_t)TE_WK_TILE_BYTES;
+}
+
+// GROW: caplen and len of the record header at LDS byte h (any alignment) + 4, the
+// VLAN push's length change (tcpedit.c:112-113)
+__device__ __forceinline__ void hdr_grow4(uint8_t *S, uint32_t h) {
+    const uint32_t h8 = h + 8, al = h8 & ~3u, s8 = 8u * (h8 & 3u);
+    uint32_t *w = (uint32_t *)(S + al);
+    const uint32_t q0 = w[0], q1 = w[1], q2 = w[2];
+    const uint32_t cap = __builtin_amdgcn_alignbyte(q1, q0, h8 & 3u) + 4u;
+    const uint32_t len = __builtin_amdgcn_alignbyte(q2, q1, h8 & 3u) + 4u;
+    if (s8 == 0) {
+        w[0] = cap;
+        w[1] = len;
+    } else {
+        const uint32_t lo = (1u << s8) - 1u;  // bytes of q0 below the caplen field
+        w[0] = (q0 & lo) | (cap << s8);
+        w[1] = (cap >> (32u - s8)) | (len << s8);
+        w[2] = (q2 & ~lo) | (len >> (32u - s8));
+    }
+}
+
+// GROW store: the output of a tile whose records each gained 4 bytes at packet offset
+// 12 (the pushed {TPID, TCI}).  Record j starts 4 j bytes later than in the input, so
+// the output is the input byte stream with a 4-byte tag inserted before input byte
+// rel_j + 28 (tile-relative output offset T_j = rel_j + 28 + 4 j).  Consecutive tags
+// are >= 62 bytes apart, so a 16-byte output chunk meets at most one: its bytes come
+// from the input 4 m bytes back (m = tags wholly before the chunk), the tag, and the
+// input 4 (m + 1) bytes back, all dword-aligned in LDS.  M[c] = m per chunk comes from
+// one mark per tag and a prefix max.  OS: the tile's output start in gout coordinates.
+__device__ __forceinline__ void wk_store_grow(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
+                                              uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t my_rel,
+                                              bool on, uint32_t tag, int lane) {
+    const uint64_t OE = OS + span_len + 4ull * npkt;
+    const uint64_t C0 = (OS + 15) & ~15ull;
+    const uint32_t o0 = (uint32_t)(C0 - OS);
+    const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);  // <= 403
+    uint16_t *M = (uint16_t *)P;  // 512 entries
+    uint32_t *T = P + 256;        // 64 tags + sentinel
+    *(uint4 *)(M + 8 * lane) = make_uint4(0, 0, 0, 0);
+    if (on) {
+        const uint32_t Tj = my_rel + 28u + 4u * (uint32_t)lane;
+        T[lane] = Tj;
+        const uint32_t cj = (Tj + 4u - o0 + 15u) >> 4;  // first chunk starting at or after the tag's end
+        if (cj < nown) M[cj] = (uint16_t)(lane + 1);
+    }
+    if (lane == 0) T[npkt] = 0x7fffffffu;
+    {  // prefix max over M, 8 entries a lane
+        const uint4 q = *(const uint4 *)(M + 8 * lane);
+        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
+                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+#pragma unroll
+        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
+        uint32_t incl = e[7];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl = max(incl, y);
+        }
+        uint32_t excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
+        *(uint4 *)(M + 8 * lane) =
+            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+    }
+    const uint8_t *img = S + LDS_FRONT + g0;  // input byte x of the tile
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {  // lanes past the output repeat its last chunk (same bytes)
+        const uint32_t cc = umin32((uint32_t)lane + 64u * k, nown - 1u);
+        const uint32_t m = M[cc], Tm = T[m];
+        const uint32_t o = o0 + 16u * cc;
+        const uint32_t *D = (const uint32_t *)(img + o - 4u * m - 4u);
+        const uint32_t d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3], d4 = D[4];
+        const uint32_t dd[5] = {d0, d1, d2, d3, d4};
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = (int)Tm - (int)(o + 4u * (uint32_t)i);  // the tag's start relative to this dword
+            const uint32_t before = dd[i + 1], after = dd[i];
+            const int tp = t < 0 ? 0 : (t > 3 ? 3 : t), tn = t > -1 ? 1 : (t < -3 ? 3 : -t);
+            const uint32_t mp = (1u << (8 * tp)) - 1u, mn = (1u << (8 * (4 - tn))) - 1u;
+            const uint32_t vp = (before & mp) | ((tag << (8 * tp)) & ~mp);   // tag starts in this dword
+            const uint32_t vn = ((tag >> (8 * tn)) & mn) | (after & ~mn);    // tag started tn bytes earlier
+            w[i] = t >= 4 ? before : (t <= -4 ? after : (t >= 0 ? vp : vn));
+        }
+        *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // the leading bytes (output start to the first 16-byte boundary: before any tag)
+    const uint64_t q = (uint32_t)lane < o0 ? OS + (uint32_t)lane : C0;  // others repeat byte C0
+    gout[q] = img[(uint32_t)(q - OS)];
 }
 
 // big-endian / nanosecond input: a record header in host order and microseconds
@@ -1005,7 +1115,7 @@ __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     st32(rec + 12, ln);
 }
 
-template <uint32_t F, int DEPTH>
+template <uint32_t F, int DEPTH, bool GROW>
 __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
     __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
@@ -1028,7 +1138,8 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     uint32_t *P = PB[wid];
     const bool swp = a.in_swapped != 0, nsec = a.in_nsec != 0, conv = swp || nsec;
     const bool explicit_dir = a.fixed_dir >= 0;
-    const uint32_t extra = conv ? 16u : 0u;  // the next record's header rides along (conversion)
+    // the next record's header rides along (conversion; GROW: its caplen/len + 4)
+    const uint32_t extra = (conv || GROW) ? 16u : 0u;
     g_cu8 *gin = (g_cu8 *)a.in;
     g_u8 *gout = (g_u8 *)a.out + ((int64_t)a.out_base - (int64_t)a.rec0);
     const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
@@ -1161,6 +1272,8 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
 #else
             bool ok = fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
             ok = ok || !edit;
+            // GROW: a record written unedited is not pushed either; the scan placement takes it
+            if constexpr (GROW) ok = ok && !nosend;
             st.tail = st.tail && edit;
 #endif
             if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
@@ -1232,13 +1345,18 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
                     }
                 }
                 if (conv) conv_hdr(S + r0, swp, nsec);
+                if constexpr (GROW) hdr_grow4(S, r0);  // after the write-back, which rewrote len's bytes
                 ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
             }
             if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
+            if (GROW && lane == (int)(npkt & 63u)) hdr_grow4(S, LDS_FRONT + g0 + tile.span_len);
 
             WK_STAMP(3)  // phase B
             // ---- store: the chunks that start in the span, then the leading bytes ----
-            {
+            if constexpr (GROW) {
+                wk_store_grow(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0, my_rel, on,
+                              a.vlan_tag_word, lane);
+            } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
                 const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
@@ -1369,13 +1487,15 @@ extern "C" int te_fast_grid(void) {
 #ifndef TE_WK_DEPTH_LEAN
 #define TE_WK_DEPTH_LEAN 1
 #endif
-#define TE_WAVE_INSTANCES(X) \
-    X(0u, TE_WK_DEPTH_LEAN) X(TE_FF_SEED, TE_WK_DEPTH_LEAN) X(TE_FF_PORTMAP | TE_FF_RWIP, 1) X(TE_FF_ALL, 1)
+#define TE_WAVE_INSTANCES(X)                                                                         \
+    X(0u, TE_WK_DEPTH_LEAN, false) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, false)                              \
+    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, false) X(TE_FF_ALL, 1, false) X(TE_FF_ALL, 1, true)
 static const struct {
     uint32_t feat;
+    bool grow;
     const void *fn;
 } wave_inst[] = {
-#define TE_WI(f, d) {f, (const void *)te_wave_tiles<f, d>},
+#define TE_WI(f, d, g) {f, g, (const void *)te_wave_tiles<f, d, g>},
     TE_WAVE_INSTANCES(TE_WI)
 #undef TE_WI
 };
@@ -1390,7 +1510,7 @@ extern "C" int te_wave_grid(void) {
     if (c) return c;
     int cus = cu_count(), per_cu = 0;
     if (!cus) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL, 1>, WKB, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL, 1, false>, WKB, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     c = cus * per_cu;
     return c;
@@ -1423,11 +1543,13 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     a.scratch = L->scratch;
     a.rec0 = L->rec0;
     a.static_off = (uint32_t)L->static_off;
+    a.static_grow = (uint32_t)L->static_grow;
+    a.grow_bad = L->grow_bad;
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
     hipError_t e;
-    const bool fast = L->fast && L->static_off && !L->slot_layout && L->n_tiles > 0;
+    const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow) && L->n_tiles > 0;
     if (fast && !L->generic_only) {
         // the fast kernel zeroes the generic kernel's words itself: no memset launch
         FastArgs f;
@@ -1460,9 +1582,19 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.seed_sw = __builtin_bswap32(ch->seed);
         f.seed_on = ch->seed != 0;
         f.skip_bcast = ch->skip_broadcast != 0;
+        const bool grow = L->static_grow != 0;
+        if (grow) {  // the pushed {TPID, TCI} of an untagged frame, as dlt_en10mb_encode builds it
+            uint16_t tci = __builtin_bswap16((uint16_t)(ch->vlan_tag & 0x0fffu));
+            if (ch->vlan_pri < 255) tci = (uint16_t)(tci + __builtin_bswap16((uint16_t)(ch->vlan_pri << 13)));
+            if (ch->vlan_cfi < 255) tci = (uint16_t)(tci + __builtin_bswap16((uint16_t)(ch->vlan_cfi << 12)));
+            f.vlan_tag_word = (uint32_t)__builtin_bswap16((uint16_t)ch->vlan_proto) | ((uint32_t)tci << 16);
+        } else {
+            f.vlan_tag_word = 0;
+        }
         const void *wfn = nullptr;
         for (const auto &wi : wave_inst)
-            if (!wfn && (fast_feat(ch) & ~wi.feat) == 0) wfn = wi.fn;
+            if (!wfn && wi.grow == grow && (fast_feat(ch) & ~wi.feat) == 0) wfn = wi.fn;
+        if (!wfn) return -1;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
         int fgrid = wave ? te_wave_grid() : te_fast_grid();
         if (fgrid < 1) return -1;

@@ -314,3 +314,92 @@ def test_tcprewrite_tool_file_to_file(built, tmp_path, mode):
             cmd += ["-c", os.path.join(G.GOLDEN_DIR, case[2])]
         subprocess.run(cmd, check=True, capture_output=True, timeout=60)
         assert_same(out.read_bytes(), G.read(name))
+
+
+# ---------------------------------------------------------------- VLAN add: static +4 placement
+def test_vlan_add_static_grow_matches_oracle_and_scan(built, monkeypatch):
+    """--enet-vlan=add places record i at its input offset + 4 i (no scan); the same
+    capture placed by scan + look-back (TCPEDIT_HIP_NO_GROW) and the oracle agree."""
+    pcap = S.pcap_imix(30_000, seed=11)
+    cache = S.tcpprep_cache(30_000, seed=3)
+    _, exp = O.rewrite(pcap, C4_ARGS, cache)
+    rc, out = gpu_rewrite(pcap, C4_ARGS, cache)
+    assert rc == 0
+    assert_same(out, exp)
+    monkeypatch.setenv("TCPEDIT_HIP_NO_GROW", "1")
+    rc, out2 = gpu_rewrite(pcap, C4_ARGS, cache)
+    assert rc == 0
+    assert_same(out2, exp)
+
+
+def test_vlan_add_unedited_records_fall_back_to_scan(built):
+    """Records the tcpprep cache marks NOSEND are written unedited (no VLAN tag, no +4):
+    the static placement sees them, and the batch is placed again by scan -- on every
+    run of the same batch."""
+    n = 20_000
+    pcap = S.pcap_imix(n, seed=12)
+    cache = S.tcpprep_cache(n, seed=4, nosend_every=97)
+    _, exp = O.rewrite(pcap, C4_ARGS, cache)
+    te = TA.TcpEdit(C4_ARGS)
+    try:
+        b = TA.Batch(te, pcap, cache)
+        for _ in range(3):
+            assert b.run() == 0
+            assert_same(b.output(), exp)
+        b.close()
+    finally:
+        te.close()
+
+
+def test_vlan_add_hard_error_truncates_at_static_offset(built):
+    """A hard error under VLAN add ends the output at that record's statically placed
+    offset (+4 per earlier record), as the oracle does."""
+    recs = S.records(S.pcap_imix(2_000, seed=13))
+    ts, tu, cl, ln, d = recs[1_234]
+    d = bytearray(d)
+    assert d[12:14] == b"\x08\x00"
+    d[14] = 0x55  # IP version 5 with ethertype IPv4 -> TCPEDIT_ERROR (edit_packet.c:73-79)
+    recs[1_234] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs)
+    args = ["--enet-vlan=add", "--enet-vlan-tag=7", "--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out = gpu_rewrite(pcap, args)
+    assert rc_o == -1 and rc == TA.TCPEDIT_ERROR
+    assert_same(out, exp)
+    assert len(S.records(out)) == 1_234
+
+
+def _mixed_sizes_pcap(seed):
+    """IPv4/IPv6 x UDP/TCP records of assorted sizes (odd ones too), interleaved"""
+    rng = random.Random(seed)
+    parts = []
+    for size, v6, proto in [(42, False, 17), (61, False, 17), (64, False, 6), (77, False, 6), (79, False, 17),
+                            (90, True, 17), (97, True, 6), (333, False, 6), (1514, True, 17), (65, False, 17)]:
+        parts += S.records(S.pcap_fixed(300, size, seed=rng.randrange(1 << 20), ipv6=v6, proto=proto))
+    rng.shuffle(parts)
+    return S.build_pcap(parts)
+
+
+@pytest.mark.parametrize("args", [
+    ["--enet-vlan=add", "--enet-vlan-tag=45", "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"],
+    ["--enet-vlan=add", "--enet-vlan-tag=4095", "--enet-vlan-proto=802.1ad", "--seed=9", "--fixcsum"],
+    ["--enet-vlan=add", "--enet-vlan-tag=1", "--portmap=53:5353", "--pnat=10.0.0.0/8:192.168.0.0/16",
+     "--fixcsum"],
+], ids=["tag-pri-cfi", "qinq-seed", "portmap-pnat"])
+def test_vlan_add_wave_lane_mixed_shapes(built, args):
+    """The wave lane's VLAN push (static +4 placement, tags inserted in the store) on
+    v4/v6 TCP/UDP records of odd and even sizes, against the oracle."""
+    pcap = _mixed_sizes_pcap(21)
+    _, exp = O.rewrite(pcap, args)
+    te = TA.TcpEdit(args)
+    try:
+        b = TA.Batch(te, pcap)
+        assert b.run() == 0
+        r = b.result()
+        assert r.fast_kind == 2 and r.generic_tiles < r.n_tiles // 2  # the wave lane pushed most tiles
+        assert_same(b.output(), exp)
+        assert b.run() == 0  # the second run (generic pass left out by the hint) too
+        assert_same(b.output(), exp)
+        b.close()
+    finally:
+        te.close()
