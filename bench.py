@@ -33,8 +33,17 @@ WORKLOADS = {
            "--pnat + --portmap + --fixcsum on IMIX 64/570/1514 7:4:1 (BASELINE configs[2])"),
     "c5": ("pcap_mixed_v4v6", dict(size=1514), ["--fixcsum"],
            "--fixcsum on 1514B mixed IPv4/IPv6 TCP/UDP (BASELINE configs[4])"),
+    "c4": ("pcap_imix", dict(), ["--endpoints=10.10.0.1:10.10.0.2", "--enet-dmac=00:12:13:14:15:16,00:22:33:44:55:66",
+                                 "--enet-smac=00:22:33:44:55:66,00:12:13:14:15:16", "--enet-vlan=add",
+                                 "--enet-vlan-tag=45", "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"],
+           "tcpreplay-edit chain (endpoints + tcpprep cache, enet MACs, VLAN add, fixcsum) on IMIX: one GPU's "
+           "12.5M-record share of the 100M-record 8-GPU job (BASELINE configs[3])"),
+    "c2x10": ("pcap_fixed", dict(size=64), ["--seed=42", "--fixcsum"],
+              "--seed=42 --fixcsum on 10M x 64B (C2 at 1.6 GB moved: launch amortised, HBM- not cache-resident; "
+              "SURVEY 8(d))"),
 }
-DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000}
+DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000}
+CACHED = {"c4"}  # workloads with a tcpprep cache (synth.tcpprep_cache: C2S/S2C runs by flow)
 
 
 def make_pcap(workload, n, seed):
@@ -45,10 +54,12 @@ def make_pcap(workload, n, seed):
 
 def run_workload(workload, n, steps, warmup, seed, device, verify=False):
     import tcpreplay_amd as TA
+    from tcpreplay_amd import synth
     args = WORKLOADS[workload][2]
     pcap = make_pcap(workload, n, seed)
+    cache = synth.tcpprep_cache(n, seed=seed) if workload in CACHED else None
     te = TA.TcpEdit(args, device=device)
-    b = TA.Batch(te, pcap)
+    b = TA.Batch(te, pcap, cache)
     rc = b.run()  # first (untimed) run: also the correctness check below
     r = b.result()
     if rc != 0 or r.unsupported or r.errors:
@@ -56,7 +67,7 @@ def run_workload(workload, n, steps, warmup, seed, device, verify=False):
     if verify:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
-        rc_o, exp = oracle_lib.rewrite(pcap, args)
+        rc_o, exp = oracle_lib.rewrite(pcap, args, cache)
         if b.output() != exp:
             raise RuntimeError(f"{workload}: device output differs from the oracle")
     if warmup:
@@ -125,7 +136,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
-    ap.add_argument("--extra", default="c3,c5", help="secondary configs measured at N=1 (comma list, '' = none)")
+    ap.add_argument("--extra", default="c3,c4,c5,c2x10",
+                    help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
                     "half --cpu-threads threads)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline "
@@ -278,7 +290,7 @@ def main():
                 pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 5)"),
                 one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
                                    "pageable copies (median of 3)"))
-        if not opt.no_cpu_baseline:
+        if not opt.no_cpu_baseline and opt.workload not in CACHED:
             wl_args = WORKLOADS[opt.workload][2]
             v1, runs1, el1, _ = cpu_baseline(pcap, wl_args, n, opt.cpu_seconds / 2)
             thr = max(1, opt.cpu_threads)
