@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 
 #include "te_internal.h"
 
@@ -63,10 +64,16 @@ struct tcpedit_batch_s {
     uint64_t *slots_host;    /* their {packets, bytes, edited, -} totals, read back after a run */
     hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
     int idx_pinned;          /* tiles / pkt_rel are pinned arrays of fixed capacity (a pipeline slot) */
+    uint8_t *res_pinned;     /* pipeline slot: page-locked landing area of a run's counters, error
+                                words and wave-lane slots (a D2H into pageable memory would block) */
     uint64_t idx_cap_tiles, idx_cap_pkts;
     uint64_t walk_end;       /* image offset where the record walk stopped ... */
     int walk_stop;           /* ... because: 0 bytes ran out, 1 libpcap's oversize stop, 2 a hard error */
     int kev_n;
+    /* the parallel record walk's per-stretch index arrays, kept for the batch's next walk */
+    te_tile_t *wk_tiles[64];
+    uint16_t *wk_rel[64];
+    uint64_t wk_cap_t[64], wk_cap_p[64];
     /* device side */
     uint8_t *d_in, *d_out, *d_status, *d_scratch, *d_dirbits;
     uint64_t dirbits_len;
@@ -156,8 +163,187 @@ static uint32_t rd32(const uint8_t *p, int swapped)
     return swapped ? __builtin_bswap32(v) : v;
 }
 
-/* Walk the records (what libpcap's pcap_next does for tcprewrite.c:289) and
- * cut them into tiles whose LDS slots fit TE_SLOT_BYTES. */
+/* One stretch of the record walk (what libpcap's pcap_next does for tcprewrite.c:289):
+ * records from `start` on, cut into tiles, until a record would start at or past
+ * `stop_at` (the next stretch's first record), the bytes run out, or libpcap stops.
+ * Tile first_pkt and scratch_off are relative to the stretch. */
+typedef struct {
+    /* the cut (same for every stretch) */
+    const uint8_t *img;
+    size_t len;
+    int swapped, pad, slot_mode, grow_fast, wave;
+    uint32_t budget, max_pkts;
+    /* the stretch */
+    size_t start, stop_at;
+    te_tile_t *tiles;
+    uint16_t *pkt_rel;
+    uint64_t n_tiles, n_pkts, cap_tiles, cap_pkts;
+    int fixed;               /* the arrays cannot grow (a pipeline slot's pinned index) */
+    uint64_t rec_bytes;      /* sum of 16 + data + 4 (output room) */
+    uint64_t scratch_bytes;
+    int has_zero_cap;
+    int64_t stop_error_pkt;  /* stretch-relative, or -1 */
+    int walk_stop;           /* 0 ran out / reached stop_at, 1 oversize, 2 hard error */
+    size_t end;              /* offset of the first record not taken */
+    int fail;                /* 1 index overflow, 2 out of memory, 3 too many records */
+} te_walk_t;
+
+static int walk_grow(void **arr, uint64_t *cap, size_t elem, int fixed)
+{
+    if (fixed)
+        return -1;
+    void *n = realloc(*arr, elem * (*cap) * 2);
+    if (!n)
+        return -1;
+    *arr = n;
+    *cap *= 2;
+    return 0;
+}
+
+static void walk_range(te_walk_t *w)
+{
+    const uint8_t *img = w->img;
+    const size_t len = w->len;
+    size_t off = w->start;
+    te_tile_t cur;
+    memset(&cur, 0, sizeof(cur));
+    uint32_t cur_slots = 0;
+    int open = 0;
+#define TE_PUSH_TILE()                                                                          \
+    do {                                                                                        \
+        if (w->n_tiles == w->cap_tiles &&                                                      \
+            walk_grow((void **)&w->tiles, &w->cap_tiles, sizeof(te_tile_t), w->fixed) < 0) {    \
+            w->fail = w->fixed ? 1 : 2;                                                         \
+            goto out;                                                                           \
+        }                                                                                       \
+        w->tiles[w->n_tiles++] = cur;                                                           \
+    } while (0)
+    /* the walk is a dependent chain of header loads at record strides the hardware
+       prefetcher does not follow (IMIX: ~100 ns a record): stream the lines 4 KiB ahead */
+    size_t pf = off;
+    while (off + 16 <= len && off < w->stop_at) {
+        for (const size_t pf_end = off + 4096 < len ? off + 4096 : len; pf < pf_end; pf += 64)
+            __builtin_prefetch(img + pf);
+        uint32_t caplen = rd32(img + off + 8, w->swapped), plen = rd32(img + off + 12, w->swapped);
+        if (caplen > 262144u) { /* libpcap stops at an oversize record ... */
+            w->walk_stop = 1;
+            break;
+        }
+        if (off + 16 + caplen > len)
+            break; /* ... and at a truncated one (or a pipeline chunk ends here) */
+        if (plen > 262144u) {
+            /* tcprewrite.c:296-297 errx()s here: the output keeps earlier records */
+            w->stop_error_pkt = (int64_t)w->n_pkts;
+            w->walk_stop = 2;
+            break;
+        }
+        if (caplen == 0)
+            w->has_zero_cap = 1;
+        uint32_t data = w->pad && plen > caplen ? plen : caplen;
+        uint32_t g = (uint32_t)(off & 15);
+        uint32_t slot = TE_SLOT_BYTES_OF(g, data);
+        int huge, fits;
+        if (w->slot_mode && !w->grow_fast) {
+            huge = slot > TE_SLOT_BYTES;
+            fits = open && cur_slots + slot <= TE_SLOT_BYTES;
+        } else {
+            huge = !TE_CONTIG_FITS_IN(g, 16 + caplen, w->budget);
+            fits = open && TE_CONTIG_FITS_IN(cur.span_off & 15, off + 16 + caplen - cur.span_off, w->budget);
+        }
+        /* wave lane: a record too large for a wave image but not for the generic kernel's
+           LDS slot is a tile of its own, left to the generic kernel (no HBM scratch) */
+        const int solo =
+            huge && w->wave && (w->slot_mode ? slot <= TE_SLOT_BYTES : TE_CONTIG_FITS(g, 16 + caplen));
+        if (solo)
+            huge = 0;
+        if (open && (huge || solo || cur.npkt >= w->max_pkts || !fits)) {
+            TE_PUSH_TILE();
+            open = 0;
+        }
+        if (!open) {
+            memset(&cur, 0, sizeof(cur));
+            cur.span_off = off;
+            cur.first_pkt = (uint32_t)w->n_pkts;
+            cur.scratch_off = TE_NO_SCRATCH;
+            cur_slots = 0;
+            open = 1;
+        }
+        if (w->n_pkts == w->cap_pkts &&
+            walk_grow((void **)&w->pkt_rel, &w->cap_pkts, sizeof(uint16_t), w->fixed) < 0) {
+            w->fail = w->fixed ? 1 : 2;
+            goto out;
+        }
+        w->pkt_rel[w->n_pkts++] = (uint16_t)(off - cur.span_off);
+        cur.npkt++;
+        cur.span_len = (uint32_t)(off + 16 + caplen - cur.span_off);
+        cur_slots += slot;
+        w->rec_bytes += 16 + (uint64_t)data + 4;
+        if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
+            cur.scratch_off = w->scratch_bytes;
+            w->scratch_bytes += (slot + TE_LDS_FRONT + 64 + 255) & ~255u;
+            TE_PUSH_TILE();
+            open = 0;
+        } else if (solo) {
+            cur.flags |= TE_TILE_SOLO;
+            TE_PUSH_TILE();
+            open = 0;
+        }
+        off += 16 + caplen;
+        if (w->n_pkts >= 0xffffffffull) {
+            w->fail = 3;
+            goto out;
+        }
+    }
+    if (open)
+        TE_PUSH_TILE();
+out:
+#undef TE_PUSH_TILE
+    w->end = off;
+}
+
+/* a plausible record chain at p: `n` consecutive headers within the image whose
+   lengths libpcap would accept and whose microsecond/nanosecond field is in range */
+static int chain_plausible(const uint8_t *img, size_t len, size_t p, int swapped, int nsec, int n)
+{
+    for (int i = 0; i < n; i++) {
+        if (p + 16 > len)
+            return i > 0;
+        const uint32_t frac = rd32(img + p + 4, swapped), cl = rd32(img + p + 8, swapped),
+                       pl = rd32(img + p + 12, swapped);
+        if (cl > 262144u || pl > 262144u || frac >= (nsec ? 1000000000u : 1000000u) || p + 16 + cl > len)
+            return 0;
+        p += 16 + cl;
+    }
+    return 1;
+}
+
+static int walk_threads(void)
+{
+    static int n = 0;
+    if (!n) {
+        const char *e = getenv("TCPEDIT_HIP_WALK_THREADS");
+        n = e && atoi(e) > 0 ? atoi(e) : 8;
+        if (n > 64)
+            n = 64;
+    }
+    return n;
+}
+
+static void *walk_thread(void *arg)
+{
+    walk_range((te_walk_t *)arg);
+    return NULL;
+}
+
+#define TE_WALK_PART_MIN ((size_t)2 << 20) /* bytes per stretch of a parallel walk, at least */
+
+/* Walk the records and cut them into tiles.  A large image is walked as up to
+ * TCPEDIT_HIP_WALK_THREADS stretches at once: stretch i > 0 starts at a guessed record
+ * boundary (the first plausible chain of headers after an even split point), and it
+ * counts only if stretch i - 1, walking from a known boundary, ends exactly there.
+ * From the first stretch that does not, the walk goes on sequentially, so the index is
+ * the sequential walk's records whatever the guesses (the tile cut may differ: any cut
+ * is valid). */
 static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, const uint8_t *img, size_t len)
 {
     if (len < 24) {
@@ -176,127 +362,213 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         return -1;
     }
     b->linktype = rd32(hdr + 20, b->swapped) & 0x03ffffffu;
-    const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
-    const int slot_mode = pad || t->cfg.vlan == TE_VLAN_ADD;
-    b->slot_layout = slot_mode;
+    te_walk_t proto;
+    memset(&proto, 0, sizeof(proto));
+    proto.img = img;
+    proto.len = len;
+    proto.swapped = b->swapped;
+    proto.pad = t->cfg.fixlen == TE_FIXLEN_PAD;
+    proto.slot_mode = proto.pad || t->cfg.vlan == TE_VLAN_ADD;
+    b->slot_layout = proto.slot_mode;
     /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
        are cut to the wave image (their per-record slots then fit the generic kernel's) */
-    const int grow_fast = !pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
-                          fast_kind_pref() == TE_FAST_WAVE;
-    b->fast_tiles = (!slot_mode && fast_capable(&t->cfg)) || grow_fast;
+    proto.grow_fast = !proto.pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
+                      fast_kind_pref() == TE_FAST_WAVE;
+    b->fast_tiles = (!proto.slot_mode && fast_capable(&t->cfg)) || proto.grow_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
-    const int wave = b->fast_kind == TE_FAST_WAVE;
-    const uint32_t budget = wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
-    const uint32_t max_pkts = wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
+    proto.wave = b->fast_kind == TE_FAST_WAVE;
+    proto.budget = proto.wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
+    proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
+    proto.stop_error_pkt = -1;
+
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     if (b->idx_pinned) { /* a pipeline slot: the chunk budget bounds both (16 B per record at least) */
         cap_tiles = b->idx_cap_tiles;
         cap_pk = b->idx_cap_pkts;
     } else {
+        free(b->tiles);
+        free(b->pkt_rel);
         b->tiles = malloc(sizeof(te_tile_t) * cap_tiles);
         b->pkt_rel = malloc(sizeof(uint16_t) * cap_pk);
-    }
-#define TE_GROW(arr, cap, n)                                                       \
-    if ((n) == (cap)) {                                                           \
-        if (b->idx_pinned) {                                                      \
-            te_seterr(t, "pipeline slot index overflow");                         \
-            return -1;                                                            \
-        }                                                                         \
-        (arr) = realloc((arr), sizeof(*(arr)) * ((cap) *= 2));                    \
-    }
-    b->n_pkts = b->n_tiles = 0;
-    b->out_cap = 24 + 64;
-    b->scratch_bytes = 0;
-    b->stop_error_pkt = -1;
-    b->has_zero_cap = 0;
-    size_t off = 24;
-    b->walk_stop = 0;
-    te_tile_t cur;
-    memset(&cur, 0, sizeof(cur));
-    uint32_t cur_slots = 0;
-    int open = 0;
-    /* the walk is a dependent chain of header loads at record strides the hardware
-       prefetcher does not follow (IMIX: ~100 ns a record): stream the lines 4 KiB ahead */
-    size_t pf = 24;
-    while (off + 16 <= len) {
-        for (const size_t pf_end = off + 4096 < len ? off + 4096 : len; pf < pf_end; pf += 64)
-            __builtin_prefetch(img + pf);
-        uint32_t caplen = rd32(img + off + 8, b->swapped), plen = rd32(img + off + 12, b->swapped);
-        if (caplen > 262144u) { /* libpcap stops at an oversize record ... */
-            b->walk_stop = 1;
-            break;
-        }
-        if (off + 16 + caplen > len)
-            break; /* ... and at a truncated one (or a pipeline chunk ends here) */
-        if (plen > 262144u) {
-            /* tcprewrite.c:296-297 errx()s here: the output keeps earlier records */
-            b->stop_error_pkt = (int64_t)b->n_pkts;
-            b->walk_stop = 2;
-            break;
-        }
-        if (caplen == 0)
-            b->has_zero_cap = 1;
-        uint32_t data = pad && plen > caplen ? plen : caplen;
-        uint32_t g = (uint32_t)(off & 15);
-        uint32_t slot = TE_SLOT_BYTES_OF(g, data);
-        int huge, fits;
-        if (slot_mode && !grow_fast) {
-            huge = slot > TE_SLOT_BYTES;
-            fits = open && cur_slots + slot <= TE_SLOT_BYTES;
-        } else {
-            huge = !TE_CONTIG_FITS_IN(g, 16 + caplen, budget);
-            fits = open && TE_CONTIG_FITS_IN(cur.span_off & 15, off + 16 + caplen - cur.span_off, budget);
-        }
-        /* wave lane: a record too large for a wave image but not for the generic kernel's
-           LDS slot is a tile of its own, left to the generic kernel (no HBM scratch) */
-        const int solo = huge && wave && (slot_mode ? slot <= TE_SLOT_BYTES : TE_CONTIG_FITS(g, 16 + caplen));
-        if (solo)
-            huge = 0;
-        if (open && (huge || solo || cur.npkt >= max_pkts || !fits)) {
-            TE_GROW(b->tiles, cap_tiles, b->n_tiles)
-            b->tiles[b->n_tiles++] = cur;
-            open = 0;
-        }
-        if (!open) {
-            memset(&cur, 0, sizeof(cur));
-            cur.span_off = off;
-            cur.first_pkt = (uint32_t)b->n_pkts;
-            cur.scratch_off = TE_NO_SCRATCH;
-            cur_slots = 0;
-            open = 1;
-        }
-        TE_GROW(b->pkt_rel, cap_pk, b->n_pkts)
-        b->pkt_rel[b->n_pkts++] = (uint16_t)(off - cur.span_off);
-        cur.npkt++;
-        cur.span_len = (uint32_t)(off + 16 + caplen - cur.span_off);
-        cur_slots += slot;
-        b->out_cap += 16 + (uint64_t)data + 4;
-        if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
-            cur.scratch_off = b->scratch_bytes;
-            b->scratch_bytes += (slot + TE_LDS_FRONT + 64 + 255) & ~255u;
-            TE_GROW(b->tiles, cap_tiles, b->n_tiles)
-            b->tiles[b->n_tiles++] = cur;
-            open = 0;
-        } else if (solo) {
-            cur.flags |= TE_TILE_SOLO;
-            TE_GROW(b->tiles, cap_tiles, b->n_tiles)
-            b->tiles[b->n_tiles++] = cur;
-            open = 0;
-        }
-        off += 16 + caplen;
-        if (b->n_pkts >= 0xffffffffull) {
-            te_seterr(t, "too many records for one batch");
+        if (!b->tiles || !b->pkt_rel) {
+            te_seterr(t, "out of host memory");
             return -1;
         }
     }
-    if (open) {
-        TE_GROW(b->tiles, cap_tiles, b->n_tiles)
-        b->tiles[b->n_tiles++] = cur;
+    /* the stretches: [24, q1), [q1, q2), ... */
+    int parts = walk_threads();
+    if ((size_t)parts > (len - 24) / TE_WALK_PART_MIN)
+        parts = (int)((len - 24) / TE_WALK_PART_MIN);
+    if (parts < 1)
+        parts = 1;
+    size_t q[65];
+    q[0] = 24;
+    int np = 1;
+    for (int i = 1; i < parts; i++) {
+        const size_t s0 = 24 + (len - 24) / parts * i, lim = s0 + (1u << 20) < len ? s0 + (1u << 20) : len;
+        size_t p = s0 > q[np - 1] ? s0 : q[np - 1] + 1;
+        for (; p + 16 <= lim; p++)
+            if (chain_plausible(img, len, p, b->swapped, b->nsec, 8))
+                break;
+        if (p + 16 <= lim)
+            q[np++] = p;
     }
-#undef TE_GROW
-    b->walk_end = off;
+    q[np] = (size_t)-1;
+    te_walk_t w[64];
+    pthread_t th[64];
+    int started[64] = {0};
+    for (int i = 0; i < np; i++) {
+        w[i] = proto;
+        w[i].start = q[i];
+        w[i].stop_at = q[i + 1];
+        if (i == 0) { /* stretch 0 writes the batch's own arrays */
+            w[i].tiles = b->tiles;
+            w[i].pkt_rel = b->pkt_rel;
+            w[i].cap_tiles = cap_tiles;
+            w[i].cap_pkts = cap_pk;
+            w[i].fixed = b->idx_pinned;
+        } else { /* the batch's kept arrays for this stretch, grown as the walk needs */
+            const uint64_t span = (i + 1 < np ? q[i + 1] : len) - q[i];
+            const uint64_t want_p = span / 64 + 64, want_t = span / 1024 + 64;
+            if (b->wk_cap_p[i] < want_p) {
+                free(b->wk_rel[i]);
+                b->wk_rel[i] = malloc(sizeof(uint16_t) * want_p);
+                b->wk_cap_p[i] = b->wk_rel[i] ? want_p : 0;
+            }
+            if (b->wk_cap_t[i] < want_t) {
+                free(b->wk_tiles[i]);
+                b->wk_tiles[i] = malloc(sizeof(te_tile_t) * want_t);
+                b->wk_cap_t[i] = b->wk_tiles[i] ? want_t : 0;
+            }
+            w[i].tiles = b->wk_tiles[i];
+            w[i].pkt_rel = b->wk_rel[i];
+            w[i].cap_tiles = b->wk_cap_t[i];
+            w[i].cap_pkts = b->wk_cap_p[i];
+            if (!w[i].tiles || !w[i].pkt_rel) {
+                w[i].fail = 2;
+                continue;
+            }
+            started[i] = pthread_create(&th[i], NULL, walk_thread, &w[i]) == 0;
+            if (!started[i])
+                walk_range(&w[i]);
+        }
+    }
+    walk_range(&w[0]);
+    for (int i = 1; i < np; i++)
+        if (started[i])
+            pthread_join(th[i], NULL);
+    /* stitch: stretch i counts while every earlier one ended exactly at its start */
+    te_walk_t *m = &w[0];
+    int rc = 0, i = 1;
+    for (; i < np && !m->fail; i++) {
+        te_walk_t *x = &w[i];
+        if (m->end != x->start || m->walk_stop || x->fail)
+            break;
+        if (m->n_tiles + x->n_tiles > m->cap_tiles || m->n_pkts + x->n_pkts > m->cap_pkts) {
+            if (m->fixed || walk_grow((void **)&m->tiles, &m->cap_tiles, sizeof(te_tile_t), 0) < 0 ||
+                walk_grow((void **)&m->pkt_rel, &m->cap_pkts, sizeof(uint16_t), 0) < 0) {
+                m->fail = m->fixed ? 1 : 2;
+                break;
+            }
+            i--; /* grown by 2x: retry this stretch */
+            continue;
+        }
+        for (uint64_t k = 0; k < x->n_tiles; k++) {
+            te_tile_t tl = x->tiles[k];
+            tl.first_pkt += (uint32_t)m->n_pkts;
+            if (tl.scratch_off != TE_NO_SCRATCH)
+                tl.scratch_off += m->scratch_bytes;
+            m->tiles[m->n_tiles++] = tl;
+        }
+        memcpy(m->pkt_rel + m->n_pkts, x->pkt_rel, sizeof(uint16_t) * x->n_pkts);
+        if (x->stop_error_pkt >= 0)
+            m->stop_error_pkt = (int64_t)m->n_pkts + x->stop_error_pkt;
+        m->n_pkts += x->n_pkts;
+        m->rec_bytes += x->rec_bytes;
+        m->scratch_bytes += x->scratch_bytes;
+        m->has_zero_cap |= x->has_zero_cap;
+        m->walk_stop = x->walk_stop;
+        m->end = x->end;
+        m->stop_at = x->stop_at;
+    }
+    if (!m->fail && i < np && !m->walk_stop && m->end + 16 <= len) {
+        /* a guess was wrong (or a stretch failed): the rest, sequentially */
+        m->stop_at = (size_t)-1;
+        const size_t from = m->end;
+        te_walk_t rest = proto;
+        rest.start = from;
+        rest.stop_at = (size_t)-1;
+        rest.tiles = m->tiles + m->n_tiles;
+        rest.pkt_rel = m->pkt_rel + m->n_pkts;
+        rest.cap_tiles = m->cap_tiles - m->n_tiles;
+        rest.cap_pkts = m->cap_pkts - m->n_pkts;
+        rest.fixed = 1;
+        walk_range(&rest);
+        if (rest.fail == 1 && !m->fixed) { /* room for the rest: grow to the worst case, walk again */
+            const uint64_t need = m->n_pkts + (len - from) / 16 + 2;
+            te_tile_t *nt = realloc(m->tiles, sizeof(te_tile_t) * need);
+            uint16_t *np2 = nt ? realloc(m->pkt_rel, sizeof(uint16_t) * need) : NULL;
+            if (nt)
+                m->tiles = nt;
+            if (np2)
+                m->pkt_rel = np2;
+            if (nt && np2) {
+                m->cap_tiles = m->cap_pkts = need;
+                rest = proto;
+                rest.start = from;
+                rest.stop_at = (size_t)-1;
+                rest.tiles = m->tiles + m->n_tiles;
+                rest.pkt_rel = m->pkt_rel + m->n_pkts;
+                rest.cap_tiles = rest.cap_pkts = need - m->n_pkts;
+                rest.fixed = 1;
+                walk_range(&rest);
+            } else {
+                rest.fail = 2;
+            }
+        }
+        for (uint64_t k = 0; k < rest.n_tiles; k++) {
+            rest.tiles[k].first_pkt += (uint32_t)m->n_pkts;
+            if (rest.tiles[k].scratch_off != TE_NO_SCRATCH)
+                rest.tiles[k].scratch_off += m->scratch_bytes;
+        }
+        if (rest.stop_error_pkt >= 0)
+            m->stop_error_pkt = (int64_t)m->n_pkts + rest.stop_error_pkt;
+        m->n_tiles += rest.n_tiles;
+        m->n_pkts += rest.n_pkts;
+        m->rec_bytes += rest.rec_bytes;
+        m->scratch_bytes += rest.scratch_bytes;
+        m->has_zero_cap |= rest.has_zero_cap;
+        m->walk_stop = rest.walk_stop;
+        m->end = rest.end;
+        m->fail = rest.fail;
+    }
+    for (int j = 1; j < np; j++) { /* keep what the walks grew to */
+        if (w[j].tiles) {
+            b->wk_tiles[j] = w[j].tiles;
+            b->wk_cap_t[j] = w[j].cap_tiles;
+        }
+        if (w[j].pkt_rel) {
+            b->wk_rel[j] = w[j].pkt_rel;
+            b->wk_cap_p[j] = w[j].cap_pkts;
+        }
+    }
+    b->tiles = m->tiles;
+    b->pkt_rel = m->pkt_rel;
+    if (m->fail) {
+        te_seterr(t, m->fail == 1 ? "pipeline slot index overflow"
+                     : m->fail == 3 ? "too many records for one batch" : "out of host memory");
+        rc = -1;
+    }
+    b->n_tiles = m->n_tiles;
+    b->n_pkts = m->n_pkts;
+    b->out_cap = 24 + 64 + m->rec_bytes;
+    b->scratch_bytes = m->scratch_bytes;
+    b->stop_error_pkt = m->stop_error_pkt;
+    b->has_zero_cap = m->has_zero_cap;
+    b->walk_stop = m->walk_stop;
+    b->walk_end = m->end;
     b->in_len = len;
-    return 0;
+    return rc;
 }
 
 static void batch_free_dev(tcpedit_batch_t *b)
@@ -329,6 +601,12 @@ void tcpedit_batch_close(tcpedit_batch_t *b)
         hipEventDestroy(b->kev[i]);
     free(b->kev);
     free(b->slots_host);
+    for (int i = 0; i < 64; i++) {
+        free(b->wk_tiles[i]);
+        free(b->wk_rel[i]);
+    }
+    if (b->res_pinned)
+        hipHostFree(b->res_pinned);
     if (b->idx_pinned) {
         hipHostFree(b->tiles);
         hipHostFree(b->pkt_rel);
@@ -875,6 +1153,10 @@ static int host_locked(const void *p)
 #define TE_PIPE_SLOTS 2
 #define TE_PIPE_CHUNK_DEFAULT ((size_t)16 << 20)
 
+/* res_pinned layout: counters | error words | wave-lane slots */
+#define TE_RES_ERR 96
+#define TE_RES_SLOTS 128
+
 struct te_pipe_s {
     size_t chunk;                      /* record-byte budget of a chunk (slot capacity) */
     hipStream_t s_h2d, s_d2h;
@@ -927,6 +1209,7 @@ static tcpedit_batch_t *pipe_slot_open(tcpedit_t *t, size_t chunk)
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->idx_cap_pkts + 1)));
     HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->idx_cap_tiles + 1)));
     HIPCHK(t, hipMalloc((void **)&b->d_ws, WS_SLOTS(b->idx_cap_tiles) + 64 + 32 * (uint64_t)te_wave_grid()));
+    HIPCHK(t, hipHostMalloc((void **)&b->res_pinned, TE_RES_SLOTS + 32 * (uint64_t)te_wave_grid(), 0));
     HIPCHK(t, hipEventCreate(&b->ev0));
     HIPCHK(t, hipEventCreate(&b->ev1));
     return b;
@@ -993,8 +1276,10 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     tcpedit_batch_t *b = P->slot[s];
     if (*stopped == 2)
         return 0;
+    memcpy(b->counters, b->res_pinned, sizeof(b->counters));
+    memcpy(b->err, b->res_pinned + TE_RES_ERR, sizeof(b->err));
     for (int i = 0; i < b->last_fgrid; i++) {
-        const uint64_t *v = b->slots_host + 4 * (size_t)i;
+        const uint64_t *v = (const uint64_t *)(b->res_pinned + TE_RES_SLOTS) + 4 * (size_t)i;
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
@@ -1157,6 +1442,10 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         double ti = te_now();
         t_wait += ti - tw;
         const size_t avail = in_len - off, take = avail < chunk_bytes ? avail : chunk_bytes;
+        /* the chunk's bytes go up while the host walks them (the slot's input is free: its
+           last edit is done); the walk decides how many of them are whole records */
+        HIPCHK(t, hipMemcpyAsync(b->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));
+        HIPCHK(t, hipMemcpyAsync(b->d_in + 24, img + off, take, hipMemcpyHostToDevice, P->s_h2d));
         b->pkt_base = pkts;
         b->launches = 0;
         b->gen_hint_ok = 0;
@@ -1183,8 +1472,6 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         const size_t rec_bytes = (size_t)(b->walk_end - 24);
         /* ---- H2D: header, records, index; the kernel stream waits for it and for the
                D2H of the chunk this slot held before ---- */
-        HIPCHK(t, hipMemcpyAsync(b->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));
-        HIPCHK(t, hipMemcpyAsync(b->d_in + 24, img + off, rec_bytes, hipMemcpyHostToDevice, P->s_h2d));
         HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice,
                                  P->s_h2d));
         HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
@@ -1199,14 +1486,13 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
             goto fail_drain;
         }
-        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters), hipMemcpyDeviceToHost,
+        HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_ERR, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost,
                                  t->stream));
-        HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
-        if (b->last_fgrid) {
-            b->slots_host = malloc(32 * (size_t)b->last_fgrid);
-            HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
-                                     hipMemcpyDeviceToHost, t->stream));
-        }
+        if (b->last_fgrid)
+            HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
+                                     32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
         inflight[s] = 1;
         chunk_pkt_base[s] = pkts;

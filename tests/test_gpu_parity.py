@@ -403,3 +403,43 @@ def test_vlan_add_wave_lane_mixed_shapes(built, args):
         b.close()
     finally:
         te.close()
+
+
+# ---------------------------------------------------------------- parallel record walk
+def test_parallel_walk_survives_fake_record_chains(built, monkeypatch):
+    """The host walks a large capture as parallel stretches starting at guessed record
+    boundaries.  Payloads full of valid-looking pcap record headers make the guesses
+    land inside packets; each wrong guess is caught (the previous stretch does not end
+    there) and the walk goes on sequentially, so the output is the oracle's."""
+    monkeypatch.setenv("TCPEDIT_HIP_WALK_THREADS", "8")
+    fake = b"".join(struct.pack("<IIII", 1, 2, 12, 12) + bytes(range(12)) for _ in range(50))  # 1400 B
+    recs = []
+    for ts, tu, cl, ln, d in S.records(S.pcap_fixed(8_000, 1_442, seed=31)):
+        d = bytearray(d)
+        d[42:42 + len(fake)] = fake
+        recs.append((ts, tu, cl, ln, bytes(d)))
+    pcap = S.build_pcap(recs)
+    assert len(pcap) > 10 << 20
+    for args in (["--fixcsum"], ["--seed=3", "--fixcsum"]):
+        _, exp = O.rewrite(pcap, args)
+        rc, out = gpu_rewrite(pcap, args)
+        assert rc == 0
+        assert_same(out, exp)
+        rc, out = pipe_rewrite(pcap, args, chunk=16 << 20)
+        assert rc == 0
+        assert_same(bytes(out), exp)
+
+
+def test_parallel_walk_stops_where_libpcap_stops(built, monkeypatch):
+    """An oversize record deep in a large capture ends the walk there (libpcap's stop),
+    whichever stretch meets it."""
+    monkeypatch.setenv("TCPEDIT_HIP_WALK_THREADS", "8")
+    recs = S.records(S.pcap_fixed(150_000, 64, seed=32))
+    pcap = bytearray(S.build_pcap(recs))
+    cut = 24 + 80 * 111_111
+    struct.pack_into("<I", pcap, cut + 8, 300_000)  # caplen > 262144: pcap_next stops
+    pcap = bytes(pcap)
+    _, exp = O.rewrite(pcap, ["--fixcsum"])
+    rc, out = gpu_rewrite(pcap, ["--fixcsum"])
+    assert_same(out, exp)
+    assert len(S.records(out)) == 111_111
