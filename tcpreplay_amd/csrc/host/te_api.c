@@ -329,10 +329,80 @@ static int walk_threads(void)
     return n;
 }
 
-static void *walk_thread(void *arg)
+/* A small process-wide pool of walker threads (created on first use; thread creation
+ * per chunk cost about as much as the walk itself).  Jobs carry their caller's
+ * pending counter, so concurrent callers share the pool safely.  A forked child
+ * starts without the threads, so it starts a pool of its own. */
+typedef struct {
+    te_walk_t *w;
+    int *pending;
+} te_job_t;
+#define TE_POOL_Q 256
+static pthread_mutex_t pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t pool_cv = PTHREAD_COND_INITIALIZER, pool_done = PTHREAD_COND_INITIALIZER;
+static te_job_t pool_q[TE_POOL_Q];
+static int pool_head, pool_tail, pool_n, pool_atfork;
+
+static void pool_child_reset(void)
 {
-    walk_range((te_walk_t *)arg);
+    pthread_mutex_init(&pool_mu, NULL);
+    pthread_cond_init(&pool_cv, NULL);
+    pthread_cond_init(&pool_done, NULL);
+    pool_head = pool_tail = pool_n = 0;
+}
+
+static void *pool_worker(void *arg)
+{
+    (void)arg;
+    for (;;) {
+        pthread_mutex_lock(&pool_mu);
+        while (pool_head == pool_tail)
+            pthread_cond_wait(&pool_cv, &pool_mu);
+        te_job_t j = pool_q[pool_head % TE_POOL_Q];
+        pool_head++;
+        pthread_mutex_unlock(&pool_mu);
+        walk_range(j.w);
+        pthread_mutex_lock(&pool_mu);
+        (*j.pending)--;
+        pthread_cond_broadcast(&pool_done);
+        pthread_mutex_unlock(&pool_mu);
+    }
     return NULL;
+}
+
+/* queue a stretch; returns 0, or -1 (the caller then walks it itself) */
+static int pool_submit(te_walk_t *w, int *pending, int want_threads)
+{
+    pthread_mutex_lock(&pool_mu);
+    if (!pool_atfork) {
+        pthread_atfork(NULL, NULL, pool_child_reset);
+        pool_atfork = 1;
+    }
+    while (pool_n < want_threads) {
+        pthread_t th;
+        if (pthread_create(&th, NULL, pool_worker, NULL) != 0)
+            break;
+        pthread_detach(th);
+        pool_n++;
+    }
+    if (pool_n == 0 || pool_tail - pool_head >= TE_POOL_Q) {
+        pthread_mutex_unlock(&pool_mu);
+        return -1;
+    }
+    pool_q[pool_tail % TE_POOL_Q] = (te_job_t){w, pending};
+    pool_tail++;
+    (*pending)++;
+    pthread_cond_signal(&pool_cv);
+    pthread_mutex_unlock(&pool_mu);
+    return 0;
+}
+
+static void pool_wait(int *pending)
+{
+    pthread_mutex_lock(&pool_mu);
+    while (*pending)
+        pthread_cond_wait(&pool_done, &pool_mu);
+    pthread_mutex_unlock(&pool_mu);
 }
 
 #define TE_WALK_PART_MIN ((size_t)2 << 20) /* bytes per stretch of a parallel walk, at least */
@@ -415,8 +485,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     }
     q[np] = (size_t)-1;
     te_walk_t w[64];
-    pthread_t th[64];
-    int started[64] = {0};
+    int pending = 0;
     for (int i = 0; i < np; i++) {
         w[i] = proto;
         w[i].start = q[i];
@@ -448,15 +517,12 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
                 w[i].fail = 2;
                 continue;
             }
-            started[i] = pthread_create(&th[i], NULL, walk_thread, &w[i]) == 0;
-            if (!started[i])
+            if (pool_submit(&w[i], &pending, walk_threads() - 1) < 0)
                 walk_range(&w[i]);
         }
     }
     walk_range(&w[0]);
-    for (int i = 1; i < np; i++)
-        if (started[i])
-            pthread_join(th[i], NULL);
+    pool_wait(&pending);
     /* stitch: stretch i counts while every earlier one ended exactly at its start */
     te_walk_t *m = &w[0];
     int rc = 0, i = 1;
