@@ -159,7 +159,15 @@ typedef struct {
     uint16_t vlan_proto;
     bool l2_skip_broadcast; /* tcpeditdlt_t.skip_broadcast (--skipl2broadcast) */
     bool skip_soft_errors;
+    /* the encoder (tcpedit_dlt_post_args, dlt_plugins.c:168-204): en10mb, user or hdlc */
+    int encoder;            /* ENC_EN10MB / ENC_USER / ENC_HDLC */
+    int out_linktype;       /* tcpedit_dlt_output_dlt (dlt_plugins.c:268-283) */
+    int user_length;        /* user_config_t.length (user_types.h:49-55), -1 = no --user-dlink */
+    uint8_t user_l2client[255], user_l2server[255];
+    uint16_t hdlc_address, hdlc_control; /* hdlc_config_t (hdlc_types.h), 65535 = unset */
+    int user_dlt_set, user_dlt;
 } ocfg_t;
+enum { ENC_EN10MB = 0, ENC_USER, ENC_HDLC };
 
 /* decoder/encoder per-context scratch (tcpeditdlt_t + en10mb_extra_t) which
  * the reference keeps across packets (plugins_types.h:100-131). */
@@ -1610,6 +1618,58 @@ static void en10mb_merge_layer3(const ostate_t *s, uint8_t *packet, int pktlen, 
     }
 }
 
+/* dlt_user_encode: plugins/dlt_user/user.c:223-268 -- the decoded L2 header
+ * (ctx->l2len bytes) replaced by the --user-dlink bytes for the direction */
+static int user_encode(const ocfg_t *c, const ostate_t *s, uint8_t *packet, int pktlen, int dir)
+{
+    if (pktlen == 0)
+        return TCPEDIT_ERROR;
+    if (s->l2len != c->user_length)
+        memmove(packet + c->user_length, packet + s->l2len, (size_t)(pktlen - s->l2len));
+    pktlen += c->user_length - s->l2len;
+    if (dir == DIR_C2S)
+        memcpy(packet, c->user_l2client, (size_t)c->user_length);
+    else if (dir == DIR_S2C)
+        memcpy(packet, c->user_l2server, (size_t)c->user_length);
+    else
+        return TCPEDIT_ERROR;
+    return pktlen;
+}
+
+/* dlt_hdlc_encode: plugins/dlt_hdlc/hdlc.c:223-290 -- a 4-byte Cisco HDLC header
+ * {address, control, protocol}; an Ethernet decode leaves no HDLC fields to fall back on */
+static int hdlc_encode(const ocfg_t *c, const ostate_t *s, uint8_t *packet, int pktlen)
+{
+    if (pktlen < 4)
+        return TCPEDIT_ERROR;
+    if (s->l2len != 4)
+        memmove(packet + 4, packet + s->l2len, (size_t)(pktlen - s->l2len));
+    const int newpktlen = pktlen + 4 - s->l2len;
+    if (c->hdlc_address >= 65535) {
+        seterr("Non-HDLC packet requires --hdlc-address");
+        return TCPEDIT_ERROR;
+    }
+    packet[0] = (uint8_t)c->hdlc_address;
+    if (c->hdlc_control >= 65535) {
+        seterr("Non-HDLC packet requires --hdlc-control");
+        return TCPEDIT_ERROR;
+    }
+    packet[1] = (uint8_t)c->hdlc_control;
+    st16(packet + 2, (uint16_t)s->proto); /* hdlc->protocol = ctx->proto */
+    return newpktlen;
+}
+
+/* the encoder's L2 length (tcpedit_dlt_l2len on the encoder DLT, tcpedit.c:116):
+ * en10mb's parse, user.c:325-342 (the configured length), hdlc.c:355-366 (4) */
+static int encoder_l2len(const ocfg_t *c, const uint8_t *packet, int pktlen)
+{
+    if (c->encoder == ENC_USER)
+        return c->user_length;
+    if (c->encoder == ENC_HDLC)
+        return pktlen < 4 ? -1 : 4;
+    return en10mb_l2len(packet, pktlen);
+}
+
 /* ------------------------------------------------------------------------- */
 /* tcpedit_packet: src/tcpedit/tcpedit.c:46-366 (fuzzing out of scope)       */
 /* ------------------------------------------------------------------------- */
@@ -1634,7 +1694,12 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
         int rc = en10mb_decode(s, packet, (int)h->caplen);
         if (rc == TCPEDIT_ERROR)
             return TCPEDIT_SOFT_ERROR;
-        pktlen = en10mb_encode(c, s, packet, (int)h->caplen, direction);
+        if (c->encoder == ENC_USER)
+            pktlen = user_encode(c, s, packet, (int)h->caplen, direction);
+        else if (c->encoder == ENC_HDLC)
+            pktlen = hdlc_encode(c, s, packet, (int)h->caplen);
+        else
+            pktlen = en10mb_encode(c, s, packet, (int)h->caplen, direction);
         if (pktlen < 0)
             return TCPEDIT_SOFT_ERROR;
     }
@@ -1642,14 +1707,14 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
     h->caplen += lendiff;
     h->len += lendiff;
 
-    l2len = en10mb_l2len(packet, (int)h->caplen); /* :116 */
+    l2len = encoder_l2len(c, packet, (int)h->caplen); /* :116 */
     if (l2len == -1)
         return TCPEDIT_SOFT_ERROR;
 
     if (l2proto == htons(ETHERTYPE_IP)) { /* :123-148 */
         if (h->caplen < (uint32_t)l2len + 20)
             return TCPEDIT_SOFT_ERROR;
-        int l2 = en10mb_l2len(packet, (int)h->caplen); /* dlt_en10mb_get_layer3 en10mb.c:768-779 */
+        int l2 = encoder_l2len(c, packet, (int)h->caplen); /* the encoder's get_layer3 (en10mb.c:768-779, user.c:284-298, hdlc.c:313-330) */
         if (l2 == -1 || (int)h->caplen < l2 || (int)h->caplen <= l2)
             return TCPEDIT_SOFT_ERROR;
         ip = packet + l2;
@@ -1658,7 +1723,7 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
     } else if (l2proto == htons(ETHERTYPE_IP6)) { /* :149-173 */
         if (h->caplen < (uint32_t)l2len + 40)
             return TCPEDIT_SOFT_ERROR;
-        int l2 = en10mb_l2len(packet, (int)h->caplen);
+        int l2 = encoder_l2len(c, packet, (int)h->caplen);
         if (l2 == -1 || (int)h->caplen < l2 || (int)h->caplen <= l2)
             return TCPEDIT_SOFT_ERROR;
         ip6 = packet + l2;
@@ -1758,7 +1823,8 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
             *warned = 1;
     }
 
-    en10mb_merge_layer3(s, packet, (int)h->caplen, ip, ip6); /* :356-361 */
+    if (c->encoder == ENC_EN10MB) /* :356-361; user/hdlc merge in place (dlt_utils.c:189-221) */
+        en10mb_merge_layer3(s, packet, (int)h->caplen, ip, ip6);
     return retval;
 }
 
@@ -1771,7 +1837,8 @@ enum {
     O_FIXHDRLEN, O_MTU, O_MTU_TRUNC, O_EFCS, O_TTL, O_TOS, O_TCLASS, O_FLOWLABEL, O_FIXLEN, O_FUZZ_SEED,
     O_FUZZ_FACTOR, O_DLT, O_SKIPL2BROADCAST, O_ENET_DMAC, O_ENET_SMAC, O_ENET_SUBSMAC, O_ENET_MAC_SEED,
     O_ENET_MAC_SEED_KEEP_BYTES, O_ENET_VLAN, O_ENET_VLAN_TAG, O_ENET_VLAN_CFI, O_ENET_VLAN_PRI, O_ENET_VLAN_PROTO,
-    O_SKIP_SOFT_ERRORS, O_CACHEFILE, O_INFILE, O_OUTFILE, O__N
+    O_SKIP_SOFT_ERRORS, O_CACHEFILE, O_INFILE, O_OUTFILE, O_USER_DLT, O_USER_DLINK, O_HDLC_CONTROL,
+    O_HDLC_ADDRESS, O__N
 };
 static const struct {
     const char *name;
@@ -1815,6 +1882,10 @@ static const struct {
     [O_CACHEFILE] = {"cachefile", 'c', 1, 0},
     [O_INFILE] = {"infile", 'i', 1, 0},
     [O_OUTFILE] = {"outfile", 'o', 1, 0},
+    [O_USER_DLT] = {"user-dlt", 0, 1, 0},     /* user_opts.def */
+    [O_USER_DLINK] = {"user-dlink", 0, 1, 1},
+    [O_HDLC_CONTROL] = {"hdlc-control", 0, 1, 0}, /* hdlc_opts.def */
+    [O_HDLC_ADDRESS] = {"hdlc-address", 0, 1, 0},
 };
 
 typedef struct {
@@ -1879,6 +1950,28 @@ static int parse_argv(oopts_t *o, int argc, const char **argv)
 }
 
 static long opt_num(const oopts_t *o, int idx) { return strtol(o->arg[idx], NULL, 0); }
+
+/* read_hexstring: src/common/utils.c:331-380 -- comma-separated hex bytes (strtol base
+ * 16, so "0x0f" and "f" alike); -1 where the reference errx()s on a byte > 0xff */
+static int read_hexstring(const char *l2string, uint8_t *hex, int hexlen)
+{
+    char buf[4096];
+    int numbytes = 0;
+    snprintf(buf, sizeof(buf), "%s", l2string);
+    memset(hex, 0, (size_t)hexlen);
+    char *save = NULL, *tok = strtok_r(buf, ",", &save);
+    if (!tok)
+        return -1;
+    for (; tok; tok = strtok_r(NULL, ",", &save)) {
+        if (numbytes + 1 > hexlen)
+            break; /* "Hex buffer too small for data- skipping data" */
+        const unsigned long v = strtoul(tok, NULL, 16);
+        if (v > 0xff)
+            return -1;
+        hex[numbytes++] = (uint8_t)v;
+    }
+    return numbytes;
+}
 
 /* cidr2cidr: cidr.c:130-221 */
 static int cidr2cidr(char *cidr, ocidr_t *out)
@@ -2291,11 +2384,53 @@ static int oracle_post_args(ocfg_t *c, const oopts_t *o)
             return -1;
         }
     }
-    /* tcpedit_dlt_post_args: dlt_plugins.c:168-204 */
-    if (o->have[O_DLT] && strcmp(o->arg[O_DLT], "en10mb") != 0) {
-        seterr("--dlt=%s is out of the oracle's scope (en10mb only)", o->arg[O_DLT]);
+    /* tcpedit_dlt_post_args: dlt_plugins.c:168-204 -- the encoder by name */
+    c->encoder = ENC_EN10MB;
+    c->out_linktype = 1; /* DLT_EN10MB */
+    c->user_length = -1;
+    c->hdlc_address = c->hdlc_control = 65535;
+    if (o->have[O_DLT]) {
+        if (strcmp(o->arg[O_DLT], "user") == 0) {
+            c->encoder = ENC_USER;
+        } else if (strcmp(o->arg[O_DLT], "hdlc") == 0) {
+            c->encoder = ENC_HDLC;
+            c->out_linktype = 104; /* DLT_C_HDLC */
+        } else if (strcmp(o->arg[O_DLT], "en10mb") != 0) {
+            seterr("--dlt=%s is out of the oracle's scope (en10mb, user, hdlc)", o->arg[O_DLT]);
+            return -1;
+        }
+    }
+    /* dlt_user_parse_opts: user.c:158-205 (--user-dlt, else the decoder's DLT) */
+    if (o->have[O_USER_DLT])
+        c->user_dlt_set = 1, c->user_dlt = (int)opt_num(o, O_USER_DLT);
+    if (c->encoder == ENC_USER)
+        c->out_linktype = c->user_dlt_set ? c->user_dlt : 1;
+    if (o->have[O_USER_DLINK]) {
+        for (int k = 0; k < o->nstack[O_USER_DLINK]; k++) {
+            uint8_t *dst = k == 0 ? c->user_l2server : c->user_l2client;
+            const int n = read_hexstring(o->stack[O_USER_DLINK][k], dst, 255);
+            if (n < 0) {
+                seterr("Invalid hex string: %s", o->stack[O_USER_DLINK][k]);
+                return -1;
+            }
+            if (k == 0) {
+                c->user_length = n;
+                memcpy(c->user_l2client, c->user_l2server, (size_t)n);
+            } else if (n != c->user_length) {
+                seterr("both --dlink's must contain the same number of bytes");
+                return -1;
+            }
+        }
+    }
+    if (c->encoder == ENC_USER && c->user_length < 0) {
+        seterr("--dlt=user requires --user-dlink");
         return -1;
     }
+    /* dlt_hdlc_parse_opts: hdlc.c:156-180 */
+    if (o->have[O_HDLC_CONTROL])
+        c->hdlc_control = (uint16_t)opt_num(o, O_HDLC_CONTROL);
+    if (o->have[O_HDLC_ADDRESS])
+        c->hdlc_address = (uint16_t)opt_num(o, O_HDLC_ADDRESS);
     if (o->have[O_SKIPL2BROADCAST])
         c->l2_skip_broadcast = true;
     /* dlt_en10mb_parse_opts: en10mb.c:226-396 */
@@ -2514,7 +2649,7 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
         goto out;
     }
     {
-        uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, DLT_EN10MB};
+        uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, (uint32_t)c.out_linktype};
         memcpy(out, hdr, 24);
         op = 24;
     }
