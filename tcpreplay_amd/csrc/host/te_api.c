@@ -64,6 +64,7 @@ struct tcpedit_batch_s {
     uint64_t *slots_host;    /* their {packets, bytes, edited, -} totals, read back after a run */
     hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
     int idx_pinned;          /* tiles / pkt_rel are pinned arrays of fixed capacity (a pipeline slot) */
+    uint8_t ohdr[24];        /* the output file header, the source of its upload */
     uint8_t *res_pinned;     /* pipeline slot: page-locked landing area of a run's counters, error
                                 words and wave-lane slots (a D2H into pageable memory would block) */
     uint64_t idx_cap_tiles, idx_cap_pkts;
@@ -107,7 +108,7 @@ struct tcpedit_batch_s {
 static int static_capable(const te_dev_cfg_t *c)
 {
     return !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate &&
-           !c->skip_soft_errors;
+           !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB;
 }
 
 /* options the register-resident fast lane carries (fast_lane.hpp); anything
@@ -118,11 +119,20 @@ static int fast_capable(const te_dev_cfg_t *c)
            c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
 
+/* the most a record's L2 header can grow: a VLAN push (4 bytes) or a user header longer
+   than Ethernet's 14 (device: at most TE_HEAD, more is flagged unsupported) */
+static uint32_t rec_growth(const te_dev_cfg_t *c)
+{
+    const int user = c->encoder == TE_ENC_USER ? c->user_length - 14 : 0;
+    return user > 4 ? (uint32_t)user : 4u;
+}
+
 /* VLAN add as the only size change, on the wave lane (static +4 placement): the other
  * fast-lane conditions, and a tag to push (an untagged frame without one is an error) */
 static int fast_capable_grow(const te_dev_cfg_t *c)
 {
-    return c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
+    return c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs &&
+           c->fixlen == TE_FIXLEN_OFF &&
            !c->mtu_truncate && !c->skip_soft_errors && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 &&
            c->tclass < 0 && c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 &&
            !c->random_set;
@@ -173,6 +183,7 @@ typedef struct {
     size_t len;
     int swapped, pad, slot_mode, grow_fast, wave;
     uint32_t budget, max_pkts;
+    uint32_t growth;         /* output room per record beyond its input (rec_growth) */
     /* the stretch */
     size_t start, stop_at;
     te_tile_t *tiles;
@@ -277,7 +288,7 @@ static void walk_range(te_walk_t *w)
         cur.npkt++;
         cur.span_len = (uint32_t)(off + 16 + caplen - cur.span_off);
         cur_slots += slot;
-        w->rec_bytes += 16 + (uint64_t)data + 4;
+        w->rec_bytes += 16 + (uint64_t)data + w->growth;
         if (huge) { /* a record larger than a tile: its slot lives in HBM scratch */
             cur.scratch_off = w->scratch_bytes;
             w->scratch_bytes += (slot + TE_LDS_FRONT + 64 + 255) & ~255u;
@@ -438,7 +449,9 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     proto.len = len;
     proto.swapped = b->swapped;
     proto.pad = t->cfg.fixlen == TE_FIXLEN_PAD;
-    proto.slot_mode = proto.pad || t->cfg.vlan == TE_VLAN_ADD;
+    /* slots with headroom: VLAN push, fixlen pad, a user L2 header longer than Ethernet's */
+    proto.slot_mode = proto.pad || (t->cfg.encoder == TE_ENC_EN10MB && t->cfg.vlan == TE_VLAN_ADD) ||
+                      (t->cfg.encoder == TE_ENC_USER && t->cfg.user_length > 14);
     b->slot_layout = proto.slot_mode;
     /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
        are cut to the wave image (their per-record slots then fit the generic kernel's) */
@@ -450,6 +463,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     proto.budget = proto.wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
     proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
     proto.stop_error_pkt = -1;
+    proto.growth = rec_growth(&t->cfg);
 
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     if (b->idx_pinned) { /* a pipeline slot: the chunk budget bounds both (16 B per record at least) */
@@ -902,15 +916,25 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     return rc;
 }
 
+/* the output file header: pcap_open_dead(out_dlt, 65535) + pcap_dump_open
+   (tcprewrite.c:124,147), LE microsecond, linktype = the encoder's output DLT */
+static void out_header(const tcpedit_t *t, uint8_t *h)
+{
+    static const uint8_t base[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                     0xff, 0xff, 0, 0, 1, 0, 0, 0};
+    memcpy(h, base, 24);
+    const uint32_t lt = (uint32_t)t->cfg.out_linktype;
+    memcpy(h + 20, &lt, 4);
+}
+
 static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
 {
     float ms = 0;
     if (te_upload_cfg(t) < 0)
         return TCPEDIT_ERROR;
-    static const uint8_t hdr[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                    0xff, 0xff, 0, 0, 1, 0, 0, 0};
     /* pcap_open_dead(out_dlt, 65535) + pcap_dump_open (tcprewrite.c:124,147) */
-    HIPCHK(t, hipMemcpyAsync(b->d_out, hdr, 24, hipMemcpyHostToDevice, t->stream));
+    out_header(t, b->ohdr);
+    HIPCHK(t, hipMemcpyAsync(b->d_out, b->ohdr, 24, hipMemcpyHostToDevice, t->stream));
     HIPCHK(t, hipEventRecord(b->ev0, t->stream));
     if (launch(b, fixed_dir) != 0) {
         te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1402,6 +1426,7 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
     memcpy(&magic, img, 4);
     const int sw = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
     const int pad = t->cfg.fixlen == TE_FIXLEN_PAD;
+    const size_t growth = rec_growth(&t->cfg);
     size_t bound = 24 + 64, off = 24, pf = 24;
     while (off + 16 <= in_len) {
         for (const size_t pf_end = off + 4096 < in_len ? off + 4096 : in_len; pf < pf_end; pf += 64)
@@ -1409,7 +1434,7 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
         const uint32_t caplen = rd32(img + off + 8, sw), plen = rd32(img + off + 12, sw);
         if (caplen > 262144u || off + 16 + caplen > in_len)
             break;
-        bound += 16 + (size_t)(pad && plen > caplen && plen <= 262144u ? plen : caplen) + 4;
+        bound += 16 + (size_t)(pad && plen > caplen && plen <= 262144u ? plen : caplen) + growth;
         off += 16 + caplen;
     }
     return bound;
@@ -1460,9 +1485,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     memcpy(P->hdr, img, 24);
     {
         /* pcap_open_dead(out_dlt, 65535) + pcap_dump_open (tcprewrite.c:124,147) */
-        static const uint8_t ohdr[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                         0xff, 0xff, 0, 0, 1, 0, 0, 0};
-        memcpy(dst, ohdr, 24);
+        out_header(t, dst);
     }
     if (cache) {
         const uint8_t *cd;
@@ -1676,7 +1699,14 @@ int tcpedit_checkerror(tcpedit_t *t, int rcode, const char *prefix)
     return TCPEDIT_ERROR;
 }
 
-int tcpedit_get_output_dlt(tcpedit_t *t) { return t ? 1 : -1; }
+int tcpedit_get_output_dlt(tcpedit_t *t)
+{
+    if (!t)
+        return -1;
+    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+        return -1;
+    return t->cfg.out_linktype; /* tcpedit_dlt_output_dlt (dlt_plugins.c:268-283) */
+}
 
 int tcpedit_get_dev_cfg(tcpedit_t *t, void *out, size_t len, uint16_t *portlut)
 {

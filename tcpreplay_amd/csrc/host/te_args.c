@@ -452,6 +452,28 @@ static int dual_mac(const char *arg, uint8_t *first, uint8_t *second)
     return ret;
 }
 
+/* read_hexstring (src/common/utils.c:331-380): comma-separated hex bytes, strtol base
+ * 16; -1 where the reference errx()s (no byte, or a byte > 0xff) */
+static int read_hexstring(const char *l2string, uint8_t *hex, int hexlen)
+{
+    char buf[4096];
+    int numbytes = 0;
+    snprintf(buf, sizeof(buf), "%s", l2string);
+    memset(hex, 0, (size_t)hexlen);
+    char *save = NULL, *tok = strtok_r(buf, ",", &save);
+    if (!tok)
+        return -1;
+    for (; tok; tok = strtok_r(NULL, ",", &save)) {
+        if (numbytes + 1 > hexlen)
+            break; /* "Hex buffer too small for data- skipping data" */
+        const unsigned long v = strtoul(tok, NULL, 16);
+        if (v > 0xff)
+            return -1;
+        hex[numbytes++] = (uint8_t)v;
+    }
+    return numbytes;
+}
+
 /* ------------------------------------------------------------------------- */
 /* derivation                                                                */
 /* ------------------------------------------------------------------------- */
@@ -680,14 +702,65 @@ int te_derive_cfg(tcpedit_t *t)
         te_seterr(t, "input DLT %d: only DLT_EN10MB (1) is supported by this build", t->dlt);
         return -1;
     }
-    if (t->have[OPT_DLT] && strcmp(t->arg[OPT_DLT], "en10mb") != 0) {
-        te_seterr(t, "--dlt=%s: only the en10mb encoder is supported by this build (SURVEY.md 8f rank 3)",
-                  t->arg[OPT_DLT]);
+    c->encoder = TE_ENC_EN10MB;
+    c->out_linktype = 1; /* DLT_EN10MB */
+    c->user_length = -1;
+    c->hdlc_address = c->hdlc_control = 65535;
+    if (t->have[OPT_DLT]) {
+        if (strcmp(t->arg[OPT_DLT], "user") == 0) {
+            c->encoder = TE_ENC_USER;
+        } else if (strcmp(t->arg[OPT_DLT], "hdlc") == 0) {
+            c->encoder = TE_ENC_HDLC;
+            c->out_linktype = 104; /* DLT_C_HDLC */
+        } else if (strcmp(t->arg[OPT_DLT], "en10mb") != 0) {
+            te_seterr(t, "--dlt=%s: the en10mb, user and hdlc encoders are supported by this build", t->arg[OPT_DLT]);
+            return -1;
+        }
+    }
+    { /* dlt_user_parse_opts (user.c:158-205): --user-dlt, else the decoder's DLT */
+        long v = 1;
+        if (t->have[OPT_USER_DLT] && !num_arg(t, OPT_USER_DLT, 0, 65535, &v))
+            return -1;
+        if (c->encoder == TE_ENC_USER)
+            c->out_linktype = (int32_t)v;
+        for (int k = 0; k < t->nstack[OPT_USER_DLINK]; k++) {
+            uint8_t *dst = k == 0 ? c->user_l2server : c->user_l2client;
+            const int n = read_hexstring(t->stack[OPT_USER_DLINK][k], dst, 255);
+            if (n < 0) {
+                te_seterr(t, "Invalid hex string byte in --user-dlink=%s", t->stack[OPT_USER_DLINK][k]);
+                return -1;
+            }
+            if (k == 0) {
+                c->user_length = n;
+                memcpy(c->user_l2client, c->user_l2server, (size_t)n);
+            } else if (n != c->user_length) {
+                te_seterr(t, "both --dlink's must contain the same number of bytes");
+                return -1;
+            }
+        }
+        if (c->encoder == TE_ENC_USER && c->user_length < 0) {
+            te_seterr(t, "--dlt=user requires --user-dlink");
+            return -1;
+        }
+    }
+    if (c->encoder == TE_ENC_HDLC && (!t->have[OPT_HDLC_ADDRESS] || !t->have[OPT_HDLC_CONTROL])) {
+        /* dlt_hdlc_encode (hdlc.c:270-288) fails every Ethernet-decoded packet without them,
+           after its memmove: the reference writes those soft errors half-moved */
+        te_seterr(t, "--dlt=hdlc needs --hdlc-address and --hdlc-control for Ethernet input");
         return -1;
     }
-    if (t->have[OPT_USER_DLT] || t->have[OPT_USER_DLINK] || t->have[OPT_HDLC_CONTROL] || t->have[OPT_HDLC_ADDRESS]) {
-        te_seterr(t, "user/hdlc DLT plugin options need --dlt=user/hdlc, not supported by this build");
-        return -1;
+    { /* dlt_hdlc_parse_opts (hdlc.c:156-180) */
+        long v;
+        if (t->have[OPT_HDLC_CONTROL]) {
+            if (!num_arg(t, OPT_HDLC_CONTROL, 0, 255, &v))
+                return -1;
+            c->hdlc_control = (uint32_t)v;
+        }
+        if (t->have[OPT_HDLC_ADDRESS]) {
+            if (!num_arg(t, OPT_HDLC_ADDRESS, 0, 255, &v))
+                return -1;
+            c->hdlc_address = (uint32_t)v;
+        }
     }
     c->l2_skip_broadcast = t->have[OPT_SKIPL2BROADCAST] != 0;
 

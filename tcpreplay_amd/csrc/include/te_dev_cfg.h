@@ -31,7 +31,9 @@ typedef struct {
 
 enum { TE_TTL_OFF = 0, TE_TTL_SET, TE_TTL_ADD, TE_TTL_SUB };       /* tcpedit_types.h:38-43 */
 enum { TE_FIXLEN_OFF = 0, TE_FIXLEN_PAD, TE_FIXLEN_TRUNC, TE_FIXLEN_DEL };
-enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };                  /* en10mb_types.h:50-54 */
+enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };
+enum { TE_ENC_EN10MB = 0, TE_ENC_USER, TE_ENC_HDLC };
+#define TE_USER_L2MAX 256 /* USER_L2MAXLEN (255, user_types.h:37), rounded */                  /* en10mb_types.h:50-54 */
 enum { TE_MASK_SMAC1 = 1, TE_MASK_SMAC2 = 2, TE_MASK_DMAC1 = 4, TE_MASK_DMAC2 = 8 };
 enum { TE_DIR_NOSEND = 0, TE_DIR_C2S = 1, TE_DIR_S2C = 2 };          /* cache.h:77-80 */
 
@@ -70,6 +72,14 @@ typedef struct {
     int32_t n_pm;
     uint16_t pm_from[TE_MAX_PM];
     uint16_t pm_to[TE_MAX_PM];
+    /* the encoder (tcpedit_dlt_post_args, dlt_plugins.c:168-204) and its options:
+     * user_config_t (dlt_user/user_types.h:46-55), hdlc_config_t (dlt_hdlc/hdlc_types.h) */
+    int32_t encoder;        /* TE_ENC_* */
+    int32_t out_linktype;   /* tcpedit_dlt_output_dlt (dlt_plugins.c:268-283) */
+    int32_t user_length;    /* --user-dlink bytes, -1 = none */
+    uint32_t hdlc_address, hdlc_control; /* 65535 = unset */
+    uint8_t user_l2client[TE_USER_L2MAX];
+    uint8_t user_l2server[TE_USER_L2MAX];
 } te_dev_cfg_t;
 
 /* Per-packet status byte written by the device (one per input record). */

@@ -983,6 +983,52 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
     return pktlen;
 }
 
+// Replace a decoded L2 header of s.l2len bytes by n new ones (dlt_user_encode's and
+// dlt_hdlc_encode's memmove, user.c:245-253, hdlc.c:239-247): the payload stays where
+// it is and the record's 16-byte pcap header moves, as the VLAN push/pop does above.
+// A longer header moves into the slot's headroom (TE_HEAD bytes); more than that is
+// flagged unsupported.  The caller writes the n header bytes at the new pk.d.
+DI bool l2_replace(Pkt &pk, int l2len, int n) {
+    const int delta = l2len - n;
+    if (delta == 0) return true;
+    if (-delta > TE_HEAD) {
+        pk.unsupported = true;
+        return false;
+    }
+    u8 *src = pk.d - 16, *dst = pk.d - 16 + delta;
+    if (delta > 0)
+        for (int i = 15; i >= 0; --i) dst[i] = src[i];
+    else
+        for (int i = 0; i < 16; ++i) dst[i] = src[i];
+    pk.d += delta;
+    pk.avail -= delta;
+    pk.phys -= delta;
+    return true;
+}
+
+// dlt_user_encode (plugins/dlt_user/user.c:223-268): the --user-dlink bytes of the direction
+DI int user_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen, int dir) {
+    if (pktlen == 0) return RC_ERROR;
+    if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;
+    const int n = cfg.user_length;
+    if (!l2_replace(pk, s.l2len, n)) return RC_ERROR;
+    const u8 *src = dir == TE_DIR_C2S ? cfg.user_l2client : cfg.user_l2server;
+    for (int i = 0; i < n; ++i) pk.d[i] = src[i];
+    return pktlen + n - s.l2len;
+}
+
+// dlt_hdlc_encode (plugins/dlt_hdlc/hdlc.c:223-290): {address, control, protocol}; the
+// host requires --hdlc-address and --hdlc-control (an Ethernet decode has no HDLC
+// fields to fall back on, so the reference fails every packet without them)
+DI int hdlc_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen) {
+    if (pktlen < 4) return RC_ERROR;
+    if (!l2_replace(pk, s.l2len, 4)) return RC_ERROR;
+    pk.d[0] = (u8)cfg.hdlc_address;
+    pk.d[1] = (u8)cfg.hdlc_control;
+    st16(pk.d + 2, (u16)s.proto);  // hdlc->protocol = ctx->proto
+    return pktlen + 4 - s.l2len;
+}
+
 // dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC; the
 // en10mb decoder never sets dst_modified (memcmp of untouched bytes, :614).
 DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) {
@@ -1038,14 +1084,22 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
         s.l2offset = 0;
     } else {
         if (en10mb_decode(pk.d, (int)pk.caplen, s) == RC_ERROR) return RC_SOFT;
-        pktlen = en10mb_encode(pk, cfg, s, (int)pk.caplen, dir);
+        if (cfg.encoder == TE_ENC_USER)
+            pktlen = user_encode(pk, cfg, s, (int)pk.caplen, dir);
+        else if (cfg.encoder == TE_ENC_HDLC)
+            pktlen = hdlc_encode(pk, cfg, s, (int)pk.caplen);
+        else
+            pktlen = en10mb_encode(pk, cfg, s, (int)pk.caplen, dir);
         if (pktlen < 0) return RC_SOFT;
     }
     int lendiff = pktlen - (int)pk.caplen;  // :111-113
     pk.caplen += lendiff;
     pk.len += lendiff;
 
-    int l2len = en10mb_l2len(pk.d, (int)pk.caplen);  // :116
+    // :116, the encoder's L2 length: en10mb's parse, user.c:325-342, hdlc.c:355-366
+    int l2len = cfg.encoder == TE_ENC_USER   ? cfg.user_length
+                : cfg.encoder == TE_ENC_HDLC ? (pk.caplen < 4 ? -1 : 4)
+                                             : en10mb_l2len(pk.d, (int)pk.caplen);
     if (l2len == -1) return RC_SOFT;
 
     if (l2proto == 0x0008) {  // htons(ETHERTYPE_IP)  :123-148
@@ -1223,7 +1277,8 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
         if (retval == RC_WARN) warned = true;
     }
 
-    en10mb_merge_layer3(pk, s, ip, ip6);  // :356-361
+    // :356-361; the user and hdlc encoders merge in place (dlt_utils.c:189-221)
+    if (cfg.encoder == TE_ENC_EN10MB) en10mb_merge_layer3(pk, s, ip, ip6);
     return retval;
 }
 

@@ -29,4 +29,7 @@ class DevCfg(ctypes.Structure):
         ("random_set", ctypes.c_uint32), ("random_keep", ctypes.c_int32), ("random_mask", ctypes.c_uint8 * 8),
         ("mac_mask", ctypes.c_int32), ("vlan", ctypes.c_int32), ("vlan_tag", ctypes.c_uint32),
         ("vlan_pri", ctypes.c_uint32), ("vlan_cfi", ctypes.c_uint32), ("vlan_proto", ctypes.c_uint32),
-        ("n_pm", ctypes.c_int32), ("pm_from", ctypes.c_uint16 * MAXPM), ("pm_to", ctypes.c_uint16 * MAXPM)]
+        ("n_pm", ctypes.c_int32), ("pm_from", ctypes.c_uint16 * MAXPM), ("pm_to", ctypes.c_uint16 * MAXPM),
+        ("encoder", ctypes.c_int32), ("out_linktype", ctypes.c_int32), ("user_length", ctypes.c_int32),
+        ("hdlc_address", ctypes.c_uint32), ("hdlc_control", ctypes.c_uint32),
+        ("user_l2client", ctypes.c_uint8 * 256), ("user_l2server", ctypes.c_uint8 * 256)]

@@ -443,3 +443,37 @@ def test_parallel_walk_stops_where_libpcap_stops(built, monkeypatch):
     rc, out = gpu_rewrite(pcap, ["--fixcsum"])
     assert_same(out, exp)
     assert len(S.records(out)) == 111_111
+
+
+# ---------------------------------------------------------------- user / Cisco HDLC encoders
+@pytest.mark.parametrize("args,linktype", [
+    (["--dlt=user", "--user-dlink=1,2,3,4,5,6,7,8,9,a,b,c,d,e,f,10,11,12,8,0", "--user-dlt=147", "--fixcsum"], 147),
+    (["--dlt=user", "--user-dlink=aa,bb,8,0", "--user-dlink=cc,dd,8,0", "--seed=7", "--fixcsum"], 1),
+    (["--dlt=hdlc", "--hdlc-address=0x0f", "--hdlc-control=3", "--pnat=10.0.0.0/8:192.168.0.0/16", "--fixcsum"],
+     104),
+], ids=["user-20B-longer", "user-client-server", "hdlc"])
+def test_dlt_encoders_match_oracle(built, args, linktype):
+    """The user and HDLC encoders (L2 header replaced, payload in place, pcap header
+    moved; a longer user header into the slot headroom) on v4/v6 TCP/UDP records of
+    assorted sizes, VLAN-tagged ones among them, with a tcpprep cache for direction."""
+    recs = S.records(_mixed_sizes_pcap(41)) + S.records(G.read("test.pcap"))
+    pcap = S.build_pcap(recs)
+    cache = S.tcpprep_cache(len(recs), seed=5)
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    rc, out = gpu_rewrite(pcap, args, cache)
+    assert rc == rc_o
+    assert_same(out, exp)
+    assert struct.unpack_from("<I", out, 20)[0] == linktype
+    te = TA.TcpEdit(args)
+    try:
+        assert te._L.tcpedit_get_output_dlt(te._ctx) == linktype
+    finally:
+        te.close()
+
+
+def test_dlt_user_header_past_the_headroom_fails_loudly(built):
+    """A user header more than 16 bytes longer than the decoded one does not fit the
+    slot headroom: the batch fails naming the record instead of guessing."""
+    args = ["--dlt=user", "--user-dlink=" + ",".join(["1"] * 40)]
+    rc, out = gpu_rewrite(S.pcap_fixed(100, 64, seed=3), args)
+    assert rc == TA.TCPEDIT_ERROR
