@@ -4,7 +4,8 @@
  * A plain-C, single-threaded CPU restatement of the reference's per-packet
  * edit path: libtcpedit's tcpedit_packet() (src/tcpedit/tcpedit.c:46-366) as
  * driven by tcprewrite's rewrite_packets() (src/tcprewrite.c:260-373), for
- * DLT_EN10MB input and output.  Every function cites the reference file:line
+ * DLT_EN10MB input and the en10mb, user and hdlc encoders, --fuzz-seed included
+ * (src/tcpedit/fuzzing.c, with the reference's second L2/L3 pass after a fuzz).  Every function cites the reference file:line
  * it restates (paths relative to appneta/tcpreplay 4.5.5).
  *
  * Pinning: this restatement is checked byte-for-byte against the reference's
@@ -144,7 +145,8 @@ typedef struct {
     oport_t *portmap;
     int n_portmap;
     int mtu;
-    uint32_t fuzz_seed;
+    uint32_t fuzz_seed;     /* tcpedit->fuzz_seed (mixed like the seed, parse_args.c:213-235) */
+    uint32_t fuzz_factor;   /* --fuzz-factor, default 8 (tcpedit_opts.def:325-330) */
     /* en10mb_config_t */
     uint8_t intf1_dmac[6], intf1_smac[6], intf2_dmac[6], intf2_smac[6];
     uint8_t (*subs)[2][6];
@@ -1671,7 +1673,175 @@ static int encoder_l2len(const ocfg_t *c, const uint8_t *packet, int pktlen)
 }
 
 /* ------------------------------------------------------------------------- */
-/* tcpedit_packet: src/tcpedit/tcpedit.c:46-366 (fuzzing out of scope)       */
+/* fuzzing: src/tcpedit/fuzzing.c:12-297 (state: fuzzing_init's statics)      */
+/* ------------------------------------------------------------------------- */
+static uint32_t g_fuzz_state, g_fuzz_factor; /* fuzz_seed, fuzz_factor (fuzzing.c:8-20) */
+
+/* the encoder's proto function on the edited packet (plugin_proto): en10mb.c:741-762,
+   user.c:273-282 (always an error), hdlc.c:299-311 (the protocol field) */
+static int encoder_proto(const ocfg_t *c, const uint8_t *packet, int pktlen)
+{
+    if (c->encoder == ENC_USER)
+        return TCPEDIT_ERROR;
+    if (c->encoder == ENC_HDLC)
+        return pktlen < 4 ? TCPEDIT_ERROR : ld16(packet + 2);
+    return en10mb_proto(packet, pktlen);
+}
+
+#define SGT_MAX_SIZE 16
+static int fuzz_get_sgt_size(uint32_t r, uint32_t caplen) /* fuzzing.c:23-35 */
+{
+    if (caplen == 0)
+        return 0;
+    if (caplen <= SGT_MAX_SIZE)
+        return 1;
+    return (int)(1 + (r % (SGT_MAX_SIZE - 1)));
+}
+
+static int fuzz_reduce_packet_size(ohdr_t *h, uint32_t new_len) /* fuzzing.c:37-60 */
+{
+    if (h->len < h->caplen)
+        return -1;
+    if (new_len > h->caplen)
+        return -1;
+    if (new_len == h->caplen)
+        return 0;
+    h->len = new_len;
+    h->caplen = h->len;
+    return 1;
+}
+
+enum { FZ_DROP, FZ_REDUCE, FZ_START_ZERO, FZ_START_RANDOM, FZ_START_FF, FZ_MID_ZERO, FZ_MID_RANDOM, FZ_MID_FF,
+       FZ_END_ZERO, FZ_END_RANDOM, FZ_END_FF, FZ_TOTAL }; /* fuzzing.h */
+
+static int oracle_fuzzing(const ocfg_t *c, ohdr_t *h, uint8_t *packet) /* fuzzing.c:62-297 */
+{
+    int chksum_update_required = 0;
+    uint32_t r = tcpr_random(&g_fuzz_state), s;
+    if ((r % g_fuzz_factor) != 0)
+        return 0;
+    uint8_t *end_ptr = packet + h->caplen, *l4data;
+    const int l2len = encoder_l2len(c, packet, (int)h->caplen);
+    const uint16_t l2proto = ntohs((uint16_t)encoder_proto(c, packet, (int)h->caplen));
+    int l4len;
+    uint8_t l4proto;
+    if (l2len == -1 || (int)h->caplen < l2len)
+        return 0;
+    if ((int)h->caplen <= l2len) /* plugin_get_layer3 -> tcpedit_dlt_l3data_copy (dlt_utils.c:196) */
+        return 0;
+    uint8_t *l3data = packet + l2len;
+    switch (l2proto) {
+    case ETHERTYPE_IP:
+        l4data = get_layer4_v4(packet + l2len, end_ptr);
+        if (!l4data)
+            return 0;
+        l4len = (int)(l4data - packet); /* an offset, as the reference has it */
+        l4proto = l3data[9];
+        break;
+    case ETHERTYPE_IP6:
+        l4data = get_layer4_v6(packet + l2len, end_ptr);
+        if (!l4data)
+            return 0;
+        l4len = (int)(l4data - packet);
+        l4proto = l3data[6];
+        break;
+    default:
+        l4len = (int)h->caplen - l2len;
+        l4data = packet + l2len;
+        l4proto = 255; /* IPPROTO_RAW */
+    }
+    if (l4proto == 6) {
+        l4len -= 20;
+        l4data += 20;
+    } else if (l4proto == 17) {
+        l4len -= 8;
+        l4data += 8;
+    }
+    if (l4len <= 1 || l4data > end_ptr)
+        return 0;
+    r ^= r >> 16;
+    s = r % FZ_TOTAL;
+    switch (s) {
+    case FZ_DROP:
+        if (fuzz_reduce_packet_size(h, 0) < 0)
+            return 0;
+        break;
+    case FZ_REDUCE: {
+        const uint32_t new_len = (r % (uint32_t)(l4len - 1)) + 1;
+        if (fuzz_reduce_packet_size(h, new_len) < 0)
+            return 0;
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_START_ZERO: {
+        const uint32_t sgt = (uint32_t)fuzz_get_sgt_size(r, (uint32_t)l4len);
+        memset(l4data, 0x00, sgt);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_START_RANDOM: {
+        const uint32_t sgt = (uint32_t)fuzz_get_sgt_size(r, (uint32_t)l4len);
+        if (!sgt)
+            return 0;
+        for (uint32_t i = 0; i < sgt; i++)
+            l4data[i] = l4data[i] ^ (uint8_t)(r >> 4);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_START_FF: {
+        const uint32_t sgt = (uint32_t)fuzz_get_sgt_size(r, (uint32_t)l4len);
+        if (!sgt)
+            return 0;
+        memset(l4data, 0xff, sgt);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_MID_ZERO:
+    case FZ_MID_FF: {
+        if (l4len <= 2)
+            return 0;
+        const uint32_t offset = ((r >> 16) % (uint32_t)(l4len - 1)) + 1;
+        const uint32_t sgt = (uint32_t)fuzz_get_sgt_size(r, (uint32_t)l4len - offset);
+        if (!sgt)
+            return 0;
+        memset(l4data + offset, s == FZ_MID_ZERO ? 0x00 : 0xff, sgt);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_END_ZERO:
+    case FZ_END_FF: {
+        const int sgt = fuzz_get_sgt_size(r, (uint32_t)l4len);
+        if (!sgt || sgt > l4len)
+            return 0;
+        memset(l4data + l4len - sgt, s == FZ_END_ZERO ? 0x00 : 0xff, (size_t)sgt);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_END_RANDOM: {
+        const int sgt = fuzz_get_sgt_size(r, (uint32_t)l4len);
+        if (!sgt || sgt > l4len)
+            return 0;
+        for (int i = l4len - sgt; i < l4len; i++)
+            l4data[i] = l4data[i] ^ (uint8_t)(r >> 4);
+        chksum_update_required = 1;
+        break;
+    }
+    case FZ_MID_RANDOM: {
+        const uint32_t offset = ((r >> 16) % (uint32_t)(l4len - 1)) + 1;
+        const int sgt = fuzz_get_sgt_size(r, (uint32_t)l4len - offset);
+        if (!sgt || sgt > l4len)
+            return 0;
+        for (uint32_t i = offset; i < offset + (uint32_t)sgt; i++)
+            l4data[i] = l4data[i] ^ (uint8_t)(r >> 4);
+        chksum_update_required = 1;
+        break;
+    }
+    }
+    return chksum_update_required;
+}
+
+/* ------------------------------------------------------------------------- */
+/* tcpedit_packet: src/tcpedit/tcpedit.c:46-366                              */
 /* ------------------------------------------------------------------------- */
 static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_t *packet, int direction, int *warned)
 {
@@ -1684,6 +1854,10 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
             h->caplen -= 4;
         h->len -= 4;
     }
+    int fuzz_once = c->fuzz_seed != 0; /* :48 */
+again: /* :89 -- a fuzzed packet goes through L2 and the per-family edits once more */
+    ip = ip6 = NULL;
+    retval = 0;
     if ((l2proto = en10mb_proto(packet, (int)h->caplen)) < 0) /* :96 */
         return TCPEDIT_SOFT_ERROR;
 
@@ -1764,6 +1938,13 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
         }
         if (c->tcp_sequence_enable)
             rewrite_ipv6_tcp_sequence(c, ip6, l3len);
+    }
+
+    if (fuzz_once) { /* :250-258 */
+        fuzz_once = 0;
+        retval = oracle_fuzzing(c, h, packet);
+        needtorecalc += retval;
+        goto again;
     }
 
     if (c->fixlen || c->mtu_truncate) { /* :261-265 */
@@ -2362,6 +2543,14 @@ static int oracle_post_args(ocfg_t *c, const oopts_t *o)
             }
         }
     }
+    if (o->have[O_SEED] && o->have[O_FUZZ_SEED]) { /* seed: flags-cant = fuzz-seed (tcpedit_opts.def:46-48) */
+        seterr("--seed and --fuzz-seed are mutually exclusive");
+        return -1;
+    }
+    if (o->have[O_FUZZ_FACTOR] && !o->have[O_FUZZ_SEED]) { /* fuzz-factor: flags-must = fuzz-seed (:324-326) */
+        seterr("--fuzz-factor requires --fuzz-seed");
+        return -1;
+    }
     if (o->have[O_SEED]) {
         c->rewrite_ip = true;
         seed = (uint32_t)opt_num(o, O_SEED);
@@ -2374,8 +2563,11 @@ static int oracle_post_args(ocfg_t *c, const oopts_t *o)
         c->seed = seed;
     if (o->have[O_FUZZ_SEED]) {
         c->fuzz_seed = seed;
-        seterr("--fuzz-seed is out of the oracle's scope");
-        return -1;
+        c->fuzz_factor = o->have[O_FUZZ_FACTOR] ? (uint32_t)opt_num(o, O_FUZZ_FACTOR) : 8;
+        if (c->fuzz_factor < 1) {
+            seterr("--fuzz-factor must be >= 1");
+            return -1;
+        }
     }
     if (o->have[O_ENDPOINTS]) {
         c->rewrite_ip = true;
@@ -2656,6 +2848,8 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
     buf = calloc(1, MAXPACKET + 65536); /* static pktdata_buff (tcprewrite.c:267-280), zeroed by safe_malloc */
     ostate_t st;
     memset(&st, 0, sizeof(st));
+    g_fuzz_state = c.fuzz_seed; /* fuzzing_init (tcprewrite.c:102-103, fuzzing.c:12-20) */
+    g_fuzz_factor = c.fuzz_factor ? c.fuzz_factor : 8;
     size_t ip_ = 24;
     uint64_t packetnum = 0;
     while (ip_ + 16 <= in_len) {

@@ -3,8 +3,8 @@ little-endian `standard_littleendian` target whose outputs are test/test2.*).
 
 Each case: (golden file, input file, cache file or None, argument list, in_scope).
 Inputs and expected outputs are the reference's fixtures, copied verbatim under
-tests/golden/.  The case marked out of scope needs --fuzz-seed, which SURVEY.md
-§8(f) ranks as "next" (rank 4); the user and hdlc encoders (rank 3) are in.
+tests/golden/.  Every case is in scope: the user and hdlc encoders (SURVEY.md §8(f)
+rank 3) and --fuzz-seed (rank 4) included.
 """
 import os
 
@@ -53,7 +53,7 @@ CASES = [
     ("test2.rewrite_2ttl-hdrfix", "test.pcap", None, ["--ttl=+59", "--fixhdrlen"], True),
     ("test2.rewrite_3ttl-hdrfix", "test.pcap", None, ["--ttl=-59", "--fixhdrlen"], True),
     ("test2.rewrite_mtutrunc", "test.pcap", None, ["--mtu-trunc", "--mtu=300"], True),
-    ("test2.rewrite_l7fuzzing", "test.pcap", None, ["--fuzz-seed=42", "--fuzz-factor=2"], False),
+    ("test2.rewrite_l7fuzzing", "test.pcap", None, ["--fuzz-seed=42", "--fuzz-factor=2"], True),
     ("test2.rewrite_fixcsum", "test.pcap", None, ["--fixcsum"], True),
     ("test2.rewrite_fixlen_pad", "test.pcap", None, ["--fixlen=pad"], True),
     ("test2.rewrite_fixlen_trunc", "test.pcap", None, ["--fixlen=trunc"], True),

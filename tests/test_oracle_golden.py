@@ -17,11 +17,16 @@ def test_oracle_matches_reference_golden(built, case):
     assert out == G.read(name)
 
 
-@pytest.mark.parametrize("case", [c for c in G.CASES if not c[4]], ids=[c[0] for c in G.CASES if not c[4]])
-def test_out_of_scope_cases_are_rejected(built, case):
-    name, inp, cache, args, _ = case
+def test_every_reference_golden_is_in_scope():
+    assert all(c[4] for c in G.CASES) and len(G.IN_SCOPE) == 33
+
+
+@pytest.mark.parametrize("args", [["--seed=1", "--fuzz-seed=2"], ["--fuzz-factor=2"], ["--fuzz-seed=1", "--fuzz-factor=0"]])
+def test_fuzz_option_constraints(built, args):
+    # seed: flags-cant = fuzz-seed; fuzz-factor: flags-must = fuzz-seed, arg-range 1->
+    # (src/tcpedit/tcpedit_opts.def:46-48, 324-330)
     with pytest.raises(ValueError):
-        O.rewrite(G.read(inp), args)
+        O.rewrite(G.read("test.pcap"), args)
 
 
 def test_seed_mixer_matches_survey_values(built):
