@@ -83,6 +83,8 @@ struct tcpedit_batch_s {
     uint8_t *d_ws;           /* err[0..2] | ticket, done | counters | tile_state[] | list count */
     uint32_t *d_tile_list;   /* fast lane: tiles left to the generic kernel */
     uint32_t last_cnt_off;   /* workspace offset of the last launch's counter set */
+    uint32_t *d_fuzz;        /* --fuzz-seed: per-record RNG states, then a word per 1024 records */
+    uint64_t fuzz_cap;       /* records d_fuzz has room for */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
     /* results */
@@ -108,7 +110,7 @@ struct tcpedit_batch_s {
 static int static_capable(const te_dev_cfg_t *c)
 {
     return !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate &&
-           !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB;
+           !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB && !c->fuzz_seed;
 }
 
 /* options the register-resident fast lane carries (fast_lane.hpp); anything
@@ -124,7 +126,8 @@ static int fast_capable(const te_dev_cfg_t *c)
 static uint32_t rec_growth(const te_dev_cfg_t *c)
 {
     const int user = c->encoder == TE_ENC_USER ? c->user_length - 14 : 0;
-    return user > 4 ? (uint32_t)user : 4u;
+    const uint32_t g = user > 4 ? (uint32_t)user : 4u;
+    return c->fuzz_seed ? 2 * g : g; /* a fuzzed record is encoded twice (tcpedit.c:250-258) */
 }
 
 /* VLAN add as the only size change, on the wave lane (static +4 placement): the other
@@ -132,6 +135,7 @@ static uint32_t rec_growth(const te_dev_cfg_t *c)
 static int fast_capable_grow(const te_dev_cfg_t *c)
 {
     return c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs &&
+           !c->fuzz_seed &&
            c->fixlen == TE_FIXLEN_OFF &&
            !c->mtu_truncate && !c->skip_soft_errors && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 &&
            c->tclass < 0 && c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 &&
@@ -662,6 +666,9 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_pkt_rel);
     hipFree(b->d_ws);
     hipFree(b->d_tile_list);
+    hipFree(b->d_fuzz);
+    b->d_fuzz = NULL;
+    b->fuzz_cap = 0;
     b->d_tile_list = NULL;
     b->d_in = b->d_out = b->d_status = b->d_scratch = b->d_dirbits = b->d_ws = NULL;
     b->d_tiles = NULL;
@@ -762,6 +769,12 @@ int te_upload_cfg(tcpedit_t *t)
             HIPCHK(t, hipMalloc((void **)&t->d_portlut, 65536 * sizeof(uint16_t)));
         HIPCHK(t, hipMemcpyAsync(t->d_portlut, t->portlut, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
                                  t->stream));
+    }
+    if (t->cfg.fuzz_seed) { /* fuzzing_init (fuzzing.c:12-20): the run-wide RNG state */
+        if (!t->d_fuzz_words)
+            HIPCHK(t, hipMalloc((void **)&t->d_fuzz_words, 4 * sizeof(uint32_t)));
+        const uint32_t w[4] = {t->cfg.fuzz_seed, t->cfg.fuzz_seed, 0, 0};
+        HIPCHK(t, hipMemcpyAsync(t->d_fuzz_words, w, sizeof(w), hipMemcpyHostToDevice, t->stream));
     }
     HIPCHK(t, hipStreamSynchronize(t->stream));
     t->dev_dirty = 0;
@@ -880,7 +893,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     /* VLAN add as the only size change: every record grows by 4 bytes or is a hard error
        (dlt_en10mb_encode, en10mb.c:520-575), so outputs sit at input offset + 4 x index */
     L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
-                    !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap &&
+                    !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap && !c->fuzz_seed &&
                     !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env();
     L.grow_bad = (uint32_t *)(b->d_ws + WS_GROW_BAD);
     b->last_grow = L.static_grow;
@@ -908,6 +921,24 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
                      b->gen_hint_gen == t->cfg_gen && b->last_listed == 0;
     if (generic_only)
         L.grid = b->last_listed ? (int)b->last_listed : 1;
+    if (c->fuzz_seed && !L.fast && b->n_pkts) {
+        /* --fuzz-seed: room for a state per record and a word per 1024 records */
+        const uint64_t need = b->n_pkts;
+        if (b->fuzz_cap < need) {
+            hipFree(b->d_fuzz);
+            b->d_fuzz = NULL;
+            b->fuzz_cap = 0;
+            if (hipMalloc((void **)&b->d_fuzz, 4 * (need + need / 1024 + 2)) != hipSuccess)
+                return -1;
+            b->fuzz_cap = need;
+        }
+        if (b->n_pkts > 0xffffffffull || !t->d_fuzz_words)
+            return -1;
+        L.fuzz_states = b->d_fuzz;
+        L.fuzz_blk = b->d_fuzz + b->fuzz_cap + 1;
+        L.fuzz_words = t->d_fuzz_words;
+        L.n_pkts = (uint32_t)b->n_pkts;
+    }
     const int rc = te_launch_edit(&L, t->stream);
     if (!generic_only) {
         b->last_skipped = L.skip_generic;
@@ -1888,6 +1919,7 @@ int tcpedit_close(tcpedit_t **tp)
     free(t->portlut);
     hipFree(t->d_cfg);
     hipFree(t->d_portlut);
+    hipFree(t->d_fuzz_words);
     te_pipe_free(t);
     if (t->stream)
         hipStreamDestroy(t->stream);

@@ -683,10 +683,10 @@ int te_derive_cfg(tcpedit_t *t)
         rnd = te_tcpr_random(&seed);
     if (t->have[OPT_SEED])
         c->seed = seed;
-    if (t->have[OPT_FUZZ_SEED]) {
+    if (t->have[OPT_FUZZ_SEED]) { /* :232-235; fuzzing_init (tcprewrite.c:102-103) */
         t->fuzz_seed = seed;
-        te_seterr(t, "--fuzz-seed is not supported by this build yet (SURVEY.md section 8f, rank 4)");
-        return -1;
+        c->fuzz_seed = seed;
+        c->fuzz_factor = t->fuzz_factor;
     }
     if (t->have[OPT_ENDPOINTS]) {
         c->rewrite_ip = 1;

@@ -33,6 +33,7 @@ enum { TE_TTL_OFF = 0, TE_TTL_SET, TE_TTL_ADD, TE_TTL_SUB };       /* tcpedit_ty
 enum { TE_FIXLEN_OFF = 0, TE_FIXLEN_PAD, TE_FIXLEN_TRUNC, TE_FIXLEN_DEL };
 enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };
 enum { TE_ENC_EN10MB = 0, TE_ENC_USER, TE_ENC_HDLC };
+enum { TE_FUZZ_OFF = 0, TE_FUZZ_PROBE, TE_FUZZ_APPLY }; /* the generic kernel's fuzz passes */
 #define TE_USER_L2MAX 256 /* USER_L2MAXLEN (255, user_types.h:37), rounded */                  /* en10mb_types.h:50-54 */
 enum { TE_MASK_SMAC1 = 1, TE_MASK_SMAC2 = 2, TE_MASK_DMAC1 = 4, TE_MASK_DMAC2 = 8 };
 enum { TE_DIR_NOSEND = 0, TE_DIR_C2S = 1, TE_DIR_S2C = 2 };          /* cache.h:77-80 */
@@ -80,6 +81,8 @@ typedef struct {
     uint32_t hdlc_address, hdlc_control; /* 65535 = unset */
     uint8_t user_l2client[TE_USER_L2MAX];
     uint8_t user_l2server[TE_USER_L2MAX];
+    /* --fuzz-seed (fuzzing.c:12-20): the mixed seed (0 = off) and --fuzz-factor */
+    uint32_t fuzz_seed, fuzz_factor;
 } te_dev_cfg_t;
 
 /* Per-packet status byte written by the device (one per input record). */

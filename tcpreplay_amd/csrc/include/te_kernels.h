@@ -114,6 +114,11 @@ typedef struct {
     uint64_t *counters_next;  /* fast lane: the other parity's counter set, zeroed for the next launch */
     uint64_t *ws_zero;        /* device: 4 words (err, ticket) the fast kernel zeroes */
     void *ev_k0, *ev_k1;      /* optional hipEvent_t pair recorded around the dominant edit kernel */
+    /* --fuzz-seed (generic lane only): a reach pass, then per-record RNG states, then the edit */
+    uint32_t *fuzz_states;    /* device: n_pkts words, or NULL (no fuzzing) */
+    uint32_t *fuzz_blk;       /* device: a word per 1024 records */
+    uint32_t *fuzz_words;     /* device: [0] the context's running RNG state, [1] this launch's start */
+    uint32_t n_pkts;          /* records in the launch */
 } te_launch_t;
 
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */

@@ -1055,11 +1055,129 @@ DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) 
     }
 }
 
+// the encoder's L2 length (plugin_l2len): en10mb's parse (en10mb.c:917-943),
+// user.c:325-342, hdlc.c:355-366
+DI int encoder_l2len(const Pkt &pk, const te_dev_cfg_t &cfg) {
+    return cfg.encoder == TE_ENC_USER   ? cfg.user_length
+           : cfg.encoder == TE_ENC_HDLC ? (pk.caplen < 4 ? -1 : 4)
+                                        : en10mb_l2len(pk.d, (int)pk.caplen);
+}
+
 // ---------------------------------------------------------------------------
-// tcpedit_packet (src/tcpedit/tcpedit.c:46-366), minus fuzzing (out of scope).
+// --fuzz-seed: fuzzing() (src/tcpedit/fuzzing.c:62-297) for one packet.  The
+// reference draws one tcpr_random() from a run-wide state per packet that
+// reaches this step (tcpedit.c:250-258); the launch hands each such packet the
+// state it would see, found by a reach pass, a prefix count and an LCG jump
+// (te_fuzz_states).  Writes the reference makes past caplen (its l4len is an
+// offset from the packet start, fuzzing.c:118,127) land in its static buffer and
+// never reach the output: here they are kept only inside this lane's slot.
+// ---------------------------------------------------------------------------
+DI u32 tcpr_random_dev(u32 &seed) {  // utils.c:436-458
+    u32 n = seed, r;
+    n = n * 1103515245u + 12345u;
+    r = (u32)((int)(n / 65536) % 2048);
+    n = n * 1103515245u + 12345u;
+    r = (r << 10) ^ (u32)((int)(n / 65536) % 1024);
+    n = n * 1103515245u + 12345u;
+    r = (r << 10) ^ (u32)((int)(n / 65536) % 1024);
+    seed = n;
+    return r;
+}
+
+DI u32 fuzz_sgt_size(u32 r, u32 caplen) {  // fuzzing.c:23-35
+    return caplen == 0 ? 0u : caplen <= 16 ? 1u : 1u + r % 15u;
+}
+
+DI void fuzz_fill(Pkt &pk, int from, int n, int how, u8 x) {  // how: 0 = 0x00, 1 = 0xff, 2 = ^x
+    for (int i = 0; i < n; ++i) {
+        const int j = from + i;
+        // past the lane's slot: the reference's stale buffer, never output.  A byte past
+        // `phys` stays unknown here (an XOR of a stale byte), and any later read of one
+        // is flagged where it happens.
+        if (j < 0 || j >= (int)pk.avail) continue;
+        pk.d[j] = how == 0 ? (u8)0 : how == 1 ? (u8)0xff : (u8)(pk.d[j] ^ x);
+    }
+}
+
+DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
+    u32 r = tcpr_random_dev(state);
+    if (r % cfg.fuzz_factor) return 0;
+    const int caplen = (int)pk.caplen;
+    const int l2len = encoder_l2len(pk, cfg);
+    int proto = -1;  // plugin_proto: en10mb.c:741-762, user.c:271-279 (always an error), hdlc.c:300-312
+    if (cfg.encoder == TE_ENC_HDLC) {
+        if (caplen >= 4) proto = ld16(pk.d + 2);
+    } else if (cfg.encoder == TE_ENC_EN10MB && caplen >= 14) {
+        L2 q;
+        if (get_l2len_protocol(pk.d, pk.caplen, q) != -1) proto = bswap16(q.protocol);
+    }
+    const u16 l2proto = bswap16((u16)proto);
+    if (l2len == -1 || caplen < l2len || caplen <= l2len) return 0;  // :95-109, dlt_utils.c:195
+    int l4off, l4len;  // l4data - packet, and the reference's l4len
+    u8 l4proto;
+    if (l2proto == 0x0800 || l2proto == 0x86DD) {
+        const u8 *ip = pk.d + l2len;
+        const bool v4 = l2proto == 0x0800;
+        const int l4 = v4 ? l4_v4(ip, caplen - l2len) : l4_v6(ip, 0, caplen - l2len);
+        if (l4 < 0) return 0;
+        l4off = l2len + l4;
+        l4len = l4off;  // an offset, as the reference has it (fuzzing.c:118,127)
+        const int pb = l2len + (v4 ? 9 : 6);
+        if (pb >= (int)pk.phys) pk.unsupported = true;
+        l4proto = ip[v4 ? 9 : 6];
+    } else {
+        l4len = caplen - l2len;
+        l4off = l2len;
+        l4proto = 255;
+    }
+    if (l4proto == 6) {
+        l4len -= 20;
+        l4off += 20;
+    } else if (l4proto == 17) {
+        l4len -= 8;
+        l4off += 8;
+    }
+    if (l4len <= 1 || l4off > caplen) return 0;
+    r ^= r >> 16;
+    const u32 act = r % 11u;  // fuzzing.h: DROP, REDUCE, START_{0,R,FF}, MID_{0,R,FF}, END_{0,R,FF}
+    const u8 x = (u8)(r >> 4);
+    if (act <= 1) {  // fuzz_reduce_packet_size (fuzzing.c:37-60)
+        const u32 nl = act == 0 ? 0u : r % (u32)(l4len - 1) + 1u;
+        if (pk.len < pk.caplen || nl > pk.caplen) return 0;
+        if (nl == pk.caplen) return act;
+        pk.len = pk.caplen = nl;
+        return act;
+    }
+    if (act <= 4) {  // START_*
+        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);
+        if (!sgt && act != 2) return 0;
+        fuzz_fill(pk, l4off, sgt, act == 2 ? 0 : act == 4 ? 1 : 2, x);
+        return 1;
+    }
+    if (act <= 7) {  // MID_*
+        if (act != 6 && l4len <= 2) return 0;
+        const u32 off = ((r >> 16) % (u32)(l4len - 1)) + 1u;
+        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len - off);
+        if (!sgt || (act == 6 && sgt > l4len)) return 0;
+        fuzz_fill(pk, l4off + (int)off, sgt, act == 5 ? 0 : act == 7 ? 1 : 2, x);
+        return 1;
+    }
+    const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);  // END_*
+    if (!sgt || sgt > l4len) return 0;
+    fuzz_fill(pk, l4off + l4len - sgt, sgt, act == 8 ? 0 : act == 10 ? 1 : 2, x);
+    return 1;
+}
+
+// ---------------------------------------------------------------------------
+// tcpedit_packet (src/tcpedit/tcpedit.c:46-366).
 // Returns RC_* ; *warned set when the checksum step warned (:351-353).
+// fz_mode: TE_FUZZ_OFF; TE_FUZZ_PROBE returns RC_REACHED at the fuzz step (the
+// reach pass); TE_FUZZ_APPLY fuzzes with RNG state fz_state there.
 // ---------------------------------------------------------------------------
-DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int dir, bool &warned) {
+constexpr int RC_REACHED = 3;
+template <bool FZ = false>
+DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int dir, bool &warned,
+                      u32 fz_mode = TE_FUZZ_OFF, u32 fz_state = 0) {
     warned = false;
     u8 *ip = nullptr, *ip6 = nullptr;
     int needtorecalc = 0, retval = 0;
@@ -1068,8 +1186,13 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
         if (pk.caplen == pk.len) pk.caplen -= 4;
         pk.len -= 4;
     }
+    bool fuzz_once = FZ && fz_mode != TE_FUZZ_OFF;  // :49
+    int l2proto, l2len, l3len;
+    Dec s;
+again:  // :89 -- after the fuzz step the packet goes through L2 and the L3 edits once more
+    ip = ip6 = nullptr;
+    retval = 0;
     // l2proto (:96): dlt_en10mb_proto (en10mb.c:741-762), network-order value
-    int l2proto;
     {
         if (pk.caplen < 14) return RC_SOFT;
         L2 r;
@@ -1078,7 +1201,6 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
     }
     // tcpedit_dlt_process (dlt_plugins.c:210-238)
     int pktlen;
-    Dec s;
     if (dir == TE_DIR_NOSEND) {
         pktlen = (int)pk.caplen;
         s.l2offset = 0;
@@ -1096,10 +1218,7 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
     pk.caplen += lendiff;
     pk.len += lendiff;
 
-    // :116, the encoder's L2 length: en10mb's parse, user.c:325-342, hdlc.c:355-366
-    int l2len = cfg.encoder == TE_ENC_USER   ? cfg.user_length
-                : cfg.encoder == TE_ENC_HDLC ? (pk.caplen < 4 ? -1 : 4)
-                                             : en10mb_l2len(pk.d, (int)pk.caplen);
+    l2len = encoder_l2len(pk, cfg);  // :116
     if (l2len == -1) return RC_SOFT;
 
     if (l2proto == 0x0008) {  // htons(ETHERTYPE_IP)  :123-148
@@ -1114,7 +1233,7 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
         if (l4_v6(ip6, 0, (int)pk.caplen - l2len) < 0) return RC_SOFT;
     }
 
-    int l3len = (int)pk.caplen - l2len;
+    l3len = (int)pk.caplen - l2len;
     if (ip) {  // :182-206
         if (cfg.tos > -1) {
             u16 oldv = ld16(ip);
@@ -1188,6 +1307,16 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
         if (cfg.tcp_sequence_enable && ip6[6] == 6) {  // rewrite_sequence.c:76-92
             int l4 = l4_v6(ip6, 0, l3len);
             if (l4 >= 0) rewrite_seqs(pk, cfg, ip6 + l4);
+        }
+    }
+
+    if constexpr (FZ) {
+        if (fuzz_once) {  // :250-258
+            if (fz_mode == TE_FUZZ_PROBE) return RC_REACHED;
+            fuzz_once = false;
+            retval = fuzz_packet(pk, cfg, fz_state);
+            needtorecalc += retval;
+            goto again;
         }
     }
 

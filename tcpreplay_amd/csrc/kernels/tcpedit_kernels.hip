@@ -77,6 +77,10 @@ struct LaunchArgs {
     const uint32_t *tile_list;
     const uint32_t *list_cnt;        // this launch's count
     unsigned long long *counters_next;  // zeroed here for the next launch (fast lane parity)
+    // --fuzz-seed: TE_FUZZ_PROBE writes status[i] = 1 for a record that reaches the fuzz
+    // step and nothing else; TE_FUZZ_APPLY fuzzes record i with RNG state fuzz_state[i]
+    uint32_t fuzz_mode;
+    const uint32_t *fuzz_state;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -195,7 +199,7 @@ __device__ __forceinline__ uint32_t sel_bytes(uint32_t x, uint32_t y, int b0, in
 // ---------------------------------------------------------------------------
 // tile body.  S = slot buffer (LDS, or HBM scratch for a huge record).
 // ---------------------------------------------------------------------------
-template <int MODE, typename P>
+template <int MODE, bool FZ, typename P>
 __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t, P S,
                                           TileShared &sh, const te_dev_cfg_t &cfg) {
     const int tid = threadIdx.x;
@@ -320,8 +324,11 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
             st |= TE_ST_NOSEND;
         } else {
-            rc = tcpedit_packet(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned);
+            const uint32_t fzs = a.fuzz_mode == TE_FUZZ_APPLY ? a.fuzz_state[tile.first_pkt + tid] : 0u;
+            rc = tcpedit_packet<FZ>(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned, a.fuzz_mode,
+                                    fzs);
         }
+        if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) st = rc == RC_REACHED ? 1 : 0;
         if (pk.unsupported) st |= TE_ST_UNSUPPORTED;
         if (warned) st |= TE_ST_WARNED;
         bool write = true;
@@ -354,6 +361,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (write) out_sz = 16 + pk.caplen;
         ((g_u8 *)a.status)[tile.first_pkt + tid] = st;
     }
+    if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) return;  // the reach pass writes nothing else
 
     // ---- tile output offsets ----
     // static_off: sizes are preserved, so output offsets are the input offsets
@@ -490,18 +498,19 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
 // address the kernel passes in: the kernarg-pointer builtin is only defined in
 // a kernel entry (a callee gets null), and taking &a in the kernel would copy
 // the arguments to scratch for every tile.
+template <bool FZ>
 __device__ __attribute__((noinline)) void huge_tile(const TE_AS_CONST LaunchArgs *ka, uint32_t t,
                                                     const te_dev_cfg_t &cfg) {
     const LaunchArgs &a = *(const LaunchArgs *)ka;
     __shared__ TileShared hsh;
     const te_tile_t tile = a.tiles[t];
-    tile_body<MODE_SLOT>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
+    tile_body<MODE_SLOT, FZ>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
 }
 
 #ifndef TE_MIN_WAVES
 #define TE_MIN_WAVES 3
 #endif
-template <int MODE>
+template <int MODE, bool FZ = false>
 __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
@@ -525,9 +534,9 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         if (listed) t = a.tile_list[t];
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
-            tile_body<MODE>(a, tile, t, slots, sh, cfg);
+            tile_body<MODE, FZ>(a, tile, t, slots, sh, cfg);
         else
-            huge_tile((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
+            huge_tile<FZ>((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
         __syncthreads();
     }
 }
@@ -1468,6 +1477,82 @@ static int resident_blocks(int slot_layout) {
     return c;
 }
 
+// ===========================================================================
+// --fuzz-seed RNG states.  The reference draws one tcpr_random() (three LCG steps,
+// utils.c:436-458) from a run-wide state for every record that reaches the fuzz
+// step, in record order (tcpedit.c:250-258, fuzzing.c:87).  After the reach pass
+// (status[i] = 1 for such a record) record i's state is the run's state advanced
+// by 3 x (reaching records before i): a count, an exclusive scan and an LCG jump.
+// words[0] is the context's running state, words[1] this launch's starting state.
+// ===========================================================================
+constexpr int FZ_PER_THREAD = 4, FZ_BLOCK = 256, FZ_PER_BLOCK = FZ_PER_THREAD * FZ_BLOCK;
+
+__device__ __forceinline__ uint32_t lcg_jump(uint32_t x, uint64_t k) {  // k steps of n*1103515245+12345
+    uint32_t am = 1, ap = 0, cm = 1103515245u, cp = 12345u;
+    while (k) {
+        if (k & 1) {
+            am *= cm;
+            ap = ap * cm + cp;
+        }
+        cp = (cm + 1u) * cp;
+        cm *= cm;
+        k >>= 1;
+    }
+    return am * x + ap;
+}
+
+__device__ __forceinline__ uint32_t fz_flags(const uint8_t *st, uint32_t n, uint32_t i0, uint32_t f[FZ_PER_THREAD]) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < FZ_PER_THREAD; ++k) {
+        f[k] = i0 + k < n ? (st[i0 + k] & 1u) : 0u;
+        c += f[k];
+    }
+    return c;
+}
+
+__global__ void __launch_bounds__(FZ_BLOCK) te_fuzz_count(const uint8_t *st, uint32_t n, uint32_t *blk) {
+    __shared__ uint32_t wsum[FZ_BLOCK / 64];
+    uint32_t f[FZ_PER_THREAD], tot;
+    const uint32_t c = fz_flags(st, n, blockIdx.x * FZ_PER_BLOCK + threadIdx.x * FZ_PER_THREAD, f);
+    block_exscan<FZ_BLOCK>(c, wsum, tot);
+    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// one block: exclusive scan of the block counts in place, then the state words
+__global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nblk, uint32_t *words) {
+    __shared__ uint32_t wsum[1024 / 64];
+    uint64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < nblk ? blk[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exscan<1024>(v, wsum, tot);
+        if (i < nblk) blk[i] = (uint32_t)carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t s0 = words[0];
+        words[1] = s0;
+        words[0] = lcg_jump(s0, 3ull * carry);
+    }
+}
+
+__global__ void __launch_bounds__(FZ_BLOCK) te_fuzz_states(const uint8_t *st, uint32_t n, const uint32_t *blk,
+                                                           const uint32_t *words, uint32_t *states) {
+    __shared__ uint32_t wsum[FZ_BLOCK / 64];
+    uint32_t f[FZ_PER_THREAD], tot;
+    const uint32_t i0 = blockIdx.x * FZ_PER_BLOCK + threadIdx.x * FZ_PER_THREAD;
+    const uint32_t c = fz_flags(st, n, i0, f);
+    uint32_t rank = blk[blockIdx.x] + block_exscan<FZ_BLOCK>(c, wsum, tot);
+    const uint32_t s0 = words[1];
+#pragma unroll
+    for (int k = 0; k < FZ_PER_THREAD; ++k) {
+        if (i0 + k < n) states[i0 + k] = lcg_jump(s0, 3ull * rank);
+        rank += f[k];
+    }
+}
+
 extern "C" int te_fast_grid(void) {
     static int c = 0;
     if (c) return c;
@@ -1548,6 +1633,8 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
+    a.fuzz_mode = TE_FUZZ_OFF;
+    a.fuzz_state = nullptr;
     hipError_t e;
     const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow) && L->n_tiles > 0;
     if (fast && !L->generic_only) {
@@ -1632,9 +1719,34 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     const int res = resident_blocks(L->slot_layout);
     int grid = L->grid > 0 && L->grid < res ? L->grid : res;
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
+    if (L->fuzz_states && !fast) {
+        // --fuzz-seed: reach pass, per-record RNG states, then the edit pass below
+        if (!L->fuzz_blk || !L->fuzz_words || L->n_pkts == 0) return -1;
+        a.fuzz_mode = TE_FUZZ_PROBE;
+        if (L->slot_layout)
+            hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else
+            hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        const uint32_t nblk = (L->n_pkts + FZ_PER_BLOCK - 1) / FZ_PER_BLOCK;
+        hipLaunchKernelGGL(te_fuzz_count, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
+                           L->n_pkts, L->fuzz_blk);
+        hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words);
+        hipLaunchKernelGGL(te_fuzz_states, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
+                           L->n_pkts, (const uint32_t *)L->fuzz_blk, (const uint32_t *)L->fuzz_words,
+                           L->fuzz_states);
+        if (hipGetLastError() != hipSuccess) return -1;
+        e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);  // the reach pass took tickets
+        if (e != hipSuccess) return -1;
+        a.fuzz_mode = TE_FUZZ_APPLY;
+        a.fuzz_state = L->fuzz_states;
+    }
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
-    if (L->slot_layout)
+    if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
+        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.fuzz_mode != TE_FUZZ_OFF)
+        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (L->slot_layout)
         hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
     else
         hipLaunchKernelGGL(te_edit_tiles<MODE_CONTIG>, dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -154,3 +154,16 @@ def test_gpu_required_without_device(built):
     te = TA.TcpEdit(["--fixcsum"])
     with pytest.raises(RuntimeError, match="no HIP device"):
         TA.Batch(te, open(os.path.join(ROOT, "tests", "golden", "test.pcap"), "rb").read())
+
+
+def test_fuzz_options_reach_the_device_config(built):
+    import oracle_lib as O
+    _, c, _ = derive(["--fuzz-seed=42", "--fuzz-factor=2"])
+    assert c.fuzz_seed == O.mix_seed(42) and c.fuzz_factor == 2
+    _, c, _ = derive(["--fuzz-seed=42"])  # fuzz-factor defaults to 8 (tcpedit_opts.def:324-330)
+    assert c.fuzz_seed == O.mix_seed(42) and c.fuzz_factor == 8
+    _, c, _ = derive(["--fixcsum"])
+    assert c.fuzz_seed == 0
+    for bad in (["--fuzz-factor=2"], ["--fuzz-seed=1", "--fuzz-factor=0"]):
+        with pytest.raises(ValueError):
+            derive(bad)
