@@ -135,6 +135,16 @@ int tcpedit_batch_time(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double
 int tcpedit_batch_time_kernels(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run,
                                double *ms_kernel);
 void tcpedit_batch_close(tcpedit_batch_t *b);
+/* --fuzz-seed across shards.  The reference draws one tcpr_random() per record that
+ * reaches the fuzz step from ONE run-wide state (fuzzing.c:8-20,87; tcpedit.c:250-258),
+ * so a shard's stream starts after the draws of every earlier shard.
+ * tcpedit_batch_fuzz_reach: records of the batch that reach the fuzz step (0 without
+ * --fuzz-seed), counted on the device without editing or moving the state; <0 on error.
+ * tcpedit_fuzz_skip: advance the context's state by `draws` tcpr_random() calls, as if
+ * that many earlier records had reached the step (replaces fuzzing_init's seed for a
+ * shard, fuzzing.c:12-20). */
+int64_t tcpedit_batch_fuzz_reach(tcpedit_t *tcpedit, tcpedit_batch_t *b);
+int tcpedit_fuzz_skip(tcpedit_t *tcpedit, uint64_t draws);
 /* device pointers, for callers that keep the data in HBM (e.g. a sender) */
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b);
 uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b);

@@ -1676,6 +1676,9 @@ static int encoder_l2len(const ocfg_t *c, const uint8_t *packet, int pktlen)
 /* fuzzing: src/tcpedit/fuzzing.c:12-297 (state: fuzzing_init's statics)      */
 /* ------------------------------------------------------------------------- */
 static uint32_t g_fuzz_state, g_fuzz_factor; /* fuzz_seed, fuzz_factor (fuzzing.c:8-20) */
+/* test hooks for a sharded run: the draws the last run made, and draws to skip at the
+   start of the next runs (a shard's stream starts after the earlier shards' draws) */
+static uint64_t g_fuzz_draws, g_fuzz_skip;
 
 /* the encoder's proto function on the edited packet (plugin_proto): en10mb.c:741-762,
    user.c:273-282 (always an error), hdlc.c:299-311 (the protocol field) */
@@ -1718,6 +1721,7 @@ static int oracle_fuzzing(const ocfg_t *c, ohdr_t *h, uint8_t *packet) /* fuzzin
 {
     int chksum_update_required = 0;
     uint32_t r = tcpr_random(&g_fuzz_state), s;
+    g_fuzz_draws++;
     if ((r % g_fuzz_factor) != 0)
         return 0;
     uint8_t *end_ptr = packet + h->caplen, *l4data;
@@ -2849,6 +2853,9 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
     ostate_t st;
     memset(&st, 0, sizeof(st));
     g_fuzz_state = c.fuzz_seed; /* fuzzing_init (tcprewrite.c:102-103, fuzzing.c:12-20) */
+    for (uint64_t k = 0; k < g_fuzz_skip; k++)
+        tcpr_random(&g_fuzz_state);
+    g_fuzz_draws = 0;
     g_fuzz_factor = c.fuzz_factor ? c.fuzz_factor : 8;
     size_t ip_ = 24;
     uint64_t packetnum = 0;
@@ -2915,6 +2922,9 @@ out:
 int oracle_warn_count(void) { return g_warn_count; }
 
 /* Exposed for tests: the seed/sequence mixer (parse_args.c:214-230). */
+uint64_t oracle_fuzz_draws(void) { return g_fuzz_draws; }
+void oracle_set_fuzz_skip(uint64_t draws) { g_fuzz_skip = draws; }
+
 uint32_t oracle_mix_seed(uint32_t seed)
 {
     for (int i = 0; i < 5; ++i)

@@ -80,6 +80,8 @@ def load():
         "tcpedit_batch_time_kernels": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_close": (None, [vp]),
+        "tcpedit_batch_fuzz_reach": (ctypes.c_int64, [vp, vp]),
+        "tcpedit_fuzz_skip": (c_int, [vp, u64]),
         "tcpedit_batch_device_output": (vp, [vp]),
         "tcpedit_batch_input_bytes": (u64, [vp]),
         "tcpedit_rewrite_pcap": (c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
@@ -214,6 +216,11 @@ class TcpEdit:
             return rc, bytes(memoryview(out)[:olen.value])
         return rc, memoryview(out)[:olen.value]
 
+    def fuzz_skip(self, draws: int):
+        """advance the --fuzz-seed state by `draws` tcpr_random() calls (tcpedit_fuzz_skip)"""
+        if self._L.tcpedit_fuzz_skip(self._ctx, int(draws)) < 0:
+            raise RuntimeError(self.geterr())
+
     def packet(self, hdr, data: bytearray, direction=TCPR_DIR_C2S):
         """tcpedit_packet(): edits `data` (bytearray, >= MAXPACKET bytes recommended) in place.
 
@@ -258,6 +265,13 @@ class Batch:
         if not p:
             return np.zeros(0, np.uint8)
         return np.ctypeslib.as_array(p, shape=(r.packets,)).copy()
+
+    def fuzz_reach(self) -> int:
+        """records of this batch that reach the --fuzz-seed step (tcpedit_batch_fuzz_reach)"""
+        n = self._L.tcpedit_batch_fuzz_reach(self._te._ctx, self._b)
+        if n < 0:
+            raise RuntimeError(self._te.geterr())
+        return int(n)
 
     def time(self, iters):
         ms = ctypes.c_double()

@@ -85,6 +85,7 @@ struct tcpedit_batch_s {
     uint32_t last_cnt_off;   /* workspace offset of the last launch's counter set */
     uint32_t *d_fuzz;        /* --fuzz-seed: per-record RNG states, then a word per 1024 records */
     uint64_t fuzz_cap;       /* records d_fuzz has room for */
+    int fuzz_probe_only;     /* the next launch only counts records reaching the fuzz step */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
     /* results */
@@ -938,6 +939,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.fuzz_blk = b->d_fuzz + b->fuzz_cap + 1;
         L.fuzz_words = t->d_fuzz_words;
         L.n_pkts = (uint32_t)b->n_pkts;
+        L.fuzz_probe_only = b->fuzz_probe_only;
     }
     const int rc = te_launch_edit(&L, t->stream);
     if (!generic_only) {
@@ -1042,6 +1044,64 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
     t->packetnum += b->counters[TE_CNT_PACKETS];
     t->total_bytes += b->counters[TE_CNT_BYTES_OUT];
     t->pkts_edited += b->counters[TE_CNT_EDITED];
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
+/* host copy of tcpr_random's LCG advanced by k steps (te_fuzz_states does the same on
+   the device) */
+static uint32_t lcg_jump_host(uint32_t x, uint64_t k)
+{
+    uint32_t am = 1, ap = 0, cm = 1103515245u, cp = 12345u;
+    for (; k; k >>= 1) {
+        if (k & 1) {
+            am *= cm;
+            ap = ap * cm + cp;
+        }
+        cp = (cm + 1u) * cp;
+        cm *= cm;
+    }
+    return am * x + ap;
+}
+
+int64_t tcpedit_batch_fuzz_reach(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    if (!t || !b)
+        return TCPEDIT_ERROR;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (!t->cfg.fuzz_seed || !b->n_pkts)
+        return 0;
+    uint32_t w[4];
+    b->fuzz_probe_only = 1;
+    const int rc = launch(b, -1);
+    b->fuzz_probe_only = 0;
+    if (rc != 0) {
+        te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return TCPEDIT_ERROR;
+    }
+    HIPCHK(t, hipMemcpyAsync(w, t->d_fuzz_words, sizeof(w), hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return (int64_t)w[2];
+fail:
+    return TCPEDIT_ERROR;
+}
+
+int tcpedit_fuzz_skip(tcpedit_t *t, uint64_t draws)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (!t->cfg.fuzz_seed || !draws)
+        return TCPEDIT_OK;
+    uint32_t w[4];
+    HIPCHK(t, hipMemcpyAsync(w, t->d_fuzz_words, sizeof(w), hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    w[0] = lcg_jump_host(w[0], 3 * draws); /* tcpr_random = three LCG steps (utils.c:436-458) */
+    HIPCHK(t, hipMemcpyAsync(t->d_fuzz_words, w, sizeof(w), hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
     return TCPEDIT_OK;
 fail:
     return TCPEDIT_ERROR;

@@ -117,8 +117,10 @@ typedef struct {
     /* --fuzz-seed (generic lane only): a reach pass, then per-record RNG states, then the edit */
     uint32_t *fuzz_states;    /* device: n_pkts words, or NULL (no fuzzing) */
     uint32_t *fuzz_blk;       /* device: a word per 1024 records */
-    uint32_t *fuzz_words;     /* device: [0] the context's running RNG state, [1] this launch's start */
+    uint32_t *fuzz_words;     /* device: [0] the context's running RNG state, [1] this launch's start,
+                                 [2] records of the launch that reached the fuzz step */
     uint32_t n_pkts;          /* records in the launch */
+    int fuzz_probe_only;      /* count the reaching records (words[2]) and stop: no edit, no state change */
 } te_launch_t;
 
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */

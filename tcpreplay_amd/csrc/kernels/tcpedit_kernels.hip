@@ -1520,7 +1520,8 @@ __global__ void __launch_bounds__(FZ_BLOCK) te_fuzz_count(const uint8_t *st, uin
 }
 
 // one block: exclusive scan of the block counts in place, then the state words
-__global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nblk, uint32_t *words) {
+// (words[2] = reaching records; advance = 0 leaves the running state alone)
+__global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nblk, uint32_t *words, int advance) {
     __shared__ uint32_t wsum[1024 / 64];
     uint64_t carry = 0;
     for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
@@ -1533,8 +1534,11 @@ __global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nbl
     }
     if (threadIdx.x == 0) {
         const uint32_t s0 = words[0];
-        words[1] = s0;
-        words[0] = lcg_jump(s0, 3ull * carry);
+        words[2] = (uint32_t)carry;
+        if (advance) {
+            words[1] = s0;
+            words[0] = lcg_jump(s0, 3ull * carry);
+        }
     }
 }
 
@@ -1730,7 +1734,9 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         const uint32_t nblk = (L->n_pkts + FZ_PER_BLOCK - 1) / FZ_PER_BLOCK;
         hipLaunchKernelGGL(te_fuzz_count, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
                            L->n_pkts, L->fuzz_blk);
-        hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words);
+        hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words,
+                           L->fuzz_probe_only ? 0 : 1);
+        if (L->fuzz_probe_only) return hipGetLastError() == hipSuccess ? 0 : -1;
         hipLaunchKernelGGL(te_fuzz_states, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
                            L->n_pkts, (const uint32_t *)L->fuzz_blk, (const uint32_t *)L->fuzz_words,
                            L->fuzz_states);

@@ -8,7 +8,9 @@ edited start to finish on its own GPU.  The only cross-rank traffic is
   * one all-reduce (sum) of the counter vector: RCCL over xGMI when the process
     group is "nccl", gloo on CPU.
 Each rank writes its own segment into the output file with pwrite; no packet
-data crosses a collective.
+data crosses a collective.  --fuzz-seed adds one exchange before the edit: its RNG
+is a single run-wide stream (fuzzing.c:8-20,87), so the ranks all-gather how many
+of their records reach the fuzz step and each skips the draws of the ranks before it.
 
 Hard errors keep tcprewrite's semantics (tcprewrite.c:156-160): the output is
 cut at the first failing record in file order, so the first erroring shard is
@@ -63,13 +65,23 @@ def plan(pcap: bytes, n: int) -> ShardPlan:
     return ShardPlan(list(off), list(base), int(total))
 
 
-def gpu_editor(image: bytes, args, cache: Optional[bytes], pkt_base: int, device: int) -> ShardResult:
-    """Edit one shard on `device` through the C-ABI batch API."""
+def fuzz_enabled(args) -> bool:
+    """--fuzz-seed given: the one option whose records are not independent (fuzzing.c:87)"""
+    return any(a == "--fuzz-seed" or a.startswith("--fuzz-seed=") for a in args)
+
+
+def gpu_editor(image: bytes, args, cache: Optional[bytes], pkt_base: int, device: int,
+               fuzz_prefix: Optional[Callable[[int], int]] = None) -> ShardResult:
+    """Edit one shard on `device` through the C-ABI batch API.  With --fuzz-seed,
+    `fuzz_prefix(reaching records of this shard)` returns the RNG draws of every earlier
+    shard, and the context's state skips them before the edit."""
     from . import Batch, TcpEdit
     te = TcpEdit(args, device=device)
     try:
         b = Batch(te, image, cache, pkt_base=pkt_base)
         try:
+            if fuzz_prefix is not None:
+                te.fuzz_skip(fuzz_prefix(b.fuzz_reach()))
             rc = b.run()
             r = b.result()
             return ShardResult(rc, b.output(), [int(getattr(r, n)) for n in COUNTER_NAMES],
@@ -99,13 +111,26 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
     world, rank = dist.get_world_size(), dist.get_rank()
     p = plan(pcap, world)
     shard = p.image(pcap, rank)
+    cdev = _collective_device(dist)
+
+    def fuzz_prefix(reach: int) -> int:
+        # --fuzz-seed's one exchange: an exclusive prefix over ranks of the records that
+        # reach the fuzz step (8 B per rank), so every shard's RNG stream starts where
+        # the single-process run's would
+        mine = torch.tensor([reach], dtype=torch.int64, device=cdev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        return sum(int(v.item()) for v in allv[:rank])
+
+    fz = fuzz_prefix if fuzz_enabled(args) else None
     if editor is None:
         dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        res = gpu_editor(shard, args, cache, p.pkt_base[rank], dev)
+        res = gpu_editor(shard, args, cache, p.pkt_base[rank], dev, fuzz_prefix=fz)
+    elif fz is not None:
+        res = editor(shard, args, cache, p.pkt_base[rank], fuzz_prefix=fz)
     else:
         res = editor(shard, args, cache, p.pkt_base[rank])
     seg = res.image[PCAP_HDR_LEN:]
-    cdev = _collective_device(dist)
 
     # 1) placement: (segment bytes, error flag) from every rank
     mine = torch.tensor([len(seg), 1 if res.rc < 0 else 0], dtype=torch.int64, device=cdev)

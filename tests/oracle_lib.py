@@ -28,6 +28,9 @@ def load():
         lib.oracle_mix_seed.restype = ctypes.c_uint32
         lib.oracle_mix_seed.argtypes = [ctypes.c_uint32]
         lib.oracle_warn_count.restype = ctypes.c_int
+        lib.oracle_fuzz_draws.restype = ctypes.c_uint64
+        lib.oracle_set_fuzz_skip.argtypes = [ctypes.c_uint64]
+        lib.oracle_set_fuzz_skip.restype = None
         _lib = lib
     return _lib
 
@@ -57,3 +60,18 @@ def rewrite(pcap: bytes, args, cache: bytes = None, want_status=False):
 
 def mix_seed(seed: int) -> int:
     return load().oracle_mix_seed(seed)
+
+
+def fuzz_draws() -> int:
+    """tcpr_random() draws the last rewrite() made for --fuzz-seed"""
+    return int(load().oracle_fuzz_draws())
+
+
+def rewrite_skipping(pcap: bytes, args, cache: bytes = None, skip: int = 0):
+    """rewrite() with the --fuzz-seed stream advanced by `skip` draws first (a shard)"""
+    lib = load()
+    lib.oracle_set_fuzz_skip(int(skip))
+    try:
+        return rewrite(pcap, args, cache)
+    finally:
+        lib.oracle_set_fuzz_skip(0)

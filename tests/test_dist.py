@@ -36,11 +36,15 @@ def slice_cache(cache: bytes, first: int, count: int) -> bytes:
 def oracle_editor_for(pcap, world):
     p = D.plan(pcap, world)
 
-    def editor(image, args, cache, pkt_base):
+    def editor(image, args, cache, pkt_base, fuzz_prefix=None):
         k = p.pkt_base.index(pkt_base) if p.pkt_base.count(pkt_base) == 1 else \
             next(i for i in range(world) if p.pkt_base[i] == pkt_base and p.image(pcap, i) == image)
         sub = slice_cache(cache, pkt_base, p.count(k)) if cache else None
-        rc, out = O.rewrite(image, args, sub)
+        skip = 0
+        if fuzz_prefix is not None:  # reach count first (it does not depend on the RNG state)
+            O.rewrite(image, args, sub)
+            skip = fuzz_prefix(O.fuzz_draws())
+        rc, out = O.rewrite_skipping(image, args, sub, skip)
         return D.ShardResult(rc, out, [p.count(k)] + [0] * (len(D.COUNTER_NAMES) - 1))
     return editor
 
@@ -115,10 +119,14 @@ def test_slice_cache_matches_global_lookup(built):
 
 
 # ---------------------------------------------------------------- gloo world_size 2 (oracle-edited shards)
-@pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix"])
+@pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix", "fuzz_golden", "fuzz_imix"])
 def test_two_rank_rewrite_equals_single_process(built, case):
     if case == "fixcsum":
         pcap, args, cache = G.read("test.pcap"), ["--fixcsum"], None
+    elif case == "fuzz_golden":  # the exchange: ranks skip the earlier ranks' RNG draws
+        pcap, args, cache = G.read("test.pcap"), ["--fuzz-seed=42", "--fuzz-factor=2"], None
+    elif case == "fuzz_imix":
+        pcap, args, cache = S.pcap_imix(5000, seed=6), ["--fuzz-seed=5", "--fuzz-factor=1", "--fixcsum"], None
     elif case == "c4_cache":
         pcap, args, cache = G.read("test.pcap"), C4_ARGS[:1] + ["--enet-vlan=add", "--enet-vlan-tag=45",
                                                                  "--fixcsum"], G.read("test.auto_router")
@@ -148,10 +156,13 @@ def test_hard_error_truncates_at_first_failing_record(built, bad_shard):
 
 # ---------------------------------------------------------------- the device path, two ranks on one GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["c4_cache", "c3_imix"])
+@pytest.mark.parametrize("case", ["c4_cache", "c3_imix", "fuzz_imix"])
 def test_two_rank_gpu_rewrite_equals_oracle(built, case):
     if case == "c4_cache":
         pcap, args, cache = G.read("test.pcap"), C4_ARGS, G.read("test.auto_router")
+    elif case == "fuzz_imix":  # reach counts all-gathered, each rank skips the earlier draws
+        pcap, cache = S.pcap_imix(20_000, seed=7), None
+        args = ["--fuzz-seed=8", "--fuzz-factor=2", "--enet-vlan=add", "--enet-vlan-tag=9", "--fixcsum"]
     else:
         pcap, cache = S.pcap_imix(20_000, seed=6), None
         args = ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]
