@@ -41,8 +41,12 @@ WORKLOADS = {
     "c2x10": ("pcap_fixed", dict(size=64), ["--seed=42", "--fixcsum"],
               "--seed=42 --fixcsum on 10M x 64B (C2 at 1.6 GB moved: launch amortised, HBM- not cache-resident; "
               "SURVEY 8(d))"),
+    "fz": ("pcap_imix", dict(), ["--fuzz-seed=42", "--fuzz-factor=2"],
+           "--fuzz-seed=42 --fuzz-factor=2 (the l7fuzzing golden's options) on IMIX 64/570/1514 7:4:1: reach pass, "
+           "RNG-state scan, edit pass (SURVEY 8(f) rank 4)"),
 }
-DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000}
+DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
+                   "fz": 10_000_000}
 CACHED = {"c4"}  # workloads with a tcpprep cache (synth.tcpprep_cache: C2S/S2C runs by flow)
 
 
@@ -136,7 +140,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
-    ap.add_argument("--extra", default="c3,c4,c5,c2x10",
+    ap.add_argument("--extra", default="c3,c4,c5,c2x10,fz",
                     help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
                     "half --cpu-threads threads)")
