@@ -1,0 +1,431 @@
+/*
+ * tcpprep_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker, never shipped).
+ *
+ * A plain-C, single-threaded CPU restatement of tcpprep's per-packet
+ * classification pass (src/tcpprep.c:339-587 process_raw_packets) for the
+ * per-packet modes -- CIDR (-c), MAC (-e), port (-p) -- with --reverse,
+ * --nonip, --comment/--no-arg-comment and the include/exclude filters
+ * (-x/-X P:list, S:/D:/B:/E: CIDR), and the cache file writer
+ * (src/common/cache.c:146-219 write_cache, :259-314 add_cache).  The auto
+ * (tree) modes and regex mode are not restated (out of scope).
+ *
+ * Pinning: checked byte-for-byte against the reference's own cache files
+ * (test/test.cidr, .cidr_reverse, .mac, .mac_reverse, .port, .comment,
+ * .include_packets, .exclude_packets, .include_source, .include_dest, made by
+ * test/Makefile.am:93-104 from test/test.pcap), committed under tests/golden/,
+ * by tests/test_tcpprep.py.
+ *
+ * It is compiled into the same oracle/_build/liboracle.so as the tcpedit
+ * restatement (this file includes it, for the shared L2/L3/L4 locators and the
+ * CIDR parser).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.
+ */
+#include "tcpedit_oracle.c"
+
+#define TPO_MAXC 64
+
+enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3 };
+/* xX.h:34-41 */
+enum { XX_SOURCE = 1, XX_DEST = 2, XX_BOTH = 4, XX_EITHER = 8, XX_PACKET = 16, XX_EXCLUDE = 128 };
+
+typedef struct {
+    int mode, reverse, nonip, nocomment;
+    ocidr_t cidr[TPO_MAXC];
+    int ncidr;
+    uint8_t mac[TPO_MAXC][6];
+    int nmac, mac_first_empty;
+    int xx_mode;               /* 0 = none */
+    ocidr_t xx_cidr[TPO_MAXC];
+    int nxx_cidr;
+    uint64_t lmin[TPO_MAXC], lmax[TPO_MAXC];
+    int nlist;
+    uint8_t svc_tcp[65536], svc_udp[65536];
+    char comment[4096];
+    int has_comment;
+} tpo_opt_t;
+
+/* parse_cidr(..., ",") cidr.c:244-279 */
+static int tpo_cidr_list(ocidr_t *outv, int *n, char *s)
+{
+    char *tok = NULL, *net;
+    *n = 0;
+    mask_cidr6(&s, ",");
+    net = strtok_r(s, ",", &tok);
+    if (!net)
+        return 0;
+    if (!cidr2cidr(net, &outv[(*n)++]))
+        return 0;
+    for (;;) {
+        if (tok)
+            mask_cidr6(&tok, ",");
+        net = strtok_r(NULL, ",", &tok);
+        if (!net)
+            break;
+        if (*n >= TPO_MAXC || !cidr2cidr(net, &outv[(*n)++]))
+            return 0;
+    }
+    return 1;
+}
+
+/* mac2hex mac.c:37-62: partial parses leave the earlier bytes of `dst` in place */
+static void tpo_mac2hex(const char *mac, uint8_t *dst)
+{
+    while (isspace((unsigned char)*mac))
+        mac++;
+    for (int i = 0; i < 6; i++) {
+        char *pp;
+        long l = strtol(mac, &pp, 16);
+        if (pp == mac || l > 0xFF || l < 0)
+            return;
+        if (!(*pp == ':' || (i == 5 && (isspace((unsigned char)*pp) || *pp == '\0'))))
+            return;
+        dst[i] = (uint8_t)l;
+        mac = pp + 1;
+    }
+}
+
+/* parse_list list.c:61-130 (+ add_to_list :36-50); "^[0-9]+(-([0-9]+|\s*))?$" */
+static int tpo_list(tpo_opt_t *o, char *s)
+{
+    char *tok = NULL;
+    for (char *t = strtok_r(s, ",", &tok); t; t = strtok_r(NULL, ",", &tok)) {
+        char *p = t;
+        if (!isdigit((unsigned char)*p))
+            return 0;
+        while (isdigit((unsigned char)*p))
+            p++;
+        char *second = NULL;
+        if (*p == '-') {
+            *p = 0;
+            second = p + 1;
+            char *q = second;
+            if (isdigit((unsigned char)*q)) {
+                while (isdigit((unsigned char)*q))
+                    q++;
+            } else {
+                while (isspace((unsigned char)*q))
+                    q++;
+            }
+            if (*q)
+                return 0;
+        } else if (*p) {
+            return 0;
+        }
+        if (o->nlist >= TPO_MAXC)
+            return 0;
+        o->lmin[o->nlist] = strtoull(t, NULL, 0);
+        o->lmax[o->nlist] = second ? (second[0] ? strtoull(second, NULL, 0) : 0) : o->lmin[o->nlist];
+        o->nlist++;
+    }
+    return o->nlist > 0;
+}
+
+/* parse_xX_str xX.c:44-117 */
+static int tpo_xx(tpo_opt_t *o, const char *arg, int exclude)
+{
+    char buf[4096];
+    snprintf(buf, sizeof buf, "%s", arg);
+    if (!buf[0] || buf[1] != ':')
+        return 0;
+    int out;
+    switch (buf[0]) {
+    case 'B': out = XX_BOTH; break;
+    case 'D': out = XX_DEST; break;
+    case 'E': out = XX_EITHER; break;
+    case 'S': out = XX_SOURCE; break;
+    case 'P': out = XX_PACKET; break;
+    default: return 0;
+    }
+    if (out == XX_PACKET) {
+        if (!tpo_list(o, buf + 2))
+            return 0;
+    } else if (!tpo_cidr_list(o->xx_cidr, &o->nxx_cidr, buf + 2)) {
+        return 0;
+    }
+    o->xx_mode = out + (exclude ? XX_EXCLUDE : 0);
+    return 1;
+}
+
+/* option surface: tcpprep_opts.def (long forms only) */
+static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
+{
+    memset(o, 0, sizeof(*o));
+    for (int i = 0; i <= 1023; i++) /* tcpprep_init, tcpprep_api.c:50-53 */
+        o->svc_tcp[i] = o->svc_udp[i] = 1;
+    char args[4096] = "";
+    for (int i = 0; i < argc; i++) {
+        const char *a = argv[i];
+        const char *eq = strchr(a, '=');
+        const char *v = eq ? eq + 1 : "";
+        size_t nl = eq ? (size_t)(eq - a) : strlen(a);
+#define IS(n) (nl == strlen(n) && !strncmp(a, n, nl))
+        if (IS("--cidr")) {
+            char b[4096];
+            snprintf(b, sizeof b, "%s", v);
+            o->mode = TPO_CIDR;
+            if (!tpo_cidr_list(o->cidr, &o->ncidr, b))
+                return -1;
+        } else if (IS("--mac")) {
+            /* macinstring mac.c:76-115 re-tokenises the string per packet: pre-resolve it */
+            char b[4096];
+            snprintf(b, sizeof b, "%s", v);
+            o->mode = TPO_MAC;
+            uint8_t cur[6] = {0};
+            char *tok = NULL;
+            char *t = strtok_r(b, ",", &tok);
+            if (t == NULL || !strlen(t)) {
+                o->mac_first_empty = 1;
+            } else {
+                do {
+                    tpo_mac2hex(t, cur);
+                    if (o->nmac < TPO_MAXC)
+                        memcpy(o->mac[o->nmac++], cur, 6);
+                } while ((t = strtok_r(NULL, ",", &tok)) != NULL);
+            }
+        } else if (IS("--port")) {
+            o->mode = TPO_PORT;
+        } else if (IS("--reverse")) {
+            o->reverse = 1;
+        } else if (IS("--nonip")) {
+            o->nonip = 1; /* DIR_SERVER (tcpprep_opts.def:498) */
+        } else if (IS("--no-arg-comment")) {
+            o->nocomment = 1;
+        } else if (IS("--comment")) {
+            snprintf(o->comment, sizeof o->comment, "%s", v);
+            o->has_comment = 1;
+        } else if (IS("--include") || IS("--exclude")) {
+            if (!tpo_xx(o, v, IS("--exclude")))
+                return -1;
+        } else {
+            return -1;
+        }
+        if (!IS("--comment")) { /* tcpprep_api.c:160-176 skips -C <comment> */
+            strncat(args, a, sizeof args - strlen(args) - 2);
+            strcat(args, " ");
+        }
+#undef IS
+    }
+    if (!o->mode)
+        return -1;
+    /* tcpprep_post_args, tcpprep_api.c:160-197: "args\ncomment" */
+    char full[8192] = "";
+    if (!o->nocomment && args[0]) {
+        args[strlen(args) - 1] = 0;
+        snprintf(full, sizeof full, "%s", args);
+    }
+    if (o->has_comment) {
+        strcat(full, "\n");
+        strncat(full, o->comment, sizeof full - strlen(full) - 1);
+    }
+    snprintf(o->comment, sizeof o->comment, "%s", full);
+    return 0;
+}
+
+/* check_list list.c:139-156 */
+static int tpo_check_list(const tpo_opt_t *o, uint64_t v)
+{
+    for (int i = 0; i < o->nlist; i++) {
+        uint64_t mn = o->lmin[i], mx = o->lmax[i];
+        if (mn != 0 && mx != 0) {
+            if (v >= mn && v <= mx)
+                return 1;
+        } else if (mn == 0) {
+            if (v <= mx)
+                return 1;
+        } else if (v >= mn) {
+            return 1;
+        }
+    }
+    return 0;
+}
+
+/* check_ip_cidr cidr.c:535-564 / check_ip6_cidr :570-598 over a list */
+static int tpo_in4(const ocidr_t *c, int n, uint32_t ip)
+{
+    if (n == 0)
+        return 1;
+    for (int i = 0; i < n; i++)
+        if (ip_in_cidr(&c[i], ip))
+            return 1;
+    return 0;
+}
+static int tpo_in6(const ocidr_t *c, int n, const uint8_t *a)
+{
+    if (n == 0)
+        return 1;
+    for (int i = 0; i < n; i++)
+        if (ip6_in_cidr(&c[i], a))
+            return 1;
+    return 0;
+}
+
+/* process_xX_by_cidr_ipv4/ipv6 xX.c:124-236: 1 = SEND */
+static int tpo_xx_cidr(const tpo_opt_t *o, const uint8_t *ip, int v6)
+{
+    uint32_t s4 = 0, d4 = 0;
+    int s, d;
+    if (v6) {
+        s = tpo_in6(o->xx_cidr, o->nxx_cidr, ip + 8);
+        d = tpo_in6(o->xx_cidr, o->nxx_cidr, ip + 24);
+    } else {
+        memcpy(&s4, ip + 12, 4);
+        memcpy(&d4, ip + 16, 4);
+        s = tpo_in4(o->xx_cidr, o->nxx_cidr, s4);
+        d = tpo_in4(o->xx_cidr, o->nxx_cidr, d4);
+    }
+    int m = o->xx_mode & ~XX_EXCLUDE, hit;
+    switch (m) {
+    case XX_SOURCE: hit = s; break;
+    case XX_DEST: hit = d; break;
+    case XX_BOTH: hit = d && s; break;
+    case XX_EITHER: hit = d || s; break;
+    default: return (o->xx_mode & XX_EXCLUDE) ? 0 : 1; /* "Unable to determine action" */
+    }
+    return (o->xx_mode & XX_EXCLUDE) ? !hit : hit;
+}
+
+/* check_dst_port tcpprep.c:211-295: returns 1 (C2S) / 0 (S2C) / nonip */
+static int tpo_dst_port(const tpo_opt_t *o, uint8_t *ip, int v6, int len)
+{
+    uint8_t *end = ip + len, *l4;
+    uint8_t proto;
+    if (!v6) {
+        if (len < ((ip[0] & 0x0f) * 4) + 4)
+            return 0;
+        proto = ip[9];
+        l4 = get_layer4_v4(ip, end);
+    } else {
+        if (len < 40 + 4)
+            return 0;
+        proto = get_ipv6_l4proto(ip, end);
+        if ((l4 = get_layer4_v6(ip, end)) == NULL)
+            return 0;
+    }
+    if (l4 == NULL)
+        return 0;
+    if (proto == 6) {
+        if (end - l4 < 20)
+            return 0;
+        return o->svc_tcp[(l4[2] << 8) | l4[3]] ? 1 : 0;
+    }
+    if (proto == 17) {
+        if (end - l4 < 8)
+            return 0;
+        return o->svc_udp[(l4[2] << 8) | l4[3]] ? 1 : 0;
+    }
+    return o->nonip;
+}
+
+static uint32_t tpo_rd32(const uint8_t *p, int sw)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return sw ? __builtin_bswap32(v) : v;
+}
+
+/*
+ * tcpprep_oracle_run: classify a whole pcap image and write the cache file
+ * (header + comment + packed 2-bit entries) into `out`.  Returns the cache
+ * size, or -1 on an option error, -2 on a bad pcap, -3 if `cap` is too small.
+ */
+long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, uint8_t *out, size_t cap)
+{
+    static tpo_opt_t o;
+    if (tpo_parse(&o, argc, argv) < 0)
+        return -1;
+    if (len < 24)
+        return -2;
+    uint32_t magic;
+    memcpy(&magic, pcap, 4);
+    int sw;
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du)
+        sw = 0;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u)
+        sw = 1;
+    else
+        return -2;
+    size_t clen = strlen(o.comment);
+    size_t hdr = 24 + clen;
+    if (cap < hdr)
+        return -3;
+    memset(out, 0, cap);
+    uint64_t packetnum = 0, entries = 0;
+    static uint8_t pkt[MAXPACKET + 64];
+    for (size_t off = 24; off + 16 <= len;) {
+        uint32_t caplen = tpo_rd32(pcap + off + 8, sw);
+        if (caplen > 262144u || off + 16 + caplen > len)
+            break; /* libpcap stops */
+        memset(pkt, 0, caplen + 64);
+        memcpy(pkt, pcap + off + 16, caplen);
+        off += 16 + caplen;
+        packetnum++;
+        int send = 1, dir = 0, add = 1; /* dir: 1 = C2S */
+        if (o.nlist && !!(o.xx_mode & XX_EXCLUDE) == tpo_check_list(&o, packetnum)) {
+            send = 0; /* tcpprep.c:362-375 */
+            goto ADD;
+        }
+        if (o.mode != TPO_MAC) {
+            uint16_t proto = 0;
+            uint32_t l2len = 0, l2off = 0, voff = 0;
+            int res = caplen ? get_l2len_protocol(pkt, caplen, &proto, &l2len, &l2off, &voff) : -1;
+            int v4 = res != -1 && l2len + 20 <= caplen && proto == 0x0800;  /* get_ipv4 get.c:483-541 */
+            int v6 = !v4 && res != -1 && l2len + 40 <= caplen && proto == 0x86DD; /* get_ipv6 :550-608 */
+            if (!v4 && !v6) {
+                dir = o.nonip; /* add_cache(SEND, options->nonip) */
+                goto ADD;
+            }
+            uint8_t *ip = pkt + l2len;
+            if (o.nxx_cidr && o.xx_mode && !tpo_xx_cidr(&o, ip, v6)) {
+                send = 0;
+                goto ADD;
+            }
+            if (o.mode == TPO_CIDR) {
+                uint32_t s4;
+                memcpy(&s4, ip + 12, 4);
+                dir = v6 ? tpo_in6(o.cidr, o.ncidr, ip + 8) : tpo_in4(o.cidr, o.ncidr, s4);
+                if (o.reverse)
+                    dir = !dir;
+            } else {
+                dir = tpo_dst_port(&o, ip, v6, (int)caplen - (int)l2len);
+            }
+        } else {
+            if (caplen < 14) {
+                add = 0; /* tcpprep.c:465-468: `break` before add_cache */
+                goto ADD;
+            }
+            dir = 0;
+            if (!o.mac_first_empty)
+                for (int m = 0; m < o.nmac; m++)
+                    if (!memcmp(pkt + 6, o.mac[m], 6)) {
+                        dir = 1;
+                        break;
+                    }
+            if (o.reverse)
+                dir = !dir;
+        }
+    ADD:
+        if (add) { /* add_cache cache.c:259-314 */
+            size_t byte = hdr + entries / 4;
+            if (byte >= cap)
+                return -3;
+            unsigned bit = (unsigned)(entries % 4) * 2 + 1;
+            if (send) {
+                out[byte] += (uint8_t)(1u << bit);
+                if (dir == 1)
+                    out[byte] += (uint8_t)(1u << (bit - 1));
+            }
+            entries++;
+        }
+    }
+    /* write_cache cache.c:146-219 */
+    memcpy(out, "tcpprep\0", 8);
+    memcpy(out + 8, "04\0\0", 4);
+    for (int i = 0; i < 8; i++)
+        out[12 + i] = (uint8_t)(packetnum >> (56 - 8 * i));
+    out[20] = 0;
+    out[21] = 4;
+    out[22] = (uint8_t)(clen >> 8);
+    out[23] = (uint8_t)clen;
+    memcpy(out + 24, o.comment, clen);
+    return (long)(hdr + (entries + 3) / 4);
+}

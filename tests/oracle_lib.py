@@ -75,3 +75,19 @@ def rewrite_skipping(pcap: bytes, args, cache: bytes = None, skip: int = 0):
         return rewrite(pcap, args, cache)
     finally:
         lib.oracle_set_fuzz_skip(0)
+
+
+def tcpprep(pcap: bytes, args):
+    """tcpprep_oracle_run: the CPU restatement of tcpprep's per-packet modes -> cache file bytes."""
+    lib = load()
+    fn = lib.tcpprep_oracle_run
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p, ctypes.c_size_t,
+                   ctypes.c_char_p, ctypes.c_size_t]
+    argv = (ctypes.c_char_p * len(args))(*[a.encode() for a in args])
+    cap = 24 + 8192 + len(pcap) // 16 + 64
+    out = ctypes.create_string_buffer(cap)
+    n = fn(len(args), argv, pcap, len(pcap), out, cap)
+    if n < 0:
+        raise ValueError(f"tcpprep oracle failed ({n}) for {args}")
+    return out.raw[:n]
