@@ -1020,3 +1020,6 @@ int tcpedit_set_port_map(tcpedit_t *t, char *s)
     t->dev_dirty = 1;
     return TCPEDIT_OK;
 }
+
+/* one CIDR (cidr2cidr, cidr.c:130-221) for tcpprep's option parser (tp_api.c) */
+int te_parse_cidr(char *s, te_cidr_t *c) { return parse_one_cidr(s, c); }

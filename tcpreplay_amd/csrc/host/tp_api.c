@@ -1,0 +1,464 @@
+/*
+ * tp_api.c -- host side of the gfx950 tcpprep classification pass
+ * (include/tcpprep.h).  Options -> tp_dev_cfg_t, the record walk (what
+ * libpcap's pcap_next does for process_raw_packets, src/tcpprep.c:353), one
+ * kernel launch (tcpprep_kernels.hip), and the v04 cache header
+ * (write_cache, src/common/cache.c:146-219).
+ */
+#define _GNU_SOURCE
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__
+#endif
+#include <ctype.h>
+#include <hip/hip_runtime_api.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../../../include/tcpprep.h"
+#include "tp_dev_cfg.h"
+
+int te_parse_cidr(char *s, te_cidr_t *c); /* te_args.c */
+
+struct tcpprep_hip_s {
+    tp_dev_cfg_t cfg;
+    int nocomment, has_comment;
+    char comment[8192]; /* the final "args\ncomment" string */
+    char errstr[1024];
+};
+
+static int tp_err(tcpprep_hip_t *t, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t->errstr, sizeof t->errstr, fmt, ap);
+    va_end(ap);
+    return -1;
+}
+
+int tcpprep_init(tcpprep_hip_t **out)
+{
+    if (!out)
+        return -1;
+    tcpprep_hip_t *t = calloc(1, sizeof(*t));
+    if (!t)
+        return -1;
+    for (int p = 0; p <= 1023; p++) { /* tcpprep_api.c:50-53 */
+        t->cfg.svc_tcp[p >> 5] |= 1u << (p & 31);
+        t->cfg.svc_udp[p >> 5] |= 1u << (p & 31);
+    }
+    *out = t;
+    return 0;
+}
+
+int tcpprep_close(tcpprep_hip_t **t)
+{
+    if (t && *t) {
+        free(*t);
+        *t = NULL;
+    }
+    return 0;
+}
+
+const char *tcpprep_geterr(tcpprep_hip_t *t) { return t ? t->errstr : NULL; }
+
+/* parse_cidr(&list, s, ","): cidr.c:244-279 (a ',' list never hides v6 colons) */
+static int cidr_list(tcpprep_hip_t *t, const char *arg, te_cidr_t *v, int32_t *n, const char *what)
+{
+    char buf[4096], *tok = NULL;
+    snprintf(buf, sizeof buf, "%s", arg);
+    *n = 0;
+    for (char *s = strtok_r(buf, ",", &tok); s; s = strtok_r(NULL, ",", &tok)) {
+        if (*n >= TP_MAXC)
+            return tp_err(t, "%s: more than %d CIDRs", what, TP_MAXC);
+        if (!te_parse_cidr(s, &v[(*n)++]))
+            return tp_err(t, "Unable to parse %s: %s", what, arg);
+    }
+    return *n ? 0 : tp_err(t, "Unable to parse %s: %s", what, arg);
+}
+
+/* mac2hex (mac.c:37-62): a partial parse keeps the earlier bytes of dst */
+static void mac2hex(const char *mac, uint8_t *dst)
+{
+    while (isspace((unsigned char)*mac))
+        mac++;
+    for (int i = 0; i < 6; i++) {
+        char *pp;
+        long l = strtol(mac, &pp, 16);
+        if (pp == mac || l > 0xFF || l < 0)
+            return;
+        if (!(*pp == ':' || (i == 5 && (isspace((unsigned char)*pp) || *pp == '\0'))))
+            return;
+        dst[i] = (uint8_t)l;
+        mac = pp + 1;
+    }
+}
+
+/* parse_list (list.c:61-130): "^[0-9]+(-([0-9]+|\s*))?$" per ',' token */
+static int packet_list(tcpprep_hip_t *t, char *s)
+{
+    tp_dev_cfg_t *c = &t->cfg;
+    char *tok = NULL;
+    c->nlist = 0;
+    for (char *e = strtok_r(s, ",", &tok); e; e = strtok_r(NULL, ",", &tok)) {
+        char *p = e, *second = NULL;
+        if (!isdigit((unsigned char)*p))
+            return tp_err(t, "Unable to parse: %s", e);
+        while (isdigit((unsigned char)*p))
+            p++;
+        if (*p == '-') {
+            *p++ = 0;
+            second = p;
+            if (isdigit((unsigned char)*p))
+                while (isdigit((unsigned char)*p))
+                    p++;
+            else
+                while (isspace((unsigned char)*p))
+                    p++;
+        }
+        if (*p)
+            return tp_err(t, "Unable to parse: %s", e);
+        if (c->nlist >= TP_MAXC)
+            return tp_err(t, "packet list longer than %d ranges", TP_MAXC);
+        uint64_t mn = strtoull(e, NULL, 0); /* add_to_list list.c:36-50 */
+        c->lmin[c->nlist] = mn;
+        c->lmax[c->nlist] = second ? (second[0] ? strtoull(second, NULL, 0) : 0) : mn;
+        c->nlist++;
+    }
+    return c->nlist ? 0 : tp_err(t, "Unable to parse packet list");
+}
+
+/* parse_xX_str (xX.c:44-117) for -x/--include and -X/--exclude */
+static int include_exclude(tcpprep_hip_t *t, const char *arg, int exclude)
+{
+    tp_dev_cfg_t *c = &t->cfg;
+    char buf[4096];
+    snprintf(buf, sizeof buf, "%s", arg);
+    if (!buf[0] || buf[1] != ':')
+        return tp_err(t, "Syntax error for option %s", exclude ? "--exclude" : "--include");
+    int out;
+    switch (buf[0]) {
+    case 'B': out = TP_XX_BOTH; break;
+    case 'D': out = TP_XX_DEST; break;
+    case 'E': out = TP_XX_EITHER; break;
+    case 'S': out = TP_XX_SOURCE; break;
+    case 'P': out = TP_XX_PACKET; break;
+    case 'F': return tp_err(t, "BPF include/exclude filters (F:) are not supported");
+    default: return tp_err(t, "Invalid include/exclude mode: %c", buf[0]);
+    }
+    int rc = out == TP_XX_PACKET ? packet_list(t, buf + 2) : cidr_list(t, buf + 2, c->xx_cidr, &c->nxx_cidr, "include/exclude CIDR");
+    if (rc < 0)
+        return -1;
+    c->xx_mode = out + (exclude ? TP_XX_EXCLUDE : 0);
+    return 0;
+}
+
+int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
+{
+    if (!t)
+        return -1;
+    tp_dev_cfg_t *c = &t->cfg;
+    char args[4096] = "";
+    for (int i = 0; i < argc; i++) {
+        const char *a = argv[i], *eq = strchr(a, '=');
+        const char *v = eq ? eq + 1 : NULL;
+        size_t nl = eq ? (size_t)(eq - a) : strlen(a);
+#define OPT(n) (nl == sizeof(n) - 1 && !strncmp(a, n, nl))
+#define NEED_ARG()                                                   \
+    do {                                                             \
+        if (!v)                                                      \
+            return tp_err(t, "option %.*s needs a value", (int)nl, a); \
+    } while (0)
+        int rc = 0;
+        if (OPT("--cidr")) {
+            NEED_ARG();
+            c->mode = TP_MODE_CIDR;
+            rc = cidr_list(t, v, c->cidr, &c->ncidr, "--cidr");
+        } else if (OPT("--mac")) {
+            NEED_ARG();
+            c->mode = TP_MODE_MAC;
+            /* macinstring (mac.c:76-115) re-parses the list per packet: resolve it once */
+            char buf[4096], *tok = NULL;
+            snprintf(buf, sizeof buf, "%s", v);
+            uint8_t cur[6] = {0};
+            char *s = strtok_r(buf, ",", &tok);
+            c->nmac = 0;
+            c->mac_first_empty = s == NULL || !*s;
+            for (; s && !c->mac_first_empty; s = strtok_r(NULL, ",", &tok)) {
+                if (c->nmac >= TP_MAXC)
+                    return tp_err(t, "--mac: more than %d addresses", TP_MAXC);
+                mac2hex(s, cur);
+                memcpy(c->mac[c->nmac++], cur, 6);
+            }
+        } else if (OPT("--port")) {
+            c->mode = TP_MODE_PORT;
+        } else if (OPT("--reverse")) {
+            c->reverse = 1;
+        } else if (OPT("--nonip")) {
+            c->nonip = 1; /* DIR_SERVER, tcpprep_opts.def:498 */
+        } else if (OPT("--no-arg-comment")) {
+            t->nocomment = 1;
+        } else if (OPT("--comment")) {
+            NEED_ARG();
+            snprintf(t->comment, sizeof t->comment, "%s", v);
+            t->has_comment = 1;
+        } else if (OPT("--include") || OPT("--exclude")) {
+            NEED_ARG();
+            rc = include_exclude(t, v, OPT("--exclude"));
+        } else if (OPT("--auto") || OPT("--regex") || OPT("--services")) {
+            return tp_err(t, "%.*s is not served by the GPU classifier (per-packet modes only)", (int)nl, a);
+        } else {
+            return tp_err(t, "unknown option %s", a);
+        }
+        if (rc < 0)
+            return -1;
+        if (!OPT("--comment")) { /* the arg comment leaves out the -C comment (tcpprep_api.c:163-168) */
+            strncat(args, a, sizeof args - strlen(args) - 2);
+            strcat(args, " ");
+        }
+#undef OPT
+#undef NEED_ARG
+    }
+    if (!c->mode)
+        return tp_err(t, "one of --cidr, --mac, --port is required");
+    /* tcpprep_post_args (tcpprep_api.c:160-197): "args\ncomment" */
+    char full[sizeof t->comment] = "";
+    if (!t->nocomment && args[0]) {
+        args[strlen(args) - 1] = 0;
+        snprintf(full, sizeof full, "%s", args);
+    }
+    if (t->has_comment) {
+        size_t l = strlen(full);
+        snprintf(full + l, sizeof full - l, "\n%s", t->comment);
+    }
+    memcpy(t->comment, full, sizeof full);
+    if (strlen(t->comment) > 65535)
+        return tp_err(t, "comment longer than 65535 bytes");
+    return 0;
+}
+
+size_t tcpprep_cache_bound(tcpprep_hip_t *t, size_t pcap_len)
+{
+    return 24 + (t ? strlen(t->comment) : 0) + (pcap_len / 16) / 4 + 1;
+}
+
+static uint32_t rd32(const uint8_t *p, int sw)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return sw ? __builtin_bswap32(v) : v;
+}
+
+/* check_list (list.c:139-156) */
+static int check_list(const tp_dev_cfg_t *c, uint64_t v)
+{
+    for (int i = 0; i < c->nlist; i++) {
+        uint64_t mn = c->lmin[i], mx = c->lmax[i];
+        if (mn != 0 && mx != 0) {
+            if (v >= mn && v <= mx)
+                return 1;
+        } else if (mn == 0) {
+            if (v <= mx)
+                return 1;
+        } else if (v >= mn) {
+            return 1;
+        }
+    }
+    return 0;
+}
+
+typedef struct {
+    uint64_t *off;
+    uint32_t *caplen, *pktnum;
+    uint64_t n, records;
+} tp_index_t;
+
+/* the record walk: libpcap's pcap_next stops at an oversize or truncated record.
+   MAC mode leaves records shorter than an Ethernet header out of the cache
+   (tcpprep.c:465-468 `break`s before add_cache), so they get no entry -- unless
+   the include/exclude packet list, checked first (:362-375), gives them DONT_SEND. */
+static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index_t *x)
+{
+    memset(x, 0, sizeof(*x));
+    if (len < 24)
+        return tp_err(t, "pcap image too short");
+    uint32_t magic;
+    memcpy(&magic, img, 4);
+    int sw;
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du)
+        sw = 0;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u)
+        sw = 1;
+    else
+        return tp_err(t, "not a pcap file (magic 0x%08x)", magic);
+    uint32_t linktype = rd32(img + 20, sw) & 0x03ffffffu;
+    if (linktype != 1)
+        return tp_err(t, "the GPU classifier reads DLT_EN10MB captures only (linktype %u)", linktype);
+    uint64_t cap = len / 16 + 1;
+    x->off = malloc(cap * sizeof(uint64_t));
+    x->caplen = malloc(cap * sizeof(uint32_t));
+    if (!x->off || !x->caplen)
+        return tp_err(t, "out of memory");
+    int mac = t->cfg.mode == TP_MODE_MAC, gaps = 0;
+    for (size_t off = 24; off + 16 <= len;) {
+        uint32_t caplen = rd32(img + off + 8, sw);
+        if (caplen > 262144u || off + 16 + caplen > len)
+            break;
+        x->records++;
+        const tp_dev_cfg_t *c = &t->cfg;
+        int listed_out = c->nlist && check_list(c, x->records) == ((c->xx_mode & TP_XX_EXCLUDE) != 0);
+        if (mac && caplen < 14 && !listed_out) {
+            if (!gaps) { /* record numbers diverge from entry numbers from here on */
+                x->pktnum = malloc(cap * sizeof(uint32_t));
+                if (!x->pktnum)
+                    return tp_err(t, "out of memory");
+                for (uint64_t j = 0; j < x->n; j++)
+                    x->pktnum[j] = (uint32_t)(j + 1);
+                gaps = 1;
+            }
+        } else {
+            x->off[x->n] = off + 16;
+            x->caplen[x->n] = caplen;
+            if (gaps)
+                x->pktnum[x->n] = (uint32_t)x->records;
+            x->n++;
+        }
+        off += 16 + caplen;
+    }
+    if (x->records > 0xffffffffull)
+        return tp_err(t, "more than 2^32 records");
+    return 0;
+}
+
+static void index_free(tp_index_t *x)
+{
+    free(x->off);
+    free(x->caplen);
+    free(x->pktnum);
+}
+
+typedef struct {
+    uint8_t *img, *out;
+    uint64_t *off;
+    uint32_t *caplen, *pktnum;
+    tp_dev_cfg_t *cfg;
+} tp_dev_t;
+
+static void dev_free(tp_dev_t *d)
+{
+    hipFree(d->img);
+    hipFree(d->out);
+    hipFree(d->off);
+    hipFree(d->caplen);
+    hipFree(d->pktnum);
+    hipFree(d->cfg);
+}
+
+static int stage(tcpprep_hip_t *t, const void *pcap, size_t len, const tp_index_t *x, tp_dev_t *d)
+{
+    memset(d, 0, sizeof(*d));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return tp_err(t, "no HIP device available: the tcpprep classifier runs on the GPU only");
+    uint64_t n = x->n ? x->n : 1;
+    if (hipMalloc((void **)&d->img, len) != hipSuccess || hipMalloc((void **)&d->out, (n + 3) / 4) != hipSuccess ||
+        hipMalloc((void **)&d->off, n * 8) != hipSuccess || hipMalloc((void **)&d->caplen, n * 4) != hipSuccess ||
+        hipMalloc((void **)&d->cfg, sizeof(tp_dev_cfg_t)) != hipSuccess ||
+        (x->pktnum && hipMalloc((void **)&d->pktnum, n * 4) != hipSuccess)) {
+        dev_free(d);
+        return tp_err(t, "device allocation failed");
+    }
+    if (hipMemcpy(d->img, pcap, len, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d->off, x->off, x->n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d->caplen, x->caplen, x->n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d->cfg, &t->cfg, sizeof(tp_dev_cfg_t), hipMemcpyHostToDevice) != hipSuccess ||
+        (x->pktnum && hipMemcpy(d->pktnum, x->pktnum, x->n * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+        dev_free(d);
+        return tp_err(t, "host-to-device copy failed");
+    }
+    return 0;
+}
+
+int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void *outv, size_t out_cap)
+{
+    if (!t || !pcap || !outv)
+        return -1;
+    tp_index_t x;
+    if (index_pcap(t, pcap, len, &x) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    if (x.records == 0) { /* tcpprep.c:151-155 */
+        index_free(&x);
+        return tp_err(t, "No packets were processed.  Filter too limiting?");
+    }
+    size_t clen = strlen(t->comment), hdr = 24 + clen, body = (x.n + 3) / 4;
+    if (out_cap < hdr + body) {
+        index_free(&x);
+        return tp_err(t, "cache buffer too small (%zu < %zu)", out_cap, hdr + body);
+    }
+    tp_dev_t d;
+    if (stage(t, pcap, len, &x, &d) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    uint8_t *out = outv;
+    int rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL);
+    if (rc == 0 && body && hipMemcpy(out + hdr, d.out, body, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = -1;
+    if (rc == 0 && hipDeviceSynchronize() != hipSuccess)
+        rc = -1;
+    dev_free(&d);
+    if (rc < 0) {
+        index_free(&x);
+        return tp_err(t, "classification kernel failed");
+    }
+    /* tcpr_cache_file_hdr_t (cache.h:63-72), big-endian counts */
+    memcpy(out, "tcpprep\0", 8);
+    memcpy(out + 8, "04\0\0", 4);
+    for (int i = 0; i < 8; i++)
+        out[12 + i] = (uint8_t)(x.records >> (56 - 8 * i));
+    out[20] = 0;
+    out[21] = 4; /* CACHE_PACKETS_PER_BYTE */
+    out[22] = (uint8_t)(clen >> 8);
+    out[23] = (uint8_t)clen;
+    memcpy(out + 24, t->comment, clen);
+    index_free(&x);
+    return (int64_t)(hdr + body);
+}
+
+int tcpprep_time(tcpprep_hip_t *t, const void *pcap, size_t len, int iters, double *ms_kernel, uint64_t *entries)
+{
+    if (!t || !pcap || iters <= 0)
+        return -1;
+    tp_index_t x;
+    if (index_pcap(t, pcap, len, &x) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    tp_dev_t d;
+    if (stage(t, pcap, len, &x, &d) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    int rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL); /* warm-up */
+    hipEventRecord(e0, NULL);
+    for (int i = 0; i < iters && rc == 0; i++)
+        rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL);
+    hipEventRecord(e1, NULL);
+    float ms = 0;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+        rc = -1;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    dev_free(&d);
+    if (ms_kernel)
+        *ms_kernel = ms / iters;
+    if (entries)
+        *entries = x.n;
+    index_free(&x);
+    return rc < 0 ? tp_err(t, "classification kernel failed") : 0;
+}

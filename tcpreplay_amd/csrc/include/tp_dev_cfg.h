@@ -1,0 +1,38 @@
+/*
+ * tp_dev_cfg.h -- tcpprep's per-packet classification options as the gfx950
+ * kernel reads them (tcpprep_opt_t, src/tcpprep_opts.h, reduced to the
+ * per-packet modes).  Shared by the C host (tp_api.c) and the kernel.
+ */
+#ifndef TP_DEV_CFG_H
+#define TP_DEV_CFG_H
+#include <stdint.h>
+#include "te_dev_cfg.h"
+
+#define TP_MAXC 64
+
+enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3 };
+/* xX.h:34-41 */
+enum { TP_XX_SOURCE = 1, TP_XX_DEST = 2, TP_XX_BOTH = 4, TP_XX_EITHER = 8, TP_XX_PACKET = 16, TP_XX_EXCLUDE = 128 };
+
+typedef struct {
+    int32_t mode, reverse, nonip, mac_first_empty;
+    int32_t ncidr, nmac, xx_mode, nxx_cidr;
+    int32_t nlist, pad_;
+    te_cidr_t cidr[TP_MAXC];     /* -c list (check_ip_cidr: empty list matches all) */
+    te_cidr_t xx_cidr[TP_MAXC];  /* -x/-X S:/D:/B:/E: list */
+    uint8_t mac[TP_MAXC][8];     /* -e list, as macinstring's mac2hex leaves each token */
+    uint64_t lmin[TP_MAXC], lmax[TP_MAXC]; /* -x/-X P: list */
+    uint32_t svc_tcp[2048], svc_udp[2048]; /* services bitmaps (tcpprep_api.c:50-53: ports 0-1023) */
+} tp_dev_cfg_t;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* classify n_entries records (data at img + off[j], caplen[j], record number
+   pktnum[j] or j + 1) into packed 2-bit cache entries out[(n + 3) / 4] */
+int tp_launch_classify(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, const uint32_t *pktnum,
+                       uint64_t n_entries, const tp_dev_cfg_t *cfg, uint8_t *out, void *stream);
+#ifdef __cplusplus
+}
+#endif
+#endif

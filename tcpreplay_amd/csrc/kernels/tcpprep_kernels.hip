@@ -1,0 +1,162 @@
+// tcpprep_kernels.hip -- gfx950 kernel for tcpprep's per-packet classification
+// pass (src/tcpprep.c:339-587 process_raw_packets, per-packet modes).
+//
+// One lane per cache entry (one pcap record).  A lane locates the record's
+// IPv4/IPv6 header with the same L2 chain walk the edit kernels use
+// (edit_pkt.hpp: get_l2len_protocol, l4_v4, l4_v6, l4proto_v6, ip_in_cidr),
+// applies the include/exclude filter and the mode's test, and yields the 2-bit
+// cache entry add_cache (src/common/cache.c:259-314) would store: bit 1 = send,
+// bit 0 = C2S.  Four neighbouring lanes OR their entries into one byte with two
+// cross-lane shuffles, and the first of them stores it: the output is the
+// packed cache body that write_cache (cache.c:146-219) writes after the header.
+//
+// Bytes per record: the 12-byte index entry, the L2..L4 header bytes the tests
+// touch (<= 64 for untagged frames) and a quarter byte of output.  The pass is
+// a gather over the capture at record stride, so it is bound by HBM latency
+// and the record count, not by the capture's size.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "edit_pkt.hpp"
+#include "tp_dev_cfg.h"
+
+namespace {
+using namespace te;
+
+DI bool in4(const te_cidr_t *c, int n, u32 ip) {  // check_ip_cidr cidr.c:535-564
+    if (n == 0) return true;
+    for (int i = 0; i < n; ++i)
+        if (ip_in_cidr(c[i], ip)) return true;
+    return false;
+}
+
+DI bool in6(const te_cidr_t *c, int n, const u8 *a) {  // check_ip6_cidr cidr.c:570-598
+    if (n == 0) return true;
+    for (int i = 0; i < n; ++i)
+        if (ip6_in_cidr(c[i], a)) return true;
+    return false;
+}
+
+DI bool check_list(const tp_dev_cfg_t &c, uint64_t v) {  // list.c:139-156
+    for (int i = 0; i < c.nlist; ++i) {
+        uint64_t mn = c.lmin[i], mx = c.lmax[i];
+        if (mn != 0 && mx != 0) {
+            if (v >= mn && v <= mx) return true;
+        } else if (mn == 0) {
+            if (v <= mx) return true;
+        } else if (v >= mn) {
+            return true;
+        }
+    }
+    return false;
+}
+
+// process_xX_by_cidr_ipv4/ipv6 (xX.c:124-236): true = SEND
+DI bool xx_cidr(const tp_dev_cfg_t &c, const u8 *ip, bool v6) {
+    bool s, d;
+    if (v6) {
+        s = in6(c.xx_cidr, c.nxx_cidr, ip + 8);
+        d = in6(c.xx_cidr, c.nxx_cidr, ip + 24);
+    } else {
+        s = in4(c.xx_cidr, c.nxx_cidr, ld32(ip + 12));
+        d = in4(c.xx_cidr, c.nxx_cidr, ld32(ip + 16));
+    }
+    const bool ex = (c.xx_mode & TP_XX_EXCLUDE) != 0;
+    bool hit;
+    switch (c.xx_mode & ~TP_XX_EXCLUDE) {
+        case TP_XX_SOURCE: hit = s; break;
+        case TP_XX_DEST: hit = d; break;
+        case TP_XX_BOTH: hit = d && s; break;
+        case TP_XX_EITHER: hit = d || s; break;
+        default: return !ex;  // "Unable to determine action in CIDR filter mode"
+    }
+    return ex ? !hit : hit;
+}
+
+DI bool svc(const uint32_t *bits, u32 port) { return (bits[port >> 5] >> (port & 31)) & 1u; }
+
+// check_dst_port (tcpprep.c:211-295): 1 = C2S, 0 = S2C, or --nonip's value
+DI int dst_port(const tp_dev_cfg_t &c, const u8 *ip, bool v6, int len) {
+    int l4;
+    u8 proto;
+    if (!v6) {
+        if (len < ((ip[0] & 0x0f) * 4) + 4) return 0;
+        proto = ip[9];
+        l4 = l4_v4(ip, len);
+    } else {
+        if (len < 40 + 4) return 0;
+        proto = l4proto_v6(ip, len);
+        l4 = l4_v6(ip, 0, len);
+    }
+    if (l4 < 0) return 0;
+    if (proto == 6) {
+        if (len - l4 < 20) return 0;
+        return svc(c.svc_tcp, be16(ip + l4 + 2)) ? 1 : 0;
+    }
+    if (proto == 17) {
+        if (len - l4 < 8) return 0;
+        return svc(c.svc_udp, be16(ip + l4 + 2)) ? 1 : 0;
+    }
+    return c.nonip;
+}
+
+// one record -> its 2-bit cache entry
+DI u32 classify(const tp_dev_cfg_t &c, const u8 *pkt, u32 caplen, uint64_t pktnum) {
+    constexpr u32 SEND = 2, C2S = 1;
+    // include/exclude packet list (tcpprep.c:362-375)
+    if (c.nlist && check_list(c, pktnum) == ((c.xx_mode & TP_XX_EXCLUDE) != 0)) return 0;
+    int dir;
+    if (c.mode != TP_MODE_MAC) {
+        L2 r;
+        const int res = caplen ? get_l2len_protocol(pkt, caplen, r) : -1;
+        const bool v4 = res != -1 && r.l2len + 20 <= caplen && r.protocol == 0x0800;  // get_ipv4 get.c:483-541
+        const bool v6 = !v4 && res != -1 && r.l2len + 40 <= caplen && r.protocol == 0x86DD;  // get_ipv6 :550-608
+        if (!v4 && !v6) return SEND | (c.nonip == 1 ? C2S : 0);  // add_cache(SEND, options->nonip)
+        const u8 *ip = pkt + r.l2len;
+        if (c.nxx_cidr && c.xx_mode && !xx_cidr(c, ip, v6)) return 0;
+        if (c.mode == TP_MODE_CIDR) {
+            dir = v6 ? in6(c.cidr, c.ncidr, ip + 8) : in4(c.cidr, c.ncidr, ld32(ip + 12));
+            if (c.reverse) dir = !dir;
+        } else {
+            dir = dst_port(c, ip, v6, (int)caplen - (int)r.l2len);
+        }
+    } else {  // macinstring (mac.c:76-115) on the source MAC; caplen < 14 records are not indexed
+        dir = 0;
+        if (!c.mac_first_empty)
+            for (int m = 0; m < c.nmac; ++m) {
+                const u8 *a = c.mac[m];
+                bool eq = true;
+                for (int b = 0; b < 6; ++b) eq &= pkt[6 + b] == a[b];
+                if (eq) {
+                    dir = 1;
+                    break;
+                }
+            }
+        if (c.reverse) dir = !dir;
+    }
+    return SEND | (dir == 1 ? C2S : 0);
+}
+
+__global__ __launch_bounds__(256) void tp_classify(const u8 *__restrict__ img, const uint64_t *__restrict__ off,
+                                                   const uint32_t *__restrict__ caplen,
+                                                   const uint32_t *__restrict__ pktnum, uint64_t n,
+                                                   const tp_dev_cfg_t *__restrict__ cfg, u8 *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    u32 e = 0;
+    if (j < n) e = classify(*cfg, img + off[j], caplen[j], pktnum ? (uint64_t)pktnum[j] : j + 1);
+    e <<= 2 * (j & 3);
+    e |= __shfl_xor(e, 1);
+    e |= __shfl_xor(e, 2);
+    if ((j & 3) == 0 && j < n) out[j >> 2] = (u8)e;
+}
+}  // namespace
+
+extern "C" int tp_launch_classify(const uint8_t *img, const uint64_t *off, const uint32_t *caplen,
+                                  const uint32_t *pktnum, uint64_t n_entries, const tp_dev_cfg_t *cfg, uint8_t *out,
+                                  void *stream) {
+    if (n_entries == 0) return 0;
+    const uint64_t blocks = (n_entries + 255) / 256;
+    if (blocks > 0x7fffffffull) return -1;
+    hipLaunchKernelGGL(tp_classify, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, off, caplen, pktnum,
+                       n_entries, cfg, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

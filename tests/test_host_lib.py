@@ -17,10 +17,10 @@ from cfg_struct import DevCfg
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "tcpedit.h")).read()
+def header_functions(header="tcpedit.h", prefix="tcpedit_"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(tcpedit_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(" + prefix + r"[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol(built):
@@ -29,6 +29,13 @@ def test_library_exports_every_declared_symbol(built):
     assert len(names) >= 40
     missing = [n for n in names if not hasattr(L, n)]
     assert missing == []
+
+
+def test_library_exports_every_tcpprep_symbol(built):
+    L = ctypes.CDLL(TA.LIB_PATH)
+    names = header_functions("tcpprep.h", "tcpprep_")
+    assert len(names) == 7
+    assert [n for n in names if not hasattr(L, n)] == []
 
 
 def derive(args):
