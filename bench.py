@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
-    ap.add_argument("--extra", default="c3,c4,c5,c2x10,fz",
+    ap.add_argument("--extra", default="c3,c4,c5,c2x10,fz,prep",
                     help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
                     "half --cpu-threads threads)")
@@ -234,6 +234,20 @@ def main():
     if rank == 0 and world == 1:
         extra = {}
         for wl in [w for w in opt.extra.split(",") if w]:
+            if wl == "prep":
+                # tcpprep --port classification on C3's IMIX corpus:
+                # tp_classify kernel, image and index resident in HBM; algorithmic bytes per
+                # record = 12 (index) + 38 (Ethernet + IPv4 + L4 ports read) + 1/4 (cache entry)
+                from tcpreplay_amd import tcpprep as TP
+                n2 = 10_000_000
+                tp = TP.TcpPrep(["--no-arg-comment", "--port"])
+                kms2, ent = tp.time(make_pcap("c3", n2, 11), iters=max(5, opt.steps // 20))
+                tp.close()
+                extra[wl] = {"workload": "tcpprep --port on IMIX 64/570/1514 7:4:1 (C3 corpus): v04 cache "
+                                         "entries for every record", "packets": ent, "kernel_ms": round(kms2, 4),
+                             "mpkt_s": round(ent / (kms2 * 1e-3) / 1e6, 1),
+                             "gbps_algorithmic": round(ent * 50.25 / (kms2 * 1e-3) / 1e9, 1)}
+                continue
             n2 = DEFAULT_PACKETS[wl]
             te2, b2, r2, _ = run_workload(wl, n2, 0, 3, seed=11, device=0)
             ms2 = b2.time(max(5, opt.steps // 50))
