@@ -6,13 +6,16 @@
  * per-packet modes -- CIDR (-c), MAC (-e), port (-p) -- with --reverse,
  * --nonip, --comment/--no-arg-comment and the include/exclude filters
  * (-x/-X P:list, S:/D:/B:/E: CIDR), and the cache file writer
- * (src/common/cache.c:146-219 write_cache, :259-314 add_cache).  The auto
- * (tree) modes and regex mode are not restated (out of scope).
+ * (src/common/cache.c:146-219 write_cache, :259-314 add_cache), and the auto
+ * modes bridge/client/server/first (tree.c:219-565, packet2tree :653-838)
+ * with --ratio.  Router mode (process_tree's CIDR build) and regex mode are
+ * not restated (out of scope).
  *
  * Pinning: checked byte-for-byte against the reference's own cache files
  * (test/test.cidr, .cidr_reverse, .mac, .mac_reverse, .port, .comment,
  * .include_packets, .exclude_packets, .include_source, .include_dest, made by
- * test/Makefile.am:93-104 from test/test.pcap), committed under tests/golden/,
+ * and test.auto_{bridge,client,server,first}; test/Makefile.am:87-104, from
+ * test/test.pcap), committed under tests/golden/,
  * by tests/test_tcpprep.py.
  *
  * It is compiled into the same oracle/_build/liboracle.so as the tcpedit
@@ -24,12 +27,15 @@
 
 #define TPO_MAXC 64
 
-enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3 };
+enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3, TPO_AUTO = 4 };
+/* automode: defines.h.in:207 direction_e and tcpprep's BRIDGE/CLIENT/SERVER/FIRST modes */
+enum { TPA_BRIDGE = 1, TPA_CLIENT, TPA_SERVER, TPA_FIRST };
 /* xX.h:34-41 */
 enum { XX_SOURCE = 1, XX_DEST = 2, XX_BOTH = 4, XX_EITHER = 8, XX_PACKET = 16, XX_EXCLUDE = 128 };
 
 typedef struct {
-    int mode, reverse, nonip, nocomment;
+    int mode, reverse, nonip, nocomment, automode;
+    double ratio;
     ocidr_t cidr[TPO_MAXC];
     int ncidr;
     uint8_t mac[TPO_MAXC][6];
@@ -150,6 +156,7 @@ static int tpo_xx(tpo_opt_t *o, const char *arg, int exclude)
 static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
 {
     memset(o, 0, sizeof(*o));
+    o->ratio = 2.0; /* --ratio default, tcpprep_opts.def:511-516 */
     for (int i = 0; i <= 1023; i++) /* tcpprep_init, tcpprep_api.c:50-53 */
         o->svc_tcp[i] = o->svc_udp[i] = 1;
     char args[4096] = "";
@@ -184,6 +191,23 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
             }
         } else if (IS("--port")) {
             o->mode = TPO_PORT;
+        } else if (IS("--auto")) {
+            o->mode = TPO_AUTO;
+            if (!strcmp(v, "bridge"))
+                o->automode = TPA_BRIDGE;
+            else if (!strcmp(v, "client"))
+                o->automode = TPA_CLIENT;
+            else if (!strcmp(v, "server"))
+                o->automode = TPA_SERVER;
+            else if (!strcmp(v, "first"))
+                o->automode = TPA_FIRST;
+            else
+                return -1; /* router: process_tree's CIDR build is not restated */
+        } else if (IS("--ratio")) {
+            char *end;
+            o->ratio = strtod(v, &end);
+            if (o->ratio < 0)
+                return -1;
         } else if (IS("--reverse")) {
             o->reverse = 1;
         } else if (IS("--nonip")) {
@@ -207,6 +231,8 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
     }
     if (!o->mode)
         return -1;
+    if (o->mode == TPO_AUTO && o->xx_mode)
+        return -1; /* the first pass would add_cache() the filtered packets a second time */
     /* tcpprep_post_args, tcpprep_api.c:160-197: "args\ncomment" */
     char full[8192] = "";
     if (!o->nocomment && args[0]) {
@@ -323,6 +349,185 @@ static uint32_t tpo_rd32(const uint8_t *p, int sw)
     return sw ? __builtin_bswap32(v) : v;
 }
 
+
+/* ---- auto modes: tree.c's host table (RB tree there, open addressing here) ---- */
+typedef struct {
+    int used, family;
+    uint8_t addr[16];
+    uint32_t server_cnt, client_cnt;
+    int type; /* direction_e: -1 unknown, 0 client, 1 server */
+} tpo_node_t;
+
+static tpo_node_t *tpo_nodes;
+static size_t tpo_cap;
+
+static tpo_node_t *tpo_find(int family, const uint8_t *addr, int insert, int *inserted)
+{
+    /* tree_comp (tree.c:590-626) calls ipv6_cmp(&t1->u.ip6, &t1->u.ip6): every IPv6
+       address compares equal, so all IPv6 hosts share the first IPv6 node */
+    static const uint8_t v6_any[16];
+    if (family == 6)
+        addr = v6_any;
+    int n = family == 4 ? 4 : 16;
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)family;
+    for (int i = 0; i < n; i++)
+        h = (h ^ addr[i]) * 1099511628211ull;
+    for (size_t k = 0; k < tpo_cap; k++) {
+        tpo_node_t *e = &tpo_nodes[(h + k) & (tpo_cap - 1)];
+        if (!e->used) {
+            if (!insert)
+                return NULL;
+            memset(e, 0, sizeof(*e));
+            e->used = 1;
+            e->family = family;
+            memcpy(e->addr, addr, n);
+            e->type = -1; /* new_tree(), tree.c:631-644 */
+            *inserted = 1;
+            return e;
+        }
+        if (e->family == family && !memcmp(e->addr, addr, n))
+            return e;
+    }
+    return NULL;
+}
+
+/* packet2tree (tree.c:653-838): the node type a packet gives its source; -2 = len_error */
+static int tpo_packet2tree(const uint8_t *d, uint32_t caplen)
+{
+    uint16_t et = 0;
+    uint32_t l2len = 0, l2off = 0, voff = 0;
+    if (get_l2len_protocol(d, caplen, &et, &l2len, &l2off, &voff) == -1)
+        return -2;
+    long len = caplen, hl = 0;
+    uint8_t proto = 0;
+    if (et == 0x0800) {
+        if (len < (long)l2len + 20)
+            return -2;
+        proto = d[l2len + 9];
+        hl = (d[l2len] & 0x0f) * 4;
+    } else if (et == 0x86DD) {
+        if (len < (long)l2len + 40)
+            return -2;
+        proto = d[l2len + 6];
+        hl = 40;
+    }
+    const uint8_t *l4 = d + l2len + hl;
+    if (proto == 6) {
+        if (len < (long)l2len + 20 + hl)
+            return -2;
+        uint16_t sport;
+        memcpy(&sport, l4, 2);
+        if (sport == 20) /* th_sport compared without ntohs */
+            return -1;
+        if (l4[13] == 0x02)
+            return 0; /* SYN: client */
+        if (l4[13] == 0x12)
+            return 1; /* SYN|ACK: server */
+        return -1;
+    }
+    if (proto == 17) {
+        if (len < (long)l2len + 8 + hl)
+            return -2;
+        uint16_t flags;
+        if (((l4[2] << 8) | l4[3]) == 53) {
+            if (len < (long)l2len + 8 + 12 + hl)
+                return -2;
+            memcpy(&flags, l4 + 8 + 2, 2); /* dnsv4_hdr.flags, host order of network bytes */
+            return (flags & 0x8000) ? 1 : 0;
+        }
+        if (((l4[0] << 8) | l4[1]) == 53) {
+            if (len < (long)l2len + 8 + 12 + hl)
+                return -2;
+            memcpy(&flags, l4 + 8 + 2, 2);
+            return ((flags & 0x7FFFF) ^ 0x8000) ? 1 : 0;
+        }
+        return -1;
+    }
+    if (proto == 1) {
+        if (len < (long)l2len + 4 + hl)
+            return -2;
+        if (l4[0] == 3 && l4[1] == 3)
+            return 1; /* port unreachable: source is the server */
+    }
+    return -1;
+}
+
+/* the first pass of auto mode (tcpprep.c:480-496, tree.c:333-538) and tree_calculate
+   (tree.c:540-565); returns 0, or -4 on the reference's errx() paths */
+static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, int sw, uint64_t records)
+{
+    tpo_cap = 16;
+    while (tpo_cap < 4 * records + 16)
+        tpo_cap <<= 1;
+    free(tpo_nodes);
+    tpo_nodes = calloc(tpo_cap, sizeof(tpo_node_t));
+    if (!tpo_nodes)
+        return -4;
+    for (size_t off = 24; off + 16 <= len;) {
+        uint32_t caplen = tpo_rd32(pcap + off + 8, sw);
+        if (caplen > 262144u || off + 16 + caplen > len)
+            break;
+        const uint8_t *d = pcap + off + 16;
+        off += 16 + caplen;
+        uint16_t proto = 0;
+        uint32_t l2len = 0, l2off = 0, voff = 0;
+        int res = caplen ? get_l2len_protocol(d, caplen, &proto, &l2len, &l2off, &voff) : -1;
+        int v4 = res != -1 && l2len + 20 <= caplen && proto == 0x0800;
+        int v6 = !v4 && res != -1 && l2len + 40 <= caplen && proto == 0x86DD;
+        if (!v4 && !v6)
+            continue;
+        int fam = v4 ? 4 : 6, ins = 0;
+        const uint8_t *src = d + l2len + (v4 ? 12 : 8), *dst = d + l2len + (v4 ? 16 : 24);
+        if (o->automode == TPA_FIRST) { /* add_tree_first_ipv4/ipv6: first sighting wins */
+            tpo_node_t *e = tpo_find(fam, src, 1, &ins);
+            if (ins) {
+                e->type = 0;
+                e->client_cnt = 1000;
+            }
+            ins = 0;
+            e = tpo_find(fam, dst, 1, &ins);
+            if (ins) {
+                e->type = 1;
+                e->server_cnt = 1000;
+            }
+        } else { /* add_tree_ipv4/ipv6 + add_tree_node */
+            int t = tpo_packet2tree(d, caplen);
+            if (t == -2)
+                return -4; /* "packet capture length %d too small to process" */
+            tpo_node_t *e = tpo_find(fam, src, 1, &ins);
+            if (t == 1)
+                e->server_cnt++;
+            else if (t == 0)
+                e->client_cnt++;
+        }
+    }
+    for (size_t i = 0; i < tpo_cap; i++) { /* tree_calculate */
+        tpo_node_t *e = &tpo_nodes[i];
+        if (!e->used)
+            continue;
+        if (e->server_cnt > 0 || e->client_cnt > 0)
+            e->type = (double)e->server_cnt >= (double)e->client_cnt * o->ratio ? 1 : 0;
+        else
+            e->type = -1;
+    }
+    return 0;
+}
+
+/* check_ip_tree / check_ip6_tree (tree.c:219-331): tcpr_dir_t; -4 = unknown system */
+static int tpo_check_tree(const tpo_opt_t *o, int fam, const uint8_t *src)
+{
+    int ins = 0;
+    tpo_node_t *e = tpo_find(fam, src, 0, &ins);
+    int mode = o->automode == TPA_SERVER ? 1 : o->automode == TPA_CLIENT ? 0 : -1;
+    if (!e && mode == -1)
+        return -4;
+    if (e && e->type == 1)
+        return 2; /* TCPR_DIR_S2C */
+    if (e && e->type == 0)
+        return 1; /* TCPR_DIR_C2S */
+    return mode == 1 ? 2 : mode == 0 ? 1 : -1;
+}
+
 /*
  * tcpprep_oracle_run: classify a whole pcap image and write the cache file
  * (header + comment + packed 2-bit entries) into `out`.  Returns the cache
@@ -349,6 +554,18 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
     if (cap < hdr)
         return -3;
     memset(out, 0, cap);
+    if (o.mode == TPO_AUTO) {
+        uint64_t recs = 0;
+        for (size_t off = 24; off + 16 <= len;) {
+            uint32_t cl = tpo_rd32(pcap + off + 8, sw);
+            if (cl > 262144u || off + 16 + cl > len)
+                break;
+            recs++;
+            off += 16 + cl;
+        }
+        if (tpo_tree_pass(&o, pcap, len, sw, recs) < 0)
+            return -4;
+    }
     uint64_t packetnum = 0, entries = 0;
     static uint8_t pkt[MAXPACKET + 64];
     for (size_t off = 24; off + 16 <= len;) {
@@ -379,7 +596,12 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
                 send = 0;
                 goto ADD;
             }
-            if (o.mode == TPO_CIDR) {
+            if (o.mode == TPO_AUTO) { /* the second pass: ROUTER/BRIDGE/SERVER/CLIENT/FIRST_MODE cases */
+                int r = tpo_check_tree(&o, v6 ? 6 : 4, ip + (v6 ? 8 : 12));
+                if (r == -4)
+                    return -4; /* "is an unknown system... aborting" */
+                dir = r == 1;
+            } else if (o.mode == TPO_CIDR) {
                 uint32_t s4;
                 memcpy(&s4, ip + 12, 4);
                 dir = v6 ? tpo_in6(o.cidr, o.ncidr, ip + 8) : tpo_in4(o.cidr, o.ncidr, s4);

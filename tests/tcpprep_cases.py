@@ -1,4 +1,4 @@
-"""tcpprep golden cases: the argument lines of the reference's test/Makefile.am:93-104
+"""tcpprep golden cases: the argument lines of the reference's test/Makefile.am:87-104
 (tcpprep run with --no-arg-comment on test/test.pcap), in long-option form, and the
 cache files they produced (tests/golden/prep.*, copied from the reference's test/)."""
 import os
@@ -16,6 +16,10 @@ CASES = {
     "include_packets": ["--cidr=96.17.211.0/24", "--include=P:61-65,88-91"],
     "include_source": ["--cidr=96.17.211.0/24", "--include=S:96.0.0.0/8"],
     "include_dest": ["--cidr=96.17.211.0/24", "--include=D:96.0.0.0/8"],
+    "auto_bridge": ["--auto=bridge"],
+    "auto_client": ["--auto=client"],
+    "auto_server": ["--auto=server"],
+    "auto_first": ["--auto=first"],
 }
 
 
