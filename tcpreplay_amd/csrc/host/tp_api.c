@@ -47,6 +47,7 @@ int tcpprep_init(tcpprep_hip_t **out)
         t->cfg.svc_tcp[p >> 5] |= 1u << (p & 31);
         t->cfg.svc_udp[p >> 5] |= 1u << (p & 31);
     }
+    t->cfg.ratio = 2.0; /* --ratio default, tcpprep_opts.def:511-516 */
     *out = t;
     return 0;
 }
@@ -205,7 +206,26 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
         } else if (OPT("--include") || OPT("--exclude")) {
             NEED_ARG();
             rc = include_exclude(t, v, OPT("--exclude"));
-        } else if (OPT("--auto") || OPT("--regex") || OPT("--services")) {
+        } else if (OPT("--auto")) {
+            NEED_ARG();
+            c->mode = TP_MODE_AUTO; /* tcpprep_opts.def:110-130 */
+            if (!strcmp(v, "bridge"))
+                c->automode = TP_AUTO_BRIDGE;
+            else if (!strcmp(v, "client"))
+                c->automode = TP_AUTO_CLIENT;
+            else if (!strcmp(v, "server"))
+                c->automode = TP_AUTO_SERVER;
+            else if (!strcmp(v, "first"))
+                c->automode = TP_AUTO_FIRST;
+            else
+                return tp_err(t, "--auto=%s is not served by the GPU classifier (bridge, client, server, first)", v);
+        } else if (OPT("--ratio")) {
+            NEED_ARG();
+            char *end;
+            c->ratio = strtod(v, &end); /* tcpprep_api.c:210-216 */
+            if (c->ratio < 0)
+                return tp_err(t, "Ratio must be a non-negative number");
+        } else if (OPT("--regex") || OPT("--services")) {
             return tp_err(t, "%.*s is not served by the GPU classifier (per-packet modes only)", (int)nl, a);
         } else {
             return tp_err(t, "unknown option %s", a);
@@ -220,7 +240,10 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
 #undef NEED_ARG
     }
     if (!c->mode)
-        return tp_err(t, "one of --cidr, --mac, --port is required");
+        return tp_err(t, "one of --cidr, --mac, --port, --auto is required");
+    if (c->mode == TP_MODE_AUTO && c->xx_mode)
+        return tp_err(t, "--include/--exclude with --auto are not served (the reference's first pass "
+                         "would add the filtered records to the cache a second time)");
     /* tcpprep_post_args (tcpprep_api.c:160-197): "args\ncomment" */
     char full[sizeof t->comment] = "";
     if (!t->nocomment && args[0]) {
@@ -342,10 +365,20 @@ typedef struct {
     uint64_t *off;
     uint32_t *caplen, *pktnum;
     tp_dev_cfg_t *cfg;
+    tp_tree_t tree;     /* auto modes */
+    tp_tree_t *d_tree;  /* its device copy for the classify kernel */
+    size_t tree_cap;
 } tp_dev_t;
 
 static void dev_free(tp_dev_t *d)
 {
+    hipFree(d->tree.keys);
+    hipFree(d->tree.server_cnt);
+    hipFree(d->tree.client_cnt);
+    hipFree(d->tree.first);
+    hipFree(d->tree.slot);
+    hipFree(d->tree.err);
+    hipFree(d->d_tree);
     hipFree(d->img);
     hipFree(d->out);
     hipFree(d->off);
@@ -376,6 +409,46 @@ static int stage(tcpprep_hip_t *t, const void *pcap, size_t len, const tp_index_
         dev_free(d);
         return tp_err(t, "host-to-device copy failed");
     }
+    if (t->cfg.mode == TP_MODE_AUTO) {
+        size_t cap = 1024;
+        while (cap < 2 * (t->cfg.automode == TP_AUTO_FIRST ? 2 : 1) * n)
+            cap <<= 1;
+        d->tree_cap = cap;
+        d->tree.mask = cap - 1;
+        if (hipMalloc((void **)&d->tree.keys, cap * 8) != hipSuccess ||
+            hipMalloc((void **)&d->tree.server_cnt, cap * 4) != hipSuccess ||
+            hipMalloc((void **)&d->tree.client_cnt, cap * 4) != hipSuccess ||
+            hipMalloc((void **)&d->tree.first, cap * 8) != hipSuccess ||
+            hipMalloc((void **)&d->tree.slot, n * 4) != hipSuccess || hipMalloc((void **)&d->tree.err, 8) != hipSuccess ||
+            hipMalloc((void **)&d->d_tree, sizeof(tp_tree_t)) != hipSuccess ||
+            hipMemcpy(d->d_tree, &d->tree, sizeof(tp_tree_t), hipMemcpyHostToDevice) != hipSuccess) {
+            dev_free(d);
+            return tp_err(t, "device allocation failed (host table)");
+        }
+    }
+    return 0;
+}
+
+/* the auto modes' first pass (tcpprep.c:480-496 + tree_calculate's inputs): reset the
+   table, build it, and report the reference's errx() (packet2tree's len_error) */
+static int tree_pass(tcpprep_hip_t *t, const tp_dev_t *d, const tp_index_t *x, const uint8_t *img, hipStream_t st)
+{
+    size_t cap = d->tree_cap;
+    if (hipMemsetAsync(d->tree.keys, 0, cap * 8, st) != hipSuccess ||
+        hipMemsetAsync(d->tree.server_cnt, 0, cap * 4, st) != hipSuccess ||
+        hipMemsetAsync(d->tree.client_cnt, 0, cap * 4, st) != hipSuccess ||
+        hipMemsetAsync(d->tree.first, 0xff, cap * 8, st) != hipSuccess ||
+        hipMemsetAsync(d->tree.err, 0xff, 8, st) != hipSuccess)
+        return tp_err(t, "device memset failed");
+    if (tp_launch_tree(d->img, d->off, d->caplen, x->n, d->cfg, t->cfg.automode, d->tree, st) != 0)
+        return tp_err(t, "host-table kernel failed");
+    uint64_t err = 0;
+    if (hipMemcpyAsync(&err, d->tree.err, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return tp_err(t, "host-table kernel failed");
+    if (err != ~0ull) /* tree.c:835-837 */
+        return tp_err(t, "packet capture length %u too small to process", x->caplen[err]);
+    (void)img;
     return 0;
 }
 
@@ -403,7 +476,12 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
         return -1;
     }
     uint8_t *out = outv;
-    int rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL);
+    if (t->cfg.mode == TP_MODE_AUTO && tree_pass(t, &d, &x, pcap, NULL) < 0) {
+        dev_free(&d);
+        index_free(&x);
+        return -1;
+    }
+    int rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.d_tree, d.out, NULL);
     if (rc == 0 && body && hipMemcpy(out + hdr, d.out, body, hipMemcpyDeviceToHost) != hipSuccess)
         rc = -1;
     if (rc == 0 && hipDeviceSynchronize() != hipSuccess)
@@ -444,10 +522,22 @@ int tcpprep_time(tcpprep_hip_t *t, const void *pcap, size_t len, int iters, doub
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    int rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL); /* warm-up */
-    hipEventRecord(e0, NULL);
-    for (int i = 0; i < iters && rc == 0; i++)
-        rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.out, NULL);
+    /* one run = (the auto modes' table reset + build +) the classification */
+    int rc = 0;
+    for (int i = 0; i <= iters && rc == 0; i++) {
+        if (i == 1)
+            hipEventRecord(e0, NULL);
+        if (t->cfg.mode == TP_MODE_AUTO) {
+            size_t cap = d.tree_cap;
+            hipMemsetAsync(d.tree.keys, 0, cap * 8, NULL);
+            hipMemsetAsync(d.tree.server_cnt, 0, cap * 4, NULL);
+            hipMemsetAsync(d.tree.client_cnt, 0, cap * 4, NULL);
+            hipMemsetAsync(d.tree.first, 0xff, cap * 8, NULL);
+            rc = tp_launch_tree(d.img, d.off, d.caplen, x.n, d.cfg, t->cfg.automode, d.tree, NULL);
+        }
+        if (rc == 0)
+            rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.d_tree, d.out, NULL);
+    }
     hipEventRecord(e1, NULL);
     float ms = 0;
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess)

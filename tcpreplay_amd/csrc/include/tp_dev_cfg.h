@@ -10,14 +10,17 @@
 
 #define TP_MAXC 64
 
-enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3 };
+enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3, TP_MODE_AUTO = 4 };
+/* the auto modes the GPU serves (tcpprep.c:480-587; router's process_tree is not served) */
+enum { TP_AUTO_BRIDGE = 1, TP_AUTO_CLIENT, TP_AUTO_SERVER, TP_AUTO_FIRST };
 /* xX.h:34-41 */
 enum { TP_XX_SOURCE = 1, TP_XX_DEST = 2, TP_XX_BOTH = 4, TP_XX_EITHER = 8, TP_XX_PACKET = 16, TP_XX_EXCLUDE = 128 };
 
 typedef struct {
     int32_t mode, reverse, nonip, mac_first_empty;
     int32_t ncidr, nmac, xx_mode, nxx_cidr;
-    int32_t nlist, pad_;
+    int32_t nlist, automode;
+    double ratio;                /* --ratio (default 2.0) */
     te_cidr_t cidr[TP_MAXC];     /* -c list (check_ip_cidr: empty list matches all) */
     te_cidr_t xx_cidr[TP_MAXC];  /* -x/-X S:/D:/B:/E: list */
     uint8_t mac[TP_MAXC][8];     /* -e list, as macinstring's mac2hex leaves each token */
@@ -25,13 +28,29 @@ typedef struct {
     uint32_t svc_tcp[2048], svc_udp[2048]; /* services bitmaps (tcpprep_api.c:50-53: ports 0-1023) */
 } tp_dev_cfg_t;
 
+/* the auto modes' host table in HBM (tree.c's RB tree): open addressing on exact
+   64-bit keys -- IPv4: 1<<63 | address; IPv6: one key for every address, as
+   tree_comp compares an IPv6 address with itself (tree.c:618-621) */
+typedef struct {
+    uint64_t *keys;     /* 0 = empty */
+    uint32_t *server_cnt, *client_cnt;
+    uint64_t *first;    /* first mode: min over sightings of 2 * entry + (0 src | 1 dst) */
+    uint32_t *slot;     /* per entry: its source's slot, or ~0 for a non-IP record */
+    uint64_t mask;      /* capacity - 1 (power of two, >= 2x the insertions) */
+    uint64_t *err;      /* min entry index whose packet2tree hit len_error (init ~0) */
+} tp_tree_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* auto modes, first pass: build the host table (tree); then tp_launch_classify */
+int tp_launch_tree(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, uint64_t n_entries,
+                   const tp_dev_cfg_t *cfg, int automode, tp_tree_t tree, void *stream);
 /* classify n_entries records (data at img + off[j], caplen[j], record number
    pktnum[j] or j + 1) into packed 2-bit cache entries out[(n + 3) / 4] */
 int tp_launch_classify(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, const uint32_t *pktnum,
-                       uint64_t n_entries, const tp_dev_cfg_t *cfg, uint8_t *out, void *stream);
+                       uint64_t n_entries, const tp_dev_cfg_t *cfg, const tp_tree_t *tree, uint8_t *out,
+                       void *stream);
 #ifdef __cplusplus
 }
 #endif

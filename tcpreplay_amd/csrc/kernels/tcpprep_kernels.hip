@@ -99,8 +99,131 @@ DI int dst_port(const tp_dev_cfg_t &c, const u8 *ip, bool v6, int len) {
     return c.nonip;
 }
 
+
+// ---------------------------------------------------------------------------
+// Auto modes (tree.c).  First pass: every IP record inserts its source (and in
+// first mode its destination) into an open-addressing table on exact 64-bit
+// keys and bumps the node's counters; the table is the RB tree's set of
+// nodes, and atomics make the order of insertion irrelevant except where the
+// reference is order-dependent (first mode), which an atomicMin over sighting
+// order reproduces.  Second pass (classify): tree_calculate + check_ip_tree
+// per record from its source's slot.
+// ---------------------------------------------------------------------------
+constexpr uint64_t TP_V6_KEY = 1ull << 62;
+
+DI uint64_t node_key(bool v6, const u8 *addr) { return v6 ? TP_V6_KEY : (1ull << 63) | (uint64_t)ld32(addr); }
+
+DI uint32_t tree_insert(const tp_tree_t &t, uint64_t key) {
+    uint64_t h = key * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    for (uint64_t k = 0; k <= t.mask; ++k) {
+        const uint64_t s = (h + k) & t.mask;
+        const uint64_t prev = atomicCAS((unsigned long long *)&t.keys[s], 0ull, (unsigned long long)key);
+        if (prev == 0 || prev == key) return (uint32_t)s;
+    }
+    return 0xffffffffu;  // cannot happen: capacity >= 2x the insertions
+}
+
+// packet2tree (tree.c:653-838): node type for the source, -1 unknown, -2 len_error
+DI int packet2tree(const u8 *d, u32 caplen) {
+    L2 r;
+    if (get_l2len_protocol(d, caplen, r) == -1) return -2;
+    const long len = caplen;
+    long hl = 0;
+    u8 proto = 0;
+    if (r.protocol == 0x0800) {
+        if (len < (long)r.l2len + 20) return -2;
+        proto = d[r.l2len + 9];
+        hl = (d[r.l2len] & 0x0f) * 4;
+    } else if (r.protocol == 0x86DD) {
+        if (len < (long)r.l2len + 40) return -2;
+        proto = d[r.l2len + 6];
+        hl = 40;
+    }
+    const long l4 = (long)r.l2len + hl;
+    if (proto == 6) {
+        if (len < l4 + 20) return -2;
+        if (ld16(d + l4) == 20) return -1;  // th_sport == 20 without ntohs (ftp-data)
+        const u8 fl = d[l4 + 13];
+        return fl == 0x02 ? 0 : fl == 0x12 ? 1 : -1;
+    }
+    if (proto == 17) {
+        if (len < l4 + 8) return -2;
+        if (be16(d + l4 + 2) == 53) {
+            if (len < l4 + 8 + 12) return -2;
+            return (ld16(d + l4 + 10) & 0x8000) ? 1 : 0;  // dnsv4_hdr.flags unswapped
+        }
+        if (be16(d + l4) == 53) {
+            if (len < l4 + 8 + 12) return -2;
+            return ((ld16(d + l4 + 10) & 0x7FFFF) ^ 0x8000) ? 1 : 0;
+        }
+        return -1;
+    }
+    if (proto == 1) {
+        if (len < l4 + 4) return -2;
+        if (d[l4] == 3 && d[l4 + 1] == 3) return 1;  // port unreachable
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img, const uint64_t *__restrict__ off,
+                                                     const uint32_t *__restrict__ caplen, uint64_t n, int first_mode,
+                                                     tp_tree_t t) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const u8 *d = img + off[j];
+    const u32 cl = caplen[j];
+    L2 r;
+    const int res = cl ? get_l2len_protocol(d, cl, r) : -1;
+    const bool v4 = res != -1 && r.l2len + 20 <= cl && r.protocol == 0x0800;
+    const bool v6 = !v4 && res != -1 && r.l2len + 40 <= cl && r.protocol == 0x86DD;
+    if (!v4 && !v6) {
+        t.slot[j] = 0xffffffffu;
+        return;
+    }
+    const u8 *ip = d + r.l2len;
+    const uint32_t s = tree_insert(t, node_key(v6, ip + (v6 ? 8 : 12)));
+    t.slot[j] = s;
+    if (s == 0xffffffffu) {
+        atomicMin((unsigned long long *)t.err, (unsigned long long)j);
+        return;
+    }
+    if (first_mode) {  // add_tree_first_ipv4/ipv6 (tree.c:333-452): the first sighting decides
+        atomicMin((unsigned long long *)&t.first[s], (unsigned long long)(2 * j));
+        const uint32_t sd = tree_insert(t, node_key(v6, ip + (v6 ? 24 : 16)));
+        if (sd == 0xffffffffu)
+            atomicMin((unsigned long long *)t.err, (unsigned long long)j);
+        else
+            atomicMin((unsigned long long *)&t.first[sd], (unsigned long long)(2 * j + 1));
+        return;
+    }
+    const int ty = packet2tree(d, cl);  // add_tree_ipv4/ipv6 + add_tree_node (tree.c:454-538)
+    if (ty == -2)
+        atomicMin((unsigned long long *)t.err, (unsigned long long)j);
+    else if (ty == 1)
+        atomicAdd(&t.server_cnt[s], 1u);
+    else if (ty == 0)
+        atomicAdd(&t.client_cnt[s], 1u);
+}
+
+// tree_calculate (tree.c:540-565) + check_ip_tree (:219-272): the tcpr_dir_t of a source
+DI int tree_dir(const tp_dev_cfg_t &c, const tp_tree_t &t, uint32_t s) {
+    uint32_t sc, cc;
+    if (c.automode == TP_AUTO_FIRST) {
+        const bool dst_first = t.first[s] & 1;
+        sc = dst_first ? 1000 : 0;
+        cc = dst_first ? 0 : 1000;
+    } else {
+        sc = t.server_cnt[s];
+        cc = t.client_cnt[s];
+    }
+    if (sc > 0 || cc > 0) return (double)sc >= (double)cc * c.ratio ? 2 : 1;  // server: S2C, client: C2S
+    return c.automode == TP_AUTO_SERVER ? 2 : c.automode == TP_AUTO_CLIENT ? 1 : -1;
+}
+
 // one record -> its 2-bit cache entry
-DI u32 classify(const tp_dev_cfg_t &c, const u8 *pkt, u32 caplen, uint64_t pktnum) {
+DI u32 classify(const tp_dev_cfg_t &c, const tp_tree_t *t, uint64_t j, const u8 *pkt, u32 caplen,
+                 uint64_t pktnum) {
     constexpr u32 SEND = 2, C2S = 1;
     // include/exclude packet list (tcpprep.c:362-375)
     if (c.nlist && check_list(c, pktnum) == ((c.xx_mode & TP_XX_EXCLUDE) != 0)) return 0;
@@ -113,7 +236,9 @@ DI u32 classify(const tp_dev_cfg_t &c, const u8 *pkt, u32 caplen, uint64_t pktnu
         if (!v4 && !v6) return SEND | (c.nonip == 1 ? C2S : 0);  // add_cache(SEND, options->nonip)
         const u8 *ip = pkt + r.l2len;
         if (c.nxx_cidr && c.xx_mode && !xx_cidr(c, ip, v6)) return 0;
-        if (c.mode == TP_MODE_CIDR) {
+        if (c.mode == TP_MODE_AUTO) {
+            dir = tree_dir(c, *t, t->slot[j]);  // -1 (TCPR_DIR_ERROR): send bit only
+        } else if (c.mode == TP_MODE_CIDR) {
             dir = v6 ? in6(c.cidr, c.ncidr, ip + 8) : in4(c.cidr, c.ncidr, ld32(ip + 12));
             if (c.reverse) dir = !dir;
         } else {
@@ -139,10 +264,11 @@ DI u32 classify(const tp_dev_cfg_t &c, const u8 *pkt, u32 caplen, uint64_t pktnu
 __global__ __launch_bounds__(256) void tp_classify(const u8 *__restrict__ img, const uint64_t *__restrict__ off,
                                                    const uint32_t *__restrict__ caplen,
                                                    const uint32_t *__restrict__ pktnum, uint64_t n,
-                                                   const tp_dev_cfg_t *__restrict__ cfg, u8 *__restrict__ out) {
+                                                   const tp_dev_cfg_t *__restrict__ cfg, const tp_tree_t *tree,
+                                                   u8 *__restrict__ out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     u32 e = 0;
-    if (j < n) e = classify(*cfg, img + off[j], caplen[j], pktnum ? (uint64_t)pktnum[j] : j + 1);
+    if (j < n) e = classify(*cfg, tree, j, img + off[j], caplen[j], pktnum ? (uint64_t)pktnum[j] : j + 1);
     e <<= 2 * (j & 3);
     e |= __shfl_xor(e, 1);
     e |= __shfl_xor(e, 2);
@@ -151,12 +277,22 @@ __global__ __launch_bounds__(256) void tp_classify(const u8 *__restrict__ img, c
 }  // namespace
 
 extern "C" int tp_launch_classify(const uint8_t *img, const uint64_t *off, const uint32_t *caplen,
-                                  const uint32_t *pktnum, uint64_t n_entries, const tp_dev_cfg_t *cfg, uint8_t *out,
-                                  void *stream) {
+                                  const uint32_t *pktnum, uint64_t n_entries, const tp_dev_cfg_t *cfg,
+                                  const tp_tree_t *tree, uint8_t *out, void *stream) {
     if (n_entries == 0) return 0;
     const uint64_t blocks = (n_entries + 255) / 256;
     if (blocks > 0x7fffffffull) return -1;
     hipLaunchKernelGGL(tp_classify, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, off, caplen, pktnum,
-                       n_entries, cfg, out);
+                       n_entries, cfg, tree, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int tp_launch_tree(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, uint64_t n_entries,
+                              const tp_dev_cfg_t *cfg, int automode, tp_tree_t tree, void *stream) {
+    if (n_entries == 0) return 0;
+    const uint64_t blocks = (n_entries + 255) / 256;
+    if (blocks > 0x7fffffffull) return -1;
+    hipLaunchKernelGGL(tp_tree_build, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, off, caplen,
+                       n_entries, automode == TP_AUTO_FIRST ? 1 : 0, tree);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -64,19 +64,57 @@ OPTION_LINES = [
     ["--cidr=96.17.211.0/24", "--exclude=B:96.0.0.0/8"],
     ["--port", "--exclude=S:96.17.211.0/24"],
     ["--comment=gpu", "--port"],
+    ["--auto=bridge"],
+    ["--auto=client", "--ratio=0.5"],
+    ["--auto=server", "--nonip"],
+    ["--auto=first", "--ratio=0"],
 ]
+
+
+def _both(pcap, args):
+    """GPU and oracle results, or the fact that both refused (packet2tree's len_error)."""
+    try:
+        exp = oracle_lib.tcpprep(pcap, args)
+    except ValueError:
+        exp = "error"
+    try:
+        got = TP.cache(pcap, args)
+    except RuntimeError as e:
+        assert "too small to process" in str(e)
+        got = "error"
+    return got, exp
 
 
 @pytest.mark.parametrize("line", range(len(OPTION_LINES)))
 def test_gpu_matches_oracle_adversarial(line):
     pcap = _adversarial()
     args = OPTION_LINES[line]
-    assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
+    got, exp = _both(pcap, args)
+    assert got == exp
+
+
+@pytest.mark.parametrize("mode", ["bridge", "client", "server", "first"])
+def test_gpu_auto_matches_oracle_without_short_tcp(mode):
+    """the adversarial corpus minus the truncations that make packet2tree abort"""
+    recs = [r for r in synth.records(_adversarial(seed=11)) if r[2] >= 74]
+    pcap = synth.build_pcap(recs)
+    got, exp = _both(pcap, [f"--auto={mode}"])
+    assert got == exp and got != "error"
+
+
+def test_gpu_auto_reports_len_error_like_the_reference():
+    recs = synth.records(T.test_pcap())[:20]
+    d = bytearray(recs[3][4][:40])  # an IPv4/TCP frame cut inside its TCP header
+    d[12:14], d[14], d[23] = (0x08, 0x00), 0x45, 6
+    recs[3] = (0, 0, 40, 40, bytes(d))
+    pcap = synth.build_pcap(recs)
+    assert _both(pcap, ["--auto=bridge"]) == ("error", "error")
 
 
 def test_gpu_matches_oracle_full_size_imix():
     pcap = synth.pcap_imix(500_000, seed=3)
-    for args in (["--port"], ["--cidr=10.0.0.0/9,172.16.128.0/17", "--reverse"]):
+    for args in (["--port"], ["--cidr=10.0.0.0/9,172.16.128.0/17", "--reverse"], ["--auto=bridge"],
+                 ["--auto=first"]):
         assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
 
 
@@ -110,6 +148,7 @@ def test_mac_mode_short_records_get_no_entry():
 
 
 def test_rejects_unsupported_modes_loudly():
-    for args in (["--auto=bridge"], ["--regex=96.*"], ["--port", "--include=F:tcp"], []):
+    for args in (["--auto=router"], ["--regex=96.*"], ["--port", "--include=F:tcp"], [],
+                 ["--auto=bridge", "--include=P:1-5"]):
         with pytest.raises(ValueError):
             TP.TcpPrep(args)
