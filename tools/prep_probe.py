@@ -17,7 +17,7 @@ def main():
                      ("imix_10m", lambda: synth.pcap_imix(10_000_000, seed=1))):
         t0 = time.time()
         pcap = mk()
-        for mode in (["--port"], ["--cidr=10.0.0.0/9,172.16.128.0/17"]):
+        for mode in (["--port"], ["--cidr=10.0.0.0/9,172.16.128.0/17"], ["--auto=bridge"], ["--auto=first"]):
             tp = TP.TcpPrep(["--no-arg-comment"] + mode)
             ms, n = tp.time(pcap, iters=50)
             tp.close()
