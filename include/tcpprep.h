@@ -10,7 +10,7 @@
  *                                       --nonip, --comment, --no-arg-comment, --include, --exclude)
  *   - tcpprep_cache_pcap             <- process_raw_packets + write_cache
  *                                       (src/tcpprep.c:339-587, src/common/cache.c:146-219)
- * Auto modes bridge/client/server/first (--auto, --ratio) are served; router and regex are not.
+ * Auto modes bridge/client/server/first/router (--auto, --ratio, --minmask, --maxmask) are served; regex is not.
  * Classification runs in the gfx950 kernel tp_classify; there is no CPU path.
  */
 #ifndef TCPPREP_HIP_H

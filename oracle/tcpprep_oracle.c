@@ -8,13 +8,13 @@
  * (-x/-X P:list, S:/D:/B:/E: CIDR), and the cache file writer
  * (src/common/cache.c:146-219 write_cache, :259-314 add_cache), and the auto
  * modes bridge/client/server/first (tree.c:219-565, packet2tree :653-838)
- * with --ratio.  Router mode (process_tree's CIDR build) and regex mode are
- * not restated (out of scope).
+ * with --ratio, and router (whose CIDR build never matches, see tpo_check_tree).
+ * Regex mode is not restated (out of scope).
  *
  * Pinning: checked byte-for-byte against the reference's own cache files
  * (test/test.cidr, .cidr_reverse, .mac, .mac_reverse, .port, .comment,
  * .include_packets, .exclude_packets, .include_source, .include_dest, made by
- * and test.auto_{bridge,client,server,first}; test/Makefile.am:87-104, from
+ * and test.auto_{bridge,client,server,first,router}; test/Makefile.am:87-104, from
  * test/test.pcap), committed under tests/golden/,
  * by tests/test_tcpprep.py.
  *
@@ -29,12 +29,12 @@
 
 enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3, TPO_AUTO = 4 };
 /* automode: defines.h.in:207 direction_e and tcpprep's BRIDGE/CLIENT/SERVER/FIRST modes */
-enum { TPA_BRIDGE = 1, TPA_CLIENT, TPA_SERVER, TPA_FIRST };
+enum { TPA_BRIDGE = 1, TPA_CLIENT, TPA_SERVER, TPA_FIRST, TPA_ROUTER };
 /* xX.h:34-41 */
 enum { XX_SOURCE = 1, XX_DEST = 2, XX_BOTH = 4, XX_EITHER = 8, XX_PACKET = 16, XX_EXCLUDE = 128 };
 
 typedef struct {
-    int mode, reverse, nonip, nocomment, automode;
+    int mode, reverse, nonip, nocomment, automode, min_mask, max_mask;
     double ratio;
     ocidr_t cidr[TPO_MAXC];
     int ncidr;
@@ -157,6 +157,8 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
 {
     memset(o, 0, sizeof(*o));
     o->ratio = 2.0; /* --ratio default, tcpprep_opts.def:511-516 */
+    o->min_mask = 30; /* --minmask / --maxmask defaults, tcpprep_opts.def:528-552 */
+    o->max_mask = 8;
     for (int i = 0; i <= 1023; i++) /* tcpprep_init, tcpprep_api.c:50-53 */
         o->svc_tcp[i] = o->svc_udp[i] = 1;
     char args[4096] = "";
@@ -201,8 +203,18 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
                 o->automode = TPA_SERVER;
             else if (!strcmp(v, "first"))
                 o->automode = TPA_FIRST;
+            else if (!strcmp(v, "router"))
+                o->automode = TPA_ROUTER;
             else
-                return -1; /* router: process_tree's CIDR build is not restated */
+                return -1;
+        } else if (IS("--minmask") || IS("--maxmask")) {
+            long m = strtol(v, NULL, 0);
+            if (m < 0 || m > 32)
+                return -1;
+            if (IS("--minmask"))
+                o->min_mask = (int)m;
+            else
+                o->max_mask = (int)m;
         } else if (IS("--ratio")) {
             char *end;
             o->ratio = strtod(v, &end);
@@ -232,7 +244,9 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
     if (!o->mode)
         return -1;
     if (o->mode == TPO_AUTO && o->xx_mode)
-        return -1; /* the first pass would add_cache() the filtered packets a second time */
+        return -1;
+    if (o->min_mask <= o->max_mask)
+        return -1; /* tcpprep_api.c:204-208 */ /* the first pass would add_cache() the filtered packets a second time */
     /* tcpprep_post_args, tcpprep_api.c:160-197: "args\ncomment" */
     char full[8192] = "";
     if (!o->nocomment && args[0]) {
@@ -518,7 +532,13 @@ static int tpo_check_tree(const tpo_opt_t *o, int fam, const uint8_t *src)
 {
     int ins = 0;
     tpo_node_t *e = tpo_find(fam, src, 0, &ins);
+    /* router mode: process_tree (tree.c:156-203) builds CIDRs whose family new_cidr()
+       leaves 0, so no address is ever "in" them: it succeeds at --maxmask after one
+       tree_calculate, and the second pass is check_ip_tree(options->nonip, ...)
+       (tcpprep.c:498-509): DIR_CLIENT by default, DIR_SERVER with --nonip */
     int mode = o->automode == TPA_SERVER ? 1 : o->automode == TPA_CLIENT ? 0 : -1;
+    if (o->automode == TPA_ROUTER)
+        mode = o->nonip ? 1 : 0;
     if (!e && mode == -1)
         return -4;
     if (e && e->type == 1)

@@ -23,6 +23,7 @@ int te_parse_cidr(char *s, te_cidr_t *c); /* te_args.c */
 struct tcpprep_hip_s {
     tp_dev_cfg_t cfg;
     int nocomment, has_comment;
+    int min_mask, max_mask; /* router mode's --minmask/--maxmask (validated only) */
     char comment[8192]; /* the final "args\ncomment" string */
     char errstr[1024];
 };
@@ -48,6 +49,8 @@ int tcpprep_init(tcpprep_hip_t **out)
         t->cfg.svc_udp[p >> 5] |= 1u << (p & 31);
     }
     t->cfg.ratio = 2.0; /* --ratio default, tcpprep_opts.def:511-516 */
+    t->min_mask = 30;   /* defaults, tcpprep_opts.def:528-552 */
+    t->max_mask = 8;
     *out = t;
     return 0;
 }
@@ -217,8 +220,19 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
                 c->automode = TP_AUTO_SERVER;
             else if (!strcmp(v, "first"))
                 c->automode = TP_AUTO_FIRST;
+            else if (!strcmp(v, "router"))
+                c->automode = TP_AUTO_ROUTER;
             else
-                return tp_err(t, "--auto=%s is not served by the GPU classifier (bridge, client, server, first)", v);
+                return tp_err(t, "Invalid --auto mode: %s", v);
+        } else if (OPT("--minmask") || OPT("--maxmask")) {
+            NEED_ARG();
+            long m = strtol(v, NULL, 0); /* tcpprep_opts.def:528-552: 0..32 */
+            if (m < 0 || m > 32)
+                return tp_err(t, "%.*s must be between 0 and 32", (int)nl, a);
+            if (OPT("--minmask"))
+                t->min_mask = (int)m;
+            else
+                t->max_mask = (int)m;
         } else if (OPT("--ratio")) {
             NEED_ARG();
             char *end;
@@ -241,6 +255,9 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
     }
     if (!c->mode)
         return tp_err(t, "one of --cidr, --mac, --port, --auto is required");
+    if (t->min_mask <= t->max_mask) /* tcpprep_api.c:204-208 */
+        return tp_err(t, "Min network mask len (%d) must be less then max network mask len (%d)", t->min_mask,
+                      t->max_mask);
     if (c->mode == TP_MODE_AUTO && c->xx_mode)
         return tp_err(t, "--include/--exclude with --auto are not served (the reference's first pass "
                          "would add the filtered records to the cache a second time)");

@@ -11,8 +11,8 @@
 #define TP_MAXC 64
 
 enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3, TP_MODE_AUTO = 4 };
-/* the auto modes the GPU serves (tcpprep.c:480-587; router's process_tree is not served) */
-enum { TP_AUTO_BRIDGE = 1, TP_AUTO_CLIENT, TP_AUTO_SERVER, TP_AUTO_FIRST };
+/* the auto modes (tcpprep.c:480-587) */
+enum { TP_AUTO_BRIDGE = 1, TP_AUTO_CLIENT, TP_AUTO_SERVER, TP_AUTO_FIRST, TP_AUTO_ROUTER };
 /* xX.h:34-41 */
 enum { TP_XX_SOURCE = 1, TP_XX_DEST = 2, TP_XX_BOTH = 4, TP_XX_EITHER = 8, TP_XX_PACKET = 16, TP_XX_EXCLUDE = 128 };
 

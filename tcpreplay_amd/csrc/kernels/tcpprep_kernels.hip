@@ -218,6 +218,10 @@ DI int tree_dir(const tp_dev_cfg_t &c, const tp_tree_t &t, uint32_t s) {
         cc = t.client_cnt[s];
     }
     if (sc > 0 || cc > 0) return (double)sc >= (double)cc * c.ratio ? 2 : 1;  // server: S2C, client: C2S
+    // router: process_tree (tree.c:156-203) builds CIDRs whose family new_cidr() leaves 0, so
+    // nothing is ever "in" them and it succeeds at --maxmask; the second pass is then
+    // check_ip_tree(options->nonip, ...) (tcpprep.c:498-509): DIR_CLIENT, or DIR_SERVER with --nonip
+    if (c.automode == TP_AUTO_ROUTER) return c.nonip ? 2 : 1;
     return c.automode == TP_AUTO_SERVER ? 2 : c.automode == TP_AUTO_CLIENT ? 1 : -1;
 }
 

@@ -20,6 +20,7 @@ CASES = {
     "auto_client": ["--auto=client"],
     "auto_server": ["--auto=server"],
     "auto_first": ["--auto=first"],
+    "auto_router": ["--auto=router"],
 }
 
 

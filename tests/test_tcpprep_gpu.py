@@ -68,6 +68,7 @@ OPTION_LINES = [
     ["--auto=client", "--ratio=0.5"],
     ["--auto=server", "--nonip"],
     ["--auto=first", "--ratio=0"],
+    ["--auto=router", "--nonip", "--minmask=24", "--maxmask=16"],
 ]
 
 
@@ -93,7 +94,7 @@ def test_gpu_matches_oracle_adversarial(line):
     assert got == exp
 
 
-@pytest.mark.parametrize("mode", ["bridge", "client", "server", "first"])
+@pytest.mark.parametrize("mode", ["bridge", "client", "server", "first", "router"])
 def test_gpu_auto_matches_oracle_without_short_tcp(mode):
     """the adversarial corpus minus the truncations that make packet2tree abort"""
     recs = [r for r in synth.records(_adversarial(seed=11)) if r[2] >= 74]
@@ -148,7 +149,7 @@ def test_mac_mode_short_records_get_no_entry():
 
 
 def test_rejects_unsupported_modes_loudly():
-    for args in (["--auto=router"], ["--regex=96.*"], ["--port", "--include=F:tcp"], [],
+    for args in (["--auto=bogus"], ["--auto=router", "--minmask=8", "--maxmask=16"], ["--regex=96.*"], ["--port", "--include=F:tcp"], [],
                  ["--auto=bridge", "--include=P:1-5"]):
         with pytest.raises(ValueError):
             TP.TcpPrep(args)

@@ -13,4 +13,4 @@ def test_oracle_matches_reference_cache(name):
 
 def test_oracle_rejects_unknown_option():
     with pytest.raises(ValueError):
-        oracle_lib.tcpprep(T.test_pcap(), ["--auto=router"])
+        oracle_lib.tcpprep(T.test_pcap(), ["--auto=bogus"])
