@@ -153,3 +153,16 @@ def test_rejects_unsupported_modes_loudly():
                  ["--auto=bridge", "--include=P:1-5"]):
         with pytest.raises(ValueError):
             TP.TcpPrep(args)
+
+
+def test_tcpprep_tool_file_to_file(tmp_path):
+    """bin/tcpprep against the reference's own cache files (test/Makefile.am:87-104)"""
+    import os
+    import subprocess
+    import tcpreplay_amd as TA
+    tool = os.path.join(os.path.dirname(TA.LIB_PATH), "..", "bin", "tcpprep")
+    src = os.path.join(T.GOLDEN, "test.pcap")
+    for name in ("auto_router", "cidr_reverse", "include_packets", "comment"):
+        out = tmp_path / ("prep." + name)
+        subprocess.run([tool, "-i", src, "-o", str(out)] + T.args(name), check=True, timeout=60)
+        assert out.read_bytes() == T.golden(name)
