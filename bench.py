@@ -241,12 +241,27 @@ def main():
                 from tcpreplay_amd import tcpprep as TP
                 n2 = 10_000_000
                 tp = TP.TcpPrep(["--no-arg-comment", "--port"])
-                kms2, ent = tp.time(make_pcap("c3", n2, 11), iters=max(5, opt.steps // 20))
+                prep_pcap = make_pcap("c3", n2, 11)
+                kms2, ent = tp.time(prep_pcap, iters=max(5, opt.steps // 20))
                 tp.close()
+                # CPU baseline: the oracle (oracle/tcpprep_oracle.c, 1 thread) on the first
+                # 1M records of the same capture, only the C call timed
+                cpu_prep = None
+                if not opt.no_cpu_baseline:
+                    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+                    import oracle_lib
+                    from tcpreplay_amd import synth as _syn
+                    sample = _syn.build_pcap(_syn.records(prep_pcap[:400_000_000])[:1_000_000])
+                    t0 = time.perf_counter()
+                    oracle_lib.tcpprep(sample, ["--no-arg-comment", "--port"])
+                    cpu_s = time.perf_counter() - t0
+                    cpu_prep = {"mpkt_s": round(1e6 / cpu_s / 1e6, 2), "cores": 1, "kind": "port",
+                                "sample": "first 1M records of the same capture, oracle --port, 1 thread"}
                 extra[wl] = {"workload": "tcpprep --port on IMIX 64/570/1514 7:4:1 (C3 corpus): v04 cache "
                                          "entries for every record", "packets": ent, "kernel_ms": round(kms2, 4),
                              "mpkt_s": round(ent / (kms2 * 1e-3) / 1e6, 1),
-                             "gbps_algorithmic": round(ent * 50.25 / (kms2 * 1e-3) / 1e9, 1)}
+                             "gbps_algorithmic": round(ent * 50.25 / (kms2 * 1e-3) / 1e9, 1),
+                             "cpu_baseline": cpu_prep}
                 continue
             n2 = DEFAULT_PACKETS[wl]
             te2, b2, r2, _ = run_workload(wl, n2, 0, 3, seed=11, device=0)
