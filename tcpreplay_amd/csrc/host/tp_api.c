@@ -389,10 +389,7 @@ typedef struct {
 
 static void dev_free(tp_dev_t *d)
 {
-    hipFree(d->tree.keys);
-    hipFree(d->tree.server_cnt);
-    hipFree(d->tree.client_cnt);
-    hipFree(d->tree.first);
+    hipFree(d->tree.slots);
     hipFree(d->tree.slot);
     hipFree(d->tree.err);
     hipFree(d->d_tree);
@@ -432,10 +429,7 @@ static int stage(tcpprep_hip_t *t, const void *pcap, size_t len, const tp_index_
             cap <<= 1;
         d->tree_cap = cap;
         d->tree.mask = cap - 1;
-        if (hipMalloc((void **)&d->tree.keys, cap * 8) != hipSuccess ||
-            hipMalloc((void **)&d->tree.server_cnt, cap * 4) != hipSuccess ||
-            hipMalloc((void **)&d->tree.client_cnt, cap * 4) != hipSuccess ||
-            hipMalloc((void **)&d->tree.first, cap * 8) != hipSuccess ||
+        if (hipMalloc((void **)&d->tree.slots, cap * 16) != hipSuccess ||
             hipMalloc((void **)&d->tree.slot, n * 4) != hipSuccess || hipMalloc((void **)&d->tree.err, 8) != hipSuccess ||
             hipMalloc((void **)&d->d_tree, sizeof(tp_tree_t)) != hipSuccess ||
             hipMemcpy(d->d_tree, &d->tree, sizeof(tp_tree_t), hipMemcpyHostToDevice) != hipSuccess) {
@@ -451,10 +445,7 @@ static int stage(tcpprep_hip_t *t, const void *pcap, size_t len, const tp_index_
 static int tree_pass(tcpprep_hip_t *t, const tp_dev_t *d, const tp_index_t *x, const uint8_t *img, hipStream_t st)
 {
     size_t cap = d->tree_cap;
-    if (hipMemsetAsync(d->tree.keys, 0, cap * 8, st) != hipSuccess ||
-        hipMemsetAsync(d->tree.server_cnt, 0, cap * 4, st) != hipSuccess ||
-        hipMemsetAsync(d->tree.client_cnt, 0, cap * 4, st) != hipSuccess ||
-        hipMemsetAsync(d->tree.first, 0xff, cap * 8, st) != hipSuccess ||
+    if (hipMemsetAsync(d->tree.slots, 0, cap * 16, st) != hipSuccess ||
         hipMemsetAsync(d->tree.err, 0xff, 8, st) != hipSuccess)
         return tp_err(t, "device memset failed");
     if (tp_launch_tree(d->img, d->off, d->caplen, x->n, d->cfg, t->cfg.automode, d->tree, st) != 0)
@@ -546,10 +537,7 @@ int tcpprep_time(tcpprep_hip_t *t, const void *pcap, size_t len, int iters, doub
             hipEventRecord(e0, NULL);
         if (t->cfg.mode == TP_MODE_AUTO) {
             size_t cap = d.tree_cap;
-            hipMemsetAsync(d.tree.keys, 0, cap * 8, NULL);
-            hipMemsetAsync(d.tree.server_cnt, 0, cap * 4, NULL);
-            hipMemsetAsync(d.tree.client_cnt, 0, cap * 4, NULL);
-            hipMemsetAsync(d.tree.first, 0xff, cap * 8, NULL);
+            hipMemsetAsync(d.tree.slots, 0, cap * 16, NULL);
             rc = tp_launch_tree(d.img, d.off, d.caplen, x.n, d.cfg, t->cfg.automode, d.tree, NULL);
         }
         if (rc == 0)

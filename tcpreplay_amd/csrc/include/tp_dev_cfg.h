@@ -32,9 +32,9 @@ typedef struct {
    64-bit keys -- IPv4: 1<<63 | address; IPv6: one key for every address, as
    tree_comp compares an IPv6 address with itself (tree.c:618-621) */
 typedef struct {
-    uint64_t *keys;     /* 0 = empty */
-    uint32_t *server_cnt, *client_cnt;
-    uint64_t *first;    /* first mode: min over sightings of 2 * entry + (0 src | 1 dst) */
+    uint64_t *slots;    /* 2 words per slot, one 16-byte pair: the key (0 = empty) and the node's
+                           counts (server << 32 | client), or in first mode ~min over sightings
+                           of 2 * entry + (0 source | 1 destination) */
     uint32_t *slot;     /* per entry: its source's slot, or ~0 for a non-IP record */
     uint64_t mask;      /* capacity - 1 (power of two, >= 2x the insertions) */
     uint64_t *err;      /* min entry index whose packet2tree hit len_error (init ~0) */

@@ -105,8 +105,9 @@ DI int dst_port(const tp_dev_cfg_t &c, const u8 *ip, bool v6, int len) {
 // first mode its destination) into an open-addressing table on exact 64-bit
 // keys and bumps the node's counters; the table is the RB tree's set of
 // nodes, and atomics make the order of insertion irrelevant except where the
-// reference is order-dependent (first mode), which an atomicMin over sighting
-// order reproduces.  Second pass (classify): tree_calculate + check_ip_tree
+// reference is order-dependent (first mode), which an atomicMax over the complement of the
+// sighting order reproduces.  A node's key and counts share one 16-byte pair, so the
+// counter update hits the line its insertion just brought into L2.  Second pass (classify): tree_calculate + check_ip_tree
 // per record from its source's slot.
 // ---------------------------------------------------------------------------
 constexpr uint64_t TP_V6_KEY = 1ull << 62;
@@ -118,7 +119,7 @@ DI uint32_t tree_insert(const tp_tree_t &t, uint64_t key) {
     h ^= h >> 29;
     for (uint64_t k = 0; k <= t.mask; ++k) {
         const uint64_t s = (h + k) & t.mask;
-        const uint64_t prev = atomicCAS((unsigned long long *)&t.keys[s], 0ull, (unsigned long long)key);
+        const uint64_t prev = atomicCAS((unsigned long long *)&t.slots[2 * s], 0ull, (unsigned long long)key);
         if (prev == 0 || prev == key) return (uint32_t)s;
     }
     return 0xffffffffu;  // cannot happen: capacity >= 2x the insertions
@@ -189,33 +190,32 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
         return;
     }
     if (first_mode) {  // add_tree_first_ipv4/ipv6 (tree.c:333-452): the first sighting decides
-        atomicMin((unsigned long long *)&t.first[s], (unsigned long long)(2 * j));
+        atomicMax((unsigned long long *)&t.slots[2 * s + 1], ~(unsigned long long)(2 * j));  // ~min = max ~
         const uint32_t sd = tree_insert(t, node_key(v6, ip + (v6 ? 24 : 16)));
         if (sd == 0xffffffffu)
             atomicMin((unsigned long long *)t.err, (unsigned long long)j);
         else
-            atomicMin((unsigned long long *)&t.first[sd], (unsigned long long)(2 * j + 1));
+            atomicMax((unsigned long long *)&t.slots[2 * sd + 1], ~(unsigned long long)(2 * j + 1));
         return;
     }
     const int ty = packet2tree(d, cl);  // add_tree_ipv4/ipv6 + add_tree_node (tree.c:454-538)
     if (ty == -2)
         atomicMin((unsigned long long *)t.err, (unsigned long long)j);
-    else if (ty == 1)
-        atomicAdd(&t.server_cnt[s], 1u);
-    else if (ty == 0)
-        atomicAdd(&t.client_cnt[s], 1u);
+    else if (ty >= 0)  // the counts share the key's 16-byte pair: one line per node
+        atomicAdd((unsigned long long *)&t.slots[2 * s + 1], ty == 1 ? 1ull << 32 : 1ull);
 }
 
 // tree_calculate (tree.c:540-565) + check_ip_tree (:219-272): the tcpr_dir_t of a source
 DI int tree_dir(const tp_dev_cfg_t &c, const tp_tree_t &t, uint32_t s) {
     uint32_t sc, cc;
+    const uint64_t w = t.slots[2 * s + 1];
     if (c.automode == TP_AUTO_FIRST) {
-        const bool dst_first = t.first[s] & 1;
+        const bool dst_first = ~w & 1;
         sc = dst_first ? 1000 : 0;
         cc = dst_first ? 0 : 1000;
     } else {
-        sc = t.server_cnt[s];
-        cc = t.client_cnt[s];
+        sc = (uint32_t)(w >> 32);
+        cc = (uint32_t)w;
     }
     if (sc > 0 || cc > 0) return (double)sc >= (double)cc * c.ratio ? 2 : 1;  // server: S2C, client: C2S
     // router: process_tree (tree.c:156-203) builds CIDRs whose family new_cidr() leaves 0, so
