@@ -8,6 +8,7 @@
  *   - tcpprep_parse_args             <- the AutoOpts option surface tcpprep_post_args reads
  *                                       (src/tcpprep_opts.def: --cidr, --mac, --port, --reverse,
  *                                       --nonip, --comment, --no-arg-comment, --include, --exclude)
+ *   - tcpprep_set_pkt_base           <- (new) a shard's first global record number
  *   - tcpprep_cache_pcap             <- process_raw_packets + write_cache
  *                                       (src/tcpprep.c:339-587, src/common/cache.c:146-219)
  * Auto modes bridge/client/server/first/router (--auto, --ratio, --minmask, --maxmask) are served; regex is not.
@@ -38,6 +39,12 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *ctx, const void *pcap, size_t pcap_len
    classification kernel `iters` times; mean kernel ms (hipEvents) and entries */
 int tcpprep_time(tcpprep_hip_t *ctx, const void *pcap, size_t pcap_len, int iters, double *ms_kernel,
                  uint64_t *entries);
+/* multi-GPU shards (per-packet modes): the number of records before this shard, so
+   --include/--exclude P: lists see global record numbers; 0 ok, -1 error */
+int tcpprep_set_pkt_base(tcpprep_hip_t *ctx, uint64_t pkt_base);
+/* cache entries (2-bit) the last tcpprep_cache_pcap wrote: the records, less MAC
+   mode's short ones; a shard merge places the next shard's entries after them */
+int64_t tcpprep_last_entries(tcpprep_hip_t *ctx);
 const char *tcpprep_geterr(tcpprep_hip_t *ctx);
 int tcpprep_close(tcpprep_hip_t **ctx);
 

@@ -24,6 +24,7 @@ struct tcpprep_hip_s {
     tp_dev_cfg_t cfg;
     int nocomment, has_comment;
     int min_mask, max_mask; /* router mode's --minmask/--maxmask (validated only) */
+    uint64_t last_entries;  /* cache entries the last tcpprep_cache_pcap wrote */
     char comment[8192]; /* the final "args\ncomment" string */
     char errstr[1024];
 };
@@ -65,6 +66,18 @@ int tcpprep_close(tcpprep_hip_t **t)
 }
 
 const char *tcpprep_geterr(tcpprep_hip_t *t) { return t ? t->errstr : NULL; }
+
+int64_t tcpprep_last_entries(tcpprep_hip_t *t) { return t ? (int64_t)t->last_entries : -1; }
+
+int tcpprep_set_pkt_base(tcpprep_hip_t *t, uint64_t pkt_base)
+{
+    if (!t)
+        return -1;
+    if (t->cfg.mode == TP_MODE_AUTO && pkt_base)
+        return tp_err(t, "--auto classifies by the whole capture's host table: it does not shard");
+    t->cfg.pkt_base = pkt_base;
+    return 0;
+}
 
 /* parse_cidr(&list, s, ","): cidr.c:244-279 (a ',' list never hides v6 colons) */
 static int cidr_list(tcpprep_hip_t *t, const char *arg, te_cidr_t *v, int32_t *n, const char *what)
@@ -346,7 +359,7 @@ static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index
             break;
         x->records++;
         const tp_dev_cfg_t *c = &t->cfg;
-        int listed_out = c->nlist && check_list(c, x->records) == ((c->xx_mode & TP_XX_EXCLUDE) != 0);
+        int listed_out = c->nlist && check_list(c, c->pkt_base + x->records) == ((c->xx_mode & TP_XX_EXCLUDE) != 0);
         if (mac && caplen < 14 && !listed_out) {
             if (!gaps) { /* record numbers diverge from entry numbers from here on */
                 x->pktnum = malloc(cap * sizeof(uint32_t));
@@ -509,6 +522,7 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
     out[22] = (uint8_t)(clen >> 8);
     out[23] = (uint8_t)clen;
     memcpy(out + 24, t->comment, clen);
+    t->last_entries = x.n;
     index_free(&x);
     return (int64_t)(hdr + body);
 }

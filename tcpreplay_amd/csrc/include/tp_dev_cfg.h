@@ -21,6 +21,7 @@ typedef struct {
     int32_t ncidr, nmac, xx_mode, nxx_cidr;
     int32_t nlist, automode;
     double ratio;                /* --ratio (default 2.0) */
+    uint64_t pkt_base;           /* records before this capture (a shard's place in the job) */
     te_cidr_t cidr[TP_MAXC];     /* -c list (check_ip_cidr: empty list matches all) */
     te_cidr_t xx_cidr[TP_MAXC];  /* -x/-X S:/D:/B:/E: list */
     uint8_t mac[TP_MAXC][8];     /* -e list, as macinstring's mac2hex leaves each token */

@@ -272,7 +272,8 @@ __global__ __launch_bounds__(256) void tp_classify(const u8 *__restrict__ img, c
                                                    u8 *__restrict__ out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     u32 e = 0;
-    if (j < n) e = classify(*cfg, tree, j, img + off[j], caplen[j], pktnum ? (uint64_t)pktnum[j] : j + 1);
+    if (j < n)
+        e = classify(*cfg, tree, j, img + off[j], caplen[j], cfg->pkt_base + (pktnum ? (uint64_t)pktnum[j] : j + 1));
     e <<= 2 * (j & 3);
     e |= __shfl_xor(e, 1);
     e |= __shfl_xor(e, 2);

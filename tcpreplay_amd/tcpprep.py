@@ -25,6 +25,8 @@ def _lib():
                 ("tcpprep_time", c_int, [vp, ctypes.c_char_p, sz, c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_uint64)]),
                 ("tcpprep_geterr", ctypes.c_char_p, [vp]),
+                ("tcpprep_set_pkt_base", c_int, [vp, ctypes.c_uint64]),
+                ("tcpprep_last_entries", ctypes.c_int64, [vp]),
                 ("tcpprep_close", c_int, [ctypes.POINTER(vp)])):
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
@@ -58,6 +60,13 @@ class TcpPrep:
             raise RuntimeError(self.geterr())
         return out.raw[:n]
 
+    def set_pkt_base(self, base: int):
+        if self._L.tcpprep_set_pkt_base(self._ctx, base) != 0:
+            raise ValueError(self.geterr())
+
+    def last_entries(self) -> int:
+        return self._L.tcpprep_last_entries(self._ctx)
+
     def time(self, pcap: bytes, iters=20):
         """(mean kernel ms, entries) with the image resident in HBM."""
         ms, n = ctypes.c_double(), ctypes.c_uint64()
@@ -83,3 +92,64 @@ def cache(pcap: bytes, args) -> bytes:
         return tp.cache(pcap)
     finally:
         tp.close()
+
+
+def gpu_classifier(image: bytes, args, pkt_base: int):
+    """one shard on the GPU -> (cache body bytes, entries)"""
+    tp = TcpPrep(args)
+    try:
+        tp.set_pkt_base(pkt_base)
+        c = tp.cache(image)
+        return c[24 + int.from_bytes(c[22:24], "big"):], tp.last_entries()
+    finally:
+        tp.close()
+
+
+def merge_shards(parts, records: int, comment: bytes) -> bytes:
+    """(body, entries) per shard in file order -> one v04 cache file: the shards' 2-bit
+    entries concatenated (a shard's entry count need not be a multiple of 4)."""
+    import numpy as np
+    ents = []
+    for body, n in parts:
+        b = np.frombuffer(body, np.uint8)
+        e = ((b[:, None] >> np.array([0, 2, 4, 6], np.uint8)) & 3).reshape(-1)[:n]
+        ents.append(e)
+    e = np.concatenate(ents) if ents else np.zeros(0, np.uint8)
+    pad = (-len(e)) % 4
+    e = np.concatenate([e, np.zeros(pad, np.uint8)]).reshape(-1, 4)
+    body = (e[:, 0] | (e[:, 1] << 2) | (e[:, 2] << 4) | (e[:, 3] << 6)).astype(np.uint8).tobytes()
+    hdr = b"tcpprep\0" + b"04\0\0" + records.to_bytes(8, "big") + (4).to_bytes(2, "big") + \
+        len(comment).to_bytes(2, "big")
+    return hdr + comment + body
+
+
+def comment_of(args) -> bytes:
+    """the cache comment the options give (read back from a one-record probe run)"""
+    from . import synth
+    tp = TcpPrep(args)
+    try:
+        c = tp.cache(synth.pcap_fixed(1, 64))
+    finally:
+        tp.close()
+    return c[24:24 + int.from_bytes(c[22:24], "big")]
+
+
+def prep_distributed(pcap: bytes, args, dist=None, classifier=None, comment: bytes = None):
+    """Sharded tcpprep (per-packet modes): each rank classifies its byte-balanced record
+    range (tcpedit_pcap_shards) with its global record base, one all_gather_object of
+    (body, entries) per rank, every rank assembles the same cache file.  With dist=None
+    all shards run in this process (one per 'rank' of a 2-way plan)."""
+    from .dist import plan
+    classifier = classifier or gpu_classifier
+    world = dist.get_world_size() if dist else 2
+    p = plan(pcap, world)
+    if dist:
+        r = dist.get_rank()
+        mine = classifier(p.image(pcap, r), args, p.pkt_base[r])
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+    else:
+        parts = [classifier(p.image(pcap, k), args, p.pkt_base[k]) for k in range(world)]
+    if comment is None:
+        comment = comment_of(args)
+    return merge_shards(parts, p.total, comment)
