@@ -24,6 +24,7 @@
  * cpu_baseline leg may load it.
  */
 #include "tcpedit_oracle.c"
+#include <regex.h>
 
 #define TPO_MAXC 64
 
@@ -152,6 +153,39 @@ static int tpo_xx(tpo_opt_t *o, const char *arg, int exclude)
     return 1;
 }
 
+/* parse_services common/services.c:34-93 */
+static int tpo_services(tpo_opt_t *o, const char *file)
+{
+    FILE *f = fopen(file, "r");
+    if (!f)
+        return 0;
+    regex_t preg;
+    if (regcomp(&preg, "([0-9]+)/(tcp|udp)", REG_ICASE | REG_EXTENDED) != 0) {
+        fclose(f);
+        return 0;
+    }
+    memset(o->svc_tcp, 0, sizeof o->svc_tcp);
+    memset(o->svc_udp, 0, sizeof o->svc_udp);
+    char line[1024];
+    regmatch_t pm[3];
+    while (fgets(line, sizeof line, f)) {
+        if (regexec(&preg, line, 3, pm, 0) == 0) {
+            char port[16] = {0}, proto[16] = {0};
+            int pl = pm[1].rm_eo - pm[1].rm_so, ql = pm[2].rm_eo - pm[2].rm_so;
+            strncpy(port, line + pm[1].rm_so, pl < 9 ? pl : 9);
+            strncpy(proto, line + pm[2].rm_so, ql < 9 ? ql : 9);
+            uint16_t portc = (uint16_t)strtol(port, NULL, 10);
+            if (!strcmp(proto, "tcp"))
+                o->svc_tcp[portc] = 1;
+            else if (!strcmp(proto, "udp"))
+                o->svc_udp[portc] = 1;
+        }
+    }
+    regfree(&preg);
+    fclose(f);
+    return 1;
+}
+
 /* option surface: tcpprep_opts.def (long forms only) */
 static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
 {
@@ -219,6 +253,9 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
             char *end;
             o->ratio = strtod(v, &end);
             if (o->ratio < 0)
+                return -1;
+        } else if (IS("--services")) {
+            if (!tpo_services(o, v))
                 return -1;
         } else if (IS("--reverse")) {
             o->reverse = 1;

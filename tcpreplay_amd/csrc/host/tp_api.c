@@ -10,6 +10,7 @@
 #define __HIP_PLATFORM_AMD__
 #endif
 #include <ctype.h>
+#include <regex.h>
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -170,6 +171,41 @@ static int include_exclude(tcpprep_hip_t *t, const char *arg, int exclude)
     return 0;
 }
 
+/* parse_services (common/services.c:34-93): every line matching "([0-9]+)/(tcp|udp)"
+   (REG_ICASE|REG_EXTENDED) marks a server port; the file replaces the 0-1023 default */
+static int load_services(tcpprep_hip_t *t, const char *file)
+{
+    tp_dev_cfg_t *c = &t->cfg;
+    FILE *f = fopen(file, "r");
+    if (!f)
+        return tp_err(t, "Unable to open service file: %s", file);
+    regex_t preg;
+    if (regcomp(&preg, "([0-9]+)/(tcp|udp)", REG_ICASE | REG_EXTENDED) != 0) {
+        fclose(f);
+        return tp_err(t, "Unable to compile the services regex");
+    }
+    memset(c->svc_tcp, 0, sizeof c->svc_tcp);
+    memset(c->svc_udp, 0, sizeof c->svc_udp);
+    char line[1024]; /* MAXLINE, defines.h.in */
+    regmatch_t m[3];
+    while (fgets(line, sizeof line, f)) {
+        if (regexec(&preg, line, 3, m, 0) != 0)
+            continue;
+        char port[10] = {0}, proto[10] = {0};
+        size_t pl = (size_t)(m[1].rm_eo - m[1].rm_so), ql = (size_t)(m[2].rm_eo - m[2].rm_so);
+        memcpy(port, line + m[1].rm_so, pl < 9 ? pl : 9);
+        memcpy(proto, line + m[2].rm_so, ql < 9 ? ql : 9);
+        uint16_t p = (uint16_t)strtol(port, NULL, 10);
+        if (!strcmp(proto, "tcp"))
+            c->svc_tcp[p >> 5] |= 1u << (p & 31);
+        else if (!strcmp(proto, "udp"))
+            c->svc_udp[p >> 5] |= 1u << (p & 31);
+    }
+    regfree(&preg);
+    fclose(f);
+    return 0;
+}
+
 int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
 {
     if (!t)
@@ -252,7 +288,10 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
             c->ratio = strtod(v, &end); /* tcpprep_api.c:210-216 */
             if (c->ratio < 0)
                 return tp_err(t, "Ratio must be a non-negative number");
-        } else if (OPT("--regex") || OPT("--services")) {
+        } else if (OPT("--services")) {
+            NEED_ARG();
+            rc = load_services(t, v);
+        } else if (OPT("--regex")) {
             return tp_err(t, "%.*s is not served by the GPU classifier (per-packet modes only)", (int)nl, a);
         } else {
             return tp_err(t, "unknown option %s", a);

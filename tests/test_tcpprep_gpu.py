@@ -166,3 +166,12 @@ def test_tcpprep_tool_file_to_file(tmp_path):
         out = tmp_path / ("prep." + name)
         subprocess.run([tool, "-i", src, "-o", str(out)] + T.args(name), check=True, timeout=60)
         assert out.read_bytes() == T.golden(name)
+
+
+def test_gpu_services_file_matches_oracle(tmp_path):
+    from test_tcpprep_oracle import SERVICES
+    f = tmp_path / "services"
+    f.write_text(SERVICES)
+    for pcap in (T.test_pcap(), _adversarial(), synth.pcap_imix(200_000, seed=4)):
+        args = ["--no-arg-comment", "--port", f"--services={f}"]
+        assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
