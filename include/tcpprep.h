@@ -7,7 +7,8 @@
  *   - tcpprep_init / tcpprep_close   <- tcpprep_init / tcpprep_close (src/tcpprep_api.c:40-110)
  *   - tcpprep_parse_args             <- the AutoOpts option surface tcpprep_post_args reads
  *                                       (src/tcpprep_opts.def: --cidr, --mac, --port, --reverse,
- *                                       --nonip, --comment, --no-arg-comment, --include, --exclude)
+ *                                       --nonip, --comment, --no-arg-comment, --include, --exclude,
+ *                                       --auto, --ratio, --minmask, --maxmask, --services)
  *   - tcpprep_set_pkt_base           <- (new) a shard's first global record number
  *   - tcpprep_cache_pcap             <- process_raw_packets + write_cache
  *                                       (src/tcpprep.c:339-587, src/common/cache.c:146-219)
