@@ -17,6 +17,7 @@
 #ifndef TCPEDIT_HIP_H
 #define TCPEDIT_HIP_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <sys/time.h>
@@ -45,10 +46,78 @@ struct pcap_pkthdr {
 typedef enum tcpr_dir_e { TCPR_DIR_ERROR = -1, TCPR_DIR_NOSEND = 0, TCPR_DIR_C2S = 1, TCPR_DIR_S2C = 2 } tcpr_dir_t;
 #endif
 
-/* tcpedit_types.h:47 */
+/* tcpedit_types.h:36-47 */
+typedef enum { TCPEDIT_FIXLEN_OFF = 0, TCPEDIT_FIXLEN_PAD, TCPEDIT_FIXLEN_TRUNC, TCPEDIT_FIXLEN_DEL } tcpedit_fixlen;
+typedef enum {
+    TCPEDIT_TTL_MODE_OFF = 0,
+    TCPEDIT_TTL_MODE_SET,
+    TCPEDIT_TTL_MODE_ADD,
+    TCPEDIT_TTL_MODE_SUB
+} tcpedit_ttl_mode;
+typedef enum { TCPEDIT_EDIT_BOTH = 0, TCPEDIT_EDIT_C2S, TCPEDIT_EDIT_S2C } tcpedit_direction;
 typedef enum { BEFORE_PROCESS, AFTER_PROCESS } tcpedit_coder;
+/* plugins/dlt_en10mb/en10mb_types.h:41-52 */
+typedef enum {
+    TCPEDIT_MAC_MASK_SMAC1 = 1,
+    TCPEDIT_MAC_MASK_SMAC2 = 2,
+    TCPEDIT_MAC_MASK_DMAC1 = 4,
+    TCPEDIT_MAC_MASK_DMAC2 = 8
+} tcpedit_mac_mask;
+typedef enum { TCPEDIT_VLAN_OFF = 0, TCPEDIT_VLAN_DEL, TCPEDIT_VLAN_ADD } tcpedit_vlan;
 
-typedef struct tcpedit_s tcpedit_t;
+/* ---- the context ------------------------------------------------------------
+ * A tcpedit_t * from tcpedit_init points at a context whose first bytes are laid
+ * out exactly as the reference's tcpedit_t (tcpedit_types.h:49-61 runtime,
+ * :91-153 the struct), so a reference tool compiled against its own headers and
+ * relinked against this library reads the fields it dereferences directly --
+ * tcprewrite.c:103 and tcpreplay.c:169 `tcpedit->fuzz_seed / fuzz_factor`,
+ * tcpreplay.c:256 `tcpedit->seed` -- with their derived values.  The library keeps
+ * these fields in step with its own derived tables after tcpedit_post_args and
+ * every setter.  The list pointers (cidrmap1..dstipmap, portmap) are NULL: the
+ * maps live in the device tables, and no caller outside libtcpedit reads them.
+ * dlt_ctx points at the context's DLT plugin handle (plugins_api.h). */
+typedef struct {
+    unsigned long long packetnum;   /* COUNTER (defines.h.in:103, ENABLE_64BITS) */
+    unsigned long long total_bytes;
+    unsigned long long pkts_edited;
+    int dlt1;
+    int dlt2;
+    char errstr[1024];              /* TCPEDIT_ERRSTR_LEN */
+    char warnstr[1024];
+} tcpedit_runtime_t;
+
+typedef struct tcpeditdlt_s tcpeditdlt_t;
+
+typedef struct tcpedit_ref_s {
+    bool validated;
+    tcpeditdlt_t *dlt_ctx;
+    tcpedit_runtime_t runtime;
+    bool skip_broadcast;
+    tcpedit_fixlen fixlen;
+    tcpedit_direction editdir;
+    bool rewrite_ip;
+    uint32_t tcp_sequence_enable;
+    uint32_t tcp_sequence_adjust;
+    bool fixcsum;
+    bool efcs;
+    tcpedit_ttl_mode ttl_mode;
+    uint8_t ttl_value;
+    int tos;
+    int flowlabel;
+    int tclass;
+    void *cidrmap1, *cidrmap2;      /* tcpr_cidrmap_t * */
+    void *srcipmap, *dstipmap;
+    uint32_t seed;
+    void *portmap;                  /* tcpedit_portmap_t * */
+    int mtu;
+    bool mtu_truncate;
+    int maxpacket;
+    uint32_t fuzz_seed;
+    uint32_t fuzz_factor;
+    bool fixhdrlen;
+} tcpedit_ref_t;
+
+typedef struct tcpedit_s tcpedit_t;   /* begins with a tcpedit_ref_t */
 
 /* ---- reference interface: tcpedit.h:38-55 ---------------------------------- */
 int tcpedit_init(tcpedit_t **tcpedit, int dlt);                       /* tcpedit.c:371-403 */
@@ -65,7 +134,24 @@ int tcpedit_l3proto(tcpedit_t *tcpedit, tcpedit_coder code, const unsigned char 
 uint64_t tcpedit_get_total_bytes(tcpedit_t *tcpedit);  /* declared tcpedit.h:54-55, never defined there */
 uint64_t tcpedit_get_pkts_edited(tcpedit_t *tcpedit);
 
-/* ---- parse_args.h: derive the per-run tables from the option surface ----- */
+/* ---- fuzzing.h:26 ------------------------------------------------------------
+ * The reference keeps the fuzz RNG in process-wide statics (fuzzing.c:8-20) that
+ * tcprewrite.c:103 / tcpreplay.c:169 seed after tcpedit_post_args.  Here the state
+ * lives on the device, one word per context: fuzzing_init re-seeds every context's
+ * state (and sets the factor) before its next edit.  A context whose tcpedit_post_args
+ * derived a --fuzz-seed is seeded with that value by itself when no fuzzing_init call
+ * has been made (this library's own tools never need the call). */
+void fuzzing_init(uint32_t fuzz_seed, uint32_t fuzz_factor);
+
+/* ---- parse_args.h: derive the per-run tables from the option surface -----
+ * The options come from, in this order:
+ *   1. tcpedit_parse_args / tcpedit_set_option, when either was called on the context;
+ *   2. otherwise the calling tool's AutoOpts descriptor (tcprewriteOptions,
+ *      tcpreplayOptions or tcpbridgeOptions), read field by field as libopts lays it
+ *      out (libopts/autoopts/options.h:519-579, 603-680) -- so a reference tool
+ *      relinked against this library passes its command line through unchanged;
+ *   3. otherwise the values the tcpedit_set_* setters stored.
+ * With none of the three it fails (TCPEDIT_ERROR) rather than run with no edits. */
 int tcpedit_post_args(tcpedit_t *tcpedit);                             /* parse_args.c:34-254 */
 
 /* ---- option surface (stands in for AutoOpts HAVE_OPT/OPT_ARG, Appendix C) --
@@ -79,26 +165,54 @@ int tcpedit_set_option(tcpedit_t *tcpedit, const char *name, const char *value);
 int tcpedit_parse_args(tcpedit_t *tcpedit, int argc, char **argv, int *unused);
 
 /* ---- programmatic setters: tcpedit_api.h:32-58 --------------------------- */
-int tcpedit_set_skip_broadcast(tcpedit_t *, int);
-int tcpedit_set_fixcsum(tcpedit_t *, int);
-int tcpedit_set_fixhdrlen(tcpedit_t *, int);
-int tcpedit_set_efcs(tcpedit_t *, int);
-int tcpedit_set_ttl_mode(tcpedit_t *, int);   /* 0 off, 1 set, 2 add, 3 sub */
+int tcpedit_set_encoder_dltplugin_byid(tcpedit_t *, int);            /* tcpedit_api.c:33-65 */
+int tcpedit_set_encoder_dltplugin_byname(tcpedit_t *, const char *); /* tcpedit_api.c:72-104 */
+int tcpedit_set_skip_broadcast(tcpedit_t *, bool);
+int tcpedit_set_fixlen(tcpedit_t *, tcpedit_fixlen);
+int tcpedit_set_fixcsum(tcpedit_t *, bool);
+int tcpedit_set_fixhdrlen(tcpedit_t *, bool);
+int tcpedit_set_efcs(tcpedit_t *, bool);
+int tcpedit_set_ttl_mode(tcpedit_t *, tcpedit_ttl_mode);
 int tcpedit_set_ttl_value(tcpedit_t *, uint8_t);
 int tcpedit_set_tos(tcpedit_t *, uint8_t);
 int tcpedit_set_tclass(tcpedit_t *, uint8_t);
 int tcpedit_set_flowlabel(tcpedit_t *, uint32_t);
 int tcpedit_set_seed(tcpedit_t *);            /* tcpedit_api.c:210: seed = random() */
 int tcpedit_set_mtu(tcpedit_t *, int);
-int tcpedit_set_mtu_truncate(tcpedit_t *, int);
+int tcpedit_set_mtu_truncate(tcpedit_t *, bool);
 int tcpedit_set_maxpacket(tcpedit_t *, int);
-int tcpedit_set_fixlen(tcpedit_t *, int);     /* 0 off, 1 pad, 2 trunc, 3 del */
-int tcpedit_set_tcp_sequence(tcpedit_t *, uint32_t);
 int tcpedit_set_cidrmap_s2c(tcpedit_t *, char *);
 int tcpedit_set_cidrmap_c2s(tcpedit_t *, char *);
 int tcpedit_set_srcip_map(tcpedit_t *, char *);
 int tcpedit_set_dstip_map(tcpedit_t *, char *);
 int tcpedit_set_port_map(tcpedit_t *, char *);
+/* not in tcpedit_api.h, but a setter the reference's struct is edited for directly
+ * (tcp_sequence_enable/adjust, tcpedit_types.h:104-105) */
+int tcpedit_set_tcp_sequence(tcpedit_t *, uint32_t);
+
+/* ---- EN10MB plugin setters: plugins/dlt_en10mb/en10mb_api.h:38-42 -------- */
+int tcpedit_en10mb_set_mac(tcpedit_t *tcpedit, char *mac, tcpedit_mac_mask mask);
+int tcpedit_en10mb_set_vlan_mode(tcpedit_t *tcpedit, tcpedit_vlan vlan);
+int tcpedit_en10mb_set_vlan_tag(tcpedit_t *tcpedit, uint16_t tag);
+int tcpedit_en10mb_set_vlan_priority(tcpedit_t *tcpedit, uint8_t priority);
+int tcpedit_en10mb_set_vlan_cfi(tcpedit_t *tcpedit, uint8_t cfi);
+
+/* ---- DLT plugin API: plugins_api.h:29-78 ----------------------------------
+ * The context's plugin handle (tcpedit_ref_t.dlt_ctx).  The per-packet plugin
+ * hooks (process/decode/encode/merge) have no caller outside libtcpedit: here the
+ * L2 decode and encode are fused into the edit kernel, so they are not exported.
+ * The accessors answer from the selected decoder/encoder and the L2 walk of the
+ * DLT_EN10MB plugin (get_l2len_protocol, get.c:262-451). */
+int tcpedit_dlt_post_args(tcpedit_t *tcpedit);                 /* dlt_plugins.c:168-204 */
+tcpeditdlt_t *tcpedit_dlt_init(tcpedit_t *tcpedit, int srcdlt);  /* dlt_plugins.c:111-158 */
+int tcpedit_dlt_post_init(tcpeditdlt_t *ctx);                   /* dlt_plugins.c:249-262 */
+void tcpedit_dlt_cleanup(tcpeditdlt_t *ctx);                    /* dlt_plugins.c:443-474 */
+int tcpedit_dlt_output_dlt(tcpeditdlt_t *ctx);                  /* dlt_plugins.c:268-283 */
+int tcpedit_dlt_l2len(tcpeditdlt_t *ctx, int dlt, const unsigned char *packet, const int pktlen); /* :290-314 */
+int tcpedit_dlt_proto(tcpeditdlt_t *ctx, int dlt, const unsigned char *packet, const int pktlen); /* :320-334 */
+unsigned char *tcpedit_dlt_l3data(tcpeditdlt_t *ctx, int dlt, unsigned char *packet, const int pktlen); /* :340 */
+int tcpedit_dlt_src(tcpeditdlt_t *ctx);                         /* dlt_plugins.c:424-428 */
+int tcpedit_dlt_dst(tcpeditdlt_t *ctx);                         /* dlt_plugins.c:434-438 */
 
 /* ---- batch entry point: a whole pcap image on the GPU ---------------------
  * tcpedit_batch_open copies `pcap` (a complete classic pcap file image,

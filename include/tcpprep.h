@@ -43,6 +43,9 @@ int tcpprep_time(tcpprep_hip_t *ctx, const void *pcap, size_t pcap_len, int iter
 /* multi-GPU shards (per-packet modes): the number of records before this shard, so
    --include/--exclude P: lists see global record numbers; 0 ok, -1 error */
 int tcpprep_set_pkt_base(tcpprep_hip_t *ctx, uint64_t pkt_base);
+/* the HIP device the context classifies on (hipSetDevice before staging; -1 = the calling
+   thread's current device, the default); 0 ok, -1 error */
+int tcpprep_set_device(tcpprep_hip_t *ctx, int device);
 /* cache entries (2-bit) the last tcpprep_cache_pcap wrote: the records, less MAC
    mode's short ones; a shard merge places the next shard's entries after them */
 int64_t tcpprep_last_entries(tcpprep_hip_t *ctx);

@@ -590,6 +590,13 @@ static int tpo_check_tree(const tpo_opt_t *o, int fam, const uint8_t *src)
  * (header + comment + packed 2-bit entries) into `out`.  Returns the cache
  * size, or -1 on an option error, -2 on a bad pcap, -3 if `cap` is too small.
  */
+static uint64_t tpo_pkt_base, tpo_last_entries;
+
+/* a shard's first global record number (0-based): P: lists keep global numbers */
+void tcpprep_oracle_set_pkt_base(uint64_t base) { tpo_pkt_base = base; }
+/* cache entries the last tcpprep_oracle_run wrote */
+uint64_t tcpprep_oracle_last_entries(void) { return tpo_last_entries; }
+
 long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, uint8_t *out, size_t cap)
 {
     static tpo_opt_t o;
@@ -634,7 +641,7 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
         off += 16 + caplen;
         packetnum++;
         int send = 1, dir = 0, add = 1; /* dir: 1 = C2S */
-        if (o.nlist && !!(o.xx_mode & XX_EXCLUDE) == tpo_check_list(&o, packetnum)) {
+        if (o.nlist && !!(o.xx_mode & XX_EXCLUDE) == tpo_check_list(&o, tpo_pkt_base + packetnum)) {
             send = 0; /* tcpprep.c:362-375 */
             goto ADD;
         }
@@ -706,5 +713,6 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
     out[22] = (uint8_t)(clen >> 8);
     out[23] = (uint8_t)clen;
     memcpy(out + 24, o.comment, clen);
+    tpo_last_entries = entries;
     return (long)(hdr + (entries + 3) / 4);
 }

@@ -68,6 +68,7 @@ struct tcpedit_batch_s {
     uint8_t *res_pinned;     /* pipeline slot: page-locked landing area of a run's counters, error
                                 words and wave-lane slots (a D2H into pageable memory would block) */
     uint64_t idx_cap_tiles, idx_cap_pkts;
+    uint8_t *one_img;        /* tcpedit_packet's staging: page-locked record image, then its output */
     uint64_t walk_end;       /* image offset where the record walk stopped ... */
     int walk_stop;           /* ... because: 0 bytes ran out, 1 libpcap's oversize stop, 2 a hard error */
     int kev_n;
@@ -695,6 +696,8 @@ void tcpedit_batch_close(tcpedit_batch_t *b)
     }
     if (b->res_pinned)
         hipHostFree(b->res_pinned);
+    if (b->one_img)
+        hipHostFree(b->one_img);
     if (b->idx_pinned) {
         hipHostFree(b->tiles);
         hipHostFree(b->pkt_rel);
@@ -760,6 +763,13 @@ int te_upload_cfg(tcpedit_t *t)
 {
     if (te_dev_ready(t) < 0)
         return -1;
+    if (t->cfg.fuzz_seed && te_fuzz_init_gen && t->cfg.fuzz_factor != te_fuzz_init_factor) {
+        t->cfg.fuzz_factor = te_fuzz_init_factor; /* fuzzing_init's factor (fuzzing.c:18) */
+        t->dev_dirty = 1;
+    }
+    if (t->cfg.fuzz_seed && t->fz_seeded &&
+        t->fz_gen != __atomic_load_n(&te_fuzz_init_gen, __ATOMIC_SEQ_CST))
+        t->dev_dirty = 1; /* a fuzzing_init since the last upload re-seeds the state */
     if (!t->dev_dirty && t->d_cfg)
         return 0;
     if (!t->d_cfg)
@@ -772,10 +782,19 @@ int te_upload_cfg(tcpedit_t *t)
                                  t->stream));
     }
     if (t->cfg.fuzz_seed) { /* fuzzing_init (fuzzing.c:12-20): the run-wide RNG state */
+        const uint64_t gen = __atomic_load_n(&te_fuzz_init_gen, __ATOMIC_SEQ_CST);
         if (!t->d_fuzz_words)
             HIPCHK(t, hipMalloc((void **)&t->d_fuzz_words, 4 * sizeof(uint32_t)));
-        const uint32_t w[4] = {t->cfg.fuzz_seed, t->cfg.fuzz_seed, 0, 0};
-        HIPCHK(t, hipMemcpyAsync(t->d_fuzz_words, w, sizeof(w), hipMemcpyHostToDevice, t->stream));
+        if (!t->fz_seeded || t->fz_gen != gen) {
+            /* seeded once per derivation (the tool's own fuzzing_init after post_args), and
+               again by every explicit fuzzing_init call -- not on other config uploads, so
+               the state carries across batches and tcpedit_packet calls */
+            const uint32_t s0 = gen ? te_fuzz_init_seed : t->cfg.fuzz_seed;
+            const uint32_t w[4] = {s0, s0, 0, 0};
+            HIPCHK(t, hipMemcpyAsync(t->d_fuzz_words, w, sizeof(w), hipMemcpyHostToDevice, t->stream));
+            t->fz_seeded = 1;
+            t->fz_gen = gen;
+        }
     }
     HIPCHK(t, hipStreamSynchronize(t->stream));
     t->dev_dirty = 0;
@@ -790,7 +809,7 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
 {
     if (!t || !pcap)
         return NULL;
-    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+    if (te_ensure_cfg(t) < 0)
         return NULL;
     tcpedit_batch_t *b = calloc(1, sizeof(*b));
     b->ctx = t;
@@ -1041,9 +1060,9 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         te_seterr(t, "device look-back timed out (%llu tiles)", (unsigned long long)b->err[2]);
         return TCPEDIT_ERROR;
     }
-    t->packetnum += b->counters[TE_CNT_PACKETS];
-    t->total_bytes += b->counters[TE_CNT_BYTES_OUT];
-    t->pkts_edited += b->counters[TE_CNT_EDITED];
+    t->pub.runtime.packetnum += b->counters[TE_CNT_PACKETS];
+    t->pub.runtime.total_bytes += b->counters[TE_CNT_BYTES_OUT];
+    t->pub.runtime.pkts_edited += b->counters[TE_CNT_EDITED];
     return TCPEDIT_OK;
 fail:
     return TCPEDIT_ERROR;
@@ -1495,9 +1514,9 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
         HIPCHK(t, hipMemcpyAsync(dst + *pos, b->d_out + 24, bytes, hipMemcpyDeviceToHost, P->s_d2h));
     HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
     *pos += bytes;
-    t->packetnum += b->counters[TE_CNT_PACKETS];
-    t->total_bytes += b->counters[TE_CNT_BYTES_OUT];
-    t->pkts_edited += b->counters[TE_CNT_EDITED];
+    t->pub.runtime.packetnum += b->counters[TE_CNT_PACKETS];
+    t->pub.runtime.total_bytes += b->counters[TE_CNT_BYTES_OUT];
+    t->pub.runtime.pkts_edited += b->counters[TE_CNT_EDITED];
     if (err_pkt >= 0) {
         te_seterr(t, "Error rewriting packets: packet %lld", (long long)(err_pkt + 1));
         t->pipe_err = 1;
@@ -1545,7 +1564,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         *out_len = 0;
     if (!t || !img || !dst || !out_len || out_cap < 24)
         return TCPEDIT_ERROR;
-    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+    if (te_ensure_cfg(t) < 0)
         return TCPEDIT_ERROR;
     if (in_len < 24) {
         te_seterr(t, "pcap image too short");
@@ -1739,13 +1758,11 @@ int tcpedit_init(tcpedit_t **out, int dlt)
     t->dlt = dlt;
     t->device = g_device;
     /* defaults until post_args (tcpedit.c:382-394) */
-    t->cfg.mtu = 1500;
-    t->cfg.tos = t->cfg.tclass = t->cfg.flowlabel = -1;
-    t->cfg.vlan_tag = 65535;
-    t->cfg.vlan_pri = t->cfg.vlan_cfi = 255;
-    t->cfg.vlan_proto = 0x8100;
-    t->fuzz_factor = 8;
+    te_cfg_defaults(&t->cfg, dlt);
+    t->fuzz_factor = 8; /* DEFAULT_FUZZ_FACTOR */
+    t->pub.runtime.dlt1 = t->pub.runtime.dlt2 = dlt;
     t->dev_dirty = 1;
+    te_sync_pub(t);
     if (dlt != 1) {
         te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: DLT_EN10MB)", dlt);
         return TCPEDIT_ERROR;
@@ -1753,24 +1770,58 @@ int tcpedit_init(tcpedit_t **out, int dlt)
     return TCPEDIT_OK;
 }
 
+/* parse_args.c:34-254.  The option source: the store (tcpedit_parse_args /
+ * tcpedit_set_option), else the calling tool's AutoOpts option set (te_autoopts.c),
+ * else the setters' values; with none of them there is nothing to derive from, and a
+ * run would silently apply no edits, so it is an error. */
 int tcpedit_post_args(tcpedit_t *t)
 {
     if (!t)
         return TCPEDIT_ERROR;
-    t->errstr[0] = 0;
+    t->pub.runtime.errstr[0] = 0;
+    if (!(t->opt_src & TE_SRC_STORE)) {
+        const int r = te_autoopts_import(t);
+        if (r < 0)
+            return TCPEDIT_ERROR;
+        if (r == 0) {
+            if (t->opt_src & TE_SRC_SETTERS) { /* the setter API (tcpedit_api.h) stands alone */
+                t->post_args_done = 1;
+                te_sync_pub(t);
+                return TCPEDIT_OK;
+            }
+            te_seterr(t, "tcpedit_post_args: no option source -- no AutoOpts option set "
+                         "(tcprewriteOptions/tcpreplayOptions/tcpbridgeOptions) in this process, and "
+                         "neither tcpedit_parse_args/tcpedit_set_option nor a tcpedit_set_* setter was called");
+            return TCPEDIT_ERROR;
+        }
+    }
     return te_derive_cfg(t) < 0 ? TCPEDIT_ERROR : TCPEDIT_OK;
+}
+
+/* the derivation a run needs, once: post_args, or (setter API) the setters' values as
+   they stand */
+int te_ensure_cfg(tcpedit_t *t)
+{
+    if (t->post_args_done)
+        return 0;
+    if ((t->opt_src & TE_SRC_SETTERS) && !(t->opt_src & TE_SRC_STORE)) {
+        t->post_args_done = 1;
+        te_sync_pub(t);
+        return 0;
+    }
+    return tcpedit_post_args(t) < 0 ? -1 : 0;
 }
 
 int tcpedit_validate(tcpedit_t *t)
 {
     if (!t)
         return TCPEDIT_ERROR;
-    t->validated = 1;
+    t->pub.validated = 1;
     return TCPEDIT_OK;
 }
 
-char *tcpedit_geterr(tcpedit_t *t) { return t ? t->errstr : NULL; }
-char *tcpedit_getwarn(tcpedit_t *t) { return t ? t->warnstr : NULL; }
+char *tcpedit_geterr(tcpedit_t *t) { return t ? t->pub.runtime.errstr : NULL; }
+char *tcpedit_getwarn(tcpedit_t *t) { return t ? t->pub.runtime.warnstr : NULL; }
 
 int tcpedit_checkerror(tcpedit_t *t, int rcode, const char *prefix)
 {
@@ -1794,7 +1845,7 @@ int tcpedit_get_output_dlt(tcpedit_t *t)
 {
     if (!t)
         return -1;
-    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+    if (te_ensure_cfg(t) < 0)
         return -1;
     return t->cfg.out_linktype; /* tcpedit_dlt_output_dlt (dlt_plugins.c:268-283) */
 }
@@ -1810,8 +1861,8 @@ int tcpedit_get_dev_cfg(tcpedit_t *t, void *out, size_t len, uint16_t *portlut)
     }
     return (int)sizeof(te_dev_cfg_t);
 }
-uint64_t tcpedit_get_total_bytes(tcpedit_t *t) { return t ? t->total_bytes : 0; }
-uint64_t tcpedit_get_pkts_edited(tcpedit_t *t) { return t ? t->pkts_edited : 0; }
+uint64_t tcpedit_get_total_bytes(tcpedit_t *t) { return t ? t->pub.runtime.total_bytes : 0; }
+uint64_t tcpedit_get_pkts_edited(tcpedit_t *t) { return t ? t->pub.runtime.pkts_edited : 0; }
 
 /* tcpedit_l3data / tcpedit_l3proto: L2 walk of an (un)edited frame; these are
  * the DLT plugins' l3 accessors (dlt_en10mb_get_layer3 / _proto), pure header
@@ -1881,52 +1932,181 @@ int tcpedit_l3proto(tcpedit_t *t, tcpedit_coder code, const unsigned char *packe
     (void)code;
     uint16_t pr;
     if (pktlen < 14 || host_l2(packet, pktlen, &pr) < 0)
-        return -1;
+        return 0xffff; /* ntohs(TCPEDIT_ERROR) (tcpedit.c:651) */
     return pr;
 }
 
-/* tcpedit_packet (tcpedit.c:46-366): one record through the GPU kernel. */
+/* ---- DLT plugin API (plugins_api.h:29-78) ---------------------------------- */
+int tcpedit_dlt_post_args(tcpedit_t *t) { return tcpedit_post_args(t); }
+
+tcpeditdlt_t *tcpedit_dlt_init(tcpedit_t *t, int srcdlt)
+{
+    if (!t)
+        return NULL;
+    if (srcdlt != 1) {
+        te_seterr(t, "No DLT plugin available for source DLT: 0x%x", srcdlt);
+        return NULL;
+    }
+    te_sync_pub(t);
+    return &t->dltc;
+}
+
+int tcpedit_dlt_post_init(tcpeditdlt_t *ctx) { return ctx ? TCPEDIT_OK : TCPEDIT_ERROR; }
+void tcpedit_dlt_cleanup(tcpeditdlt_t *ctx) { (void)ctx; /* owned by the tcpedit context */ }
+
+int tcpedit_dlt_output_dlt(tcpeditdlt_t *ctx)
+{
+    return ctx ? tcpedit_get_output_dlt(ctx->tcpedit) : -1;
+}
+
+int tcpedit_dlt_src(tcpeditdlt_t *ctx) { return ctx ? ctx->decoder_dlt : -1; }
+int tcpedit_dlt_dst(tcpeditdlt_t *ctx) { return ctx ? ctx->encoder_dlt : -1; }
+
+/* the L2 walks of the plugins this build decodes with (en10mb: get_l2len_protocol) */
+int tcpedit_dlt_l2len(tcpeditdlt_t *ctx, int dlt, const unsigned char *packet, const int pktlen)
+{
+    uint16_t pr;
+    if (!ctx || !packet)
+        return -1;
+    if (dlt != 1) {
+        te_seterr(ctx->tcpedit, "Unable to find plugin for DLT 0x%04x", dlt);
+        return -1;
+    }
+    const int l2 = pktlen < 14 ? -1 : host_l2(packet, pktlen, &pr);
+    if (l2 < 0 || pktlen < l2) {
+        te_seterr(ctx->tcpedit, "Packet length %d is to short to contain a layer 2 header for DLT 0x%04x", pktlen,
+                  dlt);
+        return -1;
+    }
+    return l2;
+}
+
+int tcpedit_dlt_proto(tcpeditdlt_t *ctx, int dlt, const unsigned char *packet, const int pktlen)
+{
+    uint16_t pr;
+    if (!ctx || !packet)
+        return -1;
+    if (dlt != 1) {
+        te_seterr(ctx->tcpedit, "Unable to find plugin for DLT 0x%04x", dlt);
+        return -1;
+    }
+    if (pktlen < 14 || host_l2(packet, pktlen, &pr) < 0)
+        return TCPEDIT_ERROR;
+    return (int)(uint16_t)((pr >> 8) | (pr << 8)); /* htons(ether_type) (en10mb.c:762) */
+}
+
+unsigned char *tcpedit_dlt_l3data(tcpeditdlt_t *ctx, int dlt, unsigned char *packet, const int pktlen)
+{
+    if (!ctx || dlt != 1)
+        return NULL;
+    return (unsigned char *)tcpedit_l3data(ctx->tcpedit, BEFORE_PROCESS, packet, pktlen);
+}
+
+/* tcpedit_packet's one-record batch, allocated once per context at the largest record
+ * (MAXPACKET, defines.h.in:177-182): no device allocation or free per call */
+#define TE_ONE_IN (24 + 16 + 262166 + 64)
+#define TE_ONE_OUT (24 + 16 + 262166 + 1024 + 64)
+static tcpedit_batch_t *one_ready(tcpedit_t *t)
+{
+    if (t->one)
+        return t->one;
+    if (te_dev_ready(t) < 0)
+        return NULL;
+    tcpedit_batch_t *b = calloc(1, sizeof(*b));
+    if (!b)
+        return NULL;
+    b->ctx = t;
+    b->idx_pinned = 1;
+    b->idx_cap_pkts = b->idx_cap_tiles = 2;
+    HIPCHK(t, hipHostMalloc((void **)&b->tiles, sizeof(te_tile_t) * 2, 0));
+    HIPCHK(t, hipHostMalloc((void **)&b->pkt_rel, sizeof(uint16_t) * 2, 0));
+    HIPCHK(t, hipHostMalloc((void **)&b->one_img, TE_ONE_IN + TE_ONE_OUT, 0));
+    HIPCHK(t, hipMalloc((void **)&b->d_in, TE_ONE_IN));
+    HIPCHK(t, hipMalloc((void **)&b->d_out, TE_ONE_OUT));
+    HIPCHK(t, hipMalloc((void **)&b->d_status, 16));
+    HIPCHK(t, hipMalloc((void **)&b->d_scratch, 262144 + 2048));
+    HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * 2));
+    HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * 2));
+    HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * 2));
+    b->ws_bytes = WS_SLOTS(1) + 64 + 32 * (uint64_t)te_wave_grid();
+    HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
+    HIPCHK(t, hipEventCreate(&b->ev0));
+    HIPCHK(t, hipEventCreate(&b->ev1));
+    t->one = b;
+    return b;
+fail:
+    tcpedit_batch_close(b);
+    return NULL;
+}
+
+/* tcpedit_packet (tcpedit.c:46-366): one record through the GPU kernel, staged
+ * through the context's page-locked one-record batch. */
 int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pktdata, tcpr_dir_t direction)
 {
     if (!t || !pkthdr || !*pkthdr || !pktdata || !*pktdata)
         return TCPEDIT_ERROR;
-    if (!t->post_args_done && tcpedit_post_args(t) < 0)
+    if (te_ensure_cfg(t) < 0)
         return TCPEDIT_ERROR;
     struct pcap_pkthdr *h = *pkthdr;
-    uint32_t caplen = h->caplen;
-    size_t img_len = 24 + 16 + caplen;
-    uint8_t *img = malloc(img_len);
+    const uint32_t caplen = h->caplen;
+    if (caplen > 262144u) {
+        te_seterr(t, "packet %llu: caplen %u exceeds MAX_SNAPLEN", (unsigned long long)t->pub.runtime.packetnum + 1,
+                  caplen);
+        return TCPEDIT_ERROR;
+    }
+    tcpedit_batch_t *b = one_ready(t);
+    if (!b)
+        return TCPEDIT_ERROR;
     static const uint8_t fh[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                    0x00, 0x00, 0x04, 0, 1, 0, 0, 0};
+    uint8_t *img = b->one_img, *res = b->one_img + TE_ONE_IN;
+    const size_t img_len = 24 + 16 + (size_t)caplen;
     memcpy(img, fh, 24);
-    uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
+    const uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
     memcpy(img + 24, rh, 16);
     memcpy(img + 40, *pktdata, caplen);
     uint8_t saved_skip = t->cfg.skip_soft_errors;
     t->cfg.skip_soft_errors = 0; /* tcpedit_packet itself never drops */
     t->dev_dirty |= saved_skip;
-    tcpedit_batch_t *b = tcpedit_batch_open(t, img, img_len, NULL, 0, t->packetnum);
-    free(img);
     int rc = TCPEDIT_ERROR;
-    if (!b)
+    /* a different record each call: no launch hint or placement carries over */
+    b->pkt_base = t->pub.runtime.packetnum;
+    b->launches = 0;
+    b->gen_hint_ok = 0;
+    b->grow_off = 0;
+    b->ran = 0;
+    if (index_image(t, b, img, img, img_len) < 0)
         goto out;
-    if (batch_run_dir(t, b, (int)direction) != TCPEDIT_OK)
-        goto out;
-    const uint8_t *st = tcpedit_batch_status(b);
-    if (!st)
-        goto out;
-    if (st[0] & TE_ST_UNSUPPORTED) {
-        te_seterr(t, "packet %llu: edit reads bytes past caplen (reference stale buffer, SURVEY Q8)",
-                  (unsigned long long)t->packetnum);
+    if (b->n_pkts != 1) {
+        te_seterr(t, "packet %llu: not a record", (unsigned long long)t->pub.runtime.packetnum + 1);
         goto out;
     }
-    switch (st[0] & TE_ST_RC_MASK) {
+    HIPCHK(t, hipMemcpyAsync(b->d_in, img, img_len, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t), hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream));
+    if (batch_run_dir(t, b, (int)direction) != TCPEDIT_OK)
+        goto out;
+    {
+        /* status byte and the output record in one round trip */
+        const uint64_t bound = 24 + b->out_cap < TE_ONE_OUT - 64 ? 24 + b->out_cap : TE_ONE_OUT - 64;
+        HIPCHK(t, hipMemcpyAsync(res, b->d_status, 1, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(res + 64, b->d_out, bound, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+    }
+    const uint8_t st = res[0];
+    if (st & TE_ST_UNSUPPORTED) {
+        te_seterr(t, "packet %llu: edit reads bytes past caplen (reference stale buffer, SURVEY Q8)",
+                  (unsigned long long)t->pub.runtime.packetnum);
+        goto out;
+    }
+    switch (st & TE_ST_RC_MASK) {
     case TE_ST_RC_ERROR:
-        te_seterr(t, "packet %llu: tcpedit error", (unsigned long long)t->packetnum);
+        te_seterr(t, "packet %llu: tcpedit error", (unsigned long long)t->pub.runtime.packetnum);
         rc = TCPEDIT_ERROR;
         goto out;
     case TE_ST_RC_SOFT:
-        te_seterr(t, "Packet %llu has no L3+ header or cannot be edited", (unsigned long long)t->packetnum);
+        te_seterr(t, "Packet %llu has no L3+ header or cannot be edited", (unsigned long long)t->pub.runtime.packetnum);
         rc = TCPEDIT_SOFT_ERROR;
         break;
     case TE_ST_RC_WARN:
@@ -1935,24 +2115,23 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
     default:
         rc = TCPEDIT_OK;
     }
-    if (st[0] & TE_ST_WARNED) {
-        te_setwarn(t, "packet %llu: checksum not recomputed", (unsigned long long)t->packetnum);
-        fprintf(stderr, "Warning: %s\n", t->warnstr);
+    if (st & TE_ST_WARNED) {
+        te_setwarn(t, "packet %llu: checksum not recomputed", (unsigned long long)t->pub.runtime.packetnum);
+        fprintf(stderr, "Warning: %s\n", t->pub.runtime.warnstr);
     }
     {
-        uint8_t rec[16];
         tcpedit_batch_result_t r;
         tcpedit_batch_result(b, &r);
         if (r.out_len >= 24 + 16) {
-            if (hipMemcpy(rec, b->d_out + 24, 16, hipMemcpyDeviceToHost) != hipSuccess)
-                goto out;
             uint32_t oc, ol;
-            memcpy(&oc, rec + 8, 4);
-            memcpy(&ol, rec + 12, 4);
-            if (oc > 262166u)
+            memcpy(&oc, res + 64 + 24 + 8, 4);
+            memcpy(&ol, res + 64 + 24 + 12, 4);
+            if (oc > 262166u || 40 + (uint64_t)oc > 24 + b->out_cap) {
+                te_seterr(t, "packet %llu: output record of %u bytes", (unsigned long long)t->pub.runtime.packetnum, oc);
+                rc = TCPEDIT_ERROR;
                 goto out;
-            if (hipMemcpy(*pktdata, b->d_out + 40, oc, hipMemcpyDeviceToHost) != hipSuccess)
-                goto out;
+            }
+            memcpy(*pktdata, res + 64 + 40, oc);
             h->caplen = oc;
             h->len = ol;
         } else {
@@ -1960,9 +2139,9 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
         }
     }
 out:
+fail:
     t->cfg.skip_soft_errors = saved_skip;
     t->dev_dirty |= saved_skip;
-    tcpedit_batch_close(b);
     return rc;
 }
 
@@ -1977,6 +2156,7 @@ int tcpedit_close(tcpedit_t **tp)
             free(t->stack[k][i]);
     }
     free(t->portlut);
+    tcpedit_batch_close(t->one);
     hipFree(t->d_cfg);
     hipFree(t->d_portlut);
     hipFree(t->d_fuzz_words);

@@ -66,7 +66,7 @@ void te_seterr(tcpedit_t *t, const char *fmt, ...)
 {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(t->errstr, sizeof(t->errstr), fmt, ap);
+    vsnprintf(t->pub.runtime.errstr, sizeof(t->pub.runtime.errstr), fmt, ap);
     va_end(ap);
 }
 
@@ -74,7 +74,7 @@ void te_setwarn(tcpedit_t *t, const char *fmt, ...)
 {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(t->warnstr, sizeof(t->warnstr), fmt, ap);
+    vsnprintf(t->pub.runtime.warnstr, sizeof(t->pub.runtime.warnstr), fmt, ap);
     va_end(ap);
 }
 
@@ -121,6 +121,7 @@ static int store(tcpedit_t *t, int k, const char *value)
         return -1;
     }
     t->have[k] = 1;
+    t->opt_src |= TE_SRC_STORE;
     free(t->arg[k]);
     t->arg[k] = value ? strdup(value) : NULL;
     t->post_args_done = 0;
@@ -144,6 +145,9 @@ int tcpedit_set_option(tcpedit_t *t, const char *name, const char *value)
 int tcpedit_parse_args(tcpedit_t *t, int argc, char **argv, int *unused)
 {
     int nun = 0;
+    if (!t)
+        return -1;
+    t->opt_src |= TE_SRC_STORE; /* even an empty command line is an option source */
     for (int i = 0; i < argc; i++) {
         const char *a = argv[i];
         int k = -1;
@@ -528,21 +532,82 @@ static void pm_sparse(tcpedit_t *t)
     }
 }
 
-int te_derive_cfg(tcpedit_t *t)
+/* tcpedit_init (tcpedit.c:371-403), dlt_en10mb_init (en10mb.c:117-122) and the
+ * encoder defaults of tcpedit_dlt_post_args (dlt_plugins.c:178-183: the decoder's) */
+void te_cfg_defaults(te_dev_cfg_t *c, int dlt)
 {
-    te_dev_cfg_t *c = &t->cfg;
-    long v;
-    uint32_t seed = 1, rnd = 0;
-
     memset(c, 0, sizeof(*c));
-    free(t->portlut);
-    t->portlut = NULL;
     c->mtu = 1500; /* DEFAULT_MTU (tcpedit.c:382) */
     c->tos = c->tclass = c->flowlabel = -1;
     c->vlan_tag = 65535; /* en10mb.c:117-122 */
     c->vlan_pri = 255;
     c->vlan_cfi = 255;
     c->vlan_proto = 0x8100;
+    c->encoder = TE_ENC_EN10MB;
+    c->out_linktype = dlt;
+    c->user_length = -1;
+    c->hdlc_address = c->hdlc_control = 65535;
+    c->fuzz_factor = 8; /* DEFAULT_FUZZ_FACTOR */
+}
+
+/* the DLT plugin ids of the encoders this build carries (plugins/dlt_*): the user
+ * plugin answers for DLT_USER0 (user.c:40), hdlc for DLT_C_HDLC (hdlc.c:40) */
+static int encoder_dlt(int enc) { return enc == TE_ENC_USER ? 147 : enc == TE_ENC_HDLC ? 104 : 1; }
+
+void te_sync_pub(tcpedit_t *t)
+{
+    tcpedit_ref_t *p = &t->pub;
+    const te_dev_cfg_t *c = &t->cfg;
+    p->dlt_ctx = &t->dltc;
+    t->dltc.tcpedit = t;
+    t->dltc.decoder_dlt = t->dlt;
+    t->dltc.encoder_dlt = encoder_dlt(c->encoder);
+    p->skip_broadcast = c->skip_broadcast != 0;
+    p->fixlen = (tcpedit_fixlen)c->fixlen;
+    p->editdir = TCPEDIT_EDIT_BOTH;
+    p->rewrite_ip = c->rewrite_ip != 0;
+    p->tcp_sequence_enable = c->tcp_sequence_enable;
+    p->tcp_sequence_adjust = c->tcp_sequence_adjust;
+    p->fixcsum = c->fixcsum != 0;
+    p->efcs = c->efcs != 0;
+    p->ttl_mode = (tcpedit_ttl_mode)c->ttl_mode;
+    p->ttl_value = (uint8_t)c->ttl_value;
+    p->tos = c->tos;
+    p->flowlabel = c->flowlabel;
+    p->tclass = c->tclass;
+    p->seed = c->seed;
+    p->mtu = c->mtu;
+    p->mtu_truncate = c->mtu_truncate != 0;
+    p->fuzz_seed = t->fuzz_seed;
+    p->fuzz_factor = t->fuzz_factor;
+    p->fixhdrlen = c->fixhdrlen != 0;
+}
+
+/* fuzzing_init (fuzzing.c:12-20): the process-wide seed and factor, applied to every
+ * context's device state before its next edit (te_upload_cfg) */
+uint64_t te_fuzz_init_gen;
+uint32_t te_fuzz_init_seed, te_fuzz_init_factor;
+
+void fuzzing_init(uint32_t fuzz_seed, uint32_t fuzz_factor)
+{
+    if (!fuzz_factor) { /* assert(_fuzz_factor) */
+        fprintf(stderr, "fuzzing_init: fuzz_factor must not be 0\n");
+        abort();
+    }
+    te_fuzz_init_seed = fuzz_seed;
+    te_fuzz_init_factor = fuzz_factor;
+    __atomic_add_fetch(&te_fuzz_init_gen, 1, __ATOMIC_SEQ_CST);
+}
+
+int te_derive_cfg(tcpedit_t *t)
+{
+    te_dev_cfg_t *c = &t->cfg;
+    long v;
+    uint32_t seed = 1, rnd = 0;
+
+    te_cfg_defaults(c, t->dlt);
+    free(t->portlut);
+    t->portlut = NULL;
     t->fuzz_seed = 0;
     t->fuzz_factor = 8;
 
@@ -691,7 +756,7 @@ int te_derive_cfg(tcpedit_t *t)
     if (t->have[OPT_ENDPOINTS]) {
         c->rewrite_ip = 1;
         if (!parse_endpoints(t, t->arg[OPT_ENDPOINTS])) {
-            if (!t->errstr[0])
+            if (!t->pub.runtime.errstr[0])
                 te_seterr(t, "Unable to parse --endpoints=%s", t->arg[OPT_ENDPOINTS]);
             return -1;
         }
@@ -702,18 +767,14 @@ int te_derive_cfg(tcpedit_t *t)
         te_seterr(t, "input DLT %d: only DLT_EN10MB (1) is supported by this build", t->dlt);
         return -1;
     }
-    c->encoder = TE_ENC_EN10MB;
-    c->out_linktype = 1; /* DLT_EN10MB */
-    c->user_length = -1;
-    c->hdlc_address = c->hdlc_control = 65535;
-    if (t->have[OPT_DLT]) {
+    if (t->have[OPT_DLT]) { /* tcpedit_dlt_getplugin_byname: the plugins' dlt_prefix names */
         if (strcmp(t->arg[OPT_DLT], "user") == 0) {
             c->encoder = TE_ENC_USER;
         } else if (strcmp(t->arg[OPT_DLT], "hdlc") == 0) {
             c->encoder = TE_ENC_HDLC;
             c->out_linktype = 104; /* DLT_C_HDLC */
-        } else if (strcmp(t->arg[OPT_DLT], "en10mb") != 0) {
-            te_seterr(t, "--dlt=%s: the en10mb, user and hdlc encoders are supported by this build", t->arg[OPT_DLT]);
+        } else if (strcmp(t->arg[OPT_DLT], "enet") != 0) {
+            te_seterr(t, "No output DLT plugin available for: %s (this build: enet, user, hdlc)", t->arg[OPT_DLT]);
             return -1;
         }
     }
@@ -857,20 +918,29 @@ int te_derive_cfg(tcpedit_t *t)
     c->skip_soft_errors = t->have[OPT_SKIP_SOFT_ERRORS] != 0;
     t->post_args_done = 1;
     t->dev_dirty = 1;
+    t->fz_seeded = 0; /* fuzzing_init (tcprewrite.c:103) follows post_args */
+    te_sync_pub(t);
     return 0;
 }
 
 /* ------------------------------------------------------------------------- */
 /* programmatic setters (tcpedit_api.c:33-353)                               */
 /* ------------------------------------------------------------------------- */
+static int setter_done(tcpedit_t *t)
+{
+    t->opt_src |= TE_SRC_SETTERS;
+    t->dev_dirty = 1;
+    te_sync_pub(t);
+    return TCPEDIT_OK;
+}
+
 #define SETFLAG(fn, field)                     \
-    int fn(tcpedit_t *t, int v)                \
+    int fn(tcpedit_t *t, bool v)               \
     {                                          \
         if (!t)                                \
             return TCPEDIT_ERROR;              \
         t->cfg.field = v ? 1 : 0;              \
-        t->dev_dirty = 1;                      \
-        return TCPEDIT_OK;                     \
+        return setter_done(t);                 \
     }
 SETFLAG(tcpedit_set_skip_broadcast, skip_broadcast)
 SETFLAG(tcpedit_set_fixcsum, fixcsum)
@@ -878,45 +948,40 @@ SETFLAG(tcpedit_set_fixhdrlen, fixhdrlen)
 SETFLAG(tcpedit_set_efcs, efcs)
 SETFLAG(tcpedit_set_mtu_truncate, mtu_truncate)
 
-int tcpedit_set_ttl_mode(tcpedit_t *t, int m)
+int tcpedit_set_ttl_mode(tcpedit_t *t, tcpedit_ttl_mode m)
 {
-    if (!t || m < 0 || m > 3)
+    if (!t || m < TCPEDIT_TTL_MODE_OFF || m > TCPEDIT_TTL_MODE_SUB)
         return TCPEDIT_ERROR;
     t->cfg.ttl_mode = m;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_ttl_value(tcpedit_t *t, uint8_t v)
 {
     if (!t)
         return TCPEDIT_ERROR;
     t->cfg.ttl_value = v;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_tos(tcpedit_t *t, uint8_t v)
 {
     if (!t)
         return TCPEDIT_ERROR;
     t->cfg.tos = v;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_tclass(tcpedit_t *t, uint8_t v)
 {
     if (!t)
         return TCPEDIT_ERROR;
     t->cfg.tclass = v;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_flowlabel(tcpedit_t *t, uint32_t v)
 {
     if (!t || v > 1048575)
         return TCPEDIT_ERROR;
     t->cfg.flowlabel = (int32_t)v;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_seed(tcpedit_t *t)
 {
@@ -924,29 +989,28 @@ int tcpedit_set_seed(tcpedit_t *t)
         return TCPEDIT_ERROR;
     t->cfg.seed = (uint32_t)random();
     t->cfg.rewrite_ip = 1;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_mtu(tcpedit_t *t, int mtu)
 {
     if (!t || mtu < 1 || mtu > 262144)
         return TCPEDIT_ERROR;
     t->cfg.mtu = mtu;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_maxpacket(tcpedit_t *t, int v)
 {
-    (void)v; /* tcpedit_t.maxpacket is set but never read on the edit path */
-    return t ? TCPEDIT_OK : TCPEDIT_ERROR;
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->pub.maxpacket = v; /* tcpedit_api.c:257-262: stored, never read on the edit path */
+    return TCPEDIT_OK;
 }
-int tcpedit_set_fixlen(tcpedit_t *t, int v)
+int tcpedit_set_fixlen(tcpedit_t *t, tcpedit_fixlen v)
 {
-    if (!t || v < 0 || v > 3)
+    if (!t || v < TCPEDIT_FIXLEN_OFF || v > TCPEDIT_FIXLEN_DEL)
         return TCPEDIT_ERROR;
     t->cfg.fixlen = v;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_tcp_sequence(tcpedit_t *t, uint32_t adjust)
 {
@@ -954,40 +1018,35 @@ int tcpedit_set_tcp_sequence(tcpedit_t *t, uint32_t adjust)
         return TCPEDIT_ERROR;
     t->cfg.tcp_sequence_enable = 1;
     t->cfg.tcp_sequence_adjust = adjust;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_cidrmap_s2c(tcpedit_t *t, char *s)
 {
     if (!t || !s || !parse_cidr_map(t, s, t->cfg.cidrmap2, &t->cfg.n_cidrmap2, "cidrmap"))
         return TCPEDIT_ERROR;
     t->cfg.rewrite_ip = 1;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_cidrmap_c2s(tcpedit_t *t, char *s)
 {
     if (!t || !s || !parse_cidr_map(t, s, t->cfg.cidrmap1, &t->cfg.n_cidrmap1, "cidrmap"))
         return TCPEDIT_ERROR;
     t->cfg.rewrite_ip = 1;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_srcip_map(tcpedit_t *t, char *s)
 {
     if (!t || !s || !parse_cidr_map(t, s, t->cfg.srcipmap, &t->cfg.n_srcipmap, "srcipmap"))
         return TCPEDIT_ERROR;
     t->cfg.rewrite_ip = 1;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_dstip_map(tcpedit_t *t, char *s)
 {
     if (!t || !s || !parse_cidr_map(t, s, t->cfg.dstipmap, &t->cfg.n_dstipmap, "dstipmap"))
         return TCPEDIT_ERROR;
     t->cfg.rewrite_ip = 1;
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
 }
 int tcpedit_set_port_map(tcpedit_t *t, char *s)
 {
@@ -1017,8 +1076,95 @@ int tcpedit_set_port_map(tcpedit_t *t, char *s)
     free(ents);
     t->cfg.has_portmap = 1;
     pm_sparse(t);
-    t->dev_dirty = 1;
-    return TCPEDIT_OK;
+    return setter_done(t);
+}
+
+/* tcpedit_set_encoder_dltplugin_byid/_byname (tcpedit_api.c:33-104): select the encoder
+ * once; the plugins this build carries are enet (DLT_EN10MB), user (DLT_USER0) and hdlc
+ * (DLT_C_HDLC) */
+static int set_encoder(tcpedit_t *t, int enc)
+{
+    static const char *names[] = {"enet", "user", "hdlc"};
+    if (t->encoder_set) {
+        te_seterr(t, "You have already selected a DLT encoder: %s", names[t->cfg.encoder]);
+        return TCPEDIT_ERROR;
+    }
+    t->encoder_set = 1;
+    t->cfg.encoder = enc;
+    t->cfg.out_linktype = enc == TE_ENC_HDLC ? 104 : enc == TE_ENC_USER ? t->dlt : 1;
+    return setter_done(t);
+}
+int tcpedit_set_encoder_dltplugin_byid(tcpedit_t *t, int dlt)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    const int enc = dlt == 1 ? TE_ENC_EN10MB : dlt == 147 ? TE_ENC_USER : dlt == 104 ? TE_ENC_HDLC : -1;
+    if (enc < 0) {
+        te_seterr(t, "No output DLT plugin decoder with DLT type: 0x%04x", dlt);
+        return TCPEDIT_ERROR;
+    }
+    return set_encoder(t, enc);
+}
+int tcpedit_set_encoder_dltplugin_byname(tcpedit_t *t, const char *name)
+{
+    if (!t || !name)
+        return TCPEDIT_ERROR;
+    const int enc = !strcmp(name, "enet") ? TE_ENC_EN10MB
+                    : !strcmp(name, "user") ? TE_ENC_USER
+                    : !strcmp(name, "hdlc") ? TE_ENC_HDLC : -1;
+    if (enc < 0) {
+        te_seterr(t, "No output DLT plugin available for: %s", name);
+        return TCPEDIT_ERROR;
+    }
+    return set_encoder(t, enc);
+}
+
+/* EN10MB plugin setters (plugins/dlt_en10mb/en10mb_api.c:38-192): they write the
+ * plugin config directly; set_mac adds the mask bit with `+=` as the reference does */
+int tcpedit_en10mb_set_mac(tcpedit_t *t, char *mac, tcpedit_mac_mask mask)
+{
+    if (!t || !mac)
+        return TCPEDIT_ERROR;
+    uint8_t a[6] = {0, 0, 0, 0, 0, 0};
+    mac_from_str(mac, a);
+    te_dev_cfg_t *c = &t->cfg;
+    switch (mask) {
+    case TCPEDIT_MAC_MASK_DMAC1: memcpy(c->intf1_dmac, a, 6); break;
+    case TCPEDIT_MAC_MASK_DMAC2: memcpy(c->intf2_dmac, a, 6); break;
+    case TCPEDIT_MAC_MASK_SMAC1: memcpy(c->intf1_smac, a, 6); break;
+    case TCPEDIT_MAC_MASK_SMAC2: memcpy(c->intf2_smac, a, 6); break;
+    default: return TCPEDIT_OK; /* the reference's switch has no other case */
+    }
+    c->mac_mask += (int32_t)mask;
+    return setter_done(t);
+}
+int tcpedit_en10mb_set_vlan_mode(tcpedit_t *t, tcpedit_vlan vlan)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.vlan = (int32_t)vlan;
+    return setter_done(t);
+}
+int tcpedit_en10mb_set_vlan_tag(tcpedit_t *t, uint16_t tag)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.vlan_tag = tag;
+    return setter_done(t);
+}
+int tcpedit_en10mb_set_vlan_priority(tcpedit_t *t, uint8_t priority)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.vlan_pri = priority;
+    return setter_done(t);
+}
+int tcpedit_en10mb_set_vlan_cfi(tcpedit_t *t, uint8_t cfi)
+{
+    if (!t)
+        return TCPEDIT_ERROR;
+    t->cfg.vlan_cfi = cfi;
+    return setter_done(t);
 }
 
 /* one CIDR (cidr2cidr, cidr.c:130-221) for tcpprep's option parser (tp_api.c) */

@@ -39,10 +39,23 @@ typedef struct {
 
 extern const te_optdef_t te_optdefs[OPT__N];
 
+/* the DLT plugin handle (plugins_types.h:100-131 tcpeditdlt_s, reduced to what the
+ * exported accessors answer: the selected decoder and encoder) */
+struct tcpeditdlt_s {
+    tcpedit_t *tcpedit;
+    int decoder_dlt;   /* input DLT */
+    int encoder_dlt;   /* the encoder plugin's DLT (DLT_USER0 for user) */
+};
+
+enum { TE_SRC_STORE = 1, TE_SRC_SETTERS = 2 }; /* where the options came from */
+
 struct tcpedit_s {
-    int validated;
+    tcpedit_ref_t pub;            /* the reference's tcpedit_t layout, kept in step (tcpedit.h) */
+    struct tcpeditdlt_s dltc;     /* pub.dlt_ctx points here */
     int dlt;                      /* input DLT */
     int device;
+    int opt_src;                  /* TE_SRC_* bits: the option store was filled / a setter ran */
+    int encoder_set;              /* an encoder was selected by tcpedit_set_encoder_dltplugin_* */
     /* option store (AutoOpts stand-in) */
     int have[OPT__N];
     char *arg[OPT__N];
@@ -53,10 +66,9 @@ struct tcpedit_s {
     uint16_t *portlut;            /* host copy, 65536 entries, or NULL */
     uint32_t fuzz_seed, fuzz_factor;
     int post_args_done;
-    /* runtime (tcpedit_runtime_t, tcpedit_types.h:49-61) */
-    uint64_t packetnum, total_bytes, pkts_edited;
-    char errstr[TE_ERRSTR_LEN];
-    char warnstr[TE_ERRSTR_LEN];
+    /* --fuzz-seed state seeding (fuzzing_init): the device word was seeded ... */
+    int fz_seeded;                /* ... since the last derivation ... */
+    uint64_t fz_gen;              /* ... under this fuzzing_init generation */
     /* device side */
     hipStream_t stream;
     te_dev_cfg_t *d_cfg;
@@ -69,11 +81,20 @@ struct tcpedit_s {
     int pipe_err;                 /* that call hit a hard error */
 };
 
+#define TE_ERR(t) ((t)->pub.runtime.errstr)
+#define TE_WARN(t) ((t)->pub.runtime.warnstr)
+
 void te_seterr(tcpedit_t *t, const char *fmt, ...);
 void te_setwarn(tcpedit_t *t, const char *fmt, ...);
 uint32_t te_tcpr_random(uint32_t *seed);
 int te_derive_cfg(tcpedit_t *t); /* tcpedit_post_args body */
 int te_upload_cfg(tcpedit_t *t);
+int te_ensure_cfg(tcpedit_t *t);  /* derive (or finalize setter values) once before a run */
+void te_cfg_defaults(te_dev_cfg_t *c, int dlt);
+void te_sync_pub(tcpedit_t *t);   /* mirror the derived values into the reference-layout head */
+int te_autoopts_import(tcpedit_t *t); /* 1 imported, 0 no descriptor, -1 error (te_autoopts.c) */
+extern uint64_t te_fuzz_init_gen; /* fuzzing_init calls so far, and their values */
+extern uint32_t te_fuzz_init_seed, te_fuzz_init_factor;
 typedef struct te_pipe_s te_pipe_t;
 void te_pipe_free(tcpedit_t *t);
 

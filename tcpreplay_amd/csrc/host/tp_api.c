@@ -26,6 +26,7 @@ struct tcpprep_hip_s {
     int nocomment, has_comment;
     int min_mask, max_mask; /* router mode's --minmask/--maxmask (validated only) */
     uint64_t last_entries;  /* cache entries the last tcpprep_cache_pcap wrote */
+    int device;             /* HIP device the classifier runs on (-1: the thread's current one) */
     char comment[8192]; /* the final "args\ncomment" string */
     char errstr[1024];
 };
@@ -53,6 +54,7 @@ int tcpprep_init(tcpprep_hip_t **out)
     t->cfg.ratio = 2.0; /* --ratio default, tcpprep_opts.def:511-516 */
     t->min_mask = 30;   /* defaults, tcpprep_opts.def:528-552 */
     t->max_mask = 8;
+    t->device = -1;
     *out = t;
     return 0;
 }
@@ -69,6 +71,14 @@ int tcpprep_close(tcpprep_hip_t **t)
 const char *tcpprep_geterr(tcpprep_hip_t *t) { return t ? t->errstr : NULL; }
 
 int64_t tcpprep_last_entries(tcpprep_hip_t *t) { return t ? (int64_t)t->last_entries : -1; }
+
+int tcpprep_set_device(tcpprep_hip_t *t, int device)
+{
+    if (!t || device < -1)
+        return -1;
+    t->device = device;
+    return 0;
+}
 
 int tcpprep_set_pkt_base(tcpprep_hip_t *t, uint64_t pkt_base)
 {
@@ -459,6 +469,8 @@ static int stage(tcpprep_hip_t *t, const void *pcap, size_t len, const tp_index_
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return tp_err(t, "no HIP device available: the tcpprep classifier runs on the GPU only");
+    if (t->device >= 0 && hipSetDevice(t->device) != hipSuccess)
+        return tp_err(t, "hipSetDevice(%d) failed", t->device);
     uint64_t n = x->n ? x->n : 1;
     if (hipMalloc((void **)&d->img, len) != hipSuccess || hipMalloc((void **)&d->out, (n + 3) / 4) != hipSuccess ||
         hipMalloc((void **)&d->off, n * 8) != hipSuccess || hipMalloc((void **)&d->caplen, n * 4) != hipSuccess ||

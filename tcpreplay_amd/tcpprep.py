@@ -26,6 +26,7 @@ def _lib():
                                          ctypes.POINTER(ctypes.c_uint64)]),
                 ("tcpprep_geterr", ctypes.c_char_p, [vp]),
                 ("tcpprep_set_pkt_base", c_int, [vp, ctypes.c_uint64]),
+                ("tcpprep_set_device", c_int, [vp, c_int]),
                 ("tcpprep_last_entries", ctypes.c_int64, [vp]),
                 ("tcpprep_close", c_int, [ctypes.POINTER(vp)])):
             f = getattr(L, name)
@@ -37,11 +38,14 @@ def _lib():
 class TcpPrep:
     """tcpprep_init + tcpprep_parse_args; cache(pcap) -> cache file bytes."""
 
-    def __init__(self, args):
+    def __init__(self, args, device=None):
         self._L = _lib()
         self._ctx = ctypes.c_void_p()
         if self._L.tcpprep_init(ctypes.byref(self._ctx)) != 0:
             raise MemoryError("tcpprep_init failed")
+        if device is not None and self._L.tcpprep_set_device(self._ctx, int(device)) != 0:
+            self.close()
+            raise ValueError(f"bad device {device}")
         argv = (ctypes.c_char_p * len(args))(*[a.encode() for a in args])
         if self._L.tcpprep_parse_args(self._ctx, len(args), argv) != 0:
             err = self.geterr()
@@ -94,23 +98,32 @@ def cache(pcap: bytes, args) -> bytes:
         tp.close()
 
 
-def gpu_classifier(image: bytes, args, pkt_base: int):
-    """one shard on the GPU -> (cache body bytes, entries)"""
-    tp = TcpPrep(args)
+def _local_rank():
+    import os
+    v = os.environ.get("LOCAL_RANK")
+    return int(v) if v is not None else None
+
+
+def gpu_classifier(image: bytes, args, pkt_base: int, device=None):
+    """one shard on the GPU (LOCAL_RANK's device by default, as gpu_editor) ->
+    (cache body bytes, entries, the cache comment)"""
+    tp = TcpPrep(args, device=_local_rank() if device is None else device)
     try:
         tp.set_pkt_base(pkt_base)
         c = tp.cache(image)
-        return c[24 + int.from_bytes(c[22:24], "big"):], tp.last_entries()
+        clen = int.from_bytes(c[22:24], "big")
+        return c[24 + clen:], tp.last_entries(), c[24:24 + clen]
     finally:
         tp.close()
 
 
 def merge_shards(parts, records: int, comment: bytes) -> bytes:
-    """(body, entries) per shard in file order -> one v04 cache file: the shards' 2-bit
-    entries concatenated (a shard's entry count need not be a multiple of 4)."""
+    """(body, entries[, comment]) per shard in file order -> one v04 cache file: the
+    shards' 2-bit entries concatenated (a shard's entry count need not be a multiple of 4)."""
     import numpy as np
     ents = []
-    for body, n in parts:
+    for part in parts:
+        body, n = part[0], part[1]
         b = np.frombuffer(body, np.uint8)
         e = ((b[:, None] >> np.array([0, 2, 4, 6], np.uint8)) & 3).reshape(-1)[:n]
         ents.append(e)
@@ -124,7 +137,8 @@ def merge_shards(parts, records: int, comment: bytes) -> bytes:
 
 
 def comment_of(args) -> bytes:
-    """the cache comment the options give (read back from a one-record probe run)"""
+    """the cache comment the options give (read back from a one-record probe run; only
+    for classifiers that do not return it)"""
     from . import synth
     tp = TcpPrep(args)
     try:
@@ -134,22 +148,51 @@ def comment_of(args) -> bytes:
     return c[24:24 + int.from_bytes(c[22:24], "big")]
 
 
+def _is_auto(args) -> bool:
+    return any(a == "-a" or a.startswith("--auto") for a in args)
+
+
 def prep_distributed(pcap: bytes, args, dist=None, classifier=None, comment: bytes = None):
     """Sharded tcpprep (per-packet modes): each rank classifies its byte-balanced record
     range (tcpedit_pcap_shards) with its global record base, one all_gather_object of
-    (body, entries) per rank, every rank assembles the same cache file.  With dist=None
-    all shards run in this process (one per 'rank' of a 2-way plan)."""
+    (ok, (body, entries[, comment]) or error) per rank, every rank assembles the same
+    cache file -- or every rank raises the same error.  With dist=None all shards run in
+    this process (one per 'rank' of a 2-way plan).
+
+    Decisions that end the job are taken identically on every rank before the collective
+    (--auto does not shard, an empty capture is the reference's "No packets were
+    processed"), and a classifier failure on one rank travels in the gathered tuple, so no
+    rank is left waiting in the collective."""
     from .dist import plan
     classifier = classifier or gpu_classifier
     world = dist.get_world_size() if dist else 2
+    if world > 1 and _is_auto(args):
+        raise ValueError("--auto classifies by the whole capture's host table: it does not shard")
     p = plan(pcap, world)
+    if p.total == 0:
+        raise ValueError("No packets were processed.  Filter too limiting?")
+
+    def run(k):
+        if p.count(k) == 0:  # a shard holding only the file header (fewer records than ranks)
+            return (b"", 0, None)
+        return classifier(p.image(pcap, k), args, p.pkt_base[k])
+
     if dist:
         r = dist.get_rank()
-        mine = classifier(p.image(pcap, r), args, p.pkt_base[r])
-        parts = [None] * world
-        dist.all_gather_object(parts, mine)
+        try:
+            mine = (True, run(r))
+        except Exception as e:  # noqa: BLE001 -- reported on every rank below
+            mine = (False, f"rank {r}: {e}")
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        errs = [m[1] for m in got if not m[0]]
+        if errs:
+            raise RuntimeError("; ".join(errs))
+        parts = [m[1] for m in got]
     else:
-        parts = [classifier(p.image(pcap, k), args, p.pkt_base[k]) for k in range(world)]
+        parts = [run(k) for k in range(world)]
+    if comment is None:
+        comment = next((pt[2] for pt in parts if len(pt) > 2 and pt[2] is not None), None)
     if comment is None:
         comment = comment_of(args)
     return merge_shards(parts, p.total, comment)

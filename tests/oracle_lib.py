@@ -77,9 +77,14 @@ def rewrite_skipping(pcap: bytes, args, cache: bytes = None, skip: int = 0):
         lib.oracle_set_fuzz_skip(0)
 
 
-def tcpprep(pcap: bytes, args):
-    """tcpprep_oracle_run: the CPU restatement of tcpprep's per-packet modes -> cache file bytes."""
+def tcpprep(pcap: bytes, args, pkt_base: int = 0, with_entries=False):
+    """tcpprep_oracle_run: the CPU restatement of tcpprep's per-packet modes -> cache file
+    bytes (and the entry count).  pkt_base = a shard's first global record number."""
     lib = load()
+    lib.tcpprep_oracle_set_pkt_base.argtypes = [ctypes.c_uint64]
+    lib.tcpprep_oracle_set_pkt_base.restype = None
+    lib.tcpprep_oracle_last_entries.restype = ctypes.c_uint64
+    lib.tcpprep_oracle_set_pkt_base(int(pkt_base))
     fn = lib.tcpprep_oracle_run
     fn.restype = ctypes.c_long
     fn.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p, ctypes.c_size_t,
@@ -88,6 +93,9 @@ def tcpprep(pcap: bytes, args):
     cap = 24 + 8192 + len(pcap) // 16 + 64
     out = ctypes.create_string_buffer(cap)
     n = fn(len(args), argv, pcap, len(pcap), out, cap)
+    lib.tcpprep_oracle_set_pkt_base(0)
     if n < 0:
         raise ValueError(f"tcpprep oracle failed ({n}) for {args}")
+    if with_entries:
+        return out.raw[:n], int(lib.tcpprep_oracle_last_entries())
     return out.raw[:n]
