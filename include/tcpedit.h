@@ -234,6 +234,9 @@ typedef struct {
     uint32_t fast_lane;       /* 1: the register-resident fast lane ran (size-preserving config) */
     uint32_t generic_tiles;   /* tiles the generic lane edited (all of them without the fast lane) */
     uint32_t fast_kind;       /* fast-lane kernel: 1 te_fast_tiles (block per tile), 2 te_wave_tiles (wave per tile) */
+    uint64_t stale_records;   /* written records whose edit read the reference's stale static buffer
+                                 (SURVEY Q8), reproduced by the device replay (`unsupported`: those it
+                                 could not reproduce -- the run then fails) */
 } tcpedit_batch_result_t;
 
 tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *tcpedit, const void *pcap, size_t len, const void *cache,

@@ -31,7 +31,7 @@ class BatchResult(ctypes.Structure):
                  "unsupported", "out_len")] + [
         ("first_error", ctypes.c_int64), ("first_unsupported", ctypes.c_int64), ("n_tiles", ctypes.c_uint32),
         ("kernel_ms", ctypes.c_double), ("fast_lane", ctypes.c_uint32), ("generic_tiles", ctypes.c_uint32),
-        ("fast_kind", ctypes.c_uint32)]
+        ("fast_kind", ctypes.c_uint32), ("stale_records", ctypes.c_uint64)]
 
 FAST_KERNELS = {1: "te_fast_tiles", 2: "te_wave_tiles"}
 

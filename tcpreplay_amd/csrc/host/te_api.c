@@ -69,6 +69,11 @@ struct tcpedit_batch_s {
                                 words and wave-lane slots (a D2H into pageable memory would block) */
     uint64_t idx_cap_tiles, idx_cap_pkts;
     uint8_t *one_img;        /* tcpedit_packet's staging: page-locked record image, then its output */
+    /* stale static-buffer reads: the edit's list of records to replay */
+    uint8_t *d_q8;           /* q8_cap entries of 16 bytes */
+    uint32_t q8_cap;
+    int q8_defer;            /* tcpedit_packet replays itself, over the caller's buffer */
+    uint8_t *d_q8_init;      /* tcpedit_packet: the caller's buffer bytes [0, need) */
     uint64_t walk_end;       /* image offset where the record walk stopped ... */
     int walk_stop;           /* ... because: 0 bytes ran out, 1 libpcap's oversize stop, 2 a hard error */
     int kev_n;
@@ -96,6 +101,8 @@ struct tcpedit_batch_s {
     int ran;
 };
 
+#define TE_Q8_CAP 65536u   /* stale-read records one batch may list for replay (more fail loudly) */
+#define TE_Q8_THREADS 256u /* replay threads (scratch: te_q8_slot_bytes() each, per context) */
 #define WS_ERR 0
 #define WS_ZERO 0
 #define WS_TICKET 24
@@ -669,6 +676,9 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_ws);
     hipFree(b->d_tile_list);
     hipFree(b->d_fuzz);
+    hipFree(b->d_q8);
+    hipFree(b->d_q8_init);
+    b->d_q8 = b->d_q8_init = NULL;
     b->d_fuzz = NULL;
     b->fuzz_cap = 0;
     b->d_tile_list = NULL;
@@ -840,6 +850,8 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream)); /* the list count starts at 0 */
     if (b->fast_tiles)
         HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->n_tiles + 1)));
+    b->q8_cap = (uint32_t)(b->n_pkts < TE_Q8_CAP ? b->n_pkts + 1 : TE_Q8_CAP);
+    HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * (size_t)b->q8_cap));
     if (cache) {
         const uint8_t *cd;
         if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &b->dirbits_len) < 0)
@@ -935,6 +947,8 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.ev_k0 = k0;
     L.ev_k1 = k1;
     L.generic_only = generic_only;
+    L.q8_list = b->d_q8;
+    L.q8_cap = b->d_q8 ? b->q8_cap : 0;
     /* wave lane: this batch's previous run under this config listed nothing, so the
        generic pass is left out (batch_run_dir runs it after all if a run does list) */
     L.skip_generic = !generic_only && L.fast && b->fast_kind == TE_FAST_WAVE && b->gen_hint_ok &&
@@ -977,6 +991,55 @@ static void out_header(const tcpedit_t *t, uint8_t *h)
     memcpy(h, base, 24);
     const uint32_t lt = (uint32_t)t->cfg.out_linktype;
     memcpy(h + 20, &lt, 4);
+}
+
+/* te_q8_replay over what the last launch of `b` listed, on `st`.
+ * file_start: the batch's first record is the capture's first (the reference's buffer
+ * starts zeroed there); init: the initial buffer instead (tcpedit_packet). */
+static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_start, const uint8_t *d_init,
+                  uint32_t init_len, hipStream_t st)
+{
+    if (!t->d_q8_scratch) {
+        if (hipMalloc((void **)&t->d_q8_scratch, (size_t)TE_Q8_THREADS * te_q8_slot_bytes()) != hipSuccess) {
+            t->d_q8_scratch = NULL;
+            te_seterr(t, "out of device memory (stale-buffer replay scratch)");
+            return -1;
+        }
+    }
+    te_launch_t L;
+    memset(&L, 0, sizeof(L));
+    L.cfg = t->d_cfg;
+    L.cfg_host = &t->cfg;
+    L.portlut = t->cfg.has_portmap ? t->d_portlut : NULL;
+    L.dirbits = b->d_dirbits;
+    L.dirbits_len = b->dirbits_len;
+    L.pkt_base = b->pkt_base;
+    L.fixed_dir = fixed_dir;
+    L.in = b->d_in;
+    L.tiles = b->d_tiles;
+    L.pkt_rel = b->d_pkt_rel;
+    L.n_tiles = (uint32_t)b->n_tiles;
+    L.in_swapped = (uint32_t)b->swapped;
+    L.in_nsec = (uint32_t)b->nsec;
+    L.out = b->d_out;
+    L.out_base = 24;
+    L.status = b->d_status;
+    L.counters = (uint64_t *)(b->d_ws + b->last_cnt_off);
+    L.err = (uint64_t *)(b->d_ws + WS_ERR);
+    L.q8_list = b->d_q8;
+    L.q8_cap = b->q8_cap;
+    L.q8_scratch = t->d_q8_scratch;
+    L.q8_threads = TE_Q8_THREADS;
+    L.q8_file_start = file_start;
+    L.q8_init = d_init;
+    L.q8_init_len = init_len;
+    if (t->cfg.fuzz_seed && b->d_fuzz && !b->last_fast)
+        L.fuzz_states = b->d_fuzz;
+    if (te_launch_q8(&L, st) != 0) {
+        te_seterr(t, "stale-buffer replay launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -1;
+    }
+    return 0;
 }
 
 static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
@@ -1037,6 +1100,14 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
         b->last_skipped = 0;
+    }
+    if (b->counters[TE_CNT_UNSUPPORTED] && !b->q8_defer) {
+        /* records whose edit read the reference's stale static buffer: replay them */
+        if (run_q8(t, b, fixed_dir, b->pkt_base == 0, NULL, 0, t->stream) < 0)
+            return TCPEDIT_ERROR;
+        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
     }
     for (int i = 0; i < b->last_fgrid; i++) { /* the wave lane's per-block totals */
         const uint64_t *v = b->slots_host + 4 * (size_t)i;
@@ -1146,7 +1217,7 @@ int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
         return TCPEDIT_ERROR;
     if (batch_run_dir(t, b, -1) != TCPEDIT_OK)
         return TCPEDIT_ERROR;
-    if (b->counters[TE_CNT_UNSUPPORTED]) {
+    if (b->counters[TE_CNT_Q8_FAILED]) {
         const uint8_t *st = tcpedit_batch_status(b);
         int64_t first = -1;
         for (uint64_t i = 0; st && i < b->n_pkts; i++)
@@ -1155,8 +1226,9 @@ int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
                 break;
             }
         te_seterr(t,
-                  "record %lld: its edit reads bytes past caplen, i.e. the reference's stale static packet "
-                  "buffer (SURVEY Appendix B Q8); not supported by the device path",
+                  "record %lld: its edit reads the reference's stale static packet buffer (SURVEY Appendix B "
+                  "Q8) at bytes the device replay cannot reconstruct (they come from before this batch, or "
+                  "from bytes no record wrote)",
                   (long long)(first + 1 + (int64_t)b->pkt_base));
         return TCPEDIT_ERROR;
     }
@@ -1181,7 +1253,8 @@ int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r)
     r->soft_errors = b->counters[TE_CNT_SOFT];
     r->warnings = b->counters[TE_CNT_WARN];
     r->errors = b->counters[TE_CNT_ERROR];
-    r->unsupported = b->counters[TE_CNT_UNSUPPORTED];
+    r->unsupported = b->counters[TE_CNT_Q8_FAILED];
+    r->stale_records = b->counters[TE_CNT_UNSUPPORTED];
     r->first_error = b->err[0] != ~0ull ? (int64_t)b->err[0] : -1;
     r->first_unsupported = -1;
     if (r->unsupported) {
@@ -1408,6 +1481,8 @@ static tcpedit_batch_t *pipe_slot_open(tcpedit_t *t, size_t chunk)
     HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (b->idx_cap_tiles + 1)));
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->idx_cap_pkts + 1)));
     HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->idx_cap_tiles + 1)));
+    b->q8_cap = (uint32_t)(b->idx_cap_pkts < TE_Q8_CAP ? b->idx_cap_pkts : TE_Q8_CAP);
+    HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * (size_t)b->q8_cap));
     HIPCHK(t, hipMalloc((void **)&b->d_ws, WS_SLOTS(b->idx_cap_tiles) + 64 + 32 * (uint64_t)te_wave_grid()));
     HIPCHK(t, hipHostMalloc((void **)&b->res_pinned, TE_RES_SLOTS + 32 * (uint64_t)te_wave_grid(), 0));
     HIPCHK(t, hipEventCreate(&b->ev0));
@@ -1492,9 +1567,9 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
         te_seterr(t, "device look-back timed out (%llu tiles)", (unsigned long long)b->err[2]);
         return -1;
     }
-    if (b->counters[TE_CNT_UNSUPPORTED]) {
-        te_seterr(t, "a record's edit reads bytes past caplen, i.e. the reference's stale static packet buffer "
-                     "(SURVEY Appendix B Q8); not supported by the device path");
+    if (b->counters[TE_CNT_Q8_FAILED]) {
+        te_seterr(t, "a record's edit reads the reference's stale static packet buffer (SURVEY Appendix B Q8) "
+                     "at bytes written by an earlier pipeline chunk or by no record: not reproducible here");
         return -1;
     }
     uint64_t bytes = b->counters[TE_CNT_BYTES_OUT];
@@ -1685,6 +1760,10 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
             goto fail_drain;
         }
+        /* stale static-buffer reads (Q8): the replay kernel reads the listed count on the
+           device and returns at once when it is 0; chunk 0 starts at the capture's start */
+        if (run_q8(t, b, -1, pkts == 0, NULL, 0, t->stream) < 0)
+            goto fail_drain;
         HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws + b->last_cnt_off, sizeof(b->counters),
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_ERR, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost,
@@ -2028,6 +2107,10 @@ static tcpedit_batch_t *one_ready(tcpedit_t *t)
     HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * 2));
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * 2));
     HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * 2));
+    b->q8_cap = 2;
+    b->q8_defer = 1;
+    HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * 2));
+    HIPCHK(t, hipMalloc((void **)&b->d_q8_init, 262144 + 64));
     b->ws_bytes = WS_SLOTS(1) + 64 + 32 * (uint64_t)te_wave_grid();
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
     HIPCHK(t, hipEventCreate(&b->ev0));
@@ -2094,9 +2177,23 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
         HIPCHK(t, hipMemcpyAsync(res + 64, b->d_out, bound, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
     }
+    if (res[0] & TE_ST_UNSUPPORTED) {
+        /* the edit read past caplen: in tcpedit_packet the reference reads the caller's own
+           buffer there, so replay over the caller's bytes [0, need) */
+        uint32_t ent[4];
+        HIPCHK(t, hipMemcpy(ent, b->d_q8, 16, hipMemcpyDeviceToHost));
+        const uint32_t need = ent[1] > 262144u ? 262144u : ent[1];
+        HIPCHK(t, hipMemcpyAsync(b->d_q8_init, *pktdata, need, hipMemcpyHostToDevice, t->stream));
+        if (run_q8(t, b, (int)direction, 1, b->d_q8_init, need, t->stream) < 0)
+            goto out;
+        const uint64_t bound = 24 + b->out_cap < TE_ONE_OUT - 64 ? 24 + b->out_cap : TE_ONE_OUT - 64;
+        HIPCHK(t, hipMemcpyAsync(res, b->d_status, 1, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(res + 64, b->d_out, bound, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+    }
     const uint8_t st = res[0];
     if (st & TE_ST_UNSUPPORTED) {
-        te_seterr(t, "packet %llu: edit reads bytes past caplen (reference stale buffer, SURVEY Q8)",
+        te_seterr(t, "packet %llu: the edit reads bytes past caplen the replay cannot reproduce (SURVEY Q8)",
                   (unsigned long long)t->pub.runtime.packetnum);
         goto out;
     }
@@ -2160,6 +2257,7 @@ int tcpedit_close(tcpedit_t **tp)
     hipFree(t->d_cfg);
     hipFree(t->d_portlut);
     hipFree(t->d_fuzz_words);
+    hipFree(t->d_q8_scratch);
     te_pipe_free(t);
     if (t->stream)
         hipStreamDestroy(t->stream);

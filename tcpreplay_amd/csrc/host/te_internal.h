@@ -74,6 +74,7 @@ struct tcpedit_s {
     te_dev_cfg_t *d_cfg;
     uint16_t *d_portlut;
     uint32_t *d_fuzz_words;       /* --fuzz-seed: [0] the running RNG state (te_launch_t.fuzz_words) */
+    uint8_t *d_q8_scratch;        /* te_q8_replay's emulated static buffers (allocated on first use) */
     int dev_dirty;                /* cfg changed since last upload */
     uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */

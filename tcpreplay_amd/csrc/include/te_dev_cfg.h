@@ -94,7 +94,8 @@ enum {
     TE_ST_RC_ERROR = 3,
     TE_ST_DROPPED = 0x04,     /* soft error suppressed by --skip-soft-errors */
     TE_ST_NOSEND = 0x08,      /* cache said NOSEND: written unedited */
-    TE_ST_UNSUPPORTED = 0x10, /* output would depend on bytes outside the packet */
+    TE_ST_UNSUPPORTED = 0x10, /* output depends on stale static-buffer bytes: fixed by
+                                 te_q8_replay, or (still set after it) not reproducible */
     TE_ST_WARNED = 0x20,      /* a checksum warning was emitted (tcpedit.c:351-353) */
     TE_ST_ZEROCAP = 0x40,     /* caplen 0 after editing: not written (tcprewrite.c:367) */
 };
@@ -109,7 +110,8 @@ enum {
     TE_CNT_SOFT,
     TE_CNT_WARN,
     TE_CNT_ERROR,
-    TE_CNT_UNSUPPORTED,
+    TE_CNT_UNSUPPORTED,   /* written records whose edit read stale static-buffer bytes (Q8) */
+    TE_CNT_Q8_FAILED,     /* ... that te_q8_replay could not reproduce (the batch fails) */
     TE_CNT__N
 };
 

@@ -121,6 +121,15 @@ typedef struct {
                                  [2] records of the launch that reached the fuzz step */
     uint32_t n_pkts;          /* records in the launch */
     int fuzz_probe_only;      /* count the reaching records (words[2]) and stop: no edit, no state change */
+    /* stale static-buffer reads: the edit lists such written records here as
+       {record, bytes needed, output offset lo, hi}; te_launch_q8 replays them */
+    void *q8_list;            /* device: q8_cap x 16 bytes, or NULL */
+    uint32_t q8_cap;
+    void *q8_scratch;         /* device: q8_threads x te_q8_slot_bytes() */
+    uint32_t q8_threads;      /* a multiple of 64 */
+    int q8_file_start;        /* the launch's first record is the capture's first (buffer starts zeroed) */
+    const uint8_t *q8_init;   /* device: the initial buffer instead of zeros (tcpedit_packet), or NULL */
+    uint32_t q8_init_len;
 } te_launch_t;
 
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */
@@ -129,7 +138,9 @@ int te_wave_grid(void);
 
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(te_launch_t *L, hipStream_t stream);
+int te_launch_q8(te_launch_t *L, hipStream_t stream);
 #endif
+uint64_t te_q8_slot_bytes(void);
 
 #ifdef __cplusplus
 }

@@ -59,7 +59,35 @@ struct Pkt {
     u32 phys;     // bytes from d that hold what the reference's buffer holds (its physical extent)
     u32 avail;    // bytes from d this lane may write (>= phys; slot tail or nothing)
     bool unsupported;
+    u32 need;     // unsupported: the reference's buffer bytes [0, need) from d decide the output
+    u32 ext;      // bytes from d the reference's buffer holds for this packet (its memcpy, the
+                  // encoder's memmove, --fixlen=pad, fuzz writes): te_q8_replay's buffer view
+    bool strict;  // te_q8_replay: a fuzz XOR of a byte past `phys` is a stale read too
 };
+
+// a read of bytes [.., end) from d that lie past the packet's physical bytes: the
+// reference reads its static buffer there.  The record is
+// flagged; te_q8_replay reproduces it over an emulated static buffer.
+DI void stale(Pkt &pk, int end) {
+    pk.unsupported = true;
+    if (end > (int)pk.need) pk.need = (u32)end;
+}
+// a record the replay cannot reproduce either (slot headroom, not stale bytes)
+constexpr u32 NEED_NEVER = 0xffffffffu;
+
+// te_q8_replay (pk.strict): the packet start moved from old_d to pk.d (an L2 push, pop
+// or replacement moves the head here, where the reference memmove's the rest).  Bring
+// the buffer bytes past the packet's new extent along, so that pk.d + x is the
+// reference's buffer offset x past the packet too: its memmove leaves them in place.
+DI void strict_tail(Pkt &pk, const u8 *old_d) {
+    if (!pk.strict) return;
+    const u32 V = pk.phys;  // known bytes, in the old coordinates (phys not yet adjusted)
+    if (pk.d < old_d)
+        for (u32 x = pk.ext; x < V; ++x) pk.d[x] = old_d[x];
+    else
+        for (u32 x = V; x-- > pk.ext;) pk.d[x] = old_d[x];
+    pk.phys = V > pk.ext ? V : pk.ext;
+}
 
 struct Dec {  // tcpeditdlt_t + en10mb_extra_t fields the encode/merge steps read
     u8 dstaddr[6], srcaddr[6];
@@ -368,21 +396,21 @@ DI u32 remap_ipv4(const te_dev_cfg_t &cfg, const te_cidr_t &c, u32 orig) {
 
 // remap_ipv6 (edit_packet.c:748-779) incl. its out-of-range write for
 // non-octet masks, with x86's 5-bit shift-count masking.
-// `addr_off` is the address offset from `base`; returns false if the stray
-// write would land outside the materialised slot.
-DI bool remap_ipv6(const te_dev_cfg_t &cfg, const te_cidr_t &c, u8 *addr, int room_after_addr) {
-    if (c.family != 6) return true;
-    if (cfg.skip_broadcast && mcast6(addr)) return true;
+// Returns 0, or (the stray write would land past `room_after_addr`, the packet's
+// physical bytes) 1 + the offset from addr it reads and writes.
+DI int remap_ipv6(const te_dev_cfg_t &cfg, const te_cidr_t &c, u8 *addr, int room_after_addr) {
+    if (c.family != 6) return 0;
+    if (cfg.skip_broadcast && mcast6(addr)) return 0;
     u32 j = (u32)c.masklen / 8;
     for (u32 i = 0; i < j; ++i) addr[i] = c.network6[i];
     u32 k = (u32)c.masklen % 8;
-    if (k == 0) return true;
+    if (k == 0) return 0;
     k = ~0u << (8 - k);
     u32 i = addr[j] & k;
-    if ((int)i >= room_after_addr) return false;
+    if ((int)i >= room_after_addr) return 1 + (int)i;
     u32 s1 = (8u - k) & 31u, s2 = k & 31u;
     addr[i] = (u8)((c.network6[j] & (0xffu << s1)) | (addr[i] & (0xffu >> s2)));
-    return true;
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -408,7 +436,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
     const int ipoff = (int)(ip - pk.d);
     auto readable = [&](int nbytes) -> int {  // bytes past `phys` are the reference's stale buffer
         int lim = (int)pk.phys - (ipoff + ip_hl);
-        if (nbytes > lim) pk.unsupported = true;
+        if (nbytes > lim) stale(pk, ipoff + ip_hl + nbytes);
         return nbytes <= lim ? nbytes : (lim < 0 ? 0 : lim);
     };
     u8 *l4 = ip + ip_hl;
@@ -417,7 +445,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         case 6:
         case 44: {  // IPPROTO_TCP, IPPROTO_TCP_V6FRAG (tcpr.h:655)
             if (len < 20) return RC_WARN;
-            if (ipoff + ip_hl + 18 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 18 > (int)pk.phys) { stale(pk, ipoff + ip_hl + 18); return RC_OK; }
             st16(l4 + 16, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
             sum += bswap16((u16)(6 + len));
@@ -427,7 +455,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 17: {
             if (len < 8) return RC_WARN;
-            if (ipoff + ip_hl + 8 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 8 > (int)pk.phys) { stale(pk, ipoff + ip_hl + 8); return RC_OK; }
             if (ld16(l4 + 6) == 0) break;
             st16(l4 + 6, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
@@ -438,7 +466,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 1: {
             if (len < 4) return RC_WARN;
-            if (ipoff + ip_hl + 4 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 4 > (int)pk.phys) { stale(pk, ipoff + ip_hl + 4); return RC_OK; }
             st16(l4 + 2, 0);
             if (v6) {
                 // CHECKSUM_CARRY assigns its argument; the interim value lands in
@@ -454,7 +482,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
         }
         case 58: {
             if (len < 8) return RC_WARN;
-            if (ipoff + ip_hl + 4 > (int)pk.phys) { pk.unsupported = true; return RC_OK; }
+            if (ipoff + ip_hl + 4 > (int)pk.phys) { stale(pk, ipoff + ip_hl + 4); return RC_OK; }
             st16(l4 + 2, 0);
             if (v6) sum = csum_bytes(ip + 8, 32);
             sum += bswap16((u16)(58 + len));
@@ -498,7 +526,7 @@ DI int ipv6_header_length(Pkt &pk, const u8 *ip6, u32 pkt_len, int l2len) {
     const int ipoff = (int)(ip6 - pk.d);
     for (int guard = 0; guard < 65536 && (u32)(2 + offset + l2len) < pkt_len; ++guard) {
         if (nh != 0 && nh != 43 && nh != 44) return offset;
-        if (ipoff + offset + 2 > (int)pk.phys) { pk.unsupported = true; return offset; }
+        if (ipoff + offset + 2 > (int)pk.phys) { stale(pk, ipoff + offset + 2); return offset; }
         nh = ip6[offset];
         offset += (ip6[offset + 1] + 1) << 3;
     }
@@ -553,7 +581,7 @@ DI void ipv6_addr_csum_replace(Pkt &pk, u8 *ip6, const u8 *old_ip, const u8 *new
     if (l4 < 0) return;
     int fld = proto == 6 ? 16 : (proto == 17 ? 6 : 2);
     if ((int)(ip6 - pk.d) + l4 + fld + 2 > (int)pk.phys) {  // past the physical packet: stale bytes
-        pk.unsupported = true;
+        stale(pk, (int)(ip6 - pk.d) + l4 + fld + 2);
         return;
     }
     if (proto == 17 && ld16(ip6 + l4 + 6) == 0) return;
@@ -619,7 +647,7 @@ DI int rewrite_ports(const u16 *lut, u8 proto, u8 *l4, int l4len) {
 DI void rewrite_seqs(Pkt &pk, const te_dev_cfg_t &cfg, u8 *tcp) {
     int off = (int)(tcp - pk.d);
     if (off + 18 > (int)pk.phys) {  // fields past the physical packet (stale bytes)
-        pk.unsupported = true;
+        stale(pk, off + 18);
         return;
     }
     u32 ns = be32(tcp + 4) + cfg.tcp_sequence_adjust;
@@ -686,7 +714,8 @@ DI void rewrite_ipv6_addr_pair(Pkt &pk, const te_dev_cfg_t &cfg, const te_cidr_t
 #pragma unroll
     for (int b = 0; b < 16; ++b) old[b] = ip6[aoff + b];
     int room = (int)pk.phys - ((int)(ip6 - pk.d) + aoff);
-    if (!remap_ipv6(cfg, to, ip6 + aoff, room)) pk.unsupported = true;
+    const int r = remap_ipv6(cfg, to, ip6 + aoff, room);
+    if (r) stale(pk, (int)(ip6 - pk.d) + aoff + r);
     ipv6_addr_csum_replace(pk, ip6, old, ip6 + aoff, l3len);
 }
 
@@ -745,7 +774,7 @@ DI void rewrite_ipv6l3(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip6, int dir, int l
 DI bool arp_addrs(Pkt &pk, u8 *arp, u8 **ip1, u8 **ip2) {
     int base = (int)(arp - pk.d);
     if (base + 8 > (int)pk.phys) {  // ARP header past the physical packet
-        pk.unsupported = true;
+        stale(pk, base + 8);
         return false;
     }
     if (be16(arp + 2) != 0x0800) return false;
@@ -754,7 +783,7 @@ DI bool arp_addrs(Pkt &pk, u8 *arp, u8 **ip1, u8 **ip2) {
     int o1 = 8 + arp[4];
     int o2 = o1 + arp[5] + arp[4];
     if (base + o2 + 4 > (int)pk.phys) {  // address bytes past the physical packet
-        pk.unsupported = true;
+        stale(pk, base + o2 + 4);
         return false;
     }
     *ip1 = arp + o1;
@@ -808,7 +837,7 @@ DI int untrunc_packet(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip, u8 *ip6) {
             chksum = 0;
         } else if (ip[9] == 17 && (off & 0x2000)) {
             int f = (int)(ip - pk.d) + ((ip[0] & 0x0f) << 2) + 6;
-            if (f + 2 > (int)pk.phys) pk.unsupported = true;
+            if (f + 2 > (int)pk.phys) stale(pk, f + 2);
             else st16(pk.d + f, 0);
             chksum = 0;
         }
@@ -817,9 +846,10 @@ DI int untrunc_packet(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip, u8 *ip6) {
         if (pk.len > pk.caplen) {
             // memset(packet + caplen, 0, len - caplen): the tile sized this slot
             // for max(caplen, len) when --fixlen=pad is set
-            if (pk.len > pk.avail) pk.unsupported = true;
+            if (pk.len > pk.avail) stale(pk, (int)NEED_NEVER);
             for (u32 i = pk.caplen; i < pk.avail && i < pk.len; ++i) pk.d[i] = 0;
             if (pk.len > pk.phys) pk.phys = pk.len < pk.avail ? pk.len : pk.avail;
+            if (pk.len > pk.ext) pk.ext = pk.len;
             pk.caplen = pk.len;
         } else if (pk.len < pk.caplen) {
             return -1;
@@ -904,6 +934,8 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
         if (pktlen + (newl2 - oldl2) > MAXPACKET) return RC_ERROR;
         if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;  // checked below in the reference
         // move the record header + the first oldl2 bytes instead of the tail
+        u8 *const old_d = pk.d;
+        const u32 old_phys = pk.phys;
         if (newl2 > oldl2) {  // push 4 bytes at oldl2
             u8 *src = pk.d - 16, *dst = pk.d - 20;
             for (u32 i = 0; i < 16 + oldl2; ++i) dst[i] = src[i];
@@ -914,6 +946,12 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
             pk.d += 4;
             pk.avail -= 4;
             pk.phys -= 4;
+        }
+        // the reference's memmove (en10mb.c:568-578) writes its buffer up to pktlen +- 4
+        pk.ext = (u32)(pktlen + (int)(newl2 - oldl2));
+        if (pk.strict) {
+            pk.phys = old_phys;
+            strict_tail(pk, old_d);
         }
         if (newl2 > oldl2) {
             pk.avail += 4;
@@ -992,7 +1030,7 @@ DI bool l2_replace(Pkt &pk, int l2len, int n) {
     const int delta = l2len - n;
     if (delta == 0) return true;
     if (-delta > TE_HEAD) {
-        pk.unsupported = true;
+        stale(pk, (int)NEED_NEVER);  // slot headroom, not stale bytes: not replayed
         return false;
     }
     u8 *src = pk.d - 16, *dst = pk.d - 16 + delta;
@@ -1000,9 +1038,16 @@ DI bool l2_replace(Pkt &pk, int l2len, int n) {
         for (int i = 15; i >= 0; --i) dst[i] = src[i];
     else
         for (int i = 0; i < 16; ++i) dst[i] = src[i];
+    u8 *const old_d = pk.d;
+    const u32 old_phys = pk.phys;
     pk.d += delta;
     pk.avail -= delta;
     pk.phys -= delta;
+    pk.ext = (u32)((int)pk.caplen - delta);  // user.c:245-253 / hdlc.c:239-247 memmove extent
+    if (pk.strict) {
+        pk.phys = old_phys;
+        strict_tail(pk, old_d);
+    }
     return true;
 }
 
@@ -1095,7 +1140,9 @@ DI void fuzz_fill(Pkt &pk, int from, int n, int how, u8 x) {  // how: 0 = 0x00, 
         // `phys` stays unknown here (an XOR of a stale byte), and any later read of one
         // is flagged where it happens.
         if (j < 0 || j >= (int)pk.avail) continue;
+        if (how == 2 && pk.strict && j >= (int)pk.phys) stale(pk, j + 1);
         pk.d[j] = how == 0 ? (u8)0 : how == 1 ? (u8)0xff : (u8)(pk.d[j] ^ x);
+        if ((u32)j >= pk.ext) pk.ext = (u32)j + 1;
     }
 }
 
@@ -1123,7 +1170,7 @@ DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
         l4off = l2len + l4;
         l4len = l4off;  // an offset, as the reference has it (fuzzing.c:118,127)
         const int pb = l2len + (v4 ? 9 : 6);
-        if (pb >= (int)pk.phys) pk.unsupported = true;
+        if (pb >= (int)pk.phys) stale(pk, pb + 1);
         l4proto = ip[v4 ? 9 : 6];
     } else {
         l4len = caplen - l2len;

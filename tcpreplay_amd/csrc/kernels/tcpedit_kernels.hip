@@ -81,6 +81,10 @@ struct LaunchArgs {
     // step and nothing else; TE_FUZZ_APPLY fuzzes record i with RNG state fuzz_state[i]
     uint32_t fuzz_mode;
     const uint32_t *fuzz_state;
+    // stale static-buffer reads: a written record whose edit read bytes past
+    // its physical extent is listed {record, bytes needed, output offset} for te_q8_replay
+    uint4 *q8_list;
+    uint32_t q8_cap;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -290,7 +294,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     __syncthreads();
 
     // ---- one lane per packet ----
-    uint32_t out_sz = 0;
+    uint32_t out_sz = 0, need = 0;
     uint8_t st = 0;
     unsigned long long c_in = 0;
     if (tid < (int)npkt) {
@@ -319,6 +323,9 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         pk.phys = my_cap;
         pk.avail = slot_end - (r0 + 16);
         pk.unsupported = false;
+        pk.need = 0;
+        pk.ext = caplen;
+        pk.strict = false;
         int rc = RC_OK;
         bool warned = false;
         if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
@@ -329,7 +336,6 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
                                     fzs);
         }
         if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) st = rc == RC_REACHED ? 1 : 0;
-        if (pk.unsupported) st |= TE_ST_UNSUPPORTED;
         if (warned) st |= TE_ST_WARNED;
         bool write = true;
         if (rc == RC_ERROR) {
@@ -347,6 +353,11 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (write && pk.caplen == 0) {
             st |= TE_ST_ZEROCAP;
             write = false;
+        }
+        // a stale read only matters when the record is written (its bytes are the output)
+        if (pk.unsupported && write && !(FZ && a.fuzz_mode == TE_FUZZ_PROBE)) {
+            st |= TE_ST_UNSUPPORTED;
+            need = pk.need;
         }
         uint8_t *orec = pk.d - 16;
         if (swp || a.in_nsec || pk.d != rec + 16) {
@@ -414,7 +425,8 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         v[TE_CNT_SOFT] = on && (st & TE_ST_RC_MASK) == TE_ST_RC_SOFT;
         v[TE_CNT_WARN] = (st & TE_ST_WARNED) ? 1 : 0;
         v[TE_CNT_ERROR] = on && (st & TE_ST_RC_MASK) == TE_ST_RC_ERROR;
-        v[TE_CNT_UNSUPPORTED] = (st & TE_ST_UNSUPPORTED) ? 1 : 0;
+        v[TE_CNT_UNSUPPORTED] = 0;  // counted per record below (the q8 list index)
+        v[TE_CNT_Q8_FAILED] = 0;
 #pragma unroll
         for (int k = 0; k < TE_CNT__N; ++k) {
             unsigned long long x = v[k];
@@ -436,6 +448,12 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         // zero-initialised words hold ~value: atomicMax(~x) == ~min(x)
         atomicMax(&a.err[0], ~(unsigned long long)(tile.first_pkt + tid));
         atomicMax(&a.err[1], ~(a.out_base + E + opos));
+    }
+    if (tid < (int)npkt && (st & TE_ST_UNSUPPORTED)) {  // rare: one global atomic per record
+        const unsigned long long k = atomicAdd(&a.counters[TE_CNT_UNSUPPORTED], 1ull);
+        const unsigned long long o = a.out_base + E + opos;
+        if (a.q8_list && k < a.q8_cap)
+            a.q8_list[k] = make_uint4(tile.first_pkt + tid, need, (uint32_t)o, (uint32_t)(o >> 32));
     }
 
     // ---- stream the output records: aligned 16-byte chunks ----
@@ -1452,6 +1470,206 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     }
 }
 
+// ===========================================================================
+// te_q8_replay: the reference's static packet buffer, emulated (SURVEY Appendix B
+// Q8).  tcprewrite memcpy's every record into one MAXPACKET buffer that is never
+// cleared (tcprewrite.c:267-301), so an edit that reads past a record's captured
+// bytes -- an IPv6 checksum over an overstated payload length, a TCP sequence field
+// or an ARP address past caplen, remap_ipv6's stray write -- sees what earlier
+// records left there.  The edit kernel lists each such written record with the
+// buffer extent it read ([0, need)); one thread per listed record then rebuilds the
+// buffer sequentially:
+//   * walking back from the record, it finds the latest records whose memcpy
+//     covers [0, need) (each older one only matters where it reached further), or
+//     the capture's start, where the buffer is all zeros (safe_malloc, utils.c:38-48;
+//     tcpedit_packet: the caller's own buffer);
+//   * it replays tcpedit_packet over the emulated buffer for every record from there
+//     on, in order, normalising each edit to the reference's in-place layout (the
+//     encoders' memmove: the packet starts at the buffer start, bytes past its
+//     extent keep their earlier values);
+//   * the listed record's bytes then replace what the edit kernel wrote.
+// A replay that itself meets bytes nobody has written yet (valid prefix V) or whose
+// chain leaves this batch (a later pipeline chunk, a shard) fails and is counted in
+// TE_CNT_Q8_FAILED; the host then reports the record instead of writing a guess.
+// ===========================================================================
+constexpr uint32_t Q8_HEAD = 512;                        // room for the record header's moves
+constexpr uint32_t Q8_BUF = MAXPACKET + 4096;            // the emulated buffer (+ edits past MAXPACKET)
+constexpr uint64_t Q8_SLOT = ((uint64_t)Q8_HEAD + Q8_BUF + 255) & ~255ull;
+constexpr uint32_t Q8_MAX_CHAIN = 1u << 18;              // records a replay may walk back over
+constexpr int Q8_BLOCK = 64;
+
+struct Q8Args {
+    LaunchArgs a;
+    uint8_t *scratch;       // Q8_SLOT bytes per thread
+    uint32_t n_threads;
+    uint32_t file_start;    // record 0 of the batch is the capture's first record
+    const uint8_t *init_buf;  // the initial buffer (tcpedit_packet: the caller's), else zeros
+    uint32_t init_len;
+};
+
+__device__ __forceinline__ uint32_t q8_tile(const LaunchArgs &a, uint32_t j) {
+    uint32_t lo = 0, hi = a.n_tiles - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (a.tiles[mid].first_pkt <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t q8_rec(const LaunchArgs &a, uint32_t j) {
+    return a.tiles[q8_tile(a, j)].span_off + a.pkt_rel[j];
+}
+
+// the oldest record of the newest ones whose memcpy's cover [0, need) before record
+// `pos` (each older one only matters where it reached further); -1: the batch start
+__device__ int64_t q8_chain(const LaunchArgs &a, uint32_t pos, uint32_t need) {
+    const bool swp = a.in_swapped != 0;
+    uint32_t cov = 0;
+    int64_t j0 = -1;
+    uint32_t steps = 0;
+    for (int64_t j = (int64_t)pos - 1; j >= 0; --j) {
+        if (++steps > Q8_MAX_CHAIN) return -2;
+        const uint32_t cl = ld_hdr32(a.in + q8_rec(a, (uint32_t)j) + 8, swp);
+        if (cl > cov) {
+            cov = cl;
+            j0 = j;
+            if (cov >= need) return j0;
+        }
+    }
+    return -1;
+}
+
+enum { Q8_OK = 0, Q8_FAIL = 1, Q8_DEEPER = 2 };
+
+// replay records j0..i over the emulated buffer (j0 < 0: from the batch start, whose
+// buffer is zeros or the caller's); Q8_DEEPER: record *jd read bytes past what the
+// replay has (*needd), so it has to start further back
+template <bool FZ>
+__device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t start, uint32_t i, uint64_t out_off,
+                              uint8_t *slot, uint32_t *jd, uint32_t *needd) {
+    const LaunchArgs &a = q.a;
+    const bool swp = a.in_swapped != 0;
+    uint8_t *buf = slot + Q8_HEAD;
+    uint32_t V = 0;  // bytes [0, V) of the emulated buffer are known
+    uint32_t j0 = (uint32_t)start;
+    if (start < 0) {
+        if (!q.file_start) return Q8_FAIL;  // the bytes come from before this batch
+        j0 = 0;
+        if (q.init_buf) {
+            for (uint32_t x = 0; x < q.init_len; ++x) buf[x] = q.init_buf[x];
+            V = q.init_len;
+        } else {
+            for (uint32_t x = 0; x < MAXPACKET; x += 16) *(uint4 *)(buf + x) = make_uint4(0, 0, 0, 0);
+            V = MAXPACKET;
+        }
+    }
+    for (uint32_t j = j0; j <= i; ++j) {
+        const uint8_t *rec = a.in + q8_rec(a, j);
+        const uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp) / (a.in_nsec ? 1000u : 1u);
+        const uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
+        if (caplen > MAX_SNAPLEN) return Q8_FAIL;
+        for (uint32_t x = 0; x < caplen; ++x) buf[x] = rec[16 + x];  // tcprewrite.c:301
+        if (caplen > V) V = caplen;
+        const uint64_t pktno = a.pkt_base + j;
+        int dir = TE_DIR_C2S;
+        const bool explicit_dir = a.fixed_dir >= 0;
+        if (explicit_dir) {
+            dir = a.fixed_dir;
+        } else if (a.dirbits) {
+            const uint64_t idx = pktno >> 2;
+            const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+            const uint8_t b = idx < a.dirbits_len ? a.dirbits[idx] : 0;
+            dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+        }
+        if (dir == TE_DIR_NOSEND && !explicit_dir) continue;  // written unedited: the buffer holds its input
+        uint8_t *hdr = buf - 16;
+        st32(hdr, ts_sec);
+        st32(hdr + 4, ts_frac);
+        st32(hdr + 8, caplen);
+        st32(hdr + 12, len);
+        Pkt pk;
+        pk.d = buf;
+        pk.caplen = caplen;
+        pk.len = len;
+        pk.phys = V;
+        pk.avail = Q8_BUF - 64;
+        pk.unsupported = false;
+        pk.need = 0;
+        pk.ext = caplen;
+        pk.strict = true;
+        bool warned = false;
+        const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
+        const int rc = tcpedit_packet<FZ>(pk, cfg, a.portlut, dir, warned, a.fuzz_mode, fzs);
+        if (pk.unsupported) {  // bytes nobody wrote yet in this replay (or slot headroom)
+            if (pk.need == NEED_NEVER || pk.need > MAXPACKET) return Q8_FAIL;
+            *jd = j;
+            *needd = pk.need;
+            return Q8_DEEPER;
+        }
+        if (j == i) {
+            if (rc == RC_ERROR || rc == RC_SOFT) return Q8_FAIL;  // cannot change the pass-1 layout
+            g_u8 *o = (g_u8 *)a.out + out_off;
+            const uint32_t oc = (uint32_t)o[8] | ((uint32_t)o[9] << 8) | ((uint32_t)o[10] << 16) |
+                                ((uint32_t)o[11] << 24);
+            if (oc != pk.caplen) return Q8_FAIL;
+            for (uint32_t x = 0; x < pk.caplen; ++x) o[16 + x] = pk.d[x];
+            g_u8 *st = (g_u8 *)a.status + i;
+            const uint8_t old = *st;
+            uint8_t nst = (uint8_t)(old & ~(TE_ST_UNSUPPORTED | TE_ST_WARNED | TE_ST_RC_MASK));
+            nst |= rc == RC_WARN ? TE_ST_RC_WARN : TE_ST_RC_OK;
+            if (warned) nst |= TE_ST_WARNED;
+            *st = nst;
+            const int dw = (warned ? 1 : 0) - ((old & TE_ST_WARNED) ? 1 : 0);
+            if (dw) atomicAdd(&a.counters[TE_CNT_WARN], (unsigned long long)(long long)dw);
+            return Q8_OK;
+        }
+        // back to the reference's in-place layout: the packet starts at the buffer start
+        // (strict_tail kept pk.d + x == buffer offset x for every known x)
+        const int sft = (int)(pk.d - buf);
+        const uint32_t M = pk.ext > pk.phys ? pk.ext : pk.phys;
+        if (sft < 0)  // the packet grew: it sits below the buffer start
+            for (uint32_t x = M; x-- > 0;) buf[x] = pk.d[x];
+        else if (sft > 0)  // it shrank: it sits above the buffer start
+            for (uint32_t x = 0; x < M; ++x) buf[x] = pk.d[x];
+        if (M > V) V = M;
+    }
+    return Q8_FAIL;
+}
+
+template <bool FZ>
+__device__ bool q8_replay_one(const Q8Args &q, const te_dev_cfg_t &cfg, uint4 ent, uint8_t *slot) {
+    const LaunchArgs &a = q.a;
+    const uint32_t i = ent.x, need = ent.y;
+    const uint64_t out_off = (uint64_t)ent.z | ((uint64_t)ent.w << 32);
+    if (need == NEED_NEVER || need > MAXPACKET) return false;
+    int64_t start = q8_chain(a, i, need);
+    // an earlier record of the replay may read past what it has: start further back
+    for (int iter = 0; iter < 64; ++iter) {
+        if (start < -1) return false;
+        uint32_t jd = 0, nd = 0;
+        const int r = q8_replay_from<FZ>(q, cfg, start, i, out_off, slot, &jd, &nd);
+        if (r == Q8_OK) return true;
+        if (r == Q8_FAIL || start < 0) return false;
+        const int64_t s2 = q8_chain(a, jd, nd);
+        if (s2 >= start && s2 >= 0) return false;  // no progress
+        start = s2;
+    }
+    return false;
+}
+
+template <bool FZ>
+__global__ void __launch_bounds__(Q8_BLOCK) te_q8_replay(Q8Args q) {
+    const LaunchArgs &a = q.a;
+    const unsigned long long listed = *(volatile unsigned long long *)&a.counters[TE_CNT_UNSUPPORTED];
+    const uint32_t n = (uint32_t)(listed < a.q8_cap ? listed : a.q8_cap);
+    const uint32_t g = blockIdx.x * Q8_BLOCK + threadIdx.x;
+    if (g == 0 && listed > a.q8_cap) atomicAdd(&a.counters[TE_CNT_Q8_FAILED], listed - a.q8_cap);
+    uint8_t *slot = q.scratch + (uint64_t)g * Q8_SLOT;
+    for (uint32_t e = g; e < n; e += q.n_threads)
+        if (!q8_replay_one<FZ>(q, *a.cfg, a.q8_list[e], slot)) atomicAdd(&a.counters[TE_CNT_Q8_FAILED], 1ull);
+}
+
 }  // namespace
 
 // persistent grid = the blocks that are resident at once (CUs x occupancy)
@@ -1608,8 +1826,7 @@ extern "C" int te_wave_grid(void) {
 // ---------------------------------------------------------------------------
 // C-ABI launch wrapper (called from the C host code, no torch types)
 // ---------------------------------------------------------------------------
-extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
-    LaunchArgs a;
+static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.cfg = L->cfg;
     a.portlut = L->portlut;
     a.dirbits = L->dirbits;
@@ -1639,6 +1856,37 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     a.counters_next = nullptr;
     a.fuzz_mode = TE_FUZZ_OFF;
     a.fuzz_state = nullptr;
+    a.q8_list = (uint4 *)L->q8_list;
+    a.q8_cap = L->q8_cap;
+}
+
+extern "C" uint64_t te_q8_slot_bytes(void) { return Q8_SLOT; }
+
+// te_q8_replay over the records the last edit of this launch listed (the counter on the
+// device says how many: a grid of q8_threads reads it and returns when it is 0)
+extern "C" int te_launch_q8(te_launch_t *L, hipStream_t stream) {
+    Q8Args q;
+    fill_args(q.a, L);
+    if (L->fuzz_states) {
+        q.a.fuzz_mode = TE_FUZZ_APPLY;
+        q.a.fuzz_state = L->fuzz_states;
+    }
+    q.scratch = (uint8_t *)L->q8_scratch;
+    q.n_threads = L->q8_threads;
+    q.file_start = (uint32_t)L->q8_file_start;
+    q.init_buf = L->q8_init;
+    q.init_len = L->q8_init_len;
+    if (!q.scratch || q.n_threads == 0 || q.n_threads % Q8_BLOCK || !L->q8_list || L->n_tiles == 0) return -1;
+    if (q.a.fuzz_mode == TE_FUZZ_APPLY)
+        hipLaunchKernelGGL(te_q8_replay<true>, dim3(q.n_threads / Q8_BLOCK), dim3(Q8_BLOCK), 0, stream, q);
+    else
+        hipLaunchKernelGGL(te_q8_replay<false>, dim3(q.n_threads / Q8_BLOCK), dim3(Q8_BLOCK), 0, stream, q);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
+    LaunchArgs a;
+    fill_args(a, L);
     hipError_t e;
     const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow) && L->n_tiles > 0;
     if (fast && !L->generic_only) {

@@ -1,0 +1,168 @@
+"""edits that read the reference's stale static packet buffer.
+
+tcprewrite memcpy's every record into one never-cleared MAXPACKET buffer
+(tcprewrite.c:267-301); an IPv6 checksum over an overstated payload length, a TCP
+sequence field or ARP address past caplen, or remap_ipv6's stray write reads what
+earlier records (as edited) left there.  The device lists such records and replays the
+buffer (te_q8_replay); the oracle keeps the reference's static buffer itself.  Every
+case here must come out byte-identical to the oracle -- or, where the bytes come from
+outside the batch (a later pipeline chunk), fail loudly.
+"""
+import random
+import struct
+
+import pytest
+
+import oracle_lib as O
+import tcpreplay_amd as TA
+from tcpreplay_amd import synth as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _overstate(recs, idxs, by=50):
+    """IPv6 records whose payload length claims `by` more bytes than were captured"""
+    recs = list(recs)
+    for i in idxs:
+        ts, tu, cl, ln, d = recs[i]
+        d = bytearray(d)
+        assert d[12:14] == b"\x86\xdd"
+        struct.pack_into(">H", d, 18, struct.unpack_from(">H", d, 18)[0] + by)
+        recs[i] = (ts, tu, cl, ln, bytes(d))
+    return recs
+
+
+def _mixed(n, seed):
+    rng = random.Random(seed)
+    parts = []
+    for size, v6, proto in [(90, True, 17), (97, True, 6), (200, True, 17), (333, False, 6), (1514, True, 17),
+                            (64, False, 17), (600, True, 6)]:
+        parts += S.records(S.pcap_fixed(n, size, seed=rng.randrange(1 << 20), ipv6=v6, proto=proto))
+    rng.shuffle(parts)
+    return parts
+
+
+def _gpu(pcap, args, cache=None):
+    te = TA.TcpEdit(args)
+    try:
+        b = TA.Batch(te, pcap, cache)
+        rc = b.run()
+        out, r = b.output(), b.result()
+        b.close()
+        return rc, out, r
+    finally:
+        te.close()
+
+
+def _check(pcap, args, cache=None, min_stale=1):
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    rc, out, r = _gpu(pcap, args, cache)
+    assert r.stale_records >= min_stale, "the case must exercise the replay"
+    assert r.unsupported == 0
+    assert rc == rc_o
+    assert out == exp, f"first difference at byte {next(i for i in range(min(len(out), len(exp))) if out[i] != exp[i])}"
+
+
+@pytest.mark.parametrize("args", [["--fixcsum"], ["--seed=9", "--fixcsum"], ["--enet-vlan=add", "--enet-vlan-tag=5",
+                                  "--fixcsum"], ["--efcs", "--fixcsum"], ["--fixlen=pad", "--fixcsum"],
+                                  ["--pnat=[::/0]:[2001:db8:aaaa::/36]", "--fixcsum"]])
+def test_overstated_ipv6_payloads_read_earlier_records(built, args):
+    """IPv6 records with overstated payload lengths amid records of other sizes: the
+    checksum sums bytes the previous records (as edited) left in the buffer"""
+    recs = _mixed(60, seed=len(args))
+    v6 = [i for i, r in enumerate(recs) if r[4][12:14] == b"\x86\xdd" and r[2] >= 90]
+    pick = sorted(random.Random(7).sample(v6, 25))
+    _check(S.build_pcap(_overstate(recs, pick)), args, min_stale=5)
+
+
+def test_stale_bytes_from_the_capture_start_are_zeros(built):
+    """the first record reads past its caplen: the reference's buffer starts zeroed"""
+    recs = S.records(S.pcap_fixed(5, 200, ipv6=True, proto=17, seed=3))
+    _check(S.build_pcap(_overstate(recs, [0, 1, 2, 3, 4])), ["--fixcsum"], min_stale=5)
+
+
+def test_vlan_delete_leaves_the_old_tail(built):
+    """VLAN-tagged records shrink by 4 (--enet-vlan=del): the reference's buffer keeps
+    the old last 4 bytes past the new end, where the next record's overread lands"""
+    base = S.records(S.pcap_fixed(40, 300, ipv6=True, proto=17, seed=5))
+    recs = []
+    for k, (ts, tu, cl, ln, d) in enumerate(base):
+        if k % 2 == 0:  # tagged, longer: its tail covers the next record's overread
+            d = d[:12] + b"\x81\x00\x00\x07" + d[12:] + bytes(range(40))
+            cl = ln = len(d)
+        recs.append((ts, tu, cl, ln, d))
+    recs = _overstate(recs, [k for k in range(1, 40, 2)], by=30)
+    _check(S.build_pcap(recs), ["--enet-vlan=del", "--fixcsum"], min_stale=10)
+
+
+def test_truncated_tcp_header_sequence_edit(built):
+    """--tcp-sequence on a TCP header cut by the capture reads and rewrites fields past
+    caplen: nothing of that reaches its own output, but it is in the buffer"""
+    big = S.records(S.pcap_fixed(4, 400, ipv6=False, proto=6, seed=8))
+    v6 = S.records(S.pcap_fixed(4, 200, ipv6=True, proto=6, seed=9))
+    recs = []
+    for k in range(4):
+        ts, tu, cl, ln, d = big[k]
+        recs.append((ts, tu, cl, ln, d))
+        ts, tu, cl, ln, d = big[(k + 1) % 4]
+        recs.append((ts, tu, 40, ln, d[:40]))  # TCP header cut after 6 bytes: seq fields are stale
+        recs.append(_overstate([v6[k]], [0], by=150)[0])
+    _check(S.build_pcap(recs), ["--tcp-sequence=77", "--fixcsum"], min_stale=4)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_mutated_captures_with_stale_reads(built, seed):
+    """random header mutations (truncations, len != caplen, tags) over a v4/v6 mix with
+    overstated IPv6 payloads: every option line of the differential pool"""
+    import test_gpu_parity as P
+    rng = random.Random(100 + seed)
+    recs = P.mutate(_mixed(25, seed=seed), rng)
+    v6 = [i for i, r in enumerate(recs) if r[4][12:14] == b"\x86\xdd" and r[2] >= 60]
+    recs = _overstate(recs, rng.sample(v6, min(12, len(v6))), by=rng.randrange(1, 300))
+    pcap = S.build_pcap(recs)
+    for args in P.OPTION_POOL[seed::6]:
+        rc_o, exp = O.rewrite(pcap, args)
+        rc, out, r = _gpu(pcap, args)
+        assert r.unsupported == 0 and rc == rc_o and out == exp, args
+
+
+def test_pipelined_chunk_replays_inside_the_chunk_or_fails_loudly(built):
+    """chunk 0 starts at the capture's start; in a later chunk a replay whose records all
+    lie in that chunk succeeds, one reaching back into the previous chunk is refused"""
+    recs = S.records(S.pcap_fixed(30_000, 90, ipv6=True, proto=17, seed=11))
+    cover = S.records(S.pcap_fixed(1, 400, ipv6=True, proto=17, seed=12))[0]
+    recs[20_001] = cover  # a longer record just before the overread covers it
+    ok = S.build_pcap(_overstate(recs, [3, 20_002], by=40))
+    rc_o, exp = O.rewrite(ok, ["--fixcsum"])
+    te = TA.TcpEdit(["--fixcsum"])
+    try:
+        rc, out = te.rewrite_pipelined(ok, chunk_bytes=1 << 20)
+        assert rc == rc_o == 0 and out == exp
+        bad = S.build_pcap(_overstate(recs, [15_000], by=40))  # chunk 1: same sizes back to its start
+        rc, _ = te.rewrite_pipelined(bad, chunk_bytes=1 << 20)
+        assert rc == TA.TCPEDIT_ERROR and "stale static packet buffer" in te.geterr()
+    finally:
+        te.close()
+
+
+def test_per_packet_api_reads_the_callers_buffer(built):
+    """tcpedit_packet edits the caller's buffer: with one buffer reused for every record
+    (tcprewrite's rewrite_packets) the stale bytes are the previous records', as the
+    oracle's static buffer has them"""
+    recs = _mixed(8, seed=3)
+    v6 = [i for i, r in enumerate(recs) if r[4][12:14] == b"\x86\xdd" and r[2] >= 90]
+    recs = _overstate(recs, v6[::3])
+    pcap = S.build_pcap(recs)
+    _, exp = O.rewrite(pcap, ["--fixcsum"])
+    te = TA.TcpEdit(["--fixcsum"])
+    buf = bytearray(262166)
+    got = []
+    try:
+        for ts, tu, cl, ln, d in recs:
+            buf[:cl] = d
+            rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf)
+            assert rc != TA.TCPEDIT_ERROR, te.geterr()
+            got.append((ts, tu, h["caplen"], h["len"], bytes(buf[:h["caplen"]])))
+    finally:
+        te.close()
+    assert got == S.records(exp)
