@@ -44,9 +44,18 @@ WORKLOADS = {
     "fz": ("pcap_imix", dict(), ["--fuzz-seed=42", "--fuzz-factor=2"],
            "--fuzz-seed=42 --fuzz-factor=2 (the l7fuzzing golden's options) on IMIX 64/570/1514 7:4:1: reach pass, "
            "RNG-state scan, edit pass (SURVEY 8(f) rank 4)"),
+    # common tcprewrite lines without --fixcsum or with size changes
+    "seed": ("pcap_fixed", dict(size=64), ["--seed=42"],
+             "--seed=42 without --fixcsum (incremental checksums, SURVEY Q13) on 1M x 64B"),
+    "hdr": ("pcap_imix", dict(), ["--ttl=+1", "--tos=7"],
+            "--ttl=+1 --tos=7 on IMIX 64/570/1514 7:4:1 (TTL change -> full recompute, tcpedit.c:195,338)"),
+    "vdel": ("pcap_imix", dict(vlan=0xB02D), ["--enet-vlan=del", "--fixcsum"],
+             "--enet-vlan=del --fixcsum on 802.1Q-tagged IMIX 68/574/1518 (every record -4 bytes)"),
+    "efcs": ("pcap_imix", dict(), ["--efcs", "--fixcsum"],
+             "--efcs --fixcsum on IMIX 64/570/1514 7:4:1 (every record -4 bytes)"),
 }
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
-                   "fz": 10_000_000}
+                   "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000}
 CACHED = {"c4"}  # workloads with a tcpprep cache (synth.tcpprep_cache: C2S/S2C runs by flow)
 
 
@@ -140,12 +149,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
-    ap.add_argument("--extra", default="c3,c4,c5,c2x10,fz,prep",
+    ap.add_argument("--extra", default="c3,c4,c5,c2x10,seed,hdr,vdel,efcs,fz,prep",
                     help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
                     "half --cpu-threads threads)")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline "
-                    "(the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the multi-core CPU baseline "
+                    "(default: the CPUs this process may run on, at most 16 -- the GPU box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
     ap.add_argument("--verify", action="store_true", help="compare the first run with the oracle")
@@ -326,7 +335,7 @@ def main():
         if not opt.no_cpu_baseline and opt.workload not in CACHED:
             wl_args = WORKLOADS[opt.workload][2]
             v1, runs1, el1, _ = cpu_baseline(pcap, wl_args, n, opt.cpu_seconds / 2)
-            thr = max(1, opt.cpu_threads)
+            thr = opt.cpu_threads or min(16, len(os.sched_getaffinity(0)))
             v, runs, el, used = cpu_baseline(pcap, wl_args, n, opt.cpu_seconds / 2, thr)
             result["cpu_baseline"] = {
                 "value": round(v, 3), "unit": "Mpkt/s", "cores": used, "kind": "port",

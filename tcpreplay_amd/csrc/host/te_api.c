@@ -122,12 +122,13 @@ static int static_capable(const te_dev_cfg_t *c)
            !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB && !c->fuzz_seed;
 }
 
-/* options the register-resident fast lane carries (fast_lane.hpp); anything
- * else keeps every packet on the generic lane */
+/* options the register-resident fast lane carries (fast_lane.hpp): the MAC, port,
+ * address and seed edits, the IP header edits (TOS, TTL, traffic class, flow label,
+ * TCP sequence) and both checksum modes (--fixcsum or incremental); anything else
+ * keeps every packet on the generic lane */
 static int fast_capable(const te_dev_cfg_t *c)
 {
-    return static_capable(c) && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 && c->tclass < 0 &&
-           c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+    return static_capable(c) && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
 
 /* the most a record's L2 header can grow: a VLAN push (4 bytes) or a user header longer
@@ -144,11 +145,8 @@ static uint32_t rec_growth(const te_dev_cfg_t *c)
 static int fast_capable_grow(const te_dev_cfg_t *c)
 {
     return c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs &&
-           !c->fuzz_seed &&
-           c->fixlen == TE_FIXLEN_OFF &&
-           !c->mtu_truncate && !c->skip_soft_errors && c->fixcsum && c->ttl_mode == TE_TTL_OFF && c->tos < 0 &&
-           c->tclass < 0 && c->flowlabel < 0 && !c->tcp_sequence_enable && !c->fixhdrlen && c->n_subs == 0 &&
-           !c->random_set;
+           !c->fuzz_seed && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate && !c->skip_soft_errors &&
+           !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
 
 /* IPv6 rewrites with a non-octet target mask keep the reference's stray write

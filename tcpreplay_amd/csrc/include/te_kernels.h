@@ -41,6 +41,10 @@ extern "C" {
 #define TE_FF_RWIP 4u    /* --srcipmap / --dstipmap / --pnat / --endpoints */
 #define TE_FF_SEED 8u    /* --seed */
 #define TE_FF_ALL 15u
+#define TE_FF_HDR 16u    /* --tos / --ttl / --tclass / --flowlabel / --tcp-sequence */
+#define TE_FF_INCR 32u   /* no --fixcsum: checksums follow the incremental updates (RFC 1624)
+                            unless the packet needs a recompute (needtorecalc, tcpedit.c:338) */
+#define TE_FF_ALLX 63u
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */

@@ -115,6 +115,7 @@ DI unsigned long long mac48(const u8 *m) {
 // an LDS cfg field.  The host launches the smallest instance whose F covers the
 // config (te_launch_edit).
 constexpr u32 F_MAC = TE_FF_MAC, F_PORTMAP = TE_FF_PORTMAP, F_RWIP = TE_FF_RWIP, F_SEED = TE_FF_SEED;
+constexpr u32 F_HDR = TE_FF_HDR, F_INCR = TE_FF_INCR;
 
 // the scalar options phase A reads per packet, held in SGPRs (kernel arguments)
 // instead of being re-read from the LDS cfg copy on every tile
@@ -208,6 +209,48 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
         dirty |= 0xfu;
     }
 
+    // F_INCR (no --fixcsum): the IPv4 header and TCP checksum fields follow the
+    // incremental updates too, and a packet is recomputed only when an edit asks for it
+    // (needtorecalc: a TTL/hop-limit change, tcpedit.c:195,211)
+    constexpr bool kIncr = (F & F_INCR) != 0;
+    u32 ics = hi16(H[6]);  // IPv4 header checksum (IP + 10), raw LE
+    bool recalc = false;
+    // ---- IP header edits (tcpedit.c:184-237), before the port map ----
+    if ((F & F_HDR) && cfg.tos > -1) {  // TOS (IPv4) + csum_replace2
+        const u32 oldv = lo16(H[4]), newv = (oldv & 0xffu) | ((u32)(cfg.tos & 0xff) << 8);
+        H[4] = v6 ? H[4] : with_lo16(H[4], newv);
+        if (kIncr) ics = v6 ? ics : (u32)csum_replace2_v((u16)ics, (u16)oldv, (u16)newv);
+        dirty |= v6 ? 0u : 1u << 4;
+    }
+    if ((F & F_HDR) && cfg.ttl_mode != TE_TTL_OFF) {  // rewrite_ipv4_ttl / rewrite_ipv6_hlim (edit_packet.c:627-706)
+        const u32 t0 = v6 ? H[5] >> 24 : H[6] & 0xffu, v = cfg.ttl_value & 0xffu;
+        u32 t = t0;
+        bool changed = true;
+        if (cfg.ttl_mode == TE_TTL_SET) {
+            changed = t0 != v;
+            t = v;
+        } else if (cfg.ttl_mode == TE_TTL_ADD) {
+            t = t0 + v > 255u ? 255u : t0 + v;
+        } else {
+            t = t0 <= v ? 1u : t0 - v;
+        }
+        H[5] = v6 ? ((H[5] & 0x00ffffffu) | (t << 24)) : H[5];
+        H[6] = v6 ? H[6] : ((H[6] & ~0xffu) | t);
+        if (kIncr) ics = (v6 || !changed) ? ics : (u32)csum_replace2_v((u16)ics, (u16)t0, (u16)t);
+        recalc = changed;
+        dirty |= v6 ? 1u << 5 : 1u << 6;
+    }
+    if ((F & F_HDR) && cfg.tclass > -1) {  // tcpedit.c:214-228
+        const u32 f = (bswap32(H[4]) & 0xf00fffffu) + ((u32)cfg.tclass << 20);
+        H[4] = v6 ? bswap32(f) : H[4];
+        dirty |= v6 ? 1u << 4 : 0u;
+    }
+    if ((F & F_HDR) && cfg.flowlabel > -1) {  // tcpedit.c:231-237
+        const u32 f = (bswap32(H[4]) & 0xfff00000u) + (u32)cfg.flowlabel;
+        H[4] = v6 ? bswap32(f) : H[4];
+        dirty |= v6 ? 1u << 4 : 0u;
+    }
+
     // L4 header (20 bytes) at packet offset 34 (v4) or 54 (v6)
     // bitwise selects, not `v6 ? H[14+i] : H[9+i]`: the compiler folds the
     // latter into one dynamically indexed access, which moves H to scratch
@@ -216,6 +259,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
 #pragma unroll
     for (int i = 0; i < 5; ++i) L[i] = (H[14 + i] & m6) | (H[9 + i] & ~m6);
     u32 ucs = hi16(L[1]);  // UDP checksum field (L4 + 6), raw LE
+    u32 tcs = lo16(L[4]);  // TCP checksum field (L4 + 16), raw LE (F_INCR)
     const bool udp_live = !tcp;
 
     // ---- port map (rewrite_ports, portmap.c:267-330): destination, then source ----
@@ -238,9 +282,22 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
             asm volatile("" : "+v"(nd), "+v"(ns));
         }
         ucs = ((nd != od) & udp_live & (ucs != 0)) ? (u32)csum_replace2_v((u16)ucs, (u16)od, (u16)nd) : ucs;
+        if (kIncr) tcs = ((nd != od) & tcp) ? (u32)csum_replace2_v((u16)tcs, (u16)od, (u16)nd) : tcs;
         L[0] = with_hi16(L[0], nd);
         ucs = ((ns != os) & udp_live & (ucs != 0)) ? (u32)csum_replace2_v((u16)ucs, (u16)os, (u16)ns) : ucs;
+        if (kIncr) tcs = ((ns != os) & tcp) ? (u32)csum_replace2_v((u16)tcs, (u16)os, (u16)ns) : tcs;
         L[0] = with_lo16(L[0], ns);
+    }
+    if ((F & F_HDR) && cfg.tcp_sequence_enable) {  // rewrite_seqs (rewrite_sequence.c:37-55), TCP only
+        const u32 os = L[1], ns = bswap32(bswap32(os) + cfg.tcp_sequence_adjust);
+        tcs = tcp ? (u32)csum_replace4_v((u16)tcs, os, ns) : tcs;
+        L[1] = tcp ? ns : L[1];
+        const u32 fl = (L[3] >> 8) & 0xffu;
+        const bool ack = tcp & !((fl & 0x02u) && !(fl & 0x10u));
+        const u32 oa = L[2], na = bswap32(bswap32(oa) + cfg.tcp_sequence_adjust);
+        tcs = ack ? (u32)csum_replace4_v((u16)tcs, oa, na) : tcs;
+        L[2] = ack ? na : L[2];
+        dirty |= 0x6u << (v6 ? 14 : 9);
     }
 
     constexpr bool kAddr = (F & (F_RWIP | F_SEED)) != 0;
@@ -249,8 +306,12 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
         u32 src = H[7], dst = H[8];
         // ipv4_addr_csum_replace's L4 part (edit_packet.c:259-296): only the UDP field is
         // carried, and only on an IPv4 lane whose address was replaced
-#define FL_V4_UPD(c, o, n) \
-    ucs = ((c) & !v6 & udp_live & (ucs != 0)) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs
+#define FL_V4_UPD(c, o, n)                                                                          \
+    ucs = ((c) & !v6 & udp_live & (ucs != 0)) ? (u32)csum_replace4_v((u16)ucs, (o), (n)) : ucs;    \
+    if (kIncr) {                                                                                    \
+        ics = ((c) & !v6) ? (u32)csum_replace4_v((u16)ics, (o), (n)) : ics;                         \
+        tcs = ((c) & !v6 & tcp) ? (u32)csum_replace4_v((u16)tcs, (o), (n)) : tcs;                   \
+    }
         if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv4l3 (edit_packet.c:787-878)
             bool done = false;  // the first matching entry of each list
             for (int m = 0; m < cfg.n_srcipmap; ++m) {
@@ -318,8 +379,9 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     if (edit_addr && __ballot(v6)) {
         u32 src[4] = {H[6], H[7], H[8], H[9]}, dst[4] = {H[10], H[11], H[12], H[13]};
         // ipv6_addr_csum_replace (edit_packet.c:298-330): only the UDP field is carried
-#define FL_V6_UPD(c, o, n) \
-    ucs = ((c) & v6 & udp_live & (ucs != 0)) ? (u32)csum_replace16_v((u16)ucs, (o), (n)) : ucs
+#define FL_V6_UPD(c, o, n)                                                                          \
+    ucs = ((c) & v6 & udp_live & (ucs != 0)) ? (u32)csum_replace16_v((u16)ucs, (o), (n)) : ucs;    \
+    if (kIncr) tcs = ((c) & v6 & tcp) ? (u32)csum_replace16_v((u16)tcs, (o), (n)) : tcs
 #define FL_V6_SET(a, c, n)                                 \
     _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) a[q_] = (c) ? n[q_] : a[q_];
         if ((F & F_RWIP) && cfg.rewrite_ip) {  // rewrite_ipv6l3 (edit_packet.c:884-1019); TCP/UDP: no ICMPv6 recursion
@@ -397,11 +459,13 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
 
     // ---- fix_ipv4/ipv6_checksums (edit_packet.c:55-189) -> do_checksum (checksum.c:34-170) ----
     // caplen == len, not a fragment, lengths consistent: the L4 sum always runs,
-    // except on a UDP field that is (still) 0 (checksum.c:115).
-    const bool do_l4 = tcp || ucs != 0;
-    L[4] = (do_l4 && tcp) ? with_lo16(L[4], 0) : L[4];  // th_sum (L4 + 16)
+    // except on a UDP field that is (still) 0 (checksum.c:115).  F_INCR: only for a
+    // packet an edit asked to recompute; the others keep the incremental fields.
+    const bool full = !kIncr || recalc;
+    const bool do_l4 = full && (tcp || ucs != 0);
+    L[4] = (do_l4 && tcp) ? with_lo16(L[4], 0) : ((kIncr && !full && tcp) ? with_lo16(L[4], tcs) : L[4]);
     ucs = (do_l4 && !tcp) ? 0u : ucs;                     // uh_sum (L4 + 6)
-    L[1] = with_hi16(L[1], ucs);
+    L[1] = tcp ? L[1] : with_hi16(L[1], ucs);             // (TCP: the sequence number's low half)
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         H[14 + i] = (L[i] & m6) | (H[14 + i] & ~m6);
@@ -430,7 +494,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     {  // IPv4 header checksum: do_checksum(ip, 0, ip_len) default case over 20 bytes
         const u32 h6 = with_hi16(H[6], 0);
         const u32 hs = wsum_acc(H[8], wsum_acc(H[7], wsum_acc(h6, wsum_acc(H[5], wsum_acc(H[4], 0u)))));
-        H[6] = v6 ? H[6] : with_hi16(h6, (~fold32(hs)) & 0xffffu);
+        H[6] = v6 ? H[6] : with_hi16(h6, full ? (~fold32(hs)) & 0xffffu : ics);
         dirty |= v6 ? 0u : 1u << 6;
     }
 

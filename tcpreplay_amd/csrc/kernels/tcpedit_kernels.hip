@@ -19,6 +19,7 @@
 // Records too large for a tile are edited in an HBM scratch slot instead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "edit_pkt.hpp"
 #include "te_kernels.h"
 
@@ -1796,7 +1797,9 @@ extern "C" int te_fast_grid(void) {
 #endif
 #define TE_WAVE_INSTANCES(X)                                                                         \
     X(0u, TE_WK_DEPTH_LEAN, false) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, false)                              \
-    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, false) X(TE_FF_ALL, 1, false) X(TE_FF_ALL, 1, true)
+    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, false) X(TE_FF_ALL, 1, false) X(TE_FF_ALL, 1, true)                \
+    X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, false) X(TE_FF_HDR | TE_FF_INCR, 1, false)             \
+    X(TE_FF_ALLX, 1, false) X(TE_FF_ALLX, 1, true)
 static const struct {
     uint32_t feat;
     bool grow;
@@ -1809,7 +1812,12 @@ static const struct {
 
 static uint32_t fast_feat(const te_dev_cfg_t *c) {
     return (c->mac_mask ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
-           (c->rewrite_ip ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u);
+           (c->rewrite_ip ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u) |
+           ((c->tos >= 0 || c->ttl_mode != TE_TTL_OFF || c->tclass >= 0 || c->flowlabel >= 0 ||
+             c->tcp_sequence_enable)
+                ? TE_FF_HDR
+                : 0u) |
+           (c->fixcsum ? 0u : TE_FF_INCR);
 }
 
 extern "C" int te_wave_grid(void) {
@@ -1931,8 +1939,11 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             f.vlan_tag_word = 0;
         }
         const void *wfn = nullptr;
+        // TCPEDIT_HIP_WAVE_FEAT=<mask>: add option groups to the instance choice (A/B runs)
+        static const uint32_t feat_env = getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
+        const uint32_t want = fast_feat(ch) | feat_env;
         for (const auto &wi : wave_inst)
-            if (!wfn && wi.grow == grow && (fast_feat(ch) & ~wi.feat) == 0) wfn = wi.fn;
+            if (!wfn && wi.grow == grow && (want & ~wi.feat) == 0) wfn = wi.fn;
         if (!wfn) return -1;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
         int fgrid = wave ? te_wave_grid() : te_fast_grid();

@@ -133,11 +133,27 @@ def pcap_fixed(n, size=64, seed=1, ipv6=False, proto=17):
     return PCAP_HDR.tobytes() + recs.tobytes()
 
 
-def pcap_imix(n, seed=1, chunk=1 << 20):
-    """n records cycling 64x7, 570x4, 1514x1 (deterministic 7:4:1)."""
+def _tag(recs, tci):
+    """(n, 16 + size) records -> (n, 20 + size): an 802.1Q tag {0x8100, tci} after the MACs"""
+    n, w = recs.shape
+    out = np.empty((n, w + 4), np.uint8)
+    out[:, :28] = recs[:, :28]
+    out[:, 28:32] = (0x81, 0x00, (tci >> 8) & 0xFF, tci & 0xFF)
+    out[:, 32:] = recs[:, 28:]
+    hdr = out[:, :16].copy().view("<u4")
+    hdr[:, 2] += 4
+    hdr[:, 3] += 4
+    out[:, :16] = hdr.view(np.uint8)
+    return out
+
+
+def pcap_imix(n, seed=1, chunk=1 << 20, vlan=None):
+    """n records cycling 64x7, 570x4, 1514x1 (deterministic 7:4:1); vlan=TCI: every
+    frame carries an 802.1Q tag (68/574/1518 bytes)."""
     rng = np.random.default_rng(seed)
     pat = IMIX_PATTERN
-    cyc_len = sum(16 + s for s in pat)
+    grow = 4 if vlan is not None else 0
+    cyc_len = sum(16 + s + grow for s in pat)
     parts = [PCAP_HDR.tobytes()]
     done = 0
     while done < n:
@@ -147,16 +163,18 @@ def pcap_imix(n, seed=1, chunk=1 << 20):
         off = 0
         counts = {s: pat.count(s) for s in set(pat)}
         made = {s: _records(_frames(rng, ncyc * counts[s], s, first_index=done), done) for s in counts}
+        if vlan is not None:
+            made = {s: _tag(r, vlan) for s, r in made.items()}
         used = {s: 0 for s in counts}
         for s in pat:
             rec = made[s][used[s]::counts[s]]
             used[s] += 1
-            buf[:, off:off + 16 + s] = rec
-            off += 16 + s
+            buf[:, off:off + 16 + s + grow] = rec
+            off += 16 + s + grow
         flat = buf.reshape(-1)
         if ncyc * len(pat) != m:  # trim the last partial cycle
             keep = m - (ncyc - 1) * len(pat)
-            end = (ncyc - 1) * cyc_len + sum(16 + s for s in pat[:keep])
+            end = (ncyc - 1) * cyc_len + sum(16 + s + grow for s in pat[:keep])
             flat = flat[:end]
         parts.append(flat.tobytes())
         done += m
