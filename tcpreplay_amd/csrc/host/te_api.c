@@ -471,7 +471,9 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     b->fast_tiles = (!proto.slot_mode && fast_capable(&t->cfg)) || proto.grow_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
     proto.wave = b->fast_kind == TE_FAST_WAVE;
-    proto.budget = proto.wave ? TE_WK_TILE_BYTES : b->fast_tiles ? TE_FK_TILE_BYTES : TE_SLOT_BYTES;
+    proto.budget = proto.wave        ? te_wave_tile_bytes(&t->cfg, proto.grow_fast)
+                   : b->fast_tiles ? TE_FK_TILE_BYTES
+                                   : TE_SLOT_BYTES;
     proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
     proto.stop_error_pkt = -1;
     proto.growth = rec_growth(&t->cfg);
@@ -930,6 +932,12 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.fast = b->fast_tiles && !fast_lane_off() &&
              ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)));
     L.fast_v6 = fast_v6_ok(c);
+    /* a batch whose input + output outgrow the 256 MiB Infinity Cache streams through it:
+       nontemporal loads and stores (TCPEDIT_HIP_STREAM=0/1 overrides, for A/B runs) */
+    {
+        const char *e = getenv("TCPEDIT_HIP_STREAM");
+        L.stream = e && *e ? atoi(e) != 0 : (b->in_len + b->out_cap) > ((uint64_t)256 << 20);
+    }
     L.fast_kind = b->fast_kind;
     L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
     if (L.fast && b->gen_hint_ok && b->gen_hint_gen == t->cfg_gen)

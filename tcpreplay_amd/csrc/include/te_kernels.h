@@ -112,6 +112,7 @@ typedef struct {
     int generic_only;         /* run only the generic pass over the tiles the last fast launch listed */
     int out_fgrid;            /* set by te_launch_edit: blocks of the fast-lane launch (slots written) */
     int fast_v6;              /* IPv6 packets may take the fast lane (no non-octet v6 CIDR maps) */
+    int stream;               /* wave lane: nontemporal loads/stores (the batch outgrows the MALL) */
     uint32_t *tile_list;      /* device: n_tiles entries */
     uint32_t *list_cnt;       /* device: 2 counts; launch parity p appends to [p] and zeroes [p^1] */
     uint32_t parity;
@@ -145,6 +146,8 @@ int te_launch_edit(te_launch_t *L, hipStream_t stream);
 int te_launch_q8(te_launch_t *L, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
+/* tile budget of the wave-lane instance the config launches (grow: --enet-vlan=add) */
+uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int grow);
 
 #ifdef __cplusplus
 }

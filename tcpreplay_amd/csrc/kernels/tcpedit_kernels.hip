@@ -45,6 +45,9 @@ typedef TE_AS_GLOBAL uint8_t g_u8;
 typedef TE_AS_GLOBAL const uint8_t g_cu8;
 typedef TE_AS_GLOBAL const uint4 g_cu4;
 typedef TE_AS_GLOBAL uint4 g_u4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // for the nontemporal builtins
+typedef TE_AS_GLOBAL u32x4 g_v4;
+typedef TE_AS_GLOBAL const u32x4 g_cv4;
 }  // namespace
 #include "fast_lane.hpp"
 namespace {
@@ -616,6 +619,8 @@ struct FastArgs {
     uint32_t in_swapped, in_nsec, v6_ok;
     uint32_t seed_sw, seed_on, skip_bcast;  // te_wave_tiles' phase-A knobs (fl::Knobs), in SGPRs
     uint32_t vlan_tag_word;                 // GROW: the 4 pushed bytes {TPID, TCI} as a LE dword
+    uint32_t stream;                        // nontemporal span loads and output stores (a batch larger
+                                            // than the 256 MiB Infinity Cache: read once, written once)
 };
 
 // the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
@@ -995,6 +1000,22 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_MIN_BLOCKS
 #define TE_WK_MIN_BLOCKS 4  // blocks per CU (= waves per SIMD at 256 threads): 128 VGPRs
 #endif
+// the lean instances (no option group that reads the cfg tables: no LDS copy of them)
+// fit one more block per CU -- 5 waves per SIMD at <= 102 VGPRs, 31 KiB of LDS a block
+#ifndef TE_WK_LEAN_BLOCKS
+#define TE_WK_LEAN_BLOCKS 5
+#endif
+// The lean instances also cut tiles to TE_WK_LEAN_TILE_BYTES: 63 C2 records (80 B) fill five
+// 16-byte chunk loads per lane exactly, where 64 records and the next header need six.
+#ifndef TE_WK_LEAN_TILE_BYTES
+#define TE_WK_LEAN_TILE_BYTES 5120
+#endif
+template <uint32_t F>
+struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
+    static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
+    static constexpr int blocks = reads ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
+    static constexpr int tile = reads ? TE_WK_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
+};
 #ifndef TE_WK_STORE_BARRIER
 #define TE_WK_STORE_BARRIER 1
 #endif
@@ -1003,11 +1024,14 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #endif
 constexpr int WKB = TE_WK_BLOCK;
 constexpr int WK_NW = WKB / 64;                          // waves (tiles in flight) per block
-constexpr int WK_KL = TE_WK_TILE_BYTES / 16 / 64;        // 16-byte chunks per lane per tile
-static_assert(TE_WK_TILE_BYTES % 1024 == 0 && WK_KL <= 8, "whole chunks per lane, <= 8 chunk registers");
-constexpr int WK_IMG = LDS_FRONT + TE_WK_TILE_BYTES + 128;  // image + phase-A window overrun
-constexpr int WK_NCH = TE_WK_TILE_BYTES / 16 + 2;           // chunk prefix (+ total)
-static_assert(WK_IMG % 16 == 0, "16-byte aligned wave images");
+// per tile budget TB: 16-byte chunks per lane, the LDS image (+ phase-A window overrun),
+// the chunk prefix (+ total)
+constexpr int wk_kl(int tb) { return tb / 16 / 64; }
+constexpr int wk_img(int tb) { return LDS_FRONT + tb + 128; }
+constexpr int wk_nch(int tb) { return tb / 16 + 2; }
+static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
+static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
+static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
 
 // TE_WK_STAMPS builds (diagnostics only): s_memtime per phase, summed per wave,
 // printed by a few waves at exit
@@ -1036,10 +1060,10 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
                       __builtin_amdgcn_readlane((int)v, 47) | __builtin_amdgcn_readlane((int)v, 63));
 }
 
-__device__ __forceinline__ bool wk_solo(const te_tile_t &tl) {
+__device__ __forceinline__ bool wk_solo(const te_tile_t &tl, uint32_t tb) {
     // (the last test: a span the image cannot hold never reaches the lane, whatever the cut)
     return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH ||
-           (uint32_t)(tl.span_off & 15) + tl.span_len + 16u > (uint32_t)TE_WK_TILE_BYTES;
+           (uint32_t)(tl.span_off & 15) + tl.span_len + 16u > tb;
 }
 
 // GROW: caplen and len of the record header at LDS byte h (any alignment) + 4, the
@@ -1071,7 +1095,7 @@ __device__ __forceinline__ void hdr_grow4(uint8_t *S, uint32_t h) {
 // one mark per tag and a prefix max.  OS: the tile's output start in gout coordinates.
 __device__ __forceinline__ void wk_store_grow(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
                                               uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t my_rel,
-                                              bool on, uint32_t tag, int lane) {
+                                              bool on, uint32_t tag, int lane, bool stream) {
     const uint64_t OE = OS + span_len + 4ull * npkt;
     const uint64_t C0 = (OS + 15) & ~15ull;
     const uint32_t o0 = (uint32_t)(C0 - OS);
@@ -1125,7 +1149,10 @@ __device__ __forceinline__ void wk_store_grow(const uint8_t *S, uint32_t *P, g_u
             const uint32_t vn = ((tag >> (8 * tn)) & mn) | (after & ~mn);    // tag started tn bytes earlier
             w[i] = t >= 4 ? before : (t <= -4 ? after : (t >= 0 ? vp : vn));
         }
-        *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (stream)
+            __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (g_v4 *)(gout + C0 + 16ull * cc));
+        else
+            *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
     }
     // the leading bytes (output start to the first 16-byte boundary: before any tag)
     const uint64_t q = (uint32_t)lane < o0 ? OS + (uint32_t)lane : C0;  // others repeat byte C0
@@ -1144,17 +1171,20 @@ __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
 }
 
 template <uint32_t F, int DEPTH, bool GROW>
-__global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs a) {
+__global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
+    constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = wk_img(TB), WK_NCH = wk_nch(TB);
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
     __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
-    __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
+    // per-run tables: copied only by instances whose option groups read them
+    __shared__ __attribute__((aligned(16))) uint8_t cfg_raw[WkCfg<F>::reads ? sizeof(te_dev_cfg_t) : 16];
+    const te_dev_cfg_t &cfg = *(const te_dev_cfg_t *)cfg_raw;
     __shared__ unsigned long long red[WK_NW][3];
     const int tid = threadIdx.x;
     int lane = tid & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
-    {
+    if constexpr (WkCfg<F>::reads) {
         const uint32_t *src = (const uint32_t *)a.cfg;
-        uint32_t *dst = (uint32_t *)&cfg;
+        uint32_t *dst = (uint32_t *)cfg_raw;
         for (int i = tid; i < (int)(sizeof(te_dev_cfg_t) / 4); i += WKB) dst[i] = src[i];
     }
     if (blockIdx.x == 0) {
@@ -1174,6 +1204,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     const TE_AS_CONST te_tile_t *tiles = (const TE_AS_CONST te_tile_t *)a.tiles;
     const TE_AS_CONST uint16_t *pkt_rel = (const TE_AS_CONST uint16_t *)a.pkt_rel;
     const fl::Knobs kn{a.seed_sw, a.seed_on != 0, a.skip_bcast != 0};
+    const bool stream = a.stream != 0;  // wave-uniform (an SGPR): a scalar branch per batch of loads/stores
     __syncthreads();
 
     // a tile in flight: its descriptor, its chunks in named registers, and this lane's
@@ -1197,11 +1228,16 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
     auto issue = [&](Span &R, const te_tile_t &tl) __attribute__((always_inline)) {
         R.tl = tl;
         const uint64_t a0_ = tl.span_off & ~15ull;
-        const uint32_t nc_ = wk_solo(tl) ? 1u : (uint32_t)((tl.span_off + tl.span_len + extra - a0_ + 15) >> 4);
-#define WK_LD(k)                                                           \
-    if constexpr (k < WK_KL) {                                             \
-        const uint32_t c = umin32((uint32_t)lane + k * 64u, nc_ - 1u);     \
-        R.v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));               \
+        const uint32_t nc_ = wk_solo(tl, TB) ? 1u : (uint32_t)((tl.span_off + tl.span_len + extra - a0_ + 15) >> 4);
+#define WK_LD(k)                                                                              \
+    if constexpr (k < WK_KL) {                                                                \
+        const uint32_t c = umin32((uint32_t)lane + k * 64u, nc_ - 1u);                        \
+        if (stream) {                                                                         \
+            const u32x4 nv = __builtin_nontemporal_load((g_cv4 *)(gin + a0_ + ((uint64_t)c << 4))); \
+            R.v##k = make_uint4(nv.x, nv.y, nv.z, nv.w);                                      \
+        } else {                                                                              \
+            R.v##k = *(g_cu4 *)(gin + a0_ + ((uint64_t)c << 4));                              \
+        }                                                                                     \
     }
         WK_EACH(WK_LD)
 #undef WK_LD
@@ -1231,7 +1267,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             const uint32_t npkt = tile.npkt;
             const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
             const uint32_t g0 = (uint32_t)(G0 - A0);
-            if (wk_solo(tile)) {  // a record larger than the image: the generic lane
+            if (wk_solo(tile, TB)) {  // a record larger than the image: the generic lane
                 if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
                 return;
             }
@@ -1383,7 +1419,7 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
             // ---- store: the chunks that start in the span, then the leading bytes ----
             if constexpr (GROW) {
                 wk_store_grow(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0, my_rel, on,
-                              a.vlan_tag_word, lane);
+                              a.vlan_tag_word, lane, stream);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -1393,9 +1429,14 @@ __global__ void __launch_bounds__(WKB, TE_WK_MIN_BLOCKS) te_wave_tiles(FastArgs 
                 uint4 w0, w1, w2, w3, w4, w5, w6, w7;
 #define WK_RD(k) \
         if constexpr (k < WK_KL) w##k = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
-#define WK_WR(k)                                                                                   \
-        if constexpr (k < WK_KL)                                                                       \
-            *(g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)) = w##k;
+#define WK_WR(k)                                                                                       \
+        if constexpr (k < WK_KL) {                                                                         \
+            g_u4 *dk = (g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)); \
+            if (stream)                                                                                    \
+                __builtin_nontemporal_store((u32x4){w##k.x, w##k.y, w##k.z, w##k.w}, (g_v4 *)dk);         \
+            else                                                                                           \
+                *dk = w##k;                                                                                \
+        }
                 WK_EACH(WK_RD)
 #if TE_WK_STORE_BARRIER
                 __builtin_amdgcn_sched_barrier(0);
@@ -1800,15 +1841,28 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_PORTMAP | TE_FF_RWIP, 1, false) X(TE_FF_ALL, 1, false) X(TE_FF_ALL, 1, true)                \
     X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, false) X(TE_FF_HDR | TE_FF_INCR, 1, false)             \
     X(TE_FF_ALLX, 1, false) X(TE_FF_ALLX, 1, true)
-static const struct {
+static struct {
     uint32_t feat;
     bool grow;
     const void *fn;
+    int grid;  // resident blocks of this instance (CUs x its occupancy), 0 until asked
 } wave_inst[] = {
-#define TE_WI(f, d, g) {f, g, (const void *)te_wave_tiles<f, d, g>},
+#define TE_WI(f, d, g) {f, g, (const void *)te_wave_tiles<f, d, g>, 0},
     TE_WAVE_INSTANCES(TE_WI)
 #undef TE_WI
 };
+
+static uint32_t fast_feat(const te_dev_cfg_t *c);
+// the first (smallest) instance covering the config's option groups;
+// TCPEDIT_HIP_WAVE_FEAT=<mask> adds groups to the choice (A/B runs)
+static int wave_pick(uint32_t want, bool grow) {
+    static const uint32_t feat_env =
+        getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
+    want |= feat_env;
+    for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k)
+        if (wave_inst[k].grow == grow && (want & ~wave_inst[k].feat) == 0) return k;
+    return -1;
+}
 
 static uint32_t fast_feat(const te_dev_cfg_t *c) {
     return (c->mac_mask ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
@@ -1820,14 +1874,35 @@ static uint32_t fast_feat(const te_dev_cfg_t *c) {
            (c->fixcsum ? 0u : TE_FF_INCR);
 }
 
+static int wave_inst_grid(int k) {
+    if (wave_inst[k].grid) return wave_inst[k].grid;
+    int cus = cu_count(), per_cu = 0;
+    if (!cus) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wave_inst[k].fn, WKB, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    wave_inst[k].grid = cus * per_cu;
+    return wave_inst[k].grid;
+}
+
+// the tile budget of the wave-lane instance a config launches (the host cuts tiles to it)
+static int wave_pick(uint32_t want, bool grow);
+extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int grow) {
+    const int k = wave_pick(fast_feat(c), grow != 0);
+    if (k < 0) return TE_WK_TILE_BYTES;
+    return (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) ? TE_WK_TILE_BYTES
+                                                                                       : TE_WK_LEAN_TILE_BYTES;
+}
+
+// the largest wave-lane grid of any instance (the host sizes the per-block slots by it)
 extern "C" int te_wave_grid(void) {
     static int c = 0;
     if (c) return c;
-    int cus = cu_count(), per_cu = 0;
-    if (!cus) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, te_wave_tiles<TE_FF_ALL, 1, false>, WKB, 0) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-    c = cus * per_cu;
+    int m = 0;
+    for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k) {
+        const int g = wave_inst_grid(k);
+        m = g > m ? g : m;
+    }
+    c = m;
     return c;
 }
 
@@ -1922,6 +1997,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.in_swapped = L->in_swapped;
         f.in_nsec = L->in_nsec;
         f.v6_ok = (uint32_t)L->fast_v6;
+        f.stream = (uint32_t)L->stream;
         f.slots = (unsigned long long *)L->slots;
         f.counters_next = (unsigned long long *)L->counters_next;
         const te_dev_cfg_t *ch = L->cfg_host;
@@ -1939,14 +2015,11 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             f.vlan_tag_word = 0;
         }
         const void *wfn = nullptr;
-        // TCPEDIT_HIP_WAVE_FEAT=<mask>: add option groups to the instance choice (A/B runs)
-        static const uint32_t feat_env = getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
-        const uint32_t want = fast_feat(ch) | feat_env;
-        for (const auto &wi : wave_inst)
-            if (!wfn && wi.grow == grow && (want & ~wi.feat) == 0) wfn = wi.fn;
-        if (!wfn) return -1;
+        const int wk = wave_pick(fast_feat(ch), grow);
+        if (wk < 0) return -1;
+        wfn = wave_inst[wk].fn;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
-        int fgrid = wave ? te_wave_grid() : te_fast_grid();
+        int fgrid = wave ? wave_inst_grid(wk) : te_fast_grid();
         if (fgrid < 1) return -1;
         const uint32_t need = wave ? (L->n_tiles + WK_NW - 1) / WK_NW : L->n_tiles;
         if ((uint32_t)fgrid > need) fgrid = (int)need;
