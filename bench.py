@@ -51,8 +51,8 @@ WORKLOADS = {
             "--ttl=+1 --tos=7 on IMIX 64/570/1514 7:4:1 (TTL change -> full recompute, tcpedit.c:195,338)"),
     "vdel": ("pcap_imix", dict(vlan=0xB02D), ["--enet-vlan=del", "--fixcsum"],
              "--enet-vlan=del --fixcsum on 802.1Q-tagged IMIX 68/574/1518 (every record -4 bytes)"),
-    "efcs": ("pcap_imix", dict(), ["--efcs", "--fixcsum"],
-             "--efcs --fixcsum on IMIX 64/570/1514 7:4:1 (every record -4 bytes)"),
+    "efcs": ("pcap_imix", dict(fcs=True), ["--efcs", "--fixcsum"],
+             "--efcs --fixcsum on IMIX 68/574/1518 7:4:1 frames captured with their FCS (every record -4 bytes)"),
 }
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
                    "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000}

@@ -49,7 +49,7 @@ struct tcpedit_batch_s {
     int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
     int grow_off;            /* a run found a record that broke static_grow placement ... */
     uint32_t grow_off_gen;   /* ... under this cfg_gen: place by scan from then on */
-    int last_grow;           /* the last launch placed records by static_grow */
+    int last_grow;           /* the last launch placed records by static_grow (+4) or static_shrink (-4) */
     int grow_never;          /* pipelined chunk slots: no rerun on a violation, so always scan */
     uint32_t grow_bad;       /* its violation word, read back */
     int fast_tiles;          /* tiles were cut for the fast lane ... */
@@ -147,6 +147,27 @@ static int fast_capable_grow(const te_dev_cfg_t *c)
     return c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs &&
            !c->fuzz_seed && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate && !c->skip_soft_errors &&
            !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+}
+
+/* a VLAN pop (--enet-vlan=del) or --efcs as the only size change: every record can shrink
+ * by exactly 4 bytes (a record that does not -- untagged, caplen != len, an error -- breaks
+ * the static placement and the batch is placed by scan instead).  Returns the TE_SZ_ kind. */
+static int static_shrink_kind(const te_dev_cfg_t *c)
+{
+    if (c->encoder != TE_ENC_EN10MB || c->vlan == TE_VLAN_ADD || c->fixlen != TE_FIXLEN_OFF || c->mtu_truncate ||
+        c->skip_soft_errors || c->fuzz_seed)
+        return TE_SZ_NONE;
+    if (c->efcs && c->vlan == TE_VLAN_OFF)
+        return TE_SZ_EFCS;
+    if (!c->efcs && c->vlan == TE_VLAN_DEL)
+        return TE_SZ_VDEL;
+    return TE_SZ_NONE;
+}
+
+/* ... and the wave lane carries it (its fast-lane conditions) */
+static int fast_capable_shrink(const te_dev_cfg_t *c)
+{
+    return static_shrink_kind(c) != TE_SZ_NONE && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
 
 /* IPv6 rewrites with a non-octet target mask keep the reference's stray write
@@ -468,10 +489,16 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
        are cut to the wave image (their per-record slots then fit the generic kernel's) */
     proto.grow_fast = !proto.pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
                       fast_kind_pref() == TE_FAST_WAVE;
-    b->fast_tiles = (!proto.slot_mode && fast_capable(&t->cfg)) || proto.grow_fast;
+    /* ... and a VLAN pop or --efcs (native-order microsecond input only) */
+    const int shrink_fast = !proto.slot_mode && fast_capable_shrink(&t->cfg) && !b->swapped && !b->nsec;
+    b->fast_tiles = (!proto.slot_mode && fast_capable(&t->cfg)) || proto.grow_fast || shrink_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
+    if (shrink_fast && !proto.grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
+        b->fast_tiles = 0, b->fast_kind = 0;
     proto.wave = b->fast_kind == TE_FAST_WAVE;
-    proto.budget = proto.wave        ? te_wave_tile_bytes(&t->cfg, proto.grow_fast)
+    proto.budget = proto.wave        ? te_wave_tile_bytes(&t->cfg, proto.grow_fast ? TE_SZ_GROW
+                                                                   : shrink_fast    ? static_shrink_kind(&t->cfg)
+                                                                                    : TE_SZ_NONE)
                    : b->fast_tiles ? TE_FK_TILE_BYTES
                                    : TE_SLOT_BYTES;
     proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
@@ -927,10 +954,17 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
                     !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap && !c->fuzz_seed &&
                     !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env();
+    /* a VLAN pop or --efcs as the only size change: outputs at input offset - 4 x index
+       (checked record by record like static_grow) */
+    L.static_shrink = !b->slot_layout && !b->has_zero_cap && !b->swapped && !b->nsec &&
+                              !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env()
+                          ? static_shrink_kind(c)
+                          : TE_SZ_NONE;
     L.grow_bad = (uint32_t *)(b->d_ws + WS_GROW_BAD);
-    b->last_grow = L.static_grow;
+    b->last_grow = L.static_grow ? 4 : L.static_shrink ? -4 : 0;
     L.fast = b->fast_tiles && !fast_lane_off() &&
-             ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)));
+             ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)) ||
+              (L.static_shrink && fast_capable_shrink(c)));
     L.fast_v6 = fast_v6_ok(c);
     /* a batch whose input + output outgrow the 256 MiB Infinity Cache streams through it:
        nontemporal loads and stores (TCPEDIT_HIP_STREAM=0/1 overrides, for A/B runs) */
@@ -1120,7 +1154,7 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
-        b->counters[TE_CNT_BYTES_OUT] += v[1] + (b->last_grow ? 4 * v[0] : 0); /* + the pushed tags */
+        b->counters[TE_CNT_BYTES_OUT] += v[1] + (uint64_t)((int64_t)b->last_grow * (int64_t)v[0]); /* +- 4 a record */
         b->counters[TE_CNT_EDITED] += v[2];
     }
     if (b->last_fast) { /* same batch + same config lists the same tiles next time */

@@ -34,6 +34,11 @@ extern "C" {
 #define TE_TILE_SOLO 1u        /* te_tile_t.flags: a record too large for a wave-lane image */
 #define TE_FAST_BLOCK 1        /* fast-lane kinds: te_fast_tiles (one block per tile) ... */
 #define TE_FAST_WAVE 2         /* ... or te_wave_tiles (one wave per tile) */
+/* the one record-size change a wave-lane instance (and static placement) carries */
+#define TE_SZ_NONE 0
+#define TE_SZ_GROW 1           /* --enet-vlan=add: +4 per record */
+#define TE_SZ_VDEL 2           /* --enet-vlan=del over tagged records: -4 */
+#define TE_SZ_EFCS 3           /* --efcs: -4 */
 /* option groups of the fast lane: a te_wave_tiles instance compiles in the groups of
    its mask, and te_launch_edit launches the smallest instance covering the config */
 #define TE_FF_MAC 1u     /* --enet-dmac / --enet-smac */
@@ -100,6 +105,9 @@ typedef struct {
                                  change), so record i (0-based in the launch) sits at its input offset
                                  + 4 i: no scan, no look-back.  A record that breaks this (and is not a
                                  hard error, which truncates the output there) sets *grow_bad */
+    int static_shrink;        /* TE_SZ_VDEL / TE_SZ_EFCS: every record shrinks by exactly 4
+                                 bytes (a VLAN pop, or --efcs, as the only size change): record i sits
+                                 at its input offset - 4 i; a record that breaks it sets *grow_bad */
     uint32_t *grow_bad;       /* device word, zeroed with the error words */
     /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
@@ -146,8 +154,8 @@ int te_launch_edit(te_launch_t *L, hipStream_t stream);
 int te_launch_q8(te_launch_t *L, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
-/* tile budget of the wave-lane instance the config launches (grow: --enet-vlan=add) */
-uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int grow);
+/* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */
+uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz);
 
 #ifdef __cplusplus
 }

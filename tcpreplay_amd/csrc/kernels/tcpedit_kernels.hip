@@ -75,6 +75,7 @@ struct LaunchArgs {
     uint64_t rec0;                   // static_off: input offset of the first record
     uint32_t static_off;             // output offsets == input offsets (size-preserving config)
     uint32_t static_grow;            // output offset = input offset + 4 x record index (VLAN add)
+    uint32_t static_shrink;          // output offset = input offset - 4 x record index (VLAN pop, --efcs)
     uint32_t *grow_bad;              // set when a record breaks static_grow's placement
     // after te_fast_tiles: only the listed tiles are edited here, and the last
     // block folds the fast kernel's per-block counters into `counters`
@@ -381,7 +382,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     // ---- tile output offsets ----
     // static_off: sizes are preserved, so output offsets are the input offsets
     // (no scan, no look-back); otherwise block scan + decoupled look-back.
-    const bool stat = a.static_off != 0, grow = a.static_grow != 0;
+    const bool stat = a.static_off != 0, shrink = a.static_shrink != 0, grow = a.static_grow != 0 || shrink;
     uint32_t tile_total, opos;
     bool keep = true;
     if (MODE == MODE_CONTIG && stat) {
@@ -390,13 +391,14 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (tid < TE_CNT__N) sh.cnt[tid] = 0;
         __syncthreads();
     } else if (grow) {
-        // every record before this one grew by 4 bytes (or the output ends at an earlier
-        // hard error): static placement, checked record by record
-        opos = my_rel + 4u * (uint32_t)tid;
-        tile_total = tile.span_len + 4u * npkt;
+        // every record before this one grew (shrank) by 4 bytes (or the output ends at an
+        // earlier hard error): static placement, checked record by record
+        opos = shrink ? my_rel - 4u * (uint32_t)tid : my_rel + 4u * (uint32_t)tid;
+        tile_total = shrink ? tile.span_len - 4u * npkt : tile.span_len + 4u * npkt;
         if (tid < (int)npkt) {
             sh.opfx[tid] = opos;
-            if ((st & TE_ST_RC_MASK) != TE_ST_RC_ERROR && out_sz != 16 + my_cap + 4) atomicOr(a.grow_bad, 1u);
+            if ((st & TE_ST_RC_MASK) != TE_ST_RC_ERROR && out_sz != (shrink ? 16 + my_cap - 4 : 16 + my_cap + 4))
+                atomicOr(a.grow_bad, 1u);
         }
         if (tid == 0) {
             sh.opfx[npkt] = tile_total;
@@ -440,7 +442,9 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         }
     }
     if (stat || grow) {
-        if (tid == 0) sh.out_excl = tile.span_off - a.rec0 + (grow ? 4ull * tile.first_pkt : 0ull);
+        if (tid == 0)
+            sh.out_excl = tile.span_off - a.rec0 +
+                          (shrink ? -4ull * tile.first_pkt : (grow ? 4ull * tile.first_pkt : 0ull));
     } else if (tid < 64) {
         const unsigned long long e = lookback(a.tile_state, t, tile_total, a.err);
         if (tid == 0) sh.out_excl = e;
@@ -626,12 +630,17 @@ struct FastArgs {
 // the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
 // (caplen + 2) / 4, read from the unedited image at window start wa (packet offset -2);
 // 0 when caplen + 2 is a multiple of 4 or the dword lies past the window
-__device__ __forceinline__ uint32_t window_part(const uint8_t *S, uint32_t wa, uint32_t caplen) {
+// (window_part_n: over a window of NWX dwords)
+template <int NWX>
+__device__ __forceinline__ uint32_t window_part_n(const uint8_t *S, uint32_t wa, uint32_t caplen) {
     const uint32_t t = caplen + 2, k = t >> 2, nb = t & 3u;
-    const uint32_t q = (wa & ~3u) + 4u * umin32(k, fl::NW - 1);
+    const uint32_t q = (wa & ~3u) + 4u * umin32(k, NWX - 1);
     const uint32_t e0 = *(const uint32_t *)(S + q), e1 = *(const uint32_t *)(S + q + 4);
-    const uint32_t keep = (nb != 0 && k < (uint32_t)fl::NW) ? ((1u << (8 * nb)) - 1u) : 0u;
+    const uint32_t keep = (nb != 0 && k < (uint32_t)NWX) ? ((1u << (8 * nb)) - 1u) : 0u;
     return __builtin_amdgcn_alignbyte(e1, e0, wa & 3u) & keep;
+}
+__device__ __forceinline__ uint32_t window_part(const uint8_t *S, uint32_t wa, uint32_t caplen) {
+    return window_part_n<fl::NW>(S, wa, caplen);
 }
 
 // one's-complement sum of the LE 16-bit words (absolute pairing) of bytes [b0, b1) of chunk c
@@ -1066,14 +1075,17 @@ __device__ __forceinline__ bool wk_solo(const te_tile_t &tl, uint32_t tb) {
            (uint32_t)(tl.span_off & 15) + tl.span_len + 16u > tb;
 }
 
-// GROW: caplen and len of the record header at LDS byte h (any alignment) + 4, the
-// VLAN push's length change (tcpedit.c:112-113)
-__device__ __forceinline__ void hdr_grow4(uint8_t *S, uint32_t h) {
+// size-changing instances (SZ): the one length change every record takes
+enum : int { SZ_NONE = TE_SZ_NONE, SZ_GROW = TE_SZ_GROW, SZ_VDEL = TE_SZ_VDEL, SZ_EFCS = TE_SZ_EFCS };
+
+// caplen and len of the record header at LDS byte h (any alignment) + delta: the VLAN
+// push's +4 (tcpedit.c:112-113), the VLAN pop's or --efcs's -4 (tcpedit.c:78-84)
+__device__ __forceinline__ void hdr_add4(uint8_t *S, uint32_t h, uint32_t delta) {
     const uint32_t h8 = h + 8, al = h8 & ~3u, s8 = 8u * (h8 & 3u);
     uint32_t *w = (uint32_t *)(S + al);
     const uint32_t q0 = w[0], q1 = w[1], q2 = w[2];
-    const uint32_t cap = __builtin_amdgcn_alignbyte(q1, q0, h8 & 3u) + 4u;
-    const uint32_t len = __builtin_amdgcn_alignbyte(q2, q1, h8 & 3u) + 4u;
+    const uint32_t cap = __builtin_amdgcn_alignbyte(q1, q0, h8 & 3u) + delta;
+    const uint32_t len = __builtin_amdgcn_alignbyte(q2, q1, h8 & 3u) + delta;
     if (s8 == 0) {
         w[0] = cap;
         w[1] = len;
@@ -1159,6 +1171,77 @@ __device__ __forceinline__ void wk_store_grow(const uint8_t *S, uint32_t *P, g_u
     gout[q] = img[(uint32_t)(q - OS)];
 }
 
+// SHRINK store (VLAN pop, --efcs): record j loses the 4 input bytes at tile-relative
+// offset D_j (VLAN pop: rel_j + 28, its TPID and TCI, so the inner type field lands at
+// packet offset 12 as dlt_en10mb_encode leaves it; --efcs: rel_j + 16 + caplen_j - 4, its
+// FCS).  Output byte
+// y (tile-relative) is input byte y + 4 m(y), m(y) = #{j : Y_j <= y}, Y_j = D_j - 4 j.
+// Consecutive Y_j are >= 58 bytes apart (the smallest record on the lane), so a 16-byte
+// output chunk meets at most one: its bytes come from the input 4 m and 4 (m + 1) bytes
+// on, both dword-aligned in LDS.  M[c] = m per chunk as in wk_store_grow.  Dj: this
+// lane's D_j; OS: the tile's output start in gout coordinates.
+__device__ __forceinline__ void wk_store_shrink(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
+                                                uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t Dj,
+                                                bool on, int lane, bool stream) {
+    const uint64_t OE = OS + span_len - 4ull * npkt;
+    const uint64_t C0 = (OS + 15) & ~15ull;
+    const uint32_t o0 = (uint32_t)(C0 - OS);
+    const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);
+    uint16_t *M = (uint16_t *)P;  // 512 entries
+    uint32_t *T = P + 256;        // 64 boundaries + sentinel
+    *(uint4 *)(M + 8 * lane) = make_uint4(0, 0, 0, 0);
+    if (on) {
+        const uint32_t Yj = Dj - 4u * (uint32_t)lane;
+        T[lane] = Yj;
+        const uint32_t cj = (Yj - o0 + 15u) >> 4;  // first chunk starting at or after Y_j
+        if (cj < nown) M[cj] = (uint16_t)(lane + 1);
+    }
+    if (lane == 0) T[npkt] = 0x7fffffffu;
+    {  // prefix max over M, 8 entries a lane
+        const uint4 q = *(const uint4 *)(M + 8 * lane);
+        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
+                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+#pragma unroll
+        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
+        uint32_t incl = e[7];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl = max(incl, y);
+        }
+        uint32_t excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
+        *(uint4 *)(M + 8 * lane) =
+            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+    }
+    const uint8_t *img = S + LDS_FRONT + g0;  // input byte x of the tile
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {  // lanes past the output repeat its last chunk (same bytes)
+        const uint32_t cc = umin32((uint32_t)lane + 64u * k, nown - 1u);
+        const uint32_t m = M[cc], Ym = T[m];
+        const uint32_t o = o0 + 16u * cc;
+        const uint32_t *D = (const uint32_t *)(img + o + 4u * m);
+        const uint32_t dd[5] = {D[0], D[1], D[2], D[3], D[4]};
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = (int)Ym - (int)(o + 4u * (uint32_t)i);  // the boundary relative to this dword
+            const uint32_t mk = (1u << (8 * (t < 1 ? 1 : (t > 3 ? 3 : t)))) - 1u;
+            const uint32_t mixed = (dd[i] & mk) | (dd[i + 1] & ~mk);
+            w[i] = t >= 4 ? dd[i] : (t <= 0 ? dd[i + 1] : mixed);
+        }
+        if (stream)
+            __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (g_v4 *)(gout + C0 + 16ull * cc));
+        else
+            *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // the leading bytes (output start to the first 16-byte boundary: before any deletion)
+    const uint64_t q = (uint32_t)lane < o0 ? OS + (uint32_t)lane : C0;  // others repeat byte C0
+    gout[q] = img[(uint32_t)(q - OS)];
+}
+
 // big-endian / nanosecond input: a record header in host order and microseconds
 __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     const uint32_t ts_sec = ld_hdr32(rec, swp), cl = ld_hdr32(rec + 8, swp), ln = ld_hdr32(rec + 12, swp);
@@ -1170,9 +1253,23 @@ __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     st32(rec + 12, ln);
 }
 
-template <uint32_t F, int DEPTH, bool GROW>
+// the window of a record whose VLAN tag the pop removes, as the popped packet sees it:
+// packet' bytes [-2, 12) are the input's, [12, 78) the input's [16, 82).  HX: the input
+// window [-2, 82) (NW + 1 dwords)
+__device__ __forceinline__ void vdel_view(uint32_t (&H)[fl::NW], const uint32_t (&HX)[fl::NW + 1]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) H[i] = HX[i];
+    H[3] = (HX[3] & 0xffffu) | (HX[4] & 0xffff0000u);
+#pragma unroll
+    for (int i = 4; i < fl::NW; ++i) H[i] = HX[i + 1];
+}
+
+template <uint32_t F, int DEPTH, int SZ>
 __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = wk_img(TB), WK_NCH = wk_nch(TB);
+    constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
+    // VLAN pop: the window reaches 4 input bytes further (the packet' view skips the tag)
+    constexpr int XW = VDEL ? 1 : 0;
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
     __shared__ __attribute__((aligned(16))) uint32_t PB[WK_NW][WK_NCH];
     // per-run tables: copied only by instances whose option groups read them
@@ -1196,8 +1293,8 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
     uint32_t *P = PB[wid];
     const bool swp = a.in_swapped != 0, nsec = a.in_nsec != 0, conv = swp || nsec;
     const bool explicit_dir = a.fixed_dir >= 0;
-    // the next record's header rides along (conversion; GROW: its caplen/len + 4)
-    const uint32_t extra = (conv || GROW) ? 16u : 0u;
+    // the next record's header rides along (conversion; GROW / SHRINK: its caplen/len +- 4)
+    const uint32_t extra = (conv || SZ != SZ_NONE) ? 16u : 0u;
     g_cu8 *gin = (g_cu8 *)a.in;
     g_u8 *gout = (g_u8 *)a.out + ((int64_t)a.out_base - (int64_t)a.rec0);
     const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
@@ -1294,16 +1391,30 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
             // the window to packet offset -2; each H[i] can take d[i]'s register
             uint32_t H[fl::NW], d0;
+            // SHRINK: the packet's caplen/len after the pop or the FCS strip (a record whose
+            // caplen != len keeps its caplen under --efcs: phase A defers it)
+            const uint32_t ecap = SHRINK ? caplen - 4u : caplen, elen = SHRINK ? len - 4u : len;
+            bool tagged = true;  // VDEL: a single 802.1Q / 802.1ad / QinQ-TPID tag at offset 12
             {
                 const uint32_t A4 = wa & ~3u, sh = wa & 3u;
-                uint32_t d[fl::NW + 1];
+                uint32_t d[fl::NW + 1 + XW];
 #pragma unroll
-                for (int j = 0; j <= fl::NW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
+                for (int j = 0; j <= fl::NW + XW; ++j) d[j] = *(const uint32_t *)(S + A4 + 4 * j);
+                if constexpr (VDEL) {
+                    uint32_t HX[fl::NW + 1];
 #pragma unroll
-                for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                    for (int i = 0; i <= fl::NW; ++i) HX[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                    const uint32_t tpid = HX[3] >> 16;  // raw LE: 0x8100, 0x88a8, 0x9100
+                    tagged = tpid == 0x0081u || tpid == 0xa888u || tpid == 0x0091u;
+                    vdel_view(H, HX);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < fl::NW; ++i) H[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+                }
                 d0 = d[0];
             }
-            const uint32_t part = window_part(S, wa, caplen);
+            // the partly valid dword: packet' dword k' is input dword k' + 1 under the pop
+            const uint32_t part = VDEL ? window_part_n<fl::NW + 1>(S, wa, caplen) : window_part(S, wa, ecap);
             int dir = TE_DIR_C2S;
             if (explicit_dir) {
                 dir = a.fixed_dir;
@@ -1334,10 +1445,11 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
                 nosend = true;
             }
 #else
-            bool ok = fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
+            bool ok = fl::phase_a<F>(H, ecap, elen, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
+            if constexpr (VDEL) ok = ok && tagged;
             ok = ok || !edit;
-            // GROW: a record written unedited is not pushed either; the scan placement takes it
-            if constexpr (GROW) ok = ok && !nosend;
+            // GROW / SHRINK: a record written unedited keeps its size; the scan placement takes it
+            if constexpr (SZ != SZ_NONE) ok = ok && !nosend;
             st.tail = st.tail && edit;
 #endif
             if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
@@ -1381,16 +1493,23 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             // below are scalar branches.  A lane that did not change such a dword rewrites
             // it with its own packet's bytes (never past caplen), which is harmless.
             uint32_t todo = 0;
-            if (on && !nosend) todo = st.dirty | ((wa & 3u) ? (st.dirty << 1) : 0u);
+            if (on && !nosend) {
+                todo = st.dirty;
+                // VLAN pop: packet' dword i >= 4 is input dword i + 1; input dword 4 (the popped
+                // TCI and the inner type field, unchanged) is never dirty
+                if constexpr (VDEL) todo = (todo & 0xfu) | ((todo >> 4) << 5);
+                todo |= (wa & 3u) ? (todo << 1) : 0u;
+            }
             todo = wave_or(todo);
             // every written dword ends by packet offset 78 <= caplen + 16: no per-dword test
-            const bool wide = !__ballot(on && !nosend && caplen < (uint32_t)fl::WEND - 16);
+            const bool wide = !__ballot(on && !nosend && ecap < (uint32_t)fl::WEND - 16);
             // ---- phase B + write-back of the dwords phase A touched ----
             if (on) {
                 if (!nosend) {
                     uint32_t tail = 0;
                     if (st.tail) {
-                        tail = lds_range_sum(S, P, p + fl::WEND, p + st.end);
+                        const uint32_t pv = p + (VDEL ? 4u : 0u);  // packet' byte x is LDS byte pv + x
+                        tail = lds_range_sum(S, P, pv + fl::WEND, pv + st.end);
                         if (p & 1) tail = fl::swap16(tail);  // absolute -> packet-relative pairing
                     }
                     fl::phase_b(H, st, tail);
@@ -1398,28 +1517,40 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
                     // caplen lie the next record's pcap header bytes, which no lane edits before
                     // conv_hdr (after this loop), so their original bytes go back unchanged.  A
                     // dword further out would overlap the next record's packet bytes, which its
-                    // own lane may be rewriting in this same loop.
+                    // own lane may be rewriting in this same loop.  (--efcs: past the new caplen
+                    // lie the FCS bytes, written back unchanged; the store drops them.)
                     const uint32_t A = wa & ~3u, sh = wa & 3u;
 #pragma unroll
-                    for (int j = 0; j < fl::NW; ++j) {
+                    for (int j = 0; j < fl::NW + XW; ++j) {
                         if (!((todo >> j) & 1u)) continue;
-                        const uint32_t prev = j ? H[j - 1] : (d0 << (8 * (4 - sh)));
-                        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(H[j], prev, 4 - sh) : H[j];
+                        // input dword j: packet' dword j - (j >= 4) under the pop (dword 4 carries
+                        // packet' dword 3's high half, the inner type, where the input has it)
+                        const int hj = VDEL && j >= 4 ? j - 1 : j, hp = VDEL && j >= 5 ? j - 2 : j - 1;
+                        const uint32_t cur = H[hj];
+                        const uint32_t prev = j ? H[hp] : (d0 << (8 * (4 - sh)));
+                        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(cur, prev, 4 - sh) : cur;
                         if (wide || A + 4 * j + 4 <= p + caplen + 16) *(uint32_t *)(S + A + 4 * j) = v;
                     }
                 }
                 if (conv) conv_hdr(S + r0, swp, nsec);
-                if constexpr (GROW) hdr_grow4(S, r0);  // after the write-back, which rewrote len's bytes
+                // after the write-back, which rewrote len's bytes
+                if constexpr (GROW) hdr_add4(S, r0, 4u);
+                if constexpr (SHRINK) hdr_add4(S, r0, (uint32_t)-4);
                 ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
             }
             if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
-            if (GROW && lane == (int)(npkt & 63u)) hdr_grow4(S, LDS_FRONT + g0 + tile.span_len);
+            if (GROW && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, 4u);
+            if (SHRINK && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, (uint32_t)-4);
 
             WK_STAMP(3)  // phase B
             // ---- store: the chunks that start in the span, then the leading bytes ----
             if constexpr (GROW) {
                 wk_store_grow(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0, my_rel, on,
                               a.vlan_tag_word, lane, stream);
+            } else if constexpr (SHRINK) {
+                const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
+                wk_store_shrink(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0, Dj, on, lane,
+                                stream);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -1836,14 +1967,19 @@ extern "C" int te_fast_grid(void) {
 #ifndef TE_WK_DEPTH_LEAN
 #define TE_WK_DEPTH_LEAN 1
 #endif
+// (TE_FF_INCR is a mode, not an option group: an instance with it keeps the incremental
+// checksums of a run without --fixcsum, so a launch takes one whose INCR bit matches)
+#define TE_FF_ALLH (TE_FF_ALL | TE_FF_HDR)
 #define TE_WAVE_INSTANCES(X)                                                                         \
-    X(0u, TE_WK_DEPTH_LEAN, false) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, false)                              \
-    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, false) X(TE_FF_ALL, 1, false) X(TE_FF_ALL, 1, true)                \
-    X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, false) X(TE_FF_HDR | TE_FF_INCR, 1, false)             \
-    X(TE_FF_ALLX, 1, false) X(TE_FF_ALLX, 1, true)
+    X(0u, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, SZ_NONE)                          \
+    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE) X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE)       \
+    X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE)         \
+    X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
+    X(TE_FF_ALL, 1, SZ_GROW) X(TE_FF_ALLH, 1, SZ_GROW) X(TE_FF_ALLX, 1, SZ_GROW)                      \
+    X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)
 static struct {
     uint32_t feat;
-    bool grow;
+    int sz;
     const void *fn;
     int grid;  // resident blocks of this instance (CUs x its occupancy), 0 until asked
 } wave_inst[] = {
@@ -1853,14 +1989,15 @@ static struct {
 };
 
 static uint32_t fast_feat(const te_dev_cfg_t *c);
-// the first (smallest) instance covering the config's option groups;
+// the first (smallest) instance covering the config's option groups and size change;
 // TCPEDIT_HIP_WAVE_FEAT=<mask> adds groups to the choice (A/B runs)
-static int wave_pick(uint32_t want, bool grow) {
+static int wave_pick(uint32_t want, int sz) {
     static const uint32_t feat_env =
         getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
     want |= feat_env;
     for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k)
-        if (wave_inst[k].grow == grow && (want & ~wave_inst[k].feat) == 0) return k;
+        if (wave_inst[k].sz == sz && (want & ~wave_inst[k].feat) == 0 && ((want ^ wave_inst[k].feat) & TE_FF_INCR) == 0)
+            return k;
     return -1;
 }
 
@@ -1885,9 +2022,9 @@ static int wave_inst_grid(int k) {
 }
 
 // the tile budget of the wave-lane instance a config launches (the host cuts tiles to it)
-static int wave_pick(uint32_t want, bool grow);
-extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int grow) {
-    const int k = wave_pick(fast_feat(c), grow != 0);
+static int wave_pick(uint32_t want, int sz);
+extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz) {
+    const int k = wave_pick(fast_feat(c), sz);
     if (k < 0) return TE_WK_TILE_BYTES;
     return (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) ? TE_WK_TILE_BYTES
                                                                                        : TE_WK_LEAN_TILE_BYTES;
@@ -1933,6 +2070,7 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.rec0 = L->rec0;
     a.static_off = (uint32_t)L->static_off;
     a.static_grow = (uint32_t)L->static_grow;
+    a.static_shrink = (uint32_t)L->static_shrink;
     a.grow_bad = L->grow_bad;
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
@@ -1971,7 +2109,8 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     fill_args(a, L);
     hipError_t e;
-    const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow) && L->n_tiles > 0;
+    const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink) &&
+                      L->n_tiles > 0;
     if (fast && !L->generic_only) {
         // the fast kernel zeroes the generic kernel's words itself: no memset launch
         FastArgs f;
@@ -2015,7 +2154,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             f.vlan_tag_word = 0;
         }
         const void *wfn = nullptr;
-        const int wk = wave_pick(fast_feat(ch), grow);
+        const int wk = wave_pick(fast_feat(ch), grow ? SZ_GROW : L->static_shrink);
         if (wk < 0) return -1;
         wfn = wave_inst[wk].fn;
         const bool wave = L->fast_kind == TE_FAST_WAVE;

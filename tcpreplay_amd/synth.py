@@ -126,10 +126,15 @@ def _records(frames, ts0):
     return r
 
 
-def pcap_fixed(n, size=64, seed=1, ipv6=False, proto=17):
-    """n records of `size`-byte IPv4/UDP (or IPv6, TCP) frames."""
+def pcap_fixed(n, size=64, seed=1, ipv6=False, proto=17, vlan=None, fcs=False):
+    """n records of `size`-byte IPv4/UDP (or IPv6, TCP) frames; vlan=TCI tags them,
+    fcs appends a 4-byte FCS (as pcap_imix)."""
     rng = np.random.default_rng(seed)
     recs = _records(_frames(rng, n, size, ipv6=ipv6, proto=proto), 0)
+    if vlan is not None:
+        recs = _tag(recs, vlan)
+    if fcs:
+        recs = _fcs(recs, rng)
     return PCAP_HDR.tobytes() + recs.tobytes()
 
 
@@ -147,12 +152,27 @@ def _tag(recs, tci):
     return out
 
 
-def pcap_imix(n, seed=1, chunk=1 << 20, vlan=None):
+def _fcs(recs, rng):
+    """(n, 16 + size) records -> (n, 20 + size): 4 trailing frame-check bytes (random
+    values: no edit reads them, --efcs strips them) counted in caplen and len"""
+    n, w = recs.shape
+    out = np.empty((n, w + 4), np.uint8)
+    out[:, :w] = recs
+    out[:, w:] = rng.integers(0, 256, size=(n, 4), dtype=np.uint8)
+    hdr = out[:, :16].copy().view("<u4")
+    hdr[:, 2] += 4
+    hdr[:, 3] += 4
+    out[:, :16] = hdr.view(np.uint8)
+    return out
+
+
+def pcap_imix(n, seed=1, chunk=1 << 20, vlan=None, fcs=False):
     """n records cycling 64x7, 570x4, 1514x1 (deterministic 7:4:1); vlan=TCI: every
-    frame carries an 802.1Q tag (68/574/1518 bytes)."""
+    frame carries an 802.1Q tag (68/574/1518 bytes); fcs: every frame ends in a 4-byte
+    FCS (the IP lengths exclude it, as on a capture taken with FCS)."""
     rng = np.random.default_rng(seed)
     pat = IMIX_PATTERN
-    grow = 4 if vlan is not None else 0
+    grow = (4 if vlan is not None else 0) + (4 if fcs else 0)
     cyc_len = sum(16 + s + grow for s in pat)
     parts = [PCAP_HDR.tobytes()]
     done = 0
@@ -165,6 +185,8 @@ def pcap_imix(n, seed=1, chunk=1 << 20, vlan=None):
         made = {s: _records(_frames(rng, ncyc * counts[s], s, first_index=done), done) for s in counts}
         if vlan is not None:
             made = {s: _tag(r, vlan) for s, r in made.items()}
+        if fcs:
+            made = {s: _fcs(r, rng) for s, r in made.items()}
         used = {s: 0 for s in counts}
         for s in pat:
             rec = made[s][used[s]::counts[s]]
