@@ -1097,147 +1097,174 @@ __device__ __forceinline__ void hdr_add4(uint8_t *S, uint32_t h, uint32_t delta)
     }
 }
 
-// GROW store: the output of a tile whose records each gained 4 bytes at packet offset
-// 12 (the pushed {TPID, TCI}).  Record j starts 4 j bytes later than in the input, so
-// the output is the input byte stream with a 4-byte tag inserted before input byte
-// rel_j + 28 (tile-relative output offset T_j = rel_j + 28 + 4 j).  Consecutive tags
-// are >= 62 bytes apart, so a 16-byte output chunk meets at most one: its bytes come
-// from the input 4 m bytes back (m = tags wholly before the chunk), the tag, and the
-// input 4 (m + 1) bytes back, all dword-aligned in LDS.  M[c] = m per chunk comes from
-// one mark per tag and a prefix max.  OS: the tile's output start in gout coordinates.
-__device__ __forceinline__ void wk_store_grow(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
-                                              uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t my_rel,
-                                              bool on, uint32_t tag, int lane, bool stream) {
-    const uint64_t OE = OS + span_len + 4ull * npkt;
+// inclusive scans over the wave's 64 lanes in VALU: DPP row shifts scan each 16-lane row,
+// two row broadcasts carry the rows' totals on (GFX9 DPP; __shfl_up would be six
+// ds_bpermute round trips through the LDS pipe)
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+// the previous lane's value (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t wave_prev(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
+}
+
+// Size-changing stores (GROW: a 4-byte tag pushed into every record; SHRINK: 4 bytes
+// dropped from every record).  Record j's change sits at tile-relative input offset D_j,
+// and consecutive changes are >= 58 bytes apart, so a 16-byte output chunk meets at most
+// one.  Per output chunk c one 16-bit word of the chunk map K says
+//   bits 0-6   m: the changes wholly before the chunk (its bytes come from the input 4 m
+//              bytes back under GROW, on under SHRINK), and
+//   bits 7-11  where change m meets the chunk: 0 not at all, else 4 + its offset from the
+//              chunk start (GROW: -3..15, the tag may start in the previous chunk;
+//              SHRINK: 1..15)
+// built from one mark per change and a prefix max, so each chunk's store is one map read
+// and one batch of five dword reads -- no dependent lookups.
+// LDS hand-off between lanes of one wave: its LDS accesses are performed in order, but
+// the compiler, reasoning per lane, would forward a lane's own store to its later load of
+// the same address across other lanes' stores to it (it did: the chunk map's prefix read
+// came back as the zeros this lane had written, without the other lanes' marks)
+#define WK_LANES_SYNC() asm volatile("" ::: "memory")
+
+__device__ __forceinline__ void wk_chunk_map(uint32_t *P, uint32_t nown, uint32_t o0, uint32_t X, bool on,
+                                             bool grow, int lane) {
+    uint16_t *K = (uint16_t *)P;  // 512 entries
+    *(uint4 *)(K + 8 * lane) = make_uint4(0, 0, 0, 0);
+    // the first chunk that change j lies wholly before (GROW: the tag [X, X + 4) has ended;
+    // SHRINK: the boundary X is at or before the chunk start)
+    const uint32_t wb = grow ? X + 4u : X;
+    if (on) {
+        const uint32_t cj = (wb - o0 + 15u) >> 4;
+        if (cj < nown) K[cj] = (uint16_t)(lane + 1);
+    }
+    WK_LANES_SYNC();
+    {  // prefix max over K, 8 entries a lane
+        const uint4 q = *(const uint4 *)(K + 8 * lane);
+        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
+                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+#pragma unroll
+        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
+        const uint32_t excl = wave_prev(wave_scan_max(e[7]));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
+        *(uint4 *)(K + 8 * lane) =
+            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+    }
+    WK_LANES_SYNC();
+    // the chunks change j meets (whose m is j): where
+    if (on) {
+        const uint32_t c1 = (X - o0) >> 4, t1 = X - o0 - 16u * c1;  // the chunk X lies in
+        if (grow) {
+            if (c1 < nown) K[c1] = (uint16_t)(lane | ((t1 + 4u) << 7));
+            if (t1 > 12u && c1 + 1 < nown) K[c1 + 1] = (uint16_t)(lane | ((t1 - 12u) << 7));  // its tail
+        } else if (t1 != 0 && c1 < nown) {
+            K[c1] = (uint16_t)(lane | ((t1 + 4u) << 7));
+        }
+    }
+    WK_LANES_SYNC();
+}
+
+// the 16 output bytes of a chunk that change m meets, from the 20 input bytes dd starting
+// 4 (m + 1) bytes back (GROW) / 4 m bytes on (SHRINK); tc: the change's offset from the
+// chunk start (GROW: the tag's, -3..15; SHRINK: the boundary's, 1..15)
+__device__ __forceinline__ void mix_grow(const uint32_t (&dd)[5], int tc, uint32_t tag, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int t = tc - 4 * i;  // the tag's start relative to this dword
+        const uint32_t before = dd[i + 1], after = dd[i];
+        const int tp = t < 0 ? 0 : (t > 3 ? 3 : t), tn = t > -1 ? 1 : (t < -3 ? 3 : -t);
+        const uint32_t mp = (1u << (8 * tp)) - 1u, mn = (1u << (8 * (4 - tn))) - 1u;
+        const uint32_t vp = (before & mp) | ((tag << (8 * tp)) & ~mp);   // tag starts in this dword
+        const uint32_t vn = ((tag >> (8 * tn)) & mn) | (after & ~mn);    // tag started tn bytes earlier
+        w[i] = t >= 4 ? before : (t <= -4 ? after : (t >= 0 ? vp : vn));
+    }
+}
+__device__ __forceinline__ void mix_shrink(const uint32_t (&dd)[5], int tc, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int t = tc - 4 * i;  // the boundary relative to this dword
+        const uint32_t mk = (1u << (8 * (t < 1 ? 1 : (t > 3 ? 3 : t)))) - 1u;
+        const uint32_t mixed = (dd[i] & mk) | (dd[i + 1] & ~mk);
+        w[i] = t >= 4 ? dd[i] : (t <= 0 ? dd[i + 1] : mixed);
+    }
+}
+
+__device__ __forceinline__ void wk_put16(g_u8 *gout, uint64_t at, const uint32_t (&w)[4], bool stream) {
+    if (stream)
+        __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (g_v4 *)(gout + at));
+    else
+        *(g_u4 *)(gout + at) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Size-changing stores.  Every chunk that no change meets is a plain 16-byte copy of the
+// input 4 m bytes back (GROW) / on (SHRINK): one pass over the tile's chunks stores them
+// with no byte mixing; then each record's lane builds the one or two chunks its own change
+// meets and stores them over the first pass's bytes (one wave's stores to an address are
+// performed in order).  (Mixing in the chunk pass costs every chunk the VALU work
+// of the few that need it: C4 spent a third of its kernel there.)
+template <bool GROW>
+__device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
+                                               uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t X,
+                                               bool on, uint32_t tag, int lane, bool stream) {
+    const uint64_t OE = GROW ? OS + span_len + 4ull * npkt : OS + span_len - 4ull * npkt;
     const uint64_t C0 = (OS + 15) & ~15ull;
     const uint32_t o0 = (uint32_t)(C0 - OS);
     const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);  // <= 403
-    uint16_t *M = (uint16_t *)P;  // 512 entries
-    uint32_t *T = P + 256;        // 64 tags + sentinel
-    *(uint4 *)(M + 8 * lane) = make_uint4(0, 0, 0, 0);
-    if (on) {
-        const uint32_t Tj = my_rel + 28u + 4u * (uint32_t)lane;
-        T[lane] = Tj;
-        const uint32_t cj = (Tj + 4u - o0 + 15u) >> 4;  // first chunk starting at or after the tag's end
-        if (cj < nown) M[cj] = (uint16_t)(lane + 1);
-    }
-    if (lane == 0) T[npkt] = 0x7fffffffu;
-    {  // prefix max over M, 8 entries a lane
-        const uint4 q = *(const uint4 *)(M + 8 * lane);
-        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
-                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
-#pragma unroll
-        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
-        uint32_t incl = e[7];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl = max(incl, y);
-        }
-        uint32_t excl = __shfl_up(incl, 1, 64);
-        if (lane == 0) excl = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
-        *(uint4 *)(M + 8 * lane) =
-            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
-    }
+    wk_chunk_map(P, nown, o0, X, on, GROW, lane);
+    const uint16_t *K = (const uint16_t *)P;
     const uint8_t *img = S + LDS_FRONT + g0;  // input byte x of the tile
+    // every read in flight before the first store (a store under its own branch would
+    // otherwise pull its reads in after it and wait them out one chunk at a time)
+    uint32_t kv[7], w[7][4];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nown - 1u)];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {  // lanes past the output repeat its last chunk (same bytes)
         const uint32_t cc = umin32((uint32_t)lane + 64u * k, nown - 1u);
-        const uint32_t m = M[cc], Tm = T[m];
+        const uint32_t m = kv[k] & 127u;
         const uint32_t o = o0 + 16u * cc;
-        const uint32_t *D = (const uint32_t *)(img + o - 4u * m - 4u);
-        const uint32_t d0 = D[0], d1 = D[1], d2 = D[2], d3 = D[3], d4 = D[4];
-        const uint32_t dd[5] = {d0, d1, d2, d3, d4};
-        uint32_t w[4];
+        const uint32_t *D = (const uint32_t *)(GROW ? img + o - 4u * m : img + o + 4u * m);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int t = (int)Tm - (int)(o + 4u * (uint32_t)i);  // the tag's start relative to this dword
-            const uint32_t before = dd[i + 1], after = dd[i];
-            const int tp = t < 0 ? 0 : (t > 3 ? 3 : t), tn = t > -1 ? 1 : (t < -3 ? 3 : -t);
-            const uint32_t mp = (1u << (8 * tp)) - 1u, mn = (1u << (8 * (4 - tn))) - 1u;
-            const uint32_t vp = (before & mp) | ((tag << (8 * tp)) & ~mp);   // tag starts in this dword
-            const uint32_t vn = ((tag >> (8 * tn)) & mn) | (after & ~mn);    // tag started tn bytes earlier
-            w[i] = t >= 4 ? before : (t <= -4 ? after : (t >= 0 ? vp : vn));
+        for (int i = 0; i < 4; ++i) w[k][i] = D[i];
+    }
+    WK_LANES_SYNC();
+    // every chunk stored unconditionally (a branch per store costs more than the bytes): the
+    // few a change meets are stored again below, by the same wave, in order
+#pragma unroll
+    for (int k = 0; k < 7; ++k) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
+    // the chunks this lane's change meets: both built on every lane (reads in flight
+    // together), stored where they exist
+    {
+        const uint32_t j = (uint32_t)lane, c1 = (X - o0) >> 4, t1 = X - o0 - 16u * c1;
+        uint32_t w2[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t o = o0 + 16u * umin32(c1 + (uint32_t)h, nown - 1u);
+            const uint32_t *D = (const uint32_t *)(GROW ? img + o - 4u * j - 4u : img + o + 4u * j);
+            const uint32_t dd[5] = {D[0], D[1], D[2], D[3], D[4]};
+            const int tc = (int)t1 - 16 * h;
+            if constexpr (GROW) mix_grow(dd, tc, tag, w2[h]);
+            else mix_shrink(dd, tc, w2[h]);
         }
-        if (stream)
-            __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (g_v4 *)(gout + C0 + 16ull * cc));
-        else
-            *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
+        WK_LANES_SYNC();
+        if (on && (GROW || t1 != 0) && c1 < nown) wk_put16(gout, C0 + 16ull * c1, w2[0], stream);
+        if (on && GROW && t1 > 12u && c1 + 1 < nown) wk_put16(gout, C0 + 16ull * (c1 + 1), w2[1], stream);
     }
-    // the leading bytes (output start to the first 16-byte boundary: before any tag)
-    const uint64_t q = (uint32_t)lane < o0 ? OS + (uint32_t)lane : C0;  // others repeat byte C0
-    gout[q] = img[(uint32_t)(q - OS)];
-}
-
-// SHRINK store (VLAN pop, --efcs): record j loses the 4 input bytes at tile-relative
-// offset D_j (VLAN pop: rel_j + 28, its TPID and TCI, so the inner type field lands at
-// packet offset 12 as dlt_en10mb_encode leaves it; --efcs: rel_j + 16 + caplen_j - 4, its
-// FCS).  Output byte
-// y (tile-relative) is input byte y + 4 m(y), m(y) = #{j : Y_j <= y}, Y_j = D_j - 4 j.
-// Consecutive Y_j are >= 58 bytes apart (the smallest record on the lane), so a 16-byte
-// output chunk meets at most one: its bytes come from the input 4 m and 4 (m + 1) bytes
-// on, both dword-aligned in LDS.  M[c] = m per chunk as in wk_store_grow.  Dj: this
-// lane's D_j; OS: the tile's output start in gout coordinates.
-__device__ __forceinline__ void wk_store_shrink(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
-                                                uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t Dj,
-                                                bool on, int lane, bool stream) {
-    const uint64_t OE = OS + span_len - 4ull * npkt;
-    const uint64_t C0 = (OS + 15) & ~15ull;
-    const uint32_t o0 = (uint32_t)(C0 - OS);
-    const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);
-    uint16_t *M = (uint16_t *)P;  // 512 entries
-    uint32_t *T = P + 256;        // 64 boundaries + sentinel
-    *(uint4 *)(M + 8 * lane) = make_uint4(0, 0, 0, 0);
-    if (on) {
-        const uint32_t Yj = Dj - 4u * (uint32_t)lane;
-        T[lane] = Yj;
-        const uint32_t cj = (Yj - o0 + 15u) >> 4;  // first chunk starting at or after Y_j
-        if (cj < nown) M[cj] = (uint16_t)(lane + 1);
-    }
-    if (lane == 0) T[npkt] = 0x7fffffffu;
-    {  // prefix max over M, 8 entries a lane
-        const uint4 q = *(const uint4 *)(M + 8 * lane);
-        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
-                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
-#pragma unroll
-        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
-        uint32_t incl = e[7];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl = max(incl, y);
-        }
-        uint32_t excl = __shfl_up(incl, 1, 64);
-        if (lane == 0) excl = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
-        *(uint4 *)(M + 8 * lane) =
-            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
-    }
-    const uint8_t *img = S + LDS_FRONT + g0;  // input byte x of the tile
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {  // lanes past the output repeat its last chunk (same bytes)
-        const uint32_t cc = umin32((uint32_t)lane + 64u * k, nown - 1u);
-        const uint32_t m = M[cc], Ym = T[m];
-        const uint32_t o = o0 + 16u * cc;
-        const uint32_t *D = (const uint32_t *)(img + o + 4u * m);
-        const uint32_t dd[5] = {D[0], D[1], D[2], D[3], D[4]};
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int t = (int)Ym - (int)(o + 4u * (uint32_t)i);  // the boundary relative to this dword
-            const uint32_t mk = (1u << (8 * (t < 1 ? 1 : (t > 3 ? 3 : t)))) - 1u;
-            const uint32_t mixed = (dd[i] & mk) | (dd[i + 1] & ~mk);
-            w[i] = t >= 4 ? dd[i] : (t <= 0 ? dd[i + 1] : mixed);
-        }
-        if (stream)
-            __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (g_v4 *)(gout + C0 + 16ull * cc));
-        else
-            *(g_u4 *)(gout + C0 + 16ull * cc) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    // the leading bytes (output start to the first 16-byte boundary: before any deletion)
+    // the leading bytes (output start to the first 16-byte boundary: before any change)
     const uint64_t q = (uint32_t)lane < o0 ? OS + (uint32_t)lane : C0;  // others repeat byte C0
     gout[q] = img[(uint32_t)(q - OS)];
 }
@@ -1473,12 +1500,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
                     loc[q] = tot;
                     tot += s;
                 }
-                uint32_t incl = tot;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += y;
-                }
+                const uint32_t incl = wave_scan_add(tot);
                 const uint32_t base = incl - tot;
 #pragma unroll
                 for (int q = 0; q < WK_KL; ++q) {
@@ -1487,6 +1509,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
                 }
                 if (lane == 63) P[nch] = incl;
             }
+            WK_LANES_SYNC();  // other lanes read the prefix
 
             WK_STAMP(2)  // chunk prefix
             // LDS dwords any lane writes back, as one wave-uniform mask: the per-dword tests
@@ -1542,15 +1565,17 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             if (GROW && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, 4u);
             if (SHRINK && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, (uint32_t)-4);
 
+            WK_LANES_SYNC();  // the store reads what every lane wrote back
             WK_STAMP(3)  // phase B
             // ---- store: the chunks that start in the span, then the leading bytes ----
             if constexpr (GROW) {
-                wk_store_grow(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0, my_rel, on,
-                              a.vlan_tag_word, lane, stream);
+                // record j's tag at output offset rel_j + 28 + 4 j (its input byte rel_j + 28 on)
+                wk_store_sized<true>(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0,
+                                     my_rel + 28u + 4u * (uint32_t)lane, on, a.vlan_tag_word, lane, stream);
             } else if constexpr (SHRINK) {
                 const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
-                wk_store_shrink(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0, Dj, on, lane,
-                                stream);
+                wk_store_sized<false>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
+                                      Dj - 4u * (uint32_t)lane, on, 0u, lane, stream);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -1606,6 +1631,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
         edit(t, tile, my_rel, my_dirb, my_dirv);
         WK_STAMP(4)  // stores issued
         if (t + W < n_tiles) fill(Rn);
+        WK_LANES_SYNC();  // the next tile's lanes read what every lane filled
         WK_STAMP(5)  // next span -> LDS (waits for its loads)
     };
 

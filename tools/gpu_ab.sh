@@ -1,9 +1,9 @@
-# A/B: streaming (nontemporal) mode forced on/off vs the size rule
+# A/B of library variants on the ab.py cases (diagnostic)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for v in auto s0 s1 auto; do
-  case $v in auto) env="";; s0) env="TCPEDIT_HIP_STREAM=0";; s1) env="TCPEDIT_HIP_STREAM=1";; esac
-  env $env AB_TAG=$v timeout -k 10 200 python tools/ab.py c2 c2x10 c3 c5 c4 >> gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
+for v in ${AB_VARIANTS:-nomix}; do
+  TCPEDIT_HIP_LIB=tcpreplay_amd/lib/var/libtcpedit_hip_$v.so AB_TAG=$v timeout -k 10 200 python tools/ab.py ${AB_CASES:-c4} > gpurun_out/ab_$v.log 2>&1 || { tail -3 gpurun_out/ab_$v.log; }
+  cat gpurun_out/ab_$v.log
 done
-cat gpurun_out/ab.log
+timeout -k 10 200 python tools/ab.py ${AB_CASES:-c4}
