@@ -28,7 +28,10 @@
 
 #define TPO_MAXC 64
 
-enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3, TPO_AUTO = 4 };
+enum { TPO_CIDR = 1, TPO_MAC = 2, TPO_PORT = 3, TPO_AUTO = 4, TPO_REGEX = 5 };
+/* --regex: regcomp(REG_EXTENDED | REG_NOSUB) of the option (tcpprep_opts.def:225) */
+static regex_t tpo_re;
+static int tpo_re_set;
 /* automode: defines.h.in:207 direction_e and tcpprep's BRIDGE/CLIENT/SERVER/FIRST modes */
 enum { TPA_BRIDGE = 1, TPA_CLIENT, TPA_SERVER, TPA_FIRST, TPA_ROUTER };
 /* xX.h:34-41 */
@@ -227,6 +230,13 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
             }
         } else if (IS("--port")) {
             o->mode = TPO_PORT;
+        } else if (IS("--regex")) {
+            if (tpo_re_set)
+                regfree(&tpo_re);
+            tpo_re_set = regcomp(&tpo_re, v, REG_EXTENDED | REG_NOSUB) == 0;
+            if (!tpo_re_set)
+                return -1; /* errx "Unable to compile regex" */
+            o->mode = TPO_REGEX;
         } else if (IS("--auto")) {
             o->mode = TPO_AUTO;
             if (!strcmp(v, "bridge"))
@@ -665,6 +675,13 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
                 if (r == -4)
                     return -4; /* "is an unknown system... aborting" */
                 dir = r == 1;
+            } else if (o.mode == TPO_REGEX) {
+                /* check_ipv4_regex / check_ipv6_regex (tcpprep.c:300-335): regexec on
+                   inet_ntop's string; the result is 1 or 0, which --reverse turns into 2 or
+                   leaves 0 (tcpprep.c:441-442): neither sets the C2S bit */
+                char sa[64];
+                inet_ntop(v6 ? AF_INET6 : AF_INET, ip + (v6 ? 8 : 12), sa, sizeof sa);
+                dir = regexec(&tpo_re, sa, 0, NULL, 0) == 0 && !o.reverse;
             } else if (o.mode == TPO_CIDR) {
                 uint32_t s4;
                 memcpy(&s4, ip + 12, 4);
@@ -716,3 +733,5 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
     tpo_last_entries = entries;
     return (long)(hdr + (entries + 3) / 4);
 }
+
+#include "tcpreplay_oracle.c"

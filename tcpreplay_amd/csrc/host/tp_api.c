@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include "tp_regex.h"
 #include "../../../include/tcpprep.h"
 #include "tp_dev_cfg.h"
 
@@ -302,7 +303,11 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
             NEED_ARG();
             rc = load_services(t, v);
         } else if (OPT("--regex")) {
-            return tp_err(t, "%.*s is not served by the GPU classifier (per-packet modes only)", (int)nl, a);
+            NEED_ARG();
+            c->mode = TP_MODE_REGEX; /* tcpprep_opts.def:209-231 */
+            char e[256];
+            if (tp_regex_compile(v, &c->dfa, e, sizeof e) < 0)
+                return tp_err(t, "%s", e);
         } else {
             return tp_err(t, "unknown option %s", a);
         }
@@ -316,7 +321,7 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
 #undef NEED_ARG
     }
     if (!c->mode)
-        return tp_err(t, "one of --cidr, --mac, --port, --auto is required");
+        return tp_err(t, "one of --cidr, --mac, --port, --regex, --auto is required");
     if (t->min_mask <= t->max_mask) /* tcpprep_api.c:204-208 */
         return tp_err(t, "Min network mask len (%d) must be less then max network mask len (%d)", t->min_mask,
                       t->max_mask);

@@ -10,11 +10,23 @@
 
 #define TP_MAXC 64
 
-enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3, TP_MODE_AUTO = 4 };
+enum { TP_MODE_CIDR = 1, TP_MODE_MAC = 2, TP_MODE_PORT = 3, TP_MODE_AUTO = 4, TP_MODE_REGEX = 5 };
 /* the auto modes (tcpprep.c:480-587) */
 enum { TP_AUTO_BRIDGE = 1, TP_AUTO_CLIENT, TP_AUTO_SERVER, TP_AUTO_FIRST, TP_AUTO_ROUTER };
 /* xX.h:34-41 */
 enum { TP_XX_SOURCE = 1, TP_XX_DEST = 2, TP_XX_BOTH = 4, TP_XX_EITHER = 8, TP_XX_PACKET = 16, TP_XX_EXCLUDE = 128 };
+
+/* --regex as a DFA over the characters inet_ntop prints (tp_regex.c): symbols '0'-'9',
+   'a'-'f', '.', ':' (0-17), the string start and end (18, 19); state 0 is the absorbing
+   match state */
+#define TP_NSYM 20
+#define TP_SYM_BOS 18
+#define TP_SYM_EOS 19
+#define TP_DFA_MAX 255
+typedef struct {
+    uint8_t next[TP_DFA_MAX][TP_NSYM];
+    int32_t start, nstates;
+} tp_dfa_t;
 
 typedef struct {
     int32_t mode, reverse, nonip, mac_first_empty;
@@ -27,6 +39,7 @@ typedef struct {
     uint8_t mac[TP_MAXC][8];     /* -e list, as macinstring's mac2hex leaves each token */
     uint64_t lmin[TP_MAXC], lmax[TP_MAXC]; /* -x/-X P: list */
     uint32_t svc_tcp[2048], svc_udp[2048]; /* services bitmaps (tcpprep_api.c:50-53: ports 0-1023) */
+    tp_dfa_t dfa;                /* --regex */
 } tp_dev_cfg_t;
 
 /* the auto modes' host table in HBM (tree.c's RB tree): open addressing on exact

@@ -225,9 +225,74 @@ DI int tree_dir(const tp_dev_cfg_t &c, const tp_tree_t &t, uint32_t s) {
     return c.automode == TP_AUTO_SERVER ? 2 : c.automode == TP_AUTO_CLIENT ? 1 : -1;
 }
 
+// ---- --regex (tcpprep.c:300-335): the source address as inet_ntop prints it, through
+// the host-compiled DFA (tp_regex.c) one character at a time ----
+DI int dstep(const u8 *T, int st, int k) { return T[st * TP_NSYM + k]; }
+DI int ddec(const u8 *T, int st, u32 v) {  // "%u" of an octet
+    if (v >= 100) st = dstep(T, st, (int)(v / 100));
+    if (v >= 10) st = dstep(T, st, (int)((v / 10) % 10));
+    return dstep(T, st, (int)(v % 10));
+}
+DI int dhex(const u8 *T, int st, u32 w) {  // "%x" of a 16-bit word
+    bool lead = true;
+    for (int sh = 12; sh >= 0; sh -= 4) {
+        const u32 d = (w >> sh) & 15u;
+        if (d || !lead || sh == 0) {
+            st = dstep(T, st, (int)d);
+            lead = false;
+        }
+    }
+    return st;
+}
+DI int dv4(const u8 *T, int st, const u8 *a) {  // inet_ntop4: dotted decimal
+    for (int i = 0; i < 4; ++i) {
+        if (i) st = dstep(T, st, 16);
+        st = ddec(T, st, a[i]);
+    }
+    return st;
+}
+// glibc inet_ntop6: the first longest run (>= 2) of zero words becomes "::"; an
+// IPv4-compatible (::a.b.c.d) or -mapped (::ffff:a.b.c.d) address ends in dotted form
+DI bool regex_match(const u8 *T, int start, const u8 *ip, bool v6) {
+    int st = dstep(T, start, TP_SYM_BOS);
+    if (!v6) {
+        st = dv4(T, st, ip + 12);
+    } else {
+        const u8 *a = ip + 8;
+        u32 w[8];
+        for (int i = 0; i < 8; ++i) w[i] = ((u32)a[2 * i] << 8) | a[2 * i + 1];
+        int bb = -1, bl = 0, cb = -1, cl = 0;
+        for (int i = 0; i < 8; ++i) {
+            if (w[i] == 0) {
+                if (cb < 0) cb = i, cl = 1;
+                else ++cl;
+            } else if (cb >= 0) {
+                if (bb < 0 || cl > bl) bb = cb, bl = cl;
+                cb = -1;
+            }
+        }
+        if (cb >= 0 && (bb < 0 || cl > bl)) bb = cb, bl = cl;
+        if (bb >= 0 && bl < 2) bb = -1;
+        for (int i = 0; i < 8; ++i) {
+            if (bb >= 0 && i >= bb && i < bb + bl) {
+                if (i == bb) st = dstep(T, st, 17);
+                continue;
+            }
+            if (i) st = dstep(T, st, 17);
+            if (i == 6 && bb == 0 && (bl == 6 || (bl == 5 && w[5] == 0xffffu))) {
+                st = dv4(T, st, a + 12);
+                break;
+            }
+            st = dhex(T, st, w[i]);
+        }
+        if (bb >= 0 && bb + bl == 8) st = dstep(T, st, 17);
+    }
+    return dstep(T, st, TP_SYM_EOS) == 0;
+}
+
 // one record -> its 2-bit cache entry
 DI u32 classify(const tp_dev_cfg_t &c, const tp_tree_t *t, uint64_t j, const u8 *pkt, u32 caplen,
-                 uint64_t pktnum) {
+                 uint64_t pktnum, const u8 *dfa) {
     constexpr u32 SEND = 2, C2S = 1;
     // include/exclude packet list (tcpprep.c:362-375)
     if (c.nlist && check_list(c, pktnum) == ((c.xx_mode & TP_XX_EXCLUDE) != 0)) return 0;
@@ -242,6 +307,12 @@ DI u32 classify(const tp_dev_cfg_t &c, const tp_tree_t *t, uint64_t j, const u8 
         if (c.nxx_cidr && c.xx_mode && !xx_cidr(c, ip, v6)) return 0;
         if (c.mode == TP_MODE_AUTO) {
             dir = tree_dir(c, *t, t->slot[j]);  // -1 (TCPR_DIR_ERROR): send bit only
+        } else if (c.mode == TP_MODE_REGEX) {
+            // check_ipv4_regex / check_ipv6_regex return 1 or 0; --reverse swaps only 1 and 2
+            // (tcpprep.c:441-442), so a reversed match (2) and a miss (0) both leave the
+            // direction bit clear (add_cache, cache.c:292)
+            dir = regex_match(dfa, c.dfa.start, ip, v6) ? 1 : 0;
+            if (c.reverse && dir == 1) dir = 2;
         } else if (c.mode == TP_MODE_CIDR) {
             dir = v6 ? in6(c.cidr, c.ncidr, ip + 8) : in4(c.cidr, c.ncidr, ld32(ip + 12));
             if (c.reverse) dir = !dir;
@@ -270,10 +341,18 @@ __global__ __launch_bounds__(256) void tp_classify(const u8 *__restrict__ img, c
                                                    const uint32_t *__restrict__ pktnum, uint64_t n,
                                                    const tp_dev_cfg_t *__restrict__ cfg, const tp_tree_t *tree,
                                                    u8 *__restrict__ out) {
+    // the --regex DFA in LDS (5 KiB): one dependent lookup per address character
+    __shared__ __attribute__((aligned(16))) u8 dfa[TP_DFA_MAX * TP_NSYM];
+    if (cfg->mode == TP_MODE_REGEX) {
+        const u32 *src = (const u32 *)&cfg->dfa.next[0][0];
+        for (u32 i = threadIdx.x; i < sizeof(dfa) / 4; i += blockDim.x) ((u32 *)dfa)[i] = src[i];
+        __syncthreads();
+    }
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     u32 e = 0;
     if (j < n)
-        e = classify(*cfg, tree, j, img + off[j], caplen[j], cfg->pkt_base + (pktnum ? (uint64_t)pktnum[j] : j + 1));
+        e = classify(*cfg, tree, j, img + off[j], caplen[j], cfg->pkt_base + (pktnum ? (uint64_t)pktnum[j] : j + 1),
+                     dfa);
     e <<= 2 * (j & 3);
     e |= __shfl_xor(e, 1);
     e |= __shfl_xor(e, 2);

@@ -99,3 +99,40 @@ def tcpprep(pcap: bytes, args, pkt_base: int = 0, with_entries=False):
     if with_entries:
         return out.raw[:n], int(lib.tcpprep_oracle_last_entries())
     return out.raw[:n]
+
+
+def replay_args(args):
+    """tcpreplay's options this path serves (tcpreplay_opts.def): --loop, --unique-ip,
+    --unique-ip-loops, --preload-pcap / -K -> (loops, unique_ip, unique_loops, preload)"""
+    loops, uniq, uloops, preload = 1, 0, 1.0, 0
+    for a in args:
+        k, _, v = a.partition("=")
+        if k in ("--loop", "-l"):
+            loops = int(v)
+        elif k == "--unique-ip":
+            uniq = 1
+        elif k == "--unique-ip-loops":
+            uloops = float(v)
+        elif k in ("--preload-pcap", "-K"):
+            preload = 1
+        else:
+            raise ValueError(f"unknown tcpreplay option {a}")
+    return loops, uniq, uloops, preload
+
+
+def replay(pcap: bytes, args):
+    """tcpreplay_oracle_run: `tcpreplay -w out <args> <pcap>` as the CPU restatement writes
+    it -> (output file bytes, records whose unique-ip edit failed)"""
+    lib = load()
+    fn = lib.tcpreplay_oracle_run
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                   ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]
+    loops, uniq, uloops, preload = replay_args(args)
+    cap = 24 + loops * max(len(pcap) - 24, 0) + 64
+    out = ctypes.create_string_buffer(cap)
+    failed = ctypes.c_uint64()
+    n = fn(pcap, len(pcap), loops, uniq, uloops, preload, out, cap, ctypes.byref(failed))
+    if n < 0:
+        raise ValueError(f"tcpreplay oracle failed ({n}) for {args}")
+    return out.raw[:n], int(failed.value)

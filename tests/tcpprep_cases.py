@@ -1,5 +1,5 @@
 """tcpprep golden cases: the argument lines of the reference's test/Makefile.am:87-104
-(tcpprep run with --no-arg-comment on test/test.pcap), in long-option form, and the
+(tcpprep run with --no-arg-comment on test/test.pcap; the regex lines at :96,100), in long-option form, and the
 cache files they produced (tests/golden/prep.*, copied from the reference's test/)."""
 import os
 
@@ -21,6 +21,8 @@ CASES = {
     "auto_server": ["--auto=server"],
     "auto_first": ["--auto=first"],
     "auto_router": ["--auto=router"],
+    "regex": ["--regex=96.17.211.*"],
+    "regex_reverse": ["--regex=96.17.211.*", "--reverse"],
 }
 
 

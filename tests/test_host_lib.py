@@ -38,6 +38,13 @@ def test_library_exports_every_tcpprep_symbol(built):
     assert [n for n in names if not hasattr(L, n)] == []
 
 
+def test_library_exports_every_tcpreplay_symbol(built):
+    L = ctypes.CDLL(TA.LIB_PATH)
+    names = header_functions("tcpreplay_hip.h", "tcpreplay_hip_")
+    assert len(names) == 10
+    assert [n for n in names if not hasattr(L, n)] == []
+
+
 def derive(args):
     te = TA.TcpEdit(args)
     cfg = DevCfg()

@@ -69,6 +69,10 @@ OPTION_LINES = [
     ["--auto=server", "--nonip"],
     ["--auto=first", "--ratio=0"],
     ["--auto=router", "--nonip", "--minmask=24", "--maxmask=16"],
+    ["--regex=96.17.211.*"],
+    ["--regex=^(10|96)\\.[0-9]+", "--reverse"],
+    ["--regex=::", "--nonip"],
+    ["--regex=[a-f]:[0-9]|^0\\.", "--include=P:3-90"],
 ]
 
 
@@ -149,7 +153,7 @@ def test_mac_mode_short_records_get_no_entry():
 
 
 def test_rejects_unsupported_modes_loudly():
-    for args in (["--auto=bogus"], ["--auto=router", "--minmask=8", "--maxmask=16"], ["--regex=96.*"], ["--port", "--include=F:tcp"], [],
+    for args in (["--auto=bogus"], ["--auto=router", "--minmask=8", "--maxmask=16"], ["--regex=(96"], ["--port", "--include=F:tcp"], [],
                  ["--auto=bridge", "--include=P:1-5"]):
         with pytest.raises(ValueError):
             TP.TcpPrep(args)
@@ -175,3 +179,26 @@ def test_gpu_services_file_matches_oracle(tmp_path):
     for pcap in (T.test_pcap(), _adversarial(), synth.pcap_imix(200_000, seed=4)):
         args = ["--no-arg-comment", "--port", f"--services={f}"]
         assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
+
+
+@pytest.mark.parametrize("pattern", ["::", "^::ffff:", r"^::[0-9]+\.", ":0:", "^[0-9a-f]{1,4}:[0-9a-f]{1,4}::",
+                                     r"\.(1|2)[0-9]$", "^fe80", "^[^:]+$", "(::|:0:)[1-9a-f]"])
+def test_regex_over_every_ipv6_text_shape(pattern):
+    """inet_ntop's IPv6 forms, as the device prints them through the DFA: the first
+    longest zero run compressed (or none shorter than 2 words), IPv4-compatible and
+    -mapped tails in dotted form, leading-zero-free lowercase hex; IPv4 sources too"""
+    rng = np.random.default_rng(5)
+    v6 = synth.records(synth.pcap_fixed(3000, 90, ipv6=True, seed=3))
+    v4 = synth.records(synth.pcap_fixed(500, 64, seed=4))
+    recs = []
+    for i, (ts, tu, cl, ln, d) in enumerate(v6):
+        d = bytearray(d)
+        w = [int(x) for x in rng.choice([0, 0, 0, 1, 0xffff, 0xfe80, int(rng.integers(0, 65536))], size=8)]
+        if i % 7 == 0:
+            w[:6] = [0, 0, 0, 0, 0, 0xffff if i % 14 else 0]
+        d[22:38] = b"".join(x.to_bytes(2, "big") for x in w)
+        recs.append((ts, tu, cl, ln, bytes(d)))
+    recs += v4
+    pcap = synth.build_pcap(recs)
+    args = ["--no-arg-comment", "--regex=" + pattern]
+    assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
