@@ -30,6 +30,9 @@ struct tcpprep_hip_s {
     int device;             /* HIP device the classifier runs on (-1: the thread's current one) */
     char comment[8192]; /* the final "args\ncomment" string */
     char errstr[1024];
+    uint64_t *mkeys, *mvals; /* --auto over shards: the merged host table (sorted keys) */
+    size_t mn;
+    int merged;
 };
 
 static int tp_err(tcpprep_hip_t *t, const char *fmt, ...)
@@ -63,6 +66,8 @@ int tcpprep_init(tcpprep_hip_t **out)
 int tcpprep_close(tcpprep_hip_t **t)
 {
     if (t && *t) {
+        free((*t)->mkeys);
+        free((*t)->mvals);
         free(*t);
         *t = NULL;
     }
@@ -85,9 +90,7 @@ int tcpprep_set_pkt_base(tcpprep_hip_t *t, uint64_t pkt_base)
 {
     if (!t)
         return -1;
-    if (t->cfg.mode == TP_MODE_AUTO && pkt_base)
-        return tp_err(t, "--auto classifies by the whole capture's host table: it does not shard");
-    t->cfg.pkt_base = pkt_base;
+    t->cfg.pkt_base = pkt_base; /* --auto: the shard then needs tcpprep_auto_merge's table */
     return 0;
 }
 
@@ -517,7 +520,7 @@ static int tree_pass(tcpprep_hip_t *t, const tp_dev_t *d, const tp_index_t *x, c
     if (hipMemsetAsync(d->tree.slots, 0, cap * 16, st) != hipSuccess ||
         hipMemsetAsync(d->tree.err, 0xff, 8, st) != hipSuccess)
         return tp_err(t, "device memset failed");
-    if (tp_launch_tree(d->img, d->off, d->caplen, x->n, d->cfg, t->cfg.automode, d->tree, st) != 0)
+    if (tp_launch_tree(d->img, d->off, d->caplen, x->n, d->cfg, t->cfg.automode, t->cfg.pkt_base, d->tree, st) != 0)
         return tp_err(t, "host-table kernel failed");
     uint64_t err = 0;
     if (hipMemcpyAsync(&err, d->tree.err, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -526,6 +529,108 @@ static int tree_pass(tcpprep_hip_t *t, const tp_dev_t *d, const tp_index_t *x, c
     if (err != ~0ull) /* tree.c:835-837 */
         return tp_err(t, "packet capture length %u too small to process", x->caplen[err]);
     (void)img;
+    return 0;
+}
+
+/* the merged table's values into this shard's nodes (the local build gave their slots) */
+static int apply_merged(tcpprep_hip_t *t, const tp_dev_t *d)
+{
+    if (!t->merged)
+        return 0;
+    uint64_t *dk = NULL, *dv = NULL;
+    const size_t n = t->mn ? t->mn : 1;
+    int rc = -1;
+    if (hipMalloc((void **)&dk, n * 8) == hipSuccess && hipMalloc((void **)&dv, n * 8) == hipSuccess &&
+        hipMemcpy(dk, t->mkeys, t->mn * 8, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dv, t->mvals, t->mn * 8, hipMemcpyHostToDevice) == hipSuccess &&
+        tp_launch_tree_merged(d->tree, d->tree_cap, dk, dv, t->mn, NULL) == 0 && hipDeviceSynchronize() == hipSuccess)
+        rc = 0;
+    hipFree(dk);
+    hipFree(dv);
+    return rc < 0 ? tp_err(t, "merged host table upload failed") : 0;
+}
+
+int64_t tcpprep_auto_table(tcpprep_hip_t *t, const void *pcap, size_t len, uint64_t *keys, uint64_t *vals, size_t cap)
+{
+    if (!t || !pcap || (cap && (!keys || !vals)))
+        return -1;
+    if (t->cfg.mode != TP_MODE_AUTO)
+        return tp_err(t, "tcpprep_auto_table needs --auto");
+    tp_index_t x;
+    if (index_pcap(t, pcap, len, &x) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    tp_dev_t d;
+    if (stage(t, pcap, len, &x, &d) < 0) {
+        index_free(&x);
+        return -1;
+    }
+    int64_t count = -1;
+    uint64_t *slots = NULL;
+    if (tree_pass(t, &d, &x, pcap, NULL) == 0 && (slots = malloc(d.tree_cap * 16)) &&
+        hipMemcpy(slots, d.tree.slots, d.tree_cap * 16, hipMemcpyDeviceToHost) == hipSuccess) {
+        count = 0;
+        for (size_t s = 0; s < d.tree_cap; s++)
+            if (slots[2 * s]) {
+                if ((size_t)count < cap) {
+                    keys[count] = slots[2 * s];
+                    vals[count] = slots[2 * s + 1];
+                }
+                count++;
+            }
+    } else if (!t->errstr[0]) {
+        tp_err(t, "host table read-back failed");
+    }
+    free(slots);
+    dev_free(&d);
+    index_free(&x);
+    return count;
+}
+
+static int cmp_pair(const void *a, const void *b)
+{
+    const uint64_t x = ((const uint64_t *)a)[0], y = ((const uint64_t *)b)[0];
+    return x < y ? -1 : x > y;
+}
+
+int tcpprep_auto_merge(tcpprep_hip_t *t, const uint64_t *keys, const uint64_t *vals, size_t n)
+{
+    if (!t || (n && (!keys || !vals)))
+        return -1;
+    if (t->cfg.mode != TP_MODE_AUTO)
+        return tp_err(t, "tcpprep_auto_merge needs --auto");
+    uint64_t *pr = malloc((n ? n : 1) * 16);
+    if (!pr)
+        return tp_err(t, "out of memory");
+    for (size_t i = 0; i < n; i++) {
+        pr[2 * i] = keys[i];
+        pr[2 * i + 1] = vals[i];
+    }
+    qsort(pr, n, 16, cmp_pair);
+    free(t->mkeys);
+    free(t->mvals);
+    t->mkeys = malloc((n ? n : 1) * 8);
+    t->mvals = malloc((n ? n : 1) * 8);
+    if (!t->mkeys || !t->mvals) {
+        free(pr);
+        return tp_err(t, "out of memory");
+    }
+    const int first = t->cfg.automode == TP_AUTO_FIRST;
+    size_t m = 0;
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t k = pr[2 * i], v = pr[2 * i + 1];
+        if (m && t->mkeys[m - 1] == k) { /* counts add (their halves stay below 2^32); the
+                                            earliest sighting is the largest complement */
+            t->mvals[m - 1] = first ? (v > t->mvals[m - 1] ? v : t->mvals[m - 1]) : t->mvals[m - 1] + v;
+        } else {
+            t->mkeys[m] = k;
+            t->mvals[m++] = v;
+        }
+    }
+    free(pr);
+    t->mn = m;
+    t->merged = 1;
     return 0;
 }
 
@@ -553,7 +658,13 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
         return -1;
     }
     uint8_t *out = outv;
-    if (t->cfg.mode == TP_MODE_AUTO && tree_pass(t, &d, &x, pcap, NULL) < 0) {
+    if (t->cfg.mode == TP_MODE_AUTO && t->cfg.pkt_base && !t->merged) {
+        dev_free(&d);
+        index_free(&x);
+        return tp_err(t, "--auto on a shard classifies by the whole capture's host table: "
+                         "tcpprep_auto_merge the ranks' tcpprep_auto_table first");
+    }
+    if (t->cfg.mode == TP_MODE_AUTO && (tree_pass(t, &d, &x, pcap, NULL) < 0 || apply_merged(t, &d) < 0)) {
         dev_free(&d);
         index_free(&x);
         return -1;
@@ -608,7 +719,7 @@ int tcpprep_time(tcpprep_hip_t *t, const void *pcap, size_t len, int iters, doub
         if (t->cfg.mode == TP_MODE_AUTO) {
             size_t cap = d.tree_cap;
             hipMemsetAsync(d.tree.slots, 0, cap * 16, NULL);
-            rc = tp_launch_tree(d.img, d.off, d.caplen, x.n, d.cfg, t->cfg.automode, d.tree, NULL);
+            rc = tp_launch_tree(d.img, d.off, d.caplen, x.n, d.cfg, t->cfg.automode, t->cfg.pkt_base, d.tree, NULL);
         }
         if (rc == 0)
             rc = tp_launch_classify(d.img, d.off, d.caplen, d.pktnum, x.n, d.cfg, d.d_tree, d.out, NULL);

@@ -59,7 +59,10 @@ extern "C" {
 #endif
 /* auto modes, first pass: build the host table (tree); then tp_launch_classify */
 int tp_launch_tree(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, uint64_t n_entries,
-                   const tp_dev_cfg_t *cfg, int automode, tp_tree_t tree, void *stream);
+                   const tp_dev_cfg_t *cfg, int automode, uint64_t base, tp_tree_t tree, void *stream);
+/* sharded auto modes: every node's value from the merged table (keys sorted, unique) */
+int tp_launch_tree_merged(tp_tree_t tree, uint64_t capacity, const uint64_t *keys, const uint64_t *vals, uint64_t n,
+                          void *stream);
 /* classify n_entries records (data at img + off[j], caplen[j], record number
    pktnum[j] or j + 1) into packed 2-bit cache entries out[(n + 3) / 4] */
 int tp_launch_classify(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, const uint32_t *pktnum,

@@ -169,7 +169,7 @@ DI int packet2tree(const u8 *d, u32 caplen) {
 
 __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img, const uint64_t *__restrict__ off,
                                                      const uint32_t *__restrict__ caplen, uint64_t n, int first_mode,
-                                                     tp_tree_t t) {
+                                                     uint64_t base, tp_tree_t t) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const u8 *d = img + off[j];
@@ -190,12 +190,13 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
         return;
     }
     if (first_mode) {  // add_tree_first_ipv4/ipv6 (tree.c:333-452): the first sighting decides
-        atomicMax((unsigned long long *)&t.slots[2 * s + 1], ~(unsigned long long)(2 * j));  // ~min = max ~
+        // (base: the shard's global record index, so shards' sightings merge by order)
+        atomicMax((unsigned long long *)&t.slots[2 * s + 1], ~(unsigned long long)(2 * (base + j)));  // ~min = max ~
         const uint32_t sd = tree_insert(t, node_key(v6, ip + (v6 ? 24 : 16)));
         if (sd == 0xffffffffu)
             atomicMin((unsigned long long *)t.err, (unsigned long long)j);
         else
-            atomicMax((unsigned long long *)&t.slots[2 * sd + 1], ~(unsigned long long)(2 * j + 1));
+            atomicMax((unsigned long long *)&t.slots[2 * sd + 1], ~(unsigned long long)(2 * (base + j) + 1));
         return;
     }
     const int ty = packet2tree(d, cl);  // add_tree_ipv4/ipv6 + add_tree_node (tree.c:454-538)
@@ -203,6 +204,22 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
         atomicMin((unsigned long long *)t.err, (unsigned long long)j);
     else if (ty >= 0)  // the counts share the key's 16-byte pair: one line per node
         atomicAdd((unsigned long long *)&t.slots[2 * s + 1], ty == 1 ? 1ull << 32 : 1ull);
+}
+
+// sharded auto modes: a node's value from the table merged across ranks (binary search)
+__global__ __launch_bounds__(256) void tp_tree_merged(tp_tree_t t, uint64_t cap, const uint64_t *__restrict__ keys,
+                                                      const uint64_t *__restrict__ vals, uint64_t n) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const uint64_t key = t.slots[2 * s];
+    if (!key) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < n && keys[lo] == key) t.slots[2 * s + 1] = vals[lo];
 }
 
 // tree_calculate (tree.c:540-565) + check_ip_tree (:219-272): the tcpr_dir_t of a source
@@ -371,12 +388,20 @@ extern "C" int tp_launch_classify(const uint8_t *img, const uint64_t *off, const
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+extern "C" int tp_launch_tree_merged(tp_tree_t tree, uint64_t capacity, const uint64_t *keys, const uint64_t *vals,
+                                     uint64_t n, void *stream) {
+    if (capacity == 0) return 0;
+    hipLaunchKernelGGL(tp_tree_merged, dim3((unsigned)((capacity + 255) / 256)), dim3(256), 0, (hipStream_t)stream, tree,
+                       capacity, keys, vals, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int tp_launch_tree(const uint8_t *img, const uint64_t *off, const uint32_t *caplen, uint64_t n_entries,
-                              const tp_dev_cfg_t *cfg, int automode, tp_tree_t tree, void *stream) {
+                              const tp_dev_cfg_t *cfg, int automode, uint64_t base, tp_tree_t tree, void *stream) {
     if (n_entries == 0) return 0;
     const uint64_t blocks = (n_entries + 255) / 256;
     if (blocks > 0x7fffffffull) return -1;
     hipLaunchKernelGGL(tp_tree_build, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, off, caplen,
-                       n_entries, automode == TP_AUTO_FIRST ? 1 : 0, tree);
+                       n_entries, automode == TP_AUTO_FIRST ? 1 : 0, base, tree);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -28,6 +28,8 @@ def _lib():
                 ("tcpprep_set_pkt_base", c_int, [vp, ctypes.c_uint64]),
                 ("tcpprep_set_device", c_int, [vp, c_int]),
                 ("tcpprep_last_entries", ctypes.c_int64, [vp]),
+                ("tcpprep_auto_table", ctypes.c_int64, [vp, ctypes.c_char_p, sz, vp, vp, sz]),
+                ("tcpprep_auto_merge", c_int, [vp, vp, vp, sz]),
                 ("tcpprep_close", c_int, [ctypes.POINTER(vp)])):
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
@@ -68,6 +70,26 @@ class TcpPrep:
         if self._L.tcpprep_set_pkt_base(self._ctx, base) != 0:
             raise ValueError(self.geterr())
 
+    def auto_table(self, pcap: bytes):
+        """--auto over shards: this shard's host table -> (keys, values) uint64 arrays"""
+        import numpy as np
+        n = self._L.tcpprep_auto_table(self._ctx, pcap, len(pcap), None, None, 0)
+        if n < 0:
+            raise RuntimeError(self.geterr())
+        k, v = np.zeros(max(n, 1), np.uint64), np.zeros(max(n, 1), np.uint64)
+        m = self._L.tcpprep_auto_table(self._ctx, pcap, len(pcap), k.ctypes.data, v.ctypes.data, n)
+        if m != n:
+            raise RuntimeError(self.geterr() or "host table changed between calls")
+        return k[:n], v[:n]
+
+    def auto_merge(self, keys, vals):
+        """every rank's (keys, values), concatenated: the table this shard classifies with"""
+        import numpy as np
+        k = np.ascontiguousarray(keys, np.uint64)
+        v = np.ascontiguousarray(vals, np.uint64)
+        if self._L.tcpprep_auto_merge(self._ctx, k.ctypes.data, v.ctypes.data, len(k)) != 0:
+            raise RuntimeError(self.geterr())
+
     def last_entries(self) -> int:
         return self._L.tcpprep_last_entries(self._ctx)
 
@@ -104,15 +126,27 @@ def _local_rank():
     return int(v) if v is not None else None
 
 
-def gpu_classifier(image: bytes, args, pkt_base: int, device=None):
+def gpu_classifier(image: bytes, args, pkt_base: int, device=None, merged=None):
     """one shard on the GPU (LOCAL_RANK's device by default, as gpu_editor) ->
-    (cache body bytes, entries, the cache comment)"""
+    (cache body bytes, entries, the cache comment); merged: --auto's table from every rank"""
     tp = TcpPrep(args, device=_local_rank() if device is None else device)
     try:
         tp.set_pkt_base(pkt_base)
+        if merged is not None:
+            tp.auto_merge(*merged)
         c = tp.cache(image)
         clen = int.from_bytes(c[22:24], "big")
         return c[24 + clen:], tp.last_entries(), c[24:24 + clen]
+    finally:
+        tp.close()
+
+
+def gpu_auto_table(image: bytes, args, pkt_base: int, device=None):
+    """--auto over shards, first pass: one shard's host table on the GPU -> (keys, values)"""
+    tp = TcpPrep(args, device=_local_rank() if device is None else device)
+    try:
+        tp.set_pkt_base(pkt_base)
+        return tp.auto_table(image)
     finally:
         tp.close()
 
@@ -152,35 +186,13 @@ def _is_auto(args) -> bool:
     return any(a == "-a" or a.startswith("--auto") for a in args)
 
 
-def prep_distributed(pcap: bytes, args, dist=None, classifier=None, comment: bytes = None):
-    """Sharded tcpprep (per-packet modes): each rank classifies its byte-balanced record
-    range (tcpedit_pcap_shards) with its global record base, one all_gather_object of
-    (ok, (body, entries[, comment]) or error) per rank, every rank assembles the same
-    cache file -- or every rank raises the same error.  With dist=None all shards run in
-    this process (one per 'rank' of a 2-way plan).
-
-    Decisions that end the job are taken identically on every rank before the collective
-    (--auto does not shard, an empty capture is the reference's "No packets were
-    processed"), and a classifier failure on one rank travels in the gathered tuple, so no
-    rank is left waiting in the collective."""
-    from .dist import plan
-    classifier = classifier or gpu_classifier
-    world = dist.get_world_size() if dist else 2
-    if world > 1 and _is_auto(args):
-        raise ValueError("--auto classifies by the whole capture's host table: it does not shard")
-    p = plan(pcap, world)
-    if p.total == 0:
-        raise ValueError("No packets were processed.  Filter too limiting?")
-
-    def run(k):
-        if p.count(k) == 0:  # a shard holding only the file header (fewer records than ranks)
-            return (b"", 0, None)
-        return classifier(p.image(pcap, k), args, p.pkt_base[k])
-
+def _exchange(dist, world, fn):
+    """fn() on this rank (or every shard with dist=None); one all_gather_object of
+    (ok, result or error) per rank, and every rank raises the same error"""
     if dist:
         r = dist.get_rank()
         try:
-            mine = (True, run(r))
+            mine = (True, fn(r))
         except Exception as e:  # noqa: BLE001 -- reported on every rank below
             mine = (False, f"rank {r}: {e}")
         got = [None] * world
@@ -188,9 +200,51 @@ def prep_distributed(pcap: bytes, args, dist=None, classifier=None, comment: byt
         errs = [m[1] for m in got if not m[0]]
         if errs:
             raise RuntimeError("; ".join(errs))
-        parts = [m[1] for m in got]
-    else:
-        parts = [run(k) for k in range(world)]
+        return [m[1] for m in got]
+    return [fn(k) for k in range(world)]
+
+
+def prep_distributed(pcap: bytes, args, dist=None, classifier=None, comment: bytes = None, tabler=None):
+    """Sharded tcpprep: each rank classifies its byte-balanced record range
+    (tcpedit_pcap_shards) with its global record base, one all_gather_object of
+    (ok, (body, entries[, comment]) or error) per rank, every rank assembles the same
+    cache file -- or every rank raises the same error.  With dist=None all shards run in
+    this process (one per 'rank' of a 2-way plan).
+
+    --auto first exchanges each shard's host table (tabler: the first pass, tree.c's
+    nodes with their counts / first sightings at global record numbers); every rank
+    merges all of them (tcpprep_auto_merge: counts add, the earliest sighting wins) and
+    classifies its shard by the whole capture's table, as the reference's one pass does.
+
+    Decisions that end the job are taken identically on every rank before the collective
+    (an empty capture is the reference's "No packets were processed"), and a failure on one
+    rank travels in the gathered tuple, so no rank is left waiting in a collective."""
+    import numpy as np
+    from .dist import plan
+    classifier = classifier or gpu_classifier
+    tabler = tabler or gpu_auto_table
+    world = dist.get_world_size() if dist else 2
+    p = plan(pcap, world)
+    if p.total == 0:
+        raise ValueError("No packets were processed.  Filter too limiting?")
+    auto = world > 1 and _is_auto(args)
+    merged = None
+    if auto:
+        def table(k):
+            if p.count(k) == 0:
+                return (np.zeros(0, np.uint64), np.zeros(0, np.uint64))
+            return tabler(p.image(pcap, k), args, p.pkt_base[k])
+        tabs = _exchange(dist, world, table)
+        merged = (np.concatenate([t[0] for t in tabs]), np.concatenate([t[1] for t in tabs]))
+
+    def run(k):
+        if p.count(k) == 0:  # a shard holding only the file header (fewer records than ranks)
+            return (b"", 0, None)
+        if auto:
+            return classifier(p.image(pcap, k), args, p.pkt_base[k], merged=merged)
+        return classifier(p.image(pcap, k), args, p.pkt_base[k])
+
+    parts = _exchange(dist, world, run)
     if comment is None:
         comment = next((pt[2] for pt in parts if len(pt) > 2 and pt[2] is not None), None)
     if comment is None:
