@@ -251,6 +251,12 @@ int tcpedit_batch_time(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double
  * from a hipEvent pair around that kernel in every run */
 int tcpedit_batch_time_kernels(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run,
                                double *ms_kernel);
+/* the record index rebuilt on the device from the batch's device image (te_index.hip:
+ * chunked speculative record-boundary discovery, checked against the chain, then the
+ * wave-lane tile cut), replacing the host walk's: `iters` timed builds after one sizing
+ * build, *ms = device ms per build.  0 applied; 1 not served (not a wave-lane config, or
+ * a guess missed the chain: the host index stays); TCPEDIT_ERROR on error */
+int tcpedit_batch_index_device(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms);
 void tcpedit_batch_close(tcpedit_batch_t *b);
 /* --fuzz-seed across shards.  The reference draws one tcpr_random() per record that
  * reaches the fuzz step from ONE run-wide state (fuzzing.c:8-20,87; tcpedit.c:250-258),

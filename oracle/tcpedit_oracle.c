@@ -1054,7 +1054,7 @@ static int remap_ipv6(const ocfg_t *c, const ocidr_t *cidr, uint8_t *addr)
     i = addr[i] & k;
     {
         uint32_t s1 = (8u - k) & 31u, s2 = k & 31u;
-        addr[i] = (uint8_t)((cidr->network6[j] & (0xff << s1)) | (addr[i] & (0xff >> s2)));
+        addr[i] = (uint8_t)((cidr->network6[j] & (0xffu << s1)) | (addr[i] & (0xffu >> s2)));
     }
     return 1;
 }

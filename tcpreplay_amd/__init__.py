@@ -80,6 +80,7 @@ def load():
         "tcpedit_batch_time_kernels": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double),
                                                ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_close": (None, [vp]),
+        "tcpedit_batch_index_device": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_fuzz_reach": (ctypes.c_int64, [vp, vp]),
         "tcpedit_fuzz_skip": (c_int, [vp, u64]),
         "tcpedit_batch_device_output": (vp, [vp]),
@@ -286,6 +287,16 @@ class Batch:
                                               ctypes.byref(kms)) < 0:
             raise RuntimeError(self._te.geterr())
         return ms.value, kms.value
+
+    def index_device(self, iters=1):
+        """rebuild the record index on the device (te_index.hip) -> (applied, device ms per
+        build); not applied when the config's tiles are not the wave lane's or a guess
+        missed the chain (the host index stays)"""
+        ms = ctypes.c_double()
+        rc = self._L.tcpedit_batch_index_device(self._te._ctx, self._b, int(iters), ctypes.byref(ms))
+        if rc < 0:
+            raise RuntimeError(self._te.geterr())
+        return rc == 0, ms.value
 
     def close(self):
         if self._b:

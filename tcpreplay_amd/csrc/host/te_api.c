@@ -11,6 +11,7 @@
 #include <pthread.h>
 
 #include "te_internal.h"
+#include "te_index.h"
 
 #define HIPCHK(t, call)                                                                   \
     do {                                                                                  \
@@ -64,6 +65,10 @@ struct tcpedit_batch_s {
     uint64_t *slots_host;    /* their {packets, bytes, edited, -} totals, read back after a run */
     hipEvent_t *kev;         /* event pool for tcpedit_batch_time_kernels (2 per run) */
     int idx_pinned;          /* tiles / pkt_rel are pinned arrays of fixed capacity (a pipeline slot) */
+    /* the device index (tcpedit_batch_index_device): the cut walk_range made, and whether
+       the device can make it (wave-lane tiles over contiguous records) */
+    uint32_t cut_budget, cut_max_pkts, cut_growth;
+    int cut_device_ok;
     uint8_t ohdr[24];        /* the output file header, the source of its upload */
     uint8_t *res_pinned;     /* pipeline slot: page-locked landing area of a run's counters, error
                                 words and wave-lane slots (a D2H into pageable memory would block) */
@@ -504,6 +509,10 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
     proto.stop_error_pkt = -1;
     proto.growth = rec_growth(&t->cfg);
+    b->cut_budget = proto.budget;
+    b->cut_max_pkts = proto.max_pkts;
+    b->cut_growth = proto.growth;
+    b->cut_device_ok = proto.wave && !proto.pad && (!proto.slot_mode || proto.grow_fast);
 
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     if (b->idx_pinned) { /* a pipeline slot: the chunk budget bounds both (16 B per record at least) */
@@ -1333,6 +1342,173 @@ size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap)
 
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b) { return b ? b->d_out : NULL; }
 uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b) { return b ? b->in_len : 0; }
+
+/* The record index built on the device (te_index.hip) from the batch's device image,
+ * replacing the host walk's: the count, scan and write passes `iters` times after one
+ * sizing run; *ms = device ms per index build (HIP events).  Returns 0 applied, 1 not
+ * served here (the config's tiles are not wave-lane tiles over contiguous records, or a
+ * speculative guess missed the chain: the host index stays), -1 error. */
+/* diagnostics / host tests (the sanitizer and thread-sanitizer runs): the host record
+ * walk (index_image, the walker pool included) over a pcap image, without the device */
+int tcpedit_debug_index_host(tcpedit_t *t, const void *pcap, size_t len, uint64_t *n_pkts, uint64_t *n_tiles,
+                             uint64_t *walk_end)
+{
+    if (!t || !pcap)
+        return TCPEDIT_ERROR;
+    if (te_ensure_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    tcpedit_batch_t *b = calloc(1, sizeof(*b));
+    if (!b)
+        return TCPEDIT_ERROR;
+    b->ctx = t;
+    const int rc = index_image(t, b, (const uint8_t *)pcap, (const uint8_t *)pcap, len);
+    if (rc == 0) {
+        if (n_pkts)
+            *n_pkts = b->n_pkts;
+        if (n_tiles)
+            *n_tiles = b->n_tiles;
+        if (walk_end)
+            *walk_end = b->walk_end;
+    }
+    free(b->tiles);
+    free(b->pkt_rel);
+    for (int i = 0; i < 64; i++) {
+        free(b->wk_tiles[i]);
+        free(b->wk_rel[i]);
+    }
+    free(b);
+    return rc < 0 ? TCPEDIT_ERROR : TCPEDIT_OK;
+}
+
+int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms)
+{
+    if (!t || !b || iters < 1)
+        return TCPEDIT_ERROR;
+    if (!b->cut_device_ok || b->in_len <= 24)
+        return 1;
+    const uint64_t body = b->in_len - 24;
+    const uint64_t avg = b->n_tiles ? (b->walk_end - 24) / b->n_tiles : 4096;
+    uint64_t W = (8 * (avg ? avg : 64) + 63) & ~63ull; /* about 8 tiles a window */
+    if (W < 4096)
+        W = 4096;
+    if (W > 65536)
+        W = 65536;
+    const uint64_t nwin = (body + W - 1) / W;
+    if (nwin > 0x7fffffffull)
+        return 1;
+    uint8_t *wbuf = NULL;
+    hipEvent_t e0 = NULL, e1 = NULL;
+    int rc = TCPEDIT_ERROR;
+    uint64_t tot[IDX_T__N];
+    const size_t w64 = 8 * nwin, w32 = 4 * nwin;
+    HIPCHK(t, hipMalloc((void **)&wbuf, 7 * w64 + 4 * w32 + 8 * IDX_T__N + 64));
+    IdxArgs a;
+    memset(&a, 0, sizeof a);
+    a.img = b->d_in;
+    a.len = b->in_len;
+    a.sw = b->swapped;
+    a.nsec = b->nsec;
+    a.W = W;
+    a.nwin = (uint32_t)nwin;
+    a.budget = b->cut_budget;
+    a.max_pkts = b->cut_max_pkts;
+    a.growth = b->cut_growth;
+    a.w_entry = (uint64_t *)wbuf;
+    a.w_exit = a.w_entry + nwin;
+    a.w_recbytes = a.w_exit + nwin;
+    a.w_scratch = a.w_recbytes + nwin;
+    a.p_base = a.w_scratch + nwin;
+    a.t_base = a.p_base + nwin;
+    a.s_base = a.t_base + nwin;
+    a.totals = a.s_base + nwin;
+    a.w_nrec = (uint32_t *)(a.totals + IDX_T__N);
+    a.w_ntile = a.w_nrec + nwin;
+    a.w_flags = a.w_ntile + nwin;
+    a.w_err = a.w_flags + nwin;
+    /* sizing run: count + scan, the totals, then room for the tiles */
+    if (te_launch_index(&a, 0, t->stream) || te_launch_index(&a, 1, t->stream)) {
+        te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
+        goto out;
+    }
+    HIPCHK(t, hipMemcpyAsync(tot, a.totals, sizeof tot, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    if (tot[IDX_T_BAD]) {
+        rc = 1;
+        goto out;
+    }
+    if (tot[IDX_T_RECS] != b->n_pkts) { /* the chain is the chain: a mismatch is a bug */
+        te_seterr(t, "device index found %llu records, the host walk %llu", (unsigned long long)tot[IDX_T_RECS],
+                  (unsigned long long)b->n_pkts);
+        goto out;
+    }
+    const uint64_t nt = tot[IDX_T_TILES];
+    if (nt > b->n_tiles) { /* tiles never span windows: there may be a few more */
+        hipFree(b->d_tiles);
+        b->d_tiles = NULL;
+        hipFree(b->d_tile_list);
+        b->d_tile_list = NULL;
+        hipFree(b->d_ws);
+        b->d_ws = NULL;
+        HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (nt + 1)));
+        HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (nt + 1)));
+        b->ws_bytes = WS_SLOTS(nt) + 64 + (b->fast_kind == TE_FAST_WAVE ? 32 * (uint64_t)te_wave_grid() : 0);
+        HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
+    }
+    if (tot[IDX_T_SCRATCH] > b->scratch_bytes) {
+        hipFree(b->d_scratch);
+        b->d_scratch = NULL;
+        HIPCHK(t, hipMalloc((void **)&b->d_scratch, tot[IDX_T_SCRATCH]));
+        b->scratch_bytes = tot[IDX_T_SCRATCH];
+    }
+    a.tiles = b->d_tiles;
+    a.pkt_rel = b->d_pkt_rel;
+    if (te_launch_index(&a, 2, t->stream)) {
+        te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
+        goto out;
+    }
+    /* timed runs: the three passes, device-resident end to end */
+    HIPCHK(t, hipEventCreate(&e0));
+    HIPCHK(t, hipEventCreate(&e1));
+    HIPCHK(t, hipEventRecord(e0, t->stream));
+    for (int i = 0; i < iters; i++)
+        if (te_launch_index(&a, 0, t->stream) || te_launch_index(&a, 1, t->stream) ||
+            te_launch_index(&a, 2, t->stream)) {
+            te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
+            goto out;
+        }
+    HIPCHK(t, hipEventRecord(e1, t->stream));
+    HIPCHK(t, hipEventSynchronize(e1));
+    {
+        float f = 0;
+        HIPCHK(t, hipEventElapsedTime(&f, e0, e1));
+        if (ms)
+            *ms = f / iters;
+    }
+    b->n_tiles = nt;
+    b->has_zero_cap = tot[IDX_T_ZERO] != 0;
+    b->walk_end = tot[IDX_T_END];
+    b->walk_stop = tot[IDX_T_STOP] == IDX_STOP ? 1 : tot[IDX_T_STOP] == IDX_ERROR ? 2 : 0;
+    b->stop_error_pkt = tot[IDX_T_ERR_REC] == ~0ull ? -1 : (int64_t)tot[IDX_T_ERR_REC];
+    b->out_cap = 24 + 64 + tot[IDX_T_BYTES];
+    /* the lane hints and the wave lane's per-block slots follow the new tiles */
+    HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    b->gen_hint_ok = 0;
+    b->launches = 0;
+    b->last_listed = 0;
+    b->status_valid = 0;
+    rc = 0;
+out:
+    if (e0)
+        hipEventDestroy(e0);
+    if (e1)
+        hipEventDestroy(e1);
+    hipFree(wbuf);
+    return rc;
+fail:
+    rc = TCPEDIT_ERROR;
+    goto out;
+}
 
 int tcpedit_batch_time(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms_per_run)
 {
