@@ -258,6 +258,11 @@ int tcpedit_batch_time_kernels(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters
  * a guess missed the chain: the host index stays); TCPEDIT_ERROR on error */
 int tcpedit_batch_index_device(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms);
 void tcpedit_batch_close(tcpedit_batch_t *b);
+/* pcapng input: the batch and rewrite calls take a pcapng image as libpcap's
+ * reader delivers it to tcprewrite -- classic records, microseconds, the interfaces' link
+ * type (te_pcapng.c).  This is that conversion on its own: a malloc'd classic pcap image in
+ * *out (free() it); 0, or -1 for a file libpcap would refuse */
+int tcpedit_pcapng_to_pcap(const void *in, size_t len, void **out, size_t *out_len);
 /* --fuzz-seed across shards.  The reference draws one tcpr_random() per record that
  * reaches the fuzz step from ONE run-wide state (fuzzing.c:8-20,87; tcpedit.c:250-258),
  * so a shard's stream starts after the draws of every earlier shard.

@@ -860,6 +860,15 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     tcpedit_batch_t *b = calloc(1, sizeof(*b));
     b->ctx = t;
     b->pkt_base = pkt_base;
+    uint8_t *ng = NULL; /* a pcapng image, as libpcap's reader delivers it (te_pcapng.c) */
+    if (te_is_pcapng((const uint8_t *)pcap, len)) {
+        char e[256];
+        if (te_pcapng_to_pcap((const uint8_t *)pcap, len, &ng, &len, e, sizeof e) < 0) {
+            te_seterr(t, "%s", e);
+            goto fail;
+        }
+        pcap = ng;
+    }
     if (index_image(t, b, (const uint8_t *)pcap, (const uint8_t *)pcap, len) < 0)
         goto fail;
     if (b->linktype != (uint32_t)t->dlt) {
@@ -901,8 +910,11 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     HIPCHK(t, hipEventCreate(&b->ev0));
     HIPCHK(t, hipEventCreate(&b->ev1));
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    free(ng);
     return b;
 fail:
+    hipStreamSynchronize(t->stream);
+    free(ng);
     tcpedit_batch_close(b);
     return NULL;
 }
@@ -1844,6 +1856,19 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
 int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, const void *cache, size_t cache_len,
                                    void *out, size_t out_cap, size_t *out_len, size_t chunk_bytes)
 {
+    if (t && in && te_is_pcapng((const uint8_t *)in, in_len)) { /* as libpcap's reader delivers it */
+        uint8_t *ng = NULL;
+        size_t ng_len = 0;
+        char e[256];
+        if (te_pcapng_to_pcap((const uint8_t *)in, in_len, &ng, &ng_len, e, sizeof e) < 0) {
+            te_seterr(t, "%s", e);
+            return TCPEDIT_ERROR;
+        }
+        const int rc = tcpedit_rewrite_pcap_pipelined(t, ng, ng_len, cache, cache_len, out, out_cap, out_len,
+                                                      chunk_bytes);
+        free(ng);
+        return rc;
+    }
     const uint8_t *img = in;
     uint8_t *dst = out;
     uint8_t *d_dirbits = NULL;

@@ -99,4 +99,7 @@ extern uint32_t te_fuzz_init_seed, te_fuzz_init_factor;
 typedef struct te_pipe_s te_pipe_t;
 void te_pipe_free(tcpedit_t *t);
 
+/* te_pcapng.c: a pcapng image as libpcap's reader delivers it (classic pcap, microseconds) */
+int te_is_pcapng(const uint8_t *img, size_t len);
+int te_pcapng_to_pcap(const uint8_t *in, size_t len, uint8_t **out_img, size_t *out_len, char *err, size_t errlen);
 #endif

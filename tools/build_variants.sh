@@ -13,7 +13,8 @@ while [ $# -ge 2 ]; do
     name=$1; flags=$2; shift 2
     tmp=$(mktemp -d)
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $INC $flags -c "$CS/kernels/tcpedit_kernels.hip" -o "$tmp/k.o" &
-    for f in te_args te_api te_autoopts; do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $INC $flags -c "$CS/kernels/te_index.hip" -o "$tmp/ix.o" &
+    for f in te_args te_api te_autoopts te_pcapng; do
         gcc -O2 -std=gnu11 -fPIC -D__HIP_PLATFORM_AMD__ $INC $flags -c "$CS/host/$f.c" -o "$tmp/$f.o"
     done
     wait
