@@ -2868,7 +2868,10 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
         uint32_t caplen = rh[2], len = rh[3];
         if (ip_ + 16 + caplen > in_len)
             break; /* truncated record: libpcap stops */
-        if (caplen > MAX_SNAPLEN || len > MAX_SNAPLEN) {
+        if (caplen > MAX_SNAPLEN)
+            break; /* libpcap's reader refuses the record ("invalid packet capture length"):
+                      pcap_next returns NULL and tcprewrite's loop ends (tcprewrite.c:289) */
+        if (len > MAX_SNAPLEN) { /* tcprewrite.c:296-297 errx() */
             seterr("Frame too big");
             rc = -1;
             break;

@@ -1835,6 +1835,15 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
     const uint8_t *img = in;
     if (!t || !img || in_len < 24)
         return 0;
+    if (te_is_pcapng(img, in_len)) { /* the classic image the reader delivers */
+        uint8_t *ng = NULL;
+        size_t ng_len = 0;
+        if (te_pcapng_to_pcap(img, in_len, &ng, &ng_len, NULL, 0) < 0)
+            return 24 + 64;
+        const size_t b = tcpedit_output_bound(t, ng, ng_len);
+        free(ng);
+        return b;
+    }
     uint32_t magic;
     memcpy(&magic, img, 4);
     const int sw = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
