@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
+    ap.add_argument("--no-device-index", action="store_true", help="skip the device record index line")
+    ap.add_argument("--no-packet-latency", action="store_true", help="skip the tcpedit_packet latency line")
     ap.add_argument("--extra", default="c3,c4,c5,c2x10,seed,hdr,vdel,efcs,fz,prep",
                     help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
@@ -246,6 +248,37 @@ def main():
                                       if single else "a hipEvent pair around the kernel in each of K runs",
                      "alg_bytes_per_launch": alg_bytes},
     }
+    # the per-packet API (tcpedit_packet, as tcprewrite calls it once a record): one 64-byte
+    # packet a call through the device (stage, edit, read back), beside the oracle's
+    # per-record CPU time on the bulk workload
+    if rank == 0 and not opt.no_packet_latency:
+        from tcpreplay_amd import synth as S
+        L = TA.load()
+        f = L.tcpedit_debug_packet_latency
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        te1 = TA.TcpEdit(WORKLOADS[opt.workload][2])
+        pkt = S.records(S.pcap_fixed(1, 64, seed=3))[0][4]
+        us = ctypes.c_double()
+        if f(te1._ctx, pkt, len(pkt), 2000, ctypes.byref(us)) == 0:
+            result["packet_api"] = {"us_per_call": round(us.value, 2), "calls": 2000,
+                                    "path": "tcpedit_packet: pinned staging, H2D, edit kernel, D2H, sync per call"}
+        te1.close()
+    # the record index built on the device (te_index.hip) from the HBM-resident image, in
+    # place of the host walk: its build time, and the edit over the tiles it cut -- index +
+    # edit is the device pipeline from the raw capture bytes
+    if rank == 0 and not opt.no_device_index:
+        applied, ims = b.index_device(iters=max(5, opt.steps // 20))
+        if applied:
+            pms2 = b.time(opt.steps)
+            result["device_index"] = {
+                "index_ms": round(ims, 5), "pipeline_ms": round(pms2, 5),
+                "index_plus_pipeline_ms": round(ims + pms2, 5),
+                "frac_hbm_peak_with_index": round(alg_bytes / ((ims + pms2) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "path": "windowed speculative record-boundary discovery + wave-lane tile cut on the device "
+                        "(count, scan, write passes), then the edit over those tiles"}
+        else:
+            result["device_index"] = {"applied": False}
     b.close()
     te.close()
 

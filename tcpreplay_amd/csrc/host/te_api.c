@@ -1392,6 +1392,36 @@ int tcpedit_debug_index_host(tcpedit_t *t, const void *pcap, size_t len, uint64_
     return rc < 0 ? TCPEDIT_ERROR : TCPEDIT_OK;
 }
 
+static double te_now(void);
+/* diagnostics / bench: the per-packet API's latency -- `iters` tcpedit_packet calls on
+ * one packet as tcprewrite makes them (its buffer reused, tcprewrite.c:301-317), wall
+ * microseconds per call */
+int tcpedit_debug_packet_latency(tcpedit_t *t, const uint8_t *pkt, uint32_t caplen, int iters, double *us)
+{
+    if (!t || !pkt || iters < 1 || caplen > 262144u)
+        return TCPEDIT_ERROR;
+    unsigned char *buf = malloc(262144 + 4096);
+    if (!buf)
+        return TCPEDIT_ERROR;
+    struct pcap_pkthdr h;
+    int rc = TCPEDIT_OK;
+    double t0 = 0;
+    for (int i = -1; i < iters && rc != TCPEDIT_ERROR; i++) { /* (call -1: first-use staging, untimed) */
+        if (i == 0)
+            t0 = te_now();
+        memset(&h, 0, sizeof h);
+        h.caplen = h.len = caplen;
+        memcpy(buf, pkt, caplen);
+        struct pcap_pkthdr *hp = &h;
+        unsigned char *d = buf;
+        rc = tcpedit_packet(t, &hp, &d, TCPR_DIR_C2S);
+    }
+    if (us)
+        *us = (te_now() - t0) * 1e6 / iters;
+    free(buf);
+    return rc == TCPEDIT_ERROR ? TCPEDIT_ERROR : TCPEDIT_OK;
+}
+
 int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms)
 {
     if (!t || !b || iters < 1)
