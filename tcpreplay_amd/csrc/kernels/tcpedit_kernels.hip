@@ -1138,6 +1138,15 @@ __device__ __forceinline__ uint32_t wave_prev(uint32_t v) {
 // the compiler, reasoning per lane, would forward a lane's own store to its later load of
 // the same address across other lanes' stores to it (it did: the chunk map's prefix read
 // came back as the zeros this lane had written, without the other lanes' marks)
+#ifndef WK_SKIP_TOUCHED
+#define WK_SKIP_TOUCHED 0
+#endif
+#ifndef WK_SIZED_STREAM
+#define WK_SIZED_STREAM 0
+#endif
+#ifndef WK_PLAIN_STREAM
+#define WK_PLAIN_STREAM 1
+#endif
 #define WK_LANES_SYNC() asm volatile("" ::: "memory")
 
 __device__ __forceinline__ void wk_chunk_map(uint32_t *P, uint32_t nown, uint32_t o0, uint32_t X, bool on,
@@ -1244,8 +1253,14 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
     WK_LANES_SYNC();
     // every chunk stored unconditionally (a branch per store costs more than the bytes): the
     // few a change meets are stored again below, by the same wave, in order
+#if WK_SKIP_TOUCHED
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        if ((kv[k] >> 7) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
+#else
 #pragma unroll
     for (int k = 0; k < 7; ++k) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
+#endif
     // the chunks this lane's change meets: both built on every lane (reads in flight
     // together), stored where they exist
     {
@@ -1571,11 +1586,12 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             if constexpr (GROW) {
                 // record j's tag at output offset rel_j + 28 + 4 j (its input byte rel_j + 28 on)
                 wk_store_sized<true>(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0,
-                                     my_rel + 28u + 4u * (uint32_t)lane, on, a.vlan_tag_word, lane, stream);
+                                     my_rel + 28u + 4u * (uint32_t)lane, on, a.vlan_tag_word, lane,
+                                     stream && WK_SIZED_STREAM);
             } else if constexpr (SHRINK) {
                 const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
                 wk_store_sized<false>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
-                                      Dj - 4u * (uint32_t)lane, on, 0u, lane, stream);
+                                      Dj - 4u * (uint32_t)lane, on, 0u, lane, stream && WK_SIZED_STREAM);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -1588,7 +1604,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
 #define WK_WR(k)                                                                                       \
         if constexpr (k < WK_KL) {                                                                         \
             g_u4 *dk = (g_u4 *)(gout + C0 + ((uint64_t)umin32((uint32_t)lane + 64u * k, nown - 1u) << 4)); \
-            if (stream)                                                                                    \
+            if (stream && WK_PLAIN_STREAM)                                                                 \
                 __builtin_nontemporal_store((u32x4){w##k.x, w##k.y, w##k.z, w##k.w}, (g_v4 *)dk);         \
             else                                                                                           \
                 *dk = w##k;                                                                                \

@@ -21,6 +21,8 @@ CASES = {
            ["--endpoints=10.10.0.1:10.10.0.2", "--enet-dmac=00:12:13:14:15:16,00:22:33:44:55:66",
             "--enet-smac=00:22:33:44:55:66,00:12:13:14:15:16", "--enet-vlan=add", "--enet-vlan-tag=45",
             "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"]),
+    "vdel": (lambda: S.pcap_imix(1_000_000, seed=1, vlan=0xB02D), ["--enet-vlan=del", "--fixcsum"]),
+    "efcs": (lambda: S.pcap_imix(1_000_000, seed=1, fcs=True), ["--efcs", "--fixcsum"]),
 }
 CACHES = {"c4": lambda: S.tcpprep_cache(1_000_000, seed=1)}
 
