@@ -4,7 +4,9 @@
  * A plain-C, single-threaded CPU restatement of the reference's per-packet
  * edit path: libtcpedit's tcpedit_packet() (src/tcpedit/tcpedit.c:46-366) as
  * driven by tcprewrite's rewrite_packets() (src/tcprewrite.c:260-373), for
- * DLT_EN10MB input and the en10mb, user and hdlc encoders, --fuzz-seed included
+ * DLT_EN10MB, LINUX_SLL, LINUX_SLL2, RAW, NULL, LOOP, PPP_SERIAL and C_HDLC input
+ * (the decoders of src/tcpedit/plugins/dlt_*) and the en10mb, user, hdlc, pppserial and
+ * non-encoding plugins as encoders, --fuzz-seed included
  * (src/tcpedit/fuzzing.c, with the reference's second L2/L3 pass after a fuzz).  Every function cites the reference file:line
  * it restates (paths relative to appneta/tcpreplay 4.5.5).
  *
@@ -168,8 +170,15 @@ typedef struct {
     uint8_t user_l2client[255], user_l2server[255];
     uint16_t hdlc_address, hdlc_control; /* hdlc_config_t (hdlc_types.h), 65535 = unset */
     int user_dlt_set, user_dlt;
+    int decoder;            /* DEC_*: the input DLT's plugin (tcpedit_dlt_init, dlt_plugins.c:115-160) */
+    int in_dlt;             /* the input DLT (pcap_datalink) */
 } ocfg_t;
-enum { ENC_EN10MB = 0, ENC_USER, ENC_HDLC };
+/* encoders: en10mb, user, hdlc; NOENC = linuxsll/linuxsll2/raw/null/loop, whose encode
+   always fails (linuxsll.c:201-208, linuxsll2.c:213-221, raw.c:194-201, null.c:192-198);
+   PPP = pppserial, whose encode leaves the packet as it is (pppserial.c:239-251) */
+enum { ENC_EN10MB = 0, ENC_USER, ENC_HDLC, ENC_NOENC, ENC_PPP };
+/* decoders (NULL and LOOP share dlt_null's functions, loop.c:47-64) */
+enum { DEC_EN10MB = 0, DEC_SLL, DEC_SLL2, DEC_RAW, DEC_NULL, DEC_PPP, DEC_CHDLC };
 
 /* decoder/encoder per-context scratch (tcpeditdlt_t + en10mb_extra_t) which
  * the reference keeps across packets (plugins_types.h:100-131). */
@@ -1459,6 +1468,119 @@ static int en10mb_decode(ostate_t *s, const uint8_t *pkt, int pktlen)
     return TCPEDIT_OK;
 }
 
+/* ---- the other decoders (src/tcpedit/plugins/dlt_*): plugin_proto and plugin_decode ---- */
+#define ARPHRD_ETHER 1       /* linuxsll_types.h:56 */
+#define ARPHRD_LOOPBACK 772
+
+/* dlt_null_proto: null.c:206-236 (DLT_NULL and DLT_LOOP): the address family in either
+   byte order; PF_INET6 is 10 here, and the BSDs' 24/28/30 are taken too */
+static int null_proto(const uint8_t *pkt, int pktlen)
+{
+    if (pktlen < 4)
+        return TCPEDIT_ERROR;
+    const uint32_t af = ld32(pkt), saf = __builtin_bswap32(af);
+    if (af == 2 || saf == 2)
+        return htons(ETHERTYPE_IP);
+    if (af == 10 || saf == 10 || af == 24 || saf == 24 || af == 28 || saf == 28 || af == 30 || saf == 30)
+        return htons(ETHERTYPE_IP6);
+    seterr("Unsupported DLT_NULL/DLT_LOOP PF_ type: 0x%04x", af);
+    return TCPEDIT_ERROR;
+}
+
+/* dlt_raw_proto: raw.c:206-231 (the IP version nibble) */
+static int raw_proto(const uint8_t *pkt, int pktlen)
+{
+    if (pktlen < 20)
+        return TCPEDIT_ERROR;
+    if ((pkt[0] >> 4) == 4)
+        return htons(ETHERTYPE_IP);
+    if ((pkt[0] >> 4) == 6)
+        return htons(ETHERTYPE_IP6);
+    seterr("Unsupported DLT_RAW packet: doesn't look like IPv4 or IPv6");
+    return TCPEDIT_ERROR;
+}
+
+/* the decoder's proto (tcpedit_dlt_proto on the source DLT, tcpedit.c:96) */
+static int decoder_proto(const ocfg_t *c, const uint8_t *pkt, int pktlen)
+{
+    switch (c->decoder) {
+    case DEC_SLL: /* linuxsll.c:213-226 */
+        return pktlen < 16 ? TCPEDIT_ERROR : ld16(pkt + 14);
+    case DEC_SLL2: /* linuxsll2.c:226-238 */
+        return pktlen < 20 ? TCPEDIT_ERROR : ld16(pkt);
+    case DEC_RAW:
+        return raw_proto(pkt, pktlen);
+    case DEC_NULL:
+        return null_proto(pkt, pktlen);
+    case DEC_PPP: /* pppserial.c:257-281: the ethertype in host order, so tcpedit.c:123,149 never match it */
+        if (pktlen < 4)
+            return TCPEDIT_ERROR;
+        return ntohs(ld16(pkt + 2)) == 0x0021 ? ETHERTYPE_IP : TCPEDIT_SOFT_ERROR;
+    case DEC_CHDLC: /* hdlc.c:299-311 */
+        return pktlen < 4 ? TCPEDIT_ERROR : ld16(pkt + 2);
+    default:
+        return en10mb_proto(pkt, pktlen);
+    }
+}
+
+/* the decoder (plugin_decode): l2len, proto and, for the Linux cooked headers, the source
+   address.  None of them touches the en10mb extra fields (vlan, vlan_offset, vlan_proto,
+   dst_modified), which keep their zeroed start: the decoder's extra buffer (MAXPACKET
+   bytes) is larger than en10mb_extra_t, so en10mb's init keeps it (en10mb.c:100-110) */
+static int decoder_decode(const ocfg_t *c, ostate_t *s, const uint8_t *pkt, int pktlen)
+{
+    switch (c->decoder) {
+    case DEC_SLL:  /* linuxsll.c:170-194 */
+    case DEC_SLL2: /* linuxsll2.c:181-205 */
+    {
+        const int sll = c->decoder == DEC_SLL, hl = sll ? 16 : 20;
+        if (pktlen < hl)
+            return TCPEDIT_ERROR;
+        s->proto = ld16(pkt + (sll ? 14 : 0));
+        s->l2len = hl;
+        const int type = ntohs(ld16(pkt + (sll ? 2 : 8)));
+        if (type != ARPHRD_ETHER && type != ARPHRD_LOOPBACK) {
+            seterr("DLT_LINUX_SLL pcap's must contain only ethernet or loopback packets");
+            return TCPEDIT_ERROR;
+        }
+        memcpy(s->srcaddr, pkt + (sll ? 6 : 12), 6);
+        return TCPEDIT_OK;
+    }
+    case DEC_RAW: { /* raw.c:170-190 */
+        if (pktlen == 0)
+            return TCPEDIT_ERROR;
+        const int p = raw_proto(pkt, pktlen);
+        if (p == TCPEDIT_ERROR)
+            return TCPEDIT_ERROR;
+        s->proto = (uint16_t)p;
+        s->l2len = 0;
+        return TCPEDIT_OK;
+    }
+    case DEC_NULL: { /* null.c:171-187 */
+        const int p = null_proto(pkt, pktlen);
+        if (p == TCPEDIT_ERROR)
+            return TCPEDIT_ERROR;
+        s->proto = (uint16_t)p;
+        s->l2len = 4;
+        return TCPEDIT_OK;
+    }
+    case DEC_PPP: /* pppserial.c:196-231 */
+        if (pktlen < 4)
+            return TCPEDIT_ERROR;
+        s->proto = ntohs(ld16(pkt + 2)) == 0x0021 ? htons(ETHERTYPE_IP) : ld16(pkt + 2);
+        s->l2len = 4;
+        return TCPEDIT_OK;
+    case DEC_CHDLC: /* hdlc.c:192-218 (its address/control extras are never marked filled) */
+        if (pktlen < 4)
+            return TCPEDIT_ERROR;
+        s->proto = ld16(pkt + 2);
+        s->l2len = 4;
+        return TCPEDIT_OK;
+    default:
+        return en10mb_decode(s, pkt, pktlen);
+    }
+}
+
 /* dlt_en10mb_encode: en10mb.c:479-736 (en10mb decoder -> en10mb encoder) */
 static int en10mb_encode(const ocfg_t *c, ostate_t *s, uint8_t *packet, int pktlen, int dir)
 {
@@ -1469,23 +1591,28 @@ static int en10mb_encode(const ocfg_t *c, ostate_t *s, uint8_t *packet, int pktl
         seterr("Non-VLAN tagged packet requires --enet-vlan-tag");
         return TCPEDIT_ERROR;
     }
-    switch (c->vlan) {
-    case VLAN_ADD:
-        oldl2len = s->vlan_offset;
-        newl2len = s->vlan_offset + 4;
-        break;
-    case VLAN_DEL:
-        if (s->vlan) {
-            oldl2len = s->vlan_offset + 4;
-            newl2len = s->vlan_offset;
-        }
-        break;
-    case VLAN_OFF:
-        if (s->vlan) {
+    if (c->decoder == DEC_EN10MB) {
+        switch (c->vlan) {
+        case VLAN_ADD:
             oldl2len = s->vlan_offset;
-            newl2len = s->vlan_offset;
+            newl2len = s->vlan_offset + 4;
+            break;
+        case VLAN_DEL:
+            if (s->vlan) {
+                oldl2len = s->vlan_offset + 4;
+                newl2len = s->vlan_offset;
+            }
+            break;
+        case VLAN_OFF:
+            if (s->vlan) {
+                oldl2len = s->vlan_offset;
+                newl2len = s->vlan_offset;
+            }
+            break;
         }
-        break;
+    } else { /* another DLT -> ethernet (en10mb.c:544-548) */
+        newl2len = c->vlan == VLAN_ADD ? 18 : 14;
+        oldl2len = (uint32_t)s->l2len;
     }
     if ((uint32_t)pktlen < newl2len || pktlen + newl2len - s->l2len > MAXPACKET)
         return TCPEDIT_ERROR;
@@ -1500,41 +1627,38 @@ static int en10mb_encode(const ocfg_t *c, ostate_t *s, uint8_t *packet, int pktl
     uint8_t *eth = packet + s->l2offset;
     uint8_t *dhost = eth, *shost = eth + 6;
     const bool l2skip = c->l2_skip_broadcast;
-    if (dir == DIR_C2S) {
-        if (c->mac_mask & MASK_SMAC1) {
-            if ((l2skip && is_unicast_ethernet(s->srcaddr)) || !l2skip)
-                memcpy(shost, c->intf1_smac, 6);
+    /* the decoder's address type (plugin_l2addr_type): ETHERNET for en10mb and the Linux
+       cooked headers, which have a source address (the destination stays as the zeroed
+       context left it); none for the others (en10mb.c:586-659) */
+    const bool eth_addr = c->decoder == DEC_EN10MB || c->decoder == DEC_SLL || c->decoder == DEC_SLL2;
+    if (dir == DIR_C2S || dir == DIR_S2C) {
+        const bool c2s = dir == DIR_C2S;
+        const int sm = c2s ? MASK_SMAC1 : MASK_SMAC2, dm = c2s ? MASK_DMAC1 : MASK_DMAC2;
+        if (c->mac_mask & sm) {
+            if ((eth_addr && ((l2skip && is_unicast_ethernet(s->srcaddr)) || !l2skip)) || !eth_addr)
+                memcpy(shost, c2s ? c->intf1_smac : c->intf2_smac, 6);
             else
                 memcpy(shost, s->srcaddr, 6);
-        } else {
-            s->src_modified = memcmp(shost, s->srcaddr, 6) != 0;
+        } else if (eth_addr) {
+            if (c2s)
+                s->src_modified = memcmp(shost, s->srcaddr, 6) != 0;
             memcpy(shost, s->srcaddr, 6);
+        } else {
+            seterr("Please provide a source address");
+            return TCPEDIT_ERROR;
         }
-        if (c->mac_mask & MASK_DMAC1) {
-            if ((l2skip && is_unicast_ethernet(s->dstaddr)) || !l2skip)
-                memcpy(dhost, c->intf1_dmac, 6);
+        if (c->mac_mask & dm) {
+            if ((eth_addr && ((l2skip && is_unicast_ethernet(s->dstaddr)) || !l2skip)) || !eth_addr)
+                memcpy(dhost, c2s ? c->intf1_dmac : c->intf2_dmac, 6);
             else
                 memcpy(dhost, s->dstaddr, 6);
-        } else {
-            s->dst_modified = memcmp(dhost, s->dstaddr, 6) != 0;
+        } else if (eth_addr) {
+            if (c2s) /* (S2C leaves it: the last C2S packet's value carries over) */
+                s->dst_modified = memcmp(dhost, s->dstaddr, 6) != 0;
             memcpy(dhost, s->dstaddr, 6);
-        }
-    } else if (dir == DIR_S2C) {
-        if (c->mac_mask & MASK_SMAC2) {
-            if ((l2skip && is_unicast_ethernet(s->srcaddr)) || !l2skip)
-                memcpy(shost, c->intf2_smac, 6);
-            else
-                memcpy(shost, s->srcaddr, 6);
         } else {
-            memcpy(shost, s->srcaddr, 6);
-        }
-        if (c->mac_mask & MASK_DMAC2) {
-            if ((l2skip && is_unicast_ethernet(s->dstaddr)) || !l2skip)
-                memcpy(dhost, c->intf2_dmac, 6);
-            else
-                memcpy(dhost, s->dstaddr, 6);
-        } else {
-            memcpy(dhost, s->dstaddr, 6);
+            seterr("Please provide a destination address");
+            return TCPEDIT_ERROR;
         }
     } else {
         seterr("Encoders only support C2S or C2S!");
@@ -1667,7 +1791,7 @@ static int encoder_l2len(const ocfg_t *c, const uint8_t *packet, int pktlen)
 {
     if (c->encoder == ENC_USER)
         return c->user_length;
-    if (c->encoder == ENC_HDLC)
+    if (c->encoder == ENC_HDLC || c->encoder == ENC_PPP) /* pppserial.c:335-343 */
         return pktlen < 4 ? -1 : 4;
     return en10mb_l2len(packet, pktlen);
 }
@@ -1688,6 +1812,8 @@ static int encoder_proto(const ocfg_t *c, const uint8_t *packet, int pktlen)
         return TCPEDIT_ERROR;
     if (c->encoder == ENC_HDLC)
         return pktlen < 4 ? TCPEDIT_ERROR : ld16(packet + 2);
+    if (c->encoder == ENC_PPP) /* pppserial.c:257-281 */
+        return pktlen < 4 ? TCPEDIT_ERROR : ntohs(ld16(packet + 2)) == 0x0021 ? ETHERTYPE_IP : TCPEDIT_SOFT_ERROR;
     return en10mb_proto(packet, pktlen);
 }
 
@@ -1862,20 +1988,24 @@ static int oracle_tcpedit_packet(const ocfg_t *c, ostate_t *s, ohdr_t *h, uint8_
 again: /* :89 -- a fuzzed packet goes through L2 and the per-family edits once more */
     ip = ip6 = NULL;
     retval = 0;
-    if ((l2proto = en10mb_proto(packet, (int)h->caplen)) < 0) /* :96 */
+    if ((l2proto = decoder_proto(c, packet, (int)h->caplen)) < 0) /* :96 */
         return TCPEDIT_SOFT_ERROR;
 
     /* tcpedit_dlt_process: dlt_plugins.c:210-238 */
     if (direction == DIR_NOSEND) {
         pktlen = (int)h->caplen;
     } else {
-        int rc = en10mb_decode(s, packet, (int)h->caplen);
+        int rc = decoder_decode(c, s, packet, (int)h->caplen);
         if (rc == TCPEDIT_ERROR)
             return TCPEDIT_SOFT_ERROR;
         if (c->encoder == ENC_USER)
             pktlen = user_encode(c, s, packet, (int)h->caplen, direction);
         else if (c->encoder == ENC_HDLC)
             pktlen = hdlc_encode(c, s, packet, (int)h->caplen);
+        else if (c->encoder == ENC_NOENC) /* linuxsll.c:201-208 and the like */
+            pktlen = TCPEDIT_ERROR;
+        else if (c->encoder == ENC_PPP) /* pppserial.c:239-251 */
+            pktlen = h->caplen < 4 ? TCPEDIT_ERROR : (int)h->caplen;
         else
             pktlen = en10mb_encode(c, s, packet, (int)h->caplen, direction);
         if (pktlen < 0)
@@ -2445,7 +2575,10 @@ done:
 static int oracle_post_args(ocfg_t *c, const oopts_t *o)
 {
     uint32_t seed = 1, rand_num = 0;
+    const int decoder = c->decoder, in_dlt = c->in_dlt; /* set from the input DLT */
     memset(c, 0, sizeof(*c));
+    c->decoder = decoder;
+    c->in_dlt = in_dlt;
     c->mtu = DEFAULT_MTU; /* tcpedit.c:382-390 */
     c->tos = -1;
     c->tclass = -1;
@@ -2581,26 +2714,40 @@ static int oracle_post_args(ocfg_t *c, const oopts_t *o)
         }
     }
     /* tcpedit_dlt_post_args: dlt_plugins.c:168-204 -- the encoder by name */
-    c->encoder = ENC_EN10MB;
-    c->out_linktype = 1; /* DLT_EN10MB */
-    c->user_length = -1;
-    c->hdlc_address = c->hdlc_control = 65535;
-    if (o->have[O_DLT]) {
-        if (strcmp(o->arg[O_DLT], "user") == 0) {
-            c->encoder = ENC_USER;
-        } else if (strcmp(o->arg[O_DLT], "hdlc") == 0) {
-            c->encoder = ENC_HDLC;
-            c->out_linktype = 104; /* DLT_C_HDLC */
-        } else if (strcmp(o->arg[O_DLT], "en10mb") != 0) {
-            seterr("--dlt=%s is out of the oracle's scope (en10mb, user, hdlc)", o->arg[O_DLT]);
-            return -1;
+    /* the decoder's own plugin unless --dlt names another (plugin->name: en10mb.c:61,
+       linuxsll.c:63, linuxsll2.c:66, raw.c:63, null.c:80, loop.c:69, pppserial.c:71,
+       hdlc.c:62, user.c:62) */
+    {
+        static const struct {
+            const char *name;
+            int enc, dlt;
+        } plugins[] = {{"enet", ENC_EN10MB, 1},      {"user", ENC_USER, 147},    {"hdlc", ENC_HDLC, 104},
+                       {"linuxsll", ENC_NOENC, 113}, {"linuxsll2", ENC_NOENC, 276}, {"raw", ENC_NOENC, 12},
+                       {"null", ENC_NOENC, 0},       {"loop", ENC_NOENC, 108},   {"pppserial", ENC_PPP, 50}};
+        static const int dec_enc[] = {[DEC_EN10MB] = ENC_EN10MB, [DEC_SLL] = ENC_NOENC, [DEC_SLL2] = ENC_NOENC,
+                                      [DEC_RAW] = ENC_NOENC,     [DEC_NULL] = ENC_NOENC, [DEC_PPP] = ENC_PPP,
+                                      [DEC_CHDLC] = ENC_HDLC};
+        c->encoder = dec_enc[c->decoder];
+        c->out_linktype = c->in_dlt;
+        if (o->have[O_DLT]) {
+            int k = 0, n = (int)(sizeof(plugins) / sizeof(plugins[0]));
+            while (k < n && strcmp(plugins[k].name, o->arg[O_DLT]) != 0)
+                k++;
+            if (k == n) {
+                seterr("No output DLT plugin available for: %s", o->arg[O_DLT]);
+                return -1;
+            }
+            c->encoder = plugins[k].enc;
+            c->out_linktype = plugins[k].dlt;
         }
     }
+    c->user_length = -1;
+    c->hdlc_address = c->hdlc_control = 65535;
     /* dlt_user_parse_opts: user.c:158-205 (--user-dlt, else the decoder's DLT) */
     if (o->have[O_USER_DLT])
         c->user_dlt_set = 1, c->user_dlt = (int)opt_num(o, O_USER_DLT);
     if (c->encoder == ENC_USER)
-        c->out_linktype = c->user_dlt_set ? c->user_dlt : 1;
+        c->out_linktype = c->user_dlt_set ? c->user_dlt : c->in_dlt;
     if (o->have[O_USER_DLINK]) {
         for (int k = 0; k < o->nstack[O_USER_DLINK]; k++) {
             uint8_t *dst = k == 0 ? c->user_l2server : c->user_l2client;
@@ -2796,6 +2943,33 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
     g_warn_count = 0;
     *out_len = 0;
 
+    {   /* the input DLT first: the encoder defaults to the decoder's plugin */
+        uint32_t m = 0, lt = 0;
+        if (in_len >= 24) {
+            memcpy(&m, in, 4);
+            memcpy(&lt, in + 20, 4);
+            if (m == 0xd4c3b2a1u || m == 0x4d3cb2a1u)
+                lt = bswap32_(lt);
+        }
+        lt &= 0x03ffffff;
+        if (lt == 101) /* LINKTYPE_RAW: libpcap's linktype_to_dlt gives DLT_RAW */
+            lt = 12;
+        static const struct {
+            uint32_t dlt;
+            int dec;
+        } decs[] = {{1, DEC_EN10MB}, {113, DEC_SLL}, {276, DEC_SLL2}, {12, DEC_RAW},  {0, DEC_NULL},
+                    {108, DEC_NULL}, {50, DEC_PPP},  {104, DEC_CHDLC}};
+        int k = 0;
+        while (k < 8 && decs[k].dlt != lt)
+            k++;
+        if (in_len >= 24 && k == 8) {
+            seterr("No DLT plugin available for source DLT: 0x%x (in the oracle's scope)", lt);
+            rc = -2;
+            goto out;
+        }
+        c.decoder = k < 8 ? decs[k].dec : DEC_EN10MB;
+        c.in_dlt = k < 8 ? (int)lt : 1;
+    }
     if (parse_argv(o, argc, argv) < 0 || oracle_post_args(&c, o) < 0) {
         rc = -2;
         goto out;
@@ -2830,22 +3004,15 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
         rc = -2;
         goto out;
     }
-    uint32_t linktype;
-    memcpy(&linktype, in + 20, 4);
-    if (swap)
-        linktype = bswap32_(linktype);
-    if ((linktype & 0x03ffffff) != DLT_EN10MB) {
-        seterr("only DLT_EN10MB input is in the oracle's scope");
-        rc = -2;
-        goto out;
-    }
     /* pcap_open_dead(out_dlt, 65535) + pcap_dump_open header (tcprewrite.c:124,147) */
     if (out_cap < 24) {
         rc = -2;
         goto out;
     }
     {
-        uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, (uint32_t)c.out_linktype};
+        /* pcap_dump_open writes dlt_to_linktype(dlt): DLT_RAW (12) is LINKTYPE_RAW (101) */
+        const uint32_t olt = c.out_linktype == 12 ? 101u : (uint32_t)c.out_linktype;
+        uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 65535, olt};
         memcpy(out, hdr, 24);
         op = 24;
     }

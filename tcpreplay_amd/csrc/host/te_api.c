@@ -94,6 +94,10 @@ struct tcpedit_batch_s {
     uint8_t *d_ws;           /* err[0..2] | ticket, done | counters | tile_state[] | list count */
     uint32_t *d_tile_list;   /* fast lane: tiles left to the generic kernel */
     uint32_t last_cnt_off;   /* workspace offset of the last launch's counter set */
+    uint64_t *d_l2carry;     /* 2 x (l2carry_cap + 1) scan results, then keys */
+    uint64_t l2carry_cap;
+    void *d_l2tmp;           /* ... and the scan's scratch */
+    size_t l2tmp_bytes;
     uint32_t *d_fuzz;        /* --fuzz-seed: per-record RNG states, then a word per 1024 records */
     uint64_t fuzz_cap;       /* records d_fuzz has room for */
     int fuzz_probe_only;     /* the next launch only counts records reaching the fuzz step */
@@ -121,10 +125,14 @@ struct tcpedit_batch_s {
 /* no edit step can change a record's length or drop it: efcs, VLAN add/del,
  * fixlen, MTU truncation and skipped soft errors are the only ways (plus
  * zero-length records, checked per batch) */
+/* libpcap's linktype_to_dlt for the link types this build decodes: LINKTYPE_RAW (101)
+ * is DLT_RAW (12); the others are their DLT values */
+static uint32_t te_linktype_dlt(uint32_t lt) { return lt == 101 ? 12u : lt; }
+
 static int static_capable(const te_dev_cfg_t *c)
 {
     return !c->efcs && c->vlan == TE_VLAN_OFF && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate &&
-           !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB && !c->fuzz_seed;
+           !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && !c->fuzz_seed;
 }
 
 /* options the register-resident fast lane carries (fast_lane.hpp): the MAC, port,
@@ -138,10 +146,18 @@ static int fast_capable(const te_dev_cfg_t *c)
 
 /* the most a record's L2 header can grow: a VLAN push (4 bytes) or a user header longer
    than Ethernet's 14 (device: at most TE_HEAD, more is flagged unsupported) */
+static int l2_growth(const te_dev_cfg_t *c)
+{
+    const int dl = te_decoder_l2len(c->decoder);
+    return c->encoder == TE_ENC_USER                                     ? c->user_length - dl
+           : c->encoder == TE_ENC_HDLC                                   ? 4 - dl
+           : c->encoder == TE_ENC_EN10MB && c->decoder != TE_DEC_EN10MB ? 14 - dl /* another DLT -> Ethernet */
+                                                                         : 0;
+}
 static uint32_t rec_growth(const te_dev_cfg_t *c)
 {
-    const int user = c->encoder == TE_ENC_USER ? c->user_length - 14 : 0;
-    const uint32_t g = user > 4 ? (uint32_t)user : 4u;
+    const int l2 = l2_growth(c);
+    const uint32_t g = l2 > 4 ? (uint32_t)l2 : 4u;
     return c->fuzz_seed ? 2 * g : g; /* a fuzzed record is encoded twice (tcpedit.c:250-258) */
 }
 
@@ -149,7 +165,8 @@ static uint32_t rec_growth(const te_dev_cfg_t *c)
  * fast-lane conditions, and a tag to push (an untagged frame without one is an error) */
 static int fast_capable_grow(const te_dev_cfg_t *c)
 {
-    return c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && c->vlan_tag < 65535 && !c->efcs &&
+    return c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && c->vlan == TE_VLAN_ADD &&
+           c->vlan_tag < 65535 && !c->efcs &&
            !c->fuzz_seed && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate && !c->skip_soft_errors &&
            !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
 }
@@ -159,8 +176,8 @@ static int fast_capable_grow(const te_dev_cfg_t *c)
  * the static placement and the batch is placed by scan instead).  Returns the TE_SZ_ kind. */
 static int static_shrink_kind(const te_dev_cfg_t *c)
 {
-    if (c->encoder != TE_ENC_EN10MB || c->vlan == TE_VLAN_ADD || c->fixlen != TE_FIXLEN_OFF || c->mtu_truncate ||
-        c->skip_soft_errors || c->fuzz_seed)
+    if (c->encoder != TE_ENC_EN10MB || c->decoder != TE_DEC_EN10MB || c->vlan == TE_VLAN_ADD ||
+        c->fixlen != TE_FIXLEN_OFF || c->mtu_truncate || c->skip_soft_errors || c->fuzz_seed)
         return TE_SZ_NONE;
     if (c->efcs && c->vlan == TE_VLAN_OFF)
         return TE_SZ_EFCS;
@@ -479,7 +496,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         te_seterr(t, "not a pcap file (magic 0x%08x)", magic);
         return -1;
     }
-    b->linktype = rd32(hdr + 20, b->swapped) & 0x03ffffffu;
+    b->linktype = te_linktype_dlt(rd32(hdr + 20, b->swapped) & 0x03ffffffu);
     te_walk_t proto;
     memset(&proto, 0, sizeof(proto));
     proto.img = img;
@@ -488,7 +505,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     proto.pad = t->cfg.fixlen == TE_FIXLEN_PAD;
     /* slots with headroom: VLAN push, fixlen pad, a user L2 header longer than Ethernet's */
     proto.slot_mode = proto.pad || (t->cfg.encoder == TE_ENC_EN10MB && t->cfg.vlan == TE_VLAN_ADD) ||
-                      (t->cfg.encoder == TE_ENC_USER && t->cfg.user_length > 14);
+                      l2_growth(&t->cfg) > 0;
     b->slot_layout = proto.slot_mode;
     /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
        are cut to the wave image (their per-record slots then fit the generic kernel's) */
@@ -712,6 +729,12 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_ws);
     hipFree(b->d_tile_list);
     hipFree(b->d_fuzz);
+    hipFree(b->d_l2carry);
+    hipFree(b->d_l2tmp);
+    b->d_l2carry = NULL;
+    b->d_l2tmp = NULL;
+    b->l2carry_cap = 0;
+    b->l2tmp_bytes = 0;
     hipFree(b->d_q8);
     hipFree(b->d_q8_init);
     b->d_q8 = b->d_q8_init = NULL;
@@ -816,6 +839,15 @@ int te_upload_cfg(tcpedit_t *t)
     if (t->cfg.fuzz_seed && t->fz_seeded &&
         t->fz_gen != __atomic_load_n(&te_fuzz_init_gen, __ATOMIC_SEQ_CST))
         t->dev_dirty = 1; /* a fuzzing_init since the last upload re-seeds the state */
+    {   /* the dst_modified carry, whatever set the config (post_args or setters) */
+        const te_dev_cfg_t *c = &t->cfg;
+        const uint32_t l2c = (c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2) && c->encoder == TE_ENC_EN10MB &&
+                             !(c->mac_mask & TE_MASK_DMAC1);
+        if (l2c != c->l2carry) {
+            t->cfg.l2carry = l2c;
+            t->dev_dirty = 1;
+        }
+    }
     if (!t->dev_dirty && t->d_cfg)
         return 0;
     if (!t->d_cfg)
@@ -899,6 +931,8 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * (size_t)b->q8_cap));
     if (cache) {
         const uint8_t *cd;
+        if (te_check_decoder_cfg(t, 1) < 0)
+            goto fail;
         if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &b->dirbits_len) < 0)
             goto fail;
         HIPCHK(t, hipMalloc((void **)&b->d_dirbits, b->dirbits_len + 16));
@@ -930,6 +964,43 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
 static int launch(tcpedit_batch_t *b, int fixed_dir)
 {
     return launch_ev(b, fixed_dir, NULL, NULL, 0);
+}
+
+/* the dst_modified carry's buffers for a launch over b (the context's word,
+ * zeroed when first allocated: the reference's zeroed en10mb extra) */
+static int l2carry_bufs(tcpedit_t *t, tcpedit_batch_t *b, te_launch_t *L)
+{
+    if (b->n_pkts >= 0xffffffffull)
+        return -1;
+    if (!t->d_l2word) {
+        if (hipMalloc((void **)&t->d_l2word, sizeof(uint32_t)) != hipSuccess ||
+            hipMemsetAsync(t->d_l2word, 0, sizeof(uint32_t), t->stream) != hipSuccess) {
+            t->d_l2word = NULL;
+            te_seterr(t, "out of device memory (dst_modified carry)");
+            return -1;
+        }
+    }
+    if (b->l2carry_cap < b->n_pkts) {
+        hipFree(b->d_l2carry);
+        hipFree(b->d_l2tmp);
+        b->d_l2carry = NULL;
+        b->d_l2tmp = NULL;
+        b->l2carry_cap = 0;
+        b->l2tmp_bytes = te_l2carry_temp_bytes((uint32_t)b->n_pkts);
+        if (!b->l2tmp_bytes || hipMalloc((void **)&b->d_l2carry, 16 * (b->n_pkts + 1)) != hipSuccess ||
+            hipMalloc(&b->d_l2tmp, b->l2tmp_bytes) != hipSuccess) {
+            te_seterr(t, "out of device memory (dst_modified carry)");
+            return -1;
+        }
+        b->l2carry_cap = b->n_pkts;
+    }
+    L->n_pkts = (uint32_t)b->n_pkts;
+    L->l2carry = b->d_l2carry;
+    L->l2carry_keys = b->d_l2carry + b->l2carry_cap + 1;
+    L->l2carry_word = t->d_l2word;
+    L->l2carry_tmp = b->d_l2tmp;
+    L->l2carry_tmp_bytes = b->l2tmp_bytes;
+    return 0;
 }
 
 /* generic_only: the generic pass over what the last (wave-lane) launch listed, under
@@ -1035,6 +1106,9 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.n_pkts = (uint32_t)b->n_pkts;
         L.fuzz_probe_only = b->fuzz_probe_only;
     }
+    if (c->l2carry && !L.fast && b->n_pkts && l2carry_bufs(t, b, &L) < 0)
+        return -1;
+    L.any_dec = c->decoder != TE_DEC_EN10MB || c->encoder == TE_ENC_NOENC || c->encoder == TE_ENC_PPP;
     const int rc = te_launch_edit(&L, t->stream);
     if (!generic_only) {
         b->last_skipped = L.skip_generic;
@@ -1050,7 +1124,8 @@ static void out_header(const tcpedit_t *t, uint8_t *h)
     static const uint8_t base[24] = {0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                      0xff, 0xff, 0, 0, 1, 0, 0, 0};
     memcpy(h, base, 24);
-    const uint32_t lt = (uint32_t)t->cfg.out_linktype;
+    /* pcap_dump_open writes dlt_to_linktype(dlt): DLT_RAW (12) is LINKTYPE_RAW (101) */
+    const uint32_t lt = t->cfg.out_linktype == 12 ? 101u : (uint32_t)t->cfg.out_linktype;
     memcpy(h + 20, &lt, 4);
 }
 
@@ -1096,6 +1171,8 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
     L.q8_init_len = init_len;
     if (t->cfg.fuzz_seed && b->d_fuzz && !b->last_fast)
         L.fuzz_states = b->d_fuzz;
+    if (t->cfg.l2carry && !b->last_fast)
+        L.l2carry = b->d_l2carry; /* the last launch's scan: each replayed record's carried value */
     if (te_launch_q8(&L, st) != 0) {
         te_seterr(t, "stale-buffer replay launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -1;
@@ -1941,7 +2018,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             te_seterr(t, "not a pcap file (magic 0x%08x)", magic);
             return TCPEDIT_ERROR;
         }
-        lt = rd32(img + 20, sw) & 0x03ffffffu;
+        lt = te_linktype_dlt(rd32(img + 20, sw) & 0x03ffffffu);
         if (lt != (uint32_t)t->dlt) {
             te_seterr(t, "pcap linktype %u does not match the context DLT %d", lt, t->dlt);
             return TCPEDIT_ERROR;
@@ -1954,6 +2031,8 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     }
     if (cache) {
         const uint8_t *cd;
+        if (te_check_decoder_cfg(t, 1) < 0)
+            return TCPEDIT_ERROR;
         if (cache_data(t, (const uint8_t *)cache, cache_len, &cd, &dirbits_len) < 0)
             return TCPEDIT_ERROR;
         HIPCHK(t, hipMalloc((void **)&d_dirbits, dirbits_len + 16));
@@ -2122,8 +2201,9 @@ int tcpedit_init(tcpedit_t **out, int dlt)
     t->pub.runtime.dlt1 = t->pub.runtime.dlt2 = dlt;
     t->dev_dirty = 1;
     te_sync_pub(t);
-    if (dlt != 1) {
-        te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: DLT_EN10MB)", dlt);
+    if (te_decoder_of(dlt) < 0) {
+        te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: EN10MB, LINUX_SLL, LINUX_SLL2, "
+                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC)", dlt);
         return TCPEDIT_ERROR;
     }
     return TCPEDIT_OK;
@@ -2425,6 +2505,12 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
     uint8_t *img = b->one_img, *res = b->one_img + TE_ONE_IN;
     const size_t img_len = 24 + 16 + (size_t)caplen;
     memcpy(img, fh, 24);
+    {
+        const uint32_t lt = (uint32_t)t->dlt; /* the context's DLT (its decoder) */
+        memcpy(img + 20, &lt, 4);
+    }
+    if (direction == TCPR_DIR_S2C && te_check_decoder_cfg(t, 1) < 0)
+        return TCPEDIT_ERROR;
     const uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
     memcpy(img + 24, rh, 16);
     memcpy(img + 40, *pktdata, caplen);
@@ -2537,6 +2623,7 @@ int tcpedit_close(tcpedit_t **tp)
     hipFree(t->d_cfg);
     hipFree(t->d_portlut);
     hipFree(t->d_fuzz_words);
+    hipFree(t->d_l2word);
     hipFree(t->d_q8_scratch);
     te_pipe_free(t);
     if (t->stream)

@@ -532,6 +532,81 @@ static void pm_sparse(tcpedit_t *t)
     }
 }
 
+/* the decoder plugin of an input DLT (tcpedit_dlt_init, dlt_plugins.c:115-160; the
+ * plugins' dlt_value): -1 when this build has none (JUNIPER_ETHER, IEEE802_11, radiotap) */
+int te_decoder_of(int dlt)
+{
+    switch (dlt) {
+    case 1: return TE_DEC_EN10MB;
+    case 113: return TE_DEC_SLL;   /* DLT_LINUX_SLL */
+    case 276: return TE_DEC_SLL2;  /* DLT_LINUX_SLL2 */
+    case 12: return TE_DEC_RAW;    /* DLT_RAW */
+    case 0:                        /* DLT_NULL */
+    case 108: return TE_DEC_NULL;  /* DLT_LOOP (loop.c: dlt_null's functions) */
+    case 50: return TE_DEC_PPP;    /* DLT_PPP_SERIAL (pppserial.c:41) */
+    case 104: return TE_DEC_CHDLC; /* DLT_C_HDLC */
+    default: return -1;
+    }
+}
+
+/* the decoder's own plugin as the encoder (no --dlt) */
+int te_default_encoder(int dec)
+{
+    switch (dec) {
+    case TE_DEC_EN10MB: return TE_ENC_EN10MB;
+    case TE_DEC_PPP: return TE_ENC_PPP;
+    case TE_DEC_CHDLC: return TE_ENC_HDLC;
+    default: return TE_ENC_NOENC;
+    }
+}
+
+/* the decoded L2 header's length (the encoders replace it): en10mb's varies (14 assumed
+ * for the slot headroom; VLAN/MPLS make it longer, never shorter) */
+int te_decoder_l2len(int dec)
+{
+    switch (dec) {
+    case TE_DEC_SLL: return 16;
+    case TE_DEC_SLL2: return 20;
+    case TE_DEC_RAW: return 0;
+    case TE_DEC_NULL:
+    case TE_DEC_PPP:
+    case TE_DEC_CHDLC: return 4;
+    default: return 14;
+    }
+}
+
+/* the decoder/encoder pairs this build does not serve, refused loudly, and the Q18
+ * carry flag.  s2c: records may be S2C (a tcpprep cache, or tcpedit_packet's caller). */
+int te_check_decoder_cfg(tcpedit_t *t, int s2c)
+{
+    te_dev_cfg_t *c = &t->cfg;
+    const int foreign = c->decoder != TE_DEC_EN10MB;
+    const int eth_addr = c->decoder == TE_DEC_EN10MB || c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2;
+    c->l2carry = (c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2) && c->encoder == TE_ENC_EN10MB &&
+                 !(c->mac_mask & TE_MASK_DMAC1);
+    if (foreign && c->encoder == TE_ENC_EN10MB) {
+        if (c->vlan == TE_VLAN_ADD) {
+            /* en10mb.c:696-715 writes the tag at the never-set vlan_offset 0 of another decoder */
+            te_seterr(t, "--enet-vlan=add on DLT %d input is not served by this build", t->dlt);
+            return -1;
+        }
+        /* en10mb.c:592-659: a decoder without Ethernet addresses needs both MACs, or every
+           packet fails after the encoder's memmove (written half-moved): not served */
+        const int need = TE_MASK_SMAC1 | TE_MASK_DMAC1 | (s2c ? TE_MASK_SMAC2 | TE_MASK_DMAC2 : 0);
+        if (!eth_addr && (c->mac_mask & need) != need) {
+            te_seterr(t, "DLT %d input into --dlt=enet needs --enet-smac and --enet-dmac%s", t->dlt,
+                      s2c ? " for both directions" : "");
+            return -1;
+        }
+    }
+    if (c->fuzz_seed && (foreign || (c->encoder != TE_ENC_EN10MB && c->encoder != TE_ENC_USER &&
+                                     c->encoder != TE_ENC_HDLC))) {
+        te_seterr(t, "--fuzz-seed with DLT %d input or this encoder is not served by this build", t->dlt);
+        return -1;
+    }
+    return 0;
+}
+
 /* tcpedit_init (tcpedit.c:371-403), dlt_en10mb_init (en10mb.c:117-122) and the
  * encoder defaults of tcpedit_dlt_post_args (dlt_plugins.c:178-183: the decoder's) */
 void te_cfg_defaults(te_dev_cfg_t *c, int dlt)
@@ -543,7 +618,8 @@ void te_cfg_defaults(te_dev_cfg_t *c, int dlt)
     c->vlan_pri = 255;
     c->vlan_cfi = 255;
     c->vlan_proto = 0x8100;
-    c->encoder = TE_ENC_EN10MB;
+    c->decoder = te_decoder_of(dlt);
+    c->encoder = te_default_encoder(c->decoder);
     c->out_linktype = dlt;
     c->user_length = -1;
     c->hdlc_address = c->hdlc_control = 65535;
@@ -552,7 +628,18 @@ void te_cfg_defaults(te_dev_cfg_t *c, int dlt)
 
 /* the DLT plugin ids of the encoders this build carries (plugins/dlt_*): the user
  * plugin answers for DLT_USER0 (user.c:40), hdlc for DLT_C_HDLC (hdlc.c:40) */
-static int encoder_dlt(int enc) { return enc == TE_ENC_USER ? 147 : enc == TE_ENC_HDLC ? 104 : 1; }
+static int encoder_dlt(const tcpedit_t *t, int enc)
+{
+    if (enc == TE_ENC_USER)
+        return 147;
+    if (enc == TE_ENC_HDLC)
+        return 104;
+    if (enc == TE_ENC_PPP)
+        return 50;
+    if (enc == TE_ENC_NOENC)
+        return t->cfg.out_linktype; /* the non-encoding plugin named (or the decoder's own) */
+    return 1;
+}
 
 void te_sync_pub(tcpedit_t *t)
 {
@@ -561,7 +648,7 @@ void te_sync_pub(tcpedit_t *t)
     p->dlt_ctx = &t->dltc;
     t->dltc.tcpedit = t;
     t->dltc.decoder_dlt = t->dlt;
-    t->dltc.encoder_dlt = encoder_dlt(c->encoder);
+    t->dltc.encoder_dlt = encoder_dlt(t, c->encoder);
     p->skip_broadcast = c->skip_broadcast != 0;
     p->fixlen = (tcpedit_fixlen)c->fixlen;
     p->editdir = TCPEDIT_EDIT_BOTH;
@@ -763,27 +850,37 @@ int te_derive_cfg(tcpedit_t *t)
     }
 
     /* tcpedit_dlt_post_args (dlt_plugins.c:168-204): encoder = --dlt or decoder */
-    if (t->dlt != 1) {
-        te_seterr(t, "input DLT %d: only DLT_EN10MB (1) is supported by this build", t->dlt);
+    c->decoder = te_decoder_of(t->dlt);
+    if (c->decoder < 0) {
+        te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: EN10MB, LINUX_SLL, LINUX_SLL2, "
+                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC)", t->dlt);
         return -1;
     }
-    if (t->have[OPT_DLT]) { /* tcpedit_dlt_getplugin_byname: the plugins' dlt_prefix names */
-        if (strcmp(t->arg[OPT_DLT], "user") == 0) {
-            c->encoder = TE_ENC_USER;
-        } else if (strcmp(t->arg[OPT_DLT], "hdlc") == 0) {
-            c->encoder = TE_ENC_HDLC;
-            c->out_linktype = 104; /* DLT_C_HDLC */
-        } else if (strcmp(t->arg[OPT_DLT], "enet") != 0) {
-            te_seterr(t, "No output DLT plugin available for: %s (this build: enet, user, hdlc)", t->arg[OPT_DLT]);
+    c->encoder = te_default_encoder(c->decoder);
+    c->out_linktype = t->dlt;
+    if (t->have[OPT_DLT]) { /* tcpedit_dlt_getplugin_byname: the plugins' registered names */
+        static const struct {
+            const char *name;
+            int enc, dlt;
+        } plugins[] = {{"enet", TE_ENC_EN10MB, 1},      {"user", TE_ENC_USER, 147},    {"hdlc", TE_ENC_HDLC, 104},
+                       {"linuxsll", TE_ENC_NOENC, 113}, {"linuxsll2", TE_ENC_NOENC, 276}, {"raw", TE_ENC_NOENC, 12},
+                       {"null", TE_ENC_NOENC, 0},       {"loop", TE_ENC_NOENC, 108},   {"pppserial", TE_ENC_PPP, 50}};
+        size_t k = 0;
+        while (k < sizeof(plugins) / sizeof(plugins[0]) && strcmp(plugins[k].name, t->arg[OPT_DLT]) != 0)
+            k++;
+        if (k == sizeof(plugins) / sizeof(plugins[0])) {
+            te_seterr(t, "No output DLT plugin available for: %s", t->arg[OPT_DLT]);
             return -1;
         }
+        c->encoder = plugins[k].enc;
+        c->out_linktype = plugins[k].dlt;
     }
     { /* dlt_user_parse_opts (user.c:158-205): --user-dlt, else the decoder's DLT */
         long v = 1;
         if (t->have[OPT_USER_DLT] && !num_arg(t, OPT_USER_DLT, 0, 65535, &v))
             return -1;
         if (c->encoder == TE_ENC_USER)
-            c->out_linktype = (int32_t)v;
+            c->out_linktype = t->have[OPT_USER_DLT] ? (int32_t)v : t->dlt;
         for (int k = 0; k < t->nstack[OPT_USER_DLINK]; k++) {
             uint8_t *dst = k == 0 ? c->user_l2server : c->user_l2client;
             const int n = read_hexstring(t->stack[OPT_USER_DLINK][k], dst, 255);
@@ -804,10 +901,12 @@ int te_derive_cfg(tcpedit_t *t)
             return -1;
         }
     }
-    if (c->encoder == TE_ENC_HDLC && (!t->have[OPT_HDLC_ADDRESS] || !t->have[OPT_HDLC_CONTROL])) {
-        /* dlt_hdlc_encode (hdlc.c:270-288) fails every Ethernet-decoded packet without them,
-           after its memmove: the reference writes those soft errors half-moved */
-        te_seterr(t, "--dlt=hdlc needs --hdlc-address and --hdlc-control for Ethernet input");
+    if (c->encoder == TE_ENC_HDLC && (!t->have[OPT_HDLC_ADDRESS] || !t->have[OPT_HDLC_CONTROL]) &&
+        te_decoder_l2len(c->decoder) != 4) {
+        /* dlt_hdlc_encode (hdlc.c:270-288) fails every packet without them (no decoder marks
+           the HDLC extra filled), after its memmove: the reference writes those soft errors
+           half-moved.  A 4-byte decoded header is not moved (its packets fail cleanly). */
+        te_seterr(t, "--dlt=hdlc needs --hdlc-address and --hdlc-control for this input");
         return -1;
     }
     { /* dlt_hdlc_parse_opts (hdlc.c:156-180) */
@@ -916,6 +1015,8 @@ int te_derive_cfg(tcpedit_t *t)
         }
     }
     c->skip_soft_errors = t->have[OPT_SKIP_SOFT_ERRORS] != 0;
+    if (te_check_decoder_cfg(t, 0) < 0)
+        return -1;
     t->post_args_done = 1;
     t->dev_dirty = 1;
     t->fz_seeded = 0; /* fuzzing_init (tcprewrite.c:103) follows post_args */

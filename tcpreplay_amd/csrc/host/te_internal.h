@@ -75,6 +75,7 @@ struct tcpedit_s {
     uint16_t *d_portlut;
     uint32_t *d_fuzz_words;       /* --fuzz-seed: [0] the running RNG state (te_launch_t.fuzz_words) */
     uint8_t *d_q8_scratch;        /* te_q8_replay's emulated static buffers (allocated on first use) */
+    uint32_t *d_l2word;           /* the en10mb encoder's dst_modified after the last launch */
     int dev_dirty;                /* cfg changed since last upload */
     uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */
@@ -92,6 +93,10 @@ int te_derive_cfg(tcpedit_t *t); /* tcpedit_post_args body */
 int te_upload_cfg(tcpedit_t *t);
 int te_ensure_cfg(tcpedit_t *t);  /* derive (or finalize setter values) once before a run */
 void te_cfg_defaults(te_dev_cfg_t *c, int dlt);
+int te_decoder_of(int dlt);
+int te_default_encoder(int dec);
+int te_decoder_l2len(int dec);
+int te_check_decoder_cfg(tcpedit_t *t, int s2c);
 void te_sync_pub(tcpedit_t *t);   /* mirror the derived values into the reference-layout head */
 int te_autoopts_import(tcpedit_t *t); /* 1 imported, 0 no descriptor, -1 error (te_autoopts.c) */
 extern uint64_t te_fuzz_init_gen; /* fuzzing_init calls so far, and their values */

@@ -32,7 +32,12 @@ typedef struct {
 enum { TE_TTL_OFF = 0, TE_TTL_SET, TE_TTL_ADD, TE_TTL_SUB };       /* tcpedit_types.h:38-43 */
 enum { TE_FIXLEN_OFF = 0, TE_FIXLEN_PAD, TE_FIXLEN_TRUNC, TE_FIXLEN_DEL };
 enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };
-enum { TE_ENC_EN10MB = 0, TE_ENC_USER, TE_ENC_HDLC };
+/* encoders: en10mb, user, hdlc; NOENC = linuxsll/linuxsll2/raw/null/loop, whose encode
+   always fails (linuxsll.c:201-208, ...); PPP = pppserial, whose encode is a no-op
+   (pppserial.c:239-251) */
+enum { TE_ENC_EN10MB = 0, TE_ENC_USER, TE_ENC_HDLC, TE_ENC_NOENC, TE_ENC_PPP };
+/* decoders (tcpedit_dlt_init by the input DLT; NULL and LOOP share dlt_null's functions) */
+enum { TE_DEC_EN10MB = 0, TE_DEC_SLL, TE_DEC_SLL2, TE_DEC_RAW, TE_DEC_NULL, TE_DEC_PPP, TE_DEC_CHDLC };
 enum { TE_FUZZ_OFF = 0, TE_FUZZ_PROBE, TE_FUZZ_APPLY }; /* the generic kernel's fuzz passes */
 #define TE_USER_L2MAX 256 /* USER_L2MAXLEN (255, user_types.h:37), rounded */                  /* en10mb_types.h:50-54 */
 enum { TE_MASK_SMAC1 = 1, TE_MASK_SMAC2 = 2, TE_MASK_DMAC1 = 4, TE_MASK_DMAC2 = 8 };
@@ -83,6 +88,11 @@ typedef struct {
     uint8_t user_l2server[TE_USER_L2MAX];
     /* --fuzz-seed (fuzzing.c:12-20): the mixed seed (0 = off) and --fuzz-factor */
     uint32_t fuzz_seed, fuzz_factor;
+    /* the decoder (TE_DEC_*) and whether the launch hands each record the en10mb encoder's
+       dst_modified carried from the last C2S record (a Linux cooked decoder
+       into the en10mb encoder without --enet-dmac; te_l2carry_mark + a max scan) */
+    int32_t decoder;
+    uint32_t l2carry;
 } te_dev_cfg_t;
 
 /* Per-packet status byte written by the device (one per input record). */

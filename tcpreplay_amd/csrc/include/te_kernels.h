@@ -143,7 +143,19 @@ typedef struct {
     int q8_file_start;        /* the launch's first record is the capture's first (buffer starts zeroed) */
     const uint8_t *q8_init;   /* device: the initial buffer instead of zeros (tcpedit_packet), or NULL */
     uint32_t q8_init_len;
+    /* SURVEY Q18 (a Linux cooked decoder into the en10mb encoder without --enet-dmac): the
+       dst_modified carry.  NULL: none (every record's value is its own or false) */
+    uint64_t *l2carry;        /* device: n_pkts + 1 scan results */
+    uint64_t *l2carry_keys;   /* device: n_pkts + 1 keys */
+    uint32_t *l2carry_word;   /* device: the context's value after its last launch */
+    void *l2carry_tmp;        /* device: te_l2carry_temp_bytes(n_pkts) of scan scratch */
+    size_t l2carry_tmp_bytes;
+    int any_dec;              /* a non-Ethernet decoder or a non-encoding / pppserial encoder: the
+                                 generic kernel's instance that carries them */
 } te_launch_t;
+
+/* scan scratch the dst_modified carry needs for a launch of n_pkts records */
+size_t te_l2carry_temp_bytes(uint32_t n_pkts);
 
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */
 int te_fast_grid(void);

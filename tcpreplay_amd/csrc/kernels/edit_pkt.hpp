@@ -63,6 +63,7 @@ struct Pkt {
     u32 ext;      // bytes from d the reference's buffer holds for this packet (its memcpy, the
                   // encoder's memmove, --fixlen=pad, fuzz writes): te_q8_replay's buffer view
     bool strict;  // te_q8_replay: a fuzz XOR of a byte past `phys` is a stale read too
+    u8 l2carry = 0;  // the en10mb encoder's dst_modified as the last C2S record left it (Q18)
 };
 
 // a read of bytes [.., end) from d that lie past the packet's physical bytes: the
@@ -97,6 +98,7 @@ struct Dec {  // tcpeditdlt_t + en10mb_extra_t fields the encode/merge steps rea
     int vlan;
     u32 vlan_offset;
     u16 vlan_tag, vlan_pri, vlan_cfi, vlan_proto;
+    bool dst_modified;   // en10mb_extra_t.dst_modified (read by the multicast MAC update)
 };
 
 // ---------------------------------------------------------------------------
@@ -914,6 +916,172 @@ DI int en10mb_decode(const u8 *pkt, int pktlen, Dec &s) {
     return RC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The other decoders (src/tcpedit/plugins/dlt_*): plugin_proto and plugin_decode.
+// ---------------------------------------------------------------------------
+constexpr int RC_PROTO_SOFT = -2;  // TCPEDIT_SOFT_ERROR from a proto function (pppserial)
+
+// dlt_null_proto (null.c:206-236, DLT_NULL and DLT_LOOP): the address family in either
+// byte order (PF_INET6 is 10 here; the BSDs' 24/28/30 are taken too)
+DI int null_proto(const u8 *p, u32 caplen) {
+    if (caplen < 4) return RC_ERROR;
+    const u32 af = ld32(p), saf = bswap32(af);
+    if (af == 2 || saf == 2) return 0x0008;  // htons(ETHERTYPE_IP)
+    if (af == 10 || saf == 10 || af == 24 || saf == 24 || af == 28 || saf == 28 || af == 30 || saf == 30)
+        return 0xDD86;  // htons(ETHERTYPE_IP6)
+    return RC_ERROR;
+}
+// dlt_raw_proto (raw.c:206-231): the IP version nibble
+DI int raw_proto(const u8 *p, u32 caplen) {
+    if (caplen < 20) return RC_ERROR;
+    return (p[0] >> 4) == 4 ? 0x0008 : (p[0] >> 4) == 6 ? 0xDD86 : RC_ERROR;
+}
+// the decoder's proto (tcpedit_dlt_proto on the source DLT, tcpedit.c:96): the ethertype
+// as the little-endian u16 of its network-order bytes, or < 0
+DI int decoder_proto(const Pkt &pk, const te_dev_cfg_t &cfg) {
+    const u8 *d = pk.d;
+    const u32 n = pk.caplen;
+    switch (cfg.decoder) {
+    case TE_DEC_SLL: return n < 16 ? RC_ERROR : (int)ld16(d + 14);  // linuxsll.c:213-226
+    case TE_DEC_SLL2: return n < 20 ? RC_ERROR : (int)ld16(d);      // linuxsll2.c:226-238
+    case TE_DEC_RAW: return raw_proto(d, n);
+    case TE_DEC_NULL: return null_proto(d, n);
+    // pppserial.c:257-281: the ethertype in host order (0x0800), which tcpedit.c:123,149
+    // never take for IPv4; anything but PPP's IPv4 protocol is a soft error
+    case TE_DEC_PPP: return n < 4 ? RC_ERROR : be16(d + 2) == 0x0021 ? 0x0800 : RC_PROTO_SOFT;
+    case TE_DEC_CHDLC: return n < 4 ? RC_ERROR : (int)ld16(d + 2);  // hdlc.c:299-311
+    default: {  // dlt_en10mb_proto (en10mb.c:741-762)
+        if (n < 14) return RC_ERROR;
+        L2 r;
+        if (get_l2len_protocol(d, n, r) == -1) return RC_ERROR;
+        return bswap16(r.protocol);
+    }
+    }
+}
+// the decoder (plugin_decode) for the non-Ethernet DLTs: l2len, proto and, for the Linux
+// cooked headers, the source address.  None of them sets the en10mb extra fields, which
+// keep the zeroed start of the decoder's (larger) extra buffer (en10mb.c:100-110).
+DI int foreign_decode(const Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
+    const u8 *d = pk.d;
+    const u32 n = pk.caplen;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) s.dstaddr[i] = s.srcaddr[i] = 0;
+    s.proto_vlan_tag = 0;
+    s.l2offset = 0;
+    s.vlan = 0;
+    s.vlan_offset = 0;
+    s.vlan_tag = s.vlan_pri = s.vlan_cfi = s.vlan_proto = 0;
+    switch (cfg.decoder) {
+    case TE_DEC_SLL:     // linuxsll.c:170-194
+    case TE_DEC_SLL2: {  // linuxsll2.c:181-205
+        const bool sll = cfg.decoder == TE_DEC_SLL;
+        const u32 hl = sll ? 16u : 20u;
+        if (n < hl) return RC_ERROR;
+        s.proto = ld16(d + (sll ? 14 : 0));
+        s.l2len = (int)hl;
+        const u16 type = be16(d + (sll ? 2 : 8));
+        if (type != 1 && type != 772) return RC_ERROR;  // ARPHRD_ETHER, ARPHRD_LOOPBACK
+#pragma unroll
+        for (int i = 0; i < 6; ++i) s.srcaddr[i] = d[(sll ? 6 : 12) + i];
+        return RC_OK;
+    }
+    case TE_DEC_RAW: {  // raw.c:170-190
+        if (n == 0) return RC_ERROR;
+        const int p = raw_proto(d, n);
+        if (p < 0) return RC_ERROR;
+        s.proto = p;
+        s.l2len = 0;
+        return RC_OK;
+    }
+    case TE_DEC_NULL: {  // null.c:171-187
+        const int p = null_proto(d, n);
+        if (p < 0) return RC_ERROR;
+        s.proto = p;
+        s.l2len = 4;
+        return RC_OK;
+    }
+    case TE_DEC_PPP:  // pppserial.c:196-231
+        if (n < 4) return RC_ERROR;
+        s.proto = be16(d + 2) == 0x0021 ? 0x0008 : (int)ld16(d + 2);
+        s.l2len = 4;
+        return RC_OK;
+    default:  // TE_DEC_CHDLC, hdlc.c:192-218 (its address/control extras are never marked filled)
+        if (n < 4) return RC_ERROR;
+        s.proto = ld16(d + 2);
+        s.l2len = 4;
+        return RC_OK;
+    }
+}
+
+// subsmac and the MAC seed over the new Ethernet addresses (en10mb.c:662-690)
+DI void en10mb_mac_rules(const te_dev_cfg_t &cfg, u8 *dh, u8 *sh) {
+    for (int e = 0; e < cfg.n_subs; ++e) {
+        const u8 *t = cfg.subs[e], *rw = cfg.subs[e] + 6;
+        bool md = true, ms = true;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            md &= dh[i] == t[i];
+            ms &= sh[i] == t[i];
+        }
+        if (md)
+            for (int i = 0; i < 6; ++i) dh[i] = rw[i];
+        if (ms)
+            for (int i = 0; i < 6; ++i) sh[i] = rw[i];
+    }
+    if (cfg.random_set) {
+        int us = is_unicast_ethernet(sh), ud = is_unicast_ethernet(dh);
+        for (int i = cfg.random_keep; i < 6; ++i) {
+            int ms = cfg.random_mask[i] * us, md = cfg.random_mask[i] * ud;
+            sh[i] = (u8)((sh[i] ^ ms) - (sh[i] & ms));  // MAC_MASK_APPLY (en10mb.h:29-30)
+            dh[i] = (u8)((dh[i] ^ md) - (dh[i] & md));
+        }
+        if (!cfg.random_keep) {
+            sh[0] &= (u8)~(0x01 * us);
+            dh[0] &= (u8)~(0x01 * ud);
+        }
+    }
+}
+
+DI bool l2_replace(Pkt &pk, int l2len, int n);
+
+// dlt_en10mb_encode for another decoder (en10mb.c:544-548 and on): a 14-byte Ethernet
+// header replaces the decoded one (the host refuses VLAN add here, and the configs where
+// an address is missing, which the reference fails after its memmove).  Addresses:
+// the options', else -- the Linux cooked headers' ETHERNET address type -- the decoded
+// source and the context's never-set (zero) destination.  A C2S record without
+// --enet-dmac sets dst_modified (its old first 6 bytes against that zero destination).
+DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int dir) {
+    if (pktlen < 14) return RC_ERROR;
+    if (pktlen + 14 - s.l2len > MAXPACKET) return RC_ERROR;
+    if (pktlen < s.l2len) return RC_ERROR;
+    if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;
+    const bool eth_addr = cfg.decoder == TE_DEC_SLL || cfg.decoder == TE_DEC_SLL2;
+    const bool c2s = dir == TE_DIR_C2S;
+    const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
+    if (!eth_addr && (!(cfg.mac_mask & sm) || !(cfg.mac_mask & dm))) return RC_ERROR;
+    bool old_nz = false;  // memcmp(eth->ether_dhost, ctx->dstaddr (zero), 6) before the writes
+#pragma unroll
+    for (int i = 0; i < 6; ++i) old_nz |= pk.d[i] != 0;
+    if (!l2_replace(pk, s.l2len, 14)) return RC_ERROR;
+    pktlen += 14 - s.l2len;
+    u8 *dh = pk.d, *sh = pk.d + 6;
+    const bool l2skip = cfg.l2_skip_broadcast;
+    const u8 *smac = c2s ? cfg.intf1_smac : cfg.intf2_smac;
+    const u8 *dmac = c2s ? cfg.intf1_dmac : cfg.intf2_dmac;
+    const bool use_s = (cfg.mac_mask & sm) && (!eth_addr || !l2skip || is_unicast_ethernet(s.srcaddr));
+    const bool use_d = (cfg.mac_mask & dm) && (!eth_addr || !l2skip || is_unicast_ethernet(s.dstaddr));
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        sh[i] = use_s ? smac[i] : s.srcaddr[i];
+        dh[i] = use_d ? dmac[i] : s.dstaddr[i];
+    }
+    if (c2s && !(cfg.mac_mask & dm)) s.dst_modified = old_nz;
+    en10mb_mac_rules(cfg, dh, sh);
+    st16(pk.d + 12, (u16)s.proto);
+    if (cfg.vlan == TE_VLAN_DEL) st16(pk.d + 12, 0);  // htons(extra->vlan_proto), never set
+    return pktlen;
+}
+
 // Returns the new packet length (or RC_ERROR).  May move the packet start
 // (pk.d) by -4 (VLAN push) / +4 (VLAN pop) together with its record header.
 DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int dir) {
@@ -977,31 +1145,7 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
     } else {
         return RC_ERROR;
     }
-    for (int e = 0; e < cfg.n_subs; ++e) {
-        const u8 *t = cfg.subs[e], *rw = cfg.subs[e] + 6;
-        bool md = true, ms = true;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            md &= dh[i] == t[i];
-            ms &= sh[i] == t[i];
-        }
-        if (md)
-            for (int i = 0; i < 6; ++i) dh[i] = rw[i];
-        if (ms)
-            for (int i = 0; i < 6; ++i) sh[i] = rw[i];
-    }
-    if (cfg.random_set) {
-        int us = is_unicast_ethernet(sh), ud = is_unicast_ethernet(dh);
-        for (int i = cfg.random_keep; i < 6; ++i) {
-            int ms = cfg.random_mask[i] * us, md = cfg.random_mask[i] * ud;
-            sh[i] = (u8)((sh[i] ^ ms) - (sh[i] & ms));  // MAC_MASK_APPLY (en10mb.h:29-30)
-            dh[i] = (u8)((dh[i] ^ md) - (dh[i] & md));
-        }
-        if (!cfg.random_keep) {
-            sh[0] &= (u8)~(0x01 * us);
-            dh[0] &= (u8)~(0x01 * ud);
-        }
-    }
+    en10mb_mac_rules(cfg, dh, sh);
     if (newl2 == 14) st16(eth + 12, (u16)s.proto);
     if (cfg.vlan == TE_VLAN_ADD || (cfg.vlan == TE_VLAN_OFF && s.vlan)) {
         u8 *vh = pk.d + s.vlan_offset;  // {tci, tpid}
@@ -1062,27 +1206,31 @@ DI int user_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen, i
     return pktlen + n - s.l2len;
 }
 
-// dlt_hdlc_encode (plugins/dlt_hdlc/hdlc.c:223-290): {address, control, protocol}; the
-// host requires --hdlc-address and --hdlc-control (an Ethernet decode has no HDLC
-// fields to fall back on, so the reference fails every packet without them)
+// dlt_hdlc_encode (plugins/dlt_hdlc/hdlc.c:223-290): {address, control, protocol}; no
+// decoder marks its HDLC extra filled, so without --hdlc-address and --hdlc-control the
+// reference fails every packet (the host refuses that unless the decoded L2 is 4 bytes)
 DI int hdlc_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen) {
     if (pktlen < 4) return RC_ERROR;
     if (!l2_replace(pk, s.l2len, 4)) return RC_ERROR;
+    // no option and no filled HDLC extra: an error (the host refuses it where the
+    // reference's memmove above would have moved the packet first)
+    if (cfg.hdlc_address >= 65535 || cfg.hdlc_control >= 65535) return RC_ERROR;
     pk.d[0] = (u8)cfg.hdlc_address;
     pk.d[1] = (u8)cfg.hdlc_control;
     st16(pk.d + 2, (u16)s.proto);  // hdlc->protocol = ctx->proto
     return pktlen + 4 - s.l2len;
 }
 
-// dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC; the
-// en10mb decoder never sets dst_modified (memcmp of untouched bytes, :614).
+// dlt_en10mb_merge_layer3 (en10mb.c:847-887): multicast destination MAC unless
+// dst_modified (never set behind the en10mb decoder: a memcmp of untouched bytes, :614;
+// behind a Linux cooked decoder, Q18).
 DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) {
     int pktlen = (int)pk.caplen;
     int l2len = en10mb_l2len(pk.d, pktlen);
     if (l2len == -1 || pktlen < l2len) return;
     u8 *dh = pk.d + s.l2offset;
     if (ip) {
-        if (pktlen >= 34) {
+        if (pktlen >= 34 && !s.dst_modified) {
             u32 dst = ld32(ip + 16);
             if (mcast4(dst)) {
                 u32 c = bswap32(dst);
@@ -1091,7 +1239,7 @@ DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) 
             }
         }
     } else if (ip6) {
-        if (pktlen >= 54) {
+        if (pktlen >= 54 && !s.dst_modified) {
             const u8 *a = ip6 + 24;
             if (a[0] == 0xff) {
                 dh[0] = 0x33; dh[1] = 0x33; dh[2] = a[12]; dh[3] = a[13]; dh[4] = a[14]; dh[5] = a[15];
@@ -1103,9 +1251,9 @@ DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) 
 // the encoder's L2 length (plugin_l2len): en10mb's parse (en10mb.c:917-943),
 // user.c:325-342, hdlc.c:355-366
 DI int encoder_l2len(const Pkt &pk, const te_dev_cfg_t &cfg) {
-    return cfg.encoder == TE_ENC_USER   ? cfg.user_length
-           : cfg.encoder == TE_ENC_HDLC ? (pk.caplen < 4 ? -1 : 4)
-                                        : en10mb_l2len(pk.d, (int)pk.caplen);
+    return cfg.encoder == TE_ENC_USER                                   ? cfg.user_length
+           : (cfg.encoder == TE_ENC_HDLC || cfg.encoder == TE_ENC_PPP) ? (pk.caplen < 4 ? -1 : 4)  // pppserial.c:335-343
+                                                                       : en10mb_l2len(pk.d, (int)pk.caplen);
 }
 
 // ---------------------------------------------------------------------------
@@ -1222,7 +1370,10 @@ DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
 // reach pass); TE_FUZZ_APPLY fuzzes with RNG state fz_state there.
 // ---------------------------------------------------------------------------
 constexpr int RC_REACHED = 3;
-template <bool FZ = false>
+// ANYDEC: the instance for the other decoders and encoders (cfg.decoder != EN10MB, or a
+// non-encoding / pppserial encoder); without it those paths are compiled out, so the
+// Ethernet edit keeps its register budget.
+template <bool FZ = false, bool ANYDEC = false>
 DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int dir, bool &warned,
                       u32 fz_mode = TE_FUZZ_OFF, u32 fz_state = 0) {
     warned = false;
@@ -1239,24 +1390,34 @@ DI int tcpedit_packet(Pkt &pk, const te_dev_cfg_t &cfg, const u16 *portlut, int 
 again:  // :89 -- after the fuzz step the packet goes through L2 and the L3 edits once more
     ip = ip6 = nullptr;
     retval = 0;
-    // l2proto (:96): dlt_en10mb_proto (en10mb.c:741-762), network-order value
-    {
-        if (pk.caplen < 14) return RC_SOFT;
+    // l2proto (:96): the decoder's proto, network-order value
+    if constexpr (ANYDEC) {
+        l2proto = decoder_proto(pk, cfg);
+    } else {  // dlt_en10mb_proto (en10mb.c:741-762)
         L2 r;
-        if (get_l2len_protocol(pk.d, pk.caplen, r) == -1) return RC_SOFT;
-        l2proto = bswap16(r.protocol);
+        l2proto = pk.caplen < 14 || get_l2len_protocol(pk.d, pk.caplen, r) == -1 ? RC_ERROR : bswap16(r.protocol);
     }
+    if (l2proto < 0) return RC_SOFT;
+    s.dst_modified = pk.l2carry != 0;
     // tcpedit_dlt_process (dlt_plugins.c:210-238)
     int pktlen;
     if (dir == TE_DIR_NOSEND) {
         pktlen = (int)pk.caplen;
         s.l2offset = 0;
     } else {
-        if (en10mb_decode(pk.d, (int)pk.caplen, s) == RC_ERROR) return RC_SOFT;
+        if ((ANYDEC && cfg.decoder != TE_DEC_EN10MB ? foreign_decode(pk, cfg, s)
+                                                    : en10mb_decode(pk.d, (int)pk.caplen, s)) == RC_ERROR)
+            return RC_SOFT;
         if (cfg.encoder == TE_ENC_USER)
             pktlen = user_encode(pk, cfg, s, (int)pk.caplen, dir);
         else if (cfg.encoder == TE_ENC_HDLC)
             pktlen = hdlc_encode(pk, cfg, s, (int)pk.caplen);
+        else if (ANYDEC && cfg.encoder == TE_ENC_NOENC)  // linuxsll.c:201-208 and the like
+            pktlen = RC_ERROR;
+        else if (ANYDEC && cfg.encoder == TE_ENC_PPP)  // pppserial.c:239-251
+            pktlen = pk.caplen < 4 ? RC_ERROR : (int)pk.caplen;
+        else if (ANYDEC && cfg.decoder != TE_DEC_EN10MB)
+            pktlen = en10mb_encode_foreign(pk, cfg, s, (int)pk.caplen, dir);
         else
             pktlen = en10mb_encode(pk, cfg, s, (int)pk.caplen, dir);
         if (pktlen < 0) return RC_SOFT;

@@ -18,6 +18,7 @@
 //      common case) are one contiguous LDS -> HBM copy.
 // Records too large for a tile are edited in an HBM scratch slot instead.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdlib.h>
 #include "edit_pkt.hpp"
@@ -90,6 +91,9 @@ struct LaunchArgs {
     // its physical extent is listed {record, bytes needed, output offset} for te_q8_replay
     uint4 *q8_list;
     uint32_t q8_cap;
+    // per record (launch-relative index), the last C2S record's dst_modified
+    // ((position << 1) | value, 0 = none yet): te_l2carry_mark + an inclusive max scan
+    const unsigned long long *l2carry;
 };
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
@@ -208,7 +212,7 @@ __device__ __forceinline__ uint32_t sel_bytes(uint32_t x, uint32_t y, int b0, in
 // ---------------------------------------------------------------------------
 // tile body.  S = slot buffer (LDS, or HBM scratch for a huge record).
 // ---------------------------------------------------------------------------
-template <int MODE, bool FZ, typename P>
+template <int MODE, bool FZ, typename P, bool AD = false>
 __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t, P S,
                                           TileShared &sh, const te_dev_cfg_t &cfg) {
     const int tid = threadIdx.x;
@@ -331,14 +335,15 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         pk.need = 0;
         pk.ext = caplen;
         pk.strict = false;
+        pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[tile.first_pkt + tid] & 1u) : 0;
         int rc = RC_OK;
         bool warned = false;
         if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
             st |= TE_ST_NOSEND;
         } else {
             const uint32_t fzs = a.fuzz_mode == TE_FUZZ_APPLY ? a.fuzz_state[tile.first_pkt + tid] : 0u;
-            rc = tcpedit_packet<FZ>(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned, a.fuzz_mode,
-                                    fzs);
+            rc = tcpedit_packet<FZ, AD>(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned,
+                                        a.fuzz_mode, fzs);
         }
         if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) st = rc == RC_REACHED ? 1 : 0;
         if (warned) st |= TE_ST_WARNED;
@@ -524,19 +529,20 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
 // address the kernel passes in: the kernarg-pointer builtin is only defined in
 // a kernel entry (a callee gets null), and taking &a in the kernel would copy
 // the arguments to scratch for every tile.
-template <bool FZ>
+template <bool FZ, bool AD>
 __device__ __attribute__((noinline)) void huge_tile(const TE_AS_CONST LaunchArgs *ka, uint32_t t,
                                                     const te_dev_cfg_t &cfg) {
     const LaunchArgs &a = *(const LaunchArgs *)ka;
     __shared__ TileShared hsh;
     const te_tile_t tile = a.tiles[t];
-    tile_body<MODE_SLOT, FZ>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
+    tile_body<MODE_SLOT, FZ, g_u8 *, AD>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
 }
 
 #ifndef TE_MIN_WAVES
 #define TE_MIN_WAVES 3
 #endif
-template <int MODE, bool FZ = false>
+// AD: the instance that also carries the non-Ethernet decoders and encoders (tcpedit_packet)
+template <int MODE, bool FZ = false, bool AD = false>
 __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
@@ -560,9 +566,9 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         if (listed) t = a.tile_list[t];
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
-            tile_body<MODE, FZ>(a, tile, t, slots, sh, cfg);
+            tile_body<MODE, FZ, uint8_t *, AD>(a, tile, t, slots, sh, cfg);
         else
-            huge_tile<FZ>((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
+            huge_tile<FZ, AD>((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
         __syncthreads();
     }
 }
@@ -1813,9 +1819,10 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         pk.need = 0;
         pk.ext = caplen;
         pk.strict = true;
+        pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[j] & 1u) : 0;
         bool warned = false;
         const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
-        const int rc = tcpedit_packet<FZ>(pk, cfg, a.portlut, dir, warned, a.fuzz_mode, fzs);
+        const int rc = tcpedit_packet<FZ, true>(pk, cfg, a.portlut, dir, warned, a.fuzz_mode, fzs);
         if (pk.unsupported) {  // bytes nobody wrote yet in this replay (or slot headroom)
             if (pk.need == NEED_NEVER || pk.need > MAXPACKET) return Q8_FAIL;
             *jd = j;
@@ -2121,6 +2128,84 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.fuzz_state = nullptr;
     a.q8_list = (uint4 *)L->q8_list;
     a.q8_cap = L->q8_cap;
+    a.l2carry = (const unsigned long long *)L->l2carry;
+}
+
+// ===========================================================================
+// a Linux cooked (SLL/SLL2) decoder into the en10mb encoder without
+// --enet-dmac.  Every C2S record that reaches the encoder's address step sets the
+// encoder's dst_modified (its first 6 bytes against the context's zero destination,
+// en10mb.c:612-615); an S2C record leaves it, and the multicast MAC update of every
+// record reads it (en10mb.c:868-882).  So a record sees the value of the last C2S record
+// at or before it: one thread per record writes key[j + 1] = ((j + 1) << 1) | value for a
+// C2S record (0 for the others), key[0] carries the context's value from the previous
+// launch, and an inclusive max scan gives each record its predecessor's (scan[j]); the
+// last entry goes back to the context word for the next launch.
+// ===========================================================================
+__global__ __launch_bounds__(256) void te_l2carry_mark(LaunchArgs a, unsigned long long *key, const uint32_t *word) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) key[0] = *word & 1u;
+    const te_tile_t tile = a.tiles[blockIdx.x];
+    if (threadIdx.x >= tile.npkt) return;
+    const uint32_t j = tile.first_pkt + threadIdx.x;
+    const te_dev_cfg_t &cfg = *a.cfg;
+    const bool swp = a.in_swapped != 0;
+    const uint8_t *rec = a.in + tile.span_off + a.pkt_rel[j];
+    uint32_t caplen = ld_hdr32(rec + 8, swp);
+    const uint32_t len = ld_hdr32(rec + 12, swp);
+    if (cfg.efcs && len > 4 && caplen == len) caplen -= 4;  // tcpedit.c:78-84
+    int dir = TE_DIR_C2S;
+    if (a.fixed_dir >= 0) {
+        dir = a.fixed_dir;
+    } else if (a.dirbits) {
+        const uint64_t pktno = a.pkt_base + j;
+        const uint64_t idx = pktno >> 2;
+        const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+        const uint8_t b = idx < a.dirbits_len ? a.dirbits[idx] : 0;
+        dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+    }
+    const bool sll = cfg.decoder == TE_DEC_SLL;
+    const uint8_t *d = rec + 16;
+    bool writer = dir == TE_DIR_C2S && caplen >= (sll ? 16u : 20u);  // the proto and decode length checks
+    if (writer) {
+        const uint16_t type = (uint16_t)(d[sll ? 2 : 8] << 8 | d[sll ? 3 : 9]);
+        writer = type == 1 || type == 772;  // decode: ARPHRD_ETHER / ARPHRD_LOOPBACK
+    }
+    bool nz = false;
+    if (writer)
+        for (int i = 0; i < 6; ++i) nz |= d[i] != 0;
+    key[j + 1] = writer ? ((unsigned long long)(j + 1) << 1 | (nz ? 1u : 0u)) : 0ull;
+}
+
+__global__ void te_l2carry_save(const unsigned long long *scan, uint32_t n, uint32_t *word) {
+    if (threadIdx.x == 0) *word = (uint32_t)(scan[n] & 1u);
+}
+
+struct MaxU64 {
+    __device__ __forceinline__ unsigned long long operator()(unsigned long long x, unsigned long long y) const {
+        return x > y ? x : y;
+    }
+};
+
+extern "C" size_t te_l2carry_temp_bytes(uint32_t n_pkts) {
+    size_t t = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, t, (const unsigned long long *)nullptr,
+                                          (unsigned long long *)nullptr, MaxU64(), (int)n_pkts + 1) != hipSuccess)
+        return 0;
+    return t;
+}
+
+// the keys and the scan before the edit (the edit then reads L->l2carry)
+static int l2carry_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stream) {
+    if (!L->l2carry) return 0;
+    if (!L->l2carry_keys || !L->l2carry_word || !L->l2carry_tmp || L->n_tiles == 0) return -1;
+    hipLaunchKernelGGL(te_l2carry_mark, dim3(L->n_tiles), dim3(256), 0, stream, a,
+                       (unsigned long long *)L->l2carry_keys, (const uint32_t *)L->l2carry_word);
+    size_t tb = L->l2carry_tmp_bytes;
+    if (hipcub::DeviceScan::InclusiveScan(L->l2carry_tmp, tb, (const unsigned long long *)L->l2carry_keys,
+                                          (unsigned long long *)L->l2carry, MaxU64(), (int)L->n_pkts + 1,
+                                          stream) != hipSuccess)
+        return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" uint64_t te_q8_slot_bytes(void) { return Q8_SLOT; }
@@ -2259,17 +2344,25 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         a.fuzz_mode = TE_FUZZ_APPLY;
         a.fuzz_state = L->fuzz_states;
     }
+    if (!fast && l2carry_prepare(L, a, stream) != 0) return -1;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
     if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
         hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.fuzz_mode != TE_FUZZ_OFF)
         hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (L->any_dec && L->slot_layout)
+        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (L->any_dec)
+        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (L->slot_layout)
         hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
     else
         hipLaunchKernelGGL(te_edit_tiles<MODE_CONTIG>, dim3(grid), dim3(BLOCK), 0, stream, a);
     if (ev && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
+    if (!fast && L->l2carry)  // the last record's value, for the next launch (the Q8 replay reads the array)
+        hipLaunchKernelGGL(te_l2carry_save, dim3(1), dim3(64), 0, stream, (const unsigned long long *)L->l2carry,
+                           L->n_pkts, L->l2carry_word);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
 }

@@ -262,3 +262,58 @@ def build_pcap(recs, linktype=1):
     for ts, tu, cl, ln, data in recs:
         parts.append(np.array([ts, tu, cl, ln], "<u4").tobytes() + bytes(data[:cl]))
     return b"".join(parts)
+
+
+# link types of the non-Ethernet decoders (the pcap header's linktype field)
+LINKTYPES = {"sll": 113, "sll2": 276, "raw": 101, "raw12": 12, "null": 0, "loop": 108, "ppp": 50, "chdlc": 104}
+
+
+def reframe(pcap: bytes, kind: str, seed=1, odd_every=0):
+    """An Ethernet II capture re-framed for another DLT: the 14-byte Ethernet header is
+    replaced by the link's own header (the L3 bytes, timestamps and the caplen/len
+    difference are kept):
+      sll    Linux cooked v1 (16 B): packet type, ARPHRD_ETHER, address length 6, the
+             source MAC (+2 pad), the ethertype
+      sll2   Linux cooked v2 (20 B): ethertype, reserved, ifindex, ARPHRD_ETHER, packet
+             type, address length, source MAC (+2 pad)
+      raw / raw12  no header (linktype 101 / 12)
+      null   the address family in host (little-endian) order: 2 or, for IPv6, one of the
+             four values the reference takes (10, 24, 28, 30)
+      loop   the address family in network order
+      ppp    PPP in HDLC-like framing: ff 03 and the PPP protocol (0x0021 IPv4, 0x0057 IPv6)
+      chdlc  Cisco HDLC: address 0x0f, control 0, the ethertype
+    odd_every=k: every k-th record gets a header the decoder refuses or does not take as
+    IP (SLL: ARPHRD 0x0200; NULL/LOOP: family 7; PPP: protocol 0xc021; RAW: version 5)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i, (ts, tu, cl, ln, d) in enumerate(records(pcap)):
+        if cl < 14:
+            out.append((ts, tu, cl, ln, d))
+            continue
+        et, dmac, smac, l3 = d[12:14], d[0:6], d[6:12], d[14:]
+        v6 = et == b"\x86\xdd"
+        odd = odd_every and i % odd_every == odd_every - 1
+        if kind == "sll":
+            h = bytes([0, int(rng.integers(0, 5))]) + (b"\x02\x00" if odd else
+                                                          (b"\x00\x01" if i % 3 else b"\x03\x04")) + \
+                b"\x00\x06" + smac + b"\x00\x00" + et
+        elif kind == "sll2":
+            h = et + b"\x00\x00" + int(i % 7 + 1).to_bytes(4, "big") + (b"\x02\x00" if odd else b"\x00\x01") + \
+                bytes([int(rng.integers(0, 5)), 6]) + smac + b"\x00\x00"
+        elif kind in ("raw", "raw12"):
+            h = b""
+            if odd:
+                l3 = bytes([0x50 | (l3[0] & 15)]) + l3[1:]
+        elif kind in ("null", "loop"):
+            af = 7 if odd else ([10, 24, 28, 30][i % 4] if v6 else 2)
+            h = af.to_bytes(4, "big" if kind == "loop" else "little")
+        elif kind == "ppp":
+            h = b"\xff\x03" + (b"\xc0\x21" if odd else (b"\x00\x57" if v6 else b"\x00\x21"))
+        elif kind == "chdlc":
+            h = b"\x0f\x00" + et
+        else:
+            raise ValueError(kind)
+        nd = h + l3
+        dl = len(nd) - len(d)
+        out.append((ts, tu, cl + dl, ln + dl, nd))
+    return build_pcap(out, LINKTYPES[kind])

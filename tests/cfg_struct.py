@@ -33,4 +33,5 @@ class DevCfg(ctypes.Structure):
         ("encoder", ctypes.c_int32), ("out_linktype", ctypes.c_int32), ("user_length", ctypes.c_int32),
         ("hdlc_address", ctypes.c_uint32), ("hdlc_control", ctypes.c_uint32),
         ("user_l2client", ctypes.c_uint8 * 256), ("user_l2server", ctypes.c_uint8 * 256),
-        ("fuzz_seed", ctypes.c_uint32), ("fuzz_factor", ctypes.c_uint32)]
+        ("fuzz_seed", ctypes.c_uint32), ("fuzz_factor", ctypes.c_uint32),
+        ("decoder", ctypes.c_int32), ("l2carry", ctypes.c_uint32)]
