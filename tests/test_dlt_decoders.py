@@ -110,7 +110,8 @@ ARGSETS = [
     ["--dlt=enet"] + MACS + ["--fixcsum"],
     ["--dlt=enet"] + MACS + ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353", "--fixcsum"],
     ["--dlt=enet"] + MACS + ["--seed=11", "--ttl=+2", "--efcs"],
-    ["--dlt=enet"] + MACS + ["--enet-vlan=del", "--enet-mac-seed=9", "--fixcsum"],
+    # (--enet-mac-seed cannot be combined with --enet-smac/--enet-dmac: dlt_en10mb.def:62-63)
+    ["--dlt=enet"] + MACS + ["--enet-vlan=del", "--tos=5", "--mtu-trunc", "--mtu=400", "--fixcsum"],
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fixcsum"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
     ["--dlt=pppserial", "--fixcsum"],
