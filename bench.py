@@ -65,19 +65,51 @@ def make_pcap(workload, n, seed):
     return getattr(synth, gen)(n, seed=seed, **kw)
 
 
-def run_workload(workload, n, steps, warmup, seed, device, verify=False):
+STRONG_BLOCK = 1_250_000  # records generated once per rank and repeated (--strong)
+
+
+def make_share(workload, total, rank, world, seed):
+    """--strong: rank's share [rank*total/world, (rank+1)*total/world) of one `total`-record
+    capture, generated on this rank alone so no host holds more than its share: a
+    STRONG_BLOCK-record block of the workload repeated (the record mix and sizes of the
+    config; the endpoints/cache edits vary by global record number through the cache),
+    returned as (file header, records, first global record, records)."""
+    first, last = total * rank // world, total * (rank + 1) // world
+    cnt = last - first
+    blk = min(cnt, STRONG_BLOCK) if cnt else 0
+    block = make_pcap(workload, max(blk, 1), seed + rank)
+    body = block[24:] if blk else b""
+    reps, tail = (cnt // blk, cnt % blk) if blk else (0, 0)
+    parts = [body] * reps
+    if tail:  # the first `tail` records of the block
+        off, k = 24, 0
+        while k < tail:
+            off += 16 + int.from_bytes(block[off + 8:off + 12], "little")
+            k += 1
+        parts.append(block[24:off])
+    return block[:24], b"".join(parts), first, cnt
+
+
+def run_workload(workload, n, steps, warmup, seed, device, verify=False, share=None, total=None):
     import tcpreplay_amd as TA
     from tcpreplay_amd import synth
     args = WORKLOADS[workload][2]
-    pcap = make_pcap(workload, n, seed)
-    cache = synth.tcpprep_cache(n, seed=seed) if workload in CACHED else None
-    te = TA.TcpEdit(args, device=device)
-    b = TA.Batch(te, pcap, cache)
+    if share is not None:  # --strong: this rank's records of the one capture, in place
+        hdr, body, first, n = share
+        cache = synth.tcpprep_cache(total, seed=seed) if workload in CACHED else None
+        te = TA.TcpEdit(args, device=device)
+        b = TA.Batch(te, body, cache, pkt_base=first, hdr=hdr)
+        pcap = None
+    else:
+        pcap = make_pcap(workload, n, seed)
+        cache = synth.tcpprep_cache(n, seed=seed) if workload in CACHED else None
+        te = TA.TcpEdit(args, device=device)
+        b = TA.Batch(te, pcap, cache)
     rc = b.run()  # first (untimed) run: also the correctness check below
     r = b.result()
     if rc != 0 or r.unsupported or r.errors:
         raise RuntimeError(f"{workload}: device run failed rc={rc} ({te.geterr()})")
-    if verify:
+    if verify and pcap is not None:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         rc_o, exp = oracle_lib.rewrite(pcap, args, cache)
@@ -160,7 +192,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
     ap.add_argument("--verify", action="store_true", help="compare the first run with the oracle")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one --records-record capture split over the ranks (each rank "
+                         "generates only its share); c4 defaults to BASELINE configs[3]'s 100M records")
+    ap.add_argument("--records", type=int, default=0, help="--strong: the job's total records "
+                    "(default 100M for c4, else the config's size)")
     opt = ap.parse_args()
+    if opt.strong:  # one big job: the per-config side lines measure other things
+        opt.extra, opt.no_e2e, opt.no_cpu_baseline = "", True, True
+        opt.no_device_index = opt.no_packet_latency = True
 
     import torch
     import torch.distributed as dist
@@ -174,9 +214,18 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    n = opt.packets or DEFAULT_PACKETS[opt.workload]
-    te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank, device=local,
-                                  verify=opt.verify)
+    total = 0
+    if opt.strong:
+        total = opt.records or (100_000_000 if opt.workload == "c4" else DEFAULT_PACKETS[opt.workload])
+        share = make_share(opt.workload, total, rank, world, seed=1)
+        n = share[3]
+        te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1, device=local,
+                                      share=share, total=total)
+        del share
+    else:
+        n = opt.packets or DEFAULT_PACKETS[opt.workload]
+        te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank, device=local,
+                                      verify=opt.verify)
     alg_bytes = r.bytes_in + r.bytes_out  # sum(16+caplen_in) + sum(16+caplen_out) per launch
 
     def barrier():
@@ -216,7 +265,7 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
+    if os.path.exists(tfile) and not opt.strong:  # (profiled at the config's default size)
         try:
             tj = json.load(open(tfile))
             traffic = tj.get(opt.workload, {}).get("hbm_bytes_per_launch")
@@ -231,14 +280,16 @@ def main():
         "warmup": opt.warmup,
         "ms_per_step": round(elapsed / opt.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if opt.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (tcpreplay_amd.synth, seeded per rank)",
-        "config": {"workload": WORKLOADS[opt.workload][3], "packets_per_gpu": n,
+        "config": {"workload": (f"{WORKLOADS[opt.workload][2]} over one {total}-record capture split into "
+                                f"{world} byte-balanced shares (BASELINE configs[3] for c4)")
+                               if opt.strong else WORKLOADS[opt.workload][3], "packets_per_gpu": n,
                    "tcpedit_args": WORKLOADS[opt.workload][2], "parallelism": f"shard{world}",
-                   "global_records": n * world},
-        "gbps_algorithmic": round(alg_bytes * opt.steps * world / elapsed / 1e9, 2),
+                   "global_records": total if opt.strong else n * world},
+        "gbps_algorithmic": round((int(cnt[1].item()) + int(cnt[2].item())) / elapsed / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": TA.FAST_KERNELS.get(r.fast_kind, "te_edit_tiles"),

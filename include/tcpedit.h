@@ -241,9 +241,17 @@ typedef struct {
 
 tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *tcpedit, const void *pcap, size_t len, const void *cache,
                                     size_t cache_len, uint64_t pkt_base);
+/* a shard of a capture where it lies (e.g. the caller's mmap of the file): the file's
+ * 24-byte header and seg_len bytes of whole records, read in place (no host copy), global
+ * record numbers from pkt_base -- the per-rank open of a sharded job (tcprewrite.c:289's
+ * loop over one rank's byte range) */
+tcpedit_batch_t *tcpedit_batch_open_segment(tcpedit_t *tcpedit, const void *hdr, const void *seg, size_t seg_len,
+                                            const void *cache, size_t cache_len, uint64_t pkt_base);
 int tcpedit_batch_run(tcpedit_t *tcpedit, tcpedit_batch_t *b);     /* TCPEDIT_OK / TCPEDIT_ERROR */
 int tcpedit_batch_result(tcpedit_batch_t *b, tcpedit_batch_result_t *r);
 size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap); /* D2H, returns bytes */
+/* D2H of the output records only (no file header): a shard's segment of the job's file */
+size_t tcpedit_batch_output_records(tcpedit_batch_t *b, void *dst, size_t cap);
 const uint8_t *tcpedit_batch_status(tcpedit_batch_t *b);           /* per-record TE_ST_* bytes */
 /* times `iters` back-to-back device runs with hipEvents on the run's stream */
 int tcpedit_batch_time(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run);

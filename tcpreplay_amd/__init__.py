@@ -75,6 +75,8 @@ def load():
         "tcpedit_batch_run": (c_int, [vp, vp]),
         "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),
         "tcpedit_batch_output": (sz, [vp, vp, sz]),
+        "tcpedit_batch_open_segment": (vp, [vp, vp, vp, sz, vp, sz, u64]),
+        "tcpedit_batch_output_records": (sz, [vp, vp, sz]),
         "tcpedit_batch_status": (ctypes.POINTER(ctypes.c_uint8), [vp]),
         "tcpedit_batch_time": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_time_kernels": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double),
@@ -127,10 +129,13 @@ class PinnedBuffer:
 
 
 def _buf(data):
+    """(keep-alive, address, length) of any bytes-like object (bytes, bytearray,
+    memoryview, mmap, numpy array) without copying it; (None, None, 0) for None"""
     if data is None:
-        return None, 0
-    b = ctypes.create_string_buffer(bytes(data), len(data))
-    return b, len(data)
+        return None, None, 0
+    import numpy as np
+    a = np.frombuffer(data, np.uint8)
+    return a, a.ctypes.data, a.size
 
 
 class TcpEdit:
@@ -209,7 +214,7 @@ class TcpEdit:
         if own:
             out = bytearray(max(L.tcpedit_output_bound(self._ctx, inp, n), 24))
         ob = (ctypes.c_char * len(out)).from_buffer(out)
-        cb, cn = _buf(cache)
+        _kc, cb, cn = _buf(cache)
         olen = ctypes.c_size_t(0)
         rc = L.tcpedit_rewrite_pcap_pipelined(self._ctx, inp, n, cb, cn, ob, len(out), ctypes.byref(olen),
                                               int(chunk_bytes))
@@ -235,13 +240,23 @@ class TcpEdit:
 
 
 class Batch:
-    """A pcap image staged in HBM (tcpedit_batch_open)."""
+    """A pcap image staged in HBM (tcpedit_batch_open).  With `hdr` (the file's 24-byte
+    header), `pcap` is a segment of whole records -- e.g. a rank's byte range of an mmap'd
+    capture -- read in place (tcpedit_batch_open_segment).  No host copy is made of
+    either: any bytes-like object is passed by address."""
 
-    def __init__(self, te: TcpEdit, pcap: bytes, cache: bytes = None, pkt_base=0):
+    def __init__(self, te: TcpEdit, pcap, cache=None, pkt_base=0, hdr=None):
         self._te, self._L = te, te._L
-        self._in, n = _buf(pcap)
-        self._cache, cn = _buf(cache)
-        self._b = self._L.tcpedit_batch_open(te._ctx, self._in, n, self._cache, cn, pkt_base)
+        keep, p, n = _buf(pcap)
+        kc, c, cn = _buf(cache)
+        if hdr is None:
+            self._b = self._L.tcpedit_batch_open(te._ctx, p, n, c, cn, pkt_base)
+        else:
+            kh, h, hn = _buf(hdr)
+            if hn < 24:
+                raise ValueError("hdr: the 24-byte pcap file header")
+            self._b = self._L.tcpedit_batch_open_segment(te._ctx, h, p, n, c, cn, pkt_base)
+        del keep, kc  # the library has read and uploaded both
         if not self._b:
             raise RuntimeError(te.geterr())
 
@@ -258,6 +273,15 @@ class Batch:
         out = ctypes.create_string_buffer(max(1, r.out_len))
         n = self._L.tcpedit_batch_output(self._b, out, r.out_len)
         return out.raw[:n]
+
+    def output_records_into(self, dst) -> int:
+        """D2H of the output records (no file header) straight into the writable buffer
+        `dst` (a bytearray, or an mmap of the job's output file at this shard's offset);
+        returns the bytes written"""
+        a, p, n = _buf(dst)
+        if n and not a.flags.writeable:
+            raise ValueError("dst must be writable")
+        return int(self._L.tcpedit_batch_output_records(self._b, p, n))
 
     def status(self):
         import numpy as np

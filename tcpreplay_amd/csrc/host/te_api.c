@@ -882,26 +882,26 @@ fail:
     return -1;
 }
 
-tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, const void *cache, size_t cache_len,
-                                    uint64_t pkt_base)
+/* A batch over the pcap file header `hdr` (24 bytes) and the records `seg` (seg_len
+ * bytes, whole records): a shard of a capture edited where it lies -- e.g. in the
+ * caller's mmap of the file -- with no host copy (the index walk reads it in place, one
+ * H2D copy puts header and records together in HBM).  tcpedit_batch_open is the same
+ * over a whole image. */
+static tcpedit_batch_t *batch_open(tcpedit_t *t, const uint8_t *hdr, const uint8_t *seg, size_t seg_len,
+                                   const void *cache, size_t cache_len, uint64_t pkt_base, uint8_t *ng)
 {
-    if (!t || !pcap)
-        return NULL;
-    if (te_ensure_cfg(t) < 0)
-        return NULL;
+    const size_t len = 24 + seg_len;
     tcpedit_batch_t *b = calloc(1, sizeof(*b));
+    if (!b) {
+        te_seterr(t, "out of host memory");
+        free(ng);
+        return NULL;
+    }
     b->ctx = t;
     b->pkt_base = pkt_base;
-    uint8_t *ng = NULL; /* a pcapng image, as libpcap's reader delivers it (te_pcapng.c) */
-    if (te_is_pcapng((const uint8_t *)pcap, len)) {
-        char e[256];
-        if (te_pcapng_to_pcap((const uint8_t *)pcap, len, &ng, &len, e, sizeof e) < 0) {
-            te_seterr(t, "%s", e);
-            goto fail;
-        }
-        pcap = ng;
-    }
-    if (index_image(t, b, (const uint8_t *)pcap, (const uint8_t *)pcap, len) < 0)
+    /* index_image walks img[24, len): img is positioned so img + 24 is the first record
+       (its first 24 bytes are never read; the header comes from hdr) */
+    if (index_image(t, b, hdr, seg - 24, len) < 0)
         goto fail;
     if (b->linktype != (uint32_t)t->dlt) {
         te_seterr(t, "pcap linktype %u does not match the context DLT %d", b->linktype, t->dlt);
@@ -910,7 +910,9 @@ tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, 
     if (te_upload_cfg(t) < 0)
         goto fail;
     HIPCHK(t, hipMalloc((void **)&b->d_in, len + 64));
-    HIPCHK(t, hipMemcpyAsync(b->d_in, pcap, len, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipMemcpyAsync(b->d_in, hdr, 24, hipMemcpyHostToDevice, t->stream));
+    if (seg_len)
+        HIPCHK(t, hipMemcpyAsync(b->d_in + 24, seg, seg_len, hipMemcpyHostToDevice, t->stream));
     HIPCHK(t, hipMalloc((void **)&b->d_out, b->out_cap + 64));
     HIPCHK(t, hipMalloc((void **)&b->d_status, b->n_pkts + 16));
     if (b->scratch_bytes)
@@ -951,6 +953,43 @@ fail:
     free(ng);
     tcpedit_batch_close(b);
     return NULL;
+}
+
+tcpedit_batch_t *tcpedit_batch_open(tcpedit_t *t, const void *pcap, size_t len, const void *cache, size_t cache_len,
+                                    uint64_t pkt_base)
+{
+    if (!t || !pcap)
+        return NULL;
+    if (te_ensure_cfg(t) < 0)
+        return NULL;
+    uint8_t *ng = NULL; /* a pcapng image, as libpcap's reader delivers it (te_pcapng.c) */
+    if (te_is_pcapng((const uint8_t *)pcap, len)) {
+        char e[256];
+        if (te_pcapng_to_pcap((const uint8_t *)pcap, len, &ng, &len, e, sizeof e) < 0) {
+            te_seterr(t, "%s", e);
+            return NULL;
+        }
+        pcap = ng;
+    }
+    if (len < 24) {
+        te_seterr(t, "pcap image too short");
+        free(ng);
+        return NULL;
+    }
+    return batch_open(t, (const uint8_t *)pcap, (const uint8_t *)pcap + 24, len - 24, cache, cache_len, pkt_base,
+                      ng);
+}
+
+tcpedit_batch_t *tcpedit_batch_open_segment(tcpedit_t *t, const void *hdr, const void *seg, size_t seg_len,
+                                            const void *cache, size_t cache_len, uint64_t pkt_base)
+{
+    if (!t || !hdr || (!seg && seg_len))
+        return NULL;
+    if (te_ensure_cfg(t) < 0)
+        return NULL;
+    static const uint8_t none[1];
+    return batch_open(t, (const uint8_t *)hdr, seg ? (const uint8_t *)seg : none, seg_len, cache, cache_len,
+                      pkt_base, NULL);
 }
 
 /* TCPEDIT_HIP_NO_FAST=1 keeps every packet on the generic lane (A/B checks) */
@@ -1425,6 +1464,17 @@ size_t tcpedit_batch_output(tcpedit_batch_t *b, void *dst, size_t cap)
         return 0;
     size_t n = r.out_len < cap ? r.out_len : cap;
     if (hipMemcpy(dst, b->d_out, n, hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return n;
+}
+
+size_t tcpedit_batch_output_records(tcpedit_batch_t *b, void *dst, size_t cap)
+{
+    tcpedit_batch_result_t r;
+    if (tcpedit_batch_result(b, &r) != TCPEDIT_OK || r.out_len < 24)
+        return 0;
+    size_t n = r.out_len - 24 < cap ? r.out_len - 24 : cap;
+    if (n && hipMemcpy(dst, b->d_out + 24, n, hipMemcpyDeviceToHost) != hipSuccess)
         return 0;
     return n;
 }

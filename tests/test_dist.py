@@ -49,6 +49,23 @@ def oracle_editor_for(pcap, world):
     return editor
 
 
+def oracle_segment_editor(hdr, seg, cache, pkt_base, fuzz_prefix=None):
+    """rewrite_file_distributed's editor contract on the oracle: the shard's records in
+    place behind the file header, global record numbers from pkt_base"""
+    image = bytes(hdr) + bytes(seg)
+    count = D.plan(image, 1).total
+    sub = slice_cache(cache, pkt_base, count) if cache else None
+    skip = 0
+    if fuzz_prefix is not None:
+        O.rewrite(image, args_of_job, sub)
+        skip = fuzz_prefix(O.fuzz_draws())
+    rc, out = O.rewrite_skipping(image, args_of_job, sub, skip)
+    return D.ShardResult(rc, out, [count] + [0] * (len(D.COUNTER_NAMES) - 1))
+
+
+args_of_job = []
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -64,6 +81,44 @@ def _worker(rank, world, port, pcap, args, cache, out_path, use_gpu, q):
         q.put((rank, rc, counters))
     finally:
         dist.destroy_process_group()
+
+
+def _file_worker(rank, world, port, in_path, args, cache_path, out_path, use_gpu, q):
+    import torch.distributed as dist
+    global args_of_job
+    args_of_job = args
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        editor = None if use_gpu else oracle_segment_editor
+        rc, counters, wrote, off = D.rewrite_file_distributed(in_path, args, out_path, cache_path, device=0,
+                                                              editor=editor)
+        q.put((rank, rc, counters, wrote, off))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_file_world(pcap, args, cache=None, world=2, use_gpu=False):
+    """rewrite_file_distributed over files: the plan broadcast from rank 0, each rank's
+    byte range read in place from an mmap, outputs written into mmaps of the output file"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        in_path, out_path = os.path.join(d, "in.pcap"), os.path.join(d, "out.pcap")
+        open(in_path, "wb").write(pcap)
+        cache_path = None
+        if cache is not None:
+            cache_path = os.path.join(d, "in.cache")
+            open(cache_path, "wb").write(cache)
+        procs = [ctx.Process(target=_file_worker, args=(r, world, port, in_path, args, cache_path, out_path,
+                                                        use_gpu, q)) for r in range(world)]
+        for pr in procs:
+            pr.start()
+        for pr in procs:
+            pr.join(300)
+            assert pr.exitcode == 0
+        res = sorted(q.get() for _ in range(world))
+        return open(out_path, "rb").read(), res
 
 
 def run_world(pcap, args, cache=None, world=2, use_gpu=False):
@@ -139,6 +194,41 @@ def test_two_rank_rewrite_equals_single_process(built, case):
     assert res[0][2]["packets"] == res[1][2]["packets"] == D.plan(pcap, 2).total
 
 
+@pytest.mark.parametrize("case,world", [("c4_cache", 2), ("fuzz_golden", 2), ("seed_imix", 3), ("tiny", 4)])
+def test_file_ranks_equal_single_process(built, case, world):
+    """the file-based job: rank 0's plan broadcast, per-rank mmap segments, output
+    written into mmaps of each rank's range; a capture with fewer records than ranks
+    leaves ranks with nothing to write"""
+    if case == "fuzz_golden":
+        pcap, args, cache = G.read("test.pcap"), ["--fuzz-seed=42", "--fuzz-factor=2"], None
+    elif case == "c4_cache":
+        pcap, args, cache = G.read("test.pcap"), C4_ARGS[:1] + ["--enet-vlan=add", "--enet-vlan-tag=45",
+                                                                 "--fixcsum"], G.read("test.auto_router")
+    elif case == "tiny":
+        pcap, args, cache = S.pcap_fixed(2, 64, seed=3), ["--seed=9", "--fixcsum"], None
+    else:
+        pcap, args, cache = S.pcap_imix(7000, seed=4), ["--seed=42", "--fixcsum"], None
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    out, res = run_file_world(pcap, args, cache, world=world)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
+    assert all(r[2]["packets"] == D.plan(pcap, world).total for r in res)
+    assert sum(r[3] for r in res) == len(exp) - 24
+
+
+def test_file_ranks_truncate_at_first_failing_record(built):
+    recs = S.records(S.pcap_fixed(40, 64, seed=5))
+    ts, tu, cl, ln, d = recs[12]
+    d = bytearray(d)
+    d[14] = 0x55
+    recs[12] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    out, res = run_file_world(pcap, ["--fixcsum"], world=2)
+    assert rc_o == -1 and all(r[1] == -1 for r in res)
+    assert out == exp and len(S.records(out)) == 12
+
+
 @pytest.mark.parametrize("bad_shard", [0, 1])
 def test_hard_error_truncates_at_first_failing_record(built, bad_shard):
     recs = S.records(S.pcap_fixed(40, 64, seed=5))
@@ -170,3 +260,62 @@ def test_two_rank_gpu_rewrite_equals_oracle(built, case):
     out, res = run_world(pcap, args, cache, use_gpu=True)
     assert rc_o == 0 and all(r[1] == 0 for r in res)
     assert out == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c4_cache", "fuzz_imix"])
+def test_two_rank_gpu_file_rewrite_equals_oracle(built, case):
+    """the file-based job on the device: segments read in place, outputs D2H'd into mmaps"""
+    if case == "c4_cache":
+        pcap, args, cache = G.read("test.pcap"), C4_ARGS, G.read("test.auto_router")
+    else:
+        pcap, cache = S.pcap_imix(20_000, seed=7), None
+        args = ["--fuzz-seed=8", "--fuzz-factor=2", "--enet-vlan=add", "--enet-vlan-tag=9", "--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    out, res = run_file_world(pcap, args, cache, use_gpu=True)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_c4_rank_share_at_nonzero_base_equals_oracle(built):
+    """BASELINE configs[3] at its real per-GPU size: the 4th of 8 ranks' 12.5M-record share
+    of the 100M-record C4 job (its records at global numbers 37.5M.., the job's cache
+    covering all 50M records before and in it), opened as a segment in place, equals the
+    oracle over the same records with the cache sliced at the same base"""
+    import tcpreplay_amd as TA
+    from concurrent.futures import ThreadPoolExecutor
+    n, base, rep = 12_500_000, 37_500_000, 10
+    block = S.pcap_imix(n // rep, seed=41)
+    pcap = block[:24] + block[24:] * rep  # 4.6 GB: the block's records 10 times over
+    cache = S.tcpprep_cache(base + n, seed=5, nosend_every=0)
+    te = TA.TcpEdit(C4_ARGS, device=0)
+    try:
+        b = TA.Batch(te, memoryview(pcap)[24:], cache, pkt_base=base, hdr=pcap[:24])
+        try:
+            assert b.run() == 0, te.geterr()
+            r = b.result()
+            got = bytearray(r.out_len - 24)
+            assert b.output_records_into(got) == len(got)
+        finally:
+            b.close()
+    finally:
+        te.close()
+    assert r.packets == n
+    # the oracle in 8 threads over byte-balanced sub-shards (each its own call, its cache
+    # sliced at its own global base); the C4 records read nothing past their own bytes
+    p = D.plan(pcap, 8)
+    shard_cache = slice_cache(cache, base, n)  # the share's directions (one unpack)
+
+    def one(k):
+        return O.rewrite(p.image(pcap, k), C4_ARGS, slice_cache(shard_cache, p.pkt_base[k], p.count(k)))
+    with ThreadPoolExecutor(8) as ex:
+        parts = list(ex.map(one, range(8)))
+    assert all(rc == 0 for rc, _ in parts)
+    pos = 0
+    for _, out in parts:
+        seg = memoryview(out)[24:]
+        assert got[pos:pos + len(seg)] == seg
+        pos += len(seg)
+    assert pos == len(got)
