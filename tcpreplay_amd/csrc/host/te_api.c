@@ -366,6 +366,68 @@ out:
     w->end = off;
 }
 
+/* Tile balance for small batches.  Wave w of the wave lane's W takes tiles w, w + W, ...
+ * (static dealing), so a batch of T tiles runs ceil(T / W) rounds and, when T is just
+ * past a multiple of W, its last round has few waves busy: latency-bound, nearly as long
+ * as a full one (C2: 15,873 greedy tiles of 63 records over 5,120 waves is 3.1 rounds,
+ * timed as 4).  Re-cut the record sequence to ceil(n / (R W)) records a tile, R = the
+ * rounds the greedy cut needs, so every wave takes R tiles of the same size.  Tiles of
+ * one record too large for the image (solo, scratch) stay as they are and bound the
+ * re-cut; every new tile satisfies the walk's budget test.  Only for batches of a few
+ * rounds (the tail is 1/R of the run) whose tiles are count- rather than byte-limited. */
+#define TE_BALANCE_MAX_ROUNDS 8
+static int balance_tiles(tcpedit_batch_t *b, uint32_t waves, uint32_t budget, uint32_t max_pkts)
+{
+    const uint64_t T = b->n_tiles, n = b->n_pkts;
+    const char *e = getenv("TCPEDIT_HIP_BALANCE");
+    if ((e && *e == '0') || !waves || T == 0 || T > (uint64_t)waves * TE_BALANCE_MAX_ROUNDS)
+        return 0;
+    const uint64_t R = (T + waves - 1) / waves, target = R * waves;
+    const uint64_t per = (n + target - 1) / target;
+    if (per >= max_pkts || T * 100 >= target * 97) /* byte-limited tiles, or balanced already */
+        return 0;
+    te_tile_t *nt = malloc(sizeof(te_tile_t) * (target + T + 16));
+    if (!nt)
+        return 0; /* the greedy cut stands */
+    uint64_t cnt = 0;
+    te_tile_t cur;
+    int open = 0;
+    for (uint64_t t = 0; t < T; t++) {
+        const te_tile_t ot = b->tiles[t];
+        if ((ot.flags & TE_TILE_SOLO) || ot.scratch_off != TE_NO_SCRATCH) {
+            if (open)
+                nt[cnt++] = cur, open = 0;
+            nt[cnt++] = ot;
+            continue;
+        }
+        const uint64_t tend = ot.span_off + ot.span_len;
+        for (uint32_t k = 0; k < ot.npkt; k++) {
+            const uint32_t j = ot.first_pkt + k;
+            const uint64_t off = ot.span_off + b->pkt_rel[j];
+            const uint64_t end = k + 1 < ot.npkt ? ot.span_off + b->pkt_rel[j + 1] : tend;
+            if (open && (cur.npkt >= per || !TE_CONTIG_FITS_IN(cur.span_off & 15, end - cur.span_off, budget)))
+                nt[cnt++] = cur, open = 0;
+            if (!open) {
+                memset(&cur, 0, sizeof(cur));
+                cur.span_off = off;
+                cur.first_pkt = j;
+                cur.scratch_off = TE_NO_SCRATCH;
+                open = 1;
+            }
+            /* (record j's old offset was read above, before this write) */
+            b->pkt_rel[j] = (uint16_t)(off - cur.span_off);
+            cur.npkt++;
+            cur.span_len = (uint32_t)(end - cur.span_off);
+        }
+    }
+    if (open)
+        nt[cnt++] = cur;
+    free(b->tiles);
+    b->tiles = nt;
+    b->n_tiles = cnt;
+    return 1;
+}
+
 /* a plausible record chain at p: `n` consecutive headers within the image whose
    lengths libpcap would accept and whose microsecond/nanosecond field is in range */
 static int chain_plausible(const uint8_t *img, size_t len, size_t p, int swapped, int nsec, int n)
@@ -707,6 +769,9 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     }
     b->n_tiles = m->n_tiles;
     b->n_pkts = m->n_pkts;
+    if (!rc && proto.wave && !proto.slot_mode && !b->idx_pinned)
+        balance_tiles(b, te_wave_waves(&t->cfg, shrink_fast ? static_shrink_kind(&t->cfg) : TE_SZ_NONE),
+                      proto.budget, proto.max_pkts);
     b->out_cap = 24 + 64 + m->rec_bytes;
     b->scratch_bytes = m->scratch_bytes;
     b->stop_error_pkt = m->stop_error_pkt;

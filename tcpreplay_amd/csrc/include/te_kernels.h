@@ -160,6 +160,7 @@ size_t te_l2carry_temp_bytes(uint32_t n_pkts);
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */
 int te_fast_grid(void);
 int te_wave_grid(void);
+uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz);
 
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(te_launch_t *L, hipStream_t stream);

@@ -2079,6 +2079,13 @@ extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz) {
                                                                                        : TE_WK_LEAN_TILE_BYTES;
 }
 
+// the waves a config's wave-lane launch runs (its instance's resident grid x 4): the host
+// balances a small batch's tile cut to a whole number of rounds of them
+extern "C" uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz) {
+    const int k = wave_pick(fast_feat(c), sz);
+    return k < 0 ? 0u : (uint32_t)wave_inst_grid(k) * (uint32_t)WK_NW;
+}
+
 // the largest wave-lane grid of any instance (the host sizes the per-block slots by it)
 extern "C" int te_wave_grid(void) {
     static int c = 0;
