@@ -178,7 +178,7 @@ typedef struct {
    PPP = pppserial, whose encode leaves the packet as it is (pppserial.c:239-251) */
 enum { ENC_EN10MB = 0, ENC_USER, ENC_HDLC, ENC_NOENC, ENC_PPP };
 /* decoders (NULL and LOOP share dlt_null's functions, loop.c:47-64) */
-enum { DEC_EN10MB = 0, DEC_SLL, DEC_SLL2, DEC_RAW, DEC_NULL, DEC_PPP, DEC_CHDLC };
+enum { DEC_EN10MB = 0, DEC_SLL, DEC_SLL2, DEC_RAW, DEC_NULL, DEC_PPP, DEC_CHDLC, DEC_JNPR, DEC_80211, DEC_RADIOTAP };
 
 /* decoder/encoder per-context scratch (tcpeditdlt_t + en10mb_extra_t) which
  * the reference keeps across packets (plugins_types.h:100-131). */
@@ -1500,10 +1500,195 @@ static int raw_proto(const uint8_t *pkt, int pktlen)
     return TCPEDIT_ERROR;
 }
 
+/* ---- DLT_IEEE802_11 (plugins/dlt_ieee80211/ieee80211.c, ieee80211_hdr.c).  The frame
+   control word is read with ntohs, so the masks of ieee80211_types.h:33-76 apply to
+   (byte0 << 8 | byte1): type/subtype in the high byte, the DS/WEP flags in the low one. */
+#define I80211_FC_TYPE_MASK 0x0F00
+#define I80211_FC_TYPE_DATA 0x0800
+#define I80211_FC_SUBTYPE_MASK 0xF000
+#define I80211_FC_SUBTYPE_QOS 0x8000
+#define I80211_FC_SUBTYPE_NULL 0xC000
+#define I80211_FC_WEP_MASK 0x0040
+#define I80211_USE_4(fc) (((fc)&3) == 3) /* ieee80211_USE_4: TO_DS and FROM_DS */
+
+static uint16_t i80211_fc(const uint8_t *pkt) { return (uint16_t)(pkt[0] << 8 | pkt[1]); }
+
+/* dlt_ieee80211_l2len: ieee80211.c:333-371 (0, not -1, for a short frame) */
+static int i80211_l2len(const uint8_t *pkt, int pktlen)
+{
+    if (pktlen < 2)
+        return 0;
+    const uint16_t fc = i80211_fc(pkt);
+    int hdrlen = I80211_USE_4(fc) ? 30 : 24; /* ieee80211_addr4_hdr_t / ieee80211_hdr_t */
+    if ((fc & I80211_FC_SUBTYPE_QOS) == I80211_FC_SUBTYPE_QOS)
+        hdrlen += 2;
+    if (pktlen >= hdrlen + 8) /* struct tcpr_802_2snap_hdr: 8 bytes, tcpr_802_2_hdr: 3 */
+        hdrlen += pkt[hdrlen] == 0xAA && pkt[hdrlen + 1] == 0xAA ? 8 : 3;
+    if (pktlen < hdrlen)
+        return 0;
+    return hdrlen;
+}
+
+/* ieee80211_is_data: ieee80211_hdr.c:36-92 */
+static int i80211_is_data(const uint8_t *pkt, int pktlen)
+{
+    if (pktlen <= 24)
+        return 0;
+    const uint16_t fc = i80211_fc(pkt);
+    if ((fc & I80211_FC_SUBTYPE_MASK) == I80211_FC_SUBTYPE_NULL)
+        return 1;
+    if ((fc & I80211_FC_TYPE_MASK) == I80211_FC_TYPE_DATA)
+        return 1;
+    int hdrlen = (fc & I80211_FC_SUBTYPE_MASK) >= I80211_FC_SUBTYPE_QOS ? 2 : 0;
+    hdrlen += I80211_USE_4(fc) ? 30 : 24;
+    if (pktlen < hdrlen + 8)
+        return 0;
+    return pkt[hdrlen] == 0xAA && pkt[hdrlen + 1] == 0xAA;
+}
+
+/* ieee80211_get_src / ieee80211_get_dst: ieee80211_hdr.c:120-184 (addr1 at 4, addr2 at 10,
+   addr3 at 16, addr4 at 24) */
+static const uint8_t *i80211_src(const uint8_t *pkt)
+{
+    const uint16_t fc = i80211_fc(pkt);
+    if (I80211_USE_4(fc))
+        return pkt + 24;
+    return (fc & 3) == 2 ? pkt + 16 : pkt + 10; /* FROM_DS: addr3; TO_DS or neither: addr2 */
+}
+static const uint8_t *i80211_dst(const uint8_t *pkt)
+{
+    const uint16_t fc = i80211_fc(pkt);
+    if (I80211_USE_4(fc))
+        return pkt + 16;
+    return (fc & 3) == 2 ? pkt + 4 : pkt + 16; /* FROM_DS: addr1; TO_DS or neither: addr3 */
+}
+
+/* dlt_ieee80211_proto: ieee80211.c:246-291.  The SNAP header is read at the computed offset
+   whatever the captured length (past it: the static buffer's bytes). */
+static int i80211_proto(const uint8_t *pkt, int pktlen)
+{
+    const int l2len = i80211_l2len(pkt, pktlen);
+    if (pktlen < l2len)
+        return TCPEDIT_ERROR;
+    const uint16_t fc = i80211_fc(pkt);
+    if ((fc & I80211_FC_TYPE_MASK) != I80211_FC_TYPE_DATA)
+        return TCPEDIT_SOFT_ERROR;
+    int hdrlen = (fc & I80211_FC_SUBTYPE_QOS) == I80211_FC_SUBTYPE_QOS ? 2 : 0;
+    hdrlen += I80211_USE_4(fc) ? 30 : 24;
+    if (pkt[hdrlen] == 0xAA && pkt[hdrlen + 1] == 0xAA)
+        return ld16(pkt + hdrlen + 6); /* snap_type, network order */
+    return TCPEDIT_SOFT_ERROR;
+}
+
+/* dlt_ieee80211_decode: ieee80211.c:184-224 */
+static int i80211_decode(ostate_t *s, const uint8_t *pkt, int pktlen)
+{
+    const int l2len = i80211_l2len(pkt, pktlen);
+    if (pktlen < l2len)
+        return TCPEDIT_ERROR;
+    if (!i80211_is_data(pkt, pktlen)) {
+        seterr("Packet is not a normal 802.11 data frame");
+        return TCPEDIT_SOFT_ERROR;
+    }
+    if (pktlen >= 24 && (i80211_fc(pkt) & I80211_FC_WEP_MASK) == I80211_FC_WEP_MASK) { /* is_encrypted */
+        seterr("Packet is encrypted.  Unable to decode frame.");
+        return TCPEDIT_SOFT_ERROR;
+    }
+    s->l2len = l2len;
+    s->l2offset = 0;
+    memcpy(s->srcaddr, i80211_src(pkt), 6);
+    memcpy(s->dstaddr, i80211_dst(pkt), 6);
+    s->proto = (uint16_t)i80211_proto(pkt, pktlen);
+    return TCPEDIT_OK;
+}
+
+/* ---- DLT_JUNIPER_ETHER (plugins/dlt_jnpr_ether/jnpr_ether.c): a 6-byte header {magic
+   4d 47 43, options, extension length (BE)}, TLV extensions, then an Ethernet frame that
+   an en10mb sub-decoder decodes.  tcpedit_dlt_copy_decoder_state (dlt_utils.c:249-271)
+   hands the sub-decoder's addresses, proto and -- by pointer -- its en10mb extra (the
+   inner frame's VLAN fields; dst_modified lives there too) to the encoder, and adds its
+   l2len; ctx->l2offset stays 0. */
+#define JNPR_HEADER_LEN 6
+/* dlt_jnpr_ether_proto: jnpr_ether.c:310-345 */
+static int jnpr_proto(const uint8_t *pkt, int pktlen)
+{
+    if (pktlen < JNPR_HEADER_LEN)
+        return TCPEDIT_ERROR;
+    if ((pkt[3] & 0x80) != 0x80) /* JUNIPER_ETHER_L2PRESENT */
+        return TCPEDIT_ERROR;
+    const int hl = (pkt[4] << 8 | pkt[5]) + JNPR_HEADER_LEN;
+    if (hl > pktlen)
+        return TCPEDIT_ERROR;
+    return en10mb_proto(pkt + hl, pktlen - hl);
+}
+/* dlt_jnpr_ether_decode: jnpr_ether.c:201-282.  A frame whose extensions do not say
+   Ethernet (media type 1, encapsulation 14) is a TCPEDIT_WARN: the encoder then runs on
+   the previous frame's decoded state with this frame's Juniper header length. */
+static int jnpr_decode(ostate_t *s, const uint8_t *pkt, int pktlen)
+{
+    if (pktlen < JNPR_HEADER_LEN)
+        return TCPEDIT_ERROR;
+    if (pkt[0] != 0x4d || pkt[1] != 0x47 || pkt[2] != 0x43) {
+        seterr("Invalid magic 0x%02X%02X%02X", pkt[0], pkt[1], pkt[2]);
+        return TCPEDIT_ERROR;
+    }
+    if ((pkt[3] & 0x80) != 0x80) {
+        seterr("Frame is missing L2 Header: %x", pkt[3]);
+        return TCPEDIT_ERROR;
+    }
+    const int hl = (pkt[4] << 8 | pkt[5]) + JNPR_HEADER_LEN;
+    if (pktlen < hl + 14) {
+        seterr("Frame is too short! %d < %d", pktlen, hl + 14);
+        return TCPEDIT_ERROR;
+    }
+    s->l2len = hl;
+    s->l2offset = 0;
+    int ext = JNPR_HEADER_LEN, dlt = 0, encap = 0;
+    while (ext < hl - 2) {
+        const int ext_len = pkt[ext + 1];
+        if (pkt[ext] == 3) /* JUNIPER_ETHER_EXT_MEDIA_TYPE */
+            dlt = pkt[ext + 2];
+        else if (pkt[ext] == 6) /* JUNIPER_ETHER_EXT_ENCAPSULATION */
+            encap = pkt[ext + 2];
+        if (dlt != 0 && encap != 0)
+            break;
+        ext += ext_len + 2;
+    }
+    if (ext > hl) {
+        seterr("Extension to long! %d", ext - hl);
+        return TCPEDIT_ERROR;
+    }
+    if (dlt != 1 || encap != 14) {
+        seterr("packet DLT %d and encapsulation type %u not supported", dlt, encap);
+        return TCPEDIT_WARN;
+    }
+    /* the sub-decoder (an en10mb context of its own: its l2offset is not copied back) */
+    if (en10mb_decode(s, pkt + hl, pktlen - hl) == TCPEDIT_ERROR)
+        return TCPEDIT_ERROR;
+    s->l2len += hl;
+    s->l2offset = 0;
+    return TCPEDIT_OK;
+}
+
 /* the decoder's proto (tcpedit_dlt_proto on the source DLT, tcpedit.c:96) */
 static int decoder_proto(const ocfg_t *c, const uint8_t *pkt, int pktlen)
 {
     switch (c->decoder) {
+    case DEC_JNPR:
+        return jnpr_proto(pkt, pktlen);
+    case DEC_80211:
+        return i80211_proto(pkt, pktlen);
+    case DEC_RADIOTAP: { /* radiotap.c:134-155 */
+        if (pktlen < 8) /* sizeof(radiotap_hdr_t) */
+            return TCPEDIT_ERROR;
+        const int radiolen = pkt[2] | pkt[3] << 8; /* it_len, little endian */
+        if (radiolen > pktlen)
+            return TCPEDIT_ERROR;
+        /* dlt_radiotap_get_80211 (radiotap.c:344-364) copies the 802.11 frame into its
+           extra buffer only when it is at least MAXPACKET bytes long, which no record is:
+           the 802.11 proto reads the extra's zeros -- frame control 0, not a data frame */
+        return TCPEDIT_SOFT_ERROR;
+    }
     case DEC_SLL: /* linuxsll.c:213-226 */
         return pktlen < 16 ? TCPEDIT_ERROR : ld16(pkt + 14);
     case DEC_SLL2: /* linuxsll2.c:226-238 */
@@ -1576,6 +1761,12 @@ static int decoder_decode(const ocfg_t *c, ostate_t *s, const uint8_t *pkt, int 
         s->proto = ld16(pkt + 2);
         s->l2len = 4;
         return TCPEDIT_OK;
+    case DEC_JNPR:
+        return jnpr_decode(s, pkt, pktlen);
+    case DEC_80211:
+        return i80211_decode(s, pkt, pktlen);
+    case DEC_RADIOTAP: /* (its proto never lets a record get here) */
+        return TCPEDIT_ERROR;
     default:
         return en10mb_decode(s, pkt, pktlen);
     }
@@ -1630,7 +1821,8 @@ static int en10mb_encode(const ocfg_t *c, ostate_t *s, uint8_t *packet, int pktl
     /* the decoder's address type (plugin_l2addr_type): ETHERNET for en10mb and the Linux
        cooked headers, which have a source address (the destination stays as the zeroed
        context left it); none for the others (en10mb.c:586-659) */
-    const bool eth_addr = c->decoder == DEC_EN10MB || c->decoder == DEC_SLL || c->decoder == DEC_SLL2;
+    const bool eth_addr = c->decoder == DEC_EN10MB || c->decoder == DEC_SLL || c->decoder == DEC_SLL2 ||
+                          c->decoder == DEC_JNPR || c->decoder == DEC_80211 || c->decoder == DEC_RADIOTAP;
     if (dir == DIR_C2S || dir == DIR_S2C) {
         const bool c2s = dir == DIR_C2S;
         const int sm = c2s ? MASK_SMAC1 : MASK_SMAC2, dm = c2s ? MASK_DMAC1 : MASK_DMAC2;
@@ -1996,7 +2188,7 @@ again: /* :89 -- a fuzzed packet goes through L2 and the per-family edits once m
         pktlen = (int)h->caplen;
     } else {
         int rc = decoder_decode(c, s, packet, (int)h->caplen);
-        if (rc == TCPEDIT_ERROR)
+        if (rc == TCPEDIT_ERROR || rc == TCPEDIT_SOFT_ERROR) /* (a TCPEDIT_WARN goes on to encode) */
             return TCPEDIT_SOFT_ERROR;
         if (c->encoder == ENC_USER)
             pktlen = user_encode(c, s, packet, (int)h->caplen, direction);
@@ -2723,10 +2915,12 @@ static int oracle_post_args(ocfg_t *c, const oopts_t *o)
             int enc, dlt;
         } plugins[] = {{"enet", ENC_EN10MB, 1},      {"user", ENC_USER, 147},    {"hdlc", ENC_HDLC, 104},
                        {"linuxsll", ENC_NOENC, 113}, {"linuxsll2", ENC_NOENC, 276}, {"raw", ENC_NOENC, 12},
-                       {"null", ENC_NOENC, 0},       {"loop", ENC_NOENC, 108},   {"pppserial", ENC_PPP, 50}};
+                       {"null", ENC_NOENC, 0},       {"loop", ENC_NOENC, 108},   {"pppserial", ENC_PPP, 50},
+                       {"jnpr_eth", ENC_NOENC, 178}, {"ieee80211", ENC_NOENC, 105}, {"radiotap", ENC_NOENC, 127}};
         static const int dec_enc[] = {[DEC_EN10MB] = ENC_EN10MB, [DEC_SLL] = ENC_NOENC, [DEC_SLL2] = ENC_NOENC,
                                       [DEC_RAW] = ENC_NOENC,     [DEC_NULL] = ENC_NOENC, [DEC_PPP] = ENC_PPP,
-                                      [DEC_CHDLC] = ENC_HDLC};
+                                      [DEC_CHDLC] = ENC_HDLC,    [DEC_JNPR] = ENC_NOENC, [DEC_80211] = ENC_NOENC,
+                                      [DEC_RADIOTAP] = ENC_NOENC};
         c->encoder = dec_enc[c->decoder];
         c->out_linktype = c->in_dlt;
         if (o->have[O_DLT]) {
@@ -2958,17 +3152,19 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
             uint32_t dlt;
             int dec;
         } decs[] = {{1, DEC_EN10MB}, {113, DEC_SLL}, {276, DEC_SLL2}, {12, DEC_RAW},  {0, DEC_NULL},
-                    {108, DEC_NULL}, {50, DEC_PPP},  {104, DEC_CHDLC}};
+                    {108, DEC_NULL}, {50, DEC_PPP},  {104, DEC_CHDLC}, {178, DEC_JNPR}, {105, DEC_80211},
+                    {127, DEC_RADIOTAP}};
+        const int ndec = (int)(sizeof(decs) / sizeof(decs[0]));
         int k = 0;
-        while (k < 8 && decs[k].dlt != lt)
+        while (k < ndec && decs[k].dlt != lt)
             k++;
-        if (in_len >= 24 && k == 8) {
+        if (in_len >= 24 && k == ndec) {
             seterr("No DLT plugin available for source DLT: 0x%x (in the oracle's scope)", lt);
             rc = -2;
             goto out;
         }
-        c.decoder = k < 8 ? decs[k].dec : DEC_EN10MB;
-        c.in_dlt = k < 8 ? (int)lt : 1;
+        c.decoder = k < ndec ? decs[k].dec : DEC_EN10MB;
+        c.in_dlt = k < ndec ? (int)lt : 1;
     }
     if (parse_argv(o, argc, argv) < 0 || oracle_post_args(&c, o) < 0) {
         rc = -2;

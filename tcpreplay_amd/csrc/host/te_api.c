@@ -906,7 +906,7 @@ int te_upload_cfg(tcpedit_t *t)
         t->dev_dirty = 1; /* a fuzzing_init since the last upload re-seeds the state */
     {   /* the dst_modified carry, whatever set the config (post_args or setters) */
         const te_dev_cfg_t *c = &t->cfg;
-        const uint32_t l2c = (c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2) && c->encoder == TE_ENC_EN10MB &&
+        const uint32_t l2c = TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB &&
                              !(c->mac_mask & TE_MASK_DMAC1);
         if (l2c != c->l2carry) {
             t->cfg.l2carry = l2c;
@@ -2318,7 +2318,7 @@ int tcpedit_init(tcpedit_t **out, int dlt)
     te_sync_pub(t);
     if (te_decoder_of(dlt) < 0) {
         te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: EN10MB, LINUX_SLL, LINUX_SLL2, "
-                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC)", dlt);
+                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC, JUNIPER_ETHER, IEEE802_11, IEEE802_11_RADIO)", dlt);
         return TCPEDIT_ERROR;
     }
     return TCPEDIT_OK;

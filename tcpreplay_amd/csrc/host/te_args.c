@@ -533,7 +533,7 @@ static void pm_sparse(tcpedit_t *t)
 }
 
 /* the decoder plugin of an input DLT (tcpedit_dlt_init, dlt_plugins.c:115-160; the
- * plugins' dlt_value): -1 when this build has none (JUNIPER_ETHER, IEEE802_11, radiotap) */
+ * plugins' dlt_value): -1 when this build has none */
 int te_decoder_of(int dlt)
 {
     switch (dlt) {
@@ -545,6 +545,9 @@ int te_decoder_of(int dlt)
     case 108: return TE_DEC_NULL;  /* DLT_LOOP (loop.c: dlt_null's functions) */
     case 50: return TE_DEC_PPP;    /* DLT_PPP_SERIAL (pppserial.c:41) */
     case 104: return TE_DEC_CHDLC; /* DLT_C_HDLC */
+    case 178: return TE_DEC_JNPR;  /* DLT_JUNIPER_ETHER (jnpr_ether.c:44) */
+    case 105: return TE_DEC_80211; /* DLT_IEEE802_11 (ieee80211.c:38) */
+    case 127: return TE_DEC_RADIOTAP; /* DLT_IEEE802_11_RADIO (radiotap.c:32) */
     default: return -1;
     }
 }
@@ -571,6 +574,9 @@ int te_decoder_l2len(int dec)
     case TE_DEC_NULL:
     case TE_DEC_PPP:
     case TE_DEC_CHDLC: return 4;
+    case TE_DEC_JNPR: return 20;     /* the 6-byte Juniper header and the inner Ethernet, at least */
+    case TE_DEC_80211: return 24;    /* ieee80211_hdr_t, at least */
+    case TE_DEC_RADIOTAP: return 24; /* (never encoded: every record is a soft error) */
     default: return 14;
     }
 }
@@ -581,8 +587,8 @@ int te_check_decoder_cfg(tcpedit_t *t, int s2c)
 {
     te_dev_cfg_t *c = &t->cfg;
     const int foreign = c->decoder != TE_DEC_EN10MB;
-    const int eth_addr = c->decoder == TE_DEC_EN10MB || c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2;
-    c->l2carry = (c->decoder == TE_DEC_SLL || c->decoder == TE_DEC_SLL2) && c->encoder == TE_ENC_EN10MB &&
+    const int eth_addr = c->decoder == TE_DEC_EN10MB || TE_DEC_ETH_ADDR(c->decoder);
+    c->l2carry = TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB &&
                  !(c->mac_mask & TE_MASK_DMAC1);
     if (foreign && c->encoder == TE_ENC_EN10MB) {
         if (c->vlan == TE_VLAN_ADD) {
@@ -853,7 +859,7 @@ int te_derive_cfg(tcpedit_t *t)
     c->decoder = te_decoder_of(t->dlt);
     if (c->decoder < 0) {
         te_seterr(t, "No DLT plugin available for source DLT: 0x%x (this build: EN10MB, LINUX_SLL, LINUX_SLL2, "
-                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC)", t->dlt);
+                     "RAW, NULL, LOOP, PPP_SERIAL, C_HDLC, JUNIPER_ETHER, IEEE802_11, IEEE802_11_RADIO)", t->dlt);
         return -1;
     }
     c->encoder = te_default_encoder(c->decoder);
@@ -864,7 +870,8 @@ int te_derive_cfg(tcpedit_t *t)
             int enc, dlt;
         } plugins[] = {{"enet", TE_ENC_EN10MB, 1},      {"user", TE_ENC_USER, 147},    {"hdlc", TE_ENC_HDLC, 104},
                        {"linuxsll", TE_ENC_NOENC, 113}, {"linuxsll2", TE_ENC_NOENC, 276}, {"raw", TE_ENC_NOENC, 12},
-                       {"null", TE_ENC_NOENC, 0},       {"loop", TE_ENC_NOENC, 108},   {"pppserial", TE_ENC_PPP, 50}};
+                       {"null", TE_ENC_NOENC, 0},       {"loop", TE_ENC_NOENC, 108},   {"pppserial", TE_ENC_PPP, 50},
+                       {"jnpr_eth", TE_ENC_NOENC, 178}, {"ieee80211", TE_ENC_NOENC, 105}, {"radiotap", TE_ENC_NOENC, 127}};
         size_t k = 0;
         while (k < sizeof(plugins) / sizeof(plugins[0]) && strcmp(plugins[k].name, t->arg[OPT_DLT]) != 0)
             k++;

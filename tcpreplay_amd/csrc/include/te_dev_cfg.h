@@ -37,7 +37,12 @@ enum { TE_VLAN_OFF = 0, TE_VLAN_DEL, TE_VLAN_ADD };
    (pppserial.c:239-251) */
 enum { TE_ENC_EN10MB = 0, TE_ENC_USER, TE_ENC_HDLC, TE_ENC_NOENC, TE_ENC_PPP };
 /* decoders (tcpedit_dlt_init by the input DLT; NULL and LOOP share dlt_null's functions) */
-enum { TE_DEC_EN10MB = 0, TE_DEC_SLL, TE_DEC_SLL2, TE_DEC_RAW, TE_DEC_NULL, TE_DEC_PPP, TE_DEC_CHDLC };
+enum { TE_DEC_EN10MB = 0, TE_DEC_SLL, TE_DEC_SLL2, TE_DEC_RAW, TE_DEC_NULL, TE_DEC_PPP, TE_DEC_CHDLC,
+       TE_DEC_JNPR, TE_DEC_80211, TE_DEC_RADIOTAP };
+/* decoders whose plugin_l2addr_type is ETHERNET besides en10mb: the en10mb encoder takes
+   their decoded addresses and sets dst_modified from them */
+#define TE_DEC_ETH_ADDR(d) ((d) == TE_DEC_SLL || (d) == TE_DEC_SLL2 || (d) == TE_DEC_JNPR || (d) == TE_DEC_80211 || \
+                            (d) == TE_DEC_RADIOTAP)
 enum { TE_FUZZ_OFF = 0, TE_FUZZ_PROBE, TE_FUZZ_APPLY }; /* the generic kernel's fuzz passes */
 #define TE_USER_L2MAX 256 /* USER_L2MAXLEN (255, user_types.h:37), rounded */                  /* en10mb_types.h:50-54 */
 enum { TE_MASK_SMAC1 = 1, TE_MASK_SMAC2 = 2, TE_MASK_DMAC1 = 4, TE_MASK_DMAC2 = 8 };

@@ -936,12 +936,59 @@ DI int raw_proto(const u8 *p, u32 caplen) {
     if (caplen < 20) return RC_ERROR;
     return (p[0] >> 4) == 4 ? 0x0008 : (p[0] >> 4) == 6 ? 0xDD86 : RC_ERROR;
 }
+// a byte the reference reads at packet offset `off` whatever the captured length: past the
+// record's physical bytes it reads its static buffer (Q8: flagged, replayed)
+DI u32 byte_at(Pkt &pk, int off) {
+    if (off + 1 > (int)pk.phys) stale(pk, off + 1);
+    return off < (int)pk.avail ? pk.d[off] : 0u;
+}
+// dlt_en10mb_proto (en10mb.c:741-762) of the Ethernet frame at p
+DI int en10mb_proto_at(const u8 *p, u32 n) {
+    if (n < 14) return RC_ERROR;
+    L2 r;
+    if (get_l2len_protocol(p, n, r) == -1) return RC_ERROR;
+    return bswap16(r.protocol);
+}
+
+// DLT_IEEE802_11 (plugins/dlt_ieee80211): the frame control word is read with ntohs, so
+// the masks of ieee80211_types.h:33-76 apply to (byte0 << 8 | byte1)
+DI u32 w80211_fc(const u8 *d) { return (u32)d[0] << 8 | d[1]; }
+DI int w80211_hdr(u32 fc, bool qos) { return (qos ? 2 : 0) + ((fc & 3u) == 3u ? 30 : 24); }  // + QoS, 4 addresses
+// dlt_ieee80211_l2len (ieee80211.c:333-371): 0, not -1, for a short frame
+DI int w80211_l2len(const u8 *d, int n) {
+    if (n < 2) return 0;
+    const u32 fc = w80211_fc(d);
+    int h = w80211_hdr(fc, (fc & 0x8000u) == 0x8000u);
+    if (n >= h + 8) h += d[h] == 0xAA && d[h + 1] == 0xAA ? 8 : 3;  // 802.2 SNAP or 802.2
+    return n < h ? 0 : h;
+}
+// dlt_ieee80211_proto (ieee80211.c:246-291): the SNAP type, read at its offset whatever the
+// captured length
+DI int w80211_proto(Pkt &pk) {
+    const u32 fc = byte_at(pk, 0) << 8 | byte_at(pk, 1);
+    if ((fc & 0x0F00u) != 0x0800u) return RC_PROTO_SOFT;  // not a data frame
+    const int h = w80211_hdr(fc, (fc & 0x8000u) == 0x8000u);
+    if (byte_at(pk, h) == 0xAA && byte_at(pk, h + 1) == 0xAA) return (int)(byte_at(pk, h + 6) | byte_at(pk, h + 7) << 8);
+    return RC_PROTO_SOFT;
+}
+
 // the decoder's proto (tcpedit_dlt_proto on the source DLT, tcpedit.c:96): the ethertype
 // as the little-endian u16 of its network-order bytes, or < 0
-DI int decoder_proto(const Pkt &pk, const te_dev_cfg_t &cfg) {
+DI int decoder_proto(Pkt &pk, const te_dev_cfg_t &cfg) {
     const u8 *d = pk.d;
     const u32 n = pk.caplen;
     switch (cfg.decoder) {
+    case TE_DEC_JNPR: {  // dlt_jnpr_ether_proto (jnpr_ether.c:310-345): the inner frame's
+        if (n < 6 || !(d[3] & 0x80)) return RC_ERROR;  // JUNIPER_ETHER_L2PRESENT
+        const u32 hl = ((u32)d[4] << 8 | d[5]) + 6u;
+        if (hl > n) return RC_ERROR;
+        return en10mb_proto_at(d + hl, n - hl);
+    }
+    case TE_DEC_80211: return w80211_proto(pk);
+    // radiotap.c:134-155, 344-364: the 802.11 frame is copied into the plugin's MAXPACKET
+    // extra buffer only when at least that long, which no record is -- the 802.11 proto
+    // reads zeros there, not a data frame: every record is a soft error
+    case TE_DEC_RADIOTAP: return RC_PROTO_SOFT;
     case TE_DEC_SLL: return n < 16 ? RC_ERROR : (int)ld16(d + 14);  // linuxsll.c:213-226
     case TE_DEC_SLL2: return n < 20 ? RC_ERROR : (int)ld16(d);      // linuxsll2.c:226-238
     case TE_DEC_RAW: return raw_proto(d, n);
@@ -950,18 +997,15 @@ DI int decoder_proto(const Pkt &pk, const te_dev_cfg_t &cfg) {
     // never take for IPv4; anything but PPP's IPv4 protocol is a soft error
     case TE_DEC_PPP: return n < 4 ? RC_ERROR : be16(d + 2) == 0x0021 ? 0x0800 : RC_PROTO_SOFT;
     case TE_DEC_CHDLC: return n < 4 ? RC_ERROR : (int)ld16(d + 2);  // hdlc.c:299-311
-    default: {  // dlt_en10mb_proto (en10mb.c:741-762)
-        if (n < 14) return RC_ERROR;
-        L2 r;
-        if (get_l2len_protocol(d, n, r) == -1) return RC_ERROR;
-        return bswap16(r.protocol);
-    }
+    default: return en10mb_proto_at(d, n);  // dlt_en10mb_proto
     }
 }
 // the decoder (plugin_decode) for the non-Ethernet DLTs: l2len, proto and, for the Linux
 // cooked headers, the source address.  None of them sets the en10mb extra fields, which
-// keep the zeroed start of the decoder's (larger) extra buffer (en10mb.c:100-110).
-DI int foreign_decode(const Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
+// keep the zeroed start of the decoder's (larger) extra buffer (en10mb.c:100-110) --
+// except the Juniper decoder, whose en10mb sub-decoder's extra becomes the encoder's.
+// (A soft error from the decoder is returned as RC_ERROR: both make the record RC_SOFT.)
+DI int foreign_decode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
     const u8 *d = pk.d;
     const u32 n = pk.caplen;
 #pragma unroll
@@ -1005,6 +1049,62 @@ DI int foreign_decode(const Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
         s.proto = be16(d + 2) == 0x0021 ? 0x0008 : (int)ld16(d + 2);
         s.l2len = 4;
         return RC_OK;
+    case TE_DEC_JNPR: {  // dlt_jnpr_ether_decode (jnpr_ether.c:201-282)
+        if (n < 6) return RC_ERROR;
+        if (d[0] != 0x4d || d[1] != 0x47 || d[2] != 0x43) return RC_ERROR;  // JUNIPER_ETHER_MAGIC
+        if (!(d[3] & 0x80)) return RC_ERROR;                                 // no L2 header
+        const u32 hl = ((u32)d[4] << 8 | d[5]) + 6u;
+        if (n < hl + 14) return RC_ERROR;
+        // the extension TLVs: media type (3) and encapsulation (6), first byte of each value
+        u32 ext = 6, dlt = 0, enc = 0;
+        while (ext + 2 < hl) {
+            const u32 el = d[ext + 1];
+            if (d[ext] == 3) dlt = d[ext + 2];
+            else if (d[ext] == 6) enc = d[ext + 2];
+            if (dlt && enc) break;
+            ext += el + 2;
+        }
+        if (ext > hl) return RC_ERROR;
+        // TCPEDIT_WARN: the reference encodes this frame with the previous frame's decoded
+        // state (the decode left it); not reproduced here -- the record fails the run loudly
+        if (dlt != 1 || enc != 14) {
+            stale(pk, (int)NEED_NEVER);
+            return RC_ERROR;
+        }
+        // the en10mb sub-decoder (tcpedit_dlt_copy_decoder_state, dlt_utils.c:249-271: its
+        // addresses, proto and extra; the l2lens add; ctx->l2offset stays 0)
+        if (en10mb_decode(d + hl, (int)(n - hl), s) == RC_ERROR) return RC_ERROR;
+        s.l2len += (int)hl;
+        s.l2offset = 0;
+        return RC_OK;
+    }
+    case TE_DEC_80211: {  // dlt_ieee80211_decode (ieee80211.c:184-224)
+        const int l2 = w80211_l2len(d, (int)n);
+        const u32 fc = n >= 2 ? w80211_fc(d) : 0u;  // (n < 2: the proto was a stale read already)
+        bool data;                                    // ieee80211_is_data (ieee80211_hdr.c:36-92)
+        if (n <= 24) {
+            data = false;
+        } else if ((fc & 0xF000u) == 0xC000u || (fc & 0x0F00u) == 0x0800u) {
+            data = true;
+        } else {
+            const int h = w80211_hdr(fc, (fc & 0xF000u) >= 0x8000u);
+            data = (int)n >= h + 8 && d[h] == 0xAA && d[h + 1] == 0xAA;
+        }
+        if (!data) return RC_ERROR;                       // TCPEDIT_SOFT_ERROR
+        if (n >= 24 && (fc & 0x40u)) return RC_ERROR;     // encrypted: TCPEDIT_SOFT_ERROR
+        s.l2len = l2;
+        // ieee80211_get_src/dst (ieee80211_hdr.c:120-184): by the DS bits
+        const int ds = (int)(fc & 3u);
+        const int so = ds == 3 ? 24 : ds == 2 ? 16 : 10, dof = ds == 3 ? 16 : ds == 2 ? 4 : 16;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            s.srcaddr[i] = (u8)byte_at(pk, so + i);
+            s.dstaddr[i] = (u8)byte_at(pk, dof + i);
+        }
+        s.proto = w80211_proto(pk);
+        return RC_OK;
+    }
+    case TE_DEC_RADIOTAP: return RC_ERROR;  // (its proto stops every record first)
     default:  // TE_DEC_CHDLC, hdlc.c:192-218 (its address/control extras are never marked filled)
         if (n < 4) return RC_ERROR;
         s.proto = ld16(d + 2);
@@ -1055,13 +1155,13 @@ DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktle
     if (pktlen + 14 - s.l2len > MAXPACKET) return RC_ERROR;
     if (pktlen < s.l2len) return RC_ERROR;
     if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;
-    const bool eth_addr = cfg.decoder == TE_DEC_SLL || cfg.decoder == TE_DEC_SLL2;
+    const bool eth_addr = TE_DEC_ETH_ADDR(cfg.decoder);
     const bool c2s = dir == TE_DIR_C2S;
     const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
     if (!eth_addr && (!(cfg.mac_mask & sm) || !(cfg.mac_mask & dm))) return RC_ERROR;
-    bool old_nz = false;  // memcmp(eth->ether_dhost, ctx->dstaddr (zero), 6) before the writes
+    bool old_nz = false;  // memcmp(eth->ether_dhost, ctx->dstaddr, 6) before the writes
 #pragma unroll
-    for (int i = 0; i < 6; ++i) old_nz |= pk.d[i] != 0;
+    for (int i = 0; i < 6; ++i) old_nz |= pk.d[i] != s.dstaddr[i];
     if (!l2_replace(pk, s.l2len, 14)) return RC_ERROR;
     pktlen += 14 - s.l2len;
     u8 *dh = pk.d, *sh = pk.d + 6;
@@ -1078,7 +1178,20 @@ DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktle
     if (c2s && !(cfg.mac_mask & dm)) s.dst_modified = old_nz;
     en10mb_mac_rules(cfg, dh, sh);
     st16(pk.d + 12, (u16)s.proto);
-    if (cfg.vlan == TE_VLAN_DEL) st16(pk.d + 12, 0);  // htons(extra->vlan_proto), never set
+    // the VLAN fields of the decoder's extra: zero (never set) but for the Juniper decoder,
+    // whose inner frame's en10mb decode filled them (en10mb.c:696-732)
+    if (cfg.vlan == TE_VLAN_OFF && s.vlan) {  // the TCI written at the inner frame's tag offset
+        if ((int)s.vlan_offset + 2 > pktlen) {
+            stale(pk, (int)NEED_NEVER);  // (past the new frame: the static buffer)
+        } else {
+            u8 *vh = pk.d + s.vlan_offset;
+            st16(vh, bswap16((u16)((cfg.vlan_tag < 65535 ? (u16)cfg.vlan_tag & 0x0fff : s.vlan_tag))));
+            st16(vh, (u16)(ld16(vh) + bswap16(cfg.vlan_pri < 255 ? (u16)(cfg.vlan_pri << 13) : s.vlan_pri)));
+            st16(vh, (u16)(ld16(vh) + bswap16(cfg.vlan_cfi < 255 ? (u16)(cfg.vlan_cfi << 12) : s.vlan_cfi)));
+        }
+    } else if (cfg.vlan == TE_VLAN_DEL) {
+        st16(pk.d + 12, bswap16((u16)s.vlan_proto));  // htons(extra->vlan_proto)
+    }
     return pktlen;
 }
 

@@ -2170,16 +2170,28 @@ __global__ __launch_bounds__(256) void te_l2carry_mark(LaunchArgs a, unsigned lo
         const uint8_t b = idx < a.dirbits_len ? a.dirbits[idx] : 0;
         dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
     }
-    const bool sll = cfg.decoder == TE_DEC_SLL;
-    const uint8_t *d = rec + 16;
-    bool writer = dir == TE_DIR_C2S && caplen >= (sll ? 16u : 20u);  // the proto and decode length checks
-    if (writer) {
-        const uint16_t type = (uint16_t)(d[sll ? 2 : 8] << 8 | d[sll ? 3 : 9]);
-        writer = type == 1 || type == 772;  // decode: ARPHRD_ETHER / ARPHRD_LOOPBACK
-    }
+    // a writer: a C2S record that reaches the encoder's address step -- the decoder's proto
+    // and decode succeed (tcpedit.c:96, dlt_plugins.c:210-238) and en10mb.c:544-585's length
+    // checks pass -- run by the edit's own decoder functions over the record in HBM
+    Pkt pk;
+    pk.d = const_cast<uint8_t *>(rec + 16);
+    pk.caplen = caplen;
+    pk.len = len;
+    pk.phys = pk.avail = pk.ext = caplen;
+    pk.unsupported = false;
+    pk.need = 0;
+    pk.strict = false;
+    bool writer = dir == TE_DIR_C2S && decoder_proto(pk, cfg) >= 0;
+    Dec s;
+    s.dst_modified = false;
+    if (writer) writer = foreign_decode(pk, cfg, s) != RC_ERROR;
+    const int pktlen = (int)caplen;
+    if (writer) writer = pktlen >= 14 && pktlen >= s.l2len && pktlen + 14 - s.l2len <= (int)MAXPACKET;
+    // dst_modified: the frame's first 6 bytes (the encoder's memmove leaves them) against
+    // the decoded destination (en10mb.c:612-615)
     bool nz = false;
     if (writer)
-        for (int i = 0; i < 6; ++i) nz |= d[i] != 0;
+        for (int i = 0; i < 6; ++i) nz |= pk.d[i] != s.dstaddr[i];
     key[j + 1] = writer ? ((unsigned long long)(j + 1) << 1 | (nz ? 1u : 0u)) : 0ull;
 }
 

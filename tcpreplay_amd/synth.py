@@ -266,6 +266,60 @@ def build_pcap(recs, linktype=1):
 
 # link types of the non-Ethernet decoders (the pcap header's linktype field)
 LINKTYPES = {"sll": 113, "sll2": 276, "raw": 101, "raw12": 12, "null": 0, "loop": 108, "ppp": 50, "chdlc": 104}
+# ... and of the Juniper Ethernet, 802.11 and radiotap decoders
+LINKTYPES_MORE = {"jnpr": 178, "80211": 105, "radiotap": 127}
+
+
+def _jnpr(i, d, odd, rng):
+    """a Juniper Ethernet header {4d 47 43, options (L2 present | direction), extension
+    length} with TLV extensions (an ifindex TLV first on some records), media type 1 and
+    encapsulation 14, then the whole Ethernet frame; every 4th inner frame carries an
+    802.1Q tag.  odd: a bad magic (a decoder error)."""
+    ext = b""
+    if i % 3 == 1:
+        ext += b"\x01\x04" + int(i).to_bytes(4, "big")
+    ext += (b"\x06\x01\x0e\x03\x01\x01" if i % 2 else b"\x03\x01\x01\x06\x01\x0e")
+    if i % 5 == 2:
+        ext += b"\x04\x02\x00\x07"  # a TLV after both (the walk has stopped)
+    magic = b"\x4d\x47\x44" if odd else b"\x4d\x47\x43"
+    h = magic + bytes([0x80 | (i & 1)]) + len(ext).to_bytes(2, "big") + ext
+    if i % 4 == 3:
+        d = d[:12] + b"\x81\x00" + int(0x2000 | (i % 4095)).to_bytes(2, "big") + d[12:]
+    return h + d
+
+
+def _w80211(i, d, odd, rng):
+    """an 802.11 data frame: frame control (data, or QoS data on every 3rd record; the
+    DS bits cycle 0..3, four addresses for ToDS|FromDS), duration, addresses, sequence,
+    [QoS control], an 802.2 SNAP header with the ethertype, then the L3 bytes.  odd: a
+    management frame, a protected frame or an 802.2 header without SNAP, in turn."""
+    ds = i % 4
+    qos = i % 3 == 0
+    b0 = 0x88 if qos else 0x08
+    b1 = ds
+    llc = b"\xaa\xaa\x03\x00\x00\x00" + d[12:14]
+    if odd:
+        k = (i // 7) % 3
+        if k == 0:
+            b0 = 0x80  # a beacon: not a data frame
+        elif k == 1:
+            b1 |= 0x40  # protected
+        else:
+            llc = b"\x42\x42\x03" + bytes(5)
+    a = [d[0:6], d[6:12], bytes(rng.integers(0, 256, 6, dtype=np.uint8)), bytes(rng.integers(0, 256, 6, dtype=np.uint8))]
+    hdr = bytes([b0, b1]) + b"\x2c\x00" + a[0] + a[1] + a[2] + (i % 4096 * 16).to_bytes(2, "little")
+    if ds == 3:
+        hdr += a[3]
+    if qos:
+        hdr += bytes([i % 8, 0])
+    return hdr + llc + d[14:]
+
+
+def _radiotap(i, d, odd, rng):
+    """a radiotap header (version 0, length 8 + 4 k, present flags) before an 802.11 frame"""
+    extra = 4 * (i % 3)
+    rt = b"\x00\x00" + (8 + extra).to_bytes(2, "little") + (0x0000002e).to_bytes(4, "little") + bytes(extra)
+    return rt + _w80211(i, d, odd, rng)
 
 
 def reframe(pcap: bytes, kind: str, seed=1, odd_every=0):
@@ -282,6 +336,8 @@ def reframe(pcap: bytes, kind: str, seed=1, odd_every=0):
       loop   the address family in network order
       ppp    PPP in HDLC-like framing: ff 03 and the PPP protocol (0x0021 IPv4, 0x0057 IPv6)
       chdlc  Cisco HDLC: address 0x0f, control 0, the ethertype
+      jnpr / 80211 / radiotap  see _jnpr, _w80211, _radiotap (the whole frame is kept or
+             rebuilt around the L3 bytes)
     odd_every=k: every k-th record gets a header the decoder refuses or does not take as
     IP (SLL: ARPHRD 0x0200; NULL/LOOP: family 7; PPP: protocol 0xc021; RAW: version 5)."""
     rng = np.random.default_rng(seed)
@@ -311,9 +367,14 @@ def reframe(pcap: bytes, kind: str, seed=1, odd_every=0):
             h = b"\xff\x03" + (b"\xc0\x21" if odd else (b"\x00\x57" if v6 else b"\x00\x21"))
         elif kind == "chdlc":
             h = b"\x0f\x00" + et
+        elif kind in LINKTYPES_MORE:
+            nd = {"jnpr": _jnpr, "80211": _w80211, "radiotap": _radiotap}[kind](i, d, odd, rng)
+            dl = len(nd) - len(d)
+            out.append((ts, tu, cl + dl, ln + dl, nd))
+            continue
         else:
             raise ValueError(kind)
         nd = h + l3
         dl = len(nd) - len(d)
         out.append((ts, tu, cl + dl, ln + dl, nd))
-    return build_pcap(out, LINKTYPES[kind])
+    return build_pcap(out, {**LINKTYPES, **LINKTYPES_MORE}[kind])

@@ -97,11 +97,11 @@ def test_unserved_combinations_are_refused(built):
     te = TA.TcpEdit
     for dlt, args in [(12, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
                       (12, ["--dlt=enet"]), (0, ["--dlt=enet", "--enet-smac=00:11:22:33:44:55"]),
-                      (113, ["--fuzz-seed=3"]), (113, ["--dlt=hdlc"]), (1, ["--dlt=ieee80211"])]:
+                      (113, ["--fuzz-seed=3"]), (113, ["--dlt=hdlc"]), (1, ["--dlt=tokenring"])]:
         with pytest.raises(Exception):
             te(args, dlt=dlt)
     with pytest.raises(Exception):
-        te(["--fixcsum"], dlt=105)  # IEEE802_11: no decoder in this build
+        te(["--fixcsum"], dlt=9)  # DLT_PPP: the reference has no plugin for it either
 
 
 # ------------------------------------------------------------------------- GPU

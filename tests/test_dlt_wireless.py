@@ -1,0 +1,191 @@
+"""The Juniper Ethernet, 802.11 and radiotap decoders: DLT_JUNIPER_ETHER
+(src/tcpedit/plugins/dlt_jnpr_ether/jnpr_ether.c), DLT_IEEE802_11 (dlt_ieee80211/ieee80211.c,
+ieee80211_hdr.c) and DLT_IEEE802_11_RADIO (dlt_radiotap/radiotap.c), as decoders into the
+en10mb encoder (--dlt=enet) and into their own plugins (which refuse to encode).
+
+Parity is unpinned: the reference ships no capture of these link types.  The oracle's
+restatement (oracle/tcpedit_oracle.c jnpr_*, i80211_*, the radiotap proto) is checked here
+against outputs built independently from the synthetic framings (CPU), and the GPU against
+the oracle, bit-exact.  Reference behaviours kept:
+  * radiotap: dlt_radiotap_get_80211 copies the 802.11 frame into its MAXPACKET extra
+    buffer only when the frame is at least that long, so the 802.11 proto reads zeros and
+    every record is a soft error, written as read (radiotap.c:344-364);
+  * 802.11: frame control read with ntohs; the source/destination by the DS bits; the
+    SNAP type as the proto; management, protected and non-SNAP frames are soft errors;
+  * Juniper: the inner Ethernet frame's en10mb decode supplies addresses, proto and the
+    VLAN fields (by the extra pointer), so --enet-vlan=del writes the inner type and a
+    tagged inner frame without --enet-vlan gets its TCI written at offset 14 of the new
+    frame; a frame whose extensions are not Ethernet is a TCPEDIT_WARN that re-uses the
+    previous frame's decoded state -- the device refuses such a record loudly."""
+import pytest
+
+import oracle_lib as O
+import tcpreplay_amd as TA
+from tcpreplay_amd import synth as S
+
+KINDS = list(S.LINKTYPES_MORE)
+DLT_OF = {"jnpr": 178, "80211": 105, "radiotap": 127}
+MACS = ["--enet-smac=00:11:22:33:44:55,00:aa:bb:cc:dd:ee", "--enet-dmac=00:66:77:88:99:aa,00:12:34:56:78:9a"]
+DMAC, SMAC = bytes.fromhex("00667788" "99aa"), bytes.fromhex("001122334455")
+
+
+def _base(n=600, seed=3):
+    return S.pcap_imix(n, seed=seed)
+
+
+def _w80211_ok(d):
+    fc = d[0] << 8 | d[1]
+    if (fc & 0x0F00) != 0x0800 or (fc & 0x40):
+        return None
+    h = (2 if fc & 0x8000 else 0) + (30 if fc & 3 == 3 else 24)
+    if d[h:h + 2] != b"\xaa\xaa":
+        return None
+    return h + 8, d[h + 6:h + 8]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_oracle_own_encoder_writes_the_capture_unedited(built, kind):
+    """no --dlt: the decoder's own plugin refuses to encode -- every record a soft error,
+    written as read; with --skip-soft-errors nothing is written"""
+    pcap = S.reframe(_base(), kind, odd_every=7)
+    rc, out = O.rewrite(pcap, ["--fixcsum", "--seed=7"])
+    assert rc == 0 and S.records(out) == S.records(pcap)
+    assert int.from_bytes(out[20:24], "little") == DLT_OF[kind]
+    rc, out = O.rewrite(pcap, ["--fixcsum", "--skip-soft-errors"])
+    assert rc == 0 and S.records(out) == []
+
+
+def test_oracle_radiotap_is_always_a_soft_error(built):
+    pcap = S.reframe(_base(), "radiotap")
+    rc, out = O.rewrite(pcap, ["--dlt=enet"] + MACS + ["--fixcsum"])
+    assert rc == 0 and S.records(out) == S.records(pcap)
+    assert int.from_bytes(out[20:24], "little") == 1
+
+
+def test_oracle_80211_into_ethernet_matches_the_layout(built):
+    """data frames become {the given MACs, the SNAP type, the L3 bytes}; management,
+    protected and non-SNAP frames are written as read"""
+    pcap = S.reframe(_base(), "80211", odd_every=7)
+    rc, out = O.rewrite(pcap, ["--dlt=enet"] + MACS)
+    assert rc == 0
+    exp = []
+    for ts, tu, cl, ln, d in S.records(pcap):
+        ok = _w80211_ok(d)
+        if ok is None:
+            exp.append((ts, tu, cl, ln, d))
+            continue
+        hl, et = ok
+        nd = DMAC + SMAC + et + d[hl:]
+        exp.append((ts, tu, cl + len(nd) - len(d), ln + len(nd) - len(d), nd))
+    assert S.records(out) == exp
+
+
+def test_oracle_80211_addresses_by_ds_bits(built):
+    """without --enet-smac/--enet-dmac the 802.11 source and destination are written:
+    addr2/addr3 (no DS bit, ToDS), addr3/addr1 (FromDS), addr4/addr3 (both)"""
+    pcap = S.reframe(_base(80), "80211")
+    rc, out = O.rewrite(pcap, ["--dlt=enet"])
+    assert rc == 0
+    for r_in, r_out in zip(S.records(pcap), S.records(out)):
+        d, o = r_in[4], r_out[4]
+        ds = d[1] & 3
+        src = {0: d[10:16], 1: d[10:16], 2: d[16:22], 3: d[24:30]}[ds]
+        dst = {0: d[16:22], 1: d[16:22], 2: d[4:10], 3: d[16:22]}[ds]
+        assert o[:6] == dst and o[6:12] == src
+
+
+def test_oracle_jnpr_into_ethernet_strips_header_and_tag(built):
+    """--enet-vlan=del: the Juniper header and the inner Ethernet header (with its 802.1Q
+    tag) become {the given MACs, the inner L3 type}; bad-magic records stay as read"""
+    base = S.records(_base())
+    pcap = S.reframe(S.build_pcap(base), "jnpr", odd_every=7)
+    rc, out = O.rewrite(pcap, ["--dlt=enet", "--enet-vlan=del"] + MACS)
+    assert rc == 0
+    exp = []
+    for k, ((ts, tu, cl, ln, d), (_, _, _, _, e)) in enumerate(zip(S.records(pcap), base)):
+        if d[:3] != b"\x4d\x47\x43":
+            exp.append((ts, tu, cl, ln, d))
+            continue
+        nd = DMAC + SMAC + e[12:]
+        exp.append((ts, tu, cl + len(nd) - len(d), ln + len(nd) - len(d), nd))
+    assert S.records(out) == exp
+
+
+def test_unserved_combinations_are_refused(built):
+    for dlt, args in [(178, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
+                      (105, ["--fuzz-seed=3"]), (127, ["--fuzz-seed=3", "--dlt=enet"] + MACS)]:
+        with pytest.raises(Exception):
+            TA.TcpEdit(args, dlt=dlt)
+
+
+# ------------------------------------------------------------------------- GPU
+ARGSETS = [
+    ["--fixcsum"],
+    ["--dlt=enet"] + MACS + ["--fixcsum"],
+    ["--dlt=enet"] + MACS + ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353", "--fixcsum"],
+    ["--dlt=enet"] + MACS + ["--seed=11", "--ttl=+2", "--efcs"],
+    ["--dlt=enet", "--enet-vlan=del", "--tos=5", "--mtu-trunc", "--mtu=400", "--fixcsum"] + MACS,
+    ["--dlt=enet", "--seed=3", "--fixcsum"],  # the decoded addresses (802.11, Juniper's inner frame)
+    ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fixcsum"],
+    ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
+]
+
+
+def _gpu_vs_oracle(pcap, args, dlt, cache=None):
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    te = TA.TcpEdit(args, dlt=dlt)
+    try:
+        rc, out = te.rewrite(pcap, cache)
+        assert (rc, out) == (rc_o, exp), args
+        rc, out = te.rewrite_pipelined(pcap, cache, chunk_bytes=1 << 16)
+        assert (rc, out) == (rc_o, exp), args
+    finally:
+        te.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("k", range(len(ARGSETS)))
+def test_gpu_matches_oracle(built, kind, k):
+    pcap = S.reframe(_base(3000, seed=k + 1), kind, odd_every=11)
+    _gpu_vs_oracle(pcap, ARGSETS[k], DLT_OF[kind])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["jnpr", "80211"])
+def test_gpu_dst_modified_carries_across_s2c_records(built, kind):
+    """SURVEY Q18 behind these decoders: a C2S record without --enet-dmac sets the en10mb
+    encoder's dst_modified (the frame's first 6 bytes against the decoded destination), an
+    S2C record keeps the last C2S record's value, the multicast MAC update reads it"""
+    base = S.records(_base(4000, seed=21))
+    recs = []
+    for i, (ts, tu, cl, ln, d) in enumerate(base):
+        d = bytearray(d)
+        if i % 3 == 0 and d[12:14] == b"\x08\x00":
+            d[30:34] = bytes([224 + i % 16, 1, 2, 3])
+        recs.append((ts, tu, cl, ln, bytes(d)))
+    pcap = S.reframe(S.build_pcap(recs), kind)
+    cache = S.tcpprep_cache(len(base), seed=5, nosend_every=9)
+    args = ["--dlt=enet", "--fixcsum"]
+    _gpu_vs_oracle(pcap, args, DLT_OF[kind], cache)
+
+
+@pytest.mark.gpu
+def test_gpu_jnpr_non_ethernet_extension_is_refused(built):
+    """a Juniper frame whose extensions are not Ethernet (TCPEDIT_WARN: the reference
+    encodes it with the previous frame's decoded state) fails the run loudly on the device"""
+    recs = S.records(S.reframe(_base(200, seed=4), "jnpr"))
+    ts, tu, cl, ln, d = recs[50]
+    d = bytearray(d)
+    k = d.find(b"\x06\x01\x0e")
+    d[k + 2] = 0x0f  # encapsulation 15
+    recs[50] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs, 178)
+    rc_o, exp = O.rewrite(pcap, ["--dlt=enet"] + MACS)
+    assert rc_o == 0
+    te = TA.TcpEdit(["--dlt=enet"] + MACS, dlt=178)
+    try:
+        rc, out = te.rewrite(pcap)
+        assert rc == -1 and "record 51" in te.geterr()  # (1-based, as the reference counts)
+    finally:
+        te.close()
