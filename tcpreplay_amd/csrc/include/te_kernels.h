@@ -14,7 +14,9 @@ extern "C" {
 
 #define TE_BLOCK 256           /* threads per block = max packets per tile */
 #define TE_MAX_PKTS 256
-#define TE_SLOT_BYTES 36864    /* LDS slot budget per block (4 blocks / CU) */
+#ifndef TE_SLOT_BYTES
+#define TE_SLOT_BYTES 36864    /* LDS slot budget per block (3 blocks / CU) */
+#endif
 #define TE_HEAD 16             /* headroom before each record (VLAN push) */
 #define TE_TAIL_BYTES 16       /* zeroed bytes after each packet's data */
 #define TE_NO_SCRATCH 0xffffffffffffffffull

@@ -23,6 +23,10 @@ CASES = {
             "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"]),
     "vdel": (lambda: S.pcap_imix(1_000_000, seed=1, vlan=0xB02D), ["--enet-vlan=del", "--fixcsum"]),
     "efcs": (lambda: S.pcap_imix(1_000_000, seed=1, fcs=True), ["--efcs", "--fixcsum"]),
+    # generic-lane configs (size changes by record, MAC seed, fuzzing)
+    "mtu": (lambda: S.pcap_imix(1_000_000, seed=1), ["--mtu=1000", "--mtu-trunc", "--fixcsum"]),
+    "macseed": (lambda: S.pcap_imix(1_000_000, seed=1), ["--enet-mac-seed=42", "--fixcsum"]),
+    "fz": (lambda: S.pcap_imix(1_000_000, seed=1), ["--fuzz-seed=42", "--fuzz-factor=2"]),
 }
 CACHES = {"c4": lambda: S.tcpprep_cache(1_000_000, seed=1)}
 
