@@ -72,9 +72,17 @@ def free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, pcap, args, cache, out_path, use_gpu, q):
+def _init(backend, rank, world, port):
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: the collectives' tensors live on this rank's GPU
+        import torch
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    return dist
+
+
+def _worker(rank, world, port, pcap, args, cache, out_path, use_gpu, q, backend="gloo"):
+    dist = _init(backend, rank, world, port)
     try:
         editor = None if use_gpu else oracle_editor_for(pcap, world)
         rc, counters, seg, off = D.rewrite_distributed(pcap, args, cache, out_path, editor=editor, device=0)
@@ -83,11 +91,10 @@ def _worker(rank, world, port, pcap, args, cache, out_path, use_gpu, q):
         dist.destroy_process_group()
 
 
-def _file_worker(rank, world, port, in_path, args, cache_path, out_path, use_gpu, q):
-    import torch.distributed as dist
+def _file_worker(rank, world, port, in_path, args, cache_path, out_path, use_gpu, q, backend="gloo"):
     global args_of_job
     args_of_job = args
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist = _init(backend, rank, world, port)
     try:
         editor = None if use_gpu else oracle_segment_editor
         rc, counters, wrote, off = D.rewrite_file_distributed(in_path, args, out_path, cache_path, device=0,
@@ -97,7 +104,7 @@ def _file_worker(rank, world, port, in_path, args, cache_path, out_path, use_gpu
         dist.destroy_process_group()
 
 
-def run_file_world(pcap, args, cache=None, world=2, use_gpu=False):
+def run_file_world(pcap, args, cache=None, world=2, use_gpu=False, backend="gloo"):
     """rewrite_file_distributed over files: the plan broadcast from rank 0, each rank's
     byte range read in place from an mmap, outputs written into mmaps of the output file"""
     ctx = mp.get_context("spawn")
@@ -111,7 +118,7 @@ def run_file_world(pcap, args, cache=None, world=2, use_gpu=False):
             cache_path = os.path.join(d, "in.cache")
             open(cache_path, "wb").write(cache)
         procs = [ctx.Process(target=_file_worker, args=(r, world, port, in_path, args, cache_path, out_path,
-                                                        use_gpu, q)) for r in range(world)]
+                                                        use_gpu, q, backend)) for r in range(world)]
         for pr in procs:
             pr.start()
         for pr in procs:
@@ -121,13 +128,13 @@ def run_file_world(pcap, args, cache=None, world=2, use_gpu=False):
         return open(out_path, "rb").read(), res
 
 
-def run_world(pcap, args, cache=None, world=2, use_gpu=False):
+def run_world(pcap, args, cache=None, world=2, use_gpu=False, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     with tempfile.TemporaryDirectory() as d:
         out_path = os.path.join(d, "out.pcap")
-        procs = [ctx.Process(target=_worker, args=(r, world, port, pcap, args, cache, out_path, use_gpu, q))
+        procs = [ctx.Process(target=_worker, args=(r, world, port, pcap, args, cache, out_path, use_gpu, q, backend))
                  for r in range(world)]
         for pr in procs:
             pr.start()
@@ -275,6 +282,23 @@ def test_two_rank_gpu_file_rewrite_equals_oracle(built, case):
     out, res = run_file_world(pcap, args, cache, use_gpu=True)
     assert rc_o == 0 and all(r[1] == 0 for r in res)
     assert out == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c3_imix", "fuzz_imix"])
+def test_nccl_rank_rewrite_equals_oracle(built, case):
+    """the collectives over RCCL (backend "nccl", CUDA tensors: the 16-byte segment
+    all-gather, the counter all-reduce, the fuzz reach all-gather) at world size 1 -- one
+    GPU on the test box, and RCCL refuses two ranks on one device -- for both the bytes job
+    and the file job"""
+    pcap = S.pcap_imix(20_000, seed=6 if case == "c3_imix" else 7)
+    args = (["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"] if case == "c3_imix"
+            else ["--fuzz-seed=8", "--fuzz-factor=2", "--fixcsum"])
+    rc_o, exp = O.rewrite(pcap, args, None)
+    out, res = run_world(pcap, args, None, world=1, use_gpu=True, backend="nccl")
+    assert rc_o == 0 and res[0][1] == 0 and out == exp
+    out, res = run_file_world(pcap, args, None, world=1, use_gpu=True, backend="nccl")
+    assert res[0][1] == 0 and out == exp
 
 
 @pytest.mark.gpu
