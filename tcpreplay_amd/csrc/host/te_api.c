@@ -68,6 +68,7 @@ struct tcpedit_batch_s {
     /* the device index (tcpedit_batch_index_device): the cut walk_range made, and whether
        the device can make it (wave-lane tiles over contiguous records) */
     uint32_t cut_budget, cut_max_pkts, cut_growth;
+    uint64_t cut_tiles; /* the walk's greedy tile count (before balance_tiles re-cuts a small batch) */
     int cut_device_ok;
     uint8_t ohdr[24];        /* the output file header, the source of its upload */
     uint8_t *res_pinned;     /* pipeline slot: page-locked landing area of a run's counters, error
@@ -768,6 +769,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         rc = -1;
     }
     b->n_tiles = m->n_tiles;
+    b->cut_tiles = m->n_tiles;
     b->n_pkts = m->n_pkts;
     if (!rc && proto.wave && !proto.slot_mode && !b->idx_pinned)
         balance_tiles(b, te_wave_waves(&t->cfg, shrink_fast ? static_shrink_kind(&t->cfg) : TE_SZ_NONE),
@@ -1621,8 +1623,10 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
     if (!b->cut_device_ok || b->in_len <= 24)
         return 1;
     const uint64_t body = b->in_len - 24;
-    const uint64_t avg = b->n_tiles ? (b->walk_end - 24) / b->n_tiles : 4096;
-    uint64_t W = (8 * (avg ? avg : 64) + 63) & ~63ull; /* about 8 tiles a window */
+    /* about 8 greedy tiles a window (the device cuts greedily; a balanced re-cut's smaller
+       tiles would shrink the windows and give the speculation more starts to be fooled at) */
+    const uint64_t avg = b->cut_tiles ? (b->walk_end - 24) / b->cut_tiles : 4096;
+    uint64_t W = (8 * (avg ? avg : 64) + 63) & ~63ull;
     if (W < 4096)
         W = 4096;
     if (W > 65536)

@@ -209,6 +209,22 @@ __device__ __forceinline__ uint32_t sel_bytes(uint32_t x, uint32_t y, int b0, in
     return (x & ~m) | (y & m);
 }
 
+// TE_GK_STAMPS builds (diagnostics only): s_memtime per tile phase, wave 0's view (so a
+// phase includes the barrier wait behind it), summed per block, printed by a few blocks
+#if TE_GK_STAMPS
+__shared__ unsigned long long gk_ph[6], gk_last;
+#define GK_STAMP(i)                                                        \
+    if (threadIdx.x == 0) {                                                \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        gk_ph[i] += now_ - gk_last;                                        \
+        gk_last = now_;                                                    \
+    }
+#else
+#define GK_STAMP(i)
+#endif
+
 // ---------------------------------------------------------------------------
 // tile body.  S = slot buffer (LDS, or HBM scratch for a huge record).
 // ---------------------------------------------------------------------------
@@ -259,6 +275,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     }
     __syncthreads();
 
+    GK_STAMP(0);  // positions
     // ---- stream the span into LDS: aligned 16-byte chunks ----
     {
         const uint64_t Aend = G0 + tile.span_len;
@@ -301,6 +318,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         }
     }
     __syncthreads();
+    GK_STAMP(1);  // span load
 
     // ---- one lane per packet ----
     uint32_t out_sz = 0, need = 0;
@@ -382,6 +400,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (write) out_sz = 16 + pk.caplen;
         ((g_u8 *)a.status)[tile.first_pkt + tid] = st;
     }
+    GK_STAMP(2);  // edit (wave 0's lanes)
     if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) return;  // the reach pass writes nothing else
 
     // ---- tile output offsets ----
@@ -469,6 +488,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             a.q8_list[k] = make_uint4(tile.first_pkt + tid, need, (uint32_t)o, (uint32_t)(o >> 32));
     }
 
+    GK_STAMP(3);  // placement, counters, look-back
     // ---- stream the output records: aligned 16-byte chunks ----
     if (tile_total == 0) return;
     const uint64_t Gs = a.out_base + E;
@@ -522,6 +542,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             }
         }
     }
+    GK_STAMP(4);  // output store
 }
 
 // records larger than a tile: same body over an HBM scratch slot, kept out of
@@ -557,12 +578,23 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         uint32_t *dst = (uint32_t *)&cfg;
         for (int i = threadIdx.x; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
     }
+#if TE_GK_STAMPS
+    uint32_t gk_nt = 0;
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 6; ++i) gk_ph[i] = 0;
+        gk_last = __builtin_amdgcn_s_memtime();
+    }
+#endif
     for (;;) {
         if (threadIdx.x == 0) sh.tile_id = atomicAdd(a.ticket, 1u);
         __syncthreads();
         uint32_t t = sh.tile_id;
         __syncthreads();
+        GK_STAMP(5);  // ticket + the previous tile's tail
         if (t >= n_work) break;
+#if TE_GK_STAMPS
+        ++gk_nt;
+#endif
         if (listed) t = a.tile_list[t];
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
@@ -571,6 +603,11 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
             huge_tile<FZ, AD>((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
         __syncthreads();
     }
+#if TE_GK_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 4)
+        printf("GK block %u tiles %u pos %llu load %llu edit %llu place %llu store %llu ticket %llu\n", blockIdx.x,
+               gk_nt, gk_ph[0], gk_ph[1], gk_ph[2], gk_ph[3], gk_ph[4], gk_ph[5]);
+#endif
 }
 
 // ===========================================================================
