@@ -275,6 +275,18 @@ DI u32 fold16(unsigned long long s) {
 }
 
 // sum of `len` bytes at p, weights relative to p (even offset -> low byte).
+// The dword body takes eight loads per step, all in flight before the first add (one
+// lane sums a whole packet, so a dependent load per dword left the LDS latency exposed
+// on every 4 bytes of a 1500-byte payload); each dword adds as its two 16-bit words
+// (v_sad_u16), which folds to the same one's-complement value as the dword sum
+// (2^16 == 1 mod 0xffff, and both sums are 0 only for all-zero bytes).
+DI u32 wsum_acc16(u32 x, u32 acc) {
+#ifdef TE_HOST_EMU
+    return acc + (x & 0xffffu) + (x >> 16);
+#else
+    return __builtin_amdgcn_sad_u16(x, 0u, acc);
+#endif
+}
 DI u32 csum_bytes(const u8 *p, int len) {
     if (len <= 0) return 0;
     uintptr_t a = (uintptr_t)p;
@@ -287,8 +299,16 @@ DI u32 csum_bytes(const u8 *p, int len) {
         ++i;
     }
     const u32 *w = (const u32 *)(b + i);
-    int nw = (len - i) >> 2;
-    for (int k = 0; k < nw; ++k) s += w[k];
+    const int nw = (len - i) >> 2;
+    int k = 0;
+    for (; k + 8 <= nw; k += 8) {  // <= 8 dwords x 0x1fffe per step: no u32 overflow
+        const u32 x0 = w[k], x1 = w[k + 1], x2 = w[k + 2], x3 = w[k + 3];
+        const u32 x4 = w[k + 4], x5 = w[k + 5], x6 = w[k + 6], x7 = w[k + 7];
+        u32 acc = wsum_acc16(x0, wsum_acc16(x1, wsum_acc16(x2, wsum_acc16(x3, 0u))));
+        acc = wsum_acc16(x4, wsum_acc16(x5, wsum_acc16(x6, wsum_acc16(x7, acc))));
+        s += acc;
+    }
+    for (; k < nw; ++k) s += w[k];
     i += nw << 2;
     for (; i < len; ++i) s += (u32)b[i] << (8 * ((a + i) & 1));
     u32 f = fold16(s);
