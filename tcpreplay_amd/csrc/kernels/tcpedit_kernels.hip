@@ -209,6 +209,9 @@ __device__ __forceinline__ uint32_t sel_bytes(uint32_t x, uint32_t y, int b0, in
     return (x & ~m) | (y & m);
 }
 
+#ifndef TE_GK_LOAD_K
+#define TE_GK_LOAD_K 5
+#endif
 // TE_GK_STAMPS builds (diagnostics only): s_memtime per tile phase, wave 0's view (so a
 // phase includes the barrier wait behind it), summed per block, printed by a few blocks
 #if TE_GK_STAMPS
@@ -283,7 +286,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if constexpr (MODE == MODE_CONTIG) {
             // every chunk a lane owns is in flight before the first LDS store: one HBM
             // round trip per tile instead of one per chunk
-            constexpr int K = 5;  // 16-byte chunks per lane per batch
+            constexpr int K = TE_GK_LOAD_K;  // 16-byte chunks per lane per batch
             for (uint32_t c0 = tid; c0 < nchunks; c0 += K * BLOCK) {
                 uint4 v[K];
 #pragma unroll
