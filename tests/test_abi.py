@@ -29,7 +29,16 @@ ABI_BIN = os.path.join(ABI_DIR, "_build", "tcprewrite_abi")
 
 @pytest.fixture(scope="module")
 def abi(built):
-    subprocess.check_call(["make", "-s", "-C", ABI_DIR])
+    # one make at a time (pytest-xdist workers share the build dir: a relink while
+    # another worker runs the binary fails with ETXTBSY)
+    import fcntl
+    os.makedirs(os.path.join(ABI_DIR, "_build"), exist_ok=True)
+    with open(os.path.join(ABI_DIR, "_build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            subprocess.check_call(["make", "-s", "-C", ABI_DIR])
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return ABI_BIN
 
 
