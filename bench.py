@@ -6,9 +6,16 @@ BASELINE configs[1]: `--seed=42 --fixcsum` over 1M x 64 B synthetic UDP
 records.  A "step" is one pass of the whole device pipeline (one kernel:
 parse + edit + checksum + scan + compaction) over that batch, inputs already
 resident in HBM.  With --gpus N (one process per GPU, torch.distributed over
-RCCL) every rank rewrites its own 1M-record shard -- packets are independent,
-so there is no data-path collective, only one all-reduce of the counters per
-job -- and `value` is the aggregate packets/s over the max-over-ranks time.
+RCCL) every rank rewrites its own 10M-record shard (HBM-resident; N = 1's
+`c2x10` side line is the same per-GPU workload) -- packets are independent, so
+there is no data-path collective, only one all-reduce of the counters per job
+-- and `value` is the aggregate packets/s over the max-over-ranks time; a
+`strong_c4` side line runs BASELINE configs[3] (100M records split over the
+ranks).
+
+Every workload's first (untimed) run is checked byte for byte against the
+oracle (tests/oracle_lib.check_rewrite) before it is timed: `verified` and
+`verified_records` in the JSON line (--no-verify skips it).
 
 Prints ONE JSON line on rank 0.
 """
@@ -58,6 +65,7 @@ WORKLOADS = {
             "--mtu=1000 --mtu-trunc --fixcsum on IMIX 64/570/1514 7:4:1 (1514 B records cut to 1014 B: "
             "per-record sizes, block scan + look-back placement on the generic lane)"),
 }
+PER_RANK_PACKETS = {"c2": 10_000_000}  # N > 1 per-rank shard (HBM-resident)
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
                    "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000,
                    "mtu": 4_000_000}
@@ -95,7 +103,46 @@ def make_share(workload, total, rank, world, seed):
     return block[:24], b"".join(parts), first, cnt
 
 
-def run_workload(workload, n, steps, warmup, seed, device, verify=False, share=None, total=None):
+def verify_threads():
+    """checker threads: the CPUs this process may run on, at most 16 (the GPU box's CPU share)"""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def check_output(b, pcap, args, cache, pkt_base=0, hdr=None):
+    """Parity on the bench's own clock (outside the timed region): the device output of the
+    batch's first run against the oracle (tests/oracle_lib.check_rewrite, the CPU restatement
+    of tcpedit_packet) on the same input and options, byte for byte.  Records are
+    independent unless --fuzz-seed or a stale static-buffer read (Q8) carries state, so the
+    oracle runs on byte-balanced shards of whole records on `verify_threads()` threads,
+    else on one.  Returns the records checked; raises on any difference."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    r = b.result()
+    dev = b.output_np()
+    if hdr is not None:  # a --strong share: file header + this rank's records
+        import numpy as np
+        src = np.empty(24 + len(pcap), np.uint8)
+        src[:24] = np.frombuffer(hdr, np.uint8)[:24]
+        src[24:] = np.frombuffer(pcap, np.uint8)
+        pcap = src
+    sharded = not any(a.startswith("--fuzz-seed") for a in args) and r.stale_records == 0
+    n = oracle_lib.check_rewrite(pcap, args, cache, dev, threads=verify_threads(), sharded=sharded,
+                                 pkt_base=pkt_base)
+    if n != r.packets:
+        raise RuntimeError(f"checker walked {n} records, the device {r.packets}")
+    return n
+
+
+def check_output_bytes(pcap, args, cache, out):
+    """check_output for an output image already on the host"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    return oracle_lib.check_rewrite(pcap, args, cache, out, threads=verify_threads())
+
+
+def run_workload(workload, n, steps, warmup, seed, device, verify=True, share=None, total=None):
+    """Open the workload's batch, run it once (untimed) and, with `verify`, check that run's
+    output against the oracle.  Returns (context, batch, result, pcap, records verified)."""
     import tcpreplay_amd as TA
     from tcpreplay_amd import synth
     args = WORKLOADS[workload][2]
@@ -110,19 +157,19 @@ def run_workload(workload, n, steps, warmup, seed, device, verify=False, share=N
         cache = synth.tcpprep_cache(n, seed=seed) if workload in CACHED else None
         te = TA.TcpEdit(args, device=device)
         b = TA.Batch(te, pcap, cache)
-    rc = b.run()  # first (untimed) run: also the correctness check below
+    rc = b.run()  # first (untimed) run: also the run the checker compares
     r = b.result()
     if rc != 0 or r.unsupported or r.errors:
         raise RuntimeError(f"{workload}: device run failed rc={rc} ({te.geterr()})")
-    if verify and pcap is not None:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib
-        rc_o, exp = oracle_lib.rewrite(pcap, args, cache)
-        if b.output() != exp:
-            raise RuntimeError(f"{workload}: device output differs from the oracle")
+    checked = 0
+    if verify:
+        if share is not None:
+            checked = check_output(b, share[1], args, cache, pkt_base=share[2], hdr=share[0])
+        else:
+            checked = check_output(b, pcap, args, cache)
     if warmup:
         b.time(warmup)
-    return te, b, r, pcap
+    return te, b, r, pcap, checked
 
 
 def _pcap_shards(pcap, parts):
@@ -179,6 +226,39 @@ def cpu_baseline(pcap, args, n_pkts, budget_s=10.0, threads=1):
     return runs * n_pkts / el / 1e6, runs, el, len(jobs)
 
 
+def strong_side(opt, world, rank, local, barrier):
+    """N > 1 side line: BASELINE configs[3] as written -- one 100M-record c4 capture split
+    into `world` byte-balanced shares, each rank generating and editing only its own
+    (strong scaling; the same code path as the verified c4 12.5M-record side line at N = 1).
+    Whole-job records/s over the max-over-ranks time of K passes."""
+    import torch
+    import torch.distributed as dist
+    total = 100_000_000
+    share = make_share("c4", total, rank, world, seed=1)
+    te, b, r, _, _ = run_workload("c4", share[3], 0, 2, seed=1, device=local, share=share, total=total,
+                                  verify=False)
+    del share
+    k = max(3, min(opt.steps, 20))
+    byt = torch.tensor([r.bytes_in + r.bytes_out, r.packets], dtype=torch.int64, device="cuda")
+    barrier()
+    t0 = time.perf_counter()
+    b.time(k)
+    barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    dist.all_reduce(byt)
+    b.close()
+    te.close()
+    sec = float(el.item()) / k
+    return {"workload": f"{WORKLOADS['c4'][2]} over one {total}-record IMIX capture split into {world} "
+                        "byte-balanced shares (BASELINE configs[3], strong scaling)",
+            "records": int(byt[1].item()), "ms_per_pass": round(sec * 1e3, 4),
+            "mpkt_s": round(int(byt[1].item()) / sec / 1e6, 1),
+            "gbps_algorithmic": round(int(byt[0].item()) / sec / 1e9, 1),
+            "frac_hbm_peak_per_gpu": round(int(byt[0].item()) / sec / 1e9 / world / HBM_PEAK_GBS, 4),
+            "verified": False, "note": "not re-checked here (host memory); the c4 code path is checked at N=1"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,7 +276,10 @@ def main():
                     "(default: the CPUs this process may run on, at most 16 -- the GPU box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
-    ap.add_argument("--verify", action="store_true", help="compare the first run with the oracle")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of every workload's "
+                    "first run (on by default: the bench line is parity evidence)")
+    ap.add_argument("--no-strong-side", action="store_true", help="N > 1: skip the BASELINE configs[3] line "
+                    "(c4, 100M records split over the ranks)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: one --records-record capture split over the ranks (each rank "
                          "generates only its share); c4 defaults to BASELINE configs[3]'s 100M records")
@@ -224,13 +307,20 @@ def main():
         total = opt.records or (100_000_000 if opt.workload == "c4" else DEFAULT_PACKETS[opt.workload])
         share = make_share(opt.workload, total, rank, world, seed=1)
         n = share[3]
-        te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1, device=local,
-                                      share=share, total=total)
+        # verified when the share is small enough for the checker's host memory
+        te, b, r, pcap, checked = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1, device=local,
+                                               share=share, total=total,
+                                               verify=not opt.no_verify and n <= 20_000_000)
         del share
     else:
-        n = opt.packets or DEFAULT_PACKETS[opt.workload]
-        te, b, r, pcap = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank, device=local,
-                                      verify=opt.verify)
+        # N = 1: BASELINE configs[1] (1M x 64 B).  N > 1: every rank weak-scales a
+        # 10M-record shard of the same config (1.6 GB moved per pass, so the curve measures
+        # HBM, not the 256 MiB Infinity Cache a 1M shard sits in; N = 1's c2x10 side line
+        # is the same per-GPU workload)
+        n = opt.packets or (PER_RANK_PACKETS.get(opt.workload, DEFAULT_PACKETS[opt.workload]) if world > 1
+                            else DEFAULT_PACKETS[opt.workload])
+        te, b, r, pcap, checked = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank,
+                                               device=local, verify=not opt.no_verify)
     alg_bytes = r.bytes_in + r.bytes_out  # sum(16+caplen_in) + sum(16+caplen_out) per launch
 
     def barrier():
@@ -273,9 +363,19 @@ def main():
     if os.path.exists(tfile) and not opt.strong:  # (profiled at the config's default size)
         try:
             tj = json.load(open(tfile))
-            traffic = tj.get(opt.workload, {}).get("hbm_bytes_per_launch")
+            tkey = "c2x10" if opt.workload == "c2" and n == DEFAULT_PACKETS["c2x10"] else opt.workload
+            traffic = tj.get(tkey, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    # every rank checked its first run against the oracle (or did not): one flag, one count
+    chk = torch.tensor([checked, 1 if checked else 0], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(chk)
+    if n == DEFAULT_PACKETS[opt.workload] or opt.strong:
+        desc = WORKLOADS[opt.workload][3]
+    else:
+        desc = f"{WORKLOADS[opt.workload][2]} on {n} records per GPU of the {opt.workload} corpus " \
+               f"({'HBM-resident weak-scaling shard; ' if world > 1 else ''}{WORKLOADS[opt.workload][3]})"
     result = {
         "metric": "Mpackets/s device-resident tcpedit rewrite+fixcsum",
         "value": round(value, 3),
@@ -291,7 +391,7 @@ def main():
         "data": "synthetic (tcpreplay_amd.synth, seeded per rank)",
         "config": {"workload": (f"{WORKLOADS[opt.workload][2]} over one {total}-record capture split into "
                                 f"{world} byte-balanced shares (BASELINE configs[3] for c4)")
-                               if opt.strong else WORKLOADS[opt.workload][3], "packets_per_gpu": n,
+                               if opt.strong else desc, "packets_per_gpu": n,
                    "tcpedit_args": WORKLOADS[opt.workload][2], "parallelism": f"shard{world}",
                    "global_records": total if opt.strong else n * world},
         "gbps_algorithmic": round((int(cnt[1].item()) + int(cnt[2].item())) / elapsed / 1e9, 2),
@@ -303,6 +403,9 @@ def main():
                      "kernel_timing": "K back-to-back launches of the kernel alone between two hipEvents"
                                       if single else "a hipEvent pair around the kernel in each of K runs",
                      "alg_bytes_per_launch": alg_bytes},
+        # parity on the bench's clock: each rank's first run == the oracle, byte for byte
+        "verified": int(chk[1].item()) == world,
+        "verified_records": int(chk[0].item()),
     }
     # the per-packet API (tcpedit_packet, as tcprewrite calls it once a record): one 64-byte
     # packet a call through the device (stage, edit, read back), beside the oracle's
@@ -337,6 +440,8 @@ def main():
             result["device_index"] = {"applied": False}
     b.close()
     te.close()
+    if world > 1 and not opt.strong and not opt.no_strong_side:
+        result["strong_c4"] = strong_side(opt, world, rank, local, barrier)
 
     if rank == 0 and world == 1:
         extra = {}
@@ -371,7 +476,7 @@ def main():
                              "cpu_baseline": cpu_prep}
                 continue
             n2 = DEFAULT_PACKETS[wl]
-            te2, b2, r2, _ = run_workload(wl, n2, 0, 3, seed=11, device=0)
+            te2, b2, r2, _, chk2 = run_workload(wl, n2, 0, 3, seed=11, device=0, verify=not opt.no_verify)
             ms2 = b2.time(max(5, opt.steps // 50))
             _, kms2 = b2.time_kernels(max(5, opt.steps // 50))
             ab = r2.bytes_in + r2.bytes_out
@@ -379,7 +484,8 @@ def main():
                          "kernel_ms": round(kms2, 4), "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),
                          "gbps_algorithmic": round(ab / (ms2 * 1e-3) / 1e9, 1),
                          "frac_hbm_peak": round(ab / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "kernel_frac_hbm_peak": round(ab / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                         "kernel_frac_hbm_peak": round(ab / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "verified": chk2 == n2, "verified_records": chk2}
             b2.close()
             te2.close()
         if extra:
@@ -395,6 +501,8 @@ def main():
             te3 = TA.TcpEdit(WORKLOADS[opt.workload][2], device=0)
             src = bytearray(pcap)
             rc3, out3 = te3.rewrite_pipelined(src)  # sizes the device slots
+            if not opt.no_verify:  # the pipelined path's output is the oracle's too
+                check_output_bytes(pcap, WORKLOADS[opt.workload][2], None, out3)
             bound = te3.output_bound(src)
             pin_in, pin_out = TA.PinnedBuffer(len(pcap)), TA.PinnedBuffer(bound)
             pin_in.view[:] = pcap

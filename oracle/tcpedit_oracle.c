@@ -198,8 +198,8 @@ typedef struct {
     uint32_t caplen, len;
 } ohdr_t;
 
-static char g_err[1024];
-static int g_warn_count;
+static __thread char g_err[1024]; /* per thread: a checker runs shards on threads */
+static __thread int g_warn_count;
 
 static void seterr(const char *fmt, ...)
 {
@@ -1991,10 +1991,10 @@ static int encoder_l2len(const ocfg_t *c, const uint8_t *packet, int pktlen)
 /* ------------------------------------------------------------------------- */
 /* fuzzing: src/tcpedit/fuzzing.c:12-297 (state: fuzzing_init's statics)      */
 /* ------------------------------------------------------------------------- */
-static uint32_t g_fuzz_state, g_fuzz_factor; /* fuzz_seed, fuzz_factor (fuzzing.c:8-20) */
+static __thread uint32_t g_fuzz_state, g_fuzz_factor; /* fuzz_seed, fuzz_factor (fuzzing.c:8-20) */
 /* test hooks for a sharded run: the draws the last run made, and draws to skip at the
    start of the next runs (a shard's stream starts after the earlier shards' draws) */
-static uint64_t g_fuzz_draws, g_fuzz_skip;
+static __thread uint64_t g_fuzz_draws, g_fuzz_skip;
 
 /* the encoder's proto function on the edited packet (plugin_proto): en10mb.c:741-762,
    user.c:273-282 (always an error), hdlc.c:299-311 (the protocol field) */
@@ -3120,9 +3120,14 @@ static inline uint32_t bswap32_(uint32_t v) { return __builtin_bswap32(v); }
 
 /* Returns 0 on success, -1 on a hard error (output holds the packets written
  * before it, as tcprewrite's exit(-1) leaves it), -2 on bad input/options. */
-int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, size_t cache_len, int argc,
-                       const char **argv, uint8_t *out, size_t out_cap, size_t *out_len, int8_t *pkt_status,
-                       uint64_t max_status, char *errbuf, int errlen)
+/* oracle_rewrite_mem over a shard of a capture: `in` holds the file header and a run of
+ * whole records whose first is record pkt_base (0-based) of the whole capture, so the
+ * tcpprep cache is read at global record numbers (a checker splits a capture of
+ * independent records over threads this way; --fuzz-seed and stale reads (Q8) carry
+ * state across records and must run unsplit). */
+int oracle_rewrite_mem_base(const uint8_t *in, size_t in_len, const uint8_t *cache, size_t cache_len, int argc,
+                            const char **argv, uint8_t *out, size_t out_cap, size_t *out_len, int8_t *pkt_status,
+                            uint64_t max_status, char *errbuf, int errlen, uint64_t pkt_base)
 {
     oopts_t *o = calloc(1, sizeof(oopts_t));
     ocfg_t c;
@@ -3245,7 +3250,7 @@ int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, s
         ip_ += 16 + caplen;
         int dir = DIR_C2S;
         if (cdata)
-            dir = check_cache(cdata, cdata_len, packetnum);
+            dir = check_cache(cdata, cdata_len, pkt_base + packetnum);
         ohdr_t h = {caplen, len};
         int prc = 0, warned = 0;
         if (dir != DIR_NOSEND) {
@@ -3285,6 +3290,14 @@ out:
     return rc;
 }
 
+int oracle_rewrite_mem(const uint8_t *in, size_t in_len, const uint8_t *cache, size_t cache_len, int argc,
+                       const char **argv, uint8_t *out, size_t out_cap, size_t *out_len, int8_t *pkt_status,
+                       uint64_t max_status, char *errbuf, int errlen)
+{
+    return oracle_rewrite_mem_base(in, in_len, cache, cache_len, argc, argv, out, out_cap, out_len, pkt_status,
+                                   max_status, errbuf, errlen, 0);
+}
+
 int oracle_warn_count(void) { return g_warn_count; }
 
 /* Exposed for tests: the seed/sequence mixer (parse_args.c:214-230). */
@@ -3296,4 +3309,41 @@ uint32_t oracle_mix_seed(uint32_t seed)
     for (int i = 0; i < 5; ++i)
         tcpr_random(&seed);
     return seed;
+}
+
+/* Checker helper: cut a capture's records into `parts` byte-balanced runs of whole
+ * records (libpcap's stop rules end the walk).  cuts[k] = file offset where run k starts,
+ * first[k] = its first record (0-based); cuts[parts] = end of the last whole record.
+ * Returns the records walked. */
+uint64_t oracle_shard_cuts(const uint8_t *in, size_t in_len, int parts, uint64_t *cuts, uint64_t *first)
+{
+    uint32_t magic = 0;
+    if (in_len >= 4)
+        memcpy(&magic, in, 4);
+    const int swap = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
+    size_t pos = 24, target = in_len > 24 ? (in_len - 24) / (size_t)parts : 0;
+    uint64_t n = 0;
+    int k = 1;
+    cuts[0] = 24;
+    first[0] = 0;
+    while (pos + 16 <= in_len) {
+        while (k < parts && pos >= 24 + target * (size_t)k) {
+            cuts[k] = pos;
+            first[k] = n;
+            k++;
+        }
+        uint32_t caplen;
+        memcpy(&caplen, in + pos + 8, 4);
+        if (swap)
+            caplen = bswap32_(caplen);
+        if (caplen > MAX_SNAPLEN || pos + 16 + caplen > in_len)
+            break;
+        pos += 16 + caplen;
+        n++;
+    }
+    for (; k <= parts; k++) {
+        cuts[k] = pos;
+        first[k] = n;
+    }
+    return n;
 }

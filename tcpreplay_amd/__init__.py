@@ -85,6 +85,8 @@ def load():
         "tcpedit_batch_index_device": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_fuzz_reach": (ctypes.c_int64, [vp, vp]),
         "tcpedit_fuzz_skip": (c_int, [vp, u64]),
+        "tcpedit_batch_l2carry_out": (c_int, [vp, vp]),
+        "tcpedit_set_l2carry": (c_int, [vp, c_int]),
         "tcpedit_batch_device_output": (vp, [vp]),
         "tcpedit_batch_input_bytes": (u64, [vp]),
         "tcpedit_rewrite_pcap": (c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
@@ -227,6 +229,12 @@ class TcpEdit:
         if self._L.tcpedit_fuzz_skip(self._ctx, int(draws)) < 0:
             raise RuntimeError(self.geterr())
 
+    def set_l2carry(self, value: int):
+        """seed the en10mb encoder's dst_modified carry as an earlier shard
+        left it (tcpedit_set_l2carry)"""
+        if self._L.tcpedit_set_l2carry(self._ctx, int(value)) < 0:
+            raise RuntimeError(self.geterr())
+
     def packet(self, hdr, data: bytearray, direction=TCPR_DIR_C2S):
         """tcpedit_packet(): edits `data` (bytearray, >= MAXPACKET bytes recommended) in place.
 
@@ -274,6 +282,14 @@ class Batch:
         n = self._L.tcpedit_batch_output(self._b, out, r.out_len)
         return out.raw[:n]
 
+    def output_np(self):
+        """the output image as a numpy uint8 array (one D2H copy, no intermediate bytes)"""
+        import numpy as np
+        r = self.result()
+        out = np.empty(max(1, r.out_len), np.uint8)
+        n = self._L.tcpedit_batch_output(self._b, out.ctypes.data, r.out_len)
+        return out[:n]
+
     def output_records_into(self, dst) -> int:
         """D2H of the output records (no file header) straight into the writable buffer
         `dst` (a bytearray, or an mmap of the job's output file at this shard's offset);
@@ -297,6 +313,14 @@ class Batch:
         if n < 0:
             raise RuntimeError(self._te.geterr())
         return int(n)
+
+    def l2carry_out(self) -> int:
+        """the dst_modified value this batch's last writer leaves (0/1), or 2 when no record
+        writes it (tcpedit_batch_l2carry_out)"""
+        v = self._L.tcpedit_batch_l2carry_out(self._te._ctx, self._b)
+        if v < 0:
+            raise RuntimeError(self._te.geterr())
+        return int(v)
 
     def time(self, iters):
         ms = ctypes.c_double()

@@ -9,14 +9,16 @@
  *                     section (its interfaces replace the earlier ones)
  *   IDB (1)           linktype, snaplen, if_tsresol (option 9), if_tsoffset (option 14)
  *   EPB (6)           interface, 64-bit timestamp, captured / original length, data
- *   SPB (3)           original length; captured = min(original, interface 0's snaplen)
+ *   SPB (3)           original length; captured = min(original, the snapshot length)
  *   OPB (2, obsolete) interface (16 bits), drops, timestamp, lengths, data
  *   others            skipped (name resolution, statistics, secrets, custom blocks)
  *
  * Timestamps are converted to seconds and microseconds as libpcap does: units per second
  * from if_tsresol (10^n, or 2^n with the high bit), if_tsoffset added to the seconds, the
  * fraction scaled to microseconds (truncating).  Every interface must have the first
- * one's link type (libpcap refuses a file that mixes them).
+ * one's link type (libpcap refuses a file that mixes them).  The capture's snapshot
+ * length is the first interface's snaplen (0, or more than 262144, meaning 262144, as
+ * pcap_adjust_snapshot has it), and a record's captured length is cut to it.
  * Parity is unpinned: the reference holds no pcapng fixture; tests/test_pcapng.py checks
  * the conversion against the classic capture a pcapng file was written from.
  */
@@ -135,7 +137,7 @@ int te_pcapng_to_pcap(const uint8_t *in, size_t len, uint8_t **out_img, size_t *
         return ng_err(err, errlen, "out of host memory");
     }
     int nif = 0, sw = 0;
-    uint32_t linktype = 0, snaplen = 0;
+    uint32_t linktype = 0, snaplen = 0, snapshot = 262144u;
     int have_link = 0;
     size_t p = 0;
     while (p + 12 <= len) {
@@ -166,6 +168,8 @@ int te_pcapng_to_pcap(const uint8_t *in, size_t len, uint8_t **out_img, size_t *
             if (!have_link) {
                 linktype = f.linktype;
                 snaplen = f.snaplen;
+                /* pcap_adjust_snapshot: 0 or more than the maximum means the maximum */
+                snapshot = (snaplen == 0 || snaplen > 262144u) ? 262144u : snaplen;
                 have_link = 1;
             } else if (f.linktype != linktype) {
                 free(out);
@@ -179,18 +183,19 @@ int te_pcapng_to_pcap(const uint8_t *in, size_t len, uint8_t **out_img, size_t *
             const uint32_t ifn = type == 6 ? ng32(b, sw) : ng16(b, sw);
             const uint64_t ts = (uint64_t)ng32(b + 4, sw) << 32 | ng32(b + 8, sw);
             const uint32_t cl = ng32(b + 12, sw), ol = ng32(b + 16, sw);
-            if ((int)ifn >= nif || b + 20 + cl > bend)
+            /* unsigned compares: an interface id or length read from the file never indexes
+               or reaches past what the block holds */
+            if (ifn >= (uint32_t)nif || (size_t)cl > (size_t)(bend - (b + 20)))
                 goto bad;
-            if (ng_put(&out, &n, &cap, &ifs[ifn], ts, cl, ol, b + 20) < 0)
+            /* libpcap's reader cuts a record to the capture's snapshot length */
+            if (ng_put(&out, &n, &cap, &ifs[ifn], ts, cl > snapshot ? snapshot : cl, ol, b + 20) < 0)
                 goto oom;
         } else if (type == 3) { /* SPB: interface 0, no timestamp */
             if (b + 4 > bend || nif < 1)
                 goto bad;
             const uint32_t ol = ng32(b, sw);
-            uint32_t cl = ol;
-            if (ifs[0].snaplen && cl > ifs[0].snaplen)
-                cl = ifs[0].snaplen;
-            if (b + 4 + cl > bend)
+            uint32_t cl = ol > snapshot ? snapshot : ol;
+            if ((size_t)cl > (size_t)(bend - (b + 4)))
                 cl = (uint32_t)(bend - (b + 4));
             if (ng_put(&out, &n, &cap, &ifs[0], 0, cl, ol, b + 4) < 0)
                 goto oom;

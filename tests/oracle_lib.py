@@ -136,3 +136,71 @@ def replay(pcap: bytes, args):
     if n < 0:
         raise ValueError(f"tcpreplay oracle failed ({n}) for {args}")
     return out.raw[:n], int(failed.value)
+
+
+def check_rewrite(pcap, args, cache, dev_out, threads=16, sharded=True, pkt_base=0):
+    """The checker bench.py runs outside its timed region: the oracle's tcprewrite output
+    for (pcap, args, cache) must equal `dev_out` (the device's output image, any
+    bytes-like object) byte for byte.  With `sharded` the records are cut into `threads`
+    byte-balanced runs, each rewritten by the oracle on its own thread at its global record
+    number (oracle_rewrite_mem_base); only valid when records are independent (no
+    --fuzz-seed, no stale static-buffer reads).  `pkt_base`: the capture's first record is
+    record pkt_base of the job (a shard), for the tcpprep cache lookups.  Returns the records checked; raises
+    AssertionError naming the first differing run."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib = load()
+    fn = lib.oracle_rewrite_mem_base
+    fn.restype = ctypes.c_int
+    fn.argtypes = lib.oracle_rewrite_mem.argtypes + [ctypes.c_uint64]
+    cutf = lib.oracle_shard_cuts
+    cutf.restype = ctypes.c_uint64
+    cutf.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    src = np.frombuffer(pcap, np.uint8)
+    dev = np.frombuffer(dev_out, np.uint8)
+    parts = max(1, int(threads)) if sharded else 1
+    cuts = np.zeros(parts + 1, np.uint64)
+    first = np.zeros(parts + 1, np.uint64)
+    nrec = int(cutf(src.ctypes.data, src.size, parts, cuts.ctypes.data, first.ctypes.data))
+    argv = (ctypes.c_char_p * max(1, len(args)))(*[a.encode() for a in args])
+    cbuf = np.frombuffer(cache, np.uint8) if cache else None
+    hdr = src[:24]
+
+    def one(k):
+        a, b = int(cuts[k]), int(cuts[k + 1])
+        if b <= a and k > 0:
+            return k, 0, None, None
+        if parts == 1:  # the whole capture, trailing bytes and all
+            shard = src
+        else:
+            shard = np.empty(24 + b - a, np.uint8)
+            shard[:24] = hdr
+            shard[24:] = src[a:b]
+        cap = 2 * shard.size + 1024 + 262144
+        out = np.empty(cap, np.uint8)
+        olen = ctypes.c_size_t(0)
+        err = ctypes.create_string_buffer(1024)
+        rc = fn(shard.ctypes.data, shard.size, cbuf.ctypes.data if cbuf is not None else None,
+                cbuf.size if cbuf is not None else 0, len(args), argv, out.ctypes.data, cap, ctypes.byref(olen),
+                None, 0, err, 1024, int(pkt_base) + int(first[k]))
+        return k, rc, out[:olen.value], err.value.decode(errors="replace")
+
+    pos = 24
+    with ThreadPoolExecutor(max_workers=parts) as ex:
+        for k, rc, out, err in ex.map(one, range(parts)):
+            if out is None:
+                continue
+            if rc != 0:
+                raise AssertionError(f"oracle run {k} failed rc={rc}: {err}")
+            if k == 0 and bytes(dev[:24]) != bytes(out[:24]):
+                raise AssertionError("output file header differs from the oracle's")
+            body = out[24:]
+            seg = dev[pos:pos + body.size]
+            if seg.size != body.size or not np.array_equal(seg, body):
+                bad = np.flatnonzero(seg != body[:seg.size])
+                where = int(bad[0]) if bad.size else min(seg.size, body.size)
+                raise AssertionError(f"device output differs from the oracle in run {k} (records from "
+                                     f"{int(first[k])}): output byte {pos + where}")
+            pos += body.size
+    if pos != dev.size:
+        raise AssertionError(f"device output is {dev.size} bytes, the oracle's {pos}")
+    return nrec

@@ -5,7 +5,7 @@
  * call is made: nothing here needs a GPU.
  *
  *   san_driver <cases file> <pcap>...
- * cases file: one case a line, tab-separated fields: a tool (rewrite | prep | replay | re)
+ * cases file: one case a line, tab-separated fields: a tool (rewrite | prep | replay | re | ng)
  * then its arguments.
  */
 #include <stdint.h>
@@ -124,6 +124,15 @@ int main(int argc, char **argv)
             }
         } else if (!strcmp(av[0], "re") && ac >= 3) {
             tcpprep_regex_dfa_match(av[1], av[2]);
+        } else if (!strcmp(av[0], "ng") && ac >= 2) { /* a pcapng file through the converter */
+            size_t nl = 0;
+            uint8_t *ng = slurp(av[1], &nl);
+            void *cl = NULL;
+            size_t cn = 0;
+            if (ng && tcpedit_pcapng_to_pcap(ng, nl, &cl, &cn) == 0)
+                walked += cn > 24;
+            free(cl);
+            free(ng);
         }
     }
     fclose(cf);

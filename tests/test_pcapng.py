@@ -126,3 +126,38 @@ def test_gpu_rewrites_pcapng_as_the_classic_capture(built, args):
         assert rc == 0 and out == exp
     finally:
         te.close()
+
+
+@pytest.mark.parametrize("ifn", [1, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF])
+def test_epb_interface_id_out_of_range_is_refused(built, ifn):
+    """an EPB naming an interface the section never described is a malformed block (the id
+    is compared unsigned: 0x80000000 and up must not pass as negative)"""
+    e = "<"
+    out = _block(e, 0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+    out += _block(e, 1, struct.pack(e + "HHI", 1, 0, 65535))
+    out += _block(e, 6, struct.pack(e + "IIIII", ifn, 0, 0, 60, 60) + bytes(60))
+    assert _convert(out) is None
+
+
+def test_epb_captured_length_past_the_block_is_refused(built):
+    e = "<"
+    out = _block(e, 0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+    out += _block(e, 1, struct.pack(e + "HHI", 1, 0, 65535))
+    out += _block(e, 6, struct.pack(e + "IIIII", 0, 0, 0, 0xFFFFFFF0, 60) + bytes(60))
+    assert _convert(out) is None
+
+
+@pytest.mark.parametrize("snaplen,want", [(100, 100), (0, 1514), (1 << 20, 1514)])
+def test_records_are_cut_to_the_snapshot_length(built, snaplen, want):
+    """libpcap's pcap-ng reader cuts a record whose captured length exceeds the capture's
+    snapshot length (the first IDB's snaplen; 0 or more than 262144 meaning 262144) to it.
+    Stated from libpcap's behaviour; parity unpinned (no reference pcapng fixture)."""
+    recs = S.records(S.pcap_fixed(5, 1514, seed=4))
+    e = "<"
+    out = _block(e, 0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+    out += _block(e, 1, struct.pack(e + "HHI", 1, 0, snaplen))
+    for ts, tu, cl, ln, d in recs:
+        out += _block(e, 6, struct.pack(e + "IIIII", 0, 0, 0, cl, ln) + d)
+    got = S.records(_convert(out))
+    assert [(r[2], r[3]) for r in got] == [(want, 1514)] * 5
+    assert [r[4] for r in got] == [d[:want] for *_, d in recs]

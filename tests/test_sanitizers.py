@@ -16,7 +16,29 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SAN = os.path.join(HERE, "sanitize")
 
 
-def _cases(path):
+def _pcapng_files(tmp):
+    """pcapng images for the converter: good ones and malformed blocks (interface ids past
+    the described interfaces, including ones negative as an int, captured lengths past the
+    block, truncation)"""
+    import struct
+    import test_pcapng as N
+    e = "<"
+    shb = N._block(e, 0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+    idb = N._block(e, 1, struct.pack(e + "HHI", 1, 0, 100))
+    imgs = [N.to_pcapng(G.read("test.pcap")), N.to_pcapng(G.read("test.pcap"), ">", 9, 7, "opb")]
+    for ifn, cl in [(1, 60), (0x80000000, 60), (0xFFFFFFFF, 60), (0, 0xFFFFFFF0), (0, 0x7FFFFFFF), (0, 200)]:
+        imgs.append(shb + idb + N._block(e, 6, struct.pack(e + "IIIII", ifn, 0, 0, cl, 60) + bytes(60)))
+    imgs.append(imgs[0][:-7])
+    paths = []
+    for k, img in enumerate(imgs):
+        p = os.path.join(tmp, f"ng{k}.pcapng")
+        with open(p, "wb") as f:
+            f.write(img)
+        paths.append(p)
+    return paths
+
+
+def _cases(path, ng_paths=()):
     import test_gpu_parity as P
     lines = [["rewrite"] + a for a in P.OPTION_POOL]
     lines += [["rewrite", "--bogus"], ["rewrite", "--pnat=not-a-cidr"], ["rewrite", "--portmap=70000:1"],
@@ -28,6 +50,7 @@ def _cases(path):
               "[^0-9.:]", "a{64}", "((1|2)+3?)*$"]:
         for s_ in ["96.17.211.1", "::ffff:1.2.3.4", "2001:db8::1", "0.0.0.0", ""]:
             lines.append(["re", r, s_ or "1"])
+    lines += [["ng", p] for p in ng_paths]
     with open(path, "w") as f:
         for ln in lines:
             f.write("\t".join(ln) + "\n")
@@ -63,7 +86,7 @@ def drivers(built):
 @pytest.mark.parametrize("kind", ["asan", "tsan"])
 def test_host_code_is_clean_under_the_sanitizers(drivers, tmp_path, kind):
     cases = str(tmp_path / "cases.tsv")
-    _cases(cases)
+    _cases(cases, _pcapng_files(str(tmp_path)))
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1",
                TCPEDIT_HIP_WALK_THREADS="8")
