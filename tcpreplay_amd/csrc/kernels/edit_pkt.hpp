@@ -275,11 +275,9 @@ DI u32 fold16(unsigned long long s) {
 }
 
 // sum of `len` bytes at p, weights relative to p (even offset -> low byte).
-// The dword body takes eight loads per step, all in flight before the first add (one
-// lane sums a whole packet, so a dependent load per dword left the LDS latency exposed
-// on every 4 bytes of a 1500-byte payload); each dword adds as its two 16-bit words
-// (v_sad_u16), which folds to the same one's-complement value as the dword sum
-// (2^16 == 1 mod 0xffff, and both sums are 0 only for all-zero bytes).
+// Each dword adds as its two 16-bit words (v_sad_u16), which folds to the same
+// one's-complement value as the dword sum (2^16 == 1 mod 0xffff, and both sums are 0 only
+// for all-zero bytes).
 DI u32 wsum_acc16(u32 x, u32 acc) {
 #ifdef TE_HOST_EMU
     return acc + (x & 0xffffu) + (x >> 16);
@@ -287,34 +285,64 @@ DI u32 wsum_acc16(u32 x, u32 acc) {
     return __builtin_amdgcn_sad_u16(x, 0u, acc);
 #endif
 }
-DI u32 csum_bytes(const u8 *p, int len) {
+// mask of bytes [lo, hi) of a dword, lo and hi clamped to [0, 4]
+DI u32 dmask(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    const u32 mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+    const u32 ml = lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+    return mh & ~ml;
+}
+#ifdef TE_HOST_EMU
+DI u32 csum_bytes(const u8 *p, int len) {  // (host debugging harness: byte loop)
     if (len <= 0) return 0;
-    uintptr_t a = (uintptr_t)p;
-    const u8 *b = p;
+    const uintptr_t a = (uintptr_t)p;
     unsigned long long s = 0;
-    int i = 0;
-    // head: bytes until 4-aligned (absolute weights)
-    while (i < len && ((a + i) & 3)) {
-        s += (u32)b[i] << (8 * ((a + i) & 1));
-        ++i;
-    }
-    const u32 *w = (const u32 *)(b + i);
-    const int nw = (len - i) >> 2;
-    int k = 0;
-    for (; k + 8 <= nw; k += 8) {  // <= 8 dwords x 0x1fffe per step: no u32 overflow
-        const u32 x0 = w[k], x1 = w[k + 1], x2 = w[k + 2], x3 = w[k + 3];
-        const u32 x4 = w[k + 4], x5 = w[k + 5], x6 = w[k + 6], x7 = w[k + 7];
-        u32 acc = wsum_acc16(x0, wsum_acc16(x1, wsum_acc16(x2, wsum_acc16(x3, 0u))));
-        acc = wsum_acc16(x4, wsum_acc16(x5, wsum_acc16(x6, wsum_acc16(x7, acc))));
-        s += acc;
-    }
-    for (; k < nw; ++k) s += w[k];
-    i += nw << 2;
-    for (; i < len; ++i) s += (u32)b[i] << (8 * ((a + i) & 1));
+    for (int i = 0; i < len; ++i) s += (u32)p[i] << (8 * ((a + i) & 1));
     u32 f = fold16(s);
-    if (a & 1) f = ((f >> 8) | (f << 8)) & 0xffff;  // absolute -> relative weights
+    if (a & 1) f = ((f >> 8) | (f << 8)) & 0xffff;
     return f;
 }
+#else
+// The bytes are read as whole aligned 16-byte quads: the quad holding p, every quad up to
+// the one holding p + len - 1, and no other.  Each load therefore lies inside the aligned
+// 16-byte granule of a byte the packet owns -- it cannot cross a page, or reach past the
+// end (or before the start) of the LDS tile or HBM scratch slot by more than that
+// granule's other bytes -- and the first and last quads' bytes outside [p, p + len) are
+// masked off.  (A 16-byte-load variant that read quads past the last one holding a packet
+// byte is the one the round-2 notes record as faulting in the fast-lane tests; every load
+// here is bounded by construction, and tests/test_gpu_parity.py puts huge records flush
+// against the end of the image, the scratch slot and the output.)  One lane sums a whole
+// packet, so the middle quads go four at a time, all in flight before the first add.
+DI uint32_t quad_sum(const uint4 v, uint32_t acc) {
+    return wsum_acc16(v.x, wsum_acc16(v.y, wsum_acc16(v.z, wsum_acc16(v.w, acc))));
+}
+DI uint32_t quad_sum_masked(const uint4 v, int off, int lo, int hi, uint32_t acc) {
+    // bytes [lo, hi) of the quad run, quad byte 0 at run offset `off`
+    return wsum_acc16(v.x & dmask(lo - off, hi - off),
+                      wsum_acc16(v.y & dmask(lo - off - 4, hi - off - 4),
+                                 wsum_acc16(v.z & dmask(lo - off - 8, hi - off - 8),
+                                            wsum_acc16(v.w & dmask(lo - off - 12, hi - off - 12), acc))));
+}
+DI u32 csum_bytes(const u8 *p, int len) {
+    if (len <= 0) return 0;
+    const int h = (int)((uintptr_t)p & 15u);  // p's byte within its quad
+    const uint4 *Q = (const uint4 *)(p - h);   // (same granule as p: pointer arithmetic keeps the address space)
+    const int hi = h + len;                    // run offsets [h, hi) are the packet's
+    const int nq = (hi + 15) >> 4;             // quads 0 .. nq - 1
+    unsigned long long s = quad_sum_masked(Q[0], 0, h, hi, 0u);
+    int k = 1;
+    for (; k + 4 <= nq - 1; k += 4) {  // 16 dwords x 0x1fffe: no u32 overflow
+        const uint4 v0 = Q[k], v1 = Q[k + 1], v2 = Q[k + 2], v3 = Q[k + 3];
+        s += quad_sum(v0, quad_sum(v1, quad_sum(v2, quad_sum(v3, 0u))));
+    }
+    for (; k < nq - 1; ++k) s += quad_sum(Q[k], 0u);
+    if (nq > 1) s += quad_sum_masked(Q[nq - 1], 16 * (nq - 1), h, hi, 0u);
+    u32 f = fold16(s);
+    if (h & 1) f = ((f >> 8) | (f << 8)) & 0xffff;  // absolute -> relative weights
+    return f;
+}
+#endif
 
 // CHECKSUM_CARRY (checksum.h:25) applied to a plain non-negative sum
 DI u16 csum_carry(unsigned long long x) { return (u16)(~fold16(x) & 0xffff); }

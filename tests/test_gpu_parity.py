@@ -214,6 +214,26 @@ def test_huge_records_use_the_hbm_slot_path(built, args):
     assert_same(out, exp)
 
 
+@pytest.mark.parametrize("args", [["--fixcsum"], ["--mtu-trunc", "--mtu=262000", "--fixcsum"],
+                                  ["--enet-subsmac=00:11:22:33:44:55,00:aa:bb:cc:dd:ee", "--fixcsum"],
+                                  ["--fuzz-seed=3", "--fuzz-factor=1", "--fixcsum"]])
+def test_checksum_reads_flush_against_buffer_ends(built, args):
+    """csum_bytes reads whole aligned 16-byte quads: each holds at least one of the packet's
+    bytes, so no read leaves the granule of a byte it owns.  Records placed flush against
+    the end of every buffer the generic lane sums in -- the input image (last record ends
+    the capture, at every residue mod 16), a huge record's HBM scratch slot (> 36 KiB
+    records, odd sizes, IPv4 and IPv6) and the last LDS tile -- must equal the oracle."""
+    for tail, v6, proto in [(100_001, True, 17), (100_013, False, 6), (65_535, True, 6), (262_143, False, 17),
+                            (1_514, False, 17), (1_513, True, 6), (61, False, 17), (77, False, 6), (95, True, 17)]:
+        recs = S.records(S.pcap_imix(300, seed=tail % 97))
+        recs += S.records(S.pcap_fixed(1, tail, seed=tail % 13, ipv6=v6, proto=proto))
+        pcap = S.build_pcap(recs)
+        rc_o, exp = O.rewrite(pcap, args)
+        rc, out = gpu_rewrite(pcap, args)
+        assert rc == rc_o == 0, (tail, args)
+        assert_same(out, exp)
+
+
 def test_nanosecond_capture_is_written_in_microseconds(built):
     p = bytearray(G.read("test.pcap"))
     p[0:4] = struct.pack("<I", 0xA1B23C4D)
