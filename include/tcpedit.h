@@ -281,6 +281,14 @@ int tcpedit_pcapng_to_pcap(const void *in, size_t len, void **out, size_t *out_l
  * shard, fuzzing.c:12-20). */
 int64_t tcpedit_batch_fuzz_reach(tcpedit_t *tcpedit, tcpedit_batch_t *b);
 int tcpedit_fuzz_skip(tcpedit_t *tcpedit, uint64_t draws);
+/* The en10mb encoder's dst_modified across shards (a cooked, Juniper or 802.11
+ * decoder into en10mb without --enet-dmac; en10mb.c:597,612-615 set it on C2S records and
+ * S2C records keep it, so a shard's first records read what an earlier shard left).
+ * tcpedit_batch_l2carry_out: the value the batch's last writer leaves (0 or 1), or 2 when
+ * no record of it writes (or the config has no carry); found on the device before any edit.
+ * tcpedit_set_l2carry: seed the context with the nearest earlier shard's value. */
+int tcpedit_batch_l2carry_out(tcpedit_t *tcpedit, tcpedit_batch_t *b);
+int tcpedit_set_l2carry(tcpedit_t *tcpedit, int value);
 /* device pointers, for callers that keep the data in HBM (e.g. a sender) */
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b);
 uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b);

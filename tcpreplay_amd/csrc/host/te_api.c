@@ -233,8 +233,10 @@ static uint32_t rd32(const uint8_t *p, int swapped)
  * `stop_at` (the next stretch's first record), the bytes run out, or libpcap stops.
  * Tile first_pkt and scratch_off are relative to the stretch. */
 typedef struct {
-    /* the cut (same for every stretch) */
-    const uint8_t *img;
+    /* the cut (same for every stretch).  Offsets are file offsets: record bytes at file
+       offset o (o >= 24) are recs[o - 24], so no pointer before the caller's records is
+       ever formed (a shard's records may start its buffer) */
+    const uint8_t *recs;
     size_t len;
     int swapped, pad, slot_mode, grow_fast, wave;
     uint32_t budget, max_pkts;
@@ -268,7 +270,7 @@ static int walk_grow(void **arr, uint64_t *cap, size_t elem, int fixed)
 
 static void walk_range(te_walk_t *w)
 {
-    const uint8_t *img = w->img;
+    const uint8_t *recs = w->recs;
     const size_t len = w->len;
     size_t off = w->start;
     te_tile_t cur;
@@ -289,8 +291,8 @@ static void walk_range(te_walk_t *w)
     size_t pf = off;
     while (off + 16 <= len && off < w->stop_at) {
         for (const size_t pf_end = off + 4096 < len ? off + 4096 : len; pf < pf_end; pf += 64)
-            __builtin_prefetch(img + pf);
-        uint32_t caplen = rd32(img + off + 8, w->swapped), plen = rd32(img + off + 12, w->swapped);
+            __builtin_prefetch(recs + (pf - 24));
+        uint32_t caplen = rd32(recs + (off - 24) + 8, w->swapped), plen = rd32(recs + (off - 24) + 12, w->swapped);
         if (caplen > 262144u) { /* libpcap stops at an oversize record ... */
             w->walk_stop = 1;
             break;
@@ -431,13 +433,13 @@ static int balance_tiles(tcpedit_batch_t *b, uint32_t waves, uint32_t budget, ui
 
 /* a plausible record chain at p: `n` consecutive headers within the image whose
    lengths libpcap would accept and whose microsecond/nanosecond field is in range */
-static int chain_plausible(const uint8_t *img, size_t len, size_t p, int swapped, int nsec, int n)
+static int chain_plausible(const uint8_t *recs, size_t len, size_t p, int swapped, int nsec, int n)
 {
     for (int i = 0; i < n; i++) {
         if (p + 16 > len)
             return i > 0;
-        const uint32_t frac = rd32(img + p + 4, swapped), cl = rd32(img + p + 8, swapped),
-                       pl = rd32(img + p + 12, swapped);
+        const uint8_t *h = recs + (p - 24); /* (file offset p >= 24) */
+        const uint32_t frac = rd32(h + 4, swapped), cl = rd32(h + 8, swapped), pl = rd32(h + 12, swapped);
         if (cl > 262144u || pl > 262144u || frac >= (nsec ? 1000000000u : 1000000u) || p + 16 + cl > len)
             return 0;
         p += 16 + cl;
@@ -542,7 +544,7 @@ static void pool_wait(int *pending)
  * From the first stretch that does not, the walk goes on sequentially, so the index is
  * the sequential walk's records whatever the guesses (the tile cut may differ: any cut
  * is valid). */
-static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, const uint8_t *img, size_t len)
+static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, const uint8_t *recs, size_t len)
 {
     if (len < 24) {
         te_seterr(t, "pcap image too short");
@@ -562,7 +564,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     b->linktype = te_linktype_dlt(rd32(hdr + 20, b->swapped) & 0x03ffffffu);
     te_walk_t proto;
     memset(&proto, 0, sizeof(proto));
-    proto.img = img;
+    proto.recs = recs;
     proto.len = len;
     proto.swapped = b->swapped;
     proto.pad = t->cfg.fixlen == TE_FIXLEN_PAD;
@@ -621,7 +623,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         const size_t s0 = 24 + (len - 24) / parts * i, lim = s0 + (1u << 20) < len ? s0 + (1u << 20) : len;
         size_t p = s0 > q[np - 1] ? s0 : q[np - 1] + 1;
         for (; p + 16 <= lim; p++)
-            if (chain_plausible(img, len, p, b->swapped, b->nsec, 8))
+            if (chain_plausible(recs, len, p, b->swapped, b->nsec, 8))
                 break;
         if (p + 16 <= lim)
             q[np++] = p;
@@ -966,9 +968,9 @@ static tcpedit_batch_t *batch_open(tcpedit_t *t, const uint8_t *hdr, const uint8
     }
     b->ctx = t;
     b->pkt_base = pkt_base;
-    /* index_image walks img[24, len): img is positioned so img + 24 is the first record
-       (its first 24 bytes are never read; the header comes from hdr) */
-    if (index_image(t, b, hdr, seg - 24, len) < 0)
+    /* index_image walks file offsets [24, len) of hdr + seg (the header from hdr, the
+       records from seg) */
+    if (index_image(t, b, hdr, seg, len) < 0)
         goto fail;
     if (b->linktype != (uint32_t)t->dlt) {
         te_seterr(t, "pcap linktype %u does not match the context DLT %d", b->linktype, t->dlt);
@@ -1422,6 +1424,64 @@ fail:
     return TCPEDIT_ERROR;
 }
 
+/* SURVEY Q18 across shards: the dst_modified value the batch's last C2S writer leaves (0
+ * or 1), or 2 when no record of the batch writes it (the carry passes through unchanged)
+ * -- found by the carry's own mark + scan, before any edit, so that the ranks of a sharded
+ * job can exchange it and each seed its context with the nearest earlier shard's value
+ * (tcpedit_set_l2carry).  2 as well for a config without the carry. */
+int tcpedit_batch_l2carry_out(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    if (!t || !b)
+        return TCPEDIT_ERROR;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (!t->cfg.l2carry || !b->n_pkts)
+        return 2;
+    te_launch_t L;
+    memset(&L, 0, sizeof(L));
+    L.cfg = t->d_cfg;
+    L.cfg_host = &t->cfg;
+    L.dirbits = b->d_dirbits;
+    L.dirbits_len = b->dirbits_len;
+    L.pkt_base = b->pkt_base;
+    L.fixed_dir = -1;
+    L.in = b->d_in;
+    L.tiles = b->d_tiles;
+    L.pkt_rel = b->d_pkt_rel;
+    L.n_tiles = (uint32_t)b->n_tiles;
+    L.in_swapped = (uint32_t)b->swapped;
+    L.in_nsec = (uint32_t)b->nsec;
+    if (l2carry_bufs(t, b, &L) < 0)
+        return TCPEDIT_ERROR;
+    if (te_launch_l2carry(&L, t->stream) != 0) {
+        te_seterr(t, "dst_modified carry launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return TCPEDIT_ERROR;
+    }
+    uint64_t last = 0;
+    HIPCHK(t, hipMemcpyAsync(&last, L.l2carry + b->n_pkts, sizeof(last), hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return (last >> 1) ? (int)(last & 1u) : 2; /* position 0 is the context's own word */
+fail:
+    return TCPEDIT_ERROR;
+}
+
+/* seed the context's dst_modified carry as an earlier shard left it */
+int tcpedit_set_l2carry(tcpedit_t *t, int value)
+{
+    if (!t || value < 0 || value > 1)
+        return TCPEDIT_ERROR;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (!t->d_l2word)
+        HIPCHK(t, hipMalloc((void **)&t->d_l2word, sizeof(uint32_t)));
+    const uint32_t w = (uint32_t)value;
+    HIPCHK(t, hipMemcpyAsync(t->d_l2word, &w, sizeof(w), hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
 int tcpedit_fuzz_skip(tcpedit_t *t, uint64_t draws)
 {
     if (!t)
@@ -1567,7 +1627,7 @@ int tcpedit_debug_index_host(tcpedit_t *t, const void *pcap, size_t len, uint64_
     if (!b)
         return TCPEDIT_ERROR;
     b->ctx = t;
-    const int rc = index_image(t, b, (const uint8_t *)pcap, (const uint8_t *)pcap, len);
+    const int rc = index_image(t, b, (const uint8_t *)pcap, (const uint8_t *)pcap + (len >= 24 ? 24 : 0), len);
     if (rc == 0) {
         if (n_pkts)
             *n_pkts = b->n_pkts;
@@ -2203,7 +2263,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         b->gen_hint_ok = 0;
         free(b->slots_host);
         b->slots_host = NULL;
-        if (index_image(t, b, img, img + off - 24, take + 24) < 0)
+        if (index_image(t, b, img, img + off, take + 24) < 0)
             goto fail;
         t_index += te_now() - ti;
         if (b->n_pkts == 0) { /* the walk stopped at the chunk's first record */
@@ -2643,7 +2703,7 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
     b->gen_hint_ok = 0;
     b->grow_off = 0;
     b->ran = 0;
-    if (index_image(t, b, img, img, img_len) < 0)
+    if (index_image(t, b, img, img + 24, img_len) < 0)
         goto out;
     if (b->n_pkts != 1) {
         te_seterr(t, "packet %llu: not a record", (unsigned long long)t->pub.runtime.packetnum + 1);

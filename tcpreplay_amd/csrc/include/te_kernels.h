@@ -167,6 +167,7 @@ uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz);
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(te_launch_t *L, hipStream_t stream);
 int te_launch_q8(te_launch_t *L, hipStream_t stream);
+int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
 /* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */

@@ -2267,6 +2267,14 @@ static int l2carry_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stre
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the keys and the scan alone (tcpedit_batch_l2carry_out: a shard's carry-out before any
+// shard edits, so the ranks can exchange them)
+extern "C" int te_launch_l2carry(te_launch_t *L, hipStream_t stream) {
+    LaunchArgs a;
+    fill_args(a, L);
+    return l2carry_prepare(L, a, stream);
+}
+
 extern "C" uint64_t te_q8_slot_bytes(void) { return Q8_SLOT; }
 
 // te_q8_replay over the records the last edit of this launch listed (the counter on the

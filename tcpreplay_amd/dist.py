@@ -8,9 +8,15 @@ edited start to finish on its own GPU.  The only cross-rank traffic is
   * one all-reduce (sum) of the counter vector: RCCL over xGMI when the process
     group is "nccl", gloo on CPU.
 Each rank writes its own segment into the output file with pwrite; no packet
-data crosses a collective.  --fuzz-seed adds one exchange before the edit: its RNG
-is a single run-wide stream (fuzzing.c:8-20,87), so the ranks all-gather how many
-of their records reach the fuzz step and each skips the draws of the ranks before it.
+data crosses a collective.  Before the edit the ranks exchange 24 B each -- (shard
+opened, records reaching the fuzz step, dst_modified carry-out) -- for the two edits
+that carry state across records: --fuzz-seed's RNG is a single run-wide stream
+(fuzzing.c:8-20,87), so each rank skips the draws of the ranks before it; and a cooked,
+Juniper or 802.11 decoder into en10mb without --enet-dmac carries the encoder's
+dst_modified from the last C2S record to later ones (en10mb.c:597,612-615),
+so each rank seeds its context with the nearest earlier shard's value.  Every rank
+takes part in every collective even when its shard failed to open (it sends a sentinel
+and all ranks raise after), so no rank is left waiting.
 
 Hard errors keep tcprewrite's semantics (tcprewrite.c:156-160): the output is
 cut at the first failing record in file order, so the first erroring shard is
@@ -73,6 +79,18 @@ def plan(pcap, n: int) -> ShardPlan:
     return ShardPlan(list(off), list(base), int(total))
 
 
+def capture_dlt(hdr) -> int:
+    """the DLT tcprewrite hands tcpedit_init (pcap_datalink of the file, tcprewrite.c:80):
+    the header's link type in the file's byte order, LINKTYPE_RAW (101) as DLT_RAW (12)"""
+    import struct
+    h = bytes(hdr[:PCAP_HDR_LEN])
+    if len(h) < PCAP_HDR_LEN:
+        return 1
+    big = h[:4] in (b"\xa1\xb2\xc3\xd4", b"\xa1\xb2\x3c\x4d")
+    lt = struct.unpack_from(">I" if big else "<I", h, 20)[0] & 0x03FFFFFF
+    return 12 if lt == 101 else lt
+
+
 def fuzz_enabled(args) -> bool:
     """--fuzz-seed given: the one option whose records are not independent (fuzzing.c:87)"""
     return any(a == "--fuzz-seed" or a.startswith("--fuzz-seed=") for a in args)
@@ -80,26 +98,33 @@ def fuzz_enabled(args) -> bool:
 
 def gpu_editor(image, args, cache: Optional[bytes], pkt_base: int, device: int,
                fuzz_prefix: Optional[Callable[[int], int]] = None, hdr=None) -> ShardResult:
-    """Edit one shard on `device` through the C-ABI batch API.  `image` is a whole pcap
-    image, or with `hdr` (the file header) the shard's records in place.  With
-    --fuzz-seed, `fuzz_prefix(reaching records of this shard)` returns the RNG draws of
-    every earlier shard, and the context's state skips them before the edit."""
-    from . import Batch, TcpEdit
-    te = TcpEdit(args, device=device)
+    """Edit one shard on `device` through the C-ABI batch API (a single process: no
+    exchange).  `image` is a whole pcap image, or with `hdr` (the file header) the shard's
+    records in place.  With --fuzz-seed, `fuzz_prefix(reaching records of this shard)`
+    returns the RNG draws of every earlier shard, and the context's state skips them."""
+    sh = _DeviceShard(hdr, image, args, cache, pkt_base, device)
     try:
-        b = Batch(te, image, cache, pkt_base=pkt_base, hdr=hdr)
-        try:
-            if fuzz_prefix is not None:
-                te.fuzz_skip(fuzz_prefix(b.fuzz_reach()))
-            rc = b.run()
-            r = b.result()
-            return ShardResult(rc, b.output(), [int(getattr(r, n)) for n in COUNTER_NAMES],
-                               te.geterr() if rc != 0 else "")
-        finally:
-            b.close()
+        sh.run(fuzz_prefix(sh.reach) if fuzz_prefix is not None else 0, None)
+        return ShardResult(sh.rc, sh.b.output(), sh.counters, sh.error)
     finally:
-        te.close()
+        sh.close()
 
+
+def _pre_edit(dist, cdev, ok: bool, reach: int, carry: int):
+    """The one exchange before the edit, on every rank: (shard opened, fuzz reach,
+    dst_modified carry-out) per rank.  Returns (ranks that failed, fuzz draws of the
+    earlier ranks, the dst_modified value the nearest earlier writing shard left, or 0:
+    the reference's zeroed en10mb extra)."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    mine = torch.tensor([1 if ok else 0, reach, carry], dtype=torch.int64, device=cdev)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [[int(x) for x in v.tolist()] for v in allv]
+    bad = [r for r in range(world) if not rows[r][0]]
+    skip = sum(rows[r][1] for r in range(rank))
+    carry_in = next((rows[r][2] for r in range(rank - 1, -1, -1) if rows[r][2] in (0, 1)), 0)
+    return bad, skip, carry_in
 
 def _collective_device(dist):
     import torch
@@ -130,13 +155,26 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
         dist.all_gather(allv, mine)
         return sum(int(v.item()) for v in allv[:rank])
 
-    fz = fuzz_prefix if fuzz_enabled(args) else None
     if editor is None:  # the shard's records in place: no host copy
         dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        res = gpu_editor(p.segment(pcap, rank), args, cache, p.pkt_base[rank], dev, fuzz_prefix=fz,
-                         hdr=bytes(pcap[:PCAP_HDR_LEN]))
-    elif fz is not None:
-        res = editor(p.image(pcap, rank), args, cache, p.pkt_base[rank], fuzz_prefix=fz)
+        sh, err = None, ""
+        try:
+            sh = _DeviceShard(bytes(pcap[:PCAP_HDR_LEN]), p.segment(pcap, rank), args, cache, p.pkt_base[rank],
+                              dev)
+        except Exception as e:  # noqa: BLE001 -- every rank raises after the exchange
+            err = f"rank {rank}: {e}"
+        bad, skip, carry_in = _pre_edit(dist, cdev, sh is not None, sh.reach if sh else 0, sh.carry if sh else 2)
+        if bad:
+            if sh is not None:
+                sh.close()
+            raise RuntimeError(err or f"rank {bad[0]} failed to open its shard")
+        try:
+            sh.run(skip, carry_in)
+            res = ShardResult(sh.rc, sh.b.output(), sh.counters, sh.error)
+        finally:
+            sh.close()
+    elif fuzz_enabled(args):
+        res = editor(p.image(pcap, rank), args, cache, p.pkt_base[rank], fuzz_prefix=fuzz_prefix)
     else:
         res = editor(p.image(pcap, rank), args, cache, p.pkt_base[rank])
     seg = res.image[PCAP_HDR_LEN:]
@@ -176,21 +214,31 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
 
 
 class _DeviceShard:
-    """a rank's shard edited on its GPU, its output left in HBM until written"""
+    """a rank's shard on its GPU: opened (and its pre-edit facts found: records reaching
+    the fuzz step, the dst_modified carry-out) by the constructor, edited by run(), its
+    output left in HBM until written"""
 
-    def __init__(self, hdr, seg, args, cache, pkt_base, device, fuzz_prefix):
+    def __init__(self, hdr, seg, args, cache, pkt_base, device):
         from . import Batch, TcpEdit
-        self.te = TcpEdit(args, device=device)
+        self.te = TcpEdit(args, dlt=capture_dlt(hdr if hdr is not None else seg), device=device)
         self.b = None
         try:
             self.b = Batch(self.te, seg, cache, pkt_base=pkt_base, hdr=hdr)
-            if fuzz_prefix is not None:
-                self.te.fuzz_skip(fuzz_prefix(self.b.fuzz_reach()))
-            self.rc = self.b.run()
-            r = self.b.result()
+            self.reach = self.b.fuzz_reach() if fuzz_enabled(args) else 0
+            self.carry = self.b.l2carry_out()
         except Exception:
             self.close()
             raise
+        self.rc, self.counters, self.seg_len, self.error = None, [0] * len(COUNTER_NAMES), 0, ""
+
+    def run(self, fuzz_skip: int, carry_in: Optional[int]):
+        """the edit, after the earlier shards' fuzz draws and with their carry"""
+        if fuzz_skip:
+            self.te.fuzz_skip(fuzz_skip)
+        if carry_in is not None:
+            self.te.set_l2carry(carry_in)
+        self.rc = self.b.run()
+        r = self.b.result()
         self.counters = [int(getattr(r, n)) for n in COUNTER_NAMES]
         self.seg_len = max(0, int(r.out_len) - PCAP_HDR_LEN)
         self.error = self.te.geterr() if self.rc != 0 else ""
@@ -283,16 +331,32 @@ def rewrite_file_distributed(in_path: str, args, out_path: str, cache_path: Opti
 
         hdr = bytes(mm[:PCAP_HDR_LEN])
         sh, err = None, ""
-        try:
-            if editor is None:
-                dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-                sh = _DeviceShard(hdr, p.segment(mm, rank), args, cache, p.pkt_base[rank], dev, fz)
-            elif fz is not None:
-                sh = _HostShard(editor(hdr, p.segment(mm, rank), cache, p.pkt_base[rank], fuzz_prefix=fz))
-            else:
-                sh = _HostShard(editor(hdr, p.segment(mm, rank), cache, p.pkt_base[rank]))
-        except Exception as e:  # noqa: BLE001 -- travels in the all-gather below
-            err = f"rank {rank}: {e}"
+        if editor is None:
+            dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+            try:
+                sh = _DeviceShard(hdr, p.segment(mm, rank), args, cache, p.pkt_base[rank], dev)
+            except Exception as e:  # noqa: BLE001 -- travels in the exchange below
+                err = f"rank {rank}: {e}"
+            # every rank, opened or not: no rank is left waiting in a collective
+            bad, skip, carry_in = _pre_edit(dist, cdev, sh is not None, sh.reach if sh else 0,
+                                            sh.carry if sh else 2)
+            if sh is not None:
+                try:
+                    if bad:
+                        raise RuntimeError(f"rank {bad[0]} failed to open its shard")
+                    sh.run(skip, carry_in)
+                except Exception as e:  # noqa: BLE001 -- travels in the all-gather below
+                    err = err or f"rank {rank}: {e}"
+                    sh.close()
+                    sh = None
+        else:
+            try:
+                if fz is not None:
+                    sh = _HostShard(editor(hdr, p.segment(mm, rank), cache, p.pkt_base[rank], fuzz_prefix=fz))
+                else:
+                    sh = _HostShard(editor(hdr, p.segment(mm, rank), cache, p.pkt_base[rank]))
+            except Exception as e:  # noqa: BLE001 -- travels in the all-gather below
+                err = f"rank {rank}: {e}"
         try:
             # placement: (segment bytes, flag) from every rank; flag 1 a hard error in the
             # shard (tcprewrite.c:156-160), 2 the rank could not edit at all
@@ -318,19 +382,31 @@ def rewrite_file_distributed(in_path: str, args, out_path: str, cache_path: Opti
                     f.write(sh.header())
                     f.truncate(end)
             dist.barrier()
+            werr = ""
             if write:
-                gran = mmap.ALLOCATIONGRANULARITY
-                base = offset - offset % gran
-                with open(out_path, "r+b") as f:
-                    om = mmap.mmap(f.fileno(), offset - base + write, offset=base)
-                    try:
-                        got = sh.write_into(memoryview(om)[offset - base:offset - base + write])
-                        om.flush()
-                    finally:
-                        om.close()
-                if got != write:
-                    raise RuntimeError(f"rank {rank}: wrote {got} of {write} output bytes")
-            dist.barrier()
+                try:
+                    gran = mmap.ALLOCATIONGRANULARITY
+                    base = offset - offset % gran
+                    with open(out_path, "r+b") as f:
+                        om = mmap.mmap(f.fileno(), offset - base + write, offset=base)
+                        try:
+                            got = sh.write_into(memoryview(om)[offset - base:offset - base + write])
+                            om.flush()
+                        finally:
+                            om.close()
+                    if got != write:
+                        werr = f"rank {rank}: wrote {got} of {write} output bytes"
+                except Exception as e:  # noqa: BLE001 -- gathered below, raised on every rank
+                    werr = f"rank {rank}: {e}"
+            # the write outcome travels in a gather (not a barrier), so every rank raises
+            okv = torch.tensor([0 if werr else 1], dtype=torch.int64, device=cdev)
+            oks = [torch.zeros_like(okv) for _ in range(world)]
+            dist.all_gather(oks, okv)
+            if werr:
+                raise RuntimeError(werr)
+            failed = [r_ for r_ in range(world) if not int(oks[r_].item())]
+            if failed:
+                raise RuntimeError(f"rank {failed[0]} failed to write its output segment")
             return (-1 if first_err < world else 0), job, write, offset
         finally:
             if sh is not None:

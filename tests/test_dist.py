@@ -343,3 +343,69 @@ def test_c4_rank_share_at_nonzero_base_equals_oracle(built):
         assert got[pos:pos + len(seg)] == seg
         pos += len(seg)
     assert pos == len(got)
+
+
+def _cache_of(dirs):
+    """a tcpprep v04 cache (cache.h:63-72) from per-record directions (1 C2S, 2 S2C)"""
+    body = bytearray((len(dirs) + 3) // 4)
+    for i, d in enumerate(dirs):
+        body[i // 4] |= (0b11 if d == 1 else 0b10) << (2 * (i % 4))
+    return b"tcpprep\0" + b"04\0\0" + struct.pack(">QHH", len(dirs), 4, 0) + bytes(body)
+
+
+def q18_job(kind="sll"):
+    """SURVEY Q18 across a shard cut: a cooked capture whose IPv4 destinations are all
+    multicast; every record before the 2-rank cut is C2S (the last one sets the en10mb
+    encoder's dst_modified: its cooked header's first bytes are not the zero destination),
+    every record after it S2C, so shard 1's records keep shard 0's carry and skip the
+    multicast MAC update the reference skips too"""
+    recs = []
+    for i, (ts, tu, cl, ln, d) in enumerate(S.records(S.pcap_imix(3000, seed=23))):
+        d = bytearray(d)
+        if d[12:14] == b"\x08\x00":
+            d[30:34] = bytes([224 + i % 16, 1, 2, 3])
+        recs.append((ts, tu, cl, ln, bytes(d)))
+    pcap = S.reframe(S.build_pcap(recs), kind)
+    cut = D.plan(pcap, 2).pkt_base[1]
+    cache = _cache_of([1 if i < cut else 2 for i in range(len(recs))])
+    return pcap, ["--dlt=enet", "--fixcsum"], cache, {"sll": 113, "sll2": 276}[kind]
+
+
+def _q18_worker(rank, world, port, kind, use_file, d, q):
+    dist = _init("gloo", rank, world, port)
+    try:
+        pcap, args, cache, dlt = q18_job(kind)  # (dist opens each context at the capture's DLT)
+        out_path = os.path.join(d, "out.pcap")
+        if use_file:
+            in_path, c_path = os.path.join(d, "in.pcap"), os.path.join(d, "in.cache")
+            rc, counters, _, _ = D.rewrite_file_distributed(in_path, args, out_path, c_path, device=0)
+        else:
+            rc, counters, seg, off = D.rewrite_distributed(pcap, args, cache, out_path, device=0)
+        q.put((rank, rc))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,use_file", [("sll", False), ("sll2", True)])
+def test_two_rank_gpu_q18_carry_crosses_the_cut(built, kind, use_file):
+    """the dst_modified carry of the last C2S record of shard 0 reaches shard
+    1's first S2C records (the pre-edit exchange), as the single-process reference run has it"""
+    pcap, args, cache, _ = q18_job(kind)
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "in.pcap"), "wb").write(pcap)
+        open(os.path.join(d, "in.cache"), "wb").write(cache)
+        procs = [ctx.Process(target=_q18_worker, args=(r, 2, port, kind, use_file, d, q)) for r in range(2)]
+        for pr in procs:
+            pr.start()
+        for pr in procs:
+            pr.join(300)
+            assert pr.exitcode == 0
+        res = sorted(q.get() for _ in range(2))
+        out = open(os.path.join(d, "out.pcap"), "rb").read()
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
