@@ -60,6 +60,8 @@ WORKLOADS = {
              "--enet-vlan=del --fixcsum on 802.1Q-tagged IMIX 68/574/1518 (every record -4 bytes)"),
     "efcs": ("pcap_imix", dict(fcs=True), ["--efcs", "--fixcsum"],
              "--efcs --fixcsum on IMIX 68/574/1518 7:4:1 frames captured with their FCS (every record -4 bytes)"),
+    "macseed": ("pcap_imix", dict(), ["--enet-mac-seed=42", "--fixcsum"],
+                "--enet-mac-seed=42 --fixcsum on IMIX 64/570/1514 7:4:1 (MAC seed masks, en10mb.c:674-689)"),
     # the generic lane (te_edit_tiles): a size change that differs by record
     "mtu": ("pcap_imix", dict(), ["--mtu=1000", "--mtu-trunc", "--fixcsum"],
             "--mtu=1000 --mtu-trunc --fixcsum on IMIX 64/570/1514 7:4:1 (1514 B records cut to 1014 B: "
@@ -67,7 +69,7 @@ WORKLOADS = {
 }
 PER_RANK_PACKETS = {"c2": 10_000_000}  # N > 1 per-rank shard (HBM-resident)
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
-                   "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000,
+                   "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000, "macseed": 4_000_000,
                    "mtu": 4_000_000}
 CACHED = {"c4"}  # workloads with a tcpprep cache (synth.tcpprep_cache: C2S/S2C runs by flow)
 
@@ -268,7 +270,7 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="records per GPU (default: the config's size)")
     ap.add_argument("--no-device-index", action="store_true", help="skip the device record index line")
     ap.add_argument("--no-packet-latency", action="store_true", help="skip the tcpedit_packet latency line")
-    ap.add_argument("--extra", default="c3,c4,c5,c2x10,seed,hdr,vdel,efcs,mtu,fz,prep",
+    ap.add_argument("--extra", default="c3,c4,c5,c2x10,seed,hdr,vdel,efcs,macseed,mtu,fz,prep",
                     help="secondary configs measured at N=1 (comma list, '' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (half 1 thread, "
                     "half --cpu-threads threads)")

@@ -289,6 +289,23 @@ int tcpedit_fuzz_skip(tcpedit_t *tcpedit, uint64_t draws);
  * tcpedit_set_l2carry: seed the context with the nearest earlier shard's value. */
 int tcpedit_batch_l2carry_out(tcpedit_t *tcpedit, tcpedit_batch_t *b);
 int tcpedit_set_l2carry(tcpedit_t *tcpedit, int value);
+/* tcpreplay-edit's send loop, batched (send_packets.c:379-640; te_replay.c).  The reference
+ * edits each packet just before sending it (:469-474, tcpedit_packet with intf1's direction);
+ * here one --loop pass over the capture is one device batch.  With preload (--preload-pcap,
+ * -K) the first pass edits the records as read and every later pass edits the cached copy
+ * in place (get_next_packet :930-980): edits compound from pass to pass.
+ * tcpedit_replay_pass writes the pass's records as sent, in the -w dump's form
+ * (sendpacket.c:485-486: the edited header, the timestamp fraction as libpcap's nanosecond
+ * read leaves it), and returns TCPEDIT_OK or TCPEDIT_ERROR (a hard error: the records before
+ * it are in out, as tcpreplay's errx leaves its output). */
+typedef struct tcpedit_replay_s tcpedit_replay_t;
+tcpedit_replay_t *tcpedit_replay_open(tcpedit_t *tcpedit, const void *pcap, size_t len, int preload);
+size_t tcpedit_replay_bound(tcpedit_t *tcpedit, tcpedit_replay_t *r);
+int tcpedit_replay_pass(tcpedit_t *tcpedit, tcpedit_replay_t *r, void *out, size_t cap, size_t *out_len);
+void tcpedit_replay_close(tcpedit_replay_t *r);
+/* new bytes for a batch's records in place (same file and record headers: the index stands) */
+int tcpedit_batch_update_input(tcpedit_t *tcpedit, tcpedit_batch_t *b, const void *img, size_t len);
+
 /* device pointers, for callers that keep the data in HBM (e.g. a sender) */
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b);
 uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b);
@@ -313,7 +330,7 @@ void tcpedit_host_free(void *p);
  * and, if portlut != NULL, the 65536-entry port map.  Returns its size or -1. */
 int tcpedit_get_dev_cfg(tcpedit_t *tcpedit, void *out, size_t len, uint16_t *portlut);
 
-/* select the HIP device used by subsequently initialised contexts */
+/* select the HIP device used by contexts this thread initialises from now on */
 int tcpedit_set_device(int device);
 
 /* Multi-GPU sharding: cut a pcap image into `n`
@@ -325,6 +342,15 @@ int tcpedit_set_device(int device);
  * tcpedit_batch_open so tcpprep cache lookups stay global.  Host-only (no
  * device calls).  Returns the total record count, or -1 on a bad image. */
 int64_t tcpedit_pcap_shards(const void *pcap, size_t len, int n, uint64_t *off, uint64_t *pkt_base);
+
+/* Where n shards' outputs go in the job's output file, with tcprewrite's hard-error rule
+ * (tcprewrite.c:156-160: the output ends at the first failing record in file order): from
+ * each shard's output record bytes (seg_bytes, its records' bytes up to its own first error)
+ * and whether it hit a hard error, offset[k] is the file offset of shard k's records and
+ * write[k] the bytes it writes (0 for every shard after the first that failed).  Returns
+ * the file's size (24 + the bytes written).  Host-only. */
+uint64_t tcpedit_shard_place(int n, const uint64_t *seg_bytes, const int *hard_error, uint64_t *offset,
+                             uint64_t *write);
 
 #ifdef __cplusplus
 }

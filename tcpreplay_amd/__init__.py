@@ -7,6 +7,7 @@ kernels; there is no Python or CPU edit path, and importing the native library
 fails loudly when it has not been built.
 """
 import ctypes
+import struct
 import os
 
 __all__ = ["TcpEdit", "Batch", "BatchResult", "load", "LIB_PATH", "TCPEDIT_OK", "TCPEDIT_ERROR",
@@ -96,6 +97,10 @@ def load():
         "tcpedit_host_free": (None, [vp]),
         "tcpedit_set_device": (c_int, [c_int]),
         "tcpedit_get_dev_cfg": (c_int, [vp, vp, sz, vp]),
+        "tcpedit_replay_open": (vp, [vp, vp, sz, c_int]),
+        "tcpedit_replay_bound": (sz, [vp, vp]),
+        "tcpedit_replay_pass": (c_int, [vp, vp, vp, sz, ctypes.POINTER(sz)]),
+        "tcpedit_replay_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -245,6 +250,68 @@ class TcpEdit:
         dp = ctypes.c_char_p(ctypes.addressof(buf))
         rc = self._L.tcpedit_packet(self._ctx, ctypes.byref(hp), ctypes.byref(dp), direction)
         return rc, {"ts_sec": h.tv_sec, "ts_usec": h.tv_usec, "caplen": h.caplen, "len": h.len}
+
+
+class Replay:
+    """tcpreplay-edit's send loop over one capture, batched (tcpedit_replay_open): each
+    pass() edits every record as send_packets' tcpedit_packet call does
+    (send_packets.c:469-474) and returns the records as sent, in the -w dump's form
+    (16-byte headers with nanosecond fractions, no file header).  With preload (-K) the
+    passes after the first edit the cached copy in place, so edits compound."""
+
+    def __init__(self, te: TcpEdit, pcap, preload=False):
+        self._te, self._L = te, te._L
+        keep, p, n = _buf(pcap)
+        self._r = self._L.tcpedit_replay_open(te._ctx, p, n, 1 if preload else 0)
+        del keep
+        if not self._r:
+            raise RuntimeError(te.geterr())
+        self._cap = self._L.tcpedit_replay_bound(te._ctx, self._r)
+
+    def pass_(self):
+        """one --loop pass: (rc, records as sent); rc < 0 ends the run (errx), the
+        records before the failing one still returned"""
+        out = ctypes.create_string_buffer(max(1, self._cap))
+        n = ctypes.c_size_t(0)
+        rc = self._L.tcpedit_replay_pass(self._te._ctx, self._r, out, self._cap, ctypes.byref(n))
+        return rc, out.raw[:n.value]
+
+    def close(self):
+        if self._r:
+            self._L.tcpedit_replay_close(self._r)
+            self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# pcap_open_dead(DLT_EN10MB, MAX_SNAPLEN) + pcap_dump_open (sendpacket.c:945-968)
+REPLAY_DUMP_HEADER = struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0, 262144, 1)
+
+
+def replay_edit(pcap, args, loops=1, preload=False, errors=None):
+    """`tcpreplay-edit -w out --loop=loops [-K] <args> in.pcap`: (rc, the -w file's bytes);
+    a failing pass's error string is appended to `errors` (a list) when given"""
+    te = TcpEdit(args)
+    try:
+        r = Replay(te, pcap, preload)
+        try:
+            out, rc = [REPLAY_DUMP_HEADER], 0
+            for p in range(int(loops)):
+                rc, recs = r.pass_()
+                out.append(recs)
+                if rc < 0:
+                    if errors is not None:
+                        errors.append(f"pass {p}: {te.geterr()}")
+                    break
+            return rc, b"".join(out)
+        finally:
+            r.close()
+    finally:
+        te.close()
 
 
 class Batch:

@@ -23,7 +23,7 @@
         }                                                                                 \
     } while (0)
 
-static int g_device = -1;
+static __thread int g_device = -1; /* per thread: one host thread may drive each device */
 
 int tcpedit_set_device(int device)
 {
@@ -80,6 +80,10 @@ struct tcpedit_batch_s {
     uint32_t q8_cap;
     int q8_defer;            /* tcpedit_packet replays itself, over the caller's buffer */
     uint8_t *d_q8_init;      /* tcpedit_packet: the caller's buffer bytes [0, need) */
+    uint64_t walk_from;      /* the walk's first record (0: 24, the image's first) */
+    uint64_t rec0;           /* image offset of the launch's first record (0: 24) */
+    uint64_t out_base;       /* output offset of its first record in d_out (0: 24; = rec0 mod 16) */
+    uint64_t walk_limit;     /* records starting here or later are not the batch's (0: none) */
     uint64_t walk_end;       /* image offset where the record walk stopped ... */
     int walk_stop;           /* ... because: 0 bytes ran out, 1 libpcap's oversize stop, 2 a hard error */
     int kev_n;
@@ -136,13 +140,21 @@ static int static_capable(const te_dev_cfg_t *c)
            !c->skip_soft_errors && c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && !c->fuzz_seed;
 }
 
-/* options the register-resident fast lane carries (fast_lane.hpp): the MAC, port,
+/* options the register-resident fast lane carries (fast_lane.hpp): the MAC (with
+ * --enet-subsmac and --enet-mac-seed), port,
  * address and seed edits, the IP header edits (TOS, TTL, traffic class, flow label,
  * TCP sequence) and both checksum modes (--fixcsum or incremental); anything else
  * keeps every packet on the generic lane */
+/* the CIDR maps fit the config's inline lists (the fast lanes read no spill list) */
+static int cidr_inline(const te_dev_cfg_t *c)
+{
+    return c->n_cidrmap1 <= TE_MAX_CIDRMAP && c->n_cidrmap2 <= TE_MAX_CIDRMAP && c->n_srcipmap <= TE_MAX_CIDRMAP &&
+           c->n_dstipmap <= TE_MAX_CIDRMAP;
+}
+
 static int fast_capable(const te_dev_cfg_t *c)
 {
-    return static_capable(c) && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+    return static_capable(c) && !c->fixhdrlen && cidr_inline(c);
 }
 
 /* the most a record's L2 header can grow: a VLAN push (4 bytes) or a user header longer
@@ -169,7 +181,7 @@ static int fast_capable_grow(const te_dev_cfg_t *c)
     return c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && c->vlan == TE_VLAN_ADD &&
            c->vlan_tag < 65535 && !c->efcs &&
            !c->fuzz_seed && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate && !c->skip_soft_errors &&
-           !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+           !c->fixhdrlen && cidr_inline(c);
 }
 
 /* a VLAN pop (--enet-vlan=del) or --efcs as the only size change: every record can shrink
@@ -190,7 +202,7 @@ static int static_shrink_kind(const te_dev_cfg_t *c)
 /* ... and the wave lane carries it (its fast-lane conditions) */
 static int fast_capable_shrink(const te_dev_cfg_t *c)
 {
-    return static_shrink_kind(c) != TE_SZ_NONE && !c->fixhdrlen && c->n_subs == 0 && !c->random_set;
+    return static_shrink_kind(c) != TE_SZ_NONE && !c->fixhdrlen && cidr_inline(c);
 }
 
 /* IPv6 rewrites with a non-octet target mask keep the reference's stray write
@@ -200,7 +212,7 @@ static int fast_v6_ok(const te_dev_cfg_t *c)
     const te_cidrmap_t *lists[4] = {c->cidrmap1, c->cidrmap2, c->srcipmap, c->dstipmap};
     const int n[4] = {c->n_cidrmap1, c->n_cidrmap2, c->n_srcipmap, c->n_dstipmap};
     for (int l = 0; l < 4; l++)
-        for (int i = 0; i < n[l]; i++)
+        for (int i = 0; i < n[l] && i < TE_MAX_CIDRMAP; i++) /* (a longer list keeps the generic lane) */
             if (lists[l][i].to.family == 6 && lists[l][i].to.masklen % 8)
                 return 0;
     return 1;
@@ -238,7 +250,7 @@ typedef struct {
        ever formed (a shard's records may start its buffer) */
     const uint8_t *recs;
     size_t len;
-    int swapped, pad, slot_mode, grow_fast, wave;
+    int swapped, pad, slot_mode, grow_fast, wave, shrink_fast;
     uint32_t budget, max_pkts;
     uint32_t growth;         /* output room per record beyond its input (rec_growth) */
     /* the stretch */
@@ -537,6 +549,43 @@ static void pool_wait(int *pending)
 
 #define TE_WALK_PART_MIN ((size_t)2 << 20) /* bytes per stretch of a parallel walk, at least */
 
+/* The tile cut a config and capture (b->swapped, b->nsec) get: the lane (wave, block or
+ * generic), the slot layout, the tile budget; *proto is the walk's prototype. */
+static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
+{
+    memset(proto, 0, sizeof(*proto));
+    proto->swapped = b->swapped;
+    proto->pad = t->cfg.fixlen == TE_FIXLEN_PAD;
+    /* slots with headroom: VLAN push, fixlen pad, a user L2 header longer than Ethernet's */
+    proto->slot_mode = proto->pad || (t->cfg.encoder == TE_ENC_EN10MB && t->cfg.vlan == TE_VLAN_ADD) ||
+                       l2_growth(&t->cfg) > 0;
+    b->slot_layout = proto->slot_mode;
+    /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
+       are cut to the wave image (their per-record slots then fit the generic kernel's) */
+    proto->grow_fast = !proto->pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
+                       fast_kind_pref() == TE_FAST_WAVE;
+    /* ... and a VLAN pop or --efcs (native-order microsecond input only) */
+    const int shrink_fast = !proto->slot_mode && fast_capable_shrink(&t->cfg) && !b->swapped && !b->nsec;
+    b->fast_tiles = (!proto->slot_mode && fast_capable(&t->cfg)) || proto->grow_fast || shrink_fast;
+    b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
+    if (shrink_fast && !proto->grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
+        b->fast_tiles = 0, b->fast_kind = 0;
+    proto->wave = b->fast_kind == TE_FAST_WAVE;
+    proto->budget = proto->wave      ? te_wave_tile_bytes(&t->cfg, proto->grow_fast ? TE_SZ_GROW
+                                                                   : shrink_fast     ? static_shrink_kind(&t->cfg)
+                                                                                     : TE_SZ_NONE)
+                    : b->fast_tiles ? TE_FK_TILE_BYTES
+                                    : TE_SLOT_BYTES;
+    proto->max_pkts = proto->wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
+    proto->stop_error_pkt = -1;
+    proto->growth = rec_growth(&t->cfg);
+    proto->shrink_fast = shrink_fast;
+    b->cut_budget = proto->budget;
+    b->cut_max_pkts = proto->max_pkts;
+    b->cut_growth = proto->growth;
+    b->cut_device_ok = proto->wave && !proto->pad && (!proto->slot_mode || proto->grow_fast);
+}
+
 /* Walk the records and cut them into tiles.  A large image is walked as up to
  * TCPEDIT_HIP_WALK_THREADS stretches at once: stretch i > 0 starts at a guessed record
  * boundary (the first plausible chain of headers after an even split point), and it
@@ -563,38 +612,9 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     }
     b->linktype = te_linktype_dlt(rd32(hdr + 20, b->swapped) & 0x03ffffffu);
     te_walk_t proto;
-    memset(&proto, 0, sizeof(proto));
+    cut_setup(t, b, &proto);
     proto.recs = recs;
     proto.len = len;
-    proto.swapped = b->swapped;
-    proto.pad = t->cfg.fixlen == TE_FIXLEN_PAD;
-    /* slots with headroom: VLAN push, fixlen pad, a user L2 header longer than Ethernet's */
-    proto.slot_mode = proto.pad || (t->cfg.encoder == TE_ENC_EN10MB && t->cfg.vlan == TE_VLAN_ADD) ||
-                      l2_growth(&t->cfg) > 0;
-    b->slot_layout = proto.slot_mode;
-    /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
-       are cut to the wave image (their per-record slots then fit the generic kernel's) */
-    proto.grow_fast = !proto.pad && fast_capable_grow(&t->cfg) && !b->swapped && !b->nsec &&
-                      fast_kind_pref() == TE_FAST_WAVE;
-    /* ... and a VLAN pop or --efcs (native-order microsecond input only) */
-    const int shrink_fast = !proto.slot_mode && fast_capable_shrink(&t->cfg) && !b->swapped && !b->nsec;
-    b->fast_tiles = (!proto.slot_mode && fast_capable(&t->cfg)) || proto.grow_fast || shrink_fast;
-    b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
-    if (shrink_fast && !proto.grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
-        b->fast_tiles = 0, b->fast_kind = 0;
-    proto.wave = b->fast_kind == TE_FAST_WAVE;
-    proto.budget = proto.wave        ? te_wave_tile_bytes(&t->cfg, proto.grow_fast ? TE_SZ_GROW
-                                                                   : shrink_fast    ? static_shrink_kind(&t->cfg)
-                                                                                    : TE_SZ_NONE)
-                   : b->fast_tiles ? TE_FK_TILE_BYTES
-                                   : TE_SLOT_BYTES;
-    proto.max_pkts = proto.wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
-    proto.stop_error_pkt = -1;
-    proto.growth = rec_growth(&t->cfg);
-    b->cut_budget = proto.budget;
-    b->cut_max_pkts = proto.max_pkts;
-    b->cut_growth = proto.growth;
-    b->cut_device_ok = proto.wave && !proto.pad && (!proto.slot_mode || proto.grow_fast);
 
     uint64_t cap_tiles = 1024, cap_pk = 1 << 16;
     if (b->idx_pinned) { /* a pipeline slot: the chunk budget bounds both (16 B per record at least) */
@@ -610,17 +630,21 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
             return -1;
         }
     }
-    /* the stretches: [24, q1), [q1, q2), ... */
+    /* the stretches: [from, q1), [q1, q2), ..., up to the walk limit (a pipeline chunk's
+       records are the ones starting in its own bytes) */
+    const size_t from = b->walk_from ? b->walk_from : 24, limit = b->walk_limit ? b->walk_limit : (size_t)-1;
     int parts = walk_threads();
     if ((size_t)parts > (len - 24) / TE_WALK_PART_MIN)
         parts = (int)((len - 24) / TE_WALK_PART_MIN);
     if (parts < 1)
         parts = 1;
     size_t q[65];
-    q[0] = 24;
+    q[0] = from;
     int np = 1;
     for (int i = 1; i < parts; i++) {
-        const size_t s0 = 24 + (len - 24) / parts * i, lim = s0 + (1u << 20) < len ? s0 + (1u << 20) : len;
+        const size_t s0 = from + (len - from) / parts * i, lim = s0 + (1u << 20) < len ? s0 + (1u << 20) : len;
+        if (s0 >= limit)
+            break;
         size_t p = s0 > q[np - 1] ? s0 : q[np - 1] + 1;
         for (; p + 16 <= lim; p++)
             if (chain_plausible(recs, len, p, b->swapped, b->nsec, 8))
@@ -628,7 +652,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         if (p + 16 <= lim)
             q[np++] = p;
     }
-    q[np] = (size_t)-1;
+    q[np] = limit;
     te_walk_t w[64];
     int pending = 0;
     for (int i = 0; i < np; i++) {
@@ -702,13 +726,13 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         m->end = x->end;
         m->stop_at = x->stop_at;
     }
-    if (!m->fail && i < np && !m->walk_stop && m->end + 16 <= len) {
+    if (!m->fail && i < np && !m->walk_stop && m->end + 16 <= len && m->end < limit) {
         /* a guess was wrong (or a stretch failed): the rest, sequentially */
-        m->stop_at = (size_t)-1;
+        m->stop_at = limit;
         const size_t from = m->end;
         te_walk_t rest = proto;
         rest.start = from;
-        rest.stop_at = (size_t)-1;
+        rest.stop_at = limit;
         rest.tiles = m->tiles + m->n_tiles;
         rest.pkt_rel = m->pkt_rel + m->n_pkts;
         rest.cap_tiles = m->cap_tiles - m->n_tiles;
@@ -727,7 +751,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
                 m->cap_tiles = m->cap_pkts = need;
                 rest = proto;
                 rest.start = from;
-                rest.stop_at = (size_t)-1;
+                rest.stop_at = limit;
                 rest.tiles = m->tiles + m->n_tiles;
                 rest.pkt_rel = m->pkt_rel + m->n_pkts;
                 rest.cap_tiles = rest.cap_pkts = need - m->n_pkts;
@@ -774,7 +798,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     b->cut_tiles = m->n_tiles;
     b->n_pkts = m->n_pkts;
     if (!rc && proto.wave && !proto.slot_mode && !b->idx_pinned)
-        balance_tiles(b, te_wave_waves(&t->cfg, shrink_fast ? static_shrink_kind(&t->cfg) : TE_SZ_NONE),
+        balance_tiles(b, te_wave_waves(&t->cfg, proto.shrink_fast ? static_shrink_kind(&t->cfg) : TE_SZ_NONE),
                       proto.budget, proto.max_pkts);
     b->out_cap = 24 + 64 + m->rec_bytes;
     b->scratch_bytes = m->scratch_bytes;
@@ -921,6 +945,29 @@ int te_upload_cfg(tcpedit_t *t)
         return 0;
     if (!t->d_cfg)
         HIPCHK(t, hipMalloc((void **)&t->d_cfg, sizeof(te_dev_cfg_t)));
+    {   /* CIDR map entries past the inline lists: their spill lists go up with the config */
+        const int32_t n[4] = {t->cfg.n_cidrmap1, t->cfg.n_cidrmap2, t->cfg.n_srcipmap, t->cfg.n_dstipmap};
+        for (int w = 0; w < 4; w++) {
+            const int32_t extra = n[w] > TE_MAX_CIDRMAP ? n[w] - TE_MAX_CIDRMAP : 0;
+            t->cfg.cidr_spill[w] = 0;
+            if (!extra)
+                continue;
+            if (!t->cspill[w]) {
+                te_seterr(t, "CIDR map %d: %d entries past the inline list, none parsed", w, extra);
+                return -1;
+            }
+            if (t->d_cspill_n[w] < extra) {
+                hipFree(t->d_cspill[w]);
+                t->d_cspill[w] = NULL;
+                t->d_cspill_n[w] = 0;
+                HIPCHK(t, hipMalloc((void **)&t->d_cspill[w], sizeof(te_cidrmap_t) * (size_t)extra));
+                t->d_cspill_n[w] = extra;
+            }
+            HIPCHK(t, hipMemcpyAsync(t->d_cspill[w], t->cspill[w], sizeof(te_cidrmap_t) * (size_t)extra,
+                                     hipMemcpyHostToDevice, t->stream));
+            t->cfg.cidr_spill[w] = (uint64_t)(uintptr_t)t->d_cspill[w];
+        }
+    }
     HIPCHK(t, hipMemcpyAsync(t->d_cfg, &t->cfg, sizeof(te_dev_cfg_t), hipMemcpyHostToDevice, t->stream));
     if (t->portlut) {
         if (!t->d_portlut)
@@ -1132,7 +1179,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.in_swapped = (uint32_t)b->swapped;
     L.in_nsec = (uint32_t)b->nsec;
     L.out = b->d_out;
-    L.out_base = 24;
+    L.out_base = b->out_base ? b->out_base : 24;
     L.tile_state = (uint64_t *)(b->d_ws + WS_STATE);
     L.ticket = (unsigned int *)(b->d_ws + WS_TICKET);
     L.status = b->d_status;
@@ -1148,7 +1195,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
        zero-length records are the only ways), so outputs sit at input offsets */
     const te_dev_cfg_t *c = &t->cfg;
     L.static_off = !b->slot_layout && static_capable(c) && !b->has_zero_cap;
-    L.rec0 = 24;
+    L.rec0 = b->rec0 ? b->rec0 : 24;
     /* VLAN add as the only size change: every record grows by 4 bytes or is a hard error
        (dlt_en10mb_encode, en10mb.c:520-575), so outputs sit at input offset + 4 x index */
     L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
@@ -1266,7 +1313,8 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
     L.in_swapped = (uint32_t)b->swapped;
     L.in_nsec = (uint32_t)b->nsec;
     L.out = b->d_out;
-    L.out_base = 24;
+    L.out_base = b->out_base ? b->out_base : 24;
+    L.rec0 = b->rec0 ? b->rec0 : 24;
     L.status = b->d_status;
     L.counters = (uint64_t *)(b->d_ws + b->last_cnt_off);
     L.err = (uint64_t *)(b->d_ws + WS_ERR);
@@ -1515,6 +1563,20 @@ const uint8_t *tcpedit_batch_status(tcpedit_batch_t *b)
     return b->status;
 }
 
+/* new bytes for a batch's records, in place: the same file header and record headers (so
+ * the index stands), other record bytes -- tcpreplay-edit's --preload-pcap cache, edited
+ * from pass to pass (te_replay.c) */
+int tcpedit_batch_update_input(tcpedit_t *t, tcpedit_batch_t *b, const void *img, size_t len)
+{
+    if (!t || !b || !img || len != b->in_len)
+        return TCPEDIT_ERROR;
+    HIPCHK(t, hipMemcpyAsync(b->d_in, img, len, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
 int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
 {
     if (!t || !b)
@@ -1676,104 +1738,120 @@ int tcpedit_debug_packet_latency(tcpedit_t *t, const uint8_t *pkt, uint32_t capl
     return rc == TCPEDIT_ERROR ? TCPEDIT_ERROR : TCPEDIT_OK;
 }
 
+/* the device index's workspace for a capture of `len` bytes from file offset `entry`:
+ * the zeroed words and look-back granules, then the per-window records */
+static uint64_t idx_nwin(uint64_t base, uint64_t limit)
+{
+    const uint64_t W = te_index_window_bytes();
+    return limit > base ? (limit - base + W - 1) / W : 0;
+}
+
+static void idx_layout(IdxArgs *a, uint8_t *ws, uint64_t nwin)
+{
+    a->ticket = (uint32_t *)ws;
+    a->done = a->ticket + 1;
+    a->stop_win_c = a->ticket + 2;
+    a->overflow = a->ticket + 3;
+    a->timeouts = a->ticket + 4;
+    a->scratch_ctr = (uint64_t *)(ws + 24);
+    a->state = (uint64_t *)(ws + IDX_WS_WORDS);
+    uint8_t *w = ws + IDX_WS_BYTES(nwin);
+    a->w_entry = (uint64_t *)w;
+    a->w_exit = a->w_entry + nwin;
+    a->w_pfx = a->w_exit + nwin;
+    a->w_err = a->w_pfx + nwin;
+    a->w_flags = (uint32_t *)(a->w_err + nwin);
+    a->totals = (uint64_t *)(a->w_flags + nwin + (nwin & 1));
+}
+
 int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms)
 {
     if (!t || !b || iters < 1)
         return TCPEDIT_ERROR;
     if (!b->cut_device_ok || b->in_len <= 24)
         return 1;
-    const uint64_t body = b->in_len - 24;
-    /* about 8 greedy tiles a window (the device cuts greedily; a balanced re-cut's smaller
-       tiles would shrink the windows and give the speculation more starts to be fooled at) */
-    const uint64_t avg = b->cut_tiles ? (b->walk_end - 24) / b->cut_tiles : 4096;
-    uint64_t W = (8 * (avg ? avg : 64) + 63) & ~63ull;
-    if (W < 4096)
-        W = 4096;
-    if (W > 65536)
-        W = 65536;
-    const uint64_t nwin = (body + W - 1) / W;
+    const uint64_t nwin = idx_nwin(16, b->in_len);
     if (nwin > 0x7fffffffull)
         return 1;
     uint8_t *wbuf = NULL;
     hipEvent_t e0 = NULL, e1 = NULL;
     int rc = TCPEDIT_ERROR;
     uint64_t tot[IDX_T__N];
-    const size_t w64 = 8 * nwin, w32 = 4 * nwin;
-    HIPCHK(t, hipMalloc((void **)&wbuf, 7 * w64 + 4 * w32 + 8 * IDX_T__N + 64));
+    const uint64_t zb = IDX_WS_BYTES(nwin), wsb = zb + IDX_WIN_BYTES(nwin) + 8 * (IDX_T__N + 2);
+    /* records and tiles: a tile never spans two windows, so at most one more a window */
+    const uint64_t tile_cap = b->n_tiles + nwin + 1;
+    te_tile_t *d_tiles = NULL;
+    uint16_t *d_rel = NULL;
+    HIPCHK(t, hipMalloc((void **)&wbuf, wsb));
+    HIPCHK(t, hipMalloc((void **)&d_tiles, sizeof(te_tile_t) * tile_cap));
+    HIPCHK(t, hipMalloc((void **)&d_rel, sizeof(uint16_t) * (b->n_pkts + 1)));
     IdxArgs a;
     memset(&a, 0, sizeof a);
     a.img = b->d_in;
     a.len = b->in_len;
+    a.entry = 24;
+    a.base = 16;
+    a.limit = b->in_len;
     a.sw = b->swapped;
     a.nsec = b->nsec;
-    a.W = W;
     a.nwin = (uint32_t)nwin;
     a.budget = b->cut_budget;
     a.max_pkts = b->cut_max_pkts;
     a.growth = b->cut_growth;
-    a.w_entry = (uint64_t *)wbuf;
-    a.w_exit = a.w_entry + nwin;
-    a.w_recbytes = a.w_exit + nwin;
-    a.w_scratch = a.w_recbytes + nwin;
-    a.p_base = a.w_scratch + nwin;
-    a.t_base = a.p_base + nwin;
-    a.s_base = a.t_base + nwin;
-    a.totals = a.s_base + nwin;
-    a.w_nrec = (uint32_t *)(a.totals + IDX_T__N);
-    a.w_ntile = a.w_nrec + nwin;
-    a.w_flags = a.w_ntile + nwin;
-    a.w_err = a.w_flags + nwin;
-    /* sizing run: count + scan, the totals, then room for the tiles */
-    if (te_launch_index(&a, 0, t->stream) || te_launch_index(&a, 1, t->stream)) {
-        te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
-        goto out;
-    }
-    HIPCHK(t, hipMemcpyAsync(tot, a.totals, sizeof tot, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(t, hipStreamSynchronize(t->stream));
-    if (tot[IDX_T_BAD]) {
-        rc = 1;
-        goto out;
-    }
-    if (tot[IDX_T_RECS] != b->n_pkts) { /* the chain is the chain: a mismatch is a bug */
-        te_seterr(t, "device index found %llu records, the host walk %llu", (unsigned long long)tot[IDX_T_RECS],
-                  (unsigned long long)b->n_pkts);
-        goto out;
-    }
-    const uint64_t nt = tot[IDX_T_TILES];
-    if (nt > b->n_tiles) { /* tiles never span windows: there may be a few more */
-        hipFree(b->d_tiles);
-        b->d_tiles = NULL;
-        hipFree(b->d_tile_list);
-        b->d_tile_list = NULL;
-        hipFree(b->d_ws);
-        b->d_ws = NULL;
-        HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (nt + 1)));
-        HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (nt + 1)));
-        b->ws_bytes = WS_SLOTS(nt) + 64 + (b->fast_kind == TE_FAST_WAVE ? 32 * (uint64_t)te_wave_grid() : 0);
-        HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
-    }
-    if (tot[IDX_T_SCRATCH] > b->scratch_bytes) {
-        hipFree(b->d_scratch);
-        b->d_scratch = NULL;
-        HIPCHK(t, hipMalloc((void **)&b->d_scratch, tot[IDX_T_SCRATCH]));
-        b->scratch_bytes = tot[IDX_T_SCRATCH];
-    }
-    a.tiles = b->d_tiles;
-    a.pkt_rel = b->d_pkt_rel;
-    if (te_launch_index(&a, 2, t->stream)) {
-        te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
-        goto out;
-    }
-    /* timed runs: the three passes, device-resident end to end */
+    idx_layout(&a, wbuf, nwin);
+    a.tiles = d_tiles;
+    a.pkt_rel = d_rel;
+    a.tile_cap = tile_cap;
+    a.rec_cap = b->n_pkts + 1;
+    /* the index is built into its own tiles and record offsets, swapped in below (a
+       missed guess leaves the host index as it is) */
     HIPCHK(t, hipEventCreate(&e0));
     HIPCHK(t, hipEventCreate(&e1));
-    HIPCHK(t, hipEventRecord(e0, t->stream));
-    for (int i = 0; i < iters; i++)
-        if (te_launch_index(&a, 0, t->stream) || te_launch_index(&a, 1, t->stream) ||
-            te_launch_index(&a, 2, t->stream)) {
+    for (int i = -1; i < iters; i++) { /* (run -1: the check run, untimed) */
+        if (i == 0)
+            HIPCHK(t, hipEventRecord(e0, t->stream));
+        HIPCHK(t, hipMemsetAsync(wbuf, 0, zb, t->stream));
+        if (te_launch_index(&a, t->stream)) {
             te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
             goto out;
         }
+        if (i == -1) {
+            HIPCHK(t, hipMemcpyAsync(tot, a.totals, sizeof tot, hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(t, hipStreamSynchronize(t->stream));
+            if (tot[IDX_T_BAD]) { /* a guess missed the chain: the host index stays (it is exact) */
+                if (getenv("TCPEDIT_HIP_IDX_DEBUG")) {
+                    const uint64_t q = tot[IDX_T_BADWIN];
+                    uint64_t we[3] = {0, 0, 0}, wx[3] = {0, 0, 0};
+                    uint32_t wf[3] = {0, 0, 0};
+                    if (q != 0xffffffffull && q < nwin) {
+                        const uint64_t q0 = q ? q - 1 : 0, n = q + 2 <= nwin ? q + 2 - q0 : nwin - q0;
+                        hipMemcpy(we, a.w_entry + q0, 8 * n, hipMemcpyDeviceToHost);
+                        hipMemcpy(wx, a.w_exit + q0, 8 * n, hipMemcpyDeviceToHost);
+                        hipMemcpy(wf, a.w_flags + q0, 4 * n, hipMemcpyDeviceToHost);
+                    }
+                    fprintf(stderr, "device index: bad window %llu of %llu (timeouts? %llu); entry/exit/flags around it: "
+                            "[%llx %llx %x] [%llx %llx %x] [%llx %llx %x]\n", (unsigned long long)q,
+                            (unsigned long long)nwin, (unsigned long long)tot[IDX_T_WINDOWS],
+                            (unsigned long long)we[0], (unsigned long long)wx[0], wf[0], (unsigned long long)we[1],
+                            (unsigned long long)wx[1], wf[1], (unsigned long long)we[2], (unsigned long long)wx[2], wf[2]);
+                }
+                rc = 1;
+                goto out;
+            }
+            if (tot[IDX_T_OVERFLOW] || tot[IDX_T_RECS] != b->n_pkts) { /* the chain is the chain */
+                te_seterr(t, "device index found %llu records (overflow %llu), the host walk %llu",
+                          (unsigned long long)tot[IDX_T_RECS], (unsigned long long)tot[IDX_T_OVERFLOW],
+                          (unsigned long long)b->n_pkts);
+                goto out;
+            }
+            if (tot[IDX_T_SCRATCH] > b->scratch_bytes) {
+                hipFree(b->d_scratch);
+                b->d_scratch = NULL;
+                HIPCHK(t, hipMalloc((void **)&b->d_scratch, tot[IDX_T_SCRATCH]));
+                b->scratch_bytes = tot[IDX_T_SCRATCH];
+            }
+        }
+    }
     HIPCHK(t, hipEventRecord(e1, t->stream));
     HIPCHK(t, hipEventSynchronize(e1));
     {
@@ -1782,7 +1860,25 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
         if (ms)
             *ms = f / iters;
     }
-    b->n_tiles = nt;
+    {
+        const uint64_t nt = tot[IDX_T_TILES];
+        if (nt > b->n_tiles) { /* tiles never span windows: there may be a few more */
+            hipFree(b->d_tile_list);
+            b->d_tile_list = NULL;
+            hipFree(b->d_ws);
+            b->d_ws = NULL;
+            HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (nt + 1)));
+            b->ws_bytes = WS_SLOTS(nt) + 64 + (b->fast_kind == TE_FAST_WAVE ? 32 * (uint64_t)te_wave_grid() : 0);
+            HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
+        }
+        hipFree(b->d_tiles);
+        b->d_tiles = d_tiles;
+        d_tiles = NULL;
+        hipFree(b->d_pkt_rel);
+        b->d_pkt_rel = d_rel;
+        d_rel = NULL;
+        b->n_tiles = nt;
+    }
     b->has_zero_cap = tot[IDX_T_ZERO] != 0;
     b->walk_end = tot[IDX_T_END];
     b->walk_stop = tot[IDX_T_STOP] == IDX_STOP ? 1 : tot[IDX_T_STOP] == IDX_ERROR ? 2 : 0;
@@ -1801,6 +1897,8 @@ out:
         hipEventDestroy(e0);
     if (e1)
         hipEventDestroy(e1);
+    hipFree(d_tiles);
+    hipFree(d_rel);
     hipFree(wbuf);
     return rc;
 fail:
@@ -1944,6 +2042,10 @@ static int host_locked(const void *p)
 #define TE_RES_ERR 96
 #define TE_RES_SLOTS 128
 
+/* the device-index pipeline uploads each chunk with the bytes of a record that starts in it
+   and ends past it: the largest record (16 + 262144 bytes), rounded */
+#define TE_PIPE_MARGIN ((size_t)262160 + 240)
+
 struct te_pipe_s {
     size_t chunk;                      /* record-byte budget of a chunk (slot capacity) */
     hipStream_t s_h2d, s_d2h;
@@ -1951,6 +2053,11 @@ struct te_pipe_s {
     hipEvent_t h2d_done[TE_PIPE_SLOTS], edit_done[TE_PIPE_SLOTS], d2h_done[TE_PIPE_SLOTS];
     uint64_t d_out_alloc[TE_PIPE_SLOTS], d_scratch_alloc[TE_PIPE_SLOTS];
     uint8_t *hdr;                      /* pinned copy of the 24-byte file header */
+    /* the device record index (te_index.hip) per slot: its workspace, totals (pinned), done */
+    uint8_t *d_idx[TE_PIPE_SLOTS];
+    uint64_t *h_tot[TE_PIPE_SLOTS];
+    hipEvent_t idx_done[TE_PIPE_SLOTS];
+    uint64_t idx_nwin;
 };
 
 void te_pipe_free(tcpedit_t *t)
@@ -1969,6 +2076,10 @@ void te_pipe_free(tcpedit_t *t)
             hipEventDestroy(P->edit_done[s]);
         if (P->d2h_done[s])
             hipEventDestroy(P->d2h_done[s]);
+        if (P->idx_done[s])
+            hipEventDestroy(P->idx_done[s]);
+        hipFree(P->d_idx[s]);
+        hipHostFree(P->h_tot[s]);
     }
     if (P->s_h2d)
         hipStreamDestroy(P->s_h2d);
@@ -1986,11 +2097,13 @@ static tcpedit_batch_t *pipe_slot_open(tcpedit_t *t, size_t chunk)
     b->ctx = t;
     b->idx_pinned = 1;
     b->grow_never = 1;
-    b->idx_cap_pkts = chunk / 16 + 2; /* a record is at least its 16-byte header */
-    b->idx_cap_tiles = b->idx_cap_pkts;
+    /* a record is at least its 16-byte header; the device index may also take the records
+       of a chunk's margin (TE_PIPE_MARGIN), and cut a tile more a window */
+    b->idx_cap_pkts = (chunk + TE_PIPE_MARGIN) / 16 + 2;
+    b->idx_cap_tiles = b->idx_cap_pkts + (chunk + TE_PIPE_MARGIN) / te_index_window_bytes() + 2;
     HIPCHK(t, hipHostMalloc((void **)&b->tiles, sizeof(te_tile_t) * b->idx_cap_tiles, 0));
     HIPCHK(t, hipHostMalloc((void **)&b->pkt_rel, sizeof(uint16_t) * b->idx_cap_pkts, 0));
-    HIPCHK(t, hipMalloc((void **)&b->d_in, chunk + 24 + 64));
+    HIPCHK(t, hipMalloc((void **)&b->d_in, chunk + TE_PIPE_MARGIN + 24 + 64));
     HIPCHK(t, hipMalloc((void **)&b->d_status, b->idx_cap_pkts + 16));
     HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (b->idx_cap_tiles + 1)));
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->idx_cap_pkts + 1)));
@@ -2018,12 +2131,17 @@ static int pipe_ready(tcpedit_t *t, size_t chunk)
     HIPCHK(t, hipStreamCreateWithFlags(&P->s_h2d, hipStreamNonBlocking));
     HIPCHK(t, hipStreamCreateWithFlags(&P->s_d2h, hipStreamNonBlocking));
     HIPCHK(t, hipHostMalloc((void **)&P->hdr, 64, 0));
+    P->idx_nwin = idx_nwin(16, 24 + chunk + TE_PIPE_MARGIN);
     for (int s = 0; s < TE_PIPE_SLOTS; s++) {
         if (!(P->slot[s] = pipe_slot_open(t, chunk)))
             goto fail;
         HIPCHK(t, hipEventCreateWithFlags(&P->h2d_done[s], hipEventDisableTiming));
         HIPCHK(t, hipEventCreateWithFlags(&P->edit_done[s], hipEventDisableTiming));
         HIPCHK(t, hipEventCreateWithFlags(&P->d2h_done[s], hipEventDisableTiming));
+        HIPCHK(t, hipEventCreateWithFlags(&P->idx_done[s], hipEventDisableTiming));
+        HIPCHK(t, hipMalloc((void **)&P->d_idx[s], IDX_WS_BYTES(P->idx_nwin) + IDX_WIN_BYTES(P->idx_nwin) +
+                                                       8 * (IDX_T__N + 2)));
+        HIPCHK(t, hipHostMalloc((void **)&P->h_tot[s], 8 * IDX_T__N, 0));
     }
     return 0;
 fail:
@@ -2086,10 +2204,11 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
                      "at bytes written by an earlier pipeline chunk or by no record: not reproducible here");
         return -1;
     }
+    const uint64_t ob = b->out_base ? b->out_base : 24;
     uint64_t bytes = b->counters[TE_CNT_BYTES_OUT];
     int64_t err_pkt = -1;
     if (b->err[0] != ~0ull) { /* a hard error truncates the output at the failing record */
-        bytes = b->err[1] - 24;
+        bytes = b->err[1] - ob;
         err_pkt = (int64_t)(pkt_base + b->err[0]);
     } else if (b->stop_error_pkt >= 0) {
         err_pkt = (int64_t)(pkt_base + (uint64_t)b->stop_error_pkt);
@@ -2100,7 +2219,7 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     }
     HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
     if (bytes)
-        HIPCHK(t, hipMemcpyAsync(dst + *pos, b->d_out + 24, bytes, hipMemcpyDeviceToHost, P->s_d2h));
+        HIPCHK(t, hipMemcpyAsync(dst + *pos, b->d_out + ob, bytes, hipMemcpyDeviceToHost, P->s_d2h));
     HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
     *pos += bytes;
     t->pub.runtime.packetnum += b->counters[TE_CNT_PACKETS];
@@ -2146,6 +2265,215 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
         off += 16 + caplen;
     }
     return bound;
+}
+
+/* TCPEDIT_HIP_PIPE_INDEX=host keeps the host record walk in the pipeline (A/B) */
+static int pipe_index_host_env(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_PIPE_INDEX");
+    return e && strcmp(e, "host") == 0;
+}
+
+/* The pipeline with the record index built on the device (te_index.hip), for the wave
+ * lane's configs: chunk k is the file bytes [24 + kC, 24 + (k+1)C), uploaded with the next
+ * TE_PIPE_MARGIN bytes (a record starting in it may end past it) -- a fixed byte range, so
+ * its H2D never waits for the record walk.  Its records are the ones starting in the chunk
+ * from where the previous chunk's chain ended; the device reads that position from the
+ * previous chunk's index totals (same stream), so the host's only wait per chunk is for
+ * the index's totals before it launches the edit.  A chunk whose speculation missed the
+ * chain is walked on the host from the exact position instead (te_index.hip).
+ * Returns 0 (*pos, the output end), or -1. */
+static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t in_len, uint8_t *dst, size_t out_cap,
+                        uint8_t *d_dirbits, uint64_t dirbits_len, uint64_t *pos_io, int trace)
+{
+    const size_t C = P->chunk;
+    uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0, 0};
+    int inflight[TE_PIPE_SLOTS] = {0, 0}, stopped = 0, k = 0, fallbacks = 0;
+    uint64_t entry_file = 24;  /* host copy of where chunk k's records start (file offset) */
+    uint64_t limit_img[TE_PIPE_SLOTS] = {0, 0}, file0[TE_PIPE_SLOTS] = {0, 0};
+    IdxArgs A[TE_PIPE_SLOTS];
+    const double t0 = te_now();
+    double t_wait = 0;
+    /* chunk j: upload into its slot (the slot's previous edit must be done reading d_in) */
+#define DIX_UPLOAD(j)                                                                                         \
+    do {                                                                                                      \
+        const int s_ = (j) % TE_PIPE_SLOTS;                                                                   \
+        tcpedit_batch_t *b_ = P->slot[s_];                                                                    \
+        const uint64_t f0_ = 24 + (uint64_t)(j) * C;                                                          \
+        const uint64_t fe_ = f0_ + C + TE_PIPE_MARGIN < in_len ? f0_ + C + TE_PIPE_MARGIN : in_len;          \
+        if ((j) >= TE_PIPE_SLOTS)                                                                             \
+            HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s_], 0));                                     \
+        HIPCHK(t, hipMemcpyAsync(b_->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));                     \
+        HIPCHK(t, hipMemcpyAsync(b_->d_in + 24, img + f0_, fe_ - f0_, hipMemcpyHostToDevice, P->s_h2d));      \
+        HIPCHK(t, hipEventRecord(P->h2d_done[s_], P->s_h2d));                                                 \
+        b_->in_len = 24 + (fe_ - f0_);                                                                        \
+        file0[s_] = f0_;                                                                                      \
+        limit_img[s_] = f0_ + C >= in_len ? b_->in_len : 24 + C;                                              \
+    } while (0)
+    /* chunk j's index on the compute stream, after its upload; its first record from the
+       previous chunk's totals (on the device), or 24 */
+#define DIX_INDEX(j)                                                                                          \
+    do {                                                                                                      \
+        const int s_ = (j) % TE_PIPE_SLOTS, ps_ = ((j) + TE_PIPE_SLOTS - 1) % TE_PIPE_SLOTS;                  \
+        tcpedit_batch_t *b_ = P->slot[s_];                                                                    \
+        IdxArgs *a_ = &A[s_];                                                                                 \
+        memset(a_, 0, sizeof *a_);                                                                            \
+        a_->img = b_->d_in;                                                                                   \
+        a_->len = b_->in_len;                                                                                 \
+        a_->entry = 24;                                                                                       \
+        a_->entry_ptr = (j) ? A[ps_].totals + IDX_T_END : NULL;                                               \
+        a_->entry_sub = C;                                                                                    \
+        a_->base = 16;                                                                                        \
+        a_->limit = limit_img[s_];                                                                            \
+        a_->sw = b_->swapped;                                                                                 \
+        a_->nsec = b_->nsec;                                                                                  \
+        a_->nwin = (uint32_t)idx_nwin(16, limit_img[s_]);                                                     \
+        a_->budget = b_->cut_budget;                                                                          \
+        a_->max_pkts = b_->cut_max_pkts;                                                                      \
+        a_->growth = b_->cut_growth;                                                                          \
+        idx_layout(a_, P->d_idx[s_], a_->nwin);                                                               \
+        a_->tiles = b_->d_tiles;                                                                              \
+        a_->pkt_rel = b_->d_pkt_rel;                                                                          \
+        a_->tile_cap = b_->idx_cap_tiles;                                                                     \
+        a_->rec_cap = b_->idx_cap_pkts;                                                                       \
+        HIPCHK(t, hipStreamWaitEvent(t->stream, P->h2d_done[s_], 0));                                        \
+        HIPCHK(t, hipMemsetAsync(P->d_idx[s_], 0, IDX_WS_BYTES(a_->nwin), t->stream));                       \
+        if (te_launch_index(a_, t->stream)) {                                                                 \
+            te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));            \
+            goto fail;                                                                                        \
+        }                                                                                                     \
+        HIPCHK(t, hipMemcpyAsync(P->h_tot[s_], a_->totals, 8 * IDX_T__N, hipMemcpyDeviceToHost, t->stream)); \
+        HIPCHK(t, hipEventRecord(P->idx_done[s_], t->stream));                                                \
+    } while (0)
+
+    DIX_UPLOAD(0);
+    DIX_INDEX(0);
+    for (;; k++) {
+        const int s = k % TE_PIPE_SLOTS;
+        tcpedit_batch_t *b = P->slot[s];
+        const int more = 24 + (uint64_t)(k + 1) * C < in_len;
+        if (more)
+            DIX_UPLOAD(k + 1);
+        /* ---- chunk k's index totals ---- */
+        const double tw = te_now();
+        HIPCHK(t, hipEventSynchronize(P->idx_done[s]));
+        t_wait += te_now() - tw;
+        const uint64_t *T = P->h_tot[s];
+        const uint64_t entry_img = entry_file - file0[s] + 24;
+        b->pkt_base = pkts;
+        b->launches = 0;
+        b->gen_hint_ok = 0;
+        free(b->slots_host);
+        b->slots_host = NULL;
+        /* the chunk's first record sits at entry_img (bytes before it end the previous
+           chunk's last record); its output at an offset of the same 16-byte phase (the
+           wave lane stores whole 16-byte chunks at input offsets + a multiple of 16) */
+        b->rec0 = entry_img;
+        b->out_base = 24 + ((entry_img - 24) & 15);
+        if (T[IDX_T_BAD] || T[IDX_T_OVERFLOW] || T[IDX_T_RECS] > b->idx_cap_pkts) {
+            /* the speculation missed the chain: walk this chunk on the host from the exact
+               position, and give the next chunk's index that walk's end */
+            fallbacks++;
+            b->walk_from = entry_img;
+            b->walk_limit = limit_img[s];
+            const int rc = index_image(t, b, img, img + file0[s], b->in_len);
+            b->walk_from = b->walk_limit = 0;
+            if (rc < 0)
+                goto fail;
+            b->out_cap += 16; /* (out_base) */
+            HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice,
+                                     t->stream));
+            HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
+                                     t->stream));
+            P->h_tot[s][IDX_T_END] = b->walk_end;
+            HIPCHK(t, hipMemcpyAsync(A[s].totals + IDX_T_END, &P->h_tot[s][IDX_T_END], 8, hipMemcpyHostToDevice,
+                                     t->stream));
+        } else {
+            b->n_pkts = T[IDX_T_RECS];
+            b->n_tiles = T[IDX_T_TILES];
+            b->has_zero_cap = T[IDX_T_ZERO] != 0;
+            b->walk_end = T[IDX_T_END];
+            b->walk_stop = T[IDX_T_STOP] == IDX_STOP ? 1 : T[IDX_T_STOP] == IDX_ERROR ? 2 : 0;
+            b->stop_error_pkt = T[IDX_T_ERR_REC] == ~0ull ? -1 : (int64_t)T[IDX_T_ERR_REC];
+            b->out_cap = 24 + 16 + 64 + T[IDX_T_BYTES];
+            b->scratch_bytes = T[IDX_T_SCRATCH];
+            if (T[IDX_T_SCRATCH] > P->d_scratch_alloc[s]) {
+                te_seterr(t, "device index scratch %llu > %llu", (unsigned long long)T[IDX_T_SCRATCH],
+                          (unsigned long long)P->d_scratch_alloc[s]);
+                goto fail;
+            }
+        }
+        entry_file = file0[s] + b->walk_end - 24;
+        if (b->n_pkts == 0) {
+            if (b->stop_error_pkt >= 0) {
+                te_seterr(t, "Error rewriting packets: packet %llu", (unsigned long long)(pkts + 1));
+                goto fail;
+            }
+            stopped = 1;
+        } else {
+            if (b->walk_stop || b->walk_end + 16 > b->in_len)
+                stopped = 1; /* libpcap's end, or the bytes ran out */
+            b->dirbits_len = dirbits_len;
+            b->d_dirbits = d_dirbits;
+            b->ws_bytes = WS_SLOTS(b->n_tiles) + 64 + 32 * (uint64_t)te_wave_grid();
+            if (pipe_grow(t, P, s) < 0)
+                goto fail;
+            HIPCHK(t, hipMemsetAsync(b->d_ws, 0, WS_STATE, t->stream)); /* err, ticket, both counter sets */
+            HIPCHK(t, hipMemsetAsync(b->d_ws + WS_LIST_CNT(b->n_tiles), 0, 8, t->stream));
+            HIPCHK(t, hipStreamWaitEvent(t->stream, P->d2h_done[s], 0));
+            if (launch(b, -1) != 0) {
+                te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+                goto fail;
+            }
+            if (run_q8(t, b, -1, pkts == 0, NULL, 0, t->stream) < 0)
+                goto fail;
+            HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                     hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_ERR, b->d_ws + WS_ERR, sizeof(b->err),
+                                     hipMemcpyDeviceToHost, t->stream));
+            if (b->last_fgrid)
+                HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
+                                         32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
+            inflight[s] = 1;
+            chunk_pkt_base[s] = pkts;
+            pkts += b->n_pkts;
+        }
+        if (more && !stopped)
+            DIX_INDEX(k + 1);
+        /* ---- the previous chunk: results in, D2H to its place ---- */
+        const int ps = (k + TE_PIPE_SLOTS - 1) % TE_PIPE_SLOTS;
+        if (k > 0 && inflight[ps] == 1) {
+            HIPCHK(t, hipEventSynchronize(P->edit_done[ps]));
+            inflight[ps] = 2;
+            if (pipe_finish_chunk(t, P, ps, chunk_pkt_base[ps], dst, out_cap, &pos, &stopped) < 0)
+                goto fail;
+        }
+        if (stopped || !more)
+            break;
+    }
+    for (int j = 0; j < TE_PIPE_SLOTS; j++) { /* the chunk still in flight */
+        const int s = (k + TE_PIPE_SLOTS - j) % TE_PIPE_SLOTS;
+        if (inflight[s] == 1) {
+            HIPCHK(t, hipEventSynchronize(P->edit_done[s]));
+            inflight[s] = 2;
+            if (pipe_finish_chunk(t, P, s, chunk_pkt_base[s], dst, out_cap, &pos, &stopped) < 0)
+                goto fail;
+        }
+    }
+    HIPCHK(t, hipStreamSynchronize(P->s_d2h));
+    if (trace)
+        fprintf(stderr, "pipe (device index): %d chunks, %.3f ms, index waits %.3f ms, host-walk fallbacks %d\n",
+                k + 1, (te_now() - t0) * 1e3, t_wait * 1e3, fallbacks);
+    *pos_io = pos;
+#undef DIX_UPLOAD
+#undef DIX_INDEX
+    return 0;
+fail:
+    hipStreamSynchronize(P->s_h2d);
+    hipStreamSynchronize(t->stream);
+    hipStreamSynchronize(P->s_d2h);
+    return -1;
 }
 
 int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, const void *cache, size_t cache_len,
@@ -2235,6 +2563,38 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     }
     t_reg = te_now() - t_start;
 
+    {   /* the wave lane's configs: the record index on the device */
+        tcpedit_batch_t *b0 = P->slot[0];
+        uint32_t magic;
+        memcpy(&magic, img, 4);
+        int dix = !pipe_index_host_env();
+        for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+            tcpedit_batch_t *bs = P->slot[s];
+            bs->swapped = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
+            bs->nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
+            te_walk_t proto;
+            cut_setup(t, bs, &proto);
+            dix &= bs->cut_device_ok;
+        }
+        if (dix && b0->fast_kind == TE_FAST_WAVE) {
+            /* scratch for huge records, sized for the worst chunk (the index places them) */
+            for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+                const uint64_t need = (uint64_t)chunk_bytes + TE_PIPE_MARGIN + (chunk_bytes + TE_PIPE_MARGIN) / 8 + 65536;
+                if (P->d_scratch_alloc[s] < need) {
+                    hipFree(P->slot[s]->d_scratch);
+                    P->slot[s]->d_scratch = NULL;
+                    HIPCHK(t, hipMalloc((void **)&P->slot[s]->d_scratch, need));
+                    P->d_scratch_alloc[s] = need;
+                }
+            }
+            if (pipe_run_dix(t, P, img, in_len, dst, out_cap, d_dirbits, dirbits_len, &pos, trace) < 0)
+                goto fail;
+            *out_len = pos;
+            rc = t->pipe_err ? TCPEDIT_ERROR : TCPEDIT_OK;
+            goto out;
+        }
+    }
+
     uint64_t off = 24; /* file offset of the next chunk's first record */
     int k = 0;
     for (;; k++) {
@@ -2261,6 +2621,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         b->pkt_base = pkts;
         b->launches = 0;
         b->gen_hint_ok = 0;
+        b->rec0 = b->out_base = 0;
         free(b->slots_host);
         b->slots_host = NULL;
         if (index_image(t, b, img, img + off, take + 24) < 0)
@@ -2661,8 +3022,293 @@ fail:
     return NULL;
 }
 
-/* tcpedit_packet (tcpedit.c:46-366): one record through the GPU kernel, staged
- * through the context's page-locked one-record batch. */
+/* ---- tcpedit_packet's resident server (te_packet_server) ----
+ * One block stays on the device and serves tcpedit_packet calls through host-mapped
+ * fine-grained memory: the record goes into the mapped input image, the request words
+ * and seq are stored (release), the host spins on done.  No launch, copy or stream sync
+ * per call.  The kernel leaves after TE_SRV_IDLE_TICKS without a request (and is launched
+ * again by the next call), when the context's config changes, and at tcpedit_close / exit.
+ * TCPEDIT_HIP_PACKET_SERVER=0 keeps the launch-per-call path (A/B). */
+#define TE_SRV_IN (24 + 16 + TE_SLOT_BYTES + 64)
+#define TE_SRV_OUT (24 + 16 + TE_SLOT_BYTES + 1024)
+#define TE_SRV_IDLE_TICKS 5000000ull /* 50 ms of the 100 MHz real-time clock */
+#define TE_SRV_DECLINED (-100)       /* the record goes the launch-per-call way */
+struct te_srv_s {
+    hipStream_t stream;
+    te_srv_ctl_t *ctl, *d_ctl;
+    uint8_t *in, *d_in, *out, *d_out;
+    uint8_t *d_scratch;
+    te_dev_cfg_t *d_cfg;
+    te_dev_cfg_t cfg;        /* the config the running kernel holds (skip_soft_errors 0) */
+    const uint16_t *portlut; /* ... its device port table ... */
+    const uint16_t *hportlut; /* ... built from this host table */
+    int running;             /* launched and not yet seen leaving */
+    int broken;              /* it stopped answering: the launch-per-call path from now on */
+    uint32_t seq;
+};
+
+/* live servers, stopped at exit (a resident kernel must not outlive the mappings it polls) */
+#define TE_SRV_MAX 256
+static te_srv_t *te_srv_live[TE_SRV_MAX];
+static pthread_mutex_t te_srv_mu = PTHREAD_MUTEX_INITIALIZER;
+static int te_srv_atexit_done;
+
+static void srv_stop(te_srv_t *S)
+{
+    if (!S->running)
+        return;
+    __atomic_store_n(&S->ctl->stop, 1u, __ATOMIC_RELEASE);
+    hipStreamSynchronize(S->stream);
+    S->running = 0;
+    S->ctl->stop = 0;
+}
+
+static void srv_stop_all(void)
+{
+    pthread_mutex_lock(&te_srv_mu);
+    for (int i = 0; i < TE_SRV_MAX; i++)
+        if (te_srv_live[i])
+            srv_stop(te_srv_live[i]);
+    pthread_mutex_unlock(&te_srv_mu);
+}
+
+static void srv_free(tcpedit_t *t)
+{
+    te_srv_t *S = t->srv;
+    if (!S)
+        return;
+    pthread_mutex_lock(&te_srv_mu);
+    for (int i = 0; i < TE_SRV_MAX; i++)
+        if (te_srv_live[i] == S)
+            te_srv_live[i] = NULL;
+    pthread_mutex_unlock(&te_srv_mu);
+    if (S->stream)
+        srv_stop(S);
+    if (S->ctl)
+        hipHostFree(S->ctl);
+    if (S->in)
+        hipHostFree(S->in);
+    if (S->out)
+        hipHostFree(S->out);
+    hipFree(S->d_scratch);
+    hipFree(S->d_cfg);
+    if (S->stream)
+        hipStreamDestroy(S->stream);
+    free(S);
+    t->srv = NULL;
+}
+
+static int srv_enabled(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_PACKET_SERVER");
+    return !(e && e[0] == '0');
+}
+
+static int srv_launch(tcpedit_t *t, te_srv_t *S, uint32_t start_seq)
+{
+    te_srv_launch_t L;
+    memset(&L, 0, sizeof L);
+    L.ctl = S->d_ctl;
+    L.cfg = S->d_cfg;
+    L.portlut = S->portlut;
+    L.in = S->d_in;
+    L.out = S->d_out;
+    L.scratch = S->d_scratch;
+    L.start_seq = start_seq;
+    L.idle_ticks = TE_SRV_IDLE_TICKS;
+    S->ctl->stop = 0;
+    __atomic_store_n(&S->ctl->alive, 1u, __ATOMIC_RELEASE);
+    if (te_launch_packet_server(&L, S->stream) != 0) {
+        S->ctl->alive = 0;
+        te_seterr(t, "packet server launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return -1;
+    }
+    S->running = 1;
+    return 0;
+}
+
+/* the context's server, running with its current config; NULL: decline (or an error set) */
+static te_srv_t *srv_ready(tcpedit_t *t)
+{
+    te_srv_t *S = t->srv;
+    if (!S) {
+        S = calloc(1, sizeof *S);
+        if (!S)
+            return NULL;
+        t->srv = S;
+        if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void **)&S->ctl, 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc((void **)&S->in, TE_SRV_IN, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc((void **)&S->out, TE_SRV_OUT, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&S->d_ctl, S->ctl, 0) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&S->d_in, S->in, 0) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&S->d_out, S->out, 0) != hipSuccess ||
+            hipMalloc((void **)&S->d_scratch, TE_SRV_SCRATCH) != hipSuccess ||
+            hipMemset(S->d_scratch, 0, TE_SRV_SCRATCH) != hipSuccess ||
+            hipMalloc((void **)&S->d_cfg, sizeof(te_dev_cfg_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            S->broken = 1;
+            return NULL;
+        }
+        memset(S->ctl, 0, 4096);
+        memset(S->in, 0, TE_SRV_IN);
+        pthread_mutex_lock(&te_srv_mu);
+        int slot = -1;
+        for (int i = 0; i < TE_SRV_MAX && slot < 0; i++)
+            if (!te_srv_live[i])
+                slot = i;
+        if (slot >= 0)
+            te_srv_live[slot] = S;
+        if (!te_srv_atexit_done) {
+            atexit(srv_stop_all);
+            te_srv_atexit_done = 1;
+        }
+        pthread_mutex_unlock(&te_srv_mu);
+        if (slot < 0) { /* (every slot taken: no server for this context) */
+            S->broken = 1;
+            return NULL;
+        }
+    }
+    if (S->broken)
+        return NULL;
+    te_dev_cfg_t want = t->cfg;
+    want.skip_soft_errors = 0; /* tcpedit_packet itself never drops */
+    const uint16_t *pl = t->cfg.has_portmap ? t->d_portlut : NULL;
+    if (S->running && (memcmp(&want, &S->cfg, sizeof want) != 0 || pl != S->portlut || t->portlut != S->hportlut))
+        srv_stop(S);
+    if (S->running && !__atomic_load_n(&S->ctl->alive, __ATOMIC_ACQUIRE)) { /* it left (idle) */
+        hipStreamSynchronize(S->stream);
+        S->running = 0;
+    }
+    if (!S->running) {
+        S->cfg = want;
+        S->portlut = pl;
+        S->hportlut = t->portlut;
+        if (hipMemcpyAsync(S->d_cfg, &S->cfg, sizeof S->cfg, hipMemcpyHostToDevice, S->stream) != hipSuccess ||
+            hipStreamSynchronize(t->stream) != hipSuccess || hipStreamSynchronize(S->stream) != hipSuccess) {
+            te_seterr(t, "packet server setup failed: %s", hipGetErrorString(hipGetLastError()));
+            S->broken = 1;
+            return NULL;
+        }
+        if (srv_launch(t, S, S->seq) < 0) {
+            S->broken = 1;
+            return NULL;
+        }
+    }
+    return S;
+}
+
+/* one request; 0 when served, -1 when the server stopped answering */
+static int srv_call(tcpedit_t *t, te_srv_t *S)
+{
+    te_srv_ctl_t *c = S->ctl;
+    const uint32_t q = ++S->seq;
+    __atomic_store_n(&c->seq, q, __ATOMIC_RELEASE);
+    const double t0 = te_now();
+    for (unsigned n = 1; __atomic_load_n(&c->done, __ATOMIC_ACQUIRE) != q; n++) {
+        __builtin_ia32_pause();
+        if ((n & 255) != 0)
+            continue;
+        if (!__atomic_load_n(&c->alive, __ATOMIC_ACQUIRE)) {
+            /* it left (idle timeout) before it saw this request: launch it again */
+            if (__atomic_load_n(&c->done, __ATOMIC_ACQUIRE) == q)
+                break;
+            hipStreamSynchronize(S->stream);
+            if (srv_launch(t, S, q - 1) < 0)
+                return -1;
+        } else if (te_now() - t0 > 5.0) {
+            __atomic_store_n(&c->stop, 1u, __ATOMIC_RELEASE);
+            te_seterr(t, "packet server did not answer in 5 s");
+            return -1;
+        }
+    }
+    return 0;
+}
+
+/* the status byte and output record of one tcpedit_packet edit into the caller's header
+ * and buffer (out_img: an image whose record starts at byte 24; out_len: its bytes) */
+static int packet_result(tcpedit_t *t, struct pcap_pkthdr *h, unsigned char **pktdata, uint8_t st,
+                         const uint8_t *out_img, uint64_t out_len, uint64_t cap)
+{
+    int rc;
+    switch (st & TE_ST_RC_MASK) {
+    case TE_ST_RC_ERROR:
+        te_seterr(t, "packet %llu: tcpedit error", (unsigned long long)t->pub.runtime.packetnum);
+        return TCPEDIT_ERROR;
+    case TE_ST_RC_SOFT:
+        te_seterr(t, "Packet %llu has no L3+ header or cannot be edited", (unsigned long long)t->pub.runtime.packetnum);
+        rc = TCPEDIT_SOFT_ERROR;
+        break;
+    case TE_ST_RC_WARN:
+        rc = TCPEDIT_WARN;
+        break;
+    default:
+        rc = TCPEDIT_OK;
+    }
+    if (st & TE_ST_WARNED) {
+        te_setwarn(t, "packet %llu: checksum not recomputed", (unsigned long long)t->pub.runtime.packetnum);
+        fprintf(stderr, "Warning: %s\n", t->pub.runtime.warnstr);
+    }
+    if (out_len >= 24 + 16) {
+        uint32_t oc, ol;
+        memcpy(&oc, out_img + 24 + 8, 4);
+        memcpy(&ol, out_img + 24 + 12, 4);
+        if (oc > 262166u || 40 + (uint64_t)oc > cap) {
+            te_seterr(t, "packet %llu: output record of %u bytes", (unsigned long long)t->pub.runtime.packetnum, oc);
+            return TCPEDIT_ERROR;
+        }
+        memcpy(*pktdata, out_img + 40, oc);
+        h->caplen = oc;
+        h->len = ol;
+    } else {
+        h->caplen = 0; /* edited down to zero bytes */
+    }
+    return rc;
+}
+
+/* tcpedit_packet through the resident server, or TE_SRV_DECLINED: --fuzz-seed (its state
+ * stream), the en10mb dst_modified carry, a record larger than the block's
+ * LDS slot, and an edit that reads past caplen take the launch-per-call path */
+static int packet_via_server(tcpedit_t *t, struct pcap_pkthdr *h, unsigned char **pktdata, int direction)
+{
+    if (!srv_enabled() || (t->srv && t->srv->broken))
+        return TE_SRV_DECLINED;
+    const te_dev_cfg_t *c = &t->cfg;
+    if (c->fuzz_seed || (TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB && !(c->mac_mask & TE_MASK_DMAC1)))
+        return TE_SRV_DECLINED;
+    const uint32_t caplen = h->caplen;
+    uint64_t data = caplen;
+    if (c->fixlen == TE_FIXLEN_PAD && h->len > data)
+        data = h->len;
+    if (data > 262144u || TE_SLOT_BYTES_OF(8u, data) > (uint32_t)TE_SLOT_BYTES)
+        return TE_SRV_DECLINED;
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    te_srv_t *S = srv_ready(t);
+    if (!S)
+        return TE_SRV_DECLINED; /* (no server could be set up: the launch-per-call path) */
+    const uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
+    memcpy(S->in + 24, rh, 16);
+    memcpy(S->in + 40, *pktdata, caplen);
+    memset(S->in + 40 + caplen, 0, 16);
+    S->ctl->dir = direction;
+    S->ctl->caplen = caplen;
+    S->ctl->pkt_base = t->pub.runtime.packetnum;
+    if (srv_call(t, S) < 0) {
+        S->broken = 1;
+        return TE_SRV_DECLINED;
+    }
+    const uint8_t st = (uint8_t)S->ctl->status;
+    if (st & TE_ST_UNSUPPORTED)
+        return TE_SRV_DECLINED;
+    t->pub.runtime.packetnum += S->ctl->packets;
+    t->pub.runtime.total_bytes += S->ctl->bytes_out;
+    t->pub.runtime.pkts_edited += S->ctl->edited;
+    return packet_result(t, h, pktdata, st, S->out, 24 + S->ctl->bytes_out, TE_SRV_OUT);
+}
+
+/* tcpedit_packet (tcpedit.c:46-366): one record through the resident server, or through
+ * the GPU kernel staged in the context's page-locked one-record batch. */
 int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pktdata, tcpr_dir_t direction)
 {
     if (!t || !pkthdr || !*pkthdr || !pktdata || !*pktdata)
@@ -2676,6 +3322,13 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
                   caplen);
         return TCPEDIT_ERROR;
     }
+    if (direction == TCPR_DIR_S2C && te_check_decoder_cfg(t, 1) < 0)
+        return TCPEDIT_ERROR;
+    {
+        const int r = packet_via_server(t, h, pktdata, (int)direction);
+        if (r != TE_SRV_DECLINED)
+            return r;
+    }
     tcpedit_batch_t *b = one_ready(t);
     if (!b)
         return TCPEDIT_ERROR;
@@ -2688,8 +3341,6 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
         const uint32_t lt = (uint32_t)t->dlt; /* the context's DLT (its decoder) */
         memcpy(img + 20, &lt, 4);
     }
-    if (direction == TCPR_DIR_S2C && te_check_decoder_cfg(t, 1) < 0)
-        return TCPEDIT_ERROR;
     const uint32_t rh[4] = {(uint32_t)h->ts.tv_sec, (uint32_t)h->ts.tv_usec, caplen, h->len};
     memcpy(img + 24, rh, 16);
     memcpy(img + 40, *pktdata, caplen);
@@ -2742,43 +3393,10 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
                   (unsigned long long)t->pub.runtime.packetnum);
         goto out;
     }
-    switch (st & TE_ST_RC_MASK) {
-    case TE_ST_RC_ERROR:
-        te_seterr(t, "packet %llu: tcpedit error", (unsigned long long)t->pub.runtime.packetnum);
-        rc = TCPEDIT_ERROR;
-        goto out;
-    case TE_ST_RC_SOFT:
-        te_seterr(t, "Packet %llu has no L3+ header or cannot be edited", (unsigned long long)t->pub.runtime.packetnum);
-        rc = TCPEDIT_SOFT_ERROR;
-        break;
-    case TE_ST_RC_WARN:
-        rc = TCPEDIT_WARN;
-        break;
-    default:
-        rc = TCPEDIT_OK;
-    }
-    if (st & TE_ST_WARNED) {
-        te_setwarn(t, "packet %llu: checksum not recomputed", (unsigned long long)t->pub.runtime.packetnum);
-        fprintf(stderr, "Warning: %s\n", t->pub.runtime.warnstr);
-    }
     {
         tcpedit_batch_result_t r;
         tcpedit_batch_result(b, &r);
-        if (r.out_len >= 24 + 16) {
-            uint32_t oc, ol;
-            memcpy(&oc, res + 64 + 24 + 8, 4);
-            memcpy(&ol, res + 64 + 24 + 12, 4);
-            if (oc > 262166u || 40 + (uint64_t)oc > 24 + b->out_cap) {
-                te_seterr(t, "packet %llu: output record of %u bytes", (unsigned long long)t->pub.runtime.packetnum, oc);
-                rc = TCPEDIT_ERROR;
-                goto out;
-            }
-            memcpy(*pktdata, res + 64 + 40, oc);
-            h->caplen = oc;
-            h->len = ol;
-        } else {
-            h->caplen = 0; /* edited down to zero bytes */
-        }
+        rc = packet_result(t, h, pktdata, st, res + 64, r.out_len, 24 + b->out_cap);
     }
 out:
 fail:
@@ -2798,6 +3416,11 @@ int tcpedit_close(tcpedit_t **tp)
             free(t->stack[k][i]);
     }
     free(t->portlut);
+    srv_free(t);
+    for (int w = 0; w < 4; w++) {
+        free(t->cspill[w]);
+        hipFree(t->d_cspill[w]);
+    }
     tcpedit_batch_close(t->one);
     hipFree(t->d_cfg);
     hipFree(t->d_portlut);
@@ -2810,6 +3433,20 @@ int tcpedit_close(tcpedit_t **tp)
     free(t);
     *tp = NULL;
     return 0;
+}
+
+uint64_t tcpedit_shard_place(int n, const uint64_t *seg_bytes, const int *hard_error, uint64_t *offset,
+                             uint64_t *write)
+{
+    uint64_t pos = 24;
+    int failed = 0;
+    for (int k = 0; k < n; k++) {
+        offset[k] = pos;
+        write[k] = failed ? 0 : seg_bytes[k];
+        pos += write[k];
+        failed |= hard_error[k] != 0;
+    }
+    return pos;
 }
 
 int64_t tcpedit_pcap_shards(const void *pcap, size_t len, int n, uint64_t *off, uint64_t *pkt_base)

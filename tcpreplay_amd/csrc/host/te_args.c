@@ -266,17 +266,42 @@ static int parse_pair(char *piece, te_cidrmap_t *m)
     return 1;
 }
 
+/* the map a parse fills (cfg.cidr_spill order: cidrmap1, cidrmap2, srcipmap, dstipmap) */
+static int cmap_which(tcpedit_t *t, const te_cidrmap_t *out)
+{
+    return out == t->cfg.cidrmap1 ? 0 : out == t->cfg.cidrmap2 ? 1 : out == t->cfg.srcipmap ? 2 : 3;
+}
+
+/* parse_cidr_map (cidr.c:380-418): the list is unbounded; its first TE_MAX_CIDRMAP pairs
+   go inline into the config, the rest into the context's spill list (on the device with
+   the config) */
 static int parse_cidr_map(tcpedit_t *t, const char *arg, te_cidrmap_t *out, int32_t *nout, const char *what)
 {
     char *s = strdup(arg), *save = NULL;
-    int n = 0, ok = 1;
+    int n = 0, ok = 1, cap = 0;
+    const int w = cmap_which(t, out);
+    free(t->cspill[w]);
+    t->cspill[w] = NULL;
     for (char *piece = strtok_r(s, ",", &save); piece; piece = strtok_r(NULL, ",", &save)) {
-        if (n >= TE_MAX_CIDRMAP) {
-            te_seterr(t, "%s: more than %d CIDR pairs", what, TE_MAX_CIDRMAP);
-            ok = 0;
-            break;
+        te_cidrmap_t m;
+        int rc = parse_pair(piece, &m);
+        if (rc > 0) {
+            if (n < TE_MAX_CIDRMAP) {
+                out[n] = m;
+            } else {
+                if (n - TE_MAX_CIDRMAP >= cap) {
+                    cap = cap ? 2 * cap : 16;
+                    te_cidrmap_t *g = realloc(t->cspill[w], sizeof(te_cidrmap_t) * (size_t)cap);
+                    if (!g) {
+                        te_seterr(t, "out of memory");
+                        ok = 0;
+                        break;
+                    }
+                    t->cspill[w] = g;
+                }
+                t->cspill[w][n - TE_MAX_CIDRMAP] = m;
+            }
         }
-        int rc = parse_pair(piece, &out[n]);
         if (rc < 0) {
             te_seterr(t, "Unable to parse as a valid CIDR: %s", piece);
             ok = 0;
@@ -734,6 +759,17 @@ int te_derive_cfg(tcpedit_t *t)
     if (c->n_cidrmap1 && !c->n_cidrmap2) { /* :89-94 one -N serves both directions */
         memcpy(c->cidrmap2, c->cidrmap1, sizeof(c->cidrmap1));
         c->n_cidrmap2 = c->n_cidrmap1;
+        free(t->cspill[1]);
+        t->cspill[1] = NULL;
+        if (c->n_cidrmap1 > TE_MAX_CIDRMAP) {
+            const size_t nb = sizeof(te_cidrmap_t) * (size_t)(c->n_cidrmap1 - TE_MAX_CIDRMAP);
+            t->cspill[1] = malloc(nb);
+            if (!t->cspill[1]) {
+                te_seterr(t, "out of memory");
+                return -1;
+            }
+            memcpy(t->cspill[1], t->cspill[0], nb);
+        }
     }
     c->fixcsum = t->have[OPT_FIXCSUM] != 0;
     c->fixhdrlen = t->have[OPT_FIXHDRLEN] != 0;

@@ -64,6 +64,9 @@ struct tcpedit_s {
     /* derived per-run tables */
     te_dev_cfg_t cfg;
     uint16_t *portlut;            /* host copy, 65536 entries, or NULL */
+    te_cidrmap_t *cspill[4];      /* CIDR map entries past TE_MAX_CIDRMAP (cfg.cidr_spill order) */
+    te_cidrmap_t *d_cspill[4];    /* ... on the device (uploaded with the config) */
+    int32_t d_cspill_n[4];
     uint32_t fuzz_seed, fuzz_factor;
     int post_args_done;
     /* --fuzz-seed state seeding (fuzzing_init): the device word was seeded ... */
@@ -80,6 +83,7 @@ struct tcpedit_s {
     uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */
     struct te_pipe_s *pipe;       /* tcpedit_rewrite_pcap_pipelined's slots and streams (kept) */
+    struct te_srv_s *srv;         /* tcpedit_packet's resident server (te_packet_server), or NULL */
     int pipe_err;                 /* that call hit a hard error */
 };
 
@@ -102,6 +106,7 @@ int te_autoopts_import(tcpedit_t *t); /* 1 imported, 0 no descriptor, -1 error (
 extern uint64_t te_fuzz_init_gen; /* fuzzing_init calls so far, and their values */
 extern uint32_t te_fuzz_init_seed, te_fuzz_init_factor;
 typedef struct te_pipe_s te_pipe_t;
+typedef struct te_srv_s te_srv_t;
 void te_pipe_free(tcpedit_t *t);
 
 /* te_pcapng.c: a pcapng image as libpcap's reader delivers it (classic pcap, microseconds) */

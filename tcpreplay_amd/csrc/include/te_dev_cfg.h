@@ -98,7 +98,19 @@ typedef struct {
        into the en10mb encoder without --enet-dmac; te_l2carry_mark + a max scan) */
     int32_t decoder;
     uint32_t l2carry;
+    /* CIDR maps longer than TE_MAX_CIDRMAP pairs (the reference's lists are unbounded,
+       cidr.c:290-418): device addresses of entries TE_MAX_CIDRMAP.. of cidrmap1, cidrmap2,
+       srcipmap and dstipmap (0: none), read through TE_CMAP */
+    uint64_t cidr_spill[4];
 } te_dev_cfg_t;
+
+/* entry i of CIDR map w (0 cidrmap1, 1 cidrmap2, 2 srcipmap, 3 dstipmap): the first
+   TE_MAX_CIDRMAP inline, the rest in the spill list */
+#define TE_CMAP_INLINE(c, w, i) \
+    ((w) == 0 ? (c).cidrmap1[i] : (w) == 1 ? (c).cidrmap2[i] : (w) == 2 ? (c).srcipmap[i] : (c).dstipmap[i])
+#define TE_CMAP(c, w, i)                                                                                   \
+    ((i) < TE_MAX_CIDRMAP ? TE_CMAP_INLINE(c, w, i)                                                        \
+                          : ((const te_cidrmap_t *)(uintptr_t)(c).cidr_spill[w])[(i) - TE_MAX_CIDRMAP])
 
 /* Per-packet status byte written by the device (one per input record). */
 enum {

@@ -156,6 +156,38 @@ typedef struct {
                                  generic kernel's instance that carries them */
 } te_launch_t;
 
+/* tcpedit_packet's resident server (te_packet_server, one block): a control block in
+ * host-mapped fine-grained memory.  The host writes the record at byte 24 of the mapped
+ * input image, fills the request words and stores seq (release); the kernel, polling seq,
+ * edits the record into the mapped output image (record at byte 24), writes the response
+ * words and stores done = seq (release).  It leaves when stop is set or after idle_ticks
+ * of the 100 MHz real-time clock without a request, storing alive = 0. */
+typedef struct {
+    uint32_t seq;       /* host: the request number */
+    uint32_t stop;      /* host: 1 = leave now */
+    uint32_t done;      /* device: the last request served */
+    uint32_t alive;     /* host: 1 before a launch; device: 0 when it leaves */
+    int32_t dir;        /* request: the direction (tcpedit_packet's argument) */
+    uint32_t caplen;    /* request: the record's caplen (its 16-byte header is in the image) */
+    uint64_t pkt_base;  /* request: 0-based packet number of the record */
+    /* response */
+    uint32_t status;    /* the record's TE_ST_* byte */
+    uint32_t pad_;
+    uint64_t bytes_out, packets, edited; /* the record's counters (TE_CNT_*) */
+} te_srv_ctl_t;
+
+typedef struct {
+    te_srv_ctl_t *ctl;         /* device address of the mapped control block */
+    const te_dev_cfg_t *cfg;   /* device: the server's config (copied to LDS at launch) */
+    const uint16_t *portlut;   /* device, or NULL */
+    const uint8_t *in;         /* device address of the mapped input image */
+    uint8_t *out;              /* device address of the mapped output image */
+    uint8_t *scratch;          /* device: TE_SRV_SCRATCH bytes (status, counters, error words) */
+    uint32_t start_seq;        /* the last request served before this launch */
+    uint64_t idle_ticks;       /* leave after this long without a request (100 MHz ticks) */
+} te_srv_launch_t;
+#define TE_SRV_SCRATCH 1024
+
 /* scan scratch the dst_modified carry needs for a launch of n_pkts records */
 size_t te_l2carry_temp_bytes(uint32_t n_pkts);
 
@@ -168,6 +200,7 @@ uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz);
 int te_launch_edit(te_launch_t *L, hipStream_t stream);
 int te_launch_q8(te_launch_t *L, hipStream_t stream);
 int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
+int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
 /* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */

@@ -64,6 +64,14 @@ struct Pkt {
                   // encoder's memmove, --fixlen=pad, fuzz writes): te_q8_replay's buffer view
     bool strict;  // te_q8_replay: a fuzz XOR of a byte past `phys` is a stale read too
     u8 l2carry = 0;  // the en10mb encoder's dst_modified as the last C2S record left it (Q18)
+    // the generic lane's tile (LDS) path: do_checksum leaves the L4 payload sum to the block
+    // (all 256 threads sum every record's L4 bytes in 64-byte pieces) and records the job;
+    // the lane writes the field once the block has summed (tile_body)
+    bool defer = false;
+    u8 *job_l4 = nullptr;   // first byte summed
+    int job_len = 0;        // bytes summed (0: no job)
+    u8 *job_field = nullptr;
+    u32 job_base = 0;       // the pseudo header's sum, added to the payload's
 };
 
 // a read of bytes [.., end) from d that lie past the packet's physical bytes: the
@@ -324,7 +332,9 @@ DI uint32_t quad_sum_masked(const uint4 v, int off, int lo, int hi, uint32_t acc
                                  wsum_acc16(v.z & dmask(lo - off - 8, hi - off - 8),
                                             wsum_acc16(v.w & dmask(lo - off - 12, hi - off - 12), acc))));
 }
-DI u32 csum_bytes(const u8 *p, int len) {
+// the sum of bytes [p, p + len) with absolute weights (a byte at an even address is the
+// low byte of its 16-bit word), unfolded: csum_bytes folds it and swaps for an odd p
+DI unsigned long long sum_abs(const u8 *p, int len) {
     if (len <= 0) return 0;
     const int h = (int)((uintptr_t)p & 15u);  // p's byte within its quad
     const uint4 *Q = (const uint4 *)(p - h);   // (same granule as p: pointer arithmetic keeps the address space)
@@ -338,11 +348,22 @@ DI u32 csum_bytes(const u8 *p, int len) {
     }
     for (; k < nq - 1; ++k) s += quad_sum(Q[k], 0u);
     if (nq > 1) s += quad_sum_masked(Q[nq - 1], 16 * (nq - 1), h, hi, 0u);
-    u32 f = fold16(s);
-    if (h & 1) f = ((f >> 8) | (f << 8)) & 0xffff;  // absolute -> relative weights
+    return s;
+}
+DI u32 csum_bytes(const u8 *p, int len) {
+    if (len <= 0) return 0;
+    u32 f = fold16(sum_abs(p, len));
+    if ((uintptr_t)p & 1u) f = ((f >> 8) | (f << 8)) & 0xffff;  // absolute -> relative weights
     return f;
 }
 #endif
+// a deferred job's payload sum (the fold of its pieces' absolute-weight sums) -> the sum
+// csum_bytes(job_l4, job_len) would have returned
+DI u32 csum_of_job(const u8 *l4, u32 abs_sum) {
+    u32 f = fold16(abs_sum);
+    if ((uintptr_t)l4 & 1u) f = ((f >> 8) | (f << 8)) & 0xffff;
+    return f;
+}
 
 // CHECKSUM_CARRY (checksum.h:25) applied to a plain non-negative sum
 DI u16 csum_carry(unsigned long long x) { return (u16)(~fold16(x) & 0xffff); }
@@ -463,6 +484,16 @@ DI int remap_ipv6(const te_dev_cfg_t &cfg, const te_cidr_t &c, u8 *addr, int roo
     return 0;
 }
 
+// the tile path: leave the payload sum of [l4, l4 + n) to the block (Pkt.defer)
+DI bool defer_sum(Pkt &pk, u8 *l4, int n, u8 *field, unsigned long long base) {
+    if (!pk.defer) return false;
+    pk.job_l4 = l4;
+    pk.job_len = n;
+    pk.job_field = field;
+    pk.job_base = (u32)base;  // (pseudo header + length word: far below 2^32)
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // Full checksum: do_checksum (checksum.c:34-170).  `ip` = L3 header, `end` =
 // offset of end_ptr.  Reads past the materialised slot mark the packet.
@@ -499,6 +530,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
             st16(l4 + 16, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
             sum += bswap16((u16)(6 + len));
+            if (defer_sum(pk, l4, readable(len), l4 + 16, sum)) break;
             sum += csum_bytes(l4, readable(len));
             st16(l4 + 16, csum_carry(sum));
             break;
@@ -510,6 +542,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
             st16(l4 + 6, 0);
             sum = v6 ? csum_bytes(ip + 8, 32) : csum_bytes(ip + 12, 8);
             sum += bswap16((u16)(17 + len));
+            if (defer_sum(pk, l4, readable(len), l4 + 6, sum)) break;
             sum += csum_bytes(l4, readable(len));
             st16(l4 + 6, csum_carry(sum));
             break;
@@ -526,6 +559,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
                 sum = f;
                 st16(l4 + 2, (u16)(~(f + (f >> 16)) & 0xffff));
             }
+            if (defer_sum(pk, l4, readable(len), l4 + 2, sum)) break;
             sum += csum_bytes(l4, readable(len));
             st16(l4 + 2, csum_carry(sum));
             break;
@@ -536,6 +570,7 @@ DI int do_checksum(Pkt &pk, u8 *ip, int proto, int len, int end) {
             st16(l4 + 2, 0);
             if (v6) sum = csum_bytes(ip + 8, 32);
             sum += bswap16((u16)(58 + len));
+            if (defer_sum(pk, l4, readable(len), l4 + 2, sum)) break;
             sum += csum_bytes(l4, readable(len));
             st16(l4 + 2, csum_carry(sum));
             break;
@@ -715,38 +750,40 @@ DI void rewrite_seqs(Pkt &pk, const te_dev_cfg_t &cfg, u8 *tcp) {
 // ---------------------------------------------------------------------------
 DI void rewrite_ipv4l3(const te_dev_cfg_t &cfg, u8 *ip, int dir, int len) {
     for (int m = 0; m < cfg.n_srcipmap; ++m) {
-        if (ip_in_cidr(cfg.srcipmap[m].from, ld32(ip + 12))) {
+        const te_cidrmap_t &e = TE_CMAP(cfg, 2, m);
+        if (ip_in_cidr(e.from, ld32(ip + 12))) {
             u32 o = ld32(ip + 12);
-            st32(ip + 12, remap_ipv4(cfg, cfg.srcipmap[m].to, o));
+            st32(ip + 12, remap_ipv4(cfg, e.to, o));
             ipv4_addr_csum_replace(ip, o, ld32(ip + 12), len);
             break;
         }
     }
     for (int m = 0; m < cfg.n_dstipmap; ++m) {
-        if (ip_in_cidr(cfg.dstipmap[m].from, ld32(ip + 16))) {
+        const te_cidrmap_t &e = TE_CMAP(cfg, 3, m);
+        if (ip_in_cidr(e.from, ld32(ip + 16))) {
             u32 o = ld32(ip + 16);
-            st32(ip + 16, remap_ipv4(cfg, cfg.dstipmap[m].to, o));
+            st32(ip + 16, remap_ipv4(cfg, e.to, o));
             ipv4_addr_csum_replace(ip, o, ld32(ip + 16), len);
             break;
         }
     }
     if (cfg.n_cidrmap1 == 0) return;
-    const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
-    const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+    const int w1 = dir == TE_DIR_C2S ? 0 : 1, w2 = 1 - w1;
     int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
     int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
     int i1 = 0, i2 = 0;
     bool didsrc = false, diddst = false;
     for (;;) {
-        if (!diddst && ip_in_cidr(l2[i2].from, ld32(ip + 16))) {
+        const te_cidrmap_t &e2 = TE_CMAP(cfg, w2, i2), &e1 = TE_CMAP(cfg, w1, i1);
+        if (!diddst && ip_in_cidr(e2.from, ld32(ip + 16))) {
             u32 o = ld32(ip + 16);
-            st32(ip + 16, remap_ipv4(cfg, l2[i2].to, o));
+            st32(ip + 16, remap_ipv4(cfg, e2.to, o));
             ipv4_addr_csum_replace(ip, o, ld32(ip + 16), len);
             diddst = true;
         }
-        if (!didsrc && ip_in_cidr(l1[i1].from, ld32(ip + 12))) {
+        if (!didsrc && ip_in_cidr(e1.from, ld32(ip + 12))) {
             u32 o = ld32(ip + 12);
-            st32(ip + 12, remap_ipv4(cfg, l1[i1].to, o));
+            st32(ip + 12, remap_ipv4(cfg, e1.to, o));
             ipv4_addr_csum_replace(ip, o, ld32(ip + 12), len);
             didsrc = true;
         }
@@ -772,30 +809,34 @@ DI void rewrite_ipv6_addr_pair(Pkt &pk, const te_dev_cfg_t &cfg, const te_cidr_t
 DI void rewrite_ipv6l3(Pkt &pk, const te_dev_cfg_t &cfg, u8 *ip6, int dir, int l3len) {
     // the ICMPv6-error recursion (:988-1013) is walked iteratively
     for (int depth = 0; depth < 64; ++depth) {
-        for (int m = 0; m < cfg.n_srcipmap; ++m)
-            if (ip6_in_cidr(cfg.srcipmap[m].from, ip6 + 8)) {
-                rewrite_ipv6_addr_pair(pk, cfg, cfg.srcipmap[m].to, ip6, 8, l3len);
+        for (int m = 0; m < cfg.n_srcipmap; ++m) {
+            const te_cidrmap_t &e = TE_CMAP(cfg, 2, m);
+            if (ip6_in_cidr(e.from, ip6 + 8)) {
+                rewrite_ipv6_addr_pair(pk, cfg, e.to, ip6, 8, l3len);
                 break;
             }
-        for (int m = 0; m < cfg.n_dstipmap; ++m)
-            if (ip6_in_cidr(cfg.dstipmap[m].from, ip6 + 24)) {
-                rewrite_ipv6_addr_pair(pk, cfg, cfg.dstipmap[m].to, ip6, 24, l3len);
+        }
+        for (int m = 0; m < cfg.n_dstipmap; ++m) {
+            const te_cidrmap_t &e = TE_CMAP(cfg, 3, m);
+            if (ip6_in_cidr(e.from, ip6 + 24)) {
+                rewrite_ipv6_addr_pair(pk, cfg, e.to, ip6, 24, l3len);
                 break;
             }
+        }
         if (cfg.n_cidrmap1 != 0) {
-            const te_cidrmap_t *l1 = dir == TE_DIR_C2S ? cfg.cidrmap1 : cfg.cidrmap2;
-            const te_cidrmap_t *l2 = dir == TE_DIR_C2S ? cfg.cidrmap2 : cfg.cidrmap1;
+            const int w1 = dir == TE_DIR_C2S ? 0 : 1, w2 = 1 - w1;
             int n1 = dir == TE_DIR_C2S ? cfg.n_cidrmap1 : cfg.n_cidrmap2;
             int n2 = dir == TE_DIR_C2S ? cfg.n_cidrmap2 : cfg.n_cidrmap1;
             int i1 = 0, i2 = 0;
             bool didsrc = false, diddst = false;
             for (;;) {
-                if (!diddst && ip6_in_cidr(l2[i2].from, ip6 + 24)) {
-                    rewrite_ipv6_addr_pair(pk, cfg, l2[i2].to, ip6, 24, l3len);
+                const te_cidrmap_t &e2 = TE_CMAP(cfg, w2, i2), &e1 = TE_CMAP(cfg, w1, i1);
+                if (!diddst && ip6_in_cidr(e2.from, ip6 + 24)) {
+                    rewrite_ipv6_addr_pair(pk, cfg, e2.to, ip6, 24, l3len);
                     diddst = true;
                 }
-                if (!didsrc && ip6_in_cidr(l1[i1].from, ip6 + 8)) {
-                    rewrite_ipv6_addr_pair(pk, cfg, l1[i1].to, ip6, 8, l3len);
+                if (!didsrc && ip6_in_cidr(e1.from, ip6 + 8)) {
+                    rewrite_ipv6_addr_pair(pk, cfg, e1.to, ip6, 8, l3len);
                     didsrc = true;
                 }
                 if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {
@@ -842,12 +883,11 @@ DI bool arp_addrs(Pkt &pk, u8 *arp, u8 **ip1, u8 **ip2) {
 }
 
 DI void rewrite_iparp(Pkt &pk, const te_dev_cfg_t &cfg, u8 *arp, int dir) {
-    const te_cidrmap_t *l1 = nullptr, *l2 = nullptr;
-    int n1 = 0, n2 = 0;
+    int w1 = 0, w2 = 1, n1 = 0, n2 = 0;
     if (dir == TE_DIR_C2S) {
-        l1 = cfg.cidrmap1; n1 = cfg.n_cidrmap1; l2 = cfg.cidrmap2; n2 = cfg.n_cidrmap2;
+        n1 = cfg.n_cidrmap1; n2 = cfg.n_cidrmap2;
     } else if (dir == TE_DIR_S2C) {
-        l1 = cfg.cidrmap2; n1 = cfg.n_cidrmap2; l2 = cfg.cidrmap1; n2 = cfg.n_cidrmap1;
+        w1 = 1; w2 = 0; n1 = cfg.n_cidrmap2; n2 = cfg.n_cidrmap1;
     }
     if (n1 == 0 || n2 == 0) return;
     u8 *ip1, *ip2;
@@ -857,12 +897,13 @@ DI void rewrite_iparp(Pkt &pk, const te_dev_cfg_t &cfg, u8 *arp, int dir) {
     bool didsrc = false, diddst = false;
     for (;;) {
         u8 *dsta = request ? ip1 : ip2, *srca = request ? ip2 : ip1;
-        if (!diddst && ip_in_cidr(l2[i2].from, ld32(dsta))) {
-            st32(dsta, remap_ipv4(cfg, l2[i2].to, ld32(dsta)));
+        const te_cidrmap_t &e2 = TE_CMAP(cfg, w2, i2), &e1 = TE_CMAP(cfg, w1, i1);
+        if (!diddst && ip_in_cidr(e2.from, ld32(dsta))) {
+            st32(dsta, remap_ipv4(cfg, e2.to, ld32(dsta)));
             diddst = true;
         }
-        if (!didsrc && ip_in_cidr(l1[i1].from, ld32(srca))) {
-            st32(srca, remap_ipv4(cfg, l1[i1].to, ld32(srca)));
+        if (!didsrc && ip_in_cidr(e1.from, ld32(srca))) {
+            st32(srca, remap_ipv4(cfg, e1.to, ld32(srca)));
             didsrc = true;
         }
         if (!(diddst && didsrc) && !(i1 + 1 >= n1 && i2 + 1 >= n2)) {

@@ -193,8 +193,9 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     const bool c2s = dir == TE_DIR_C2S;
 
     u32 dirty = 0;
-    // ---- en10mb_encode: MAC rewrite (no VLAN, subsmac or mac-seed here) ----
-    if ((F & F_MAC) && cfg.mac_mask) {
+    // ---- en10mb_encode: MAC rewrite, then --enet-subsmac and --enet-mac-seed over the new
+    // addresses (en10mb.c:586-689; en10mb_mac_rules) ----
+    if ((F & F_MAC) && (cfg.mac_mask || cfg.n_subs || cfg.random_set)) {
         const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
         unsigned long long dmac = (unsigned long long)hi16(H[0]) | ((unsigned long long)H[1] << 16);
         unsigned long long smac = (unsigned long long)H[2] | ((unsigned long long)lo16(H[3]) << 32);
@@ -202,6 +203,30 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
         const bool use_d = (cfg.mac_mask & dm) && (!cfg.l2_skip_broadcast || unicast48(dmac));
         smac = use_s ? mac48(c2s ? cfg.intf1_smac : cfg.intf2_smac) : smac;
         dmac = use_d ? mac48(c2s ? cfg.intf1_dmac : cfg.intf2_dmac) : dmac;
+        // subsmac: the list in order, each entry seeing the earlier entries' rewrites
+        for (int e = 0; e < cfg.n_subs; ++e) {
+            const unsigned long long tg = mac48(cfg.subs[e]), rw = mac48(cfg.subs[e] + 6);
+            dmac = dmac == tg ? rw : dmac;
+            smac = smac == tg ? rw : smac;
+        }
+        if (cfg.random_set) {  // MAC_MASK_APPLY (en10mb.h:29-30) on the bytes past the kept ones
+            const bool us = unicast48(smac), ud = unicast48(dmac);
+            unsigned long long s2 = 0, d2 = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {  // per byte, u8 arithmetic (the subtraction wraps in the byte)
+                const u32 m = i >= cfg.random_keep ? (u32)cfg.random_mask[i] : 0u;
+                const u32 mS = us ? m : 0u, mD = ud ? m : 0u;
+                const u32 xs = (u32)(smac >> (8 * i)) & 0xffu, xd = (u32)(dmac >> (8 * i)) & 0xffu;
+                s2 |= (unsigned long long)(((xs ^ mS) - (xs & mS)) & 0xffu) << (8 * i);
+                d2 |= (unsigned long long)(((xd ^ mD) - (xd & mD)) & 0xffu) << (8 * i);
+            }
+            smac = s2;
+            dmac = d2;
+            if (!cfg.random_keep) {
+                smac &= us ? ~1ull : ~0ull;
+                dmac &= ud ? ~1ull : ~0ull;
+            }
+        }
         H[0] = with_hi16(H[0], (u32)dmac);
         H[1] = (u32)(dmac >> 16);
         H[2] = (u32)smac;

@@ -175,15 +175,32 @@ __device__ __forceinline__ unsigned long long lookback(unsigned long long *state
     return excl;
 }
 
+constexpr int JPIECE = 64;                                       // bytes of a deferred-sum piece
+constexpr int JMAP = (TE_SLOT_BYTES + 64) / JPIECE + TE_MAX_PKTS;  // pieces of a tile, at most
 struct TileShared {
-    uint32_t rel[TE_MAX_PKTS + 1];   // record offset in span (+ sentinel)
+    uint32_t rel[TE_MAX_PKTS + 1];   // record offset in span (+ sentinel); after the span load:
+                                     // each record's deferred L4 sum (the pieces' folded sums)
     uint32_t rpos[TE_MAX_PKTS];      // slot position of the output record start
-    uint32_t opfx[TE_MAX_PKTS + 1];  // exclusive output prefix (+ total)
+    uint32_t opfx[TE_MAX_PKTS + 1];  // exclusive output prefix (+ total); before the placement:
+                                     // each record's deferred L4 sum start (slot offset)
     uint32_t wsum[NWAVES];
     unsigned long long cnt[TE_CNT__N];
     unsigned long long out_excl;
     uint32_t tile_id;
     uint32_t ident;                  // every record kept its input size (contiguous output)
+};
+
+// the LDS tile path's deferred L4 sums: per record (bytes << 16 | first piece), piece -> record;
+// then (the sums done) the store's output chunk -> the record holding its first byte
+constexpr int CMAP = (TE_SLOT_BYTES + LDS_FRONT + 64) / 16 + 2;
+struct JobShared {
+    union {
+        struct {
+            uint32_t jlp[TE_MAX_PKTS];
+            uint8_t jmap[JMAP];
+        };
+        uint8_t cmap[CMAP];
+    };
 };
 
 // 16 bytes of the slot buffer starting at byte `base` (any alignment): five
@@ -233,7 +250,7 @@ __shared__ unsigned long long gk_ph[6], gk_last;
 // ---------------------------------------------------------------------------
 template <int MODE, bool FZ, typename P, bool AD = false>
 __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &tile, uint32_t t, P S,
-                                          TileShared &sh, const te_dev_cfg_t &cfg) {
+                                          TileShared &sh, const te_dev_cfg_t &cfg, JobShared *js) {
     const int tid = threadIdx.x;
     const uint32_t npkt = tile.npkt;
     const uint64_t G0 = tile.span_off;  // HBM offset of the span
@@ -327,6 +344,11 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     uint32_t out_sz = 0, need = 0;
     uint8_t st = 0;
     unsigned long long c_in = 0;
+    // deferred L4 sums: the LDS tile path only (a huge record's HBM slot sums in its lane)
+    constexpr bool kDefer = __is_same(P, uint8_t *);
+    bool job = false;
+    uint8_t *job_l4 = nullptr, *job_field = nullptr;
+    uint32_t job_base = 0, njob = 0;
     if (tid < (int)npkt) {
         uint8_t *rec = (uint8_t *)(S + r0);
         if constexpr (MODE == MODE_SLOT)  // zero the room after the data (chunk stores spilled into it)
@@ -357,6 +379,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         pk.ext = caplen;
         pk.strict = false;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[tile.first_pkt + tid] & 1u) : 0;
+        pk.defer = kDefer;
         int rc = RC_OK;
         bool warned = false;
         if (dir == TE_DIR_NOSEND && !explicit_dir) {  // tcprewrite.c:314-315: written unedited
@@ -402,9 +425,44 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         sh.rpos[tid] = (uint32_t)(orec - (uint8_t *)S);
         if (write) out_sz = 16 + pk.caplen;
         ((g_u8 *)a.status)[tile.first_pkt + tid] = st;
+        if constexpr (kDefer) {
+            job = pk.job_field != nullptr;
+            job_l4 = pk.job_l4;
+            job_field = pk.job_field;
+            job_base = pk.job_base;
+            njob = job ? (uint32_t)pk.job_len : 0u;
+        }
     }
     GK_STAMP(2);  // edit (wave 0's lanes)
     if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) return;  // the reach pass writes nothing else
+
+    // ---- the deferred L4 payload sums (do_checksum, checksum.c:34-170): one packet a lane
+    // left a 1514-byte sum to one lane while its neighbours' 64-byte packets were done, so
+    // every record's payload is cut into 64-byte pieces and the block's 256 threads sum the
+    // pieces (aligned LDS quads, absolute weights), adding each into its record's slot;
+    // then each lane writes its checksum field as csum_bytes + CHECKSUM_CARRY would ----
+    if constexpr (kDefer) {
+        uint32_t npiece = (njob + JPIECE - 1) / JPIECE, tot_pieces;
+        const uint32_t pb = block_exscan(npiece, sh.wsum, tot_pieces);
+        if (tot_pieces) {  // (block-uniform)
+            // (tot_pieces <= sum of ceil(len / 64) <= slot bytes / 64 + records = JMAP)
+            if (tid < (int)npkt) {
+                sh.opfx[tid] = (uint32_t)(job_l4 - (uint8_t *)S);
+                js->jlp[tid] = njob << 16 | pb;
+                sh.rel[tid] = 0;
+                for (uint32_t q = 0; q < npiece; ++q) js->jmap[pb + q] = (uint8_t)tid;
+            }
+            __syncthreads();
+            for (uint32_t p = tid; p < tot_pieces; p += BLOCK) {
+                const uint32_t j = js->jmap[p], lp = js->jlp[j];
+                const uint32_t off = (p - (lp & 0xffffu)) * JPIECE, n = umin32(JPIECE, (lp >> 16) - off);
+                const uint8_t *pp = (const uint8_t *)S + sh.opfx[j] + off;
+                atomicAdd(&sh.rel[j], fold16(sum_abs(pp, (int)n)));
+            }
+            __syncthreads();
+            if (job) st16(job_field, csum_carry((unsigned long long)job_base + csum_of_job(job_l4, sh.rel[tid])));
+        }
+    }
 
     // ---- tile output offsets ----
     // static_off: sizes are preserved, so output offsets are the input offsets
@@ -501,6 +559,20 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
     const bool ident = MODE == MODE_CONTIG && (stat || sh.ident != 0);
     const uint32_t src0 = sh.rpos[0];  // ident: output byte q is slot byte src0 + q
     g_u8 *gout = (g_u8 *)a.out;
+    if (kDefer && !ident) {
+        // the chunk map: every record marks the output chunks whose first byte it holds
+        // (chunk c's first byte is tile byte max(16 c - g, 0)), so a chunk finds its first
+        // record in one LDS read instead of a binary search over the tile's records
+        const uint32_t g = (uint32_t)(Gs - C0);
+        if (tid < (int)npkt) {
+            const uint32_t s0 = sh.opfx[tid], s1 = sh.opfx[tid + 1];
+            if (s1 > s0) {
+                const uint32_t c_lo = s0 == 0 ? 0u : (s0 + g + 15) >> 4, c_hi = (s1 + g + 15) >> 4;
+                for (uint32_t c = c_lo; c < c_hi && c < (uint32_t)CMAP; ++c) js->cmap[c] = (uint8_t)tid;
+            }
+        }
+        __syncthreads();
+    }
     for (uint32_t c = tid; c < nchunks; c += BLOCK) {
         const uint64_t C = C0 + ((uint64_t)c << 4);
         const int64_t q0 = (int64_t)C - (int64_t)Gs;  // tile-relative output offset of the chunk
@@ -510,13 +582,18 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (ident) {
             v = read16(S, (uint32_t)((int64_t)src0 + q0));
         } else {
-            // records overlapping the chunk: binary search the first, then walk
+            // records overlapping the chunk: the first from the chunk map (the HBM slot path:
+            // a binary search), then walk
             const int64_t qf = q0 + b0;
             int lo = 0, hi = (int)npkt - 1;
-            while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
-                if ((int64_t)sh.opfx[mid] <= qf) lo = mid;
-                else hi = mid - 1;
+            if (kDefer) {
+                lo = js->cmap[c];
+            } else {
+                while (lo < hi) {
+                    int mid = (lo + hi + 1) >> 1;
+                    if ((int64_t)sh.opfx[mid] <= qf) lo = mid;
+                    else hi = mid - 1;
+                }
             }
             v = make_uint4(0, 0, 0, 0);
             for (int p = lo; p < (int)npkt && (int64_t)sh.opfx[p] < q0 + b1; ++p) {
@@ -559,7 +636,7 @@ __device__ __attribute__((noinline)) void huge_tile(const TE_AS_CONST LaunchArgs
     const LaunchArgs &a = *(const LaunchArgs *)ka;
     __shared__ TileShared hsh;
     const te_tile_t tile = a.tiles[t];
-    tile_body<MODE_SLOT, FZ, g_u8 *, AD>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg);
+    tile_body<MODE_SLOT, FZ, g_u8 *, AD>(a, tile, t, (g_u8 *)(a.scratch + tile.scratch_off), hsh, cfg, nullptr);
 }
 
 #ifndef TE_MIN_WAVES
@@ -570,6 +647,7 @@ template <int MODE, bool FZ = false, bool AD = false>
 __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
+    __shared__ JobShared js;
     __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;  // per-run tables, read uniformly by every lane
     const bool listed = a.tile_list != nullptr;
     if (a.counters_next && blockIdx.x == 0 && threadIdx.x < TE_CNT__N) a.counters_next[threadIdx.x] = 0;
@@ -601,7 +679,7 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         if (listed) t = a.tile_list[t];
         const te_tile_t tile = a.tiles[t];
         if (tile.scratch_off == TE_NO_SCRATCH)
-            tile_body<MODE, FZ, uint8_t *, AD>(a, tile, t, slots, sh, cfg);
+            tile_body<MODE, FZ, uint8_t *, AD>(a, tile, t, slots, sh, cfg, &js);
         else
             huge_tile<FZ, AD>((const TE_AS_CONST LaunchArgs *)__builtin_amdgcn_kernarg_segment_ptr(), t, cfg);
         __syncthreads();
@@ -611,6 +689,93 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
         printf("GK block %u tiles %u pos %llu load %llu edit %llu place %llu store %llu ticket %llu\n", blockIdx.x,
                gk_nt, gk_ph[0], gk_ph[1], gk_ph[2], gk_ph[3], gk_ph[4], gk_ph[5]);
 #endif
+}
+
+// ===========================================================================
+// te_packet_server: tcpedit_packet (tcpedit.c:46-366) for a caller that edits one record
+// a call.  A launch, a copy each way and a stream sync cost ~100 us a call; this block
+// stays resident instead and serves requests through host-mapped memory (te_srv_ctl_t):
+// the record is read over PCIe straight from the caller-side staging buffer, edited in
+// LDS by the generic lane's tile body (one tile of one record, slot layout, every
+// decoder), and written back over PCIe.  Acquire/release at system scope order the
+// request and response words with the bytes.  The loop ends on `stop` or after
+// idle_ticks without a request, so the grid always drains.
+// ===========================================================================
+__global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
+    __shared__ TileShared sh;
+    __shared__ JobShared js;
+    __shared__ __attribute__((aligned(16))) te_dev_cfg_t cfg;
+    __shared__ uint32_t req, quit;
+    {
+        const uint32_t *src = (const uint32_t *)s.cfg;
+        uint32_t *dst = (uint32_t *)&cfg;
+        for (int i = threadIdx.x; i < (int)(sizeof(te_dev_cfg_t) / 4); i += BLOCK) dst[i] = src[i];
+    }
+    te_srv_ctl_t *ctl = s.ctl;
+    unsigned long long *cnt = (unsigned long long *)(s.scratch + 64);
+    LaunchArgs a = {};
+    a.cfg = s.cfg;
+    a.portlut = s.portlut;
+    a.in = s.in;
+    a.out = s.out;
+    a.out_base = 24;
+    a.status = s.scratch;
+    a.counters = cnt;
+    a.err = cnt + TE_CNT__N;
+    a.tile_state = cnt + TE_CNT__N + 4;
+    a.pkt_rel = (const uint16_t *)(s.scratch + 16);  // one zero word
+    a.n_tiles = 1;
+    a.fuzz_mode = TE_FUZZ_OFF;
+    uint32_t last = s.start_seq;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t v = last, q = 0;
+            for (;;) {
+                v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (v != last) break;
+                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > s.idle_ticks) {
+                    q = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            req = v;
+            quit = q;
+        }
+        __syncthreads();
+        if (quit) break;
+        // the host's stores before its release of seq are visible from here on
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t seq = req;
+        const uint32_t caplen = *(const volatile uint32_t *)&ctl->caplen;
+        a.fixed_dir = *(const volatile int32_t *)&ctl->dir;
+        a.pkt_base = *(const volatile uint64_t *)&ctl->pkt_base;
+        te_tile_t tile;
+        tile.span_off = 24;
+        tile.scratch_off = TE_NO_SCRATCH;
+        tile.first_pkt = 0;
+        tile.npkt = 1;
+        tile.span_len = 16 + caplen;
+        tile.flags = 0;
+        tile_body<MODE_SLOT, false, uint8_t *, true>(a, tile, 0, slots, sh, cfg, &js);
+        // every lane's output stores are complete and visible to the host ...
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ctl->status = *(volatile uint8_t *)s.scratch;  // (this lane's own store: the record's lane)
+            ctl->bytes_out = sh.cnt[TE_CNT_BYTES_OUT];
+            ctl->packets = sh.cnt[TE_CNT_PACKETS];
+            ctl->edited = sh.cnt[TE_CNT_EDITED];
+            // ... before the response words and done
+            __hip_atomic_store(&ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        last = seq;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ===========================================================================
@@ -2091,7 +2256,7 @@ static int wave_pick(uint32_t want, int sz) {
 }
 
 static uint32_t fast_feat(const te_dev_cfg_t *c) {
-    return (c->mac_mask ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
+    return ((c->mac_mask || c->n_subs || c->random_set) ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
            (c->rewrite_ip ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u) |
            ((c->tos >= 0 || c->ttl_mode != TE_TTL_OFF || c->tclass >= 0 || c->flowlabel >= 0 ||
              c->tcp_sequence_enable)
@@ -2432,4 +2597,9 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
                            L->n_pkts, L->l2carry_word);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
+}
+
+extern "C" int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream) {
+    hipLaunchKernelGGL(te_packet_server, dim3(1), dim3(BLOCK), 0, stream, *S);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

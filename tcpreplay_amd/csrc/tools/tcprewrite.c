@@ -12,6 +12,10 @@
  * --pipeline[=MiB] reads the capture straight into page-locked memory and runs
  * the chunked H2D | edit | D2H pipeline (tcpedit_rewrite_pcap_pipelined) instead:
  * the same output bytes, without the per-record checksum warnings.
+ *
+ * --gpus N edits the capture on devices 0..N-1 (tcprewrite_gpus.c): byte-balanced
+ * contiguous shards, one host thread and context per device, one RCCL all-reduce of the
+ * counters, each shard's records copied into its range of the output file.
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -21,6 +25,7 @@
 
 #include "tcpedit.h"
 #include "te_dev_cfg.h"
+#include "tcprewrite_gpus.h"
 
 static void usage(void)
 {
@@ -31,7 +36,8 @@ static void usage(void)
             "    --ttl --tos --tclass --flowlabel --fixlen/-F --dlt --skipl2broadcast --enet-dmac --enet-smac\n"
             "    --enet-subsmac --enet-mac-seed --enet-mac-seed-keep-bytes --enet-vlan --enet-vlan-tag\n"
             "    --enet-vlan-cfi --enet-vlan-pri --enet-vlan-proto\n"
-            "  --pipeline[=MiB]: chunked H2D | edit | D2H from page-locked buffers (no per-record warnings)\n");
+            "  --pipeline[=MiB]: chunked H2D | edit | D2H from page-locked buffers (no per-record warnings)\n"
+            "  --gpus N: edit on devices 0..N-1 (contiguous shards, one RCCL all-reduce of the counters)\n");
 }
 
 static int g_pinned; /* read into page-locked memory (--pipeline) */
@@ -66,6 +72,7 @@ int main(int argc, char **argv)
     tcpedit_t *te = NULL;
 
     size_t pipe_mib = 0;
+    int gpus = 0;
     /* the reference reads the input DLT first (pcap_datalink(pin), tcprewrite.c:80) */
     for (int i = 1; i < argc; i++) {
         if ((!strcmp(argv[i], "-i") || !strcmp(argv[i], "--infile")) && i + 1 < argc)
@@ -76,6 +83,14 @@ int main(int argc, char **argv)
             g_pinned = 1;
         else if (!strncmp(argv[i], "--pipeline=", 11))
             g_pinned = 1, pipe_mib = strtoul(argv[i] + 11, NULL, 10);
+        else if (!strcmp(argv[i], "--gpus") && i + 1 < argc)
+            gpus = atoi(argv[++i]);
+        else if (!strncmp(argv[i], "--gpus=", 7))
+            gpus = atoi(argv[i] + 7);
+    }
+    if (gpus && g_pinned) {
+        fprintf(stderr, "tcprewrite: --gpus and --pipeline are exclusive\n");
+        return 255;
     }
     if (!infile) {
         usage();
@@ -122,6 +137,9 @@ int main(int argc, char **argv)
         } else if (!strcmp(a, "--skip-soft-errors")) {
             skip_soft = 1;
         } else if (!strcmp(a, "--pipeline") || !strncmp(a, "--pipeline=", 11)) {
+        } else if (!strcmp(a, "--gpus") && k + 1 < nun) {
+            k++;
+        } else if (!strncmp(a, "--gpus=", 7)) {
         } else {
             fprintf(stderr, "tcprewrite: unknown argument %s\n", a);
             usage();
@@ -153,6 +171,24 @@ int main(int argc, char **argv)
         return 255;
     }
 
+    if (gpus > 0) { /* the tcpedit options (the arguments tcpedit_parse_args took) to every device */
+        char **opts = calloc((size_t)argc, sizeof(char *));
+        char *tool = calloc((size_t)argc + 1, 1);
+        int nopt = 0;
+        for (int k = 0; k < nun; k++)
+            tool[unused[k] + 1] = 1;
+        for (int i = 1; i < argc; i++)
+            if (!tool[i])
+                opts[nopt++] = argv[i];
+        tcpedit_close(&te);
+        const int grc = tcprewrite_gpus(gpus, dlt, opts, nopt, skip_soft, in, in_len, cache, cache_len, outfile);
+        free(opts);
+        free(tool);
+        free(in);
+        free(cache);
+        free(unused);
+        return grc;
+    }
     if (g_pinned) { /* page-locked capture -> chunked pipeline -> page-locked output -> file */
         const size_t cap = tcpedit_output_bound(te, in, in_len);
         uint8_t *pout = tcpedit_host_alloc(cap > 24 ? cap : 24);

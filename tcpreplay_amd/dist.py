@@ -79,6 +79,22 @@ def plan(pcap, n: int) -> ShardPlan:
     return ShardPlan(list(off), list(base), int(total))
 
 
+def place(sizes: List[int], errs: List[int]):
+    """tcpedit_shard_place (native host code): where each shard's output records go in the
+    job's file with tcprewrite's hard-error rule (tcprewrite.c:156-160) -- returns
+    (offsets, bytes each shard writes, the file's size)"""
+    from . import load
+    L = load()
+    f = L.tcpedit_shard_place
+    f.restype = ctypes.c_uint64
+    f.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int),
+                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    n = len(sizes)
+    off, wr = (ctypes.c_uint64 * n)(), (ctypes.c_uint64 * n)()
+    end = f(n, (ctypes.c_uint64 * n)(*sizes), (ctypes.c_int * n)(*[1 if e else 0 for e in errs]), off, wr)
+    return list(off), list(wr), int(end)
+
+
 def capture_dlt(hdr) -> int:
     """the DLT tcprewrite hands tcpedit_init (pcap_datalink of the file, tcprewrite.c:80):
     the header's link type in the file's byte order, LINKTYPE_RAW (101) as DLT_RAW (12)"""
@@ -186,9 +202,10 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
     sizes = [int(v[0].item()) for v in allv]
     errs = [int(v[1].item()) for v in allv]
     first_err = next((r for r in range(world) if errs[r]), world)
+    offs, writes, end = place(sizes, errs)
     if rank > first_err:
         seg = b""  # records after the first hard error are never written
-    offset = PCAP_HDR_LEN + sum(sizes[:rank]) if rank <= first_err else None
+    offset = offs[rank] if rank <= first_err else None
 
     # 2) the job's counters: one all-reduce
     cnt = torch.tensor(res.counters, dtype=torch.int64, device=cdev)
@@ -196,7 +213,6 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
     counters = dict(zip(COUNTER_NAMES, [int(x) for x in cnt.tolist()]))
 
     if out_path is not None:
-        end = PCAP_HDR_LEN + sum(sizes[:first_err + 1 if first_err < world else world])
         if rank == 0:
             with open(out_path, "wb") as f:
                 f.write(res.image[:PCAP_HDR_LEN])
@@ -369,9 +385,9 @@ def rewrite_file_distributed(in_path: str, args, out_path: str, cache_path: Opti
             if 2 in flags:
                 raise RuntimeError(err or f"rank {flags.index(2)} failed to edit its shard")
             first_err = next((r_ for r_ in range(world) if flags[r_]), world)
-            end = PCAP_HDR_LEN + sum(sizes[:first_err + 1 if first_err < world else world])
-            offset = PCAP_HDR_LEN + sum(sizes[:rank]) if rank <= first_err else None
-            write = sizes[rank] if rank <= first_err else 0
+            offs, writes, end = place(sizes, flags)
+            offset = offs[rank] if rank <= first_err else None
+            write = writes[rank]
 
             cnt = torch.tensor(sh.counters, dtype=torch.int64, device=cdev)
             dist.all_reduce(cnt)

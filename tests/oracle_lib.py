@@ -138,6 +138,29 @@ def replay(pcap: bytes, args):
     return out.raw[:n], int(failed.value)
 
 
+def replay_edit(pcap: bytes, args, loops=1, preload=False):
+    """tcpreplay_edit_oracle_run: `tcpreplay-edit -w out --loop=loops [-K] <args> in.pcap`
+    restated on the CPU.  Returns (rc, the -w file's bytes); rc -1 = the run's errx (the
+    records sent before it kept), ValueError for what the restatement refuses."""
+    lib = load()
+    fn = lib.tcpreplay_edit_oracle_run
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(ctypes.c_char_p), ctypes.c_void_p, ctypes.c_size_t,
+                   ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_int]
+    argv = (ctypes.c_char_p * max(1, len(args)))(*[a.encode() for a in args])
+    cap = 24 + max(1, loops) * (2 * len(pcap) + 1024 + 262144)
+    out = ctypes.create_string_buffer(cap)
+    out_len = ctypes.c_size_t(0)
+    err = ctypes.create_string_buffer(1024)
+    inbuf = ctypes.create_string_buffer(pcap, len(pcap))
+    rc = fn(inbuf, len(pcap), int(loops), 1 if preload else 0, len(args), argv, out, cap, ctypes.byref(out_len),
+            err, 1024)
+    if rc == -2:
+        raise ValueError("oracle rejected input/options: " + err.value.decode(errors="replace"))
+    return rc, out.raw[:out_len.value]
+
+
 def check_rewrite(pcap, args, cache, dev_out, threads=16, sharded=True, pkt_base=0):
     """The checker bench.py runs outside its timed region: the oracle's tcprewrite output
     for (pcap, args, cache) must equal `dev_out` (the device's output image, any

@@ -244,3 +244,27 @@ def test_relinked_tcprewrite_reproduces_the_goldens(abi, tmp_path, case):
     assert r.returncode == 0, r.stderr.decode()
     got, exp = out.read_bytes(), G.read(name)
     assert got == exp, f"{name}: first difference at byte {next((i for i in range(min(len(got), len(exp))) if got[i] != exp[i]), min(len(got), len(exp)))}"
+
+
+def test_cidr_maps_longer_than_the_inline_list_parse(built):
+    """a CIDR map is unbounded (cidr.c:380-418): the first 16 pairs inline in the config,
+    the count covering all of them (the rest in the context's spill list)"""
+    import cfg_struct as CS
+    import tcpreplay_amd as TA
+    pairs = ",".join(f"10.{i}.0.0/16:172.{16 + i % 16}.{i}.0/24" for i in range(40))
+    for args, field in (([f"--srcipmap={pairs}"], "srcipmap"), ([f"--pnat={pairs}"], "cidrmap1")):
+        te = TA.TcpEdit(args)
+        try:
+            buf = ctypes.create_string_buffer(1 << 16)
+            n = te._L.tcpedit_get_dev_cfg(te._ctx, buf, len(buf), None)
+            cfg = CS.DevCfg.from_buffer_copy(buf.raw[:ctypes.sizeof(CS.DevCfg)])
+            assert n == ctypes.sizeof(CS.DevCfg)
+            assert getattr(cfg, "n_" + field) == 40
+            if field == "cidrmap1":
+                assert cfg.n_cidrmap2 == 40  # one -N serves both directions
+            for i in range(16):
+                e = getattr(cfg, field)[i]
+                assert e.frm.masklen == 16 and e.to.masklen == 24 and (e.to.network >> 16) & 0xff == i
+        finally:
+            te.close()
+

@@ -112,3 +112,72 @@ def test_big_endian_and_nanosecond_captures(built):
 def test_generic_configs_are_not_served(built):
     """a config whose tiles are the generic kernel's slots keeps the host index"""
     _run(S.pcap_imix(5_000, seed=15), ["--fixlen=pad", "--fixcsum"], expect_applied=False)
+
+
+# ---------------------------------------------------------------- the pipeline's index
+def _pipe(pcap, args, cache=None, chunk=1 << 20, env=None):
+    import os
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        rc_o, exp = O.rewrite(pcap, args, cache)
+        te = TA.TcpEdit(args)
+        try:
+            rc, out = te.rewrite_pipelined(pcap, cache, chunk_bytes=chunk)
+        finally:
+            te.close()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert rc == rc_o
+    assert out == exp, f"first difference at byte {next(i for i in range(min(len(out), len(exp))) if out[i] != exp[i])}"
+
+
+@pytest.mark.parametrize("name,gen,args", [
+    ("c2", lambda: S.pcap_fixed(60_000, 64, seed=21), ["--seed=42", "--fixcsum"]),
+    ("imix", lambda: S.pcap_imix(20_000, seed=22), ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353",
+                                                    "--fixcsum"]),
+    ("c5", lambda: S.pcap_mixed_v4v6(4_000, 1514, seed=23), ["--fixcsum"]),
+    ("efcs", lambda: S.pcap_imix(20_000, seed=24, fcs=True), ["--efcs", "--ttl=3"]),
+    ("mixed", lambda: F.build(F.mixed(8000, seed=25)), ["--seed=7", "--fixcsum"]),
+], ids=lambda x: x if isinstance(x, str) else "")
+def test_pipeline_device_index_matches_the_oracle(built, name, gen, args):
+    """the pipelined path with the record index built on the device: fixed 1 MiB chunks
+    (records straddle every cut; the next chunk starts where the previous chain ended,
+    read on the device)"""
+    _pipe(gen(), args)
+
+
+def test_pipeline_device_index_edges(built):
+    """records larger than a wave tile and than a generic slot across chunk cuts, caplen-0
+    records, an oversize record (libpcap stops) and a len error in a later chunk, record-like
+    payloads that fool the speculation (the chunk falls back to the host walk)"""
+    base = S.records(S.pcap_fixed(30_000, 90, seed=26))
+    big = S.records(S.pcap_fixed(3, 9000, seed=27)) + S.records(S.pcap_fixed(2, 200_000, seed=28))
+    recs = []
+    for i, r in enumerate(base):
+        recs.append(r)
+        if i % 97 == 0:
+            recs.append((1, i, i % 21, i % 21, bytes(i % 21)))
+        if i % 3001 == 0:
+            recs.append(big[(i // 3001) % len(big)])
+    args = ["--seed=3", "--fixcsum"]
+    _pipe(S.build_pcap(recs), args)
+    ts, tu, cl, ln, d = recs[25_000]
+    over = S.build_pcap(recs[:25_000]) + struct.pack("<IIII", ts, tu, 300_000, 300_000) + d + \
+        S.build_pcap(recs[25_001:])[24:]
+    _pipe(over, args)
+    err = S.build_pcap(recs[:22_222] + [(ts, tu, cl, 400_000, d)] + recs[22_223:])
+    _pipe(err, args)
+    fake = b"".join(struct.pack("<IIII", 1, 2, 12, 12) + bytes(range(12)) for _ in range(50))
+    fooled = []
+    for ts, tu, cl, ln, d in S.records(S.pcap_fixed(2_000, 1_442, seed=29)):
+        d = bytearray(d)
+        d[42:42 + len(fake)] = fake
+        fooled.append((ts, tu, cl, ln, bytes(d)))
+    _pipe(S.build_pcap(fooled), args)
+    # the host walk in the pipeline (A/B): the same bytes
+    _pipe(S.build_pcap(recs), args, env={"TCPEDIT_HIP_PIPE_INDEX": "host"})

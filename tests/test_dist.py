@@ -180,6 +180,75 @@ def test_slice_cache_matches_global_lookup(built):
         assert bits(sub, i) == bits(cache, g)
 
 
+@pytest.mark.parametrize("n", range(1, 9))
+def test_shard_place_follows_the_first_hard_error(built, n):
+    """tcpedit_shard_place (the C placement `tcprewrite --gpus` and dist.py share): shard k
+    sits after the bytes of the shards before it, and nothing after the first failing
+    shard is written (tcprewrite.c:156-160)"""
+    import random
+    rng = random.Random(n)
+    for _ in range(50):
+        sizes = [rng.choice([0, rng.randrange(1, 10_000)]) for _ in range(n)]
+        errs = [rng.random() < 0.2 for _ in range(n)]
+        offs, writes, end = D.place(sizes, errs)
+        first = next((k for k in range(n) if errs[k]), n)
+        for k in range(n):
+            assert writes[k] == (sizes[k] if k <= first else 0)
+            if k <= first:
+                assert offs[k] == 24 + sum(sizes[:k])
+        assert end == 24 + sum(sizes[:first + 1])
+
+
+def test_tcprewrite_gpus_fails_loudly_without_devices(built, tmp_path):
+    """`tcprewrite --gpus N` needs N devices: without them it says so and exits 255"""
+    import subprocess
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    inp = tmp_path / "in.pcap"
+    inp.write_bytes(S.pcap_fixed(10, 64, seed=1))
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tcpreplay_amd", "bin",
+                        "tcprewrite")
+    r = subprocess.run([tool, "--gpus", "2", "-i", str(inp), "-o", str(tmp_path / "o.pcap"), "--fixcsum"],
+                       capture_output=True, timeout=120)
+    assert r.returncode == 255 and b"device" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["c2", "c4_cache", "hard_error", "fuzz"])
+def test_tcprewrite_gpus_tool_equals_oracle(built, tmp_path, case):
+    """the C multi-GPU driver at N=1 on the box (ncclCommInitAll, the counter all-reduce,
+    the mmap placement): its output file equals the oracle's"""
+    import subprocess
+    cache = None
+    if case == "c2":
+        pcap, args = S.pcap_fixed(200_000, 64, seed=2), ["--seed=42", "--fixcsum"]
+    elif case == "c4_cache":
+        pcap, args, cache = G.read("test.pcap"), C4_ARGS, G.read("test.auto_router")
+    elif case == "fuzz":
+        pcap, args = S.pcap_imix(20_000, seed=7), ["--fuzz-seed=8", "--fuzz-factor=2", "--fixcsum"]
+    else:
+        recs = S.records(S.pcap_fixed(40, 64, seed=5))
+        ts, tu, cl, ln, d = recs[12]
+        d = bytearray(d)
+        d[14] = 0x55
+        recs[12] = (ts, tu, cl, ln, bytes(d))
+        pcap, args = S.build_pcap(recs), ["--fixcsum"]
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    inp, out = tmp_path / "in.pcap", tmp_path / "out.pcap"
+    inp.write_bytes(pcap)
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tcpreplay_amd", "bin",
+                        "tcprewrite")
+    cmd = [tool, "--gpus", "1", "-i", str(inp), "-o", str(out)] + args
+    if cache:
+        cp = tmp_path / "c.cache"
+        cp.write_bytes(cache)
+        cmd += ["-c", str(cp)]
+    r = subprocess.run(cmd, capture_output=True, timeout=120)
+    assert r.returncode == (255 if rc_o else 0), r.stderr.decode()
+    assert out.read_bytes() == exp
+
+
 # ---------------------------------------------------------------- gloo world_size 2 (oracle-edited shards)
 @pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix", "fuzz_golden", "fuzz_imix"])
 def test_two_rank_rewrite_equals_single_process(built, case):

@@ -23,6 +23,16 @@ FAST_OPTION_SETS = [
     ["--enet-dmac=00:12:13:14:15:16", "--enet-smac=00:22:33:44:55:66", "--fixcsum"],
     ["--enet-dmac=00:12:13:14:15:16", "--enet-smac=00:22:33:44:55:66", "--skipl2broadcast", "--fixcsum"],
     ["--seed=99", "--portmap=443:8443", "--pnat=172.16.0.0/12:10.99.0.0/16", "--fixcsum"],
+    # --enet-subsmac (applied in list order, each entry on the earlier ones' result) and
+    # --enet-mac-seed (per-byte masks past the kept bytes, unicast addresses only) on the
+    # wave lane (en10mb.c:659-689)
+    ["--enet-subsmac=00:11:22:33:44:55,00:aa:bb:cc:dd:ee", "--enet-subsmac=00:aa:bb:cc:dd:ee,01:00:5e:00:00:07",
+     "--enet-subsmac=00:66:77:88:99:aa,ff:ff:ff:ff:ff:ff", "--fixcsum"],
+    ["--enet-mac-seed=42", "--fixcsum"],
+    ["--enet-mac-seed=7", "--enet-mac-seed-keep-bytes=3", "--seed=5", "--fixcsum"],
+    ["--enet-mac-seed=9", "--enet-mac-seed-keep-bytes=1", "--ttl=+2"],
+    ["--enet-subsmac=00:11:22:33:44:55,00:12:34:56:78:9a", "--enet-dmac=00:12:13:14:15:16", "--skipl2broadcast",
+     "--fixcsum"],
 ]
 
 

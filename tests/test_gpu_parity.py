@@ -157,6 +157,125 @@ def test_tcpedit_packet_api(built, args):
     assert got == exp_recs
 
 
+def _per_packet(te, recs, bufsize=262166):
+    L = TA.load()
+    got = []
+    for ts, tu, cl, ln, data in recs:
+        buf = bytearray(bufsize)
+        buf[:cl] = data
+        rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf)
+        got.append((rc, h["caplen"], h["len"], bytes(buf[:h["caplen"]]) if rc != TA.TCPEDIT_ERROR else b""))
+    return got, (L.tcpedit_get_pkts_edited(te._ctx), L.tcpedit_get_total_bytes(te._ctx))
+
+
+def _launch_path(fn):
+    """run fn() with tcpedit_packet's launch-per-call path (no resident server)"""
+    old = os.environ.get("TCPEDIT_HIP_PACKET_SERVER")
+    os.environ["TCPEDIT_HIP_PACKET_SERVER"] = "0"
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop("TCPEDIT_HIP_PACKET_SERVER", None)
+        else:
+            os.environ["TCPEDIT_HIP_PACKET_SERVER"] = old
+
+
+@pytest.mark.parametrize("k", range(len(OPTION_POOL)))
+def test_packet_server_matches_the_launch_path(built, k):
+    """the resident server (te_packet_server) edits every record as the launch-per-call
+    path does: status, header, bytes and the context's counters"""
+    args = OPTION_POOL[k]
+    recs = mutate(S.records(G.read("test.pcap")), random.Random(100 + k))
+    te = TA.TcpEdit(args)
+    try:
+        got = _per_packet(te, recs)
+    finally:
+        te.close()
+    te = TA.TcpEdit(args)
+    try:
+        exp = _launch_path(lambda: _per_packet(te, recs))
+    finally:
+        te.close()
+    assert got[1] == exp[1]
+    for i, (a, b) in enumerate(zip(got[0], exp[0])):
+        assert a == b, f"record {i}"
+
+
+def test_packet_server_relaunches_after_idle_and_serves_two_contexts(built):
+    """the server leaves after 50 ms without a request and the next call launches it
+    again; two contexts keep a server each"""
+    import time
+    recs = S.records(G.read("test.pcap"))[:12]
+    pcap = S.build_pcap(recs)
+    a1, a2 = ["--seed=9", "--fixcsum"], ["--enet-vlan=add", "--enet-vlan-tag=3"]
+    exp1, exp2 = S.records(O.rewrite(pcap, a1)[1]), S.records(O.rewrite(pcap, a2)[1])
+    t1, t2 = TA.TcpEdit(a1), TA.TcpEdit(a2)
+    try:
+        for i, (ts, tu, cl, ln, data) in enumerate(recs):
+            for te, exp in ((t1, exp1), (t2, exp2)):
+                buf = bytearray(262166)
+                buf[:cl] = data
+                rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf)
+                assert rc != TA.TCPEDIT_ERROR
+                assert (ts, tu, h["caplen"], h["len"], bytes(buf[:h["caplen"]])) == exp[i]
+            if i % 4 == 3:
+                time.sleep(0.12)
+    finally:
+        t1.close()
+        t2.close()
+
+
+def test_packet_server_declines_records_larger_than_its_slot(built):
+    """a record past the block's LDS slot goes the launch-per-call way (same bytes)"""
+    rng = random.Random(7)
+    recs = S.records(S.pcap_fixed(4, 1400, seed=8))
+    big = []
+    for ts, tu, cl, ln, d in recs:
+        d = d + bytes(rng.randrange(256) for _ in range(40000))
+        big.append((ts, tu, len(d), len(d), d))
+    pcap = S.build_pcap(big + recs)
+    _, exp = O.rewrite(pcap, ["--ttl=4"])
+    te = TA.TcpEdit(["--ttl=4"])
+    try:
+        got, _ = _per_packet(te, big + recs)
+    finally:
+        te.close()
+    assert [(g[1], g[2], g[3]) for g in got] == [(e[2], e[3], e[4]) for e in S.records(exp)]
+
+
+@pytest.mark.parametrize("opt", ["srcipmap", "dstipmap", "pnat", "pnat2", "endpoints_v6"])
+def test_cidr_maps_past_the_inline_list(built, opt):
+    """CIDR maps longer than the config's 16 inline pairs: the rest from the spill list in
+    HBM, in the reference's first-match order (cidr.c:290-418)"""
+    pairs = [f"10.{i}.0.0/16:172.{16 + i % 16}.{i}.0/24" for i in range(37)]
+    pairs.append("0.0.0.0/0:198.51.100.0/24")  # the catch-all past the inline list
+    lst = ",".join(pairs)
+    if opt == "pnat2":
+        args = [f"--pnat={lst}", "--pnat=" + ",".join(reversed(pairs)), "--fixcsum"]
+    elif opt == "endpoints_v6":
+        v6 = ",".join(f"[2001:db8:{i:x}::/48]:[fd00:{i:x}::/48]" for i in range(30)) + ",[::/0]:[fd99::/64]"
+        args = [f"--pnat={lst},{v6}", "--fixcsum"]
+    else:
+        args = [f"--{opt}={lst}", "--fixcsum"]
+    rng = np.random.default_rng(5)
+    pcap = S.pcap_imix(4000, seed=11)
+    recs = S.records(pcap)
+    out_recs = []
+    for k, (ts, tu, cl, ln, d) in enumerate(recs):  # addresses spread over the 40 prefixes
+        d = bytearray(d)
+        if d[12:14] == b"\x08\x00":
+            d[26:28] = bytes([10, int(rng.integers(0, 45))])
+            d[30:32] = bytes([10, int(rng.integers(0, 45))])
+        out_recs.append((ts, tu, cl, ln, bytes(d)))
+    pcap = S.build_pcap(out_recs)
+    pcap = pcap + S.pcap_mixed_v4v6(200, 200, seed=3)[24:]
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out = gpu_rewrite(pcap, args)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
+
+
 # ---------------------------------------------------------------- edge cases
 def test_empty_capture(built):
     hdr = G.read("test.pcap")[:24]

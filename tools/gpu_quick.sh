@@ -1,7 +1,8 @@
+# a short GPU check: the tests named on the command line (one pytest process, bounded)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -x -q -m gpu -k "not full_size" > gpurun_out/gpu_tests.log 2>&1; echo "PYTEST EXIT $?" >> gpurun_out/gpu_tests.log
-tail -4 gpurun_out/gpu_tests.log
-timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
+timeout -k 10 600 python -u -m pytest -q -m gpu --timeout 120 --timeout-method thread "$@" > gpurun_out/quick.log 2>&1
+rc=$?
+tail -30 gpurun_out/quick.log
+exit $rc
