@@ -3,6 +3,7 @@ library's option parsers (tcpedit, tcpprep incl. the regex DFA compiler, tcprepl
 its record walk with the walker pool, and the CPU oracle -- built with
 -fsanitize=address,undefined and with -fsanitize=thread (tests/sanitize/Makefile) and
 driven over the option pool and captures here.  A sanitizer report fails the test."""
+import fcntl
 import os
 import subprocess
 
@@ -78,7 +79,13 @@ def _captures(tmp):
 
 @pytest.fixture(scope="module")
 def drivers(built):
-    r = subprocess.run(["make", "-s", "-C", SAN], capture_output=True, text=True, timeout=900)
+    os.makedirs(os.path.join(SAN, "_build"), exist_ok=True)
+    with open(os.path.join(SAN, "_build", ".lock"), "w") as lk:  # xdist workers share the tree
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            r = subprocess.run(["make", "-s", "-C", SAN], capture_output=True, text=True, timeout=900)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     assert r.returncode == 0, r.stderr[-3000:]
     return {k: os.path.join(SAN, "_build", k, "san_driver") for k in ("asan", "tsan")}
 
