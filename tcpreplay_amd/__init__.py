@@ -74,6 +74,7 @@ def load():
         "tcpedit_parse_args": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int)]),
         "tcpedit_batch_open": (vp, [vp, vp, sz, vp, sz, u64]),
         "tcpedit_batch_run": (c_int, [vp, vp]),
+        "tcpedit_batch_update_input": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),
         "tcpedit_batch_output": (sz, [vp, vp, sz]),
         "tcpedit_batch_open_segment": (vp, [vp, vp, vp, sz, vp, sz, u64]),
@@ -337,6 +338,13 @@ class Batch:
 
     def run(self):
         return self._L.tcpedit_batch_run(self._te._ctx, self._b)
+
+    def update_input(self, pcap):
+        """replace the staged image's bytes with `pcap` (same length, same record headers:
+        the index and tiles are kept; tcpedit_batch_update_input)"""
+        keep, p, n = _buf(pcap)
+        if self._L.tcpedit_batch_update_input(self._te._ctx, self._b, p, n) < 0:
+            raise RuntimeError(self._te.geterr())
 
     def result(self) -> BatchResult:
         r = BatchResult()

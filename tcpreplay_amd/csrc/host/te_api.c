@@ -1366,6 +1366,23 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
+    if (b->last_fast && b->last_skipped && b->last_listed) {
+        /* the hint was wrong (it can be after tcpedit_batch_update_input): run the generic
+           pass now and read the counters, error and violation words again -- before the
+           static-placement check below, since the tiles it edits can break that placement */
+        if (launch_ev(b, fixed_dir, NULL, NULL, 1) != 0) {
+            te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return TCPEDIT_ERROR;
+        }
+        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
+        if (b->last_grow) /* the listed tiles can break static placement too */
+            HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+        b->last_skipped = 0;
+    }
     if (b->last_grow && b->grow_bad) {
         /* a record did not grow by exactly 4 bytes: place this batch by scan + look-back
            from now on, and run it again that way */
@@ -1381,19 +1398,6 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
-    }
-    if (b->last_fast && b->last_skipped && b->last_listed) {
-        /* the hint was wrong (it cannot be for the same image and config): run the
-           generic pass now and read the counters and error words again */
-        if (launch_ev(b, fixed_dir, NULL, NULL, 1) != 0) {
-            te_seterr(t, "kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-            return TCPEDIT_ERROR;
-        }
-        HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
-                                 hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(t, hipStreamSynchronize(t->stream));
-        b->last_skipped = 0;
     }
     if (b->counters[TE_CNT_UNSUPPORTED] && !b->q8_defer) {
         /* records whose edit read the reference's stale static buffer: replay them */
