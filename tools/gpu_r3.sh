@@ -1,0 +1,15 @@
+# round 3 check (one gpurun call): the whole GPU suite, smoke(), then the default bench line.
+# A step that times out, aborts or faults ends the call (no further GPU step).
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { # name seconds cmd...
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/r3_$name.log" 2>&1; local rc=$?
+    tail -4 "gpurun_out/r3_$name.log"
+    [ $rc = 0 ] || { echo "step $name ended with $rc: stopping"; exit $rc; }
+}
+step suite 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+cp gpurun_out/r3_bench.log gpurun_out/r3_bench.json
