@@ -1753,10 +1753,11 @@ static uint64_t idx_nwin(uint64_t base, uint64_t limit)
 static void idx_layout(IdxArgs *a, uint8_t *ws, uint64_t nwin)
 {
     a->ticket = (uint32_t *)ws;
-    a->done = a->ticket + 1;
-    a->stop_win_c = a->ticket + 2;
-    a->overflow = a->ticket + 3;
-    a->timeouts = a->ticket + 4;
+    a->stop_win_c = a->ticket + 1;
+    a->bad_win_c = a->ticket + 2;
+    a->zero_win_c = a->ticket + 3;
+    a->ovf_win_c = a->ticket + 4;
+    a->timeouts = a->ticket + 5;
     a->scratch_ctr = (uint64_t *)(ws + 24);
     a->state = (uint64_t *)(ws + IDX_WS_WORDS);
     uint8_t *w = ws + IDX_WS_BYTES(nwin);

@@ -37,7 +37,8 @@
 #define IDX_T__N 12
 
 /* the per-launch words the pass needs zeroed, at the start of its workspace:
-   ticket, done, stop (complemented), overflow, timeouts (u32 each), scratch counter (u64) */
+   ticket, the first stop / bad / zero-caplen / overflow windows (complemented), timeouts
+   (u32 each), scratch counter (u64) */
 #define IDX_WS_WORDS 64
 #define IDX_WS_BYTES(nwin) (IDX_WS_WORDS + 8ull * (nwin) /* state */)
 /* per-window records the finishing wave reads (not zeroed) */
@@ -59,7 +60,7 @@ typedef struct {
     uint32_t nwin;      /* windows of te_index_window_bytes() from entry & ~15 */
     uint32_t budget, max_pkts, growth; /* the wave-lane tile cut (walk_range) */
     /* zeroed per launch (IDX_WS_BYTES) */
-    uint32_t *ticket, *done, *stop_win_c, *overflow, *timeouts;
+    uint32_t *ticket, *stop_win_c, *bad_win_c, *zero_win_c, *ovf_win_c, *timeouts; /* (~first window) */
     uint64_t *scratch_ctr;
     uint64_t *state;    /* nwin look-back granules */
     /* per window (IDX_WIN_BYTES) */

@@ -24,10 +24,13 @@
 //   * a decoupled look-back over windows (records | tiles in one 64-bit granule) gives the
 //     window's first record and tile numbers, and the wave writes its tiles and record
 //     offsets in place;
-//   * the last window to finish checks every window's first record against where the
-//     chain left the window before it (window 0 starts at the known first record), finds
-//     where the chain ends and writes the totals.  A guess that was wrong across windows
-//     sets IDX_T_BAD: the caller keeps the host walk's index, which is exact.
+//   * once its look-back has seen every earlier window's granule, a window checks its first
+//     record against where the chain left the nearest earlier window with a record (window
+//     kE starts at the known first record) and reports a miss as the first bad window;
+//     te_index_finish (one lane, the next launch) compares the first bad window with the
+//     first stop, finds where the chain ends and writes the totals.  A guess that was wrong
+//     across windows sets IDX_T_BAD: the caller keeps the host walk's index, which is exact.
+//     (A serial finishing loop over every window cost ~50 ns a window: 0.84 ms on C2.)
 // libpcap's ends are kept: an oversize record (caplen > 262144) or a truncated one ends
 // the chain; a len > 262144 record ends it with the reference's error (tcprewrite.c:296).
 #include <hip/hip_runtime.h>
@@ -35,6 +38,13 @@
 
 #include "te_index.h"
 
+// TE_IDX_STAMPS builds (diagnostics only): s_memtime per phase of a few windows, printed
+#if TE_IDX_STAMPS
+#define IX_STAMP(i) do { __builtin_amdgcn_sched_barrier(0); ix_t[i] = __builtin_amdgcn_s_memtime(); \
+                         __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define IX_STAMP(i)
+#endif
 namespace {
 typedef uint8_t u8;
 typedef uint16_t u16;
@@ -177,12 +187,20 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     constexpr int WN = W - O;       // bytes a window owns
     static_assert(S % 16 == 0 && S <= 128, "sub-window: whole 16-byte chunks, <= two 64-bit masks");
     __shared__ WinLds<S> L[IWAVES];
+    __shared__ u32 blk_ticket;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     WinLds<S> &M = L[wv];
-    u32 k = 0;
-    if (lane == 0) k = atomicAdd(a.ticket, 1u);
-    k = __shfl(k, 0);
-    if (k >= a.nwin) return;  // (every wave of the grid takes exactly one ticket)
+    // one ticket a block (its waves take consecutive windows): windows are numbered in the
+    // order blocks start, so a window's look-back only waits on windows already running
+    if (threadIdx.x == 0) blk_ticket = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    const u32 k = blk_ticket * IWAVES + (u32)wv;
+    if (k >= a.nwin) return;
+#if TE_IDX_STAMPS
+    unsigned long long ix_t[10] = {};
+    int ix_rounds = 0;
+#endif
+    IX_STAMP(0);
     // the first record: known to the host (a.entry), or where the previous pipeline chunk's
     // chain ended (read on the device: that chunk's index ran before this one on the stream)
     const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
@@ -218,6 +236,7 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     // moving a lane's reads of other lanes' stores across them (no block barrier: the
     // block's waves work on their own windows and may have left already)
     asm volatile("" ::: "memory");
+    IX_STAMP(1);
 
     // ---- this lane's guess: the first strong candidate in its sub-window, else the first weak ----
     const u64 lo = A0 + (u64)lane * S, hi_raw = lo + S;
@@ -267,6 +286,7 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     }
     LaneWalk w = e != IDX_NONE ? walk_lds(a, M.img, A0, e, hi) : LaneWalk{0, 0, 0};
     bool has = e != IDX_NONE;
+    IX_STAMP(2);
 
     // ---- where the chain starts: the first guess the next guess confirms (its walk ends
     // exactly there, or at a strong candidate).  A guess that is not a record start jumps by a garbage length, so it is
@@ -330,11 +350,15 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
                 change = true;
             }
         }
+#if TE_IDX_STAMPS
+        ix_rounds = round + 1;
+#endif
         if (!__ballot(change)) {
             settled = true;
             break;
         }
     }
+    IX_STAMP(3);
     if (!settled) {  // the serial lane loop (exact)
         u64 cur = IDX_NONE;
         u32 ended = 0;
@@ -366,6 +390,7 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
             ended = (u32)__shfl((int)w.stop, (int)l);
         }
     }
+    IX_STAMP(4);
     // only the window's own lanes' records count (the overlap's are window k - 1's)
     if (lane < OL) has = false;
     // the window's entry, exit and how the chain ends here
@@ -422,22 +447,51 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     }
     if (lane == 0) M.tst[ntile] = (u16)nrec;
     asm volatile("" ::: "memory");
+    IX_STAMP(5);
 
     // ---- the window's record and tile numbers ----
     const u64 agg = (u64)nrec | ((u64)ntile << REC_BITS);
-    // publish where the chain enters and leaves this window before the aggregate (the
-    // finishing wave reads them after every window has counted itself done)
+    // publish where the chain enters and leaves this window before the aggregate: a later
+    // window reads them once its look-back has seen this window's granule (release here,
+    // acquire there)
     if (lane == 0) {
         a.w_entry[k] = went;
         a.w_exit[k] = wexit;
-        a.w_flags[k] = wstop | (anyzero ? IDX_ZERO : 0u);
+        a.w_flags[k] = wstop;
+        __threadfence();
     }
+    IX_STAMP(6);
     const u64 excl = lookback(a.state, k, agg, a.timeouts);
     const u64 pbase = excl & REC_MASK, tbase = excl >> REC_BITS;
+    IX_STAMP(7);
     if (lane == 0) {
         a.w_pfx[k] = excl + agg;
         if (wstop == IDX_ERROR) a.w_err[k] = pbase + nrec;  // the record the chain stopped at
-        if (wstop) atomicMax(a.stop_win_c, ~k);  // (zeroed word: max of ~k = the first stop)
+        // (zeroed words: max of ~k = the first such window)
+        if (wstop) atomicMax(a.stop_win_c, ~k);
+        if (anyzero) atomicMax(a.zero_win_c, ~k);
+        // the chain across windows, checked here: every earlier window has published (the
+        // look-back saw their granules).  This window's first record must be where the chain
+        // left the nearest earlier window a record starts in; a window without one must be
+        // passed over whole.  Only windows up to the chain's end matter: the finishing pass
+        // compares the first bad window with the first stop.
+        __threadfence();
+        bool bad = false;
+        if (k == kE) {
+            bad = went != entry;
+        } else if (k > kE) {
+            u32 j = k - 1;
+            while (j > kE && ((volatile u64 *)a.w_entry)[j] == IDX_NONE) --j;
+            const u64 xj = ((volatile u64 *)a.w_exit)[j];
+            if (went != IDX_NONE) {
+                bad = xj != went;
+            } else {
+                const u64 qe = base + (u64)(k + 1) * WN;
+                bad = xj < (qe < a.len ? qe : a.len) &&
+                      !(((volatile u32 *)a.w_flags)[j] & (IDX_STOP | IDX_ERROR | IDX_END));
+            }
+        }
+        if (bad) atomicMax(a.bad_win_c, ~k);
     }
 
     // ---- tiles and record offsets in place ----
@@ -470,66 +524,45 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     }
     // (a window past the chain's end counts records that are not -- it may overflow: only
     // the windows up to the end are looked at)
-    if (__ballot(ovf) && lane == 0) atomicOr(&a.w_flags[k], IDX_OVF);
+    if (__ballot(ovf) && lane == 0) atomicMax(a.ovf_win_c, ~k);
+#if TE_IDX_STAMPS
+    IX_STAMP(8);
+    if (lane == 0 && (k < 3 || k % 4096 == 0 || k + 1 == a.nwin))
+        printf("IX win %u/%u settled %d rounds %d nrec %u ntile %u | stage %llu guess %llu jacobi %llu serial %llu "
+               "pos %llu cut %llu lookback %llu write %llu\n", k, a.nwin, (int)settled, ix_rounds, nrec, ntile,
+               ix_t[1] - ix_t[0], ix_t[2] - ix_t[1], ix_t[3] - ix_t[2], ix_t[4] - ix_t[3], ix_t[5] - ix_t[4],
+               ix_t[6] - ix_t[5], ix_t[7] - ix_t[6], ix_t[8] - ix_t[7]);
+#endif
+}
 
-    // ---- the last window to finish checks the chain across windows and writes totals ----
-    __threadfence();
-    u32 done = 0;
-    if (lane == 0) done = atomicAdd(a.done, 1u);
-    done = __shfl(done, 0);
-    if (done != a.nwin - 1) return;
-    __threadfence();
-    const u32 stop_c = *(volatile u32 *)a.stop_win_c;
-    const u32 last = stop_c ? ~stop_c : a.nwin - 1;
-    u32 bad = 0, zr = 0, ov = 0;
-    u32 badq = 0xffffffffu;
-    for (u32 q = lane; q <= last; q += IW) {
-        const u64 eq = ((volatile u64 *)a.w_entry)[q];
-        zr |= ((volatile u32 *)a.w_flags)[q] & IDX_ZERO;
-        ov |= ((volatile u32 *)a.w_flags)[q] & IDX_OVF;
-        if (q <= kE) {  // (windows before the first record's are not the chain's)
-            if (q == kE) bad |= eq != entry;
-            continue;
-        }
-        u32 j = q - 1;  // the nearest earlier window a record starts in
-        while (j > kE && ((volatile u64 *)a.w_entry)[j] == IDX_NONE) --j;
-        const u64 xj = ((volatile u64 *)a.w_exit)[j];
-        const u32 b0 = bad;
-        if (eq != IDX_NONE) {
-            bad |= xj != eq;
-        } else {  // no guess here: the chain must pass over the whole window
-            const u64 qe = base + (u64)(q + 1) * WN;
-            bad |= xj < (qe < a.len ? qe : a.len) && !(((volatile u32 *)a.w_flags)[j] & (IDX_STOP | IDX_ERROR | IDX_END));
-        }
-        if (bad && !b0 && q < badq) badq = q;
-    }
-    for (int o = 32; o > 0; o >>= 1) {  // (diagnostics: the first bad window)
-        const u32 y = __shfl_xor(badq, o, 64);
-        badq = y < badq ? y : badq;
-    }
-    bad = __ballot(bad != 0) != 0;
-    zr = __ballot(zr != 0) != 0;
-    ov = __ballot(ov != 0) != 0;
-    if (lane == 0) {
-        u32 j = last;
-        while (j > kE && ((volatile u64 *)a.w_entry)[j] == IDX_NONE) --j;
-        const u64 tot = ((volatile u64 *)a.w_pfx)[last];
-        const u32 fl = ((volatile u32 *)a.w_flags)[last];
-        const bool stopped = stop_c != 0;
-        a.totals[IDX_T_RECS] = tot & REC_MASK;
-        a.totals[IDX_T_TILES] = tot >> REC_BITS;
-        a.totals[IDX_T_SCRATCH] = *(volatile unsigned long long *)a.scratch_ctr;
-        a.totals[IDX_T_BAD] = bad || *(volatile u32 *)a.timeouts ? 1 : 0;
-        a.totals[IDX_T_WINDOWS] = last + 1;
-        a.totals[IDX_T_STOP] = stopped ? (fl & (IDX_STOP | IDX_ERROR | IDX_END)) : 0;
-        const u64 end = ((volatile u64 *)a.w_exit)[j];
-        a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
-        a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
-        a.totals[IDX_T_ZERO] = zr ? 1 : 0;
-        a.totals[IDX_T_ERR_REC] = stopped && (fl & IDX_ERROR) ? ((volatile u64 *)a.w_err)[last] : ~0ull;
-        a.totals[IDX_T_OVERFLOW] = ov;
-        a.totals[IDX_T_BADWIN] = badq;
-    }
+// the totals, after every window is done (one wave, the next kernel on the stream)
+__global__ __launch_bounds__(64) void te_index_finish(IdxArgs a) {
+    const int lane = threadIdx.x;
+    if (lane != 0) return;
+    const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
+    constexpr int WN = IW * TE_IDX_S - TE_IDX_OL * TE_IDX_S;
+    const u32 kE = (u32)((entry - a.base) / WN);
+    const u32 stop_c = *a.stop_win_c, bad_c = *a.bad_win_c, zero_c = *a.zero_win_c, ovf_c = *a.ovf_win_c;
+    const u32 last = stop_c ? ~stop_c : a.nwin - 1;  // windows past the chain's end do not count
+    const bool bad = bad_c && ~bad_c <= last;
+    u32 j = last;
+    while (j > kE && a.w_entry[j] == IDX_NONE) --j;
+    const u64 tot = a.w_pfx[last];
+    const u32 fl = a.w_flags[last];
+    const bool stopped = stop_c != 0;
+    a.totals[IDX_T_RECS] = tot & REC_MASK;
+    a.totals[IDX_T_TILES] = tot >> REC_BITS;
+    a.totals[IDX_T_SCRATCH] = *a.scratch_ctr;
+    a.totals[IDX_T_BAD] = bad || *a.timeouts ? 1 : 0;
+    a.totals[IDX_T_WINDOWS] = last + 1;
+    a.totals[IDX_T_STOP] = stopped ? (fl & (IDX_STOP | IDX_ERROR | IDX_END)) : 0;
+    const u64 end = a.w_exit[j];
+    a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
+    a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
+    a.totals[IDX_T_ZERO] = zero_c && ~zero_c <= last ? 1 : 0;
+    a.totals[IDX_T_ERR_REC] = stopped && (fl & IDX_ERROR) ? a.w_err[last] : ~0ull;
+    a.totals[IDX_T_OVERFLOW] = ovf_c && ~ovf_c <= last ? 1 : 0;
+    a.totals[IDX_T_BADWIN] = bad ? ~bad_c : 0xffffffffu;
 }
 }  // namespace
 
@@ -542,5 +575,6 @@ extern "C" int te_launch_index(const IdxArgs *args, void *stream) {
     if (a.nwin == 0) return 0;
     const u32 blocks = (a.nwin + IWAVES - 1) / IWAVES;
     hipLaunchKernelGGL((te_index_windows<TE_IDX_S, TE_IDX_OL>), dim3(blocks), dim3(IB), 0, st, a);
+    hipLaunchKernelGGL(te_index_finish, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
