@@ -305,6 +305,14 @@ int tcpedit_replay_pass(tcpedit_t *tcpedit, tcpedit_replay_t *r, void *out, size
 void tcpedit_replay_close(tcpedit_replay_t *r);
 /* new bytes for a batch's records in place (same file and record headers: the index stands) */
 int tcpedit_batch_update_input(tcpedit_t *tcpedit, tcpedit_batch_t *b, const void *img, size_t len);
+/* the records just before the batch's first (whole records ending where it starts: the previous
+ * shard of a sharded job, the previous chunk of a pipelined run), in the batch's format.
+ * tcprewrite edits every record in one never-cleared buffer (tcprewrite.c:267-301), so an edit
+ * that reads past its record's bytes sees what earlier records left there; when
+ * those bytes come from before the batch, the replay walks back into these records.  They are
+ * read only then (after a run lists such a record), so the bytes must stay valid until the
+ * batch's next run returns.  len 0 clears them. */
+int tcpedit_batch_set_prefix(tcpedit_t *tcpedit, tcpedit_batch_t *b, const void *recs, size_t len);
 
 /* device pointers, for callers that keep the data in HBM (e.g. a sender) */
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b);

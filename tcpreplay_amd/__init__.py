@@ -75,6 +75,7 @@ def load():
         "tcpedit_batch_open": (vp, [vp, vp, sz, vp, sz, u64]),
         "tcpedit_batch_run": (c_int, [vp, vp]),
         "tcpedit_batch_update_input": (c_int, [vp, vp, vp, sz]),
+        "tcpedit_batch_set_prefix": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),
         "tcpedit_batch_output": (sz, [vp, vp, sz]),
         "tcpedit_batch_open_segment": (vp, [vp, vp, vp, sz, vp, sz, u64]),
@@ -338,6 +339,15 @@ class Batch:
 
     def run(self):
         return self._L.tcpedit_batch_run(self._te._ctx, self._b)
+
+    def set_prefix(self, recs):
+        """the records just before this batch (whole records ending where it starts), read
+        by the SURVEY Q8 replay only when a record's stale bytes come from before the batch;
+        `recs` is passed by address and must stay alive until the next run returns"""
+        keep, p, n = _buf(recs)
+        self._prefix_keep = (recs, keep)
+        if self._L.tcpedit_batch_set_prefix(self._te._ctx, self._b, p, n) < 0:
+            raise RuntimeError(self._te.geterr())
 
     def update_input(self, pcap):
         """replace the staged image's bytes with `pcap` (same length, same record headers:

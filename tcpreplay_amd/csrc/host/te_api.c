@@ -80,6 +80,13 @@ struct tcpedit_batch_s {
     uint32_t q8_cap;
     int q8_defer;            /* tcpedit_packet replays itself, over the caller's buffer */
     uint8_t *d_q8_init;      /* tcpedit_packet: the caller's buffer bytes [0, need) */
+    const uint8_t *pre_host; /* tcpedit_batch_set_prefix: the records before the batch (caller's) */
+    size_t pre_len;
+    int pre_staged;          /* their last records are on the device: */
+    uint8_t *d_pre;          /*   bytes */
+    uint64_t *d_pre_off;     /*   offsets of npre records */
+    uint32_t npre;
+    int pre_file_start;      /*   the first of them is the capture's first record */
     uint64_t walk_from;      /* the walk's first record (0: 24, the image's first) */
     uint64_t rec0;           /* image offset of the launch's first record (0: 24) */
     uint64_t out_base;       /* output offset of its first record in d_out (0: 24; = rec0 mod 16) */
@@ -115,7 +122,9 @@ struct tcpedit_batch_s {
     int ran;
 };
 
-#define TE_Q8_CAP 65536u   /* stale-read records one batch may list for replay (more fail loudly) */
+#define TE_Q8_CAP (1u << 22) /* stale-read records one batch may list for replay (more fail loudly) */
+#define TE_Q8_PRE_RECS 16384u     /* prefix records staged for the replay, at most ... */
+#define TE_Q8_PRE_BYTES (32u << 20) /* ... and bytes */
 #define TE_Q8_THREADS 256u /* replay threads (scratch: te_q8_slot_bytes() each, per context) */
 #define WS_ERR 0
 #define WS_ZERO 0
@@ -831,6 +840,12 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_q8);
     hipFree(b->d_q8_init);
     b->d_q8 = b->d_q8_init = NULL;
+    hipFree(b->d_pre);
+    hipFree(b->d_pre_off);
+    b->d_pre = NULL;
+    b->d_pre_off = NULL;
+    b->npre = 0;
+    b->pre_staged = 0;
     b->d_fuzz = NULL;
     b->fuzz_cap = 0;
     b->d_tile_list = NULL;
@@ -1325,6 +1340,12 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
     L.q8_file_start = file_start;
     L.q8_init = d_init;
     L.q8_init_len = init_len;
+    if (b->pre_staged && b->npre) {
+        L.q8_pre = b->d_pre;
+        L.q8_pre_off = b->d_pre_off;
+        L.q8_npre = b->npre;
+        L.q8_pre_file_start = b->pre_file_start;
+    }
     if (t->cfg.fuzz_seed && b->d_fuzz && !b->last_fast)
         L.fuzz_states = b->d_fuzz;
     if (t->cfg.l2carry && !b->last_fast)
@@ -1334,6 +1355,97 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
         return -1;
     }
     return 0;
+}
+
+int tcpedit_batch_set_prefix(tcpedit_t *t, tcpedit_batch_t *b, const void *recs, size_t len)
+{
+    if (!t || !b || (len && !recs))
+        return TCPEDIT_ERROR;
+    b->pre_host = len ? (const uint8_t *)recs : NULL;
+    b->pre_len = len;
+    b->pre_staged = 0;
+    b->npre = 0;
+    return TCPEDIT_OK;
+}
+
+/* the prefix's last records (up to TE_Q8_PRE_RECS / TE_Q8_PRE_BYTES) to the device: a
+ * forward walk of its headers (the chain only runs forward), keeping a ring of offsets */
+static int stage_prefix(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    const uint8_t *r = b->pre_host;
+    const size_t len = b->pre_len;
+    uint64_t *ring = malloc(sizeof(uint64_t) * TE_Q8_PRE_RECS);
+    if (!ring) {
+        te_seterr(t, "out of memory");
+        return -1;
+    }
+    uint64_t n = 0;
+    size_t p = 0;
+    while (p + 16 <= len) {
+        const uint32_t cl = rd32(r + p + 8, b->swapped);
+        if (cl > 262144u || p + 16 + cl > len)
+            break;
+        ring[n++ % TE_Q8_PRE_RECS] = p;
+        p += 16 + (size_t)cl;
+    }
+    if (p != len) {
+        free(ring);
+        te_seterr(t, "tcpedit_batch_set_prefix: the records do not end where the batch starts (byte %zu of %zu)", p,
+                  len);
+        return -1;
+    }
+    /* the newest records that fit the limits */
+    uint64_t k = n < TE_Q8_PRE_RECS ? n : TE_Q8_PRE_RECS;
+    while (k > 1 && len - ring[(n - k) % TE_Q8_PRE_RECS] > TE_Q8_PRE_BYTES)
+        k--;
+    const uint64_t first = n - k, lo = k ? ring[first % TE_Q8_PRE_RECS] : len;
+    uint64_t *off = malloc(sizeof(uint64_t) * (k ? k : 1));
+    if (!off) {
+        free(ring);
+        te_seterr(t, "out of memory");
+        return -1;
+    }
+    for (uint64_t i = 0; i < k; i++)
+        off[i] = ring[(first + i) % TE_Q8_PRE_RECS] - lo;
+    free(ring);
+    hipFree(b->d_pre);
+    hipFree(b->d_pre_off);
+    b->d_pre = NULL;
+    b->d_pre_off = NULL;
+    if (hipMalloc((void **)&b->d_pre, (len - lo) + 64) != hipSuccess ||
+        hipMalloc((void **)&b->d_pre_off, sizeof(uint64_t) * (k ? k : 1)) != hipSuccess ||
+        hipMemcpyAsync(b->d_pre, r + lo, len - lo, hipMemcpyHostToDevice, t->stream) != hipSuccess ||
+        hipMemcpyAsync(b->d_pre_off, off, sizeof(uint64_t) * k, hipMemcpyHostToDevice, t->stream) != hipSuccess ||
+        hipStreamSynchronize(t->stream) != hipSuccess) {
+        free(off);
+        te_seterr(t, "out of device memory (prefix records)");
+        return -1;
+    }
+    free(off);
+    b->npre = (uint32_t)k;
+    /* the prefix's first record is record pkt_base - n of the job: the capture's first when 0 */
+    b->pre_file_start = first == 0 && b->pkt_base == n;
+    b->pre_staged = 1;
+    return 0;
+}
+
+/* after a run whose replay failed a record: with a prefix set, stage it and replay the
+ * listed records again (idempotent for the ones already replayed), counters re-read */
+static int retry_q8_with_prefix(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, uint64_t *counters)
+{
+    if (!b->pre_host || b->pre_staged)
+        return 0;
+    if (stage_prefix(t, b) < 0)
+        return -1;
+    HIPCHK(t, hipMemsetAsync(b->d_ws + b->last_cnt_off + 8 * TE_CNT_Q8_FAILED, 0, 8, t->stream));
+    if (run_q8(t, b, fixed_dir, b->pkt_base == 0, NULL, 0, t->stream) < 0)
+        return -1;
+    HIPCHK(t, hipMemcpyAsync(counters, b->d_ws + b->last_cnt_off, sizeof(b->counters), hipMemcpyDeviceToHost,
+                             t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return 0;
+fail:
+    return -1;
 }
 
 static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
@@ -1406,6 +1518,9 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
+        /* bytes from before the batch: walk back into the records the caller staged */
+        if (b->counters[TE_CNT_Q8_FAILED] && retry_q8_with_prefix(t, b, fixed_dir, b->counters) < 0)
+            return TCPEDIT_ERROR;
     }
     for (int i = 0; i < b->last_fgrid; i++) { /* the wave lane's per-block totals */
         const uint64_t *v = b->slots_host + 4 * (size_t)i;
@@ -1752,21 +1867,18 @@ static uint64_t idx_nwin(uint64_t base, uint64_t limit)
 
 static void idx_layout(IdxArgs *a, uint8_t *ws, uint64_t nwin)
 {
-    a->ticket = (uint32_t *)ws;
-    a->stop_win_c = a->ticket + 1;
-    a->bad_win_c = a->ticket + 2;
-    a->zero_win_c = a->ticket + 3;
-    a->ovf_win_c = a->ticket + 4;
-    a->timeouts = a->ticket + 5;
-    a->scratch_ctr = (uint64_t *)(ws + 24);
-    a->state = (uint64_t *)(ws + IDX_WS_WORDS);
-    uint8_t *w = ws + IDX_WS_BYTES(nwin);
-    a->w_entry = (uint64_t *)w;
-    a->w_exit = a->w_entry + nwin;
-    a->w_pfx = a->w_exit + nwin;
-    a->w_err = a->w_pfx + nwin;
-    a->w_flags = (uint32_t *)(a->w_err + nwin);
-    a->totals = (uint64_t *)(a->w_flags + nwin + (nwin & 1));
+    uint64_t *w = (uint64_t *)ws;
+    a->totals = w;
+    w += IDX_T__N + 2;
+    a->w_entry = w;
+    a->w_exit = w + nwin;
+    a->w_agg = w + 2 * nwin;
+    a->w_scr = w + 3 * nwin;
+    a->w_pfx = w + 4 * nwin;
+    a->w_sbase = w + 5 * nwin;
+    a->t_tile = (uint32_t *)(w + 6 * nwin);
+    a->w_flags = a->t_tile + 2ull * IDX_MAXR * nwin;
+    a->t_prel = (uint16_t *)(a->w_flags + nwin + 1);
 }
 
 int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms)
@@ -1782,7 +1894,7 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
     hipEvent_t e0 = NULL, e1 = NULL;
     int rc = TCPEDIT_ERROR;
     uint64_t tot[IDX_T__N];
-    const uint64_t zb = IDX_WS_BYTES(nwin), wsb = zb + IDX_WIN_BYTES(nwin) + 8 * (IDX_T__N + 2);
+    const uint64_t wsb = IDX_WS_BYTES(nwin);
     /* records and tiles: a tile never spans two windows, so at most one more a window */
     const uint64_t tile_cap = b->n_tiles + nwin + 1;
     te_tile_t *d_tiles = NULL;
@@ -1815,7 +1927,6 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
     for (int i = -1; i < iters; i++) { /* (run -1: the check run, untimed) */
         if (i == 0)
             HIPCHK(t, hipEventRecord(e0, t->stream));
-        HIPCHK(t, hipMemsetAsync(wbuf, 0, zb, t->stream));
         if (te_launch_index(&a, t->stream)) {
             te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));
             goto out;
@@ -2063,6 +2174,11 @@ struct te_pipe_s {
     uint64_t *h_tot[TE_PIPE_SLOTS];
     hipEvent_t idx_done[TE_PIPE_SLOTS];
     uint64_t idx_nwin;
+    /* the call's host image, and per slot the file offsets of its chunk's first record and
+       of the previous chunk's (~0: none, the chunk is the capture's first) -- for the Q8
+       replay's prefix records */
+    const uint8_t *img;
+    uint64_t first_off[TE_PIPE_SLOTS], prev_off[TE_PIPE_SLOTS];
 };
 
 void te_pipe_free(tcpedit_t *t)
@@ -2144,8 +2260,7 @@ static int pipe_ready(tcpedit_t *t, size_t chunk)
         HIPCHK(t, hipEventCreateWithFlags(&P->edit_done[s], hipEventDisableTiming));
         HIPCHK(t, hipEventCreateWithFlags(&P->d2h_done[s], hipEventDisableTiming));
         HIPCHK(t, hipEventCreateWithFlags(&P->idx_done[s], hipEventDisableTiming));
-        HIPCHK(t, hipMalloc((void **)&P->d_idx[s], IDX_WS_BYTES(P->idx_nwin) + IDX_WIN_BYTES(P->idx_nwin) +
-                                                       8 * (IDX_T__N + 2)));
+        HIPCHK(t, hipMalloc((void **)&P->d_idx[s], IDX_WS_BYTES(P->idx_nwin)));
         HIPCHK(t, hipHostMalloc((void **)&P->h_tot[s], 8 * IDX_T__N, 0));
     }
     return 0;
@@ -2189,6 +2304,15 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     if (*stopped == 2)
         return 0;
     memcpy(b->counters, b->res_pinned, sizeof(b->counters));
+    if (b->counters[TE_CNT_Q8_FAILED] && P->img && P->prev_off[s] != ~0ull) {
+        /* the stale bytes may come from earlier chunks: the replay walks back into their
+           records (the host image holds them all; the staging keeps the newest) */
+        tcpedit_batch_set_prefix(t, b, P->img + 24, P->first_off[s] - 24);
+        const int r = retry_q8_with_prefix(t, b, -1, b->counters);
+        tcpedit_batch_set_prefix(t, b, NULL, 0);
+        if (r < 0)
+            return -1;
+    }
     memcpy(b->err, b->res_pinned + TE_RES_ERR, sizeof(b->err));
     for (int i = 0; i < b->last_fgrid; i++) {
         const uint64_t *v = (const uint64_t *)(b->res_pinned + TE_RES_SLOTS) + 4 * (size_t)i;
@@ -2206,7 +2330,7 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     }
     if (b->counters[TE_CNT_Q8_FAILED]) {
         te_seterr(t, "a record's edit reads the reference's stale static packet buffer (SURVEY Appendix B Q8) "
-                     "at bytes written by an earlier pipeline chunk or by no record: not reproducible here");
+                     "at bytes written before the previous pipeline chunk or by no record: not reproducible here");
         return -1;
     }
     const uint64_t ob = b->out_base ? b->out_base : 24;
@@ -2295,6 +2419,8 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0, 0};
     int inflight[TE_PIPE_SLOTS] = {0, 0}, stopped = 0, k = 0, fallbacks = 0;
     uint64_t entry_file = 24;  /* host copy of where chunk k's records start (file offset) */
+    uint64_t prev_first = ~0ull;
+    P->img = img;
     uint64_t limit_img[TE_PIPE_SLOTS] = {0, 0}, file0[TE_PIPE_SLOTS] = {0, 0};
     IdxArgs A[TE_PIPE_SLOTS];
     const double t0 = te_now();
@@ -2342,7 +2468,6 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         a_->tile_cap = b_->idx_cap_tiles;                                                                     \
         a_->rec_cap = b_->idx_cap_pkts;                                                                       \
         HIPCHK(t, hipStreamWaitEvent(t->stream, P->h2d_done[s_], 0));                                        \
-        HIPCHK(t, hipMemsetAsync(P->d_idx[s_], 0, IDX_WS_BYTES(a_->nwin), t->stream));                       \
         if (te_launch_index(a_, t->stream)) {                                                                 \
             te_seterr(t, "device index launch failed: %s", hipGetErrorString(hipGetLastError()));            \
             goto fail;                                                                                        \
@@ -2364,7 +2489,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipEventSynchronize(P->idx_done[s]));
         t_wait += te_now() - tw;
         const uint64_t *T = P->h_tot[s];
-        const uint64_t entry_img = entry_file - file0[s] + 24;
+        const uint64_t entry_img = entry_file - file0[s] + 24, chunk_first = entry_file;
         b->pkt_base = pkts;
         b->launches = 0;
         b->gen_hint_ok = 0;
@@ -2443,6 +2568,9 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             inflight[s] = 1;
             chunk_pkt_base[s] = pkts;
             pkts += b->n_pkts;
+            P->first_off[s] = chunk_first;
+            P->prev_off[s] = prev_first;
+            prev_first = chunk_first;
         }
         if (more && !stopped)
             DIX_INDEX(k + 1);
@@ -2601,6 +2729,8 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     }
 
     uint64_t off = 24; /* file offset of the next chunk's first record */
+    uint64_t prev_first = ~0ull;
+    P->img = img;
     int k = 0;
     for (;; k++) {
         const int s = k % TE_PIPE_SLOTS;
@@ -2679,6 +2809,9 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         inflight[s] = 1;
         chunk_pkt_base[s] = pkts;
         pkts += b->n_pkts;
+        P->first_off[s] = off;
+        P->prev_off[s] = prev_first;
+        prev_first = off;
         off += rec_bytes;
 
         /* ---- the previous chunk: results in, D2H to its place ---- */

@@ -20,7 +20,6 @@
 #define IDX_ERROR 2u  /* len > 262144: the reference's error (walk_stop 2) */
 #define IDX_END 4u    /* a truncated record or the bytes ran out */
 #define IDX_ZERO 8u   /* a record with caplen 0 */
-#define IDX_OVF 16u   /* the window's tiles or records did not fit tile_cap / rec_cap */
 /* totals[] */
 #define IDX_T_RECS 0
 #define IDX_T_TILES 1
@@ -36,13 +35,13 @@
 #define IDX_T_BADWIN 11 /* diagnostics: the first window whose guess missed the chain */
 #define IDX_T__N 12
 
-/* the per-launch words the pass needs zeroed, at the start of its workspace:
-   ticket, the first stop / bad / zero-caplen / overflow windows (complemented), timeouts
-   (u32 each), scratch counter (u64) */
-#define IDX_WS_WORDS 64
-#define IDX_WS_BYTES(nwin) (IDX_WS_WORDS + 8ull * (nwin) /* state */)
-/* per-window records the finishing wave reads (not zeroed) */
-#define IDX_WIN_BYTES(nwin) (8ull * 4 * (nwin) /* entry, exit, pfx, err */ + 4ull * (nwin) /* flags */)
+/* records starting in one window, at most (a record is at least its 16-byte header) */
+#define IDX_MAXR (64 * TE_IDX_S / 16)
+/* the index's device workspace for nwin windows: per window its facts (entry, exit, flags,
+   records|tiles, scratch bytes) and prefixes (records|tiles, scratch), the totals, and the
+   count pass's cut (record offsets in their tiles, tile starts) for the write pass */
+#define IDX_WS_BYTES(nwin) (8ull * 6 * (nwin) + 4ull * ((nwin) + 1) + 8ull * (IDX_T__N + 2) + \
+                            (2ull + 8ull) * IDX_MAXR * (nwin) + 64)
 
 #ifdef __cplusplus
 extern "C" {
@@ -59,13 +58,11 @@ typedef struct {
     int32_t sw, nsec;
     uint32_t nwin;      /* windows of te_index_window_bytes() from entry & ~15 */
     uint32_t budget, max_pkts, growth; /* the wave-lane tile cut (walk_range) */
-    /* zeroed per launch (IDX_WS_BYTES) */
-    uint32_t *ticket, *stop_win_c, *bad_win_c, *zero_win_c, *ovf_win_c, *timeouts; /* (~first window) */
-    uint64_t *scratch_ctr;
-    uint64_t *state;    /* nwin look-back granules */
-    /* per window (IDX_WIN_BYTES) */
-    uint64_t *w_entry, *w_exit, *w_pfx, *w_err;
+    /* per window (IDX_WS_BYTES) */
+    uint64_t *w_entry, *w_exit, *w_agg, *w_scr, *w_pfx, *w_sbase;
     uint32_t *w_flags;
+    uint16_t *t_prel;   /* IDX_MAXR a window: each record's offset in its tile */
+    uint32_t *t_tile;   /* IDX_MAXR pairs a window: {first offset from the window, first | npkt << 16} */
     uint64_t *totals;   /* IDX_T__N words */
     /* the batch's index */
     te_tile_t *tiles;
@@ -74,7 +71,7 @@ typedef struct {
 } IdxArgs;
 /* bytes of a window */
 uint32_t te_index_window_bytes(void);
-/* the single pass (the workspace words zeroed by the caller first) */
+/* count, scan and write (nothing to zero first) */
 int te_launch_index(const IdxArgs *a, void *stream);
 #ifdef __cplusplus
 }

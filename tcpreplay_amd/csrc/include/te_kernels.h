@@ -145,6 +145,12 @@ typedef struct {
     int q8_file_start;        /* the launch's first record is the capture's first (buffer starts zeroed) */
     const uint8_t *q8_init;   /* device: the initial buffer instead of zeros (tcpedit_packet), or NULL */
     uint32_t q8_init_len;
+    /* the records just before the launch's first (the previous pipeline chunk's or shard's
+       last ones): the replay may walk back into them (records -q8_npre .. -1) */
+    const uint8_t *q8_pre;    /* device: their bytes (whole records, the launch's format) */
+    const uint64_t *q8_pre_off; /* device: q8_npre offsets into q8_pre */
+    uint32_t q8_npre;
+    int q8_pre_file_start;    /* the first of them is the capture's first record */
     /* SURVEY Q18 (a Linux cooked decoder into the en10mb encoder without --enet-dmac): the
        dst_modified carry.  NULL: none (every record's value is its own or false) */
     uint64_t *l2carry;        /* device: n_pkts + 1 scan results */

@@ -1908,7 +1908,9 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
 //   * walking back from the record, it finds the latest records whose memcpy
 //     covers [0, need) (each older one only matters where it reached further), or
 //     the capture's start, where the buffer is all zeros (safe_malloc, utils.c:38-48;
-//     tcpedit_packet: the caller's own buffer);
+//     tcpedit_packet: the caller's own buffer).  The walk may go on into the records
+//     just before the batch when the host staged them (the previous pipeline chunk's or
+//     shard's last records, record numbers -npre .. -1);
 //   * it replays tcpedit_packet over the emulated buffer for every record from there
 //     on, in order, normalising each edit to the reference's in-place layout (the
 //     encoders' memmove: the packet starts at the buffer start, bytes past its
@@ -1931,7 +1933,13 @@ struct Q8Args {
     uint32_t file_start;    // record 0 of the batch is the capture's first record
     const uint8_t *init_buf;  // the initial buffer (tcpedit_packet: the caller's), else zeros
     uint32_t init_len;
+    const uint8_t *pre;       // the records before the batch (-npre .. -1), or none
+    const uint64_t *pre_off;
+    uint32_t npre;
+    uint32_t pre_file_start;  // record -npre is the capture's first
 };
+constexpr int64_t Q8_START = -(1ll << 40);    // q8_chain: from the first record there is
+constexpr int64_t Q8_TOOLONG = -(1ll << 41);  // q8_chain: walked back too far
 
 __device__ __forceinline__ uint32_t q8_tile(const LaunchArgs &a, uint32_t j) {
     uint32_t lo = 0, hi = a.n_tiles - 1;
@@ -1947,23 +1955,29 @@ __device__ __forceinline__ uint64_t q8_rec(const LaunchArgs &a, uint32_t j) {
     return a.tiles[q8_tile(a, j)].span_off + a.pkt_rel[j];
 }
 
+// record j of the replay's range: the batch's, or (j < 0) one staged before it
+__device__ __forceinline__ const uint8_t *q8_recp(const Q8Args &q, int64_t j) {
+    return j >= 0 ? q.a.in + q8_rec(q.a, (uint32_t)j) : q.pre + q.pre_off[j + (int64_t)q.npre];
+}
+
 // the oldest record of the newest ones whose memcpy's cover [0, need) before record
-// `pos` (each older one only matters where it reached further); -1: the batch start
-__device__ int64_t q8_chain(const LaunchArgs &a, uint32_t pos, uint32_t need) {
-    const bool swp = a.in_swapped != 0;
+// `pos` (each older one only matters where it reached further); Q8_START: the first
+// record there is (the batch's, or the first staged before it)
+__device__ int64_t q8_chain(const Q8Args &q, int64_t pos, uint32_t need) {
+    const bool swp = q.a.in_swapped != 0;
     uint32_t cov = 0;
-    int64_t j0 = -1;
+    int64_t j0 = Q8_START;
     uint32_t steps = 0;
-    for (int64_t j = (int64_t)pos - 1; j >= 0; --j) {
-        if (++steps > Q8_MAX_CHAIN) return -2;
-        const uint32_t cl = ld_hdr32(a.in + q8_rec(a, (uint32_t)j) + 8, swp);
+    for (int64_t j = pos - 1; j >= -(int64_t)q.npre; --j) {
+        if (++steps > Q8_MAX_CHAIN) return Q8_TOOLONG;
+        const uint32_t cl = ld_hdr32(q8_recp(q, j) + 8, swp);
         if (cl > cov) {
             cov = cl;
             j0 = j;
             if (cov >= need) return j0;
         }
     }
-    return -1;
+    return Q8_START;
 }
 
 enum { Q8_OK = 0, Q8_FAIL = 1, Q8_DEEPER = 2 };
@@ -1973,15 +1987,17 @@ enum { Q8_OK = 0, Q8_FAIL = 1, Q8_DEEPER = 2 };
 // replay has (*needd), so it has to start further back
 template <bool FZ>
 __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t start, uint32_t i, uint64_t out_off,
-                              uint8_t *slot, uint32_t *jd, uint32_t *needd) {
+                              uint8_t *slot, int64_t *jd, uint32_t *needd) {
     const LaunchArgs &a = q.a;
     const bool swp = a.in_swapped != 0;
     uint8_t *buf = slot + Q8_HEAD;
     uint32_t V = 0;  // bytes [0, V) of the emulated buffer are known
-    uint32_t j0 = (uint32_t)start;
-    if (start < 0) {
-        if (!q.file_start) return Q8_FAIL;  // the bytes come from before this batch
-        j0 = 0;
+    int64_t j0 = start;
+    if (start == Q8_START) {
+        // the bytes come from before every record there is: the capture's start (zeros),
+        // else they are not here
+        if (!(q.npre ? q.pre_file_start : q.file_start)) return Q8_FAIL;
+        j0 = -(int64_t)q.npre;
         if (q.init_buf) {
             for (uint32_t x = 0; x < q.init_len; ++x) buf[x] = q.init_buf[x];
             V = q.init_len;
@@ -1990,14 +2006,16 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
             V = MAXPACKET;
         }
     }
-    for (uint32_t j = j0; j <= i; ++j) {
-        const uint8_t *rec = a.in + q8_rec(a, j);
+    for (int64_t j = j0; j <= (int64_t)i; ++j) {
+        const uint8_t *rec = q8_recp(q, j);
         const uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp) / (a.in_nsec ? 1000u : 1u);
         const uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
         if (caplen > MAX_SNAPLEN) return Q8_FAIL;
         for (uint32_t x = 0; x < caplen; ++x) buf[x] = rec[16 + x];  // tcprewrite.c:301
         if (caplen > V) V = caplen;
-        const uint64_t pktno = a.pkt_base + j;
+        if (j < 0 && (a.l2carry || (FZ && a.fuzz_mode == TE_FUZZ_APPLY)))
+            return Q8_FAIL;  // (a staged record's carried state is not at hand)
+        const uint64_t pktno = a.pkt_base + (uint64_t)j;
         int dir = TE_DIR_C2S;
         const bool explicit_dir = a.fixed_dir >= 0;
         if (explicit_dir) {
@@ -2034,7 +2052,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
             *needd = pk.need;
             return Q8_DEEPER;
         }
-        if (j == i) {
+        if (j == (int64_t)i) {
             if (rc == RC_ERROR || rc == RC_SOFT) return Q8_FAIL;  // cannot change the pass-1 layout
             g_u8 *o = (g_u8 *)a.out + out_off;
             const uint32_t oc = (uint32_t)o[8] | ((uint32_t)o[9] << 8) | ((uint32_t)o[10] << 16) |
@@ -2066,20 +2084,20 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
 
 template <bool FZ>
 __device__ bool q8_replay_one(const Q8Args &q, const te_dev_cfg_t &cfg, uint4 ent, uint8_t *slot) {
-    const LaunchArgs &a = q.a;
     const uint32_t i = ent.x, need = ent.y;
     const uint64_t out_off = (uint64_t)ent.z | ((uint64_t)ent.w << 32);
     if (need == NEED_NEVER || need > MAXPACKET) return false;
-    int64_t start = q8_chain(a, i, need);
+    int64_t start = q8_chain(q, i, need);
     // an earlier record of the replay may read past what it has: start further back
     for (int iter = 0; iter < 64; ++iter) {
-        if (start < -1) return false;
-        uint32_t jd = 0, nd = 0;
+        if (start == Q8_TOOLONG) return false;
+        int64_t jd = 0;
+        uint32_t nd = 0;
         const int r = q8_replay_from<FZ>(q, cfg, start, i, out_off, slot, &jd, &nd);
         if (r == Q8_OK) return true;
-        if (r == Q8_FAIL || start < 0) return false;
-        const int64_t s2 = q8_chain(a, jd, nd);
-        if (s2 >= start && s2 >= 0) return false;  // no progress
+        if (r == Q8_FAIL || start == Q8_START) return false;
+        const int64_t s2 = q8_chain(q, jd, nd);
+        if (s2 != Q8_START && s2 >= start) return false;  // no progress
         start = s2;
     }
     return false;
@@ -2456,6 +2474,10 @@ extern "C" int te_launch_q8(te_launch_t *L, hipStream_t stream) {
     q.file_start = (uint32_t)L->q8_file_start;
     q.init_buf = L->q8_init;
     q.init_len = L->q8_init_len;
+    q.pre = L->q8_npre ? L->q8_pre : nullptr;
+    q.pre_off = L->q8_npre ? L->q8_pre_off : nullptr;
+    q.npre = L->q8_pre && L->q8_pre_off ? L->q8_npre : 0u;
+    q.pre_file_start = (uint32_t)L->q8_pre_file_start;
     if (!q.scratch || q.n_threads == 0 || q.n_threads % Q8_BLOCK || !L->q8_list || L->n_tiles == 0) return -1;
     if (q.a.fuzz_mode == TE_FUZZ_APPLY)
         hipLaunchKernelGGL(te_q8_replay<true>, dim3(q.n_threads / Q8_BLOCK), dim3(Q8_BLOCK), 0, stream, q);

@@ -38,13 +38,6 @@
 
 #include "te_index.h"
 
-// TE_IDX_STAMPS builds (diagnostics only): s_memtime per phase of a few windows, printed
-#if TE_IDX_STAMPS
-#define IX_STAMP(i) do { __builtin_amdgcn_sched_barrier(0); ix_t[i] = __builtin_amdgcn_s_memtime(); \
-                         __builtin_amdgcn_sched_barrier(0); } while (0)
-#else
-#define IX_STAMP(i)
-#endif
 namespace {
 typedef uint8_t u8;
 typedef uint16_t u16;
@@ -55,8 +48,7 @@ constexpr int IW = 64;                       // lanes (sub-windows) per window
 constexpr int IB = 256;                      // threads per block: 4 windows in flight
 constexpr int IWAVES = IB / IW;
 constexpr u32 MAXCAP = 262144u;
-constexpr u64 F_AGG = 1ull << 62, F_PFX = 2ull << 62, VMASK = (1ull << 62) - 1;
-constexpr int REC_BITS = 36;                 // granule value: records | tiles << 36
+constexpr int REC_BITS = 36;                 // a window's (records | tiles << 36)
 constexpr u64 REC_MASK = (1ull << REC_BITS) - 1;
 
 // one wave's LDS: the staged window, its record offsets, per-record tile starts, tile starts
@@ -120,46 +112,6 @@ __device__ __forceinline__ LaneWalk walk_lds(const IdxArgs &a, const u32 *img, u
     return w;
 }
 
-// decoupled look-back over windows, one wave (tcpedit_kernels.hip's, for 64-bit packed
-// granules {flag:2 | value:62}, relaxed agent-scope atomics: the value is the hand-off)
-__device__ u64 lookback(u64 *state, u32 t, u64 agg, u32 *timeouts) {
-    const int lane = threadIdx.x & 63;
-    if (t == 0) {
-        if (lane == 0) __hip_atomic_store(&state[0], F_PFX | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
-    }
-    if (lane == 0) __hip_atomic_store(&state[t], F_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u64 excl = 0;
-    int64_t j = (int64_t)t - 1;
-    unsigned spins = 0;
-    while (j >= 0) {
-        const int64_t idx = j - lane;
-        u64 g = F_PFX;
-        if (idx >= 0) g = __hip_atomic_load(&state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u64 f = g & ~VMASK;
-        const u64 pm = __ballot(f == F_PFX), zm = __ballot(f == 0);
-        const int first_p = pm ? __builtin_ctzll(pm) : 64;
-        const int first_z = zm ? __builtin_ctzll(zm) : 64;
-        const int take = first_z < first_p ? first_z : (first_p < 64 ? first_p + 1 : 64);
-        u64 v = lane < take ? (g & VMASK) : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        excl += v;
-        if (first_p < first_z) break;
-        j -= take;
-        if (first_z < 64) {
-            if (++spins > (1u << 24)) {  // bounded spin: report and give up
-                if (lane == 0) atomicAdd(timeouts, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (lane == 0)
-        __hip_atomic_store(&state[t], F_PFX | ((excl + agg) & VMASK), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
-
 // a candidate's strength: 0 no header here, 1 a header whose successor is not staged (or
 // past the image), 2 a header followed by a staged acceptable one (or ending the image)
 __device__ __forceinline__ int strength(const IdxArgs &a, const u32 *img, u64 A0, u64 staged_end, u64 p) {
@@ -181,26 +133,17 @@ __device__ __forceinline__ int strength(const IdxArgs &a, const u32 *img, u64 A0
 // sub-windows, whose only job is to establish the chain entering ws (a guess there that is
 // not a record start is corrected as the chain runs on, or leaves the window before ws).
 template <int S, int OL>
-__global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
+__global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
     constexpr int W = IW * S;       // staged sub-window bytes
     constexpr int O = OL * S;       // overlap before the window
     constexpr int WN = W - O;       // bytes a window owns
     static_assert(S % 16 == 0 && S <= 128, "sub-window: whole 16-byte chunks, <= two 64-bit masks");
     __shared__ WinLds<S> L[IWAVES];
-    __shared__ u32 blk_ticket;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     WinLds<S> &M = L[wv];
-    // one ticket a block (its waves take consecutive windows): windows are numbered in the
-    // order blocks start, so a window's look-back only waits on windows already running
-    if (threadIdx.x == 0) blk_ticket = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    const u32 k = blk_ticket * IWAVES + (u32)wv;
+    const u32 k = blockIdx.x * IWAVES + (u32)wv;  // windows are independent here: no order
     if (k >= a.nwin) return;
-#if TE_IDX_STAMPS
-    unsigned long long ix_t[10] = {};
-    int ix_rounds = 0;
-#endif
-    IX_STAMP(0);
+
     // the first record: known to the host (a.entry), or where the previous pipeline chunk's
     // chain ended (read on the device: that chunk's index ran before this one on the stream)
     const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
@@ -236,7 +179,6 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     // moving a lane's reads of other lanes' stores across them (no block barrier: the
     // block's waves work on their own windows and may have left already)
     asm volatile("" ::: "memory");
-    IX_STAMP(1);
 
     // ---- this lane's guess: the first strong candidate in its sub-window, else the first weak ----
     const u64 lo = A0 + (u64)lane * S, hi_raw = lo + S;
@@ -286,7 +228,6 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     }
     LaneWalk w = e != IDX_NONE ? walk_lds(a, M.img, A0, e, hi) : LaneWalk{0, 0, 0};
     bool has = e != IDX_NONE;
-    IX_STAMP(2);
 
     // ---- where the chain starts: the first guess the next guess confirms (its walk ends
     // exactly there, or at a strong candidate).  A guess that is not a record start jumps by a garbage length, so it is
@@ -350,15 +291,11 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
                 change = true;
             }
         }
-#if TE_IDX_STAMPS
-        ix_rounds = round + 1;
-#endif
         if (!__ballot(change)) {
             settled = true;
             break;
         }
     }
-    IX_STAMP(3);
     if (!settled) {  // the serial lane loop (exact)
         u64 cur = IDX_NONE;
         u32 ended = 0;
@@ -390,7 +327,6 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
             ended = (u32)__shfl((int)w.stop, (int)l);
         }
     }
-    IX_STAMP(4);
     // only the window's own lanes' records count (the overlap's are window k - 1's)
     if (lane < OL) has = false;
     // the window's entry, exit and how the chain ends here
@@ -447,134 +383,211 @@ __global__ __launch_bounds__(IB) void te_index_windows(IdxArgs a) {
     }
     if (lane == 0) M.tst[ntile] = (u16)nrec;
     asm volatile("" ::: "memory");
-    IX_STAMP(5);
 
-    // ---- the window's record and tile numbers ----
-    const u64 agg = (u64)nrec | ((u64)ntile << REC_BITS);
-    // publish where the chain enters and leaves this window before the aggregate: a later
-    // window reads them once its look-back has seen this window's granule (release here,
-    // acquire there)
+    // ---- the window's facts for the scan, and its cut for the write pass ----
+    // (huge records -- larger than a tile -- get an HBM scratch slot: its bytes here, the
+    // slot's offset from the scan of every window's bytes)
+    u64 scr = 0;
+    for (u32 t = lane; t < ntile; t += IW) {
+        const u32 s0 = M.tst[t], s1 = M.tst[t + 1];
+        const u32 span = M.rel[s1] - M.rel[s0];
+        const u32 g = (u32)((ws + M.rel[s0]) & 15);
+        if (s1 - s0 == 1 && !TE_CONTIG_FITS_IN(g, span, a.budget) && !TE_CONTIG_FITS(g, span))
+            scr += ((u64)TE_SLOT_BYTES_OF(g, span - 16) + TE_LDS_FRONT + 64 + 255) & ~255ull;
+        if (t < (u32)IDX_MAXR) ((uint2 *)a.t_tile)[(u64)k * IDX_MAXR + t] = make_uint2(M.rel[s0], s0 | (s1 - s0) << 16);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) scr += __shfl_xor(scr, o, 64);
+    for (u32 i = lane; i < nrec; i += IW)
+        if (i < (u32)IDX_MAXR) a.t_prel[(u64)k * IDX_MAXR + i] = (u16)(M.rel[i] - M.rel[M.tsi[i]]);
     if (lane == 0) {
         a.w_entry[k] = went;
         a.w_exit[k] = wexit;
-        a.w_flags[k] = wstop;
-        __threadfence();
+        a.w_flags[k] = wstop | (anyzero ? IDX_ZERO : 0u);
+        a.w_agg[k] = (u64)nrec | ((u64)ntile << REC_BITS);
+        a.w_scr[k] = scr;
     }
-    IX_STAMP(6);
-    const u64 excl = lookback(a.state, k, agg, a.timeouts);
-    const u64 pbase = excl & REC_MASK, tbase = excl >> REC_BITS;
-    IX_STAMP(7);
-    if (lane == 0) {
-        a.w_pfx[k] = excl + agg;
-        if (wstop == IDX_ERROR) a.w_err[k] = pbase + nrec;  // the record the chain stopped at
-        // (zeroed words: max of ~k = the first such window)
-        if (wstop) atomicMax(a.stop_win_c, ~k);
-        if (anyzero) atomicMax(a.zero_win_c, ~k);
-        // the chain across windows, checked here: every earlier window has published (the
-        // look-back saw their granules).  This window's first record must be where the chain
-        // left the nearest earlier window a record starts in; a window without one must be
-        // passed over whole.  Only windows up to the chain's end matter: the finishing pass
-        // compares the first bad window with the first stop.
-        __threadfence();
+}
+
+// ---- the scan: one block over every window's facts ----
+// exclusive prefixes of (records | tiles) and of scratch bytes; the chain checked across
+// windows (a window's first record must be where the chain left the nearest earlier window
+// a record starts in; a window without one must be passed over whole); libpcap's first
+// stop; the totals.  Each thread takes a contiguous run of windows.
+constexpr int SB = 1024;
+template <typename T, typename Op>
+__device__ __forceinline__ T block_scan_ex(T v, T ident, Op op, T *sh, T &total) {
+    // exclusive scan over the block's threads in thread order (Hillis-Steele in LDS)
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < SB; o <<= 1) {
+        const T y = tid >= o ? sh[tid - o] : ident;
+        __syncthreads();
+        sh[tid] = op(sh[tid], y);
+        __syncthreads();
+    }
+    total = sh[SB - 1];
+    const T ex = tid ? sh[tid - 1] : ident;
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(SB) void te_index_scan(IdxArgs a) {
+    __shared__ u64 sh64[SB];
+    __shared__ long long shi[SB];
+    const int tid = threadIdx.x;
+    const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
+    constexpr u64 WN = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;
+    const u32 kE = (u32)((entry - a.base) / WN);
+    const u32 nw = a.nwin, per = (nw + SB - 1) / SB;
+    const u32 k0 = tid * per < nw ? tid * per : nw, k1 = k0 + per < nw ? k0 + per : nw;
+    // the first stop (windows past it are not the chain's)
+    long long fs = 0x7fffffffffffffffll, lastrec = -1;
+    u64 agg = 0, scr = 0;
+    for (u32 q = k0; q < k1; ++q) {
+        if (fs == 0x7fffffffffffffffll && (a.w_flags[q] & (IDX_STOP | IDX_ERROR | IDX_END)) &&
+            a.w_entry[q] != IDX_NONE)
+            fs = q;
+        agg += a.w_agg[q];
+        scr += a.w_scr[q];
+        if (q >= kE && a.w_entry[q] != IDX_NONE) lastrec = q;
+    }
+    long long stop_tot;
+    {
+        long long t = 0;
+        (void)block_scan_ex<long long>(fs, 0x7fffffffffffffffll, [](long long x, long long y) { return x < y ? x : y; },
+                                       shi, t);
+        stop_tot = t;
+    }
+    const u32 last = stop_tot != 0x7fffffffffffffffll ? (u32)stop_tot : nw - 1;
+    u64 tot_agg, tot_scr;
+    u64 ex_agg = block_scan_ex<u64>(agg, 0ull, [](u64 x, u64 y) { return x + y; }, sh64, tot_agg);
+    u64 ex_scr = block_scan_ex<u64>(scr, 0ull, [](u64 x, u64 y) { return x + y; }, sh64, tot_scr);
+    long long lr_all;
+    long long prev_rec = block_scan_ex<long long>(lastrec, -1ll, [](long long x, long long y) { return x > y ? x : y; },
+                                                  shi, lr_all);
+    // per window: its bases, the chain check, and where the chain ends
+    long long first_bad = 0x7fffffffffffffffll;
+    bool zero = false;
+    for (u32 q = k0; q < k1; ++q) {
+        const u64 eq = a.w_entry[q];
+        a.w_pfx[q] = ex_agg;
+        a.w_sbase[q] = ex_scr;
+        ex_agg += a.w_agg[q];
+        ex_scr += a.w_scr[q];
+        if (q > last) continue;
+        zero |= (a.w_flags[q] & IDX_ZERO) != 0;
         bool bad = false;
-        if (k == kE) {
-            bad = went != entry;
-        } else if (k > kE) {
-            u32 j = k - 1;
-            while (j > kE && ((volatile u64 *)a.w_entry)[j] == IDX_NONE) --j;
-            const u64 xj = ((volatile u64 *)a.w_exit)[j];
-            if (went != IDX_NONE) {
-                bad = xj != went;
+        if (q == kE) {
+            bad = eq != entry;
+        } else if (q > kE) {
+            const long long j = prev_rec >= (long long)kE ? prev_rec : (long long)kE;
+            const u64 xj = a.w_exit[j];
+            if (eq != IDX_NONE) {
+                bad = xj != eq;
             } else {
-                const u64 qe = base + (u64)(k + 1) * WN;
-                bad = xj < (qe < a.len ? qe : a.len) &&
-                      !(((volatile u32 *)a.w_flags)[j] & (IDX_STOP | IDX_ERROR | IDX_END));
+                const u64 qe = a.base + (u64)(q + 1) * WN;
+                bad = xj < (qe < a.len ? qe : a.len) && !(a.w_flags[j] & (IDX_STOP | IDX_ERROR | IDX_END));
             }
         }
-        if (bad) atomicMax(a.bad_win_c, ~k);
+        if (bad && first_bad == 0x7fffffffffffffffll) first_bad = q;
+        if (q >= kE && eq != IDX_NONE) prev_rec = q;
     }
+    long long fb;
+    {
+        long long t = 0;
+        (void)block_scan_ex<long long>(first_bad, 0x7fffffffffffffffll,
+                                       [](long long x, long long y) { return x < y ? x : y; }, shi, t);
+        fb = t;
+    }
+    long long zr;
+    (void)block_scan_ex<long long>(zero ? 1ll : 0ll, 0ll, [](long long x, long long y) { return x | y; }, shi, zr);
+    if (tid == 0) {
+        // the chain's last window with a record, at or before `last`
+        long long j = last;
+        while (j > (long long)kE && a.w_entry[j] == IDX_NONE) --j;
+        const u64 tot = a.w_pfx[last] + a.w_agg[last];  // inclusive (records | tiles) through `last`
+        const u32 fl = a.w_flags[last];
+        const bool stopped = stop_tot != 0x7fffffffffffffffll;
+        const bool bad = fb != 0x7fffffffffffffffll && fb <= (long long)last;
+        a.totals[IDX_T_RECS] = tot & REC_MASK;
+        a.totals[IDX_T_TILES] = tot >> REC_BITS;
+        a.totals[IDX_T_SCRATCH] = a.w_sbase[last] + a.w_scr[last];
+        a.totals[IDX_T_BAD] = bad ? 1 : 0;
+        a.totals[IDX_T_WINDOWS] = last + 1;
+        a.totals[IDX_T_STOP] = stopped ? (fl & (IDX_STOP | IDX_ERROR | IDX_END)) : 0;
+        const u64 end = a.w_exit[j];
+        a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
+        a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
+        a.totals[IDX_T_ZERO] = zr ? 1 : 0;
+        // the record the chain stopped at: the one after the stopping window's last
+        a.totals[IDX_T_ERR_REC] = stopped && (fl & IDX_ERROR) ? tot & REC_MASK : ~0ull;
+        a.totals[IDX_T_OVERFLOW] = (tot & REC_MASK) > a.rec_cap || (tot >> REC_BITS) > a.tile_cap ? 1 : 0;
+        a.totals[IDX_T_BADWIN] = bad ? (u64)fb : 0xffffffffull;
+    }
+}
 
-    // ---- tiles and record offsets in place ----
-    bool ovf = false;
-    for (u32 t = lane; t < ntile; t += IW) {
-        const u32 s0 = M.tst[t], s1 = M.tst[t + 1];
+// ---- the write pass: a wave per window puts its tiles and record offsets at its bases ----
+__global__ __launch_bounds__(IB) void te_index_write(IdxArgs a) {
+    const int lane = threadIdx.x & 63;
+    const u32 k = blockIdx.x * IWAVES + (threadIdx.x >> 6);
+    if (k >= a.nwin) return;
+    const u64 *T = a.totals;
+    if (T[IDX_T_BAD] || T[IDX_T_OVERFLOW] || k >= T[IDX_T_WINDOWS]) return;  // (the host index stays)
+    constexpr u64 WN = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;
+    const u64 ws = a.base + (u64)k * WN;
+    const u64 agg = a.w_agg[k], pfx = a.w_pfx[k];
+    const u32 nrec = (u32)(agg & REC_MASK), ntile = (u32)(agg >> REC_BITS);
+    if (!nrec) return;
+    const u64 pbase = pfx & REC_MASK, tbase = pfx >> REC_BITS;
+    const u32 rend = (u32)(a.w_exit[k] - ws);  // the window's last record's end
+    u64 sb = a.w_sbase[k];
+    for (u32 t0 = 0; t0 < ntile; t0 += IW) {
+        const u32 t = t0 + lane;
+        const bool v = t < ntile;
+        uint2 me = v ? ((const uint2 *)a.t_tile)[(u64)k * IDX_MAXR + t] : make_uint2(0, 0);
+        const u32 nx = t + 1 < ntile ? ((const uint2 *)a.t_tile)[(u64)k * IDX_MAXR + t + 1].x : rend;
         te_tile_t tl;
-        tl.span_off = ws + M.rel[s0];
-        tl.first_pkt = (u32)(pbase + s0);
-        tl.npkt = s1 - s0;
-        tl.span_len = (u32)(M.rel[s1] - M.rel[s0]);
+        tl.span_off = ws + me.x;
+        tl.first_pkt = (u32)(pbase + (me.y & 0xffffu));
+        tl.npkt = me.y >> 16;
+        tl.span_len = nx - me.x;
         tl.flags = 0;
         tl.scratch_off = TE_NO_SCRATCH;
         const u32 g = (u32)(tl.span_off & 15);
-        if (tl.npkt == 1 && !TE_CONTIG_FITS_IN(g, tl.span_len, a.budget)) {
-            if (TE_CONTIG_FITS(g, tl.span_len)) {
+        u64 mine = 0;
+        if (v && tl.npkt == 1 && !TE_CONTIG_FITS_IN(g, tl.span_len, a.budget)) {
+            if (TE_CONTIG_FITS(g, tl.span_len))
                 tl.flags = TE_TILE_SOLO;
-            } else {  // a record larger than a tile: its slot in HBM scratch
-                const u32 slot = TE_SLOT_BYTES_OF(g, tl.span_len - 16);
-                const u64 sb = (slot + TE_LDS_FRONT + 64 + 255) & ~255ull;
-                tl.scratch_off = atomicAdd((unsigned long long *)a.scratch_ctr, (unsigned long long)sb);
-            }
+            else  // a record larger than a tile: its slot in HBM scratch
+                mine = ((u64)TE_SLOT_BYTES_OF(g, tl.span_len - 16) + TE_LDS_FRONT + 64 + 255) & ~255ull;
         }
-        if (tbase + t < a.tile_cap) a.tiles[tbase + t] = tl;
-        else ovf = true;
+        u64 x = mine;  // inclusive wave scan of the slot bytes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (mine) tl.scratch_off = sb + x - mine;
+        sb += __shfl(x, 63);
+        if (v) a.tiles[tbase + t] = tl;
     }
-    for (u32 i = lane; i < nrec; i += IW) {
-        if (pbase + i < a.rec_cap) a.pkt_rel[pbase + i] = (u16)(M.rel[i] - M.rel[M.tsi[i]]);
-        else ovf = true;
-    }
-    // (a window past the chain's end counts records that are not -- it may overflow: only
-    // the windows up to the end are looked at)
-    if (__ballot(ovf) && lane == 0) atomicMax(a.ovf_win_c, ~k);
-#if TE_IDX_STAMPS
-    IX_STAMP(8);
-    if (lane == 0 && (k < 3 || k % 4096 == 0 || k + 1 == a.nwin))
-        printf("IX win %u/%u settled %d rounds %d nrec %u ntile %u | stage %llu guess %llu jacobi %llu serial %llu "
-               "pos %llu cut %llu lookback %llu write %llu\n", k, a.nwin, (int)settled, ix_rounds, nrec, ntile,
-               ix_t[1] - ix_t[0], ix_t[2] - ix_t[1], ix_t[3] - ix_t[2], ix_t[4] - ix_t[3], ix_t[5] - ix_t[4],
-               ix_t[6] - ix_t[5], ix_t[7] - ix_t[6], ix_t[8] - ix_t[7]);
-#endif
-}
-
-// the totals, after every window is done (one wave, the next kernel on the stream)
-__global__ __launch_bounds__(64) void te_index_finish(IdxArgs a) {
-    const int lane = threadIdx.x;
-    if (lane != 0) return;
-    const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
-    constexpr int WN = IW * TE_IDX_S - TE_IDX_OL * TE_IDX_S;
-    const u32 kE = (u32)((entry - a.base) / WN);
-    const u32 stop_c = *a.stop_win_c, bad_c = *a.bad_win_c, zero_c = *a.zero_win_c, ovf_c = *a.ovf_win_c;
-    const u32 last = stop_c ? ~stop_c : a.nwin - 1;  // windows past the chain's end do not count
-    const bool bad = bad_c && ~bad_c <= last;
-    u32 j = last;
-    while (j > kE && a.w_entry[j] == IDX_NONE) --j;
-    const u64 tot = a.w_pfx[last];
-    const u32 fl = a.w_flags[last];
-    const bool stopped = stop_c != 0;
-    a.totals[IDX_T_RECS] = tot & REC_MASK;
-    a.totals[IDX_T_TILES] = tot >> REC_BITS;
-    a.totals[IDX_T_SCRATCH] = *a.scratch_ctr;
-    a.totals[IDX_T_BAD] = bad || *a.timeouts ? 1 : 0;
-    a.totals[IDX_T_WINDOWS] = last + 1;
-    a.totals[IDX_T_STOP] = stopped ? (fl & (IDX_STOP | IDX_ERROR | IDX_END)) : 0;
-    const u64 end = a.w_exit[j];
-    a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
-    a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
-    a.totals[IDX_T_ZERO] = zero_c && ~zero_c <= last ? 1 : 0;
-    a.totals[IDX_T_ERR_REC] = stopped && (fl & IDX_ERROR) ? a.w_err[last] : ~0ull;
-    a.totals[IDX_T_OVERFLOW] = ovf_c && ~ovf_c <= last ? 1 : 0;
-    a.totals[IDX_T_BADWIN] = bad ? ~bad_c : 0xffffffffu;
+    for (u32 i = lane; i < nrec; i += IW) a.pkt_rel[pbase + i] = a.t_prel[(u64)k * IDX_MAXR + i];
 }
 }  // namespace
 
 extern "C" uint32_t te_index_window_bytes(void) { return IW * TE_IDX_S - TE_IDX_OL * TE_IDX_S; }
 
-// the workspace words the pass needs zeroed (state granules, ticket, done, stop, counters)
+// count (a wave per window), scan (one block), write (a wave per window): no workspace
+// needs zeroing and no window waits on another
 extern "C" int te_launch_index(const IdxArgs *args, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const IdxArgs a = *args;
     if (a.nwin == 0) return 0;
     const u32 blocks = (a.nwin + IWAVES - 1) / IWAVES;
-    hipLaunchKernelGGL((te_index_windows<TE_IDX_S, TE_IDX_OL>), dim3(blocks), dim3(IB), 0, st, a);
-    hipLaunchKernelGGL(te_index_finish, dim3(1), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((te_index_count<TE_IDX_S, TE_IDX_OL>), dim3(blocks), dim3(IB), 0, st, a);
+    hipLaunchKernelGGL(te_index_scan, dim3(1), dim3(SB), 0, st, a);
+    hipLaunchKernelGGL(te_index_write, dim3(blocks), dim3(IB), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -91,6 +91,8 @@ static void *shard_main(void *arg)
                                               J->cache_len, J->base[k]);
             if (!S->b)
                 snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
+            else if (k > 0) /* the earlier shards: read only by a stale-buffer replay */
+                tcpedit_batch_set_prefix(S->te, S->b, J->in + 24, J->off[k] - 24);
         }
     }
     if (S->b) {

@@ -176,7 +176,7 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
         sh, err = None, ""
         try:
             sh = _DeviceShard(bytes(pcap[:PCAP_HDR_LEN]), p.segment(pcap, rank), args, cache, p.pkt_base[rank],
-                              dev)
+                              dev, prefix=memoryview(pcap)[PCAP_HDR_LEN:p.offsets[rank]] if rank else None)
         except Exception as e:  # noqa: BLE001 -- every rank raises after the exchange
             err = f"rank {rank}: {e}"
         bad, skip, carry_in = _pre_edit(dist, cdev, sh is not None, sh.reach if sh else 0, sh.carry if sh else 2)
@@ -234,12 +234,17 @@ class _DeviceShard:
     the fuzz step, the dst_modified carry-out) by the constructor, edited by run(), its
     output left in HBM until written"""
 
-    def __init__(self, hdr, seg, args, cache, pkt_base, device):
+    def __init__(self, hdr, seg, args, cache, pkt_base, device, prefix=None):
         from . import Batch, TcpEdit
         self.te = TcpEdit(args, dlt=capture_dlt(hdr if hdr is not None else seg), device=device)
-        self.b = None
+        self.b, self.prefix = None, None
         try:
             self.b = Batch(self.te, seg, cache, pkt_base=pkt_base, hdr=hdr)
+            if prefix is not None and len(prefix):
+                # the earlier shards' records: read only if a record's edit reads the static
+                # buffer past this shard's bytes (SURVEY Q8), then the replay walks back into them
+                self.prefix = prefix
+                self.b.set_prefix(prefix)
             self.reach = self.b.fuzz_reach() if fuzz_enabled(args) else 0
             self.carry = self.b.l2carry_out()
         except Exception:
@@ -271,6 +276,7 @@ class _DeviceShard:
         if self.b is not None:
             self.b.close()
             self.b = None
+        self.prefix = None  # (a view of the caller's mmap: released with the batch)
         self.te.close()
 
 
@@ -350,7 +356,8 @@ def rewrite_file_distributed(in_path: str, args, out_path: str, cache_path: Opti
         if editor is None:
             dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
             try:
-                sh = _DeviceShard(hdr, p.segment(mm, rank), args, cache, p.pkt_base[rank], dev)
+                sh = _DeviceShard(hdr, p.segment(mm, rank), args, cache, p.pkt_base[rank], dev,
+                                  prefix=memoryview(mm)[PCAP_HDR_LEN:p.offsets[rank]] if rank else None)
             except Exception as e:  # noqa: BLE001 -- travels in the exchange below
                 err = f"rank {rank}: {e}"
             # every rank, opened or not: no rank is left waiting in a collective

@@ -338,6 +338,36 @@ def test_two_rank_gpu_rewrite_equals_oracle(built, case):
     assert out == exp
 
 
+def _q8_across_the_cut(world=2):
+    """IPv6 records, one overstating its payload just after the shard cut, its donor (a
+    longer record) just before it: the replay of shard 1's record walks back into shard 0"""
+    import struct
+    recs = S.records(S.pcap_fixed(3_000, 90, ipv6=True, proto=17, seed=15))
+    cover = S.records(S.pcap_fixed(1, 500, ipv6=True, proto=17, seed=16))[0]
+    cut = D.plan(S.build_pcap(recs), world).pkt_base[1]
+    recs[cut - 20] = cover
+    ts, tu, cl, ln, d = recs[cut + 20]
+    d = bytearray(d)
+    struct.pack_into(">H", d, 18, struct.unpack_from(">H", d, 18)[0] + 60)
+    recs[cut + 20] = (ts, tu, cl, ln, bytes(d))
+    pcap = S.build_pcap(recs)
+    p = D.plan(pcap, world)
+    assert p.pkt_base[1] <= cut + 20 and p.pkt_base[1] > cut - 20
+    return pcap
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_q8_donor_in_the_previous_shard(built):
+    pcap = _q8_across_the_cut()
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    out, res = run_world(pcap, ["--fixcsum"], None, use_gpu=True)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
+    out, res = run_file_world(pcap, ["--fixcsum"], None, use_gpu=True)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["c4_cache", "fuzz_imix"])
 def test_two_rank_gpu_file_rewrite_equals_oracle(built, case):

@@ -126,23 +126,56 @@ def test_mutated_captures_with_stale_reads(built, seed):
         assert r.unsupported == 0 and rc == rc_o and out == exp, args
 
 
-def test_pipelined_chunk_replays_inside_the_chunk_or_fails_loudly(built):
-    """chunk 0 starts at the capture's start; in a later chunk a replay whose records all
-    lie in that chunk succeeds, one reaching back into the previous chunk is refused"""
+def test_pipelined_chunks_replay_across_chunk_boundaries(built):
+    """chunk 0 starts at the capture's start; a later chunk's replay walks back into the
+    earlier chunks' records (tcprewrite's buffer carries across the whole run,
+    tcprewrite.c:267-280): a donor just before the chunk, and one that is the capture's
+    zeroed start two chunks back"""
     recs = S.records(S.pcap_fixed(30_000, 90, ipv6=True, proto=17, seed=11))
     cover = S.records(S.pcap_fixed(1, 400, ipv6=True, proto=17, seed=12))[0]
     recs[20_001] = cover  # a longer record just before the overread covers it
-    ok = S.build_pcap(_overstate(recs, [3, 20_002], by=40))
-    rc_o, exp = O.rewrite(ok, ["--fixcsum"])
     te = TA.TcpEdit(["--fixcsum"])
     try:
-        rc, out = te.rewrite_pipelined(ok, chunk_bytes=1 << 20)
-        assert rc == rc_o == 0 and out == exp
-        bad = S.build_pcap(_overstate(recs, [15_000], by=40))  # chunk 1: same sizes back to its start
-        rc, _ = te.rewrite_pipelined(bad, chunk_bytes=1 << 20)
-        assert rc == TA.TCPEDIT_ERROR and "stale static packet buffer" in te.geterr()
+        for bad in ([3, 20_002], [9_600, 10_400], [15_000], [25_000]):
+            pcap = S.build_pcap(_overstate(recs, bad, by=40))
+            rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+            rc, out = te.rewrite_pipelined(pcap, chunk_bytes=1 << 20)
+            assert rc == rc_o == 0, (bad, te.geterr())
+            assert out == exp, bad
     finally:
         te.close()
+
+
+def test_batch_prefix_records_feed_the_replay(built):
+    """a batch that starts mid-capture (a shard) with the records before it staged as its
+    prefix equals the oracle's whole-capture output over its records; without the prefix the
+    record is refused loudly"""
+    recs = S.records(S.pcap_fixed(4_000, 90, ipv6=True, proto=17, seed=13))
+    recs[1_990] = S.records(S.pcap_fixed(1, 500, ipv6=True, proto=17, seed=14))[0]
+    recs = _overstate(recs, [2_005, 3_100], by=60)
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    cut = 24 + sum(16 + r[2] for r in recs[:2_000])
+    exp_tail = exp[24 + sum(16 + r[2] for r in S.records(exp)[:2_000]):]
+    for with_prefix in (True, False):
+        te = TA.TcpEdit(["--fixcsum"])
+        try:
+            b = TA.Batch(te, memoryview(pcap)[cut:], pkt_base=2_000, hdr=pcap[:24])
+            if with_prefix:
+                b.set_prefix(memoryview(pcap)[24:cut])
+            rc = b.run()
+            if with_prefix:
+                assert rc == 0, te.geterr()
+                r = b.result()
+                got = bytearray(r.out_len - 24)
+                assert b.output_records_into(got) == len(got)
+                assert r.stale_records >= 2 and r.unsupported == 0
+                assert bytes(got) == exp_tail
+            else:
+                assert rc == TA.TCPEDIT_ERROR and "stale static packet buffer" in te.geterr()
+            b.close()
+        finally:
+            te.close()
 
 
 def test_per_packet_api_reads_the_callers_buffer(built):
