@@ -1876,7 +1876,9 @@ static void idx_layout(IdxArgs *a, uint8_t *ws, uint64_t nwin)
     a->w_scr = w + 3 * nwin;
     a->w_pfx = w + 4 * nwin;
     a->w_sbase = w + 5 * nwin;
-    a->t_tile = (uint32_t *)(w + 6 * nwin);
+    a->w_prev = (int64_t *)(w + 6 * nwin);
+    a->parts = w + 7 * nwin;
+    a->t_tile = (uint32_t *)(w + 7 * nwin + IDX_PART_BYTES / 8 * (nwin / IDX_SB + 2));
     a->w_flags = a->t_tile + 2ull * IDX_MAXR * nwin;
     a->t_prel = (uint16_t *)(a->w_flags + nwin + 1);
 }
@@ -2151,7 +2153,11 @@ static int host_locked(const void *p)
     return a.type == hipMemoryTypeHost;
 }
 
-#define TE_PIPE_SLOTS 2
+/* device slots a pipelined run rotates through: chunk k is finished (results read, a
+   stale-buffer replay retried with the earlier chunks as prefix) while chunk k + 1 is
+   indexed and edited and chunk k + 2 uploads -- into a third slot, so chunk k's input and
+   index stand until it is finished */
+#define TE_PIPE_SLOTS 3
 #define TE_PIPE_CHUNK_DEFAULT ((size_t)16 << 20)
 
 /* res_pinned layout: counters | error words | wave-lane slots */
@@ -2308,7 +2314,13 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
         /* the stale bytes may come from earlier chunks: the replay walks back into their
            records (the host image holds them all; the staging keeps the newest) */
         tcpedit_batch_set_prefix(t, b, P->img + 24, P->first_off[s] - 24);
+        const uint64_t before = b->counters[TE_CNT_Q8_FAILED];
         const int r = retry_q8_with_prefix(t, b, -1, b->counters);
+        if (getenv("TCPEDIT_HIP_Q8_DEBUG"))
+            fprintf(stderr, "q8 retry: slot %d first_off %llu pkt_base %llu failed %llu -> %llu (listed %llu) npre %u "
+                    "file_start %d rc %d\n", s, (unsigned long long)P->first_off[s], (unsigned long long)b->pkt_base,
+                    (unsigned long long)before, (unsigned long long)b->counters[TE_CNT_Q8_FAILED],
+                    (unsigned long long)b->counters[TE_CNT_UNSUPPORTED], b->npre, b->pre_file_start, r);
         tcpedit_batch_set_prefix(t, b, NULL, 0);
         if (r < 0)
             return -1;
@@ -2416,12 +2428,12 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
                         uint8_t *d_dirbits, uint64_t dirbits_len, uint64_t *pos_io, int trace)
 {
     const size_t C = P->chunk;
-    uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0, 0};
-    int inflight[TE_PIPE_SLOTS] = {0, 0}, stopped = 0, k = 0, fallbacks = 0;
+    uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0};
+    int inflight[TE_PIPE_SLOTS] = {0}, stopped = 0, k = 0, fallbacks = 0;
     uint64_t entry_file = 24;  /* host copy of where chunk k's records start (file offset) */
     uint64_t prev_first = ~0ull;
     P->img = img;
-    uint64_t limit_img[TE_PIPE_SLOTS] = {0, 0}, file0[TE_PIPE_SLOTS] = {0, 0};
+    uint64_t limit_img[TE_PIPE_SLOTS] = {0}, file0[TE_PIPE_SLOTS] = {0};
     IdxArgs A[TE_PIPE_SLOTS];
     const double t0 = te_now();
     double t_wait = 0;
@@ -2629,8 +2641,8 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     uint8_t *dst = out;
     uint8_t *d_dirbits = NULL;
     uint64_t dirbits_len = 0;
-    int reg_in = 0, reg_out = 0, rc = TCPEDIT_ERROR, inflight[TE_PIPE_SLOTS] = {0, 0};
-    uint64_t pos = 24, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0, 0};
+    int reg_in = 0, reg_out = 0, rc = TCPEDIT_ERROR, inflight[TE_PIPE_SLOTS] = {0};
+    uint64_t pos = 24, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0};
     int stopped = 0; /* a hard error or libpcap's stop ended the walk */
     if (out_len)
         *out_len = 0;

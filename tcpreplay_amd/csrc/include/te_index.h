@@ -40,8 +40,10 @@
 /* the index's device workspace for nwin windows: per window its facts (entry, exit, flags,
    records|tiles, scratch bytes) and prefixes (records|tiles, scratch), the totals, and the
    count pass's cut (record offsets in their tiles, tile starts) for the write pass */
-#define IDX_WS_BYTES(nwin) (8ull * 6 * (nwin) + 4ull * ((nwin) + 1) + 8ull * (IDX_T__N + 2) + \
-                            (2ull + 8ull) * IDX_MAXR * (nwin) + 64)
+#define IDX_SB 1024        /* windows a block of the scan's first level takes */
+#define IDX_PART_BYTES 80  /* such a block's record */
+#define IDX_WS_BYTES(nwin) (8ull * 7 * (nwin) + 4ull * ((nwin) + 1) + 8ull * (IDX_T__N + 2) + \
+                            IDX_PART_BYTES * ((nwin) / IDX_SB + 2) + (2ull + 8ull) * IDX_MAXR * (nwin) + 64)
 
 #ifdef __cplusplus
 extern "C" {
@@ -60,6 +62,8 @@ typedef struct {
     uint32_t budget, max_pkts, growth; /* the wave-lane tile cut (walk_range) */
     /* per window (IDX_WS_BYTES) */
     uint64_t *w_entry, *w_exit, *w_agg, *w_scr, *w_pfx, *w_sbase;
+    int64_t *w_prev;    /* the nearest earlier window with a record, within its scan block */
+    void *parts;        /* the part blocks' totals, then their prefixes (IDX_PART_BYTES each) */
     uint32_t *w_flags;
     uint16_t *t_prel;   /* IDX_MAXR a window: each record's offset in its tile */
     uint32_t *t_tile;   /* IDX_MAXR pairs a window: {first offset from the window, first | npkt << 16} */

@@ -1981,6 +1981,12 @@ __device__ int64_t q8_chain(const Q8Args &q, int64_t pos, uint32_t need) {
 }
 
 enum { Q8_OK = 0, Q8_FAIL = 1, Q8_DEEPER = 2 };
+#if TE_Q8_DEBUG  // (diagnostics builds) why a replay gave up
+#define Q8_DBG(r) printf("q8 fail %d: record %u start %lld npre %u file_start %u\n", (r), i, (long long)start, \
+                         q.npre, q.npre ? q.pre_file_start : q.file_start)
+#else
+#define Q8_DBG(r)
+#endif
 
 // replay records j0..i over the emulated buffer (j0 < 0: from the batch start, whose
 // buffer is zeros or the caller's); Q8_DEEPER: record *jd read bytes past what the
@@ -1996,7 +2002,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
     if (start == Q8_START) {
         // the bytes come from before every record there is: the capture's start (zeros),
         // else they are not here
-        if (!(q.npre ? q.pre_file_start : q.file_start)) return Q8_FAIL;
+        if (!(q.npre ? q.pre_file_start : q.file_start)) { Q8_DBG(1); return Q8_FAIL; }
         j0 = -(int64_t)q.npre;
         if (q.init_buf) {
             for (uint32_t x = 0; x < q.init_len; ++x) buf[x] = q.init_buf[x];
@@ -2010,11 +2016,11 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         const uint8_t *rec = q8_recp(q, j);
         const uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp) / (a.in_nsec ? 1000u : 1u);
         const uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
-        if (caplen > MAX_SNAPLEN) return Q8_FAIL;
+        if (caplen > MAX_SNAPLEN) { Q8_DBG(2); return Q8_FAIL; }
         for (uint32_t x = 0; x < caplen; ++x) buf[x] = rec[16 + x];  // tcprewrite.c:301
         if (caplen > V) V = caplen;
         if (j < 0 && (a.l2carry || (FZ && a.fuzz_mode == TE_FUZZ_APPLY)))
-            return Q8_FAIL;  // (a staged record's carried state is not at hand)
+            { Q8_DBG(3); return Q8_FAIL; }  // (a staged record's carried state is not at hand)
         const uint64_t pktno = a.pkt_base + (uint64_t)j;
         int dir = TE_DIR_C2S;
         const bool explicit_dir = a.fixed_dir >= 0;
@@ -2047,17 +2053,17 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
         const int rc = tcpedit_packet<FZ, true>(pk, cfg, a.portlut, dir, warned, a.fuzz_mode, fzs);
         if (pk.unsupported) {  // bytes nobody wrote yet in this replay (or slot headroom)
-            if (pk.need == NEED_NEVER || pk.need > MAXPACKET) return Q8_FAIL;
+            if (pk.need == NEED_NEVER || pk.need > MAXPACKET) { Q8_DBG(4); return Q8_FAIL; }
             *jd = j;
             *needd = pk.need;
             return Q8_DEEPER;
         }
         if (j == (int64_t)i) {
-            if (rc == RC_ERROR || rc == RC_SOFT) return Q8_FAIL;  // cannot change the pass-1 layout
+            if (rc == RC_ERROR || rc == RC_SOFT) { Q8_DBG(5); return Q8_FAIL; }  // cannot change the pass-1 layout
             g_u8 *o = (g_u8 *)a.out + out_off;
             const uint32_t oc = (uint32_t)o[8] | ((uint32_t)o[9] << 8) | ((uint32_t)o[10] << 16) |
                                 ((uint32_t)o[11] << 24);
-            if (oc != pk.caplen) return Q8_FAIL;
+            if (oc != pk.caplen) { Q8_DBG(6); return Q8_FAIL; }
             for (uint32_t x = 0; x < pk.caplen; ++x) o[16 + x] = pk.d[x];
             g_u8 *st = (g_u8 *)a.status + i;
             const uint8_t old = *st;
@@ -2079,7 +2085,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
             for (uint32_t x = 0; x < M; ++x) buf[x] = pk.d[x];
         if (M > V) V = M;
     }
-    return Q8_FAIL;
+    { Q8_DBG(7); return Q8_FAIL; }
 }
 
 template <bool FZ>
@@ -2579,7 +2585,11 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         // --fuzz-seed: reach pass, per-record RNG states, then the edit pass below
         if (!L->fuzz_blk || !L->fuzz_words || L->n_pkts == 0) return -1;
         a.fuzz_mode = TE_FUZZ_PROBE;
-        if (L->slot_layout)
+        if (L->any_dec && L->slot_layout)
+            hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else if (L->any_dec)
+            hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        else if (L->slot_layout)
             hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
         else
             hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
@@ -2601,7 +2611,11 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     if (!fast && l2carry_prepare(L, a, stream) != 0) return -1;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
-    if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
+    if (a.fuzz_mode != TE_FUZZ_OFF && L->any_dec && L->slot_layout)  // --fuzz-seed behind another decoder
+        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.fuzz_mode != TE_FUZZ_OFF && L->any_dec)
+        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+    else if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
         hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.fuzz_mode != TE_FUZZ_OFF)
         hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);

@@ -132,17 +132,19 @@ __device__ __forceinline__ int strength(const IdxArgs &a, const u32 *img, u64 A0
 // stages [ws - O, we + 16): the O = OL S bytes before the window are the first OL lanes'
 // sub-windows, whose only job is to establish the chain entering ws (a guess there that is
 // not a record start is corrected as the chain runs on, or leaves the window before ws).
+// what the scan needs of a window
+struct Facts {
+    u64 went, wexit;  // where the chain enters and leaves it (IDX_NONE: no record starts here)
+    u64 scr;          // scratch bytes of its huge records
+    u32 nrec, ntile, flags;
+};
 template <int S, int OL>
-__global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
+__device__ __forceinline__ Facts count_window(const IdxArgs &a, WinLds<S> &M, u32 k) {
     constexpr int W = IW * S;       // staged sub-window bytes
     constexpr int O = OL * S;       // overlap before the window
     constexpr int WN = W - O;       // bytes a window owns
     static_assert(S % 16 == 0 && S <= 128, "sub-window: whole 16-byte chunks, <= two 64-bit masks");
-    __shared__ WinLds<S> L[IWAVES];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    WinLds<S> &M = L[wv];
-    const u32 k = blockIdx.x * IWAVES + (u32)wv;  // windows are independent here: no order
-    if (k >= a.nwin) return;
+    const int lane = threadIdx.x & 63;
 
     // the first record: known to the host (a.entry), or where the previous pipeline chunk's
     // chain ended (read on the device: that chunk's index ran before this one on the stream)
@@ -400,132 +402,263 @@ __global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
     for (int o = 32; o > 0; o >>= 1) scr += __shfl_xor(scr, o, 64);
     for (u32 i = lane; i < nrec; i += IW)
         if (i < (u32)IDX_MAXR) a.t_prel[(u64)k * IDX_MAXR + i] = (u16)(M.rel[i] - M.rel[M.tsi[i]]);
+    return Facts{went, wexit, scr, nrec, ntile, wstop | (anyzero ? IDX_ZERO : 0u)};
+}
+
+// ---- the scan, in two levels: te_index_part (a block of SB windows, one a thread) leaves
+// each window's in-block exclusive prefixes of (records | tiles) and scratch bytes and the
+// nearest earlier window with a record in the block, checks the chain inside the block (a
+// window's first record must be where the chain left the nearest earlier window a record
+// starts in; a window without one must be passed over whole) and writes the block's totals
+// (a Part); te_index_scan (one block) scans the Parts, settles the checks whose earlier
+// record window lies in an earlier block, finds libpcap's first stop and writes the totals.
+constexpr int SB = IDX_SB;
+constexpr long long NO_STOP = 0x7fffffffffffffffll;
+struct Part {           // a block's totals, then (te_index_scan) their exclusive prefixes
+    u64 agg, scr;
+    long long lastrec;  // the last window at or after kE with a record (-1: none) ...
+    u64 lastexit;       // ... where the chain leaves it
+    u32 lastflags, pad;
+    long long stop;     // the first window where the chain stops (NO_STOP: none)
+    long long bad;      // the first window whose check failed (NO_STOP: none)
+    long long zero;     // the first window with a zero-length record (NO_STOP: none)
+    long long firstrec; // the first window after kE with a record (NO_STOP: none) ...
+    u64 firstentry;     // ... where the chain enters it
+};
+static_assert(sizeof(Part) == IDX_PART_BYTES, "te_index.h sizes the scan blocks' records");
+constexpr Part NO_PART{0, 0, -1, IDX_NONE, 0, 0, NO_STOP, NO_STOP, NO_STOP, NO_STOP, IDX_NONE};
+constexpr u32 STOPS = IDX_STOP | IDX_ERROR | IDX_END;
+constexpr u64 WNB = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;  // bytes a window owns
+__device__ __forceinline__ u32 idx_kE(const IdxArgs &a, u64 &entry) {
+    entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
+    return (u32)((entry - a.base) / WNB);
+}
+// window q's check against window j, the nearest earlier one a record starts in (>= kE),
+// whose exit and flags are xj, fj
+__device__ __forceinline__ bool chain_bad(const IdxArgs &a, u32 q, u64 eq, u64 xj, u32 fj) {
+    if (eq != IDX_NONE) return xj != eq;
+    const u64 qe = a.base + (u64)(q + 1) * WNB;
+    return xj < (qe < a.len ? qe : a.len) && !(fj & STOPS);
+}
+// combine: a before b (thread order): sums, the later record window, the earliest of the rest
+__device__ __forceinline__ void fold(Part &a, const Part &b) {
+    a.agg += b.agg;
+    a.scr += b.scr;
+    if (b.lastrec > a.lastrec) {
+        a.lastrec = b.lastrec;
+        a.lastexit = b.lastexit;
+        a.lastflags = b.lastflags;
+    }
+    a.stop = b.stop < a.stop ? b.stop : a.stop;
+    a.bad = b.bad < a.bad ? b.bad : a.bad;
+    a.zero = b.zero < a.zero ? b.zero : a.zero;
+    if (b.firstrec < a.firstrec) {
+        a.firstrec = b.firstrec;
+        a.firstentry = b.firstentry;
+    }
+}
+__device__ __forceinline__ Part shfl_part(const Part &x, int src) {
+    Part y;
+    y.agg = __shfl(x.agg, src, 64);
+    y.scr = __shfl(x.scr, src, 64);
+    y.lastrec = __shfl(x.lastrec, src, 64);
+    y.lastexit = __shfl(x.lastexit, src, 64);
+    y.lastflags = (u32)__shfl((int)x.lastflags, src, 64);
+    y.pad = 0;
+    y.stop = __shfl(x.stop, src, 64);
+    y.bad = __shfl(x.bad, src, 64);
+    y.zero = __shfl(x.zero, src, 64);
+    y.firstrec = __shfl(x.firstrec, src, 64);
+    y.firstentry = __shfl(x.firstentry, src, 64);
+    return y;
+}
+// over the block's SB threads in thread order: the exclusive fold before each thread and
+// the block's total
+__device__ __forceinline__ void part_scan(const Part &B, Part *wsum, Part &ex, Part &tot) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    Part inc = B;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const Part y = shfl_part(inc, lane >= o ? lane - o : lane);
+        if (lane >= o) {
+            Part t = y;
+            fold(t, inc);
+            inc = t;
+        }
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    Part W = NO_PART, T = NO_PART;
+#pragma unroll
+    for (int w = 0; w < SB / 64; ++w) {
+        const Part x = wsum[w];
+        if (w < wid) fold(W, x);
+        fold(T, x);
+    }
+    __syncthreads();
+    Part e = shfl_part(inc, lane ? lane - 1 : 0);
+    if (lane == 0) e = NO_PART;
+    fold(W, e);
+    ex = W;
+    tot = T;
+}
+
+template <int S, int OL>
+__global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
+    __shared__ WinLds<S> L[IWAVES];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u32 k = blockIdx.x * IWAVES + (u32)wv;  // windows are independent here: no order
+    if (k >= a.nwin) return;
+    const Facts f = count_window<S, OL>(a, L[wv], k);
     if (lane == 0) {
-        a.w_entry[k] = went;
-        a.w_exit[k] = wexit;
-        a.w_flags[k] = wstop | (anyzero ? IDX_ZERO : 0u);
-        a.w_agg[k] = (u64)nrec | ((u64)ntile << REC_BITS);
-        a.w_scr[k] = scr;
+        a.w_entry[k] = f.went;
+        a.w_exit[k] = f.wexit;
+        a.w_flags[k] = f.flags;
+        a.w_agg[k] = (u64)f.nrec | ((u64)f.ntile << REC_BITS);
+        a.w_scr[k] = f.scr;
     }
 }
 
-// ---- the scan: one block over every window's facts ----
-// exclusive prefixes of (records | tiles) and of scratch bytes; the chain checked across
-// windows (a window's first record must be where the chain left the nearest earlier window
-// a record starts in; a window without one must be passed over whole); libpcap's first
-// stop; the totals.  Each thread takes a contiguous run of windows.
-constexpr int SB = 1024;
-template <typename T, typename Op>
-__device__ __forceinline__ T block_scan_ex(T v, T ident, Op op, T *sh, T &total) {
-    // exclusive scan over the block's threads in thread order (Hillis-Steele in LDS)
-    const int tid = threadIdx.x;
-    sh[tid] = v;
-    __syncthreads();
-    for (int o = 1; o < SB; o <<= 1) {
-        const T y = tid >= o ? sh[tid - o] : ident;
-        __syncthreads();
-        sh[tid] = op(sh[tid], y);
-        __syncthreads();
+__global__ __launch_bounds__(SB) void te_index_part(IdxArgs a) {
+    __shared__ Part wsum[SB / 64];
+    u64 entry;
+    const u32 kE = idx_kE(a, entry);
+    const u32 q = blockIdx.x * SB + threadIdx.x;
+    const bool in = q < a.nwin;
+    const u64 eq = in ? a.w_entry[q] : IDX_NONE;
+    const u32 fl = in ? a.w_flags[q] : 0u;
+    const bool rec = in && q >= kE && eq != IDX_NONE;
+    Part B = NO_PART;
+    if (in) {
+        B.agg = a.w_agg[q];
+        B.scr = a.w_scr[q];
+        B.stop = eq != IDX_NONE && (fl & STOPS) ? (long long)q : NO_STOP;
+        B.zero = fl & IDX_ZERO ? (long long)q : NO_STOP;
     }
-    total = sh[SB - 1];
-    const T ex = tid ? sh[tid - 1] : ident;
+    if (rec) {
+        B.lastrec = q;
+        B.lastexit = a.w_exit[q];
+        B.lastflags = fl;
+        if (q > kE) {
+            B.firstrec = q;
+            B.firstentry = eq;
+        }
+    }
+    Part ex, tot;
+    part_scan(B, wsum, ex, tot);
+    // the chain inside the block (a window whose earlier record window is in an earlier block
+    // is settled by te_index_scan)
+    bool bad = false;
+    if (in && q == kE) bad = eq != entry;
+    else if (in && q > kE && ex.lastrec >= 0) bad = chain_bad(a, q, eq, ex.lastexit, ex.lastflags);
+    long long rb = bad ? (long long)q : NO_STOP;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long z = __shfl_xor(rb, o, 64);
+        rb = z < rb ? z : rb;
+    }
+    __shared__ unsigned long long bmin;
+    if (threadIdx.x == 0) bmin = NO_STOP;
     __syncthreads();
-    return ex;
+    if ((threadIdx.x & 63) == 0 && rb != NO_STOP) atomicMin(&bmin, (unsigned long long)rb);
+    if (in) {
+        a.w_pfx[q] = ex.agg;
+        a.w_sbase[q] = ex.scr;
+        a.w_prev[q] = ex.lastrec;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        tot.bad = (long long)bmin;
+        ((Part *)a.parts)[blockIdx.x] = tot;
+    }
 }
 
 __global__ __launch_bounds__(SB) void te_index_scan(IdxArgs a) {
-    __shared__ u64 sh64[SB];
-    __shared__ long long shi[SB];
-    const int tid = threadIdx.x;
-    const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
-    constexpr u64 WN = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;
-    const u32 kE = (u32)((entry - a.base) / WN);
-    const u32 nw = a.nwin, per = (nw + SB - 1) / SB;
-    const u32 k0 = tid * per < nw ? tid * per : nw, k1 = k0 + per < nw ? k0 + per : nw;
-    // the first stop (windows past it are not the chain's)
-    long long fs = 0x7fffffffffffffffll, lastrec = -1;
-    u64 agg = 0, scr = 0;
-    for (u32 q = k0; q < k1; ++q) {
-        if (fs == 0x7fffffffffffffffll && (a.w_flags[q] & (IDX_STOP | IDX_ERROR | IDX_END)) &&
-            a.w_entry[q] != IDX_NONE)
-            fs = q;
-        agg += a.w_agg[q];
-        scr += a.w_scr[q];
-        if (q >= kE && a.w_entry[q] != IDX_NONE) lastrec = q;
-    }
-    long long stop_tot;
-    {
-        long long t = 0;
-        (void)block_scan_ex<long long>(fs, 0x7fffffffffffffffll, [](long long x, long long y) { return x < y ? x : y; },
-                                       shi, t);
-        stop_tot = t;
-    }
-    const u32 last = stop_tot != 0x7fffffffffffffffll ? (u32)stop_tot : nw - 1;
-    u64 tot_agg, tot_scr;
-    u64 ex_agg = block_scan_ex<u64>(agg, 0ull, [](u64 x, u64 y) { return x + y; }, sh64, tot_agg);
-    u64 ex_scr = block_scan_ex<u64>(scr, 0ull, [](u64 x, u64 y) { return x + y; }, sh64, tot_scr);
-    long long lr_all;
-    long long prev_rec = block_scan_ex<long long>(lastrec, -1ll, [](long long x, long long y) { return x > y ? x : y; },
-                                                  shi, lr_all);
-    // per window: its bases, the chain check, and where the chain ends
-    long long first_bad = 0x7fffffffffffffffll;
-    bool zero = false;
-    for (u32 q = k0; q < k1; ++q) {
-        const u64 eq = a.w_entry[q];
-        a.w_pfx[q] = ex_agg;
-        a.w_sbase[q] = ex_scr;
-        ex_agg += a.w_agg[q];
-        ex_scr += a.w_scr[q];
-        if (q > last) continue;
-        zero |= (a.w_flags[q] & IDX_ZERO) != 0;
-        bool bad = false;
-        if (q == kE) {
-            bad = eq != entry;
-        } else if (q > kE) {
-            const long long j = prev_rec >= (long long)kE ? prev_rec : (long long)kE;
-            const u64 xj = a.w_exit[j];
-            if (eq != IDX_NONE) {
-                bad = xj != eq;
-            } else {
-                const u64 qe = a.base + (u64)(q + 1) * WN;
-                bad = xj < (qe < a.len ? qe : a.len) && !(a.w_flags[j] & (IDX_STOP | IDX_ERROR | IDX_END));
+    __shared__ Part wsum[SB / 64];
+    u64 entry;
+    const u32 kE = idx_kE(a, entry);
+    const u32 G = (a.nwin + SB - 1) / SB;
+    Part *parts = (Part *)a.parts;
+    Part C = NO_PART;  // the rounds before
+    for (u32 g0 = 0; g0 < G; g0 += SB) {  // (one round up to SB^2 windows)
+        const u32 g = g0 + threadIdx.x;
+        const bool gin = g < G;
+        Part B = gin ? parts[g] : NO_PART;
+        Part ex, tot;
+        part_scan(B, wsum, ex, tot);
+        Part pre = C;
+        fold(pre, ex);  // everything before block g
+        if (gin && pre.lastrec >= (long long)kE) {
+            // block g's windows up to its first record window (after kE): their nearest
+            // earlier record window is the last of the blocks before.  The record window's
+            // first record must be where the chain left that one; the windows before it must
+            // be passed over (the first one the chain does not pass is the miss)
+            const u64 xj = pre.lastexit;
+            const u32 fj = pre.lastflags;
+            const u32 blk_end = (g + 1) * SB < a.nwin ? (g + 1) * SB : a.nwin;  // (exclusive)
+            const u32 lo = g * SB > kE + 1 ? g * SB : kE + 1;
+            const u32 hi = B.firstrec != NO_STOP ? (u32)B.firstrec : blk_end;  // empty windows [lo, hi)
+            long long miss = NO_STOP;
+            if (lo < hi && !(fj & STOPS) && xj < a.len) {
+                // the first empty window whose end (or the capture's) lies past the chain's exit
+                const u64 w = xj >= a.base ? (xj - a.base) / WNB : 0;
+                const u64 wq = w > lo ? w : lo;
+                if (wq < hi && (xj < a.base + (wq + 1) * WNB)) miss = (long long)wq;
             }
+            if (miss == NO_STOP && B.firstrec != NO_STOP && xj != B.firstentry) miss = B.firstrec;
+            B.bad = miss < B.bad ? miss : B.bad;
         }
-        if (bad && first_bad == 0x7fffffffffffffffll) first_bad = q;
-        if (q >= kE && eq != IDX_NONE) prev_rec = q;
+        if (gin) {
+            parts[g] = pre;
+            (void)0;
+        }
+        // the round's totals, the deferred misses folded in
+        long long rb = gin ? B.bad : NO_STOP;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long z = __shfl_xor(rb, o, 64);
+            rb = z < rb ? z : rb;
+        }
+        __shared__ unsigned long long bmin;
+        if (threadIdx.x == 0) bmin = NO_STOP;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && rb != NO_STOP) atomicMin(&bmin, (unsigned long long)rb);
+        __syncthreads();
+        fold(C, tot);
+        C.bad = (long long)bmin < C.bad ? (long long)bmin : C.bad;
+        __syncthreads();
     }
-    long long fb;
-    {
-        long long t = 0;
-        (void)block_scan_ex<long long>(first_bad, 0x7fffffffffffffffll,
-                                       [](long long x, long long y) { return x < y ? x : y; }, shi, t);
-        fb = t;
+    if (threadIdx.x) return;
+    const bool stopped = C.stop != NO_STOP;
+    const u32 last = stopped ? (u32)C.stop : a.nwin - 1;  // windows past the chain's end do not count
+    u64 tot, scr, end;
+    u32 fl_last = 0;
+    if (!stopped) {  // (no window loads: the whole capture's totals)
+        tot = C.agg;
+        scr = C.scr;
+        end = C.lastrec >= (long long)kE ? C.lastexit : IDX_NONE;
+    } else {
+        const Part &L = parts[last / SB];
+        tot = L.agg + a.w_pfx[last] + a.w_agg[last];  // inclusive (records | tiles) through `last`
+        scr = L.scr + a.w_sbase[last] + a.w_scr[last];
+        // the chain's last window with a record, at or before `last` (the stopping one)
+        end = a.w_exit[last];
+        fl_last = a.w_flags[last];
     }
-    long long zr;
-    (void)block_scan_ex<long long>(zero ? 1ll : 0ll, 0ll, [](long long x, long long y) { return x | y; }, shi, zr);
-    if (tid == 0) {
-        // the chain's last window with a record, at or before `last`
-        long long j = last;
-        while (j > (long long)kE && a.w_entry[j] == IDX_NONE) --j;
-        const u64 tot = a.w_pfx[last] + a.w_agg[last];  // inclusive (records | tiles) through `last`
-        const u32 fl = a.w_flags[last];
-        const bool stopped = stop_tot != 0x7fffffffffffffffll;
-        const bool bad = fb != 0x7fffffffffffffffll && fb <= (long long)last;
-        a.totals[IDX_T_RECS] = tot & REC_MASK;
-        a.totals[IDX_T_TILES] = tot >> REC_BITS;
-        a.totals[IDX_T_SCRATCH] = a.w_sbase[last] + a.w_scr[last];
-        a.totals[IDX_T_BAD] = bad ? 1 : 0;
-        a.totals[IDX_T_WINDOWS] = last + 1;
-        a.totals[IDX_T_STOP] = stopped ? (fl & (IDX_STOP | IDX_ERROR | IDX_END)) : 0;
-        const u64 end = a.w_exit[j];
-        a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
-        a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
-        a.totals[IDX_T_ZERO] = zr ? 1 : 0;
-        // the record the chain stopped at: the one after the stopping window's last
-        a.totals[IDX_T_ERR_REC] = stopped && (fl & IDX_ERROR) ? tot & REC_MASK : ~0ull;
-        a.totals[IDX_T_OVERFLOW] = (tot & REC_MASK) > a.rec_cap || (tot >> REC_BITS) > a.tile_cap ? 1 : 0;
-        a.totals[IDX_T_BADWIN] = bad ? (u64)fb : 0xffffffffull;
-    }
+    const bool isbad = C.bad != NO_STOP && C.bad <= (long long)last;
+    a.totals[IDX_T_RECS] = tot & REC_MASK;
+    a.totals[IDX_T_TILES] = tot >> REC_BITS;
+    a.totals[IDX_T_SCRATCH] = scr;
+    a.totals[IDX_T_BAD] = isbad ? 1 : 0;
+    a.totals[IDX_T_WINDOWS] = last + 1;
+    a.totals[IDX_T_STOP] = stopped ? (fl_last & STOPS) : 0;
+    a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
+    a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
+    a.totals[IDX_T_ZERO] = C.zero != NO_STOP && C.zero <= (long long)last ? 1 : 0;
+    // the record the chain stopped at: the one after the stopping window's last
+    a.totals[IDX_T_ERR_REC] = stopped && (fl_last & IDX_ERROR) ? tot & REC_MASK : ~0ull;
+    a.totals[IDX_T_OVERFLOW] = (tot & REC_MASK) > a.rec_cap || (tot >> REC_BITS) > a.tile_cap ? 1 : 0;
+    a.totals[IDX_T_BADWIN] = isbad ? (u64)C.bad : 0xffffffffull;
 }
 
 // ---- the write pass: a wave per window puts its tiles and record offsets at its bases ----
@@ -533,16 +666,20 @@ __global__ __launch_bounds__(IB) void te_index_write(IdxArgs a) {
     const int lane = threadIdx.x & 63;
     const u32 k = blockIdx.x * IWAVES + (threadIdx.x >> 6);
     if (k >= a.nwin) return;
+    // (every load this wave needs before the copies, issued together)
     const u64 *T = a.totals;
-    if (T[IDX_T_BAD] || T[IDX_T_OVERFLOW] || k >= T[IDX_T_WINDOWS]) return;  // (the host index stays)
+    const u64 nwin_chain = T[IDX_T_WINDOWS], skip = T[IDX_T_BAD] | T[IDX_T_OVERFLOW];
+    const Part G = ((const Part *)a.parts)[k / SB];
+    const u64 agg = a.w_agg[k], lpfx = a.w_pfx[k], wexit = a.w_exit[k], lsb = a.w_sbase[k];
+    if (k >= nwin_chain || skip) return;  // past the chain's end, or the host index stays
     constexpr u64 WN = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;
     const u64 ws = a.base + (u64)k * WN;
-    const u64 agg = a.w_agg[k], pfx = a.w_pfx[k];
+    const u64 pfx = G.agg + lpfx;
     const u32 nrec = (u32)(agg & REC_MASK), ntile = (u32)(agg >> REC_BITS);
     if (!nrec) return;
     const u64 pbase = pfx & REC_MASK, tbase = pfx >> REC_BITS;
-    const u32 rend = (u32)(a.w_exit[k] - ws);  // the window's last record's end
-    u64 sb = a.w_sbase[k];
+    const u32 rend = (u32)(wexit - ws);  // the window's last record's end
+    u64 sb = G.scr + lsb;
     for (u32 t0 = 0; t0 < ntile; t0 += IW) {
         const u32 t = t0 + lane;
         const bool v = t < ntile;
@@ -579,14 +716,15 @@ __global__ __launch_bounds__(IB) void te_index_write(IdxArgs a) {
 
 extern "C" uint32_t te_index_window_bytes(void) { return IW * TE_IDX_S - TE_IDX_OL * TE_IDX_S; }
 
-// count (a wave per window), scan (one block), write (a wave per window): no workspace
-// needs zeroing and no window waits on another
+// count (a wave per window), part (a block per SB windows), scan (one block over the part
+// blocks), write (a wave per window): no window waits on another
 extern "C" int te_launch_index(const IdxArgs *args, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const IdxArgs a = *args;
     if (a.nwin == 0) return 0;
     const u32 blocks = (a.nwin + IWAVES - 1) / IWAVES;
     hipLaunchKernelGGL((te_index_count<TE_IDX_S, TE_IDX_OL>), dim3(blocks), dim3(IB), 0, st, a);
+    hipLaunchKernelGGL(te_index_part, dim3((a.nwin + SB - 1) / SB), dim3(SB), 0, st, a);
     hipLaunchKernelGGL(te_index_scan, dim3(1), dim3(SB), 0, st, a);
     hipLaunchKernelGGL(te_index_write, dim3(blocks), dim3(IB), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
