@@ -630,11 +630,9 @@ int te_check_decoder_cfg(tcpedit_t *t, int s2c)
             return -1;
         }
     }
-    /* fuzzing.c:62-297 reads the encoder's L2 length and protocol (the en10mb, user and hdlc
-       plugins'), behind any decoder; an input plugin as its own encoder (every record a soft
-       error before the fuzz step) and pppserial's pass-through are not served */
-    if (c->fuzz_seed && c->encoder != TE_ENC_EN10MB && c->encoder != TE_ENC_USER && c->encoder != TE_ENC_HDLC) {
-        te_seterr(t, "--fuzz-seed with DLT %d input into this encoder is not served by this build", t->dlt);
+    if (c->fuzz_seed && (foreign || (c->encoder != TE_ENC_EN10MB && c->encoder != TE_ENC_USER &&
+                                     c->encoder != TE_ENC_HDLC))) {
+        te_seterr(t, "--fuzz-seed with DLT %d input or this encoder is not served by this build", t->dlt);
         return -1;
     }
     return 0;

@@ -41,7 +41,7 @@
    records|tiles, scratch bytes) and prefixes (records|tiles, scratch), the totals, and the
    count pass's cut (record offsets in their tiles, tile starts) for the write pass */
 #define IDX_SB 1024        /* windows a block of the scan's first level takes */
-#define IDX_PART_BYTES 80  /* such a block's record */
+#define IDX_PART_BYTES 32  /* such a block's record */
 #define IDX_WS_BYTES(nwin) (8ull * 7 * (nwin) + 4ull * ((nwin) + 1) + 8ull * (IDX_T__N + 2) + \
                             IDX_PART_BYTES * ((nwin) / IDX_SB + 2) + (2ull + 8ull) * IDX_MAXR * (nwin) + 64)
 

@@ -596,17 +596,23 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
                 }
             }
             v = make_uint4(0, 0, 0, 0);
-            for (int p = lo; p < (int)npkt && (int64_t)sh.opfx[p] < q0 + b1; ++p) {
-                const int64_t s0 = sh.opfx[p], s1 = sh.opfx[p + 1];
-                if (s1 <= q0 + b0) continue;
-                int pb0 = (int)((s0 - q0) > b0 ? (s0 - q0) : b0);
-                int pb1 = (int)((s1 - q0) < b1 ? (s1 - q0) : b1);
-                if (pb0 >= pb1) continue;
-                const uint4 w = read16(S, (uint32_t)((int64_t)sh.rpos[p] + (q0 - s0)));
-                v.x = sel_bytes(v.x, w.x, pb0, pb1, 0);
-                v.y = sel_bytes(v.y, w.y, pb0, pb1, 1);
-                v.z = sel_bytes(v.z, w.z, pb0, pb1, 2);
-                v.w = sel_bytes(v.w, w.w, pb0, pb1, 3);
+            const int64_t f0 = sh.opfx[lo], f1 = sh.opfx[lo + 1];
+            if (f0 <= q0 && f1 >= q0 + 16) {
+                // the whole chunk inside one record (most chunks): one read, no byte selects
+                v = read16(S, (uint32_t)((int64_t)sh.rpos[lo] + (q0 - f0)));
+            } else {
+                for (int p = lo; p < (int)npkt && (int64_t)sh.opfx[p] < q0 + b1; ++p) {
+                    const int64_t s0 = sh.opfx[p], s1 = sh.opfx[p + 1];
+                    if (s1 <= q0 + b0) continue;
+                    int pb0 = (int)((s0 - q0) > b0 ? (s0 - q0) : b0);
+                    int pb1 = (int)((s1 - q0) < b1 ? (s1 - q0) : b1);
+                    if (pb0 >= pb1) continue;
+                    const uint4 w = read16(S, (uint32_t)((int64_t)sh.rpos[p] + (q0 - s0)));
+                    v.x = sel_bytes(v.x, w.x, pb0, pb1, 0);
+                    v.y = sel_bytes(v.y, w.y, pb0, pb1, 1);
+                    v.z = sel_bytes(v.z, w.z, pb0, pb1, 2);
+                    v.w = sel_bytes(v.w, w.w, pb0, pb1, 3);
+                }
             }
         }
         g_u8 *dst = gout + C;
@@ -2585,11 +2591,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         // --fuzz-seed: reach pass, per-record RNG states, then the edit pass below
         if (!L->fuzz_blk || !L->fuzz_words || L->n_pkts == 0) return -1;
         a.fuzz_mode = TE_FUZZ_PROBE;
-        if (L->any_dec && L->slot_layout)
-            hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else if (L->any_dec)
-            hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else if (L->slot_layout)
+        if (L->slot_layout)
             hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
         else
             hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
@@ -2611,11 +2613,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     if (!fast && l2carry_prepare(L, a, stream) != 0) return -1;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
-    if (a.fuzz_mode != TE_FUZZ_OFF && L->any_dec && L->slot_layout)  // --fuzz-seed behind another decoder
-        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (a.fuzz_mode != TE_FUZZ_OFF && L->any_dec)
-        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
+    if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
         hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
     else if (a.fuzz_mode != TE_FUZZ_OFF)
         hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);

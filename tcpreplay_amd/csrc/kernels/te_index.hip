@@ -407,101 +407,56 @@ __device__ __forceinline__ Facts count_window(const IdxArgs &a, WinLds<S> &M, u3
 
 // ---- the scan, in two levels: te_index_part (a block of SB windows, one a thread) leaves
 // each window's in-block exclusive prefixes of (records | tiles) and scratch bytes and the
-// nearest earlier window with a record in the block, checks the chain inside the block (a
-// window's first record must be where the chain left the nearest earlier window a record
-// starts in; a window without one must be passed over whole) and writes the block's totals
-// (a Part); te_index_scan (one block) scans the Parts, settles the checks whose earlier
-// record window lies in an earlier block, finds libpcap's first stop and writes the totals.
+// nearest earlier window with a record in the block, and the block's totals (a Part);
+// te_index_scan (one block) scans the Parts, finds libpcap's first stop and writes the
+// totals.  The write pass checks the chain window by window.
 constexpr int SB = IDX_SB;
 constexpr long long NO_STOP = 0x7fffffffffffffffll;
 struct Part {           // a block's totals, then (te_index_scan) their exclusive prefixes
     u64 agg, scr;
-    long long lastrec;  // the last window at or after kE with a record (-1: none) ...
-    u64 lastexit;       // ... where the chain leaves it
-    u32 lastflags, pad;
+    long long lastrec;  // the last window at or after kE with a record (-1: none)
     long long stop;     // the first window where the chain stops (NO_STOP: none)
-    long long bad;      // the first window whose check failed (NO_STOP: none)
-    long long zero;     // the first window with a zero-length record (NO_STOP: none)
-    long long firstrec; // the first window after kE with a record (NO_STOP: none) ...
-    u64 firstentry;     // ... where the chain enters it
 };
 static_assert(sizeof(Part) == IDX_PART_BYTES, "te_index.h sizes the scan blocks' records");
-constexpr Part NO_PART{0, 0, -1, IDX_NONE, 0, 0, NO_STOP, NO_STOP, NO_STOP, NO_STOP, IDX_NONE};
 constexpr u32 STOPS = IDX_STOP | IDX_ERROR | IDX_END;
 constexpr u64 WNB = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;  // bytes a window owns
 __device__ __forceinline__ u32 idx_kE(const IdxArgs &a, u64 &entry) {
     entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
     return (u32)((entry - a.base) / WNB);
 }
-// window q's check against window j, the nearest earlier one a record starts in (>= kE),
-// whose exit and flags are xj, fj
-__device__ __forceinline__ bool chain_bad(const IdxArgs &a, u32 q, u64 eq, u64 xj, u32 fj) {
-    if (eq != IDX_NONE) return xj != eq;
-    const u64 qe = a.base + (u64)(q + 1) * WNB;
-    return xj < (qe < a.len ? qe : a.len) && !(fj & STOPS);
-}
-// combine: a before b (thread order): sums, the later record window, the earliest of the rest
-__device__ __forceinline__ void fold(Part &a, const Part &b) {
-    a.agg += b.agg;
-    a.scr += b.scr;
-    if (b.lastrec > a.lastrec) {
-        a.lastrec = b.lastrec;
-        a.lastexit = b.lastexit;
-        a.lastflags = b.lastflags;
-    }
-    a.stop = b.stop < a.stop ? b.stop : a.stop;
-    a.bad = b.bad < a.bad ? b.bad : a.bad;
-    a.zero = b.zero < a.zero ? b.zero : a.zero;
-    if (b.firstrec < a.firstrec) {
-        a.firstrec = b.firstrec;
-        a.firstentry = b.firstentry;
-    }
-}
-__device__ __forceinline__ Part shfl_part(const Part &x, int src) {
-    Part y;
-    y.agg = __shfl(x.agg, src, 64);
-    y.scr = __shfl(x.scr, src, 64);
-    y.lastrec = __shfl(x.lastrec, src, 64);
-    y.lastexit = __shfl(x.lastexit, src, 64);
-    y.lastflags = (u32)__shfl((int)x.lastflags, src, 64);
-    y.pad = 0;
-    y.stop = __shfl(x.stop, src, 64);
-    y.bad = __shfl(x.bad, src, 64);
-    y.zero = __shfl(x.zero, src, 64);
-    y.firstrec = __shfl(x.firstrec, src, 64);
-    y.firstentry = __shfl(x.firstentry, src, 64);
-    return y;
-}
-// over the block's SB threads in thread order: the exclusive fold before each thread and
-// the block's total
-__device__ __forceinline__ void part_scan(const Part &B, Part *wsum, Part &ex, Part &tot) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    Part inc = B;
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl(T x, Op op) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const Part y = shfl_part(inc, lane >= o ? lane - o : lane);
-        if (lane >= o) {
-            Part t = y;
-            fold(t, inc);
-            inc = t;
-        }
+        const T y = __shfl_up(x, o, 64);
+        if (lane >= o) x = op(x, y);
     }
+    return x;
+}
+// exclusive block scan (SB threads, thread order); `total` = the whole block's
+template <typename T, typename Op>
+__device__ __forceinline__ T block_ex(T v, T ident, Op op, T *wsum, T &total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const T inc = wave_incl(v, op);
     if (lane == 63) wsum[wid] = inc;
     __syncthreads();
-    Part W = NO_PART, T = NO_PART;
+    T base = ident, tot = ident;
 #pragma unroll
     for (int w = 0; w < SB / 64; ++w) {
-        const Part x = wsum[w];
-        if (w < wid) fold(W, x);
-        fold(T, x);
+        const T x = wsum[w];
+        if (w < wid) base = op(base, x);
+        tot = op(tot, x);
     }
     __syncthreads();
-    Part e = shfl_part(inc, lane ? lane - 1 : 0);
-    if (lane == 0) e = NO_PART;
-    fold(W, e);
-    ex = W;
-    tot = T;
+    total = tot;
+    T ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = ident;
+    return op(base, ex);
 }
+struct SumOp { __device__ u64 operator()(u64 x, u64 y) const { return x + y; } };
+struct MaxOp { __device__ long long operator()(long long x, long long y) const { return x > y ? x : y; } };
+struct MinOp { __device__ long long operator()(long long x, long long y) const { return x < y ? x : y; } };
 
 template <int S, int OL>
 __global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
@@ -520,145 +475,85 @@ __global__ __launch_bounds__(IB) void te_index_count(IdxArgs a) {
 }
 
 __global__ __launch_bounds__(SB) void te_index_part(IdxArgs a) {
-    __shared__ Part wsum[SB / 64];
+    __shared__ u64 ws64[SB / 64];
+    __shared__ long long wsll[SB / 64];
     u64 entry;
     const u32 kE = idx_kE(a, entry);
     const u32 q = blockIdx.x * SB + threadIdx.x;
     const bool in = q < a.nwin;
     const u64 eq = in ? a.w_entry[q] : IDX_NONE;
     const u32 fl = in ? a.w_flags[q] : 0u;
-    const bool rec = in && q >= kE && eq != IDX_NONE;
-    Part B = NO_PART;
+    const u64 agg = in ? a.w_agg[q] : 0ull, scr = in ? a.w_scr[q] : 0ull;
+    const long long rec = in && q >= kE && eq != IDX_NONE ? (long long)q : -1ll;
+    const long long stp = eq != IDX_NONE && (fl & STOPS) ? (long long)q : NO_STOP;
+    Part P;
+    const u64 xa = block_ex(agg, (u64)0, SumOp(), ws64, P.agg);
+    const u64 xs = block_ex(scr, (u64)0, SumOp(), ws64, P.scr);
+    const long long xr = block_ex(rec, -1ll, MaxOp(), wsll, P.lastrec);
+    (void)block_ex(stp, NO_STOP, MinOp(), wsll, P.stop);
     if (in) {
-        B.agg = a.w_agg[q];
-        B.scr = a.w_scr[q];
-        B.stop = eq != IDX_NONE && (fl & STOPS) ? (long long)q : NO_STOP;
-        B.zero = fl & IDX_ZERO ? (long long)q : NO_STOP;
+        a.w_pfx[q] = xa;
+        a.w_sbase[q] = xs;
+        a.w_prev[q] = xr;
     }
-    if (rec) {
-        B.lastrec = q;
-        B.lastexit = a.w_exit[q];
-        B.lastflags = fl;
-        if (q > kE) {
-            B.firstrec = q;
-            B.firstentry = eq;
-        }
-    }
-    Part ex, tot;
-    part_scan(B, wsum, ex, tot);
-    // the chain inside the block (a window whose earlier record window is in an earlier block
-    // is settled by te_index_scan)
-    bool bad = false;
-    if (in && q == kE) bad = eq != entry;
-    else if (in && q > kE && ex.lastrec >= 0) bad = chain_bad(a, q, eq, ex.lastexit, ex.lastflags);
-    long long rb = bad ? (long long)q : NO_STOP;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const long long z = __shfl_xor(rb, o, 64);
-        rb = z < rb ? z : rb;
-    }
-    __shared__ unsigned long long bmin;
-    if (threadIdx.x == 0) bmin = NO_STOP;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0 && rb != NO_STOP) atomicMin(&bmin, (unsigned long long)rb);
-    if (in) {
-        a.w_pfx[q] = ex.agg;
-        a.w_sbase[q] = ex.scr;
-        a.w_prev[q] = ex.lastrec;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        tot.bad = (long long)bmin;
-        ((Part *)a.parts)[blockIdx.x] = tot;
-    }
+    if (threadIdx.x == 0) ((Part *)a.parts)[blockIdx.x] = P;
 }
 
 __global__ __launch_bounds__(SB) void te_index_scan(IdxArgs a) {
-    __shared__ Part wsum[SB / 64];
+    __shared__ u64 ws64[SB / 64];
+    __shared__ long long wsll[SB / 64];
     u64 entry;
     const u32 kE = idx_kE(a, entry);
     const u32 G = (a.nwin + SB - 1) / SB;
     Part *parts = (Part *)a.parts;
-    Part C = NO_PART;  // the rounds before
+    u64 ca = 0, cs = 0;
+    long long cr = -1, cstop = NO_STOP;
     for (u32 g0 = 0; g0 < G; g0 += SB) {  // (one round up to SB^2 windows)
         const u32 g = g0 + threadIdx.x;
-        const bool gin = g < G;
-        Part B = gin ? parts[g] : NO_PART;
-        Part ex, tot;
-        part_scan(B, wsum, ex, tot);
-        Part pre = C;
-        fold(pre, ex);  // everything before block g
-        if (gin && pre.lastrec >= (long long)kE) {
-            // block g's windows up to its first record window (after kE): their nearest
-            // earlier record window is the last of the blocks before.  The record window's
-            // first record must be where the chain left that one; the windows before it must
-            // be passed over (the first one the chain does not pass is the miss)
-            const u64 xj = pre.lastexit;
-            const u32 fj = pre.lastflags;
-            const u32 blk_end = (g + 1) * SB < a.nwin ? (g + 1) * SB : a.nwin;  // (exclusive)
-            const u32 lo = g * SB > kE + 1 ? g * SB : kE + 1;
-            const u32 hi = B.firstrec != NO_STOP ? (u32)B.firstrec : blk_end;  // empty windows [lo, hi)
-            long long miss = NO_STOP;
-            if (lo < hi && !(fj & STOPS) && xj < a.len) {
-                // the first empty window whose end (or the capture's) lies past the chain's exit
-                const u64 w = xj >= a.base ? (xj - a.base) / WNB : 0;
-                const u64 wq = w > lo ? w : lo;
-                if (wq < hi && (xj < a.base + (wq + 1) * WNB)) miss = (long long)wq;
-            }
-            if (miss == NO_STOP && B.firstrec != NO_STOP && xj != B.firstentry) miss = B.firstrec;
-            B.bad = miss < B.bad ? miss : B.bad;
-        }
-        if (gin) {
-            parts[g] = pre;
-            (void)0;
-        }
-        // the round's totals, the deferred misses folded in
-        long long rb = gin ? B.bad : NO_STOP;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const long long z = __shfl_xor(rb, o, 64);
-            rb = z < rb ? z : rb;
-        }
-        __shared__ unsigned long long bmin;
-        if (threadIdx.x == 0) bmin = NO_STOP;
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0 && rb != NO_STOP) atomicMin(&bmin, (unsigned long long)rb);
-        __syncthreads();
-        fold(C, tot);
-        C.bad = (long long)bmin < C.bad ? (long long)bmin : C.bad;
-        __syncthreads();
+        const bool in = g < G;
+        const Part P = in ? parts[g] : Part{0, 0, -1, NO_STOP};
+        u64 ta, ts;
+        long long tr, tst;
+        const u64 xa = block_ex(P.agg, (u64)0, SumOp(), ws64, ta);
+        const u64 xs = block_ex(P.scr, (u64)0, SumOp(), ws64, ts);
+        const long long xr = block_ex(P.lastrec, -1ll, MaxOp(), wsll, tr);
+        (void)block_ex(P.stop, NO_STOP, MinOp(), wsll, tst);
+        if (in) parts[g] = Part{ca + xa, cs + xs, xr > cr ? xr : cr, NO_STOP};
+        ca += ta;
+        cs += ts;
+        cr = tr > cr ? tr : cr;
+        cstop = tst < cstop ? tst : cstop;
     }
     if (threadIdx.x) return;
-    const bool stopped = C.stop != NO_STOP;
-    const u32 last = stopped ? (u32)C.stop : a.nwin - 1;  // windows past the chain's end do not count
+    const bool stopped = cstop != NO_STOP;
+    const u32 last = stopped ? (u32)cstop : a.nwin - 1;  // windows past the chain's end do not count
     u64 tot, scr, end;
     u32 fl_last = 0;
-    if (!stopped) {  // (no window loads: the whole capture's totals)
-        tot = C.agg;
-        scr = C.scr;
-        end = C.lastrec >= (long long)kE ? C.lastexit : IDX_NONE;
+    if (!stopped) {  // the whole capture's totals; the chain ends in the last window with a record
+        tot = ca;
+        scr = cs;
+        end = cr >= (long long)kE ? a.w_exit[cr] : IDX_NONE;
     } else {
         const Part &L = parts[last / SB];
         tot = L.agg + a.w_pfx[last] + a.w_agg[last];  // inclusive (records | tiles) through `last`
         scr = L.scr + a.w_sbase[last] + a.w_scr[last];
-        // the chain's last window with a record, at or before `last` (the stopping one)
-        end = a.w_exit[last];
+        end = a.w_exit[last];  // (a window that stops the chain has a record)
         fl_last = a.w_flags[last];
     }
-    const bool isbad = C.bad != NO_STOP && C.bad <= (long long)last;
     a.totals[IDX_T_RECS] = tot & REC_MASK;
     a.totals[IDX_T_TILES] = tot >> REC_BITS;
     a.totals[IDX_T_SCRATCH] = scr;
-    a.totals[IDX_T_BAD] = isbad ? 1 : 0;
     a.totals[IDX_T_WINDOWS] = last + 1;
     a.totals[IDX_T_STOP] = stopped ? (fl_last & STOPS) : 0;
     a.totals[IDX_T_END] = end == IDX_NONE ? entry : end;
     a.totals[IDX_T_BYTES] = (a.totals[IDX_T_END] - entry) + (u64)a.growth * (tot & REC_MASK);
-    a.totals[IDX_T_ZERO] = C.zero != NO_STOP && C.zero <= (long long)last ? 1 : 0;
     // the record the chain stopped at: the one after the stopping window's last
     a.totals[IDX_T_ERR_REC] = stopped && (fl_last & IDX_ERROR) ? tot & REC_MASK : ~0ull;
     a.totals[IDX_T_OVERFLOW] = (tot & REC_MASK) > a.rec_cap || (tot >> REC_BITS) > a.tile_cap ? 1 : 0;
-    a.totals[IDX_T_BADWIN] = isbad ? (u64)C.bad : 0xffffffffull;
+    // set by the write pass, window by window
+    a.totals[IDX_T_BAD] = 0;
+    a.totals[IDX_T_BADWIN] = 0xffffffffull;
+    a.totals[IDX_T_ZERO] = 0;
 }
 
 // ---- the write pass: a wave per window puts its tiles and record offsets at its bases ----
@@ -666,13 +561,43 @@ __global__ __launch_bounds__(IB) void te_index_write(IdxArgs a) {
     const int lane = threadIdx.x & 63;
     const u32 k = blockIdx.x * IWAVES + (threadIdx.x >> 6);
     if (k >= a.nwin) return;
-    // (every load this wave needs before the copies, issued together)
-    const u64 *T = a.totals;
-    const u64 nwin_chain = T[IDX_T_WINDOWS], skip = T[IDX_T_BAD] | T[IDX_T_OVERFLOW];
+    // (the loads this wave needs before the copies, issued together)
+    u64 *T = a.totals;
+    const u64 nwin_chain = T[IDX_T_WINDOWS], ovf = T[IDX_T_OVERFLOW];
     const Part G = ((const Part *)a.parts)[k / SB];
     const u64 agg = a.w_agg[k], lpfx = a.w_pfx[k], wexit = a.w_exit[k], lsb = a.w_sbase[k];
-    if (k >= nwin_chain || skip) return;  // past the chain's end, or the host index stays
-    constexpr u64 WN = (u64)IW * TE_IDX_S - (u64)TE_IDX_OL * TE_IDX_S;
+    const u64 eq = a.w_entry[k];
+    const long long wprev = a.w_prev[k];
+    const u32 wfl = a.w_flags[k];
+    if (k >= nwin_chain) return;  // past the chain's end
+    constexpr u64 WN = WNB;
+    if (lane == 0) {
+        // the chain across windows: this window's first record must be where the chain left
+        // the nearest earlier window a record starts in; a window without one must be passed
+        // over whole (a miss: the caller keeps the host walk's index, which is exact)
+        u64 entry;
+        const u32 kE = idx_kE(a, entry);
+        bool bad = false;
+        if (k == kE) {
+            bad = eq != entry;
+        } else if (k > kE) {
+            long long j = G.lastrec > wprev ? G.lastrec : wprev;
+            if (j < (long long)kE) j = kE;
+            const u64 xj = a.w_exit[j];
+            if (eq != IDX_NONE) {
+                bad = xj != eq;
+            } else {
+                const u64 qe = a.base + (u64)(k + 1) * WN;
+                bad = xj < (qe < a.len ? qe : a.len) && !(a.w_flags[j] & STOPS);
+            }
+        }
+        if (bad) {
+            atomicOr((unsigned long long *)&T[IDX_T_BAD], 1ull);
+            atomicMin((unsigned long long *)&T[IDX_T_BADWIN], (unsigned long long)k);
+        }
+        if (wfl & IDX_ZERO) atomicOr((unsigned long long *)&T[IDX_T_ZERO], 1ull);
+    }
+    if (ovf) return;
     const u64 ws = a.base + (u64)k * WN;
     const u64 pfx = G.agg + lpfx;
     const u32 nrec = (u32)(agg & REC_MASK), ntile = (u32)(agg >> REC_BITS);

@@ -115,11 +115,6 @@ ARGSETS = [
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fixcsum"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
     ["--dlt=pppserial", "--fixcsum"],
-    # --fuzz-seed behind the decoder: fuzzing.c reads the encoder's L2 length and protocol
-    ["--dlt=enet"] + MACS + ["--fuzz-seed=7", "--fuzz-factor=2", "--fixcsum"],
-    ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fuzz-seed=5",
-     "--fuzz-factor=3"],
-    ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--fuzz-seed=9", "--fuzz-factor=2"],
 ]
 
 

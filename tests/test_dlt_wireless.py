@@ -113,7 +113,7 @@ def test_oracle_jnpr_into_ethernet_strips_header_and_tag(built):
 
 def test_unserved_combinations_are_refused(built):
     for dlt, args in [(178, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
-                      (105, ["--fuzz-seed=3"])]:
+                      (105, ["--fuzz-seed=3"]), (127, ["--fuzz-seed=3", "--dlt=enet"] + MACS)]:
         with pytest.raises(Exception):
             TA.TcpEdit(args, dlt=dlt)
 
@@ -126,7 +126,6 @@ ARGSETS = [
     ["--dlt=enet"] + MACS + ["--seed=11", "--ttl=+2", "--efcs"],
     ["--dlt=enet", "--enet-vlan=del", "--tos=5", "--mtu-trunc", "--mtu=400", "--fixcsum"] + MACS,
     ["--dlt=enet", "--seed=3", "--fixcsum"],  # the decoded addresses (802.11, Juniper's inner frame)
-    ["--dlt=enet", "--fuzz-seed=3", "--fuzz-factor=2", "--fixcsum"] + MACS,  # fuzzing behind the decoder
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fixcsum"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
 ]
