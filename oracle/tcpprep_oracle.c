@@ -452,12 +452,84 @@ static tpo_node_t *tpo_find(int family, const uint8_t *addr, int insert, int *in
     return NULL;
 }
 
+/* get_l2len_protocol (get.c:263-452) with the capture's datalink, for the DLTs tcpprep
+   reads (tcpprep.c:108-118); the IP header is at l2len (get_ipv4/get_ipv6: packet +=
+   l2offset, l2len -= l2offset, ip = packet + l2len, get.c:509-510) */
+static int tpo_dlt = 1;
+static int tpo_l2(const uint8_t *d, uint32_t caplen, uint16_t *proto, uint32_t *l2len)
+{
+    uint32_t l2off = 0, voff = 0;
+    *proto = 0;
+    *l2len = 0;
+    if (!caplen)
+        return -1;
+    switch (tpo_dlt) {
+    case 12: /* DLT_NULL / DLT_RAW (get.c:287-293): the version nibble, no L2 bytes */
+        if ((d[0] >> 4) == 4)
+            *proto = 0x0800;
+        else if ((d[0] >> 4) == 6)
+            *proto = 0x86DD;
+        return 0;
+    case 178: { /* DLT_JUNIPER_ETHER (get.c:294-345) */
+        if (caplen < 4 || memcmp(d, "MGC", 3) != 0)
+            return -1;
+        if ((d[3] & 0x80) == 0x80) { /* JUNIPER_FLAG_EXT */
+            if (caplen < 6)
+                return -1;
+            l2off = (uint32_t)((d[4] << 8) | d[5]) + 6;
+        } else {
+            l2off = 4;
+        }
+        if ((d[3] & 0x02) == 0x02) /* JUNIPER_FLAG_NO_L2: refused before the classification */
+            return -1;
+        /* fall through to DLT_EN10MB at l2offset (get.c:347-381) */
+        uint32_t l2_net_off = 14 + l2off;
+        if (caplen <= l2_net_off + 4)
+            return -1;
+        uint16_t et = (uint16_t)((d[l2off + 12] << 8) | d[l2off + 13]);
+        if (parse_metadata(d, caplen, &et, &l2_net_off, &l2off, &voff))
+            return -1;
+        *l2len = l2_net_off;
+        if (et < 1536)
+            return -1;
+        *proto = et;
+        return 0;
+    }
+    case 50: /* DLT_PPP_SERIAL (get.c:383-400): PPP's IPv4 number counts as IPv4 */
+        if (caplen < 4)
+            return -1;
+        *l2len = 4;
+        *proto = (uint16_t)((d[2] << 8) | d[3]) == 0x0021 ? 0x0800 : (uint16_t)((d[2] << 8) | d[3]);
+        return 0;
+    case 104: /* DLT_C_HDLC (get.c:401-414) */
+        if (caplen < 4)
+            return -1;
+        *l2len = 4;
+        *proto = (uint16_t)((d[2] << 8) | d[3]);
+        return 0;
+    case 113: /* DLT_LINUX_SLL (get.c:415-428): sll_protocol at 14 */
+        if (caplen < 16)
+            return -1;
+        *l2len = 16;
+        *proto = (uint16_t)((d[14] << 8) | d[15]);
+        return 0;
+    case 276: /* DLT_LINUX_SLL2 (get.c:429-442): sll2_protocol first */
+        if (caplen < 20)
+            return -1;
+        *l2len = 20;
+        *proto = (uint16_t)((d[0] << 8) | d[1]);
+        return 0;
+    default: /* DLT_EN10MB */
+        return get_l2len_protocol(d, caplen, proto, l2len, &l2off, &voff);
+    }
+}
+
 /* packet2tree (tree.c:653-838): the node type a packet gives its source; -2 = len_error */
 static int tpo_packet2tree(const uint8_t *d, uint32_t caplen)
 {
     uint16_t et = 0;
-    uint32_t l2len = 0, l2off = 0, voff = 0;
-    if (get_l2len_protocol(d, caplen, &et, &l2len, &l2off, &voff) == -1)
+    uint32_t l2len = 0;
+    if (tpo_l2(d, caplen, &et, &l2len) == -1)
         return -2;
     long len = caplen, hl = 0;
     uint8_t proto = 0;
@@ -531,8 +603,8 @@ static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, in
         const uint8_t *d = pcap + off + 16;
         off += 16 + caplen;
         uint16_t proto = 0;
-        uint32_t l2len = 0, l2off = 0, voff = 0;
-        int res = caplen ? get_l2len_protocol(d, caplen, &proto, &l2len, &l2off, &voff) : -1;
+        uint32_t l2len = 0;
+        int res = caplen ? tpo_l2(d, caplen, &proto, &l2len) : -1;
         int v4 = res != -1 && l2len + 20 <= caplen && proto == 0x0800;
         int v6 = !v4 && res != -1 && l2len + 40 <= caplen && proto == 0x86DD;
         if (!v4 && !v6)
@@ -623,6 +695,25 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
         sw = 1;
     else
         return -2;
+    /* tcpprep.c:108-125: the link types it reads (LINKTYPE_RAW as DLT_RAW), MAC mode on
+       Ethernet only; a Juniper record without an L2 header makes the reference's get_ipv4
+       read ~4 GiB past the packet: refused (-4) */
+    uint32_t lt = tpo_rd32(pcap + 20, sw) & 0x03ffffffu;
+    tpo_dlt = lt == 101 ? 12 : (int)lt;
+    if (tpo_dlt != 1 && tpo_dlt != 113 && tpo_dlt != 276 && tpo_dlt != 12 && tpo_dlt != 104 && tpo_dlt != 178 &&
+        tpo_dlt != 50)
+        return -4; /* errx "Unsupported pcap DLT type" */
+    if (tpo_dlt != 1 && o.mode == TPO_MAC)
+        return -4; /* err "MAC mode splitting is only supported by DLT_EN10MB packet captures." */
+    if (tpo_dlt == 178)
+        for (size_t off = 24; off + 16 <= len;) {
+            uint32_t cl = tpo_rd32(pcap + off + 8, sw);
+            if (cl > 262144u || off + 16 + cl > len)
+                break;
+            if (cl >= 4 && !memcmp(pcap + off + 16, "MGC", 3) && (pcap[off + 16 + 3] & 0x02))
+                return -4;
+            off += 16 + cl;
+        }
     size_t clen = strlen(o.comment);
     size_t hdr = 24 + clen;
     if (cap < hdr)
@@ -657,8 +748,8 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
         }
         if (o.mode != TPO_MAC) {
             uint16_t proto = 0;
-            uint32_t l2len = 0, l2off = 0, voff = 0;
-            int res = caplen ? get_l2len_protocol(pkt, caplen, &proto, &l2len, &l2off, &voff) : -1;
+            uint32_t l2len = 0;
+            int res = caplen ? tpo_l2(pkt, caplen, &proto, &l2len) : -1;
             int v4 = res != -1 && l2len + 20 <= caplen && proto == 0x0800;  /* get_ipv4 get.c:483-541 */
             int v6 = !v4 && res != -1 && l2len + 40 <= caplen && proto == 0x86DD; /* get_ipv6 :550-608 */
             if (!v4 && !v6) {

@@ -401,9 +401,14 @@ static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index
         sw = 1;
     else
         return tp_err(t, "not a pcap file (magic 0x%08x)", magic);
+    /* the link types tcpprep reads (tcpprep.c:108-125: pcap_datalink, LINKTYPE_RAW as DLT_RAW) */
     uint32_t linktype = rd32(img + 20, sw) & 0x03ffffffu;
-    if (linktype != 1)
-        return tp_err(t, "the GPU classifier reads DLT_EN10MB captures only (linktype %u)", linktype);
+    const int dlt = linktype == 101 ? 12 : (int)linktype;
+    if (dlt != 1 && dlt != 113 && dlt != 276 && dlt != 12 && dlt != 104 && dlt != 178 && dlt != 50)
+        return tp_err(t, "Unsupported pcap DLT type: 0x%x", (unsigned)dlt);
+    if (dlt != 1 && t->cfg.mode == TP_MODE_MAC)
+        return tp_err(t, "MAC mode splitting is only supported by DLT_EN10MB packet captures.");
+    t->cfg.dlt = dlt;
     uint64_t cap = len / 16 + 1;
     x->off = malloc(cap * sizeof(uint64_t));
     x->caplen = malloc(cap * sizeof(uint32_t));
@@ -415,6 +420,11 @@ static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index
         if (caplen > 262144u || off + 16 + caplen > len)
             break;
         x->records++;
+        if (dlt == 178 && caplen >= 4 && !memcmp(img + off + 16, "MGC", 3) && (img[off + 16 + 3] & 0x02))
+            /* JUNIPER_FLAG_NO_L2: get_l2len_protocol leaves l2len 0 with l2offset past it, and
+               get_ipv4 then forms a pointer ~4 GiB past the packet (get.c:326-344,509-510) */
+            return tp_err(t, "record %llu: a Juniper record without an L2 header (the reference reads outside the "
+                             "packet there): not served", (unsigned long long)x->records);
         const tp_dev_cfg_t *c = &t->cfg;
         int listed_out = c->nlist && check_list(c, c->pkt_base + x->records) == ((c->xx_mode & TP_XX_EXCLUDE) != 0);
         if (mac && caplen < 14 && !listed_out) {

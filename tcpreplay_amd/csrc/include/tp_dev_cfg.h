@@ -32,6 +32,7 @@ typedef struct {
     int32_t mode, reverse, nonip, mac_first_empty;
     int32_t ncidr, nmac, xx_mode, nxx_cidr;
     int32_t nlist, automode;
+    int32_t dlt, pad_;           /* the capture's link type (get_l2len_protocol's datalink) */
     double ratio;                /* --ratio (default 2.0) */
     uint64_t pkt_base;           /* records before this capture (a shard's place in the job) */
     te_cidr_t cidr[TP_MAXC];     /* -c list (check_ip_cidr: empty list matches all) */

@@ -125,10 +125,63 @@ DI uint32_t tree_insert(const tp_tree_t &t, uint64_t key) {
     return 0xffffffffu;  // cannot happen: capacity >= 2x the insertions
 }
 
+// get_l2len_protocol over the capture's link type (get.c:263-452): the L3 protocol and
+// the bytes before the IP header, for every DLT tcpprep reads (tcpprep.c:108-118).  A
+// Juniper record without an L2 header never gets here (the host refuses the capture: the
+// reference's get_ipv4 then reads ~4 GiB past the packet, get.c:509-510)
+DI int tp_l2(const u8 *d, u32 caplen, int dlt, L2 &r) {
+    r.protocol = 0;
+    r.l2len = 0;
+    if (!caplen) return -1;
+    switch (dlt) {
+    case 1:  // DLT_EN10MB
+        return get_l2len_protocol(d, caplen, r);
+    case 12:   // DLT_RAW (linktype 101)
+    case 101:
+        r.protocol = (d[0] >> 4) == 4 ? 0x0800 : (d[0] >> 4) == 6 ? 0x86DD : 0;
+        return 0;
+    case 50:  // DLT_PPP_SERIAL: the PPP IPv4 protocol number counts as IPv4
+        if (caplen < 4) return -1;
+        r.l2len = 4;
+        r.protocol = be16(d + 2) == 0x0021 ? 0x0800 : be16(d + 2);
+        return 0;
+    case 104:  // DLT_C_HDLC
+        if (caplen < 4) return -1;
+        r.l2len = 4;
+        r.protocol = be16(d + 2);
+        return 0;
+    case 113:  // DLT_LINUX_SLL
+        if (caplen < 16) return -1;
+        r.l2len = 16;
+        r.protocol = be16(d + 14);
+        return 0;
+    case 276:  // DLT_LINUX_SLL2
+        if (caplen < 20) return -1;
+        r.l2len = 20;
+        r.protocol = be16(d);
+        return 0;
+    case 178: {  // DLT_JUNIPER_ETHER: magic, flags, extensions, then the Ethernet header
+        if (caplen < 4 || d[0] != 0x4d || d[1] != 0x47 || d[2] != 0x43) return -1;
+        u32 off = 4;
+        if (d[3] & 0x80) {
+            if (caplen < 6) return -1;
+            off = (u32)be16(d + 4) + 6;
+        }
+        if (d[3] & 0x02) return -1;
+        if (caplen <= off + 18) return -1;  // datalen <= l2_net_off + 4
+        if (get_l2len_protocol(d + off, caplen - off, r) == -1) return -1;
+        r.l2len += off;
+        return 0;
+    }
+    default:
+        return -1;
+    }
+}
+
 // packet2tree (tree.c:653-838): node type for the source, -1 unknown, -2 len_error
-DI int packet2tree(const u8 *d, u32 caplen) {
+DI int packet2tree(const u8 *d, u32 caplen, int dlt) {
     L2 r;
-    if (get_l2len_protocol(d, caplen, r) == -1) return -2;
+    if (tp_l2(d, caplen, dlt, r) == -1) return -2;
     const long len = caplen;
     long hl = 0;
     u8 proto = 0;
@@ -169,13 +222,14 @@ DI int packet2tree(const u8 *d, u32 caplen) {
 
 __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img, const uint64_t *__restrict__ off,
                                                      const uint32_t *__restrict__ caplen, uint64_t n, int first_mode,
-                                                     uint64_t base, tp_tree_t t) {
+                                                     uint64_t base, tp_tree_t t, const tp_dev_cfg_t *cfg) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const u8 *d = img + off[j];
     const u32 cl = caplen[j];
+    const int dlt = cfg->dlt;
     L2 r;
-    const int res = cl ? get_l2len_protocol(d, cl, r) : -1;
+    const int res = cl ? tp_l2(d, cl, dlt, r) : -1;
     const bool v4 = res != -1 && r.l2len + 20 <= cl && r.protocol == 0x0800;
     const bool v6 = !v4 && res != -1 && r.l2len + 40 <= cl && r.protocol == 0x86DD;
     if (!v4 && !v6) {
@@ -199,7 +253,7 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
             atomicMax((unsigned long long *)&t.slots[2 * sd + 1], ~(unsigned long long)(2 * (base + j) + 1));
         return;
     }
-    const int ty = packet2tree(d, cl);  // add_tree_ipv4/ipv6 + add_tree_node (tree.c:454-538)
+    const int ty = packet2tree(d, cl, dlt);  // add_tree_ipv4/ipv6 + add_tree_node (tree.c:454-538)
     if (ty == -2)
         atomicMin((unsigned long long *)t.err, (unsigned long long)j);
     else if (ty >= 0)  // the counts share the key's 16-byte pair: one line per node
@@ -316,7 +370,7 @@ DI u32 classify(const tp_dev_cfg_t &c, const tp_tree_t *t, uint64_t j, const u8 
     int dir;
     if (c.mode != TP_MODE_MAC) {
         L2 r;
-        const int res = caplen ? get_l2len_protocol(pkt, caplen, r) : -1;
+        const int res = caplen ? tp_l2(pkt, caplen, c.dlt, r) : -1;
         const bool v4 = res != -1 && r.l2len + 20 <= caplen && r.protocol == 0x0800;  // get_ipv4 get.c:483-541
         const bool v6 = !v4 && res != -1 && r.l2len + 40 <= caplen && r.protocol == 0x86DD;  // get_ipv6 :550-608
         if (!v4 && !v6) return SEND | (c.nonip == 1 ? C2S : 0);  // add_cache(SEND, options->nonip)
@@ -402,6 +456,6 @@ extern "C" int tp_launch_tree(const uint8_t *img, const uint64_t *off, const uin
     const uint64_t blocks = (n_entries + 255) / 256;
     if (blocks > 0x7fffffffull) return -1;
     hipLaunchKernelGGL(tp_tree_build, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, off, caplen,
-                       n_entries, automode == TP_AUTO_FIRST ? 1 : 0, base, tree);
+                       n_entries, automode == TP_AUTO_FIRST ? 1 : 0, base, tree, cfg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
