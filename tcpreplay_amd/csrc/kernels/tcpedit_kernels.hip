@@ -707,6 +707,9 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
 // request and response words with the bytes.  The loop ends on `stop` or after
 // idle_ticks without a request, so the grid always drains.
 // ===========================================================================
+static_assert(offsetof(te_srv_ctl_t, dir) % 16 == 0 && offsetof(te_srv_ctl_t, caplen) == offsetof(te_srv_ctl_t, dir) + 4 &&
+                  offsetof(te_srv_ctl_t, pkt_base) == offsetof(te_srv_ctl_t, dir) + 8,
+              "the server reads {dir, caplen, pkt_base} as one 16-byte word (the control block is page-aligned)");
 __global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
@@ -756,9 +759,11 @@ __global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
         // the host's stores before its release of seq are visible from here on
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t seq = req;
-        const uint32_t caplen = *(const volatile uint32_t *)&ctl->caplen;
-        a.fixed_dir = *(const volatile int32_t *)&ctl->dir;
-        a.pkt_base = *(const volatile uint64_t *)&ctl->pkt_base;
+        // the request words in one 16-byte read over PCIe: {dir, caplen, pkt_base}
+        const u32x4 rq = *(const volatile u32x4 *)&ctl->dir;
+        const uint32_t caplen = rq.y;
+        a.fixed_dir = (int32_t)rq.x;
+        a.pkt_base = (uint64_t)rq.z | ((uint64_t)rq.w << 32);
         te_tile_t tile;
         tile.span_off = 24;
         tile.scratch_off = TE_NO_SCRATCH;
@@ -767,17 +772,18 @@ __global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
         tile.span_len = 16 + caplen;
         tile.flags = 0;
         tile_body<MODE_SLOT, false, uint8_t *, true>(a, tile, 0, slots, sh, cfg, &js);
-        // every lane's output stores are complete and visible to the host ...
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        __syncthreads();
+        __syncthreads();  // (the block's counters are in sh.cnt)
         if (threadIdx.x == 0) {
             ctl->status = *(volatile uint8_t *)s.scratch;  // (this lane's own store: the record's lane)
             ctl->bytes_out = sh.cnt[TE_CNT_BYTES_OUT];
             ctl->packets = sh.cnt[TE_CNT_PACKETS];
             ctl->edited = sh.cnt[TE_CNT_EDITED];
-            // ... before the response words and done
-            __hip_atomic_store(&ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        // every lane's output stores and the response words are complete and visible to the
+        // host (one PCIe round trip for all of them) before done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         last = seq;
         __syncthreads();
     }

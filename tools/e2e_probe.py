@@ -9,9 +9,12 @@ os.environ["TCPEDIT_HIP_PIPE_TRACE"] = "1"
 import tcpreplay_amd as TA  # noqa: E402
 from tcpreplay_amd import synth as S  # noqa: E402
 
-for name, pcap, args in (("c2", S.pcap_fixed(1_000_000, 64, seed=1), ["--seed=42", "--fixcsum"]),
-                         ("c3_2M", S.pcap_imix(2_000_000, seed=1),
-                          ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"])):
+CHUNKS = [int(c) << 20 for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [4 << 20, 16 << 20, 64 << 20]
+CASES = (("c2", lambda: S.pcap_fixed(1_000_000, 64, seed=1), ["--seed=42", "--fixcsum"]),
+         ("c3_2M", lambda: S.pcap_imix(2_000_000, seed=1),
+          ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]))
+for name, gen, args in CASES[:int(sys.argv[2]) if len(sys.argv) > 2 else 2]:
+    pcap = gen()
     te = TA.TcpEdit(args)
     rc, ref = te.rewrite_pipelined(pcap)
     pin_in = TA.PinnedBuffer(len(pcap))
@@ -20,7 +23,7 @@ for name, pcap, args in (("c2", S.pcap_fixed(1_000_000, 64, seed=1), ["--seed=42
     pin_out = TA.PinnedBuffer(bound)
     src = bytearray(pcap)
     obuf = bytearray(bound)
-    for chunk in (4 << 20, 16 << 20, 64 << 20):
+    for chunk in CHUNKS:
         for kind in ("pageable", "pinned"):
             si, so = (src, obuf) if kind == "pageable" else (pin_in.view, pin_out.view)
             ts = []
