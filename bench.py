@@ -423,7 +423,8 @@ def main():
         us = ctypes.c_double()
         if f(te1._ctx, pkt, len(pkt), 2000, ctypes.byref(us)) == 0:
             result["packet_api"] = {"us_per_call": round(us.value, 2), "calls": 2000,
-                                    "path": "tcpedit_packet: pinned staging, H2D, edit kernel, D2H, sync per call"}
+                                    "path": "tcpedit_packet through the resident device block: record and "
+                                            "request in host-mapped memory, edited in LDS, response polled"}
         te1.close()
     # the record index built on the device (te_index.hip) from the HBM-resident image, in
     # place of the host walk: its build time, and the edit over the tiles it cut -- index +
@@ -535,8 +536,9 @@ def main():
                 return {"mpkt_s": round(n / sec / 1e6, 2), "ms": round(sec * 1e3, 3),
                         "gbps_in": round(len(pcap) / sec / 1e9, 2), "path": path}
             result["end_to_end"] = dict(
-                rate(p_s, "page-locked host capture -> 16 MiB chunks of whole records, H2D | edit | D2H on "
-                          "three streams -> page-locked host output (median of 5)"),
+                rate(p_s, "page-locked host capture -> chunks of whole records (the default: a tenth of the "
+                          "capture, 8-32 MiB), device record index | edit | D2H on three streams -> page-locked "
+                          "host output (median of 5)"),
                 pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 5)"),
                 one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
                                    "pageable copies (median of 3)"))

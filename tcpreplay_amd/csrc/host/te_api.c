@@ -2158,7 +2158,11 @@ static int host_locked(const void *p)
    indexed and edited and chunk k + 2 uploads -- into a third slot, so chunk k's input and
    index stand until it is finished */
 #define TE_PIPE_SLOTS 3
-#define TE_PIPE_CHUNK_DEFAULT ((size_t)16 << 20)
+/* the default chunk: a tenth of the capture, 8-32 MiB (measured on MI355X, tools/e2e_probe.py:
+   C2's 80 MB runs best at 8 MiB -- pipeline fill and drain are one chunk each -- and 2M IMIX
+   records (740 MB) at 12-32 MiB, where per-chunk costs dominate) */
+#define TE_PIPE_CHUNK_MIN ((size_t)8 << 20)
+#define TE_PIPE_CHUNK_MAX ((size_t)32 << 20)
 
 /* res_pinned layout: counters | error words | wave-lane slots */
 #define TE_RES_ERR 96
@@ -2654,8 +2658,10 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         te_seterr(t, "pcap image too short");
         return TCPEDIT_ERROR;
     }
-    if (chunk_bytes == 0)
-        chunk_bytes = TE_PIPE_CHUNK_DEFAULT;
+    if (chunk_bytes == 0) {
+        const size_t tenth = (in_len / 10 + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+        chunk_bytes = tenth < TE_PIPE_CHUNK_MIN ? TE_PIPE_CHUNK_MIN : tenth > TE_PIPE_CHUNK_MAX ? TE_PIPE_CHUNK_MAX : tenth;
+    }
     if (chunk_bytes < ((size_t)1 << 20))
         chunk_bytes = (size_t)1 << 20; /* >= any record (16 + 262144 B) */
     chunk_bytes = (chunk_bytes + 15) & ~(size_t)15;
