@@ -166,8 +166,8 @@ static int fast_capable(const te_dev_cfg_t *c)
     return static_capable(c) && !c->fixhdrlen && cidr_inline(c);
 }
 
-/* the most a record's L2 header can grow: a VLAN push (4 bytes) or a user header longer
-   than Ethernet's 14 (device: at most TE_HEAD, more is flagged unsupported) */
+/* the most one encode can grow a record's L2 header: an encoder header longer than the
+   decoded one (a VLAN push is counted by the callers) */
 static int l2_growth(const te_dev_cfg_t *c)
 {
     const int dl = te_decoder_l2len(c->decoder);
@@ -181,6 +181,23 @@ static uint32_t rec_growth(const te_dev_cfg_t *c)
     const int l2 = l2_growth(c);
     const uint32_t g = l2 > 4 ? (uint32_t)l2 : 4u;
     return c->fuzz_seed ? 2 * g : g; /* a fuzzed record is encoded twice (tcpedit.c:250-258) */
+}
+
+/* the generic lane's slot headroom (te_dev_cfg_t.slot_head): room for the record header to
+   move left by every growth the record's encodes can make together -- one encode, or two
+   for a fuzzed record, which goes back to `again:` and is decoded (by the input decoder,
+   whose L2 is never shorter than te_decoder_l2len) and encoded a second time
+   (tcpedit.c:89-118,250-258) */
+uint32_t te_slot_head(const te_dev_cfg_t *c)
+{
+    int g = l2_growth(c);
+    if (c->encoder == TE_ENC_EN10MB && c->vlan == TE_VLAN_ADD && g < 4)
+        g = 4; /* a VLAN push (en10mb.c:568-578) */
+    if (g < 0)
+        g = 0;
+    const uint32_t need = (uint32_t)(c->fuzz_seed ? 2 * g : g);
+    const uint32_t h = (need + 15u) & ~15u;
+    return h > TE_HEAD ? h : TE_HEAD;
 }
 
 /* VLAN add as the only size change, on the wave lane (static +4 placement): the other
@@ -261,6 +278,7 @@ typedef struct {
     size_t len;
     int swapped, pad, slot_mode, grow_fast, wave, shrink_fast;
     uint32_t budget, max_pkts;
+    uint32_t head;           /* slot headroom (te_slot_head) */
     uint32_t growth;         /* output room per record beyond its input (rec_growth) */
     /* the stretch */
     size_t start, stop_at;
@@ -330,7 +348,7 @@ static void walk_range(te_walk_t *w)
             w->has_zero_cap = 1;
         uint32_t data = w->pad && plen > caplen ? plen : caplen;
         uint32_t g = (uint32_t)(off & 15);
-        uint32_t slot = TE_SLOT_BYTES_OF(g, data);
+        uint32_t slot = TE_SLOT_BYTES_OF_H(w->head, g, data);
         int huge, fits;
         if (w->slot_mode && !w->grow_fast) {
             huge = slot > TE_SLOT_BYTES;
@@ -568,6 +586,7 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
     /* slots with headroom: VLAN push, fixlen pad, a user L2 header longer than Ethernet's */
     proto->slot_mode = proto->pad || (t->cfg.encoder == TE_ENC_EN10MB && t->cfg.vlan == TE_VLAN_ADD) ||
                        l2_growth(&t->cfg) > 0;
+    proto->head = te_slot_head(&t->cfg);
     b->slot_layout = proto->slot_mode;
     /* the wave lane also takes VLAN add (native-order microsecond input only): its tiles
        are cut to the wave image (their per-record slots then fit the generic kernel's) */
@@ -592,7 +611,8 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
     b->cut_budget = proto->budget;
     b->cut_max_pkts = proto->max_pkts;
     b->cut_growth = proto->growth;
-    b->cut_device_ok = proto->wave && !proto->pad && (!proto->slot_mode || proto->grow_fast);
+    b->cut_device_ok = proto->wave && !proto->pad && (!proto->slot_mode || proto->grow_fast) &&
+                       proto->head == TE_HEAD; /* (te_index sizes scratch slots with TE_HEAD) */
 }
 
 /* Walk the records and cut them into tiles.  A large image is walked as up to
@@ -947,6 +967,10 @@ int te_upload_cfg(tcpedit_t *t)
     if (t->cfg.fuzz_seed && t->fz_seeded &&
         t->fz_gen != __atomic_load_n(&te_fuzz_init_gen, __ATOMIC_SEQ_CST))
         t->dev_dirty = 1; /* a fuzzing_init since the last upload re-seeds the state */
+    if (t->cfg.slot_head != te_slot_head(&t->cfg)) { /* whatever set the config */
+        t->cfg.slot_head = te_slot_head(&t->cfg);
+        t->dev_dirty = 1;
+    }
     {   /* the dst_modified carry, whatever set the config (post_args or setters) */
         const te_dev_cfg_t *c = &t->cfg;
         const uint32_t l2c = TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB &&
@@ -2990,6 +3014,7 @@ int tcpedit_get_dev_cfg(tcpedit_t *t, void *out, size_t len, uint16_t *portlut)
     if (!t || !out || len < sizeof(te_dev_cfg_t))
         return -1;
     memcpy(out, &t->cfg, sizeof(te_dev_cfg_t));
+    ((te_dev_cfg_t *)out)->slot_head = te_slot_head(&t->cfg);
     if (portlut) {
         for (int p = 0; p < 65536; p++)
             portlut[p] = t->portlut ? t->portlut[p] : (uint16_t)p;
@@ -3436,7 +3461,7 @@ static int packet_via_server(tcpedit_t *t, struct pcap_pkthdr *h, unsigned char 
     uint64_t data = caplen;
     if (c->fixlen == TE_FIXLEN_PAD && h->len > data)
         data = h->len;
-    if (data > 262144u || TE_SLOT_BYTES_OF(8u, data) > (uint32_t)TE_SLOT_BYTES)
+    if (data > 262144u || TE_SLOT_BYTES_OF_H(te_slot_head(c), 8u, data) > (uint32_t)TE_SLOT_BYTES)
         return TE_SRV_DECLINED;
     if (te_upload_cfg(t) < 0)
         return TCPEDIT_ERROR;

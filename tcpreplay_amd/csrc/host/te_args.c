@@ -630,9 +630,14 @@ int te_check_decoder_cfg(tcpedit_t *t, int s2c)
             return -1;
         }
     }
-    if (c->fuzz_seed && (foreign || (c->encoder != TE_ENC_EN10MB && c->encoder != TE_ENC_USER &&
-                                     c->encoder != TE_ENC_HDLC))) {
-        te_seterr(t, "--fuzz-seed with DLT %d input or this encoder is not served by this build", t->dlt);
+    /* --fuzz-seed behind any decoder and into any encoder: a fuzzed record goes back to
+       `again:` and is decoded by the input decoder and encoded a second time (tcpedit.c:89,
+       250-258); the slot headroom holds both encodes (te_slot_head).  Not served: the
+       en10mb encoder's dst_modified carry together with it, whose writers the
+       carry's mark pass finds from the first encode only */
+    if (c->fuzz_seed && c->l2carry) {
+        te_seterr(t, "--fuzz-seed with DLT %d input into --dlt=enet without --enet-dmac is not served by this "
+                     "build", t->dlt);
         return -1;
     }
     return 0;

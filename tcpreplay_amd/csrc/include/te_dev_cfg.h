@@ -102,6 +102,12 @@ typedef struct {
        cidr.c:290-418): device addresses of entries TE_MAX_CIDRMAP.. of cidrmap1, cidrmap2,
        srcipmap and dstipmap (0: none), read through TE_CMAP */
     uint64_t cidr_spill[4];
+    /* bytes of headroom before each record's slot on the generic lane (slot layouts): room
+       for the most the record's L2 header can grow -- a VLAN push, a longer encoder header,
+       twice over for a fuzzed record, which is decoded and encoded again (tcpedit.c:89,
+       250-258) -- a multiple of 16, at least TE_HEAD */
+    uint32_t slot_head;
+    uint32_t pad_;
 } te_dev_cfg_t;
 
 /* entry i of CIDR map w (0 cidrmap1, 1 cidrmap2, 2 srcipmap, 3 dstipmap): the first

@@ -5,6 +5,7 @@
 #ifndef TE_KERNELS_H
 #define TE_KERNELS_H
 
+#include <stddef.h>
 #include <stdint.h>
 #include "te_dev_cfg.h"
 
@@ -17,7 +18,7 @@ extern "C" {
 #ifndef TE_SLOT_BYTES
 #define TE_SLOT_BYTES 36864    /* LDS slot budget per block (3 blocks / CU) */
 #endif
-#define TE_HEAD 16             /* headroom before each record (VLAN push) */
+#define TE_HEAD 16             /* least headroom before each record's slot (te_dev_cfg_t.slot_head) */
 #define TE_TAIL_BYTES 16       /* zeroed bytes after each packet's data */
 #define TE_NO_SCRATCH 0xffffffffffffffffull
 #ifndef TE_FK_TILE_BYTES
@@ -62,8 +63,9 @@ extern "C" {
 #define TE_CONTIG_FITS_IN(g, span, budget) ((uint32_t)(g) + (uint32_t)(span) + 16u <= (uint32_t)(budget))
 #define TE_CONTIG_FITS(g, span) TE_CONTIG_FITS_IN(g, span, TE_SLOT_BYTES)
 
-#define TE_SLOT_BYTES_OF(g, data) \
-    ((((uint32_t)TE_HEAD + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
+#define TE_SLOT_BYTES_OF_H(head, g, data) \
+    ((((uint32_t)(head) + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
+#define TE_SLOT_BYTES_OF(g, data) TE_SLOT_BYTES_OF_H(TE_HEAD, g, data)
 
 /* A tile = a run of consecutive pcap records processed by one block. */
 typedef struct {

@@ -63,6 +63,10 @@ struct Pkt {
     u32 ext;      // bytes from d the reference's buffer holds for this packet (its memcpy, the
                   // encoder's memmove, --fixlen=pad, fuzz writes): te_q8_replay's buffer view
     bool strict;  // te_q8_replay: a fuzz XOR of a byte past `phys` is a stale read too
+    u32 room = 0;  // bytes before the record header (d - 16) that are this lane's: the slot's
+                   // headroom, which an L2 push or a longer replacement header moves into.
+                   // Tracked across every move of the record, so the two encodes of a fuzzed
+                   // record (tcpedit.c:89,250-258) are bounded together, not each on its own
     u8 l2carry = 0;  // the en10mb encoder's dst_modified as the last C2S record left it (Q18)
     // the generic lane's tile (LDS) path: do_checksum leaves the L4 payload sum to the block
     // (all 256 threads sum every record's L4 bytes in 64-byte pieces) and records the job;
@@ -1307,6 +1311,11 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
         u8 *const old_d = pk.d;
         const u32 old_phys = pk.phys;
         if (newl2 > oldl2) {  // push 4 bytes at oldl2
+            if (pk.room < 4) {  // no headroom left: flagged, never written past the slot
+                stale(pk, (int)NEED_NEVER);
+                return RC_ERROR;
+            }
+            pk.room -= 4;
             u8 *src = pk.d - 16, *dst = pk.d - 20;
             for (u32 i = 0; i < 16 + oldl2; ++i) dst[i] = src[i];
             pk.d -= 4;
@@ -1316,6 +1325,7 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
             pk.d += 4;
             pk.avail -= 4;
             pk.phys -= 4;
+            pk.room += 4;
         }
         // the reference's memmove (en10mb.c:568-578) writes its buffer up to pktlen +- 4
         pk.ext = (u32)(pktlen + (int)(newl2 - oldl2));
@@ -1370,12 +1380,13 @@ DI int en10mb_encode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int d
 // Replace a decoded L2 header of s.l2len bytes by n new ones (dlt_user_encode's and
 // dlt_hdlc_encode's memmove, user.c:245-253, hdlc.c:239-247): the payload stays where
 // it is and the record's 16-byte pcap header moves, as the VLAN push/pop does above.
-// A longer header moves into the slot's headroom (TE_HEAD bytes); more than that is
-// flagged unsupported.  The caller writes the n header bytes at the new pk.d.
+// A longer header moves into the slot's headroom (pk.room: what earlier moves of this
+// record -- a first encode before a fuzz step's second one -- left of it); more than that
+// is flagged unsupported.  The caller writes the n header bytes at the new pk.d.
 DI bool l2_replace(Pkt &pk, int l2len, int n) {
     const int delta = l2len - n;
     if (delta == 0) return true;
-    if (-delta > TE_HEAD) {
+    if (-delta > (int)pk.room) {
         stale(pk, (int)NEED_NEVER);  // slot headroom, not stale bytes: not replayed
         return false;
     }
@@ -1389,6 +1400,7 @@ DI bool l2_replace(Pkt &pk, int l2len, int n) {
     pk.d += delta;
     pk.avail -= delta;
     pk.phys -= delta;
+    pk.room = (u32)((int)pk.room + delta);
     pk.ext = (u32)((int)pk.caplen - delta);  // user.c:245-253 / hdlc.c:239-247 memmove extent
     if (pk.strict) {
         pk.phys = old_phys;

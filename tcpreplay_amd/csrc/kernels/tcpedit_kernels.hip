@@ -277,12 +277,12 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
                 if (swp) plen = bswap32(plen);
                 if (plen > data) data = plen;
             }
-            my_slot = TE_SLOT_BYTES_OF((uint32_t)((G0 + my_rel) & 15), data);
+            my_slot = TE_SLOT_BYTES_OF_H(cfg.slot_head, (uint32_t)((G0 + my_rel) & 15), data);
         }
         uint32_t total_slot;
         uint32_t slot_base = LDS_FRONT + block_exscan(my_slot, sh.wsum, total_slot);
         if (tid < (int)npkt) {
-            r0 = slot_base + TE_HEAD + (uint32_t)((G0 + my_rel) & 15);
+            r0 = slot_base + cfg.slot_head + (uint32_t)((G0 + my_rel) & 15);
             slot_end = slot_base + my_slot;
             sh.rpos[tid] = r0;
         }
@@ -378,6 +378,9 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         pk.need = 0;
         pk.ext = caplen;
         pk.strict = false;
+        // the slot's headroom and the record's 16-byte alignment gap (slot layouts); a
+        // contiguous span has no byte before a record that is the record's own
+        pk.room = MODE == MODE_SLOT ? r0 - (slot_end - my_slot) : 0u;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[tile.first_pkt + tid] & 1u) : 0;
         pk.defer = kDefer;
         int rc = RC_OK;
@@ -2060,6 +2063,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         pk.need = 0;
         pk.ext = caplen;
         pk.strict = true;
+        pk.room = Q8_HEAD - 16;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[j] & 1u) : 0;
         bool warned = false;
         const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
@@ -2504,6 +2508,25 @@ extern "C" int te_launch_q8(te_launch_t *L, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the generic lane's instance: fuzzing (FZ), the other decoders/encoders (AD), the layout
+static void launch_generic(bool fz, bool ad, bool slot, int grid, hipStream_t stream, const LaunchArgs &a) {
+#define TE_GL(M, F, D) hipLaunchKernelGGL((te_edit_tiles<M, F, D>), dim3(grid), dim3(BLOCK), 0, stream, a)
+    if (fz && ad) {
+        if (slot) TE_GL(MODE_SLOT, true, true);
+        else TE_GL(MODE_CONTIG, true, true);
+    } else if (fz) {
+        if (slot) TE_GL(MODE_SLOT, true, false);
+        else TE_GL(MODE_CONTIG, true, false);
+    } else if (ad) {
+        if (slot) TE_GL(MODE_SLOT, false, true);
+        else TE_GL(MODE_CONTIG, false, true);
+    } else {
+        if (slot) TE_GL(MODE_SLOT, false, false);
+        else TE_GL(MODE_CONTIG, false, false);
+    }
+#undef TE_GL
+}
+
 extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     fill_args(a, L);
@@ -2597,10 +2620,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         // --fuzz-seed: reach pass, per-record RNG states, then the edit pass below
         if (!L->fuzz_blk || !L->fuzz_words || L->n_pkts == 0) return -1;
         a.fuzz_mode = TE_FUZZ_PROBE;
-        if (L->slot_layout)
-            hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-        else
-            hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
+        launch_generic(true, L->any_dec != 0, L->slot_layout != 0, grid, stream, a);
         const uint32_t nblk = (L->n_pkts + FZ_PER_BLOCK - 1) / FZ_PER_BLOCK;
         hipLaunchKernelGGL(te_fuzz_count, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
                            L->n_pkts, L->fuzz_blk);
@@ -2619,18 +2639,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     if (!fast && l2carry_prepare(L, a, stream) != 0) return -1;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
-    if (a.fuzz_mode != TE_FUZZ_OFF && L->slot_layout)
-        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (a.fuzz_mode != TE_FUZZ_OFF)
-        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (L->any_dec && L->slot_layout)
-        hipLaunchKernelGGL((te_edit_tiles<MODE_SLOT, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (L->any_dec)
-        hipLaunchKernelGGL((te_edit_tiles<MODE_CONTIG, false, true>), dim3(grid), dim3(BLOCK), 0, stream, a);
-    else if (L->slot_layout)
-        hipLaunchKernelGGL(te_edit_tiles<MODE_SLOT>, dim3(grid), dim3(BLOCK), 0, stream, a);
-    else
-        hipLaunchKernelGGL(te_edit_tiles<MODE_CONTIG>, dim3(grid), dim3(BLOCK), 0, stream, a);
+    launch_generic(a.fuzz_mode != TE_FUZZ_OFF, L->any_dec != 0, L->slot_layout != 0, grid, stream, a);
     if (ev && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
     if (!fast && L->l2carry)  // the last record's value, for the next launch (the Q8 replay reads the array)
         hipLaunchKernelGGL(te_l2carry_save, dim3(1), dim3(64), 0, stream, (const unsigned long long *)L->l2carry,

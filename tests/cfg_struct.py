@@ -34,4 +34,5 @@ class DevCfg(ctypes.Structure):
         ("hdlc_address", ctypes.c_uint32), ("hdlc_control", ctypes.c_uint32),
         ("user_l2client", ctypes.c_uint8 * 256), ("user_l2server", ctypes.c_uint8 * 256),
         ("fuzz_seed", ctypes.c_uint32), ("fuzz_factor", ctypes.c_uint32),
-        ("decoder", ctypes.c_int32), ("l2carry", ctypes.c_uint32), ("cidr_spill", ctypes.c_uint64 * 4)]
+        ("decoder", ctypes.c_int32), ("l2carry", ctypes.c_uint32), ("cidr_spill", ctypes.c_uint64 * 4),
+        ("slot_head", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]

@@ -112,8 +112,9 @@ def test_oracle_jnpr_into_ethernet_strips_header_and_tag(built):
 
 
 def test_unserved_combinations_are_refused(built):
+    # (--fuzz-seed with the en10mb encoder's dst_modified carry, SURVEY Q18: no --enet-dmac)
     for dlt, args in [(178, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
-                      (105, ["--fuzz-seed=3"]), (127, ["--fuzz-seed=3", "--dlt=enet"] + MACS)]:
+                      (105, ["--fuzz-seed=3", "--dlt=enet"]), (178, ["--fuzz-seed=3", "--dlt=enet"])]:
         with pytest.raises(Exception):
             TA.TcpEdit(args, dlt=dlt)
 
@@ -128,6 +129,12 @@ ARGSETS = [
     ["--dlt=enet", "--seed=3", "--fixcsum"],  # the decoded addresses (802.11, Juniper's inner frame)
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fixcsum"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
+    # --fuzz-seed behind the decoder: a fuzzed record is decoded and encoded twice
+    # (tcpedit.c:89,250-258)
+    ["--dlt=enet", "--fuzz-seed=3", "--fuzz-factor=2", "--fixcsum"] + MACS,
+    ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fuzz-seed=5",
+     "--fuzz-factor=1"],
+    ["--fuzz-seed=4", "--fuzz-factor=1"],
 ]
 
 
@@ -137,6 +144,11 @@ def _gpu_vs_oracle(pcap, args, dlt, cache=None):
     try:
         rc, out = te.rewrite(pcap, cache)
         assert (rc, out) == (rc_o, exp), args
+    finally:
+        te.close()
+    # a fresh context: --fuzz-seed's RNG state carries from one call to the next (fuzzing.c:8-20)
+    te = TA.TcpEdit(args, dlt=dlt)
+    try:
         rc, out = te.rewrite_pipelined(pcap, cache, chunk_bytes=1 << 16)
         assert (rc, out) == (rc_o, exp), args
     finally:

@@ -615,12 +615,16 @@ def test_dlt_encoders_match_oracle(built, args, linktype):
         te.close()
 
 
-def test_dlt_user_header_past_the_headroom_fails_loudly(built):
-    """A user header more than 16 bytes longer than the decoded one does not fit the
-    slot headroom: the batch fails naming the record instead of guessing."""
-    args = ["--dlt=user", "--user-dlink=" + ",".join(["1"] * 40)]
-    rc, out = gpu_rewrite(S.pcap_fixed(100, 64, seed=3), args)
-    assert rc == TA.TCPEDIT_ERROR
+@pytest.mark.parametrize("n", [40, 200, 255])
+def test_dlt_user_header_longer_than_ethernet(built, n):
+    """A user header up to USER_L2MAXLEN (255) bytes: the slot headroom is sized from the
+    config (te_slot_head), so every length the reference takes is served bit-exact."""
+    args = ["--dlt=user", "--user-dlink=" + ",".join(["1"] * n), "--fixcsum"]
+    pcap = S.build_pcap(S.records(S.pcap_fixed(100, 64, seed=3)) + S.records(S.pcap_imix(300, seed=4)))
+    rc_o, exp = O.rewrite(pcap, args)
+    rc, out = gpu_rewrite(pcap, args)
+    assert rc == rc_o == 0
+    assert_same(out, exp)
 
 
 # ---------------------------------------------------------------- --fuzz-seed (fuzzing.c)
