@@ -303,6 +303,13 @@ tcpedit_replay_t *tcpedit_replay_open(tcpedit_t *tcpedit, const void *pcap, size
 size_t tcpedit_replay_bound(tcpedit_t *tcpedit, tcpedit_replay_t *r);
 int tcpedit_replay_pass(tcpedit_t *tcpedit, tcpedit_replay_t *r, void *out, size_t cap, size_t *out_len);
 void tcpedit_replay_close(tcpedit_replay_t *r);
+/* tcpreplay's per-record steps around the edit, before the first pass (tcpreplay_opts.def):
+ * --include=LIST / --exclude=LIST (send_packets.c:440-447: a listed-out record is neither
+ * edited nor sent), --unique-ip and --unique-ip-loops=N (:477-483: fast_edit_packet after
+ * the edit, in the same pass).  TCPEDIT_OK or TCPEDIT_ERROR (tcpedit_geterr). */
+int tcpedit_replay_parse_args(tcpedit_t *tcpedit, tcpedit_replay_t *r, int argc, char **argv);
+/* records whose --unique-ip edit failed so far (tcpreplay's stats->failed) */
+uint64_t tcpedit_replay_failed(tcpedit_replay_t *r);
 /* new bytes for a batch's records in place (same file and record headers: the index stands) */
 int tcpedit_batch_update_input(tcpedit_t *tcpedit, tcpedit_batch_t *b, const void *img, size_t len);
 /* the records just before the batch's first (whole records ending where it starts: the previous

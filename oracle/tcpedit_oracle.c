@@ -3352,150 +3352,3 @@ uint64_t oracle_shard_cuts(const uint8_t *in, size_t in_len, int parts, uint64_t
 /* tcpreplay-edit -w <file> [--loop=N] [-K] <tcpedit options> <pcap>         */
 /* ------------------------------------------------------------------------- */
 /* Returns 0, -1 (a hard error: *out_len = the output up to it), -2 (bad input/options). */
-/* CPU restatement of tcpreplay-edit's send loop with file output (test infrastructure):
- *   main                tcpreplay.c:79-100: tcpedit_init(sendpacket_get_dlt(intf1)) -- the
- *                       -w dump interface is DLT_EN10MB (sendpacket.c:945-968) --,
- *                       tcpedit_post_args, tcpedit_validate
- *   send_packets        send_packets.c:379-640: per record, tcpedit_packet(ctx, &hdr, &data,
- *                       intf1's direction TCPR_DIR_C2S) (:469-474; -1 ends the run, errx);
- *                       the packet is sent as edited, soft errors included
- *   get_next_packet     send_packets.c:918-990: without -K every pass reads the file through
- *                       libpcap (one reused read buffer, zeroed when first mapped); with -K
- *                       the first pass still edits libpcap's buffer while caching an unedited
- *                       copy of every record (caplen + PACKET_HEADROOM 512 zeroed bytes,
- *                       defines.h.in:184) and its header, and every later pass edits the
- *                       cached bytes IN PLACE with a copy of the cached header: edits
- *                       compound from pass to pass
- *   the -w dump         sendpacket.c:485-486: pcap_dump of the edited header and bytes into
- *                       pcap_open_dead(DLT_EN10MB, MAX_SNAPLEN) (the fraction as libpcap's
- *                       nanosecond read leaves it: x1000 for a microsecond capture)
- * Parity unpinned: the reference holds no tcpreplay-edit output fixture.  Refused here as on
- * the device: --fuzz-seed with -K (fuzz writes land in the cache headroom). */
-int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int preload, int argc, const char **argv,
-                              uint8_t *out, size_t out_cap, size_t *out_len, char *errbuf, int errlen)
-{
-    oopts_t *o = calloc(1, sizeof(oopts_t));
-    ocfg_t c;
-    int rc = 0;
-    size_t op = 24;
-    uint8_t *buf = NULL, **cache = NULL;
-    uint32_t *chdr = NULL;
-    uint64_t nrec = 0;
-    memset(&c, 0, sizeof(c));
-    g_err[0] = 0;
-    c.decoder = DEC_EN10MB;
-    c.in_dlt = 1;
-    if (loops < 1 || in_len < 24 || out_cap < 24) {
-        seterr("bad arguments");
-        rc = -2;
-        goto out;
-    }
-    if (parse_argv(o, argc, argv) < 0 || oracle_post_args(&c, o) < 0) {
-        rc = -2;
-        goto out;
-    }
-    if (c.fuzz_seed && preload) {
-        seterr("--fuzz-seed with --preload-pcap is not served");
-        rc = -2;
-        goto out;
-    }
-    uint32_t magic;
-    memcpy(&magic, in, 4);
-    const int swap = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
-    const int nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
-    if (!swap && !nsec && magic != 0xa1b2c3d4u) {
-        seterr("bad pcap magic");
-        rc = -2;
-        goto out;
-    }
-    {
-        const uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 262144u, 1u};
-        memcpy(out, hdr, 24);
-    }
-    buf = calloc(1, MAXPACKET + 65536); /* libpcap's read buffer (a fresh mapping: zero) */
-    /* the records (libpcap's walk) */
-    for (size_t p = 24; p + 16 <= in_len; nrec++) {
-        uint32_t cl;
-        memcpy(&cl, in + p + 8, 4);
-        if (swap)
-            cl = bswap32_(cl);
-        if (cl > MAX_SNAPLEN || p + 16 + cl > in_len)
-            break;
-        p += 16 + cl;
-    }
-    if (preload) {
-        cache = calloc(nrec ? nrec : 1, sizeof(*cache));
-        chdr = calloc(nrec ? 4 * nrec : 1, sizeof(*chdr));
-    }
-    ostate_t st;
-    memset(&st, 0, sizeof(st));
-    g_fuzz_state = c.fuzz_seed;
-    g_fuzz_draws = 0;
-    g_fuzz_factor = c.fuzz_factor ? c.fuzz_factor : 8;
-    for (int pass = 0; pass < loops && rc == 0; pass++) {
-        size_t p = 24;
-        for (uint64_t i = 0; i < nrec; i++) {
-            uint32_t rh[4];
-            memcpy(rh, in + p, 16);
-            if (swap)
-                for (int q = 0; q < 4; q++)
-                    rh[q] = bswap32_(rh[q]);
-            if (rh[3] > MAX_SNAPLEN) { /* safe_pcap_next's errx (tcpreplay too) */
-                seterr("Frame too big");
-                rc = -1;
-                break;
-            }
-            uint8_t *data;
-            ohdr_t h = {rh[2], rh[3]};
-            if (!preload || pass == 0) {
-                memcpy(buf, in + p + 16, rh[2]);
-                data = buf;
-                if (preload) { /* the unedited copy and header the later passes use */
-                    cache[i] = calloc(1, (size_t)rh[2] + 512 + 4096);
-                    memcpy(cache[i], in + p + 16, rh[2]);
-                    memcpy(chdr + 4 * i, rh, 16);
-                }
-            } else {
-                data = cache[i];
-                h.caplen = chdr[4 * i + 2];
-                h.len = chdr[4 * i + 3];
-            }
-            p += 16 + rh[2];
-            int warned = 0;
-            const int prc = oracle_tcpedit_packet(&c, &st, &h, data, DIR_C2S, &warned);
-            if (prc == TCPEDIT_ERROR) {
-                seterr("Error editing packet #%llu", (unsigned long long)(i + 1));
-                rc = -1;
-                break;
-            }
-            if (preload && pass > 0 && h.caplen > chdr[4 * i + 2] + 512) {
-                seterr("record %llu grows past the preload cache's headroom", (unsigned long long)(i + 1));
-                rc = -2;
-                break;
-            }
-            if (op + 16 + h.caplen > out_cap) {
-                seterr("output buffer too small");
-                rc = -2;
-                break;
-            }
-            const uint32_t f = nsec ? rh[1] : rh[1] * 1000u;
-            const uint32_t orh[4] = {rh[0], f, h.caplen, h.len};
-            memcpy(out + op, orh, 16);
-            memcpy(out + op + 16, data, h.caplen);
-            op += 16 + h.caplen;
-        }
-    }
-    *out_len = op; /* (-1: the records sent before the error) */
-out:
-    if (errbuf && errlen > 0)
-        snprintf(errbuf, (size_t)errlen, "%s", g_err);
-    if (cache)
-        for (uint64_t i = 0; i < nrec; i++)
-            free(cache[i]);
-    free(cache);
-    free(chdr);
-    free(buf);
-    free_cfg(&c);
-    free(o);
-    return rc;
-}

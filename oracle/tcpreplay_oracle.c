@@ -76,11 +76,98 @@ static int tro_fast_edit(uint8_t *pkt, uint32_t caplen, uint64_t iteration, int 
     return 0;
 }
 
+/* the --include / --exclude packet list (tcpreplay_opts.def:305-360):
+ *   parse_list  src/common/list.c:61-130 -- ',' tokens (strtok_r: empty ones vanish), each
+ *               matching "^[0-9]+(-([0-9]+|\s*))?$"; add_to_list (:36-50): min by
+ *               strtoull(.., 0), max = min without '-', 0 for "N-" (open), else strtoull
+ *   check_list  src/common/list.c:139-156 -- min and max set: min <= v <= max; min 0:
+ *               v <= max; max 0: v >= min
+ * A list that does not parse is the reference's errx ("Unable to parse include/exclude
+ * rule"): -1 here. */
+typedef struct {
+    uint64_t min[4096], max[4096];
+    int n;
+} tro_list_t;
+
+static int tro_list_parse(tro_list_t *l, const char *arg)
+{
+    char buf[16384];
+    if (!arg || strlen(arg) >= sizeof buf)
+        return -1;
+    strcpy(buf, arg);
+    l->n = 0;
+    char *tok = NULL;
+    for (char *e = strtok_r(buf, ",", &tok); e; e = strtok_r(NULL, ",", &tok)) {
+        char *p = e, *second = NULL;
+        if (!isdigit((unsigned char)*p))
+            return -1;
+        while (isdigit((unsigned char)*p))
+            p++;
+        if (*p == '-') {
+            *p++ = 0;
+            second = p;
+            if (isdigit((unsigned char)*p))
+                while (isdigit((unsigned char)*p))
+                    p++;
+            else
+                while (*p == ' ' || (*p >= '\t' && *p <= '\r'))
+                    p++;
+        }
+        if (*p || l->n >= 4096)
+            return -1;
+        l->min[l->n] = strtoull(e, NULL, 0);
+        l->max[l->n] = second ? (second[0] ? strtoull(second, NULL, 0) : 0) : l->min[l->n];
+        l->n++;
+    }
+    return l->n ? 0 : -1;
+}
+
+static int tro_list_check(const tro_list_t *l, uint64_t v)
+{
+    for (int i = 0; i < l->n; i++) {
+        const uint64_t mn = l->min[i], mx = l->max[i];
+        if (mn != 0 && mx != 0) {
+            if (v >= mn && v <= mx)
+                return 1;
+        } else if (mn == 0) {
+            if (v <= mx)
+                return 1;
+        } else if (mx == 0) {
+            if (v >= mn)
+                return 1;
+        }
+    }
+    return 0;
+}
+
+/* send_packets.c:440-447: a record the list leaves out is skipped before anything else
+   (no edit, not sent, not counted) */
+static int tro_listed_out(const tro_list_t *l, int exclude, uint64_t packetnum)
+{
+    if (!l)
+        return 0;
+    const int rule_set = tro_list_check(l, packetnum);
+    return (rule_set && exclude) || (!rule_set && !exclude);
+}
+
 /* returns the output length, or -1 bad options, -2 not a pcap, -3 out too small */
+long tcpreplay_oracle_run_list(const uint8_t *pcap, size_t len, int loops, int unique_ip, double unique_loops,
+                               int preload, const char *list, int exclude, uint8_t *out, size_t cap,
+                               uint64_t *failed);
 long tcpreplay_oracle_run(const uint8_t *pcap, size_t len, int loops, int unique_ip, double unique_loops,
                           int preload, uint8_t *out, size_t cap, uint64_t *failed)
 {
+    return tcpreplay_oracle_run_list(pcap, len, loops, unique_ip, unique_loops, preload, NULL, 0, out, cap, failed);
+}
+
+long tcpreplay_oracle_run_list(const uint8_t *pcap, size_t len, int loops, int unique_ip, double unique_loops,
+                               int preload, const char *list, int exclude, uint8_t *out, size_t cap,
+                               uint64_t *failed)
+{
+    static tro_list_t lst;
     if (loops < 1 || (unique_ip && unique_loops < 1.0))
+        return -1;
+    if (list && tro_list_parse(&lst, list) < 0)
         return -1;
     if (len < 24)
         return -2;
@@ -112,6 +199,7 @@ long tcpreplay_oracle_run(const uint8_t *pcap, size_t len, int loops, int unique
     uint64_t iteration = 0, uniq = 0, last_uniq = 0;
     *failed = 0;
     for (int pass = 0; pass < loops; pass++) {
+        uint64_t packetnum = 0;
         for (size_t off = 24; off + 16 <= len;) {
             const uint32_t ts = tpo_rd32(pcap + off, sw), frac = tpo_rd32(pcap + off + 4, sw);
             const uint32_t caplen = tpo_rd32(pcap + off + 8, sw), plen = tpo_rd32(pcap + off + 12, sw);
@@ -121,6 +209,8 @@ long tcpreplay_oracle_run(const uint8_t *pcap, size_t len, int loops, int unique
             if (!preload)
                 memcpy(pkt, pcap + off + 16, caplen);
             off += 16 + caplen;
+            if (tro_listed_out(list ? &lst : NULL, exclude, ++packetnum))
+                continue;
             if (unique_ip && uniq && uniq > last_uniq && tro_fast_edit(data, caplen, uniq - 1, preload) == -1) {
                 ++*failed;
                 continue;
@@ -144,3 +234,209 @@ long tcpreplay_oracle_run(const uint8_t *pcap, size_t len, int loops, int unique
     free(cache);
     return (long)o;
 }
+
+static uint64_t g_replay_failed;
+
+/* CPU restatement of tcpreplay-edit's send loop with file output (test infrastructure):
+ *   main                tcpreplay.c:79-100: tcpedit_init(sendpacket_get_dlt(intf1)) -- the
+ *                       -w dump interface is DLT_EN10MB (sendpacket.c:945-968) --,
+ *                       tcpedit_post_args, tcpedit_validate
+ *   send_packets        send_packets.c:379-640: per record, tcpedit_packet(ctx, &hdr, &data,
+ *                       intf1's direction TCPR_DIR_C2S) (:469-474; -1 ends the run, errx);
+ *                       the packet is sent as edited, soft errors included
+ *   get_next_packet     send_packets.c:918-990: without -K every pass reads the file through
+ *                       libpcap (one reused read buffer, zeroed when first mapped); with -K
+ *                       the first pass still edits libpcap's buffer while caching an unedited
+ *                       copy of every record (caplen + PACKET_HEADROOM 512 zeroed bytes,
+ *                       defines.h.in:184) and its header, and every later pass edits the
+ *                       cached bytes IN PLACE with a copy of the cached header: edits
+ *                       compound from pass to pass
+ *   the -w dump         sendpacket.c:485-486: pcap_dump of the edited header and bytes into
+ *                       pcap_open_dead(DLT_EN10MB, MAX_SNAPLEN) (the fraction as libpcap's
+ *                       nanosecond read leaves it: x1000 for a microsecond capture)
+ * Parity unpinned: the reference holds no tcpreplay-edit output fixture.  Refused here as on
+ * the device: --fuzz-seed with -K (fuzz writes land in the cache headroom). */
+int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int preload, int argc, const char **argv,
+                              uint8_t *out, size_t out_cap, size_t *out_len, char *errbuf, int errlen)
+{
+    oopts_t *o = calloc(1, sizeof(oopts_t));
+    ocfg_t c;
+    int rc = 0;
+    size_t op = 24;
+    uint8_t *buf = NULL, **cache = NULL;
+    uint32_t *chdr = NULL;
+    uint64_t nrec = 0;
+    memset(&c, 0, sizeof(c));
+    g_err[0] = 0;
+    /* tcpreplay's own options on this path; the rest are tcpedit's */
+    static tro_list_t lst;
+    const char *list = NULL;
+    int exclude = 0, unique_ip = 0;
+    double unique_loops = 1.0;
+    const char **targv = calloc((size_t)argc + 1, sizeof(*targv));
+    int targc = 0;
+    for (int i = 0; i < argc; i++) {
+        const char *a = argv[i];
+        if (!strncmp(a, "--include=", 10) || !strncmp(a, "--exclude=", 10)) {
+            if (list) { /* flags-cant: include and exclude exclude each other (max 1) */
+                seterr("--include and --exclude: only one list");
+                rc = -2;
+                goto out;
+            }
+            exclude = a[2] == 'e';
+            list = a + 10;
+        } else if (!strcmp(a, "--unique-ip")) {
+            unique_ip = 1;
+        } else if (!strncmp(a, "--unique-ip-loops=", 18)) {
+            unique_loops = atof(a + 18);
+        } else {
+            targv[targc++] = a;
+        }
+    }
+    if (list && tro_list_parse(&lst, list) < 0) {
+        seterr("Unable to parse include/exclude rule: %s", list);
+        rc = -2;
+        goto out;
+    }
+    if (unique_ip && unique_loops < 1.0) {
+        seterr("--unique-ip-loops requires loop count >= 1.0");
+        rc = -2;
+        goto out;
+    }
+    uint64_t iteration = 0, uniq = 0, last_uniq = 0, nfailed = 0;
+    c.decoder = DEC_EN10MB;
+    c.in_dlt = 1;
+    if (loops < 1 || in_len < 24 || out_cap < 24) {
+        seterr("bad arguments");
+        rc = -2;
+        goto out;
+    }
+    if (parse_argv(o, targc, targv) < 0 || oracle_post_args(&c, o) < 0) {
+        rc = -2;
+        goto out;
+    }
+    if (c.fuzz_seed && preload) {
+        seterr("--fuzz-seed with --preload-pcap is not served");
+        rc = -2;
+        goto out;
+    }
+    uint32_t magic;
+    memcpy(&magic, in, 4);
+    const int swap = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
+    const int nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
+    if (!swap && !nsec && magic != 0xa1b2c3d4u) {
+        seterr("bad pcap magic");
+        rc = -2;
+        goto out;
+    }
+    {
+        const uint32_t hdr[6] = {0xa1b2c3d4u, 0x00040002u, 0, 0, 262144u, 1u};
+        memcpy(out, hdr, 24);
+    }
+    buf = calloc(1, MAXPACKET + 65536); /* libpcap's read buffer (a fresh mapping: zero) */
+    /* the records (libpcap's walk) */
+    for (size_t p = 24; p + 16 <= in_len; nrec++) {
+        uint32_t cl;
+        memcpy(&cl, in + p + 8, 4);
+        if (swap)
+            cl = bswap32_(cl);
+        if (cl > MAX_SNAPLEN || p + 16 + cl > in_len)
+            break;
+        p += 16 + cl;
+    }
+    if (preload) {
+        cache = calloc(nrec ? nrec : 1, sizeof(*cache));
+        chdr = calloc(nrec ? 4 * nrec : 1, sizeof(*chdr));
+    }
+    ostate_t st;
+    memset(&st, 0, sizeof(st));
+    g_fuzz_state = c.fuzz_seed;
+    g_fuzz_draws = 0;
+    g_fuzz_factor = c.fuzz_factor ? c.fuzz_factor : 8;
+    for (int pass = 0; pass < loops && rc == 0; pass++) {
+        size_t p = 24;
+        for (uint64_t i = 0; i < nrec; i++) {
+            const int listed_out = tro_listed_out(list ? &lst : NULL, exclude, i + 1); /* :440-447 */
+            uint32_t rh[4];
+            memcpy(rh, in + p, 16);
+            if (swap)
+                for (int q = 0; q < 4; q++)
+                    rh[q] = bswap32_(rh[q]);
+            if (rh[3] > MAX_SNAPLEN) { /* safe_pcap_next's errx (tcpreplay too) */
+                seterr("Frame too big");
+                rc = -1;
+                break;
+            }
+            uint8_t *data;
+            ohdr_t h = {rh[2], rh[3]};
+            if (!preload || pass == 0) {
+                memcpy(buf, in + p + 16, rh[2]);
+                data = buf;
+                if (preload) { /* the unedited copy and header the later passes use */
+                    cache[i] = calloc(1, (size_t)rh[2] + 512 + 4096);
+                    memcpy(cache[i], in + p + 16, rh[2]);
+                    memcpy(chdr + 4 * i, rh, 16);
+                }
+            } else {
+                data = cache[i];
+                h.caplen = chdr[4 * i + 2];
+                h.len = chdr[4 * i + 3];
+            }
+            p += 16 + rh[2];
+            if (listed_out)
+                continue; /* read (and cached under -K), not edited, not sent */
+            int warned = 0;
+            const int prc = oracle_tcpedit_packet(&c, &st, &h, data, DIR_C2S, &warned);
+            if (prc == TCPEDIT_ERROR) {
+                seterr("Error editing packet #%llu", (unsigned long long)(i + 1));
+                rc = -1;
+                break;
+            }
+            if (preload && pass > 0 && h.caplen > chdr[4 * i + 2] + 512) {
+                seterr("record %llu grows past the preload cache's headroom", (unsigned long long)(i + 1));
+                rc = -2;
+                break;
+            }
+            /* --unique-ip (:477-483): fast_edit_packet of the edited packet, with the header
+               as read; a record it fails is counted and not sent */
+            if (unique_ip && uniq && uniq > last_uniq &&
+                tro_fast_edit(data, rh[2], uniq - 1, preload && pass > 0) == -1) {
+                ++nfailed;
+                continue;
+            }
+            if (op + 16 + h.caplen > out_cap) {
+                seterr("output buffer too small");
+                rc = -2;
+                break;
+            }
+            const uint32_t f = nsec ? rh[1] : rh[1] * 1000u;
+            const uint32_t orh[4] = {rh[0], f, h.caplen, h.len};
+            memcpy(out + op, orh, 16);
+            memcpy(out + op + 16, data, h.caplen);
+            op += 16 + h.caplen;
+        }
+        /* increment_iteration (send_packets.c:362-372) */
+        last_uniq = uniq;
+        ++iteration;
+        if (unique_ip)
+            uniq = (iteration * 1000) / (uint64_t)(unique_loops * 1000.0) + 1;
+    }
+    g_replay_failed = nfailed;
+    *out_len = op; /* (-1: the records sent before the error) */
+out:
+    if (errbuf && errlen > 0)
+        snprintf(errbuf, (size_t)errlen, "%s", g_err);
+    if (cache)
+        for (uint64_t i = 0; i < nrec; i++)
+            free(cache[i]);
+    free(cache);
+    free(chdr);
+    free(buf);
+    free_cfg(&c);
+    free(o);
+    free(targv);
+    return rc;
+}
+
+/* records whose --unique-ip edit failed in the last tcpreplay_edit_oracle_run */
+uint64_t tcpreplay_edit_oracle_failed(void) { return g_replay_failed; }

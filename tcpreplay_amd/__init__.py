@@ -103,6 +103,8 @@ def load():
         "tcpedit_replay_bound": (sz, [vp, vp]),
         "tcpedit_replay_pass": (c_int, [vp, vp, vp, sz, ctypes.POINTER(sz)]),
         "tcpedit_replay_close": (None, [vp]),
+        "tcpedit_replay_parse_args": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_char_p)]),
+        "tcpedit_replay_failed": (ctypes.c_uint64, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -261,14 +263,27 @@ class Replay:
     (16-byte headers with nanosecond fractions, no file header).  With preload (-K) the
     passes after the first edit the cached copy in place, so edits compound."""
 
-    def __init__(self, te: TcpEdit, pcap, preload=False):
+    def __init__(self, te: TcpEdit, pcap, preload=False, replay_args=()):
+        """replay_args: tcpreplay's own options on this path (--include=LIST, --exclude=LIST,
+        --unique-ip, --unique-ip-loops=N; tcpedit_replay_parse_args)"""
         self._te, self._L = te, te._L
         keep, p, n = _buf(pcap)
         self._r = self._L.tcpedit_replay_open(te._ctx, p, n, 1 if preload else 0)
         del keep
         if not self._r:
             raise RuntimeError(te.geterr())
+        if replay_args:
+            argv = (ctypes.c_char_p * len(replay_args))(*[a.encode() for a in replay_args])
+            if self._L.tcpedit_replay_parse_args(te._ctx, self._r, len(replay_args), argv) != 0:
+                err = te.geterr()
+                self.close()
+                raise ValueError(err)
         self._cap = self._L.tcpedit_replay_bound(te._ctx, self._r)
+
+    @property
+    def failed(self):
+        """records whose --unique-ip edit failed so far (not sent)"""
+        return int(self._L.tcpedit_replay_failed(self._r))
 
     def pass_(self):
         """one --loop pass: (rc, records as sent); rc < 0 ends the run (errx), the
@@ -294,12 +309,22 @@ class Replay:
 REPLAY_DUMP_HEADER = struct.pack("<IHHiIII", 0xa1b2c3d4, 2, 4, 0, 0, 262144, 1)
 
 
+REPLAY_OPTS = ("--include=", "--exclude=", "--unique-ip-loops=")
+
+
+def split_replay_args(args):
+    """tcpreplay's own options on the tcpreplay-edit path, and the tcpedit options"""
+    mine = [a for a in args if a == "--unique-ip" or a.startswith(REPLAY_OPTS)]
+    return mine, [a for a in args if a not in mine]
+
+
 def replay_edit(pcap, args, loops=1, preload=False, errors=None):
     """`tcpreplay-edit -w out --loop=loops [-K] <args> in.pcap`: (rc, the -w file's bytes);
     a failing pass's error string is appended to `errors` (a list) when given"""
-    te = TcpEdit(args)
+    rargs, eargs = split_replay_args(args)
+    te = TcpEdit(eargs)
     try:
-        r = Replay(te, pcap, preload)
+        r = Replay(te, pcap, preload, rargs)
         try:
             out, rc = [REPLAY_DUMP_HEADER], 0
             for p in range(int(loops)):

@@ -1812,6 +1812,19 @@ size_t tcpedit_batch_output_records(tcpedit_batch_t *b, void *dst, size_t cap)
 }
 
 const void *tcpedit_batch_device_output(tcpedit_batch_t *b) { return b ? b->d_out : NULL; }
+
+/* a direction array already on the device (te_replay.c: the --include/--exclude list as a
+   tcpprep cache body), in place of the batch's; the batch owns d_bits from here on */
+int te_batch_set_dirbits_dev(tcpedit_batch_t *b, uint8_t *d_bits, uint64_t len)
+{
+    if (!b)
+        return -1;
+    hipFree(b->d_dirbits);
+    b->d_dirbits = d_bits;
+    b->dirbits_len = len;
+    b->status_valid = 0;
+    return 0;
+}
 uint64_t tcpedit_batch_input_bytes(tcpedit_batch_t *b) { return b ? b->in_len : 0; }
 
 /* The record index built on the device (te_index.hip) from the batch's device image,

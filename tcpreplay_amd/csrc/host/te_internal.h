@@ -101,6 +101,7 @@ int te_decoder_of(int dlt);
 int te_default_encoder(int dec);
 int te_decoder_l2len(int dec);
 uint32_t te_slot_head(const te_dev_cfg_t *c);
+int te_batch_set_dirbits_dev(tcpedit_batch_t *b, uint8_t *d_bits, uint64_t len);
 int te_check_decoder_cfg(tcpedit_t *t, int s2c);
 void te_sync_pub(tcpedit_t *t);   /* mirror the derived values into the reference-layout head */
 int te_autoopts_import(tcpedit_t *t); /* 1 imported, 0 no descriptor, -1 error (te_autoopts.c) */

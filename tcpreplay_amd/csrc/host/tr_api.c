@@ -8,6 +8,7 @@
  * pass runs on the device (tcpreplay_kernels.hip) and lands in one device output buffer.
  */
 #include <hip/hip_runtime_api.h>
+#include <ctype.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,8 +21,65 @@ struct tcpreplay_hip_s {
     uint32_t loops;
     int unique_ip, preload;
     double unique_loops;
+    tr_list_t list;     /* --include / --exclude (n = 0: none) */
     char err[512];
 };
+
+/* parse_list (src/common/list.c:61-130): ',' tokens (strtok_r drops empty ones), each
+   "^[0-9]+(-([0-9]+|\s*))?$"; add_to_list (:36-50) takes min by strtoull(.., 0), max = min
+   without a '-', 0 for an open "N-" */
+int tr_list_parse(tr_list_t *l, const char *arg, int exclude, char *err, size_t errlen)
+{
+    tr_list_free(l);
+    l->exclude = exclude;
+    char *buf = arg ? strdup(arg) : NULL;
+    uint32_t cap = 0;
+    int ok = buf != NULL;
+    char *tok = NULL;
+    for (char *e = ok ? strtok_r(buf, ",", &tok) : NULL; e && ok; e = strtok_r(NULL, ",", &tok)) {
+        char *p = e, *second = NULL;
+        ok = isdigit((unsigned char)*p) != 0;
+        while (isdigit((unsigned char)*p))
+            p++;
+        if (ok && *p == '-') {
+            *p++ = 0;
+            second = p;
+            if (isdigit((unsigned char)*p))
+                while (isdigit((unsigned char)*p))
+                    p++;
+            else
+                while (isspace((unsigned char)*p))
+                    p++;
+        }
+        ok = ok && !*p;
+        if (ok && l->n == cap) {
+            cap = cap ? 2 * cap : 16;
+            uint64_t *g = realloc(l->rng, 2 * sizeof(uint64_t) * cap);
+            ok = g != NULL;
+            if (g)
+                l->rng = g;
+        }
+        if (ok) {
+            l->rng[2 * l->n] = strtoull(e, NULL, 0);
+            l->rng[2 * l->n + 1] = second ? (second[0] ? strtoull(second, NULL, 0) : 0) : l->rng[2 * l->n];
+            l->n++;
+        }
+    }
+    free(buf);
+    if (!ok || !l->n) {
+        snprintf(err, errlen, "Unable to parse include/exclude rule: %s", arg ? arg : "(null)");
+        tr_list_free(l);
+        return -1;
+    }
+    return 0;
+}
+
+void tr_list_free(tr_list_t *l)
+{
+    free(l->rng);
+    l->rng = NULL;
+    l->n = 0;
+}
 
 static int tr_err(tcpreplay_hip_t *t, const char *fmt, ...)
 {
@@ -42,7 +100,12 @@ tcpreplay_hip_t *tcpreplay_hip_init(void)
     return t;
 }
 
-void tcpreplay_hip_close(tcpreplay_hip_t *t) { free(t); }
+void tcpreplay_hip_close(tcpreplay_hip_t *t)
+{
+    if (t)
+        tr_list_free(&t->list);
+    free(t);
+}
 
 const char *tcpreplay_hip_geterr(tcpreplay_hip_t *t) { return t ? t->err : "no context"; }
 
@@ -106,6 +169,14 @@ int tcpreplay_hip_parse_args(tcpreplay_hip_t *t, int argc, char **argv)
             uloops_seen = 1;
         } else if (OPT("--preload-pcap") || OPT("-K")) {
             t->preload = 1;
+        } else if (OPT("--include") || OPT("--exclude")) {
+            /* tcpreplay_opts.def:305-360 (max 1, flags-cant each other) */
+            if (!v)
+                return tr_err(t, "%.*s needs a value", (int)nl, a);
+            if (t->list.n)
+                return tr_err(t, "--include and --exclude: one packet list at most");
+            if (tr_list_parse(&t->list, v, a[2] == 'e', t->err, sizeof t->err) < 0)
+                return -1;
         } else {
             return tr_err(t, "unknown or unserved tcpreplay option %s", a);
         }
@@ -182,7 +253,8 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
     if (!off)
         return tr_err(t, "out of host memory (record index)");
     uint8_t *d_img = NULL, *d_cache = NULL, *d_out = NULL;
-    uint64_t *d_off = NULL, *d_size = NULL, *d_pos = NULL;
+    uint64_t *d_off = NULL, *d_size = NULL, *d_pos = NULL, *d_list = NULL;
+    uint64_t *d_nfail = NULL;
     void *d_patch = NULL, *d_temp = NULL, *d_tot = NULL;
     hipStream_t st = NULL;
     int64_t rc = -1;
@@ -197,6 +269,12 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
     CHK(hipMalloc(&d_temp, temp ? temp : 16));
     if (t->preload)
         CHK(hipMalloc((void **)&d_cache, len));
+    CHK(hipMalloc((void **)&d_nfail, 8));
+    CHK(hipMemsetAsync(d_nfail, 0, 8, st));
+    if (t->list.n) {
+        CHK(hipMalloc((void **)&d_list, 16 * (size_t)t->list.n));
+        CHK(hipMemcpyAsync(d_list, t->list.rng, 16 * (size_t)t->list.n, hipMemcpyHostToDevice, st));
+    }
     CHK(hipMemcpyAsync(d_img, pcap, len, hipMemcpyHostToDevice, st));
     if (d_cache)
         CHK(hipMemcpyAsync(d_cache, pcap, len, hipMemcpyHostToDevice, st));
@@ -212,6 +290,11 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
         memset(&p, 0, sizeof p);
         p.img = d_img;
         p.cache = d_cache;
+        p.cached = d_cache != NULL;
+        p.list = d_list;
+        p.nlist = t->list.n;
+        p.exclude = t->list.exclude;
+        p.nfail = d_nfail;
         p.off = d_off;
         p.n = n;
         p.swapped = sw;
@@ -231,20 +314,6 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
         CHK(hipMemcpyAsync(&last[1], d_size + n - 1, 8, hipMemcpyDeviceToHost, st));
         CHK(hipStreamSynchronize(st));
         const uint64_t pass_bytes = last[0] + last[1];
-        if (p.edit) { /* the failed records: the pass's records minus the written ones */
-            uint64_t w = 0;
-            /* count the written records: sizes are 0 exactly for the failed ones */
-            uint64_t *hs = malloc(n * 8);
-            if (!hs) {
-                tr_err(t, "out of host memory");
-                goto fail;
-            }
-            CHK(hipMemcpy(hs, d_size, n * 8, hipMemcpyDeviceToHost));
-            for (uint64_t j = 0; j < n; j++)
-                w += hs[j] != 0;
-            free(hs);
-            fails += n - w;
-        }
         o += pass_bytes;
         /* increment_iteration (send_packets.c:362-372) */
         last_uniq = uniq;
@@ -253,7 +322,12 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
             uniq = (iteration * 1000) / (uint64_t)(t->unique_loops * 1000.0) + 1;
     }
     CHK(hipMemcpyAsync(out + 24, d_out + 24, o - 24, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
+    {
+        uint64_t nf = 0; /* the records whose unique-ip edit failed, over every pass */
+        CHK(hipMemcpyAsync(&nf, d_nfail, 8, hipMemcpyDeviceToHost, st));
+        CHK(hipStreamSynchronize(st));
+        fails = nf;
+    }
     *failed = fails;
     rc = (int64_t)o;
 fail:
@@ -266,6 +340,8 @@ fail:
     hipFree(d_patch);
     hipFree(d_temp);
     hipFree(d_tot);
+    hipFree(d_list);
+    hipFree(d_nfail);
     if (st)
         hipStreamDestroy(st);
     free(off);

@@ -73,6 +73,17 @@ __device__ int fast_edit(const u8 *pkt, u32 caplen, uint64_t iteration, bool cac
     return 0;
 }
 
+// check_list (src/common/list.c:139-156) and send_packets.c:440-447's rule: true when the
+// include / exclude list leaves packet `v` (1-based within the pass) out
+__device__ __forceinline__ bool listed_out(const uint64_t *l, uint32_t n, bool exclude, uint64_t v) {
+    bool set = false;
+    for (uint32_t i = 0; i < n && !set; ++i) {
+        const uint64_t mn = l[2 * i], mx = l[2 * i + 1];
+        set = (mn != 0 && mx != 0) ? (v >= mn && v <= mx) : (mn == 0 ? v <= mx : v >= mn);
+    }
+    return set == exclude;
+}
+
 __global__ __launch_bounds__(256) void tr_mark(TrPass a) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n) return;
@@ -80,9 +91,12 @@ __global__ __launch_bounds__(256) void tr_mark(TrPass a) {
     const u8 *rec = (a.cache ? a.cache : a.img) + off;
     const u32 caplen = rd32(rec + 8, a.swapped != 0);
     u32 keep = 1, at_s = 0, src = 0, dst = 0, at_d = 0;
-    if (a.edit) {
-        if (fast_edit(rec + 16, caplen, a.iteration, a.cache != nullptr, src, dst, at_s, at_d) < 0) {
+    if (a.list && listed_out(a.list, a.nlist, a.exclude != 0, j + 1)) {
+        keep = 0;  // skipped before anything else: not edited, not sent, not counted failed
+    } else if (a.edit) {
+        if (fast_edit(rec + 16, caplen, a.iteration, a.cached != 0, src, dst, at_s, at_d) < 0) {
             keep = 0;
+            if (a.nfail) atomicAdd((unsigned long long *)a.nfail, 1ull);
         } else if (a.cache) {  // -K: the cached record itself (the next pass starts from it)
             u8 *p = a.cache + off + 16;
             for (int k = 0; k < 4; ++k) {
@@ -120,7 +134,30 @@ __global__ __launch_bounds__(256) void tr_write(TrPass a) {
         o[16 + i] = b;
     }
 }
+
+// one thread per cache byte (4 records): 11 (send, C2S) unless the list leaves it out (00)
+__global__ __launch_bounds__(256) void tr_dirbits(const uint64_t *l, uint32_t nl, int32_t exclude, uint64_t n,
+                                                  u8 *bits) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= (n + 3) / 4) return;
+    u32 v = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t j = 4 * b + k;
+        if (j < n && !listed_out(l, nl, exclude != 0, j + 1)) v |= 3u << (2 * k);
+    }
+    bits[b] = (u8)v;
+}
 }  // namespace
+
+extern "C" int tr_list_dirbits(const uint64_t *d_list, uint32_t nlist, int exclude, uint64_t n, uint8_t *d_bits,
+                               void *stream) {
+    if (n == 0) return 0;
+    const uint64_t nb = (n + 3) / 4;
+    if (nb > 0xffffffffull * 256) return -1;
+    hipLaunchKernelGGL(tr_dirbits, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_list,
+                       nlist, exclude, n, d_bits);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" size_t tr_scan_temp_bytes(uint64_t n) {
     size_t t = 0;
@@ -135,6 +172,7 @@ extern "C" int tr_launch_pass(const TrPass *p, void *temp, size_t temp_bytes, vo
     if (p->n > 0x7fffffffull) return -1;
     TrPass a = *p;
     hipLaunchKernelGGL(tr_mark, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
+    if (a.mark_only) return hipGetLastError() == hipSuccess ? 0 : -1;
     size_t tb = temp_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(temp, tb, (const unsigned long long *)a.size, (unsigned long long *)a.pos,
                                          (int)a.n, st) != hipSuccess)

@@ -101,10 +101,11 @@ def tcpprep(pcap: bytes, args, pkt_base: int = 0, with_entries=False):
     return out.raw[:n]
 
 
-def replay_args(args):
+def replay_args(args, with_list=False):
     """tcpreplay's options this path serves (tcpreplay_opts.def): --loop, --unique-ip,
-    --unique-ip-loops, --preload-pcap / -K -> (loops, unique_ip, unique_loops, preload)"""
-    loops, uniq, uloops, preload = 1, 0, 1.0, 0
+    --unique-ip-loops, --preload-pcap / -K, --include / --exclude -> (loops, unique_ip,
+    unique_loops, preload[, list, exclude])"""
+    loops, uniq, uloops, preload, lst, excl = 1, 0, 1.0, 0, None, 0
     for a in args:
         k, _, v = a.partition("=")
         if k in ("--loop", "-l"):
@@ -115,24 +116,29 @@ def replay_args(args):
             uloops = float(v)
         elif k in ("--preload-pcap", "-K"):
             preload = 1
+        elif k in ("--include", "--exclude"):
+            if lst is not None:
+                raise ValueError("--include and --exclude: one list")
+            lst, excl = v, int(k == "--exclude")
         else:
             raise ValueError(f"unknown tcpreplay option {a}")
-    return loops, uniq, uloops, preload
+    return (loops, uniq, uloops, preload, lst, excl) if with_list else (loops, uniq, uloops, preload)
 
 
 def replay(pcap: bytes, args):
     """tcpreplay_oracle_run: `tcpreplay -w out <args> <pcap>` as the CPU restatement writes
     it -> (output file bytes, records whose unique-ip edit failed)"""
     lib = load()
-    fn = lib.tcpreplay_oracle_run
+    fn = lib.tcpreplay_oracle_run_list
     fn.restype = ctypes.c_long
     fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
-                   ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]
-    loops, uniq, uloops, preload = replay_args(args)
+                   ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]
+    loops, uniq, uloops, preload, lst, excl = replay_args(args, with_list=True)
     cap = 24 + loops * max(len(pcap) - 24, 0) + 64
     out = ctypes.create_string_buffer(cap)
     failed = ctypes.c_uint64()
-    n = fn(pcap, len(pcap), loops, uniq, uloops, preload, out, cap, ctypes.byref(failed))
+    n = fn(pcap, len(pcap), loops, uniq, uloops, preload, lst.encode() if lst is not None else None, excl, out, cap,
+           ctypes.byref(failed))
     if n < 0:
         raise ValueError(f"tcpreplay oracle failed ({n}) for {args}")
     return out.raw[:n], int(failed.value)
@@ -159,6 +165,13 @@ def replay_edit(pcap: bytes, args, loops=1, preload=False):
     if rc == -2:
         raise ValueError("oracle rejected input/options: " + err.value.decode(errors="replace"))
     return rc, out.raw[:out_len.value]
+
+
+def replay_edit_failed() -> int:
+    """records whose --unique-ip edit failed in the last replay_edit (stats->failed)"""
+    fn = load().tcpreplay_edit_oracle_failed
+    fn.restype = ctypes.c_uint64
+    return int(fn())
 
 
 def check_rewrite(pcap, args, cache, dev_out, threads=16, sharded=True, pkt_base=0):

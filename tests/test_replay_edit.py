@@ -28,11 +28,18 @@ ABI_DIR = os.path.join(ROOT, "tests", "abi")
 ABI_BIN = os.path.join(ABI_DIR, "_build", "tcpreplay_edit_abi")
 
 # tcprewrite-only options (not tcpedit's): cases using them have no tcpreplay-edit analogue
-_TCPREWRITE_ONLY = ("--skip-soft-errors", "--dlt=", "--fuzz-seed")
+# (--fuzz-seed is tcpedit's, tcpreplay_opts.def:572: its passes are below)
+_TCPREWRITE_ONLY = ("--skip-soft-errors", "--dlt=")
 
 
 def _edit_cases():
     return [c for c in G.IN_SCOPE if not c[2] and not any(a.startswith(_TCPREWRITE_ONLY) for a in c[3])]
+
+
+# the reference's tcpreplay goldens of the per-pass packet list (test/Makefile.am:214-215):
+# tcpreplay-edit with no tcpedit option writes what tcpreplay writes
+LIST_GOLDENS = [("test2.replay_include", ["--include=7,11,20-23,174-"]),
+                ("test2.replay_exclude", ["--exclude=23-,11-20,2,3"])]
 
 
 def _recs(dump: bytes):
@@ -64,7 +71,7 @@ def test_one_pass_edits_as_tcprewrite_does(case):
     assert rc == 0
     assert dump[:24] == TA.REPLAY_DUMP_HEADER
     gold = S.records(G.read(name))
-    got = _recs(dump)
+    got = [r for r in _recs(dump) if r[2]]  # (pcap_dump writes a zero-length record, tcprewrite.c:367 not)
     assert len(got) == len(gold)
     for (ts, fr, cl, ln, d), (gts, gtu, gcl, gln, gd) in zip(got, gold):
         assert (ts, fr, cl, ln, d) == (gts, gtu * 1000, gcl, gln, gd)
@@ -101,6 +108,37 @@ def test_preload_compounds_efcs():
     assert p0 == p1
     for a, b in zip(p1, p2):
         assert b[2] == a[2] and b[4] == a[4][:b[2]]
+
+
+@pytest.mark.parametrize("name,args", LIST_GOLDENS)
+def test_oracle_list_pass_is_the_reference_golden(name, args):
+    """send_packets.c:440-447 before tcpedit_packet: pinned by the reference's goldens"""
+    rc, dump = O.replay_edit(G.read("test.pcap"), args)
+    assert rc == 0 and dump == G.read(name)
+
+
+def test_oracle_list_and_unique_ip_ride_the_edit_pass():
+    """one pass carries the list, the edit and fast_edit_packet (:440-483): listed-out
+    records are neither edited nor sent; the edited records of the passes where
+    unique_iteration advanced get their addresses shifted after the edit"""
+    pcap = G.read("test.pcap")
+    rc, dump = O.replay_edit(pcap, ["--include=1-100", "--unique-ip", "--seed=5"], loops=2)
+    assert rc == 0
+    failed = O.replay_edit_failed()
+    assert failed > 0  # test.pcap's non-IP records among the first 100
+    p0, p1 = _passes_n(dump, [100, 100 - failed])
+    rc, one = O.replay_edit(pcap, ["--include=1-100", "--seed=5"])
+    assert p0 == _recs(one)
+    assert len(p1) == 100 - failed
+
+
+def _passes_n(dump, counts):
+    r, out, i = _recs(dump), [], 0
+    for c in counts:
+        out.append(r[i:i + c])
+        i += c
+    assert i == len(r)
+    return out
 
 
 def test_fuzz_with_preload_is_refused():
@@ -225,3 +263,46 @@ def test_relinked_tcpreplay_edit_writes_the_oracle_dump(abi, tmp_path, loops, pr
     assert r.returncode == 0, r.stderr.decode()
     rc_o, exp = O.replay_edit(pcap, args, loops, preload)
     assert rc_o == 0 and out.read_bytes() == exp
+
+
+# --------------------------------------- the pass's other steps: the list and --unique-ip
+REPLAY_LINES = [
+    (["--include=7,11,20-23,174-"], 1, False),
+    (["--exclude=23-,11-20,2,3", "--seed=9", "--fixcsum"], 2, False),
+    (["--include=1-1500,2500-", "--unique-ip", "--pnat=10.0.0.0/8:192.168.0.0/16", "--fixcsum"], 3, False),
+    (["--exclude=5-40", "--unique-ip", "--enet-vlan=add", "--enet-vlan-tag=7", "--fixcsum"], 3, True),
+    (["--unique-ip", "--unique-ip-loops=2", "--ttl=+3"], 5, True),
+    (["--include=2-", "--unique-ip", "--efcs"], 3, True),
+    (["--fuzz-seed=42", "--fuzz-factor=2"], 3, False),  # the RNG stream runs on across passes
+    (["--exclude=1-999", "--fuzz-seed=7", "--fuzz-factor=1", "--unique-ip"], 3, False),  # no draws for them
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,args", LIST_GOLDENS)
+def test_replay_list_reproduces_the_reference_golden(built, name, args):
+    rc, out = TA.replay_edit(G.read("test.pcap"), args)
+    assert rc == 0 and out == G.read(name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(len(REPLAY_LINES)))
+def test_replay_list_unique_ip_and_fuzz_match_the_oracle(built, k):
+    args, loops, preload = REPLAY_LINES[k]
+    for pcap in (G.read("test.pcap"), S.pcap_imix(5_000, seed=40 + k)):
+        rc_o, exp = O.replay_edit(pcap, args, loops, preload)
+        failed_o = O.replay_edit_failed()
+        rargs, eargs = TA.split_replay_args(args)
+        te = TA.TcpEdit(eargs)
+        try:
+            r = TA.Replay(te, pcap, preload, rargs)
+            out = [TA.REPLAY_DUMP_HEADER]
+            for _ in range(loops):
+                rc, recs = r.pass_()
+                out.append(recs)
+            assert rc == rc_o == 0, te.geterr()
+            assert b"".join(out) == exp
+            assert r.failed == failed_o
+            r.close()
+        finally:
+            te.close()

@@ -1,8 +1,9 @@
-"""tcpreplay --unique-ip (src/send_packets.c:124-257, :362-372, :477-483) with file
-output (-w): the reference's golden test2.replay_unique_ip (test/Makefile.am:216,
-`tcpreplay -w ... -t --unique-ip --loop=2 test.pcap`), the oracle
-(oracle/tcpreplay_oracle.c) pinned to it, and the device passes (tcpreplay_kernels.hip)
-against both, bit-exact."""
+"""tcpreplay --unique-ip (src/send_packets.c:124-257, :362-372, :477-483) and the
+--include / --exclude packet list (:440-447, src/common/list.c) with file output (-w):
+the reference's goldens test2.replay_unique_ip, test2.replay_include and
+test2.replay_exclude (test/Makefile.am:214-216, `tcpreplay -w ... -t <opts> test.pcap`),
+the oracle (oracle/tcpreplay_oracle.c) pinned to them, and the device passes
+(tcpreplay_kernels.hip) against both, bit-exact."""
 import random
 import struct
 
@@ -110,3 +111,51 @@ def test_unserved_options_are_refused(built):
     for bad in (["--unique-ip-loops=2"], ["--loop=0"], ["--mbps=10"], ["--unique-ip", "--unique-ip-loops=0"]):
         with pytest.raises(ValueError):
             TR.TcpReplay(bad)
+
+
+# ------------------------------------------------------ --include / --exclude (list.c)
+LIST_GOLDENS = [("test2.replay_include", ["--include=7,11,20-23,174-"]),
+                ("test2.replay_exclude", ["--exclude=23-,11-20,2,3"])]
+LIST_LINES = [
+    ["--include=1-100,500-"], ["--exclude=0-50"], ["--include=010,2-"],  # 010: strtoull base 0 (octal 8)
+    ["--exclude=3- "], ["--include=5,5,5,0"], ["--include=2000-1500"],  # an empty range
+    ["--include=1-300,700-900", "--unique-ip", "--loop=3"],
+    ["--exclude=2-20,40-", "--unique-ip", "--loop=3", "-K"],
+    ["--include=3-", "--unique-ip", "--unique-ip-loops=2", "--loop=5"],
+]
+
+
+@pytest.mark.parametrize("name,args", LIST_GOLDENS)
+def test_oracle_reproduces_the_list_goldens(built, name, args):
+    out, failed = O.replay(G.read("test.pcap"), args)
+    assert out == G.read(name) and failed == 0
+
+
+def test_unparsable_lists_are_refused(built):
+    """parse_list's regex (list.c:72) refuses the whole list; --include and --exclude
+    exclude each other (tcpreplay_opts.def:310,340)"""
+    from tcpreplay_amd import tcpreplay as TR
+    for bad in (["--include=a"], ["--include=5-x"], ["--include=,"], ["--exclude=-3"], ["--include=1", "--exclude=2"],
+                ["--include=1 "]):
+        with pytest.raises(ValueError):
+            TR.TcpReplay(bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,args", LIST_GOLDENS)
+def test_gpu_reproduces_the_list_goldens(built, name, args):
+    from tcpreplay_amd import tcpreplay as TR
+    out, failed = TR.replay(G.read("test.pcap"), args)
+    assert out == G.read(name) and failed == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(len(LIST_LINES)))
+def test_gpu_lists_match_the_oracle(built, k):
+    """the list with --unique-ip, --loop and -K: a listed-out record is neither edited (the
+    -K cache keeps it) nor sent nor counted failed"""
+    from tcpreplay_amd import tcpreplay as TR
+    args = LIST_LINES[k]
+    for pcap in (G.read("test.pcap"), _edge_pcap(1500, seed=k + 9)):
+        exp = O.replay(pcap, args)
+        assert TR.replay(pcap, args) == exp
