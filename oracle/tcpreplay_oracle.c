@@ -400,7 +400,7 @@ int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int p
             /* --unique-ip (:477-483): fast_edit_packet of the edited packet, with the header
                as read; a record it fails is counted and not sent */
             if (unique_ip && uniq && uniq > last_uniq &&
-                tro_fast_edit(data, rh[2], uniq - 1, preload && pass > 0) == -1) {
+                tro_fast_edit(data, h.caplen, uniq - 1, preload && pass > 0) == -1) {  /* the edited header */
                 ++nfailed;
                 continue;
             }

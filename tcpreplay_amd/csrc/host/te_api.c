@@ -3238,6 +3238,7 @@ struct te_srv_s {
     const uint16_t *hportlut; /* ... built from this host table */
     int running;             /* launched and not yet seen leaving */
     int broken;              /* it stopped answering: the launch-per-call path from now on */
+    int stuck;               /* it did not leave when stopped: never synced, its buffers never freed */
     uint32_t seq;
 };
 
@@ -3247,14 +3248,33 @@ static te_srv_t *te_srv_live[TE_SRV_MAX];
 static pthread_mutex_t te_srv_mu = PTHREAD_MUTEX_INITIALIZER;
 static int te_srv_atexit_done;
 
-static void srv_stop(te_srv_t *S)
+/* stop the resident kernel: raise stop, wait (bounded) for it to store alive = 0, then
+   sync its stream.  A kernel that never leaves (a broken server, stuck in its tile body)
+   is reported and its stream is not synced -- tcpedit_close and exit must not hang on it;
+   its mappings are then leaked, not freed under it (srv_free) */
+static int srv_stop(te_srv_t *S)
 {
     if (!S->running)
-        return;
+        return 0;
     __atomic_store_n(&S->ctl->stop, 1u, __ATOMIC_RELEASE);
+    const double t0 = te_now();
+    while (__atomic_load_n(&S->ctl->alive, __ATOMIC_ACQUIRE) && !getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) {
+        if (te_now() - t0 > 2.0) {
+            fprintf(stderr, "tcpedit: the packet server kernel did not leave in 2 s; its buffers are leaked\n");
+            S->stuck = 1;
+            return -1;
+        }
+        __builtin_ia32_pause();
+    }
+    if (getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) { /* (tests: the path of a kernel that never leaves) */
+        fprintf(stderr, "tcpedit: the packet server kernel did not leave in 2 s; its buffers are leaked\n");
+        S->stuck = 1;
+        return -1;
+    }
     hipStreamSynchronize(S->stream);
     S->running = 0;
     S->ctl->stop = 0;
+    return 0;
 }
 
 static void srv_stop_all(void)
@@ -3276,8 +3296,10 @@ static void srv_free(tcpedit_t *t)
         if (te_srv_live[i] == S)
             te_srv_live[i] = NULL;
     pthread_mutex_unlock(&te_srv_mu);
-    if (S->stream)
-        srv_stop(S);
+    if (S->stream && srv_stop(S) < 0) { /* still running: leave it its mappings */
+        t->srv = NULL;
+        return;
+    }
     if (S->ctl)
         hipHostFree(S->ctl);
     if (S->in)
@@ -3368,8 +3390,11 @@ static te_srv_t *srv_ready(tcpedit_t *t)
     te_dev_cfg_t want = t->cfg;
     want.skip_soft_errors = 0; /* tcpedit_packet itself never drops */
     const uint16_t *pl = t->cfg.has_portmap ? t->d_portlut : NULL;
-    if (S->running && (memcmp(&want, &S->cfg, sizeof want) != 0 || pl != S->portlut || t->portlut != S->hportlut))
-        srv_stop(S);
+    if (S->running && (memcmp(&want, &S->cfg, sizeof want) != 0 || pl != S->portlut || t->portlut != S->hportlut) &&
+        srv_stop(S) < 0) {
+        S->broken = 1;
+        return NULL;
+    }
     if (S->running && !__atomic_load_n(&S->ctl->alive, __ATOMIC_ACQUIRE)) { /* it left (idle) */
         hipStreamSynchronize(S->stream);
         S->running = 0;
@@ -3410,9 +3435,9 @@ static int srv_call(tcpedit_t *t, te_srv_t *S)
             hipStreamSynchronize(S->stream);
             if (srv_launch(t, S, q - 1) < 0)
                 return -1;
-        } else if (te_now() - t0 > 5.0) {
-            __atomic_store_n(&c->stop, 1u, __ATOMIC_RELEASE);
+        } else if (te_now() - t0 > 5.0 || getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) {
             te_seterr(t, "packet server did not answer in 5 s");
+            srv_stop(S); /* bounded: a kernel that does not leave is left running, unsynced */
             return -1;
         }
     }
@@ -3487,7 +3512,6 @@ static int packet_via_server(tcpedit_t *t, struct pcap_pkthdr *h, unsigned char 
     memset(S->in + 40 + caplen, 0, 16);
     S->ctl->dir = direction;
     S->ctl->caplen = caplen;
-    S->ctl->pkt_base = t->pub.runtime.packetnum;
     if (srv_call(t, S) < 0) {
         S->broken = 1;
         return TE_SRV_DECLINED;

@@ -340,13 +340,14 @@ int tcpedit_replay_pass(tcpedit_t *t, tcpedit_replay_t *r, void *out, size_t cap
         }
         uint32_t h[4];
         if (st[i] & TE_ST_ZEROCAP) {
-            /* a record read with caplen 0 (no edit step can empty one): tcpedit_packet's
-               only change to it is --efcs's trim of len (tcpedit.c:78-84), then the L2 parse
-               fails (a soft error) */
+            /* a record with caplen 0 after its edit (the batch output leaves it out): read
+               that way, tcpedit_packet's only change is --efcs's trim of len (tcpedit.c:78-84)
+               before the L2 parse fails (a soft error); emptied by the edit, it is the fuzz
+               step's drop (fuzzing.c:37-60: caplen = len = 0) */
             const uint32_t ln = rp32(src + ip + 12, r->swapped);
             h[0] = rp32(src + ip, r->swapped);
             h[2] = 0;
-            h[3] = ((const tcpedit_ref_t *)t)->efcs && ln > 4 ? ln - 4 : ln;
+            h[3] = cl0 ? 0u : (((const tcpedit_ref_t *)t)->efcs && ln > 4 ? ln - 4 : ln);
         } else {
             if (op + 16 > olen) { /* (the batch wrote fewer records than it edited) */
                 err = 1;

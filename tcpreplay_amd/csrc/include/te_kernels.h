@@ -166,18 +166,21 @@ typedef struct {
 
 /* tcpedit_packet's resident server (te_packet_server, one block): a control block in
  * host-mapped fine-grained memory.  The host writes the record at byte 24 of the mapped
- * input image, fills the request words and stores seq (release); the kernel, polling seq,
- * edits the record into the mapped output image (record at byte 24), writes the response
- * words and stores done = seq (release).  It leaves when stop is set or after idle_ticks
- * of the 100 MHz real-time clock without a request, storing alive = 0. */
+ * input image, the request words dir and caplen, then seq (release); the kernel polls the
+ * first 16 bytes {seq, stop, dir, caplen} with one read -- a new seq arrives together with
+ * the request it publishes (x86 keeps the host's stores in order), so a request costs one
+ * PCIe read round trip, not two -- edits the record into the mapped output image (record
+ * at byte 24), writes the response words and stores done = seq (release).  It leaves when
+ * stop is set or after idle_ticks of the 100 MHz real-time clock without a request,
+ * storing alive = 0.  (The server edits with a fixed direction: no cache lookup, so it
+ * needs no packet number.) */
 typedef struct {
     uint32_t seq;       /* host: the request number */
     uint32_t stop;      /* host: 1 = leave now */
-    uint32_t done;      /* device: the last request served */
-    uint32_t alive;     /* host: 1 before a launch; device: 0 when it leaves */
     int32_t dir;        /* request: the direction (tcpedit_packet's argument) */
     uint32_t caplen;    /* request: the record's caplen (its 16-byte header is in the image) */
-    uint64_t pkt_base;  /* request: 0-based packet number of the record */
+    uint32_t done;      /* device: the last request served */
+    uint32_t alive;     /* host: 1 before a launch; device: 0 when it leaves */
     /* response */
     uint32_t status;    /* the record's TE_ST_* byte */
     uint32_t pad_;

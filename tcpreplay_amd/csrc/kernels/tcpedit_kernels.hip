@@ -710,9 +710,9 @@ __global__ void __launch_bounds__(BLOCK, TE_MIN_WAVES) te_edit_tiles(LaunchArgs 
 // request and response words with the bytes.  The loop ends on `stop` or after
 // idle_ticks without a request, so the grid always drains.
 // ===========================================================================
-static_assert(offsetof(te_srv_ctl_t, dir) % 16 == 0 && offsetof(te_srv_ctl_t, caplen) == offsetof(te_srv_ctl_t, dir) + 4 &&
-                  offsetof(te_srv_ctl_t, pkt_base) == offsetof(te_srv_ctl_t, dir) + 8,
-              "the server reads {dir, caplen, pkt_base} as one 16-byte word (the control block is page-aligned)");
+static_assert(offsetof(te_srv_ctl_t, seq) == 0 && offsetof(te_srv_ctl_t, stop) == 4 && offsetof(te_srv_ctl_t, dir) == 8 &&
+                  offsetof(te_srv_ctl_t, caplen) == 12,
+              "the server polls {seq, stop, dir, caplen} as one 16-byte word (the control block is page-aligned)");
 __global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
     __shared__ __attribute__((aligned(16))) uint8_t slots[TE_SLOT_BYTES + LDS_FRONT + 64];
     __shared__ TileShared sh;
@@ -739,34 +739,36 @@ __global__ void __launch_bounds__(BLOCK) te_packet_server(te_srv_launch_t s) {
     a.pkt_rel = (const uint16_t *)(s.scratch + 16);  // one zero word
     a.n_tiles = 1;
     a.fuzz_mode = TE_FUZZ_OFF;
+    a.pkt_base = 0;  // (a fixed direction: no tcpprep cache lookup by packet number)
+    __shared__ uint32_t rq_dir, rq_caplen;
     uint32_t last = s.start_seq;
     for (;;) {
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            uint32_t v = last, q = 0;
+            uint32_t q = 0;
+            u32x4 w;
             for (;;) {
-                v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (v != last) break;
-                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    __builtin_amdgcn_s_memrealtime() - t0 > s.idle_ticks) {
+                // {seq, stop, dir, caplen} in one read over PCIe: the request rides with its seq
+                w = *(const volatile u32x4 *)ctl;
+                if (w.x != last) break;
+                if (w.y || __builtin_amdgcn_s_memrealtime() - t0 > s.idle_ticks) {
                     q = 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            req = v;
+            req = w.x;
             quit = q;
+            rq_dir = w.z;
+            rq_caplen = w.w;
         }
         __syncthreads();
         if (quit) break;
-        // the host's stores before its release of seq are visible from here on
+        // the host's stores before its release of seq (the record) are visible from here on
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t seq = req;
-        // the request words in one 16-byte read over PCIe: {dir, caplen, pkt_base}
-        const u32x4 rq = *(const volatile u32x4 *)&ctl->dir;
-        const uint32_t caplen = rq.y;
-        a.fixed_dir = (int32_t)rq.x;
-        a.pkt_base = (uint64_t)rq.z | ((uint64_t)rq.w << 32);
+        const uint32_t caplen = rq_caplen;
+        a.fixed_dir = (int32_t)rq_dir;
         te_tile_t tile;
         tile.span_off = 24;
         tile.scratch_off = TE_NO_SCRATCH;

@@ -43,6 +43,8 @@ typedef struct {
     tcpedit_batch_result_t r;
     uint64_t seg;
     const uint8_t *status;
+    uint64_t *d_cnt;    /* the counter all-reduce's device buffer and stream, set up before */
+    hipStream_t cst;    /* the first barrier: a shard without them takes no device into it */
     char err[512];
 } shard_t;
 
@@ -102,6 +104,16 @@ static void *shard_main(void *arg)
         if (!S->opened)
             snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
     }
+    if (S->opened) { /* the all-reduce's device buffer and stream (RCCL reads device memory only) */
+        const char *inj = getenv("TCPREWRITE_GPUS_FAIL_COUNTERS"); /* (tests: this shard's setup fails) */
+        const int fail = inj && *inj && atoi(inj) == k;
+        if (fail || hipSetDevice(k) != hipSuccess ||
+            hipStreamCreateWithFlags(&S->cst, hipStreamNonBlocking) != hipSuccess ||
+            hipMalloc((void **)&S->d_cnt, NCNT * sizeof(uint64_t)) != hipSuccess) {
+            snprintf(S->err, sizeof S->err, "device %d: no device buffer for the counter all-reduce", k);
+            S->opened = 0;
+        }
+    }
     /* ---- the pre-edit prefix: earlier shards' fuzz draws and dst_modified carry ---- */
     pthread_barrier_wait(&J->bar);
     int all_open = 1;
@@ -134,28 +146,29 @@ static void *shard_main(void *arg)
             memcpy(cnt, v, sizeof cnt);
         }
     }
-    /* ---- the job's counters: one RCCL all-reduce over the devices ---- */
-    {
-        uint64_t *d = NULL;
-        hipStream_t st = NULL;
-        int ok = hipSetDevice(k) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
-                 hipMalloc((void **)&d, sizeof cnt) == hipSuccess &&
-                 hipMemcpy(d, cnt, sizeof cnt, hipMemcpyHostToDevice) == hipSuccess;
-        /* every thread takes part (a failed setup sends its zeros): no device is left waiting */
-        ncclResult_t nr = ncclAllReduce(d ? (const void *)d : (const void *)cnt, d ? (void *)d : (void *)cnt, NCNT,
-                                        ncclUint64, ncclSum, J->comms[k], st);
-        ok = ok && nr == ncclSuccess && hipStreamSynchronize(st) == hipSuccess &&
-             hipMemcpy(cnt, d, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess;
+    /* ---- the job's counters: one RCCL all-reduce over the devices.  Every shard opened
+       (and has its device buffer) or none takes part: each thread decided all_open from the
+       same flags after the barrier, so no device is left waiting in the collective, and a
+       failed shard ends the job with its message instead of a fault ---- */
+    if (all_open) {
+        int ok = hipSetDevice(k) == hipSuccess &&
+                 hipMemcpyAsync(S->d_cnt, cnt, sizeof cnt, hipMemcpyHostToDevice, S->cst) == hipSuccess;
+        ncclResult_t nr = ncclAllReduce(S->d_cnt, S->d_cnt, NCNT, ncclUint64, ncclSum, J->comms[k], S->cst);
+        ok = ok && nr == ncclSuccess && hipMemcpyAsync(cnt, S->d_cnt, sizeof cnt, hipMemcpyDeviceToHost, S->cst) ==
+                                            hipSuccess &&
+             hipStreamSynchronize(S->cst) == hipSuccess;
         if (!ok && !S->err[0])
             snprintf(S->err, sizeof S->err, "device %d: counter all-reduce failed (%s)", k, ncclGetErrorString(nr));
         if (!ok)
             S->rc = TCPEDIT_ERROR, S->opened = 0;
         if (k == 0)
             memcpy(J->job_cnt, cnt, sizeof cnt);
-        hipFree(d);
-        if (st)
-            hipStreamDestroy(st);
     }
+    hipFree(S->d_cnt);
+    S->d_cnt = NULL;
+    if (S->cst)
+        hipStreamDestroy(S->cst);
+    S->cst = NULL;
     /* ---- placement and the output file (thread 0), then every shard's D2H into it ---- */
     pthread_barrier_wait(&J->bar);
     if (k == 0) {

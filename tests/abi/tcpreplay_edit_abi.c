@@ -2,7 +2,8 @@
  * tcpreplay_edit_abi.c -- tcpreplay-edit's tcpedit calls and its send loop, batched,
  * against include/tcpedit.h, with file output (test program):
  *
- *   tcpreplay-edit -w <out> [--loop=N] [-K | --preload-pcap] <tcpedit options> <in.pcap>
+ *   tcpreplay-edit -w <out> [--loop=N] [-K | --preload-pcap] [--include=L | --exclude=L]
+ *                  [--unique-ip [--unique-ip-loops=N]] <tcpedit options> <in.pcap>
  *
  * main() follows src/tcpreplay.c:79-100 for the tcpedit calls:
  *   tcpedit_init(&tcpedit, sendpacket_get_dlt(intf1))  :81  (-w opens pcap_open_dead(
@@ -26,8 +27,9 @@
 int main(int argc, char **argv)
 {
     const char *wfile = NULL, *in = NULL;
-    int loops = 1, preload = 0, nopt = 0;
+    int loops = 1, preload = 0, nopt = 0, nrop = 0;
     char **opts = calloc((size_t)argc + 1, sizeof(char *));
+    char **ropts = calloc((size_t)argc + 1, sizeof(char *)); /* tcpreplay's own per-record steps */
     for (int i = 1; i < argc; i++) {
         if (!strcmp(argv[i], "-w") && i + 1 < argc)
             wfile = argv[++i];
@@ -35,6 +37,9 @@ int main(int argc, char **argv)
             loops = atoi(argv[i] + 7);
         else if (!strcmp(argv[i], "-K") || !strcmp(argv[i], "--preload-pcap"))
             preload = 1;
+        else if (!strncmp(argv[i], "--include=", 10) || !strncmp(argv[i], "--exclude=", 10) ||
+                 !strcmp(argv[i], "--unique-ip") || !strncmp(argv[i], "--unique-ip-loops=", 18))
+            ropts[nrop++] = argv[i];
         else if (argv[i][0] == '-' && argv[i][1])
             opts[nopt++] = argv[i];
         else
@@ -83,6 +88,12 @@ int main(int argc, char **argv)
         tcpedit_close(&tcpedit);
         return 255;
     }
+    if (tcpedit_replay_parse_args(tcpedit, r, nrop, ropts) != TCPEDIT_OK) {
+        fprintf(stderr, "Unable to parse include/exclude rule: %s\n", tcpedit_geterr(tcpedit));
+        tcpedit_replay_close(r);
+        tcpedit_close(&tcpedit);
+        return 255;
+    }
     FILE *o = fopen(wfile, "wb");
     const unsigned int fh[6] = {0xa1b2c3d4u, 2 | (4u << 16), 0, 0, 262144u, 1u};
     fwrite(fh, 4, 6, o);
@@ -103,5 +114,6 @@ int main(int argc, char **argv)
     free(buf);
     free(img);
     free(opts);
+    free(ropts);
     return rc;
 }

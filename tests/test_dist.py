@@ -249,6 +249,23 @@ def test_tcprewrite_gpus_tool_equals_oracle(built, tmp_path, case):
     assert out.read_bytes() == exp
 
 
+@pytest.mark.gpu
+def test_tcprewrite_gpus_counter_setup_failure_ends_cleanly(built, tmp_path):
+    """a shard whose counter all-reduce buffer cannot be set up takes no device into the
+    collective (RCCL reads device memory only): the job ends with its message, exit 255,
+    rather than a GPU fault or a hang"""
+    import subprocess
+    inp, out = tmp_path / "in.pcap", tmp_path / "out.pcap"
+    inp.write_bytes(S.pcap_fixed(2_000, 64, seed=2))
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tcpreplay_amd", "bin",
+                        "tcprewrite")
+    env = dict(os.environ, TCPREWRITE_GPUS_FAIL_COUNTERS="0")
+    r = subprocess.run([tool, "--gpus", "1", "-i", str(inp), "-o", str(out), "--fixcsum"], capture_output=True,
+                       timeout=120, env=env)
+    assert r.returncode == 255
+    assert b"no device buffer for the counter all-reduce" in r.stderr
+
+
 # ---------------------------------------------------------------- gloo world_size 2 (oracle-edited shards)
 @pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix", "fuzz_golden", "fuzz_imix"])
 def test_two_rank_rewrite_equals_single_process(built, case):

@@ -13,6 +13,7 @@ import tcpreplay_amd as TA
 from tcpreplay_amd import synth as S
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 C2_ARGS = ["--seed=42", "--fixcsum"]
 C3_ARGS = ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]
@@ -224,6 +225,33 @@ def test_packet_server_relaunches_after_idle_and_serves_two_contexts(built):
     finally:
         t1.close()
         t2.close()
+
+
+def test_packet_server_that_never_answers_ends_bounded(built, tmp_path):
+    """a server that stops answering (forced: TCPEDIT_HIP_SRV_TEST_STUCK) is stopped with a
+    bounded wait and never stream-synced: the call falls back to the launch path with the
+    same bytes, and tcpedit_close and the process exit do not hang"""
+    import subprocess
+    import sys
+    script = tmp_path / "stuck.py"
+    script.write_text(
+        "import sys\n"
+        f"sys.path[:0] = [{ROOT!r}, {os.path.join(ROOT, 'tests')!r}]\n"
+        "import golden_cases as G, oracle_lib as O, tcpreplay_amd as TA\n"
+        "from tcpreplay_amd import synth as S\n"
+        "recs = S.records(G.read('test.pcap'))[:6]\n"
+        "exp = S.records(O.rewrite(S.build_pcap(recs), ['--seed=3'])[1])\n"
+        "te = TA.TcpEdit(['--seed=3'])\n"
+        "for i, (ts, tu, cl, ln, d) in enumerate(recs):\n"
+        "    buf = bytearray(262166); buf[:cl] = d\n"
+        "    rc, h = te.packet({'ts_sec': ts, 'ts_usec': tu, 'caplen': cl, 'len': ln}, buf)\n"
+        "    assert (ts, tu, h['caplen'], h['len'], bytes(buf[:h['caplen']])) == exp[i], i\n"
+        "te.close()\n"
+        "print('ok')\n")
+    env = dict(os.environ, TCPEDIT_HIP_SRV_TEST_STUCK="1")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, timeout=100, env=env)
+    assert r.returncode == 0 and b"ok" in r.stdout, r.stderr.decode()[-2000:]
+    assert b"did not leave" in r.stderr
 
 
 def test_packet_server_declines_records_larger_than_its_slot(built):
