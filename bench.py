@@ -81,6 +81,7 @@ def make_pcap(workload, n, seed):
 
 
 STRONG_BLOCK = 1_250_000  # records generated once per rank and repeated (--strong)
+STRONG_VERIFY_MAX = 25_000_000  # --strong / the strong side line: shares checked against the oracle
 
 
 def make_share(workload, total, rank, world, seed):
@@ -237,11 +238,16 @@ def strong_side(opt, world, rank, local, barrier):
     import torch.distributed as dist
     total = 100_000_000
     share = make_share("c4", total, rank, world, seed=1)
-    te, b, r, _, _ = run_workload("c4", share[3], 0, 2, seed=1, device=local, share=share, total=total,
-                                  verify=False)
+    # each rank checks its share's first run against the sharded oracle (global record
+    # numbers, the job's cache) when the share fits the checker's host memory: every rank
+    # at N >= 4 (25M records, ~9 GB each)
+    verify = not opt.no_verify and share[3] <= STRONG_VERIFY_MAX
+    te, b, r, _, checked = run_workload("c4", share[3], 0, 2, seed=1, device=local, share=share, total=total,
+                                        verify=verify)
     del share
     k = max(3, min(opt.steps, 20))
-    byt = torch.tensor([r.bytes_in + r.bytes_out, r.packets], dtype=torch.int64, device="cuda")
+    byt = torch.tensor([r.bytes_in + r.bytes_out, r.packets, 1 if checked else 0, checked], dtype=torch.int64,
+                       device="cuda")
     barrier()
     t0 = time.perf_counter()
     b.time(k)
@@ -258,7 +264,11 @@ def strong_side(opt, world, rank, local, barrier):
             "mpkt_s": round(int(byt[1].item()) / sec / 1e6, 1),
             "gbps_algorithmic": round(int(byt[0].item()) / sec / 1e9, 1),
             "frac_hbm_peak_per_gpu": round(int(byt[0].item()) / sec / 1e9 / world / HBM_PEAK_GBS, 4),
-            "verified": False, "note": "not re-checked here (host memory); the c4 code path is checked at N=1"}
+            "verified": int(byt[2].item()) == world, "verified_records": int(byt[3].item()),
+            "note": "each rank's share checked against the oracle at its global record numbers"
+                    if int(byt[2].item()) == world else
+                    f"shares above {STRONG_VERIFY_MAX} records are not re-checked (host memory); the c4 code "
+                    "path is checked at N=1"}
 
 
 def main():
@@ -312,7 +322,7 @@ def main():
         # verified when the share is small enough for the checker's host memory
         te, b, r, pcap, checked = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1, device=local,
                                                share=share, total=total,
-                                               verify=not opt.no_verify and n <= 20_000_000)
+                                               verify=not opt.no_verify and n <= STRONG_VERIFY_MAX)
         del share
     else:
         # N = 1: BASELINE configs[1] (1M x 64 B).  N > 1: every rank weak-scales a

@@ -2195,15 +2195,17 @@ static int host_locked(const void *p)
    indexed and edited and chunk k + 2 uploads -- into a third slot, so chunk k's input and
    index stand until it is finished */
 #define TE_PIPE_SLOTS 3
+#define TE_PIPE_ANCHORS 64 /* chunk starts kept (chunks are >= 8 MiB: >= 512 MiB of anchors) */
 /* the default chunk: a tenth of the capture, 8-32 MiB (measured on MI355X, tools/e2e_probe.py:
    C2's 80 MB runs best at 8 MiB -- pipeline fill and drain are one chunk each -- and 2M IMIX
    records (740 MB) at 12-32 MiB, where per-chunk costs dominate) */
 #define TE_PIPE_CHUNK_MIN ((size_t)8 << 20)
 #define TE_PIPE_CHUNK_MAX ((size_t)32 << 20)
 
-/* res_pinned layout: counters | error words | wave-lane slots */
-#define TE_RES_ERR 96
-#define TE_RES_SLOTS 128
+/* res_pinned layout: the workspace head (error words, ticket, both counter sets: one copy
+   of d_ws[0, WS_STATE)) | wave-lane slots */
+#define TE_RES_SLOTS WS_STATE
+_Static_assert(WS_COUNTERS1 + 8 * TE_CNT__N <= WS_STATE && WS_ERR + 24 <= WS_COUNTERS, "workspace head layout");
 
 /* the device-index pipeline uploads each chunk with the bytes of a record that starts in it
    and ends past it: the largest record (16 + 262144 bytes), rounded */
@@ -2226,7 +2228,44 @@ struct te_pipe_s {
        replay's prefix records */
     const uint8_t *img;
     uint64_t first_off[TE_PIPE_SLOTS], prev_off[TE_PIPE_SLOTS];
+    /* the latest chunks' first-record offsets (a ring): known record boundaries a Q8
+       replay's prefix walk can start from instead of the capture's first record */
+    uint64_t anchor[TE_PIPE_ANCHORS];
+    uint32_t nanchor;
+    /* per slot: the chunk's output already on its way down (its D2H issued right after the
+       edit launch, a size-preserving config: output bytes = record bytes, known from the
+       index totals), ~0 when not */
+    uint64_t early[TE_PIPE_SLOTS];
+    uint32_t early_miss, early_n; /* (trace: early copies done again, early copies) */
 };
+
+/* a chunk's first record at file offset off: an anchor for later prefixes */
+static void pipe_anchor(te_pipe_t *P, uint64_t off)
+{
+    if (P->nanchor && P->anchor[(P->nanchor - 1) % TE_PIPE_ANCHORS] >= off)
+        return;
+    P->anchor[P->nanchor++ % TE_PIPE_ANCHORS] = off;
+}
+
+/* where the prefix of the chunk starting at `first` may start: the newest anchor far enough
+   back that the staged records (at most TE_Q8_PRE_BYTES, stage_prefix) are the same as a
+   walk from the capture's start would stage, else the capture's first record (24) */
+static uint64_t pipe_prefix_from(const te_pipe_t *P, uint64_t first)
+{
+    const uint64_t need = (uint64_t)TE_Q8_PRE_BYTES + 262144u + 16u;
+    if (first < 24 + need)
+        return 24;
+    const uint32_t n = P->nanchor < TE_PIPE_ANCHORS ? P->nanchor : TE_PIPE_ANCHORS;
+    uint64_t best = 24;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t a = P->anchor[(P->nanchor - 1 - i) % TE_PIPE_ANCHORS];
+        if (a <= first - need) {
+            best = a;
+            break;
+        }
+    }
+    return best;
+}
 
 void te_pipe_free(tcpedit_t *t)
 {
@@ -2295,6 +2334,9 @@ static int pipe_ready(tcpedit_t *t, size_t chunk)
         return 0;
     te_pipe_free(t);
     P = t->pipe = calloc(1, sizeof(*P));
+    if (P)
+        for (int j = 0; j < TE_PIPE_SLOTS; j++)
+            P->early[j] = ~0ull;
     P->chunk = chunk;
     HIPCHK(t, hipStreamCreateWithFlags(&P->s_h2d, hipStreamNonBlocking));
     HIPCHK(t, hipStreamCreateWithFlags(&P->s_d2h, hipStreamNonBlocking));
@@ -2350,13 +2392,22 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     tcpedit_batch_t *b = P->slot[s];
     if (*stopped == 2)
         return 0;
-    memcpy(b->counters, b->res_pinned, sizeof(b->counters));
+    memcpy(b->counters, b->res_pinned + b->last_cnt_off, sizeof(b->counters));
+    int retried = 0; /* a replay rewrote output bytes after the chunk's early D2H */
     if (b->counters[TE_CNT_Q8_FAILED] && P->img && P->prev_off[s] != ~0ull) {
+        retried = 1;
         /* the stale bytes may come from earlier chunks: the replay walks back into their
            records (the host image holds them all; the staging keeps the newest) */
-        tcpedit_batch_set_prefix(t, b, P->img + 24, P->first_off[s] - 24);
+        /* from a chunk start about TE_Q8_PRE_BYTES back (the walk is O(bytes walked)); from
+           the capture's first record only when the replay needs the buffer's initial zeros */
+        const uint64_t from = pipe_prefix_from(P, P->first_off[s]);
+        tcpedit_batch_set_prefix(t, b, P->img + from, P->first_off[s] - from);
         const uint64_t before = b->counters[TE_CNT_Q8_FAILED];
-        const int r = retry_q8_with_prefix(t, b, -1, b->counters);
+        int r = retry_q8_with_prefix(t, b, -1, b->counters);
+        if (r == 0 && from != 24 && b->counters[TE_CNT_Q8_FAILED]) {
+            tcpedit_batch_set_prefix(t, b, P->img + 24, P->first_off[s] - 24);
+            r = retry_q8_with_prefix(t, b, -1, b->counters);
+        }
         if (getenv("TCPEDIT_HIP_Q8_DEBUG"))
             fprintf(stderr, "q8 retry: slot %d first_off %llu pkt_base %llu failed %llu -> %llu (listed %llu) npre %u "
                     "file_start %d rc %d\n", s, (unsigned long long)P->first_off[s], (unsigned long long)b->pkt_base,
@@ -2366,7 +2417,7 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
         if (r < 0)
             return -1;
     }
-    memcpy(b->err, b->res_pinned + TE_RES_ERR, sizeof(b->err));
+    memcpy(b->err, b->res_pinned + WS_ERR, sizeof(b->err));
     for (int i = 0; i < b->last_fgrid; i++) {
         const uint64_t *v = (const uint64_t *)(b->res_pinned + TE_RES_SLOTS) + 4 * (size_t)i;
         b->counters[TE_CNT_PACKETS] += v[0];
@@ -2399,10 +2450,17 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
         te_seterr(t, "output buffer too small (%llu bytes needed so far)", (unsigned long long)(*pos + bytes));
         return -1;
     }
-    HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
-    if (bytes)
-        HIPCHK(t, hipMemcpyAsync(dst + *pos, b->d_out + ob, bytes, hipMemcpyDeviceToHost, P->s_d2h));
-    HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+    if (P->early[s] != ~0ull && (retried || P->early[s] != *pos))
+        P->early_miss++;
+    if (P->early[s] == ~0ull || retried || P->early[s] != *pos) {
+        /* (an early copy landed where these bytes go, unless a replay changed them since;
+           after a hard error it copied more than `bytes`, past the output's end) */
+        HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
+        if (bytes)
+            HIPCHK(t, hipMemcpyAsync(dst + *pos, b->d_out + ob, bytes, hipMemcpyDeviceToHost, P->s_d2h));
+        HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+    }
+    P->early[s] = ~0ull;
     *pos += bytes;
     t->pub.runtime.packetnum += b->counters[TE_CNT_PACKETS];
     t->pub.runtime.total_bytes += b->counters[TE_CNT_BYTES_OUT];
@@ -2449,6 +2507,53 @@ size_t tcpedit_output_bound(tcpedit_t *t, const void *in, size_t in_len)
     return bound;
 }
 
+/* The chunk schedule of a device-index pipeline: file offsets of the chunks' first bytes,
+ * st[0] = 24 ... st[n] = in_len.  The first and last chunks ramp (C/8, C/4, C/2 -- at least
+ * 1 MiB, which holds any record), the rest are about C: the D2H stream starts after a
+ * small first chunk is in and edited, and only a small last chunk's edit and D2H are left
+ * when the last H2D ends (the run's fill and drain).  Every chunk but the last is a
+ * multiple of 16 bytes long (the chunks' images share one 16-byte phase).  NULL: no memory. */
+static uint64_t *pipe_plan(size_t in_len, size_t C, int *n_out)
+{
+    const uint64_t N = in_len > 24 ? in_len - 24 : 0, MIN = (uint64_t)1 << 20;
+    uint64_t ramp[3];
+    int nr = 0;
+    for (int q = 3; q >= 1; q--) {
+        const uint64_t r = ((C >> q) < MIN ? MIN : (uint64_t)(C >> q)) & ~15ull;
+        if (r < C && (nr == 0 || ramp[nr - 1] != r))
+            ramp[nr++] = r;
+    }
+    uint64_t ramp_sum = 0;
+    for (int i = 0; i < nr; i++)
+        ramp_sum += ramp[i];
+    const int cap = (int)(N / MIN) + 2 * nr + 4;
+    uint64_t *st = malloc(sizeof(uint64_t) * (size_t)cap);
+    if (!st)
+        return NULL;
+    int n = 0;
+    uint64_t at = 24;
+    st[n++] = at;
+    if (N > 2 * ramp_sum + C) {
+        for (int i = 0; i < nr; i++)
+            st[n++] = (at += ramp[i]);
+        const uint64_t mid = N - 2 * ramp_sum, m = (mid + C - 1) / C, each = ((mid + m - 1) / m + 15) & ~15ull;
+        for (uint64_t i = 0; i + 1 < m; i++)
+            st[n++] = (at += each);
+        st[n++] = (at = 24 + N - ramp_sum); /* (the middle's last chunk takes the remainder) */
+        for (int i = nr - 1; i > 0; i--)
+            st[n++] = (at += ramp[i]);
+        st[n++] = in_len;
+    } else { /* a small capture: pieces of at most C/2 (at least 1 MiB) */
+        const uint64_t half = ((C / 2 < MIN ? MIN : C / 2) + 15) & ~15ull;
+        while (in_len - at > half)
+            st[n++] = (at += half);
+        st[n++] = in_len;
+    }
+    /* (a chunk boundary past the end cannot happen: every step stays below in_len) */
+    *n_out = n - 1;
+    return st;
+}
+
 /* TCPEDIT_HIP_PIPE_INDEX=host keeps the host record walk in the pipeline (A/B) */
 static int pipe_index_host_env(void)
 {
@@ -2469,11 +2574,29 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
                         uint8_t *d_dirbits, uint64_t dirbits_len, uint64_t *pos_io, int trace)
 {
     const size_t C = P->chunk;
+    int nch = 0;
+    /* equal chunks; TCPEDIT_HIP_PIPE_RAMP=1 ramps the first and last (A/B: on C2 it cost more
+       in per-chunk overhead than it saved in fill and drain, 2.29 vs 2.15 ms) */
+    uint64_t *cst = getenv("TCPEDIT_HIP_PIPE_RAMP") ? pipe_plan(in_len, C, &nch) : NULL;
+    if (!cst) {
+        nch = (int)((in_len - 24 + C - 1) / C);
+        if (nch < 1)
+            nch = 1;
+        cst = malloc(sizeof(uint64_t) * ((size_t)nch + 1));
+        if (!cst) {
+            te_seterr(t, "out of memory");
+            return -1;
+        }
+        for (int j = 0; j < nch; j++)
+            cst[j] = 24 + (uint64_t)j * C;
+        cst[nch] = in_len;
+    }
     uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0};
     int inflight[TE_PIPE_SLOTS] = {0}, stopped = 0, k = 0, fallbacks = 0;
     uint64_t entry_file = 24;  /* host copy of where chunk k's records start (file offset) */
     uint64_t prev_first = ~0ull;
     P->img = img;
+    P->nanchor = 0; /* (this call's capture) */
     uint64_t limit_img[TE_PIPE_SLOTS] = {0}, file0[TE_PIPE_SLOTS] = {0};
     IdxArgs A[TE_PIPE_SLOTS];
     const double t0 = te_now();
@@ -2483,8 +2606,8 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     do {                                                                                                      \
         const int s_ = (j) % TE_PIPE_SLOTS;                                                                   \
         tcpedit_batch_t *b_ = P->slot[s_];                                                                    \
-        const uint64_t f0_ = 24 + (uint64_t)(j) * C;                                                          \
-        const uint64_t fe_ = f0_ + C + TE_PIPE_MARGIN < in_len ? f0_ + C + TE_PIPE_MARGIN : in_len;          \
+        const uint64_t f0_ = cst[j], f1_ = cst[(j) + 1];                                                     \
+        const uint64_t fe_ = f1_ + TE_PIPE_MARGIN < in_len ? f1_ + TE_PIPE_MARGIN : in_len;                  \
         if ((j) >= TE_PIPE_SLOTS)                                                                             \
             HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s_], 0));                                     \
         HIPCHK(t, hipMemcpyAsync(b_->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));                     \
@@ -2492,7 +2615,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipEventRecord(P->h2d_done[s_], P->s_h2d));                                                 \
         b_->in_len = 24 + (fe_ - f0_);                                                                        \
         file0[s_] = f0_;                                                                                      \
-        limit_img[s_] = f0_ + C >= in_len ? b_->in_len : 24 + C;                                              \
+        limit_img[s_] = f1_ >= in_len ? b_->in_len : 24 + (f1_ - f0_);                                       \
     } while (0)
     /* chunk j's index on the compute stream, after its upload; its first record from the
        previous chunk's totals (on the device), or 24 */
@@ -2506,7 +2629,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         a_->len = b_->in_len;                                                                                 \
         a_->entry = 24;                                                                                       \
         a_->entry_ptr = (j) ? A[ps_].totals + IDX_T_END : NULL;                                               \
-        a_->entry_sub = C;                                                                                    \
+        a_->entry_sub = (j) ? cst[j] - cst[(j) - 1] : 0; /* the previous chunk's image is that much earlier */ \
         a_->base = 16;                                                                                        \
         a_->limit = limit_img[s_];                                                                            \
         a_->sw = b_->swapped;                                                                                 \
@@ -2529,12 +2652,16 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipEventRecord(P->idx_done[s_], t->stream));                                                \
     } while (0)
 
+    uint64_t pos_early = pos; /* where the next early D2H lands (size-preserving configs) */
+    for (int j = 0; j < TE_PIPE_SLOTS; j++)
+        P->early[j] = ~0ull;
+    P->early_n = P->early_miss = 0;
     DIX_UPLOAD(0);
     DIX_INDEX(0);
     for (;; k++) {
         const int s = k % TE_PIPE_SLOTS;
         tcpedit_batch_t *b = P->slot[s];
-        const int more = 24 + (uint64_t)(k + 1) * C < in_len;
+        const int more = k + 1 < nch;
         if (more)
             DIX_UPLOAD(k + 1);
         /* ---- chunk k's index totals ---- */
@@ -2588,9 +2715,10 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         }
         entry_file = file0[s] + b->walk_end - 24;
         if (b->n_pkts == 0) {
-            if (b->stop_error_pkt >= 0) {
+            if (b->stop_error_pkt >= 0) { /* the chunk's first record is the hard error: the
+                                             output ends with the chunks before (tcprewrite.c:296) */
                 te_seterr(t, "Error rewriting packets: packet %llu", (unsigned long long)(pkts + 1));
-                goto fail;
+                t->pipe_err = 1;
             }
             stopped = 1;
         } else {
@@ -2610,19 +2738,34 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             }
             if (run_q8(t, b, -1, pkts == 0, NULL, 0, t->stream) < 0)
                 goto fail;
-            HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws + b->last_cnt_off, sizeof(b->counters),
-                                     hipMemcpyDeviceToHost, t->stream));
-            HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_ERR, b->d_ws + WS_ERR, sizeof(b->err),
-                                     hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws, WS_STATE, hipMemcpyDeviceToHost, t->stream));
             if (b->last_fgrid)
                 HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
                                          32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
             HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
+            /* a size-preserving config writes each record at its input offset, so the chunk's
+               output is its records' bytes: start their D2H behind the edit now, without the
+               host's round trip for the results (pipe_finish_chunk checks them and copies
+               again only when a replay changed the bytes) */
+            if (!b->slot_layout && static_capable(&t->cfg) && !b->has_zero_cap && b->stop_error_pkt < 0 &&
+                !getenv("TCPEDIT_HIP_PIPE_NO_EARLY") &&
+                pos_early + (b->walk_end - entry_img) <= out_cap) {
+                const uint64_t ob_ = b->out_base ? b->out_base : 24, nb_ = b->walk_end - entry_img;
+                HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
+                HIPCHK(t, hipMemcpyAsync(dst + pos_early, b->d_out + ob_, nb_, hipMemcpyDeviceToHost, P->s_d2h));
+                HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+                P->early[s] = pos_early;
+                pos_early += nb_;
+                P->early_n++;
+            } else {
+                pos_early = ~0ull >> 1; /* (from here on the results decide every copy) */
+            }
             inflight[s] = 1;
             chunk_pkt_base[s] = pkts;
             pkts += b->n_pkts;
             P->first_off[s] = chunk_first;
             P->prev_off[s] = prev_first;
+            pipe_anchor(P, chunk_first);
             prev_first = chunk_first;
         }
         if (more && !stopped)
@@ -2649,9 +2792,11 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     }
     HIPCHK(t, hipStreamSynchronize(P->s_d2h));
     if (trace)
-        fprintf(stderr, "pipe (device index): %d chunks, %.3f ms, index waits %.3f ms, host-walk fallbacks %d\n",
-                k + 1, (te_now() - t0) * 1e3, t_wait * 1e3, fallbacks);
+        fprintf(stderr, "pipe (device index): %d chunks, %.3f ms, index waits %.3f ms, host-walk fallbacks %d, "
+                "early D2H %u (again %u)\n", k + 1, (te_now() - t0) * 1e3, t_wait * 1e3, fallbacks, P->early_n,
+                P->early_miss);
     *pos_io = pos;
+    free(cst);
 #undef DIX_UPLOAD
 #undef DIX_INDEX
     return 0;
@@ -2659,6 +2804,7 @@ fail:
     hipStreamSynchronize(P->s_h2d);
     hipStreamSynchronize(t->stream);
     hipStreamSynchronize(P->s_d2h);
+    free(cst);
     return -1;
 }
 
@@ -2786,6 +2932,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     uint64_t off = 24; /* file offset of the next chunk's first record */
     uint64_t prev_first = ~0ull;
     P->img = img;
+    P->nanchor = 0; /* (this call's capture) */
     int k = 0;
     for (;; k++) {
         const int s = k % TE_PIPE_SLOTS;
@@ -2853,10 +3000,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
            device and returns at once when it is 0; chunk 0 starts at the capture's start */
         if (run_q8(t, b, -1, pkts == 0, NULL, 0, t->stream) < 0)
             goto fail_drain;
-        HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws + b->last_cnt_off, sizeof(b->counters),
-                                 hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_ERR, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost,
-                                 t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws, WS_STATE, hipMemcpyDeviceToHost, t->stream));
         if (b->last_fgrid)
             HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
                                      32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
@@ -2866,6 +3010,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         pkts += b->n_pkts;
         P->first_off[s] = off;
         P->prev_off[s] = prev_first;
+        pipe_anchor(P, off);
         prev_first = off;
         off += rec_bytes;
 

@@ -146,6 +146,26 @@ def test_pipelined_chunks_replay_across_chunk_boundaries(built):
         te.close()
 
 
+def test_pipelined_replay_prefix_starts_at_a_chunk_anchor(built):
+    """past the first ~33 MiB a chunk's replay prefix walk starts at an earlier chunk's first
+    record (bounded work per retry): the donors of stale bytes a few thousand
+    records back are staged from there"""
+    n = 420_000  # 90-byte records: ~44 MiB
+    recs = S.records(S.pcap_fixed(n, 90, ipv6=True, proto=17, seed=21))
+    cover = S.records(S.pcap_fixed(1, 400, ipv6=True, proto=17, seed=22))[0]
+    recs[399_990] = recs[409_000] = cover  # longer records a little before the overreads cover them
+    recs = _overstate(recs, [400_001, 410_000, 412_000], by=40)
+    pcap = S.build_pcap(recs)
+    rc_o, exp = O.rewrite(pcap, ["--fixcsum"])
+    te = TA.TcpEdit(["--fixcsum"])
+    try:
+        rc, out = te.rewrite_pipelined(pcap, chunk_bytes=8 << 20)
+        assert rc == rc_o == 0, te.geterr()
+        assert out == exp
+    finally:
+        te.close()
+
+
 def test_batch_prefix_records_feed_the_replay(built):
     """a batch that starts mid-capture (a shard) with the records before it staged as its
     prefix equals the oracle's whole-capture output over its records; without the prefix the
