@@ -451,6 +451,29 @@ def main():
                         "(count, scan, write passes), then the edit over those tiles"}
         else:
             result["device_index"] = {"applied": False}
+    # the window mode (tcpedit_batch_run_fused): the record discovery fused into the wave
+    # lane -- one pass over the raw capture bytes plus the cross-window chain check, no
+    # index passes and no tile list.  Its output is checked byte for byte against the
+    # exact path's (itself checked against the oracle above).
+    if rank == 0 and not opt.no_device_index:
+        import numpy as np
+        fms = b.time_fused(opt.steps)
+        if fms is not None:
+            ref = b.output_np()
+            b.run_fused()
+            same = b.fused_fallbacks == 0 and np.array_equal(ref, b.output_np())
+            del ref
+            result["fused"] = {
+                "ms": round(fms, 5), "mpkt_s": round(r.packets / (fms * 1e-3) / 1e6, 1),
+                "frac_hbm_peak": round(alg_bytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "same_bytes_as_exact_path": bool(same),
+                "path": "window mode: each wave stages 4 KiB windows of the raw capture, finds the records "
+                        "(speculative boundary guesses checked along the chain), edits them in LDS and "
+                        "stores them; te_win_check verifies the chain across windows"}
+            if not same:
+                raise RuntimeError("fused run differs from the exact path")
+        else:
+            result["fused"] = {"applied": False}
     b.close()
     te.close()
     if world > 1 and not opt.strong and not opt.no_strong_side:

@@ -289,6 +289,17 @@ int tcpedit_fuzz_skip(tcpedit_t *tcpedit, uint64_t draws);
  * tcpedit_set_l2carry: seed the context with the nearest earlier shard's value. */
 int tcpedit_batch_l2carry_out(tcpedit_t *tcpedit, tcpedit_batch_t *b);
 int tcpedit_set_l2carry(tcpedit_t *tcpedit, int value);
+/* tcpedit_batch_run with the record discovery fused into the edit (the window mode of the
+ * wave lane): no index pass or tiles, each wave finds the records of a byte window of the
+ * image and edits them in place, the chain checked across windows after.  Batches it does
+ * not carry (size-changing or generic-lane configs, a tcpprep cache, big-endian or
+ * nanosecond input, a record it leaves to the generic lane) run tcpedit_batch_run: same
+ * output.  _time_fused: K such runs back to back, mean ms a run (TCPEDIT_ERROR when not
+ * carried); _fused_fallbacks: fused runs that took the exact path. */
+int tcpedit_batch_run_fused(tcpedit_t *tcpedit, tcpedit_batch_t *b);
+int tcpedit_batch_time_fused(tcpedit_t *tcpedit, tcpedit_batch_t *b, int iters, double *ms_per_run);
+uint64_t tcpedit_batch_fused_fallbacks(tcpedit_batch_t *b);
+
 /* tcpreplay-edit's send loop, batched (send_packets.c:379-640; te_replay.c).  The reference
  * edits each packet just before sending it (:469-474, tcpedit_packet with intf1's direction);
  * here one --loop pass over the capture is one device batch.  With preload (--preload-pcap,

@@ -74,6 +74,9 @@ def load():
         "tcpedit_parse_args": (c_int, [vp, c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_int)]),
         "tcpedit_batch_open": (vp, [vp, vp, sz, vp, sz, u64]),
         "tcpedit_batch_run": (c_int, [vp, vp]),
+        "tcpedit_batch_run_fused": (c_int, [vp, vp]),
+        "tcpedit_batch_time_fused": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
+        "tcpedit_batch_fused_fallbacks": (ctypes.c_uint64, [vp]),
         "tcpedit_batch_update_input": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_set_prefix": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),
@@ -364,6 +367,23 @@ class Batch:
 
     def run(self):
         return self._L.tcpedit_batch_run(self._te._ctx, self._b)
+
+    def run_fused(self):
+        """tcpedit_batch_run with the record discovery fused into the wave lane (window
+        mode); batches it does not carry run the exact path, same output"""
+        return self._L.tcpedit_batch_run_fused(self._te._ctx, self._b)
+
+    @property
+    def fused_fallbacks(self) -> int:
+        return int(self._L.tcpedit_batch_fused_fallbacks(self._b))
+
+    def time_fused(self, iters):
+        """ms per window-mode run (the wave lane finding its records + the chain check), or
+        None when the batch is not one the window mode carries"""
+        ms = ctypes.c_double()
+        if self._L.tcpedit_batch_time_fused(self._te._ctx, self._b, int(iters), ctypes.byref(ms)) < 0:
+            return None
+        return ms.value
 
     def set_prefix(self, recs):
         """the records just before this batch (whole records ending where it starts), read

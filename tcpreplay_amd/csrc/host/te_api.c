@@ -115,6 +115,12 @@ struct tcpedit_batch_s {
     int fuzz_probe_only;     /* the next launch only counts records reaching the fuzz step */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
+    /* window mode (tcpedit_batch_run_fused): its per-window workspace, and the window
+       request a launch takes when set */
+    uint8_t *d_win;
+    uint64_t win_cap;        /* windows d_win has room for */
+    const struct te_win_req_s *win_req;
+    uint64_t win_fallbacks;  /* fused runs that went the exact way */
     /* results */
     uint64_t counters[TE_CNT__N];
     uint64_t err[3];
@@ -846,6 +852,7 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_status);
     hipFree(b->d_scratch);
     hipFree(b->d_dirbits);
+    hipFree(b->d_win);
     hipFree(b->d_tiles);
     hipFree(b->d_pkt_rel);
     hipFree(b->d_ws);
@@ -1155,6 +1162,15 @@ static int fast_lane_off(void)
 }
 
 static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1, int generic_only);
+
+/* a window-mode launch (te_launch_t.win): the image's byte range and first record */
+typedef struct te_win_req_s {
+    uint64_t len, entry, entry_sub, base, limit;
+    const uint64_t *entry_ptr;
+    uint32_t nwin;
+} te_win_req_t;
+/* the window workspace layout of d_win for `cap` windows: entries | exits | flags | bad | tot */
+#define WIN_WS_BYTES(cap) (16ull * (cap) + 4ull * (cap) + 64)
 static int launch(tcpedit_batch_t *b, int fixed_dir)
 {
     return launch_ev(b, fixed_dir, NULL, NULL, 0);
@@ -1303,10 +1319,28 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     if (c->l2carry && !L.fast && b->n_pkts && l2carry_bufs(t, b, &L) < 0)
         return -1;
     L.any_dec = c->decoder != TE_DEC_EN10MB || c->encoder == TE_ENC_NOENC || c->encoder == TE_ENC_PPP;
+    if (b->win_req) { /* window mode: the wave lane finds the records (no tiles, no index) */
+        const te_win_req_t *q = b->win_req;
+        L.win = 1;
+        L.win_len = q->len;
+        L.win_entry = q->entry;
+        L.win_entry_ptr = q->entry_ptr;
+        L.win_entry_sub = q->entry_sub;
+        L.win_base = q->base;
+        L.win_limit = q->limit;
+        L.nwin = q->nwin;
+        L.w_entry = (uint64_t *)b->d_win;
+        L.w_exit = L.w_entry + b->win_cap;
+        L.w_flags = (uint32_t *)(L.w_exit + b->win_cap);
+        L.win_bad = L.w_flags + b->win_cap;
+        L.win_tot = (uint64_t *)(b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull));
+        L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
+        L.stream = (b->in_len + b->out_cap) > ((uint64_t)256 << 20);
+    }
     const int rc = te_launch_edit(&L, t->stream);
     if (!generic_only) {
         b->last_skipped = L.skip_generic;
-        b->last_fgrid = L.fast && b->fast_kind == TE_FAST_WAVE ? L.out_fgrid : 0;
+        b->last_fgrid = (L.fast && b->fast_kind == TE_FAST_WAVE) || L.win ? L.out_fgrid : 0;
     }
     return rc;
 }
@@ -1719,6 +1753,166 @@ int tcpedit_batch_update_input(tcpedit_t *t, tcpedit_batch_t *b, const void *img
 fail:
     return TCPEDIT_ERROR;
 }
+
+/* window mode's conditions: the wave lane's size-preserving instances over a native-order
+ * microsecond image without a tcpprep cache (the window mode has no record numbers) */
+static int fused_capable(const tcpedit_t *t, const tcpedit_batch_t *b)
+{
+    return b->fast_tiles && b->fast_kind == TE_FAST_WAVE && !b->slot_layout && static_capable(&t->cfg) &&
+           fast_capable(&t->cfg) && !b->has_zero_cap &&
+           !b->swapped && !b->nsec && !b->d_dirbits && !b->pre_host && !fast_lane_off() &&
+           b->stop_error_pkt < 0 && !b->walk_stop && b->n_pkts && !getenv("TCPEDIT_HIP_NO_FUSED");
+}
+
+static int win_ready(tcpedit_t *t, tcpedit_batch_t *b, uint64_t nwin)
+{
+    if (b->win_cap >= nwin)
+        return 0;
+    hipFree(b->d_win);
+    b->d_win = NULL;
+    b->win_cap = 0;
+    if (hipMalloc((void **)&b->d_win, WIN_WS_BYTES(nwin)) != hipSuccess) {
+        te_seterr(t, "out of device memory (window workspace)");
+        return -1;
+    }
+    b->win_cap = nwin;
+    return 0;
+}
+
+/* the window request over the batch's whole image */
+static void win_request(const tcpedit_batch_t *b, te_win_req_t *q)
+{
+    memset(q, 0, sizeof(*q));
+    q->len = b->in_len;
+    q->entry = b->rec0 ? b->rec0 : 24;
+    q->base = q->entry & ~15ull;
+    q->limit = b->walk_limit ? b->walk_limit : b->in_len;
+    q->nwin = (uint32_t)((q->limit - q->base + te_win_bytes() - 1) / te_win_bytes());
+}
+
+/* one window-mode run, results read back; 1 when the exact path has to run instead */
+static int fused_once(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    te_win_req_t q;
+    win_request(b, &q);
+    if (q.nwin == 0 || win_ready(t, b, q.nwin) < 0)
+        return 1;
+    out_header(t, b->ohdr);
+    HIPCHK(t, hipMemcpyAsync(b->d_out, b->ohdr, 24, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipEventRecord(b->ev0, t->stream));
+    b->win_req = &q;
+    const int lr = launch(b, -1);
+    b->win_req = NULL;
+    if (lr != 0)
+        return 1;
+    HIPCHK(t, hipEventRecord(b->ev1, t->stream));
+    uint32_t bad = 0;
+    uint64_t tot = 0;
+    const uint8_t *wb = b->d_win + 20ull * b->win_cap;
+    HIPCHK(t, hipMemcpyAsync(&bad, wb, 4, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipMemcpyAsync(&tot, b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull), 8, hipMemcpyDeviceToHost,
+                             t->stream));
+    if (!b->slots_host)
+        b->slots_host = malloc(32 * (size_t)te_wave_grid());
+    if (b->last_fgrid)
+        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
+                                 hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    memset(b->counters, 0, sizeof(b->counters));
+    for (int i = 0; i < b->last_fgrid; i++) {
+        const uint64_t *v = b->slots_host + 4 * (size_t)i;
+        b->counters[TE_CNT_PACKETS] += v[0];
+        b->counters[TE_CNT_WRITTEN] += v[0];
+        b->counters[TE_CNT_BYTES_IN] += v[1];
+        b->counters[TE_CNT_BYTES_OUT] += v[1];
+        b->counters[TE_CNT_EDITED] += v[2];
+    }
+    /* the chain ran where the host walk ran: to its end, every record (the index the batch
+       was opened with counts them) */
+    if (bad || tot != b->walk_end || b->counters[TE_CNT_PACKETS] != b->n_pkts || b->stop_error_pkt >= 0 ||
+        b->walk_stop)
+        return 1;
+    float ms = 0;
+    HIPCHK(t, hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->kernel_ms = ms;
+    HIPCHK(t, hipMemsetAsync(b->d_status, 0, b->n_pkts ? b->n_pkts : 1, t->stream)); /* every record OK */
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    b->err[0] = b->err[1] = ~0ull;
+    b->err[2] = 0;
+    b->last_fast = 1;
+    b->last_listed = 0;
+    b->ran = 1;
+    b->status_valid = 0;
+    t->pub.runtime.packetnum += b->counters[TE_CNT_PACKETS];
+    t->pub.runtime.total_bytes += b->counters[TE_CNT_BYTES_OUT];
+    t->pub.runtime.pkts_edited += b->counters[TE_CNT_EDITED];
+    return 0;
+fail:
+    return -1;
+}
+
+/* tcpedit_batch_run with the record discovery fused into the wave lane (window mode): no
+ * index pass and no tiles -- each wave finds the records of its byte window itself, edits
+ * them where they lie and the chain is checked across windows after.  Configs and images
+ * the window mode does not carry, and any batch where a window misses the chain or leaves
+ * a record to the generic lane, run the exact path (tcpedit_batch_run): the output is the
+ * same either way. */
+int tcpedit_batch_run_fused(tcpedit_t *t, tcpedit_batch_t *b)
+{
+    if (!t || !b)
+        return TCPEDIT_ERROR;
+    if (fused_capable(t, b)) {
+        if (te_upload_cfg(t) < 0)
+            return TCPEDIT_ERROR;
+        const int r = fused_once(t, b);
+        if (r == 0)
+            return TCPEDIT_OK;
+        if (r < 0)
+            return TCPEDIT_ERROR;
+        b->win_fallbacks++;
+    }
+    return tcpedit_batch_run(t, b);
+}
+
+/* K window-mode runs back to back (the device pipeline with the record discovery fused:
+ * the wave lane + the chain check), hipEvents around them; TCPEDIT_ERROR when the batch is
+ * not one the window mode carries */
+int tcpedit_batch_time_fused(tcpedit_t *t, tcpedit_batch_t *b, int iters, double *ms_per_run)
+{
+    hipEvent_t e0 = NULL, e1 = NULL;
+    float ms = 0;
+    int rc = TCPEDIT_ERROR;
+    if (!t || !b || iters <= 0 || !fused_capable(t, b) || te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    te_win_req_t q;
+    win_request(b, &q);
+    if (q.nwin == 0 || win_ready(t, b, q.nwin) < 0)
+        return TCPEDIT_ERROR;
+    HIPCHK(t, hipEventCreate(&e0));
+    HIPCHK(t, hipEventCreate(&e1));
+    HIPCHK(t, hipEventRecord(e0, t->stream));
+    b->win_req = &q;
+    for (int i = 0; i < iters; i++)
+        if (launch(b, -1) != 0) {
+            b->win_req = NULL;
+            te_seterr(t, "kernel launch failed");
+            goto fail;
+        }
+    b->win_req = NULL;
+    HIPCHK(t, hipEventRecord(e1, t->stream));
+    HIPCHK(t, hipEventSynchronize(e1));
+    HIPCHK(t, hipEventElapsedTime(&ms, e0, e1));
+    *ms_per_run = ms / iters;
+    rc = TCPEDIT_OK;
+fail:
+    if (e0)
+        hipEventDestroy(e0);
+    if (e1)
+        hipEventDestroy(e1);
+    return rc;
+}
+
+uint64_t tcpedit_batch_fused_fallbacks(tcpedit_batch_t *b) { return b ? b->win_fallbacks : 0; }
 
 int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
 {

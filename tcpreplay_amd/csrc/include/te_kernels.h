@@ -162,7 +162,22 @@ typedef struct {
     size_t l2carry_tmp_bytes;
     int any_dec;              /* a non-Ethernet decoder or a non-encoding / pppserial encoder: the
                                  generic kernel's instance that carries them */
+    /* window mode (te_launch_edit with win set): the wave lane finds the records itself, no
+       tiles or record index -- byte windows of the image from win_base, the first record at
+       win_entry (or *win_entry_ptr - win_entry_sub on the device), records starting at
+       win_limit on not the image's; te_win_check then checks the chain across windows */
+    int win;
+    uint64_t win_len, win_entry, win_entry_sub, win_base, win_limit;
+    const uint64_t *win_entry_ptr;
+    uint32_t nwin;
+    uint64_t *w_entry, *w_exit;  /* device: nwin words each */
+    uint32_t *w_flags;           /* device: nwin words */
+    uint32_t *win_bad;           /* device word, zeroed by the launch: bit 0 the chain missed or
+                                    stopped, bit 1 a record left to the exact path */
+    uint64_t *win_tot;           /* device: [0] the chain's end (image offset), zeroed by the launch */
 } te_launch_t;
+/* bytes a window of the window mode owns */
+uint32_t te_win_bytes(void);
 
 /* tcpedit_packet's resident server (te_packet_server, one block): a control block in
  * host-mapped fine-grained memory.  The host writes the record at byte 24 of the mapped

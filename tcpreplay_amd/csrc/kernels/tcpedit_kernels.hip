@@ -21,8 +21,10 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 #include "edit_pkt.hpp"
 #include "te_kernels.h"
+#include "te_window.hpp"
 
 using namespace te;
 
@@ -853,6 +855,17 @@ struct FastArgs {
     uint32_t vlan_tag_word;                 // GROW: the 4 pushed bytes {TPID, TCI} as a LE dword
     uint32_t stream;                        // nontemporal span loads and output stores (a batch larger
                                             // than the 256 MiB Infinity Cache: read once, written once)
+    // window mode (te_wave_tiles<..., WIN>: the record discovery fused into the edit)
+    uint64_t win_len;                       // image bytes (records end here)
+    uint64_t win_entry;                     // image offset of the first record, or, when set,
+    const uint64_t *win_entry_ptr;          //   *win_entry_ptr - win_entry_sub (a pipeline chunk:
+    uint64_t win_entry_sub;                 //   where the previous chunk's chain ended)
+    uint64_t win_base, win_limit;           // the window grid's origin; records starting at limit on
+                                            //   are not the image's
+    uint32_t nwin;
+    uint64_t *w_entry, *w_exit;             // per window: where the chain enters and leaves it
+    uint32_t *w_flags;                      // per window: IDX_STOP / IDX_ERROR / IDX_END / IDX_ZERO
+    uint32_t *win_bad;                      // bit 1: a window left a record to the exact path
 };
 
 // the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
@@ -1266,6 +1279,15 @@ constexpr int WK_NW = WKB / 64;                          // waves (tiles in flig
 constexpr int wk_kl(int tb) { return tb / 16 / 64; }
 constexpr int wk_img(int tb) { return LDS_FRONT + tb + 128; }
 constexpr int wk_nch(int tb) { return tb / 16 + 2; }
+// window mode: sub-window bytes per lane and lookback lanes of the discovery (te_window.hpp),
+// the bytes a window's last record may reach past the staged window (a longer one is left to
+// the exact path), and the window image: front pad, the staged window, that tail, slack
+constexpr int WIN_S = 64, WIN_OL = 7;
+constexpr int WIN_W = 64 * WIN_S, WIN_WN = WIN_W - WIN_OL * WIN_S;
+constexpr int WIN_TAIL = 2048;
+constexpr int WIN_IMG = LDS_FRONT + WIN_W + 48 + WIN_TAIL + 128;
+constexpr int WIN_REL = 4 * WIN_S + 1;
+static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
 static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
 static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
 static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
@@ -1534,9 +1556,16 @@ __device__ __forceinline__ void vdel_view(uint32_t (&H)[fl::NW], const uint32_t 
     for (int i = 4; i < fl::NW; ++i) H[i] = HX[i + 1];
 }
 
-template <uint32_t F, int DEPTH, int SZ>
-__global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
-    constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = wk_img(TB), WK_NCH = wk_nch(TB);
+// WIN: window mode -- no tile list: each wave takes byte windows of the image, finds the
+// records starting in its window (te_window.hpp), cuts them into tiles as the host would and
+// edits them in place in the staged window (size-preserving instances, native-order
+// microsecond input, no tcpprep cache).  Each window leaves where the chain enters and leaves
+// it for te_win_check; a record the lane cannot finish sets win_bad, and the caller then runs
+// the exact path (index + tiles) instead.
+template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
+__global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
+    constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
+    static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
     // VLAN pop: the window reaches 4 input bytes further (the packet' view skips the tag)
     constexpr int XW = VDEL ? 1 : 0;
@@ -1546,6 +1575,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
     __shared__ __attribute__((aligned(16))) uint8_t cfg_raw[WkCfg<F>::reads ? sizeof(te_dev_cfg_t) : 16];
     const te_dev_cfg_t &cfg = *(const te_dev_cfg_t *)cfg_raw;
     __shared__ unsigned long long red[WK_NW][3];
+    __shared__ uint32_t RELB[WIN ? WK_NW : 1][WIN ? WIN_REL : 1];  // window mode: record offsets
     const int tid = threadIdx.x;
     int lane = tid & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
@@ -1635,7 +1665,11 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
             const uint32_t g0 = (uint32_t)(G0 - A0);
             if (wk_solo(tile, TB)) {  // a record larger than the image: the generic lane
-                if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                if (WIN) {
+                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                } else if (lane == 0) {
+                    a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                }
                 return;
             }
 
@@ -1723,7 +1757,11 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             st.tail = st.tail && edit;
 #endif
             if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
-                if (lane == 0) a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                if (WIN) {  // (window mode: the exact path redoes the batch)
+                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                } else if (lane == 0) {
+                    a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
+                }
                 return;
             }
 
@@ -1802,7 +1840,9 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
                 // after the write-back, which rewrote len's bytes
                 if constexpr (GROW) hdr_add4(S, r0, 4u);
                 if constexpr (SHRINK) hdr_add4(S, r0, (uint32_t)-4);
-                ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
+                // (window mode: no record numbers; every record it finishes is status 0, which
+                // the caller writes for the whole batch)
+                if (!WIN) ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
             }
             if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
             if (GROW && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, 4u);
@@ -1879,6 +1919,72 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
         WK_STAMP(5)  // next span -> LDS (waits for its loads)
     };
 
+    if constexpr (WIN) {
+        // ---- window mode: wave w takes windows w, w + W, ... ----
+        IdxArgs ia;
+        ia.img = a.in;
+        ia.len = a.win_len;
+        ia.entry = a.win_entry;
+        ia.entry_ptr = a.win_entry_ptr;
+        ia.entry_sub = a.win_entry_sub;
+        ia.base = a.win_base;
+        ia.limit = a.win_limit;
+        ia.sw = 0;
+        ia.nsec = 0;
+        uint8_t *const IMG = SB[wid];       // the staged window at IMG + LDS_FRONT
+        uint32_t *const REL = RELB[WIN ? wid : 0];
+        for (uint32_t k = w0; k < a.nwin; k += W) {
+            const tew::Found fw = tew::find_window<WIN_S, WIN_OL>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+            const uint32_t wfl = fw.wstop | (fw.anyzero ? (uint32_t)IDX_ZERO : 0u);
+            if (lane == 0) {
+                a.w_entry[k] = fw.went;
+                a.w_exit[k] = fw.wexit;
+                a.w_flags[k] = wfl;
+            }
+            // a chain end or an empty record: te_win_check sends the batch to the exact path
+            if (wfl || fw.nrec == 0) continue;
+            // the bytes the window's last record reaches past the staged window, and the next
+            // record's header (the last output chunk's bytes): loaded now, or (too long) left
+            // to the exact path
+            const uint64_t need = fw.wexit + 16;
+            if (need > fw.staged_end) {
+                if (need - fw.A0 > (uint64_t)(WIN_W + 48 + WIN_TAIL)) {
+                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                    continue;
+                }
+                const uint64_t c0 = (fw.staged_end & ~15ull) - fw.A0, c1 = ((need + 15) & ~15ull) - fw.A0;
+                for (uint64_t c = c0 + 16ull * (uint32_t)lane; c < c1; c += 1024)
+                    *(uint4 *)(IMG + LDS_FRONT + c) = *(g_cu4 *)(gin + fw.A0 + c);
+                WK_LANES_SYNC();
+            }
+            // the tile cut walk_range makes: <= 64 records whose span fits the budget, a
+            // record too large for it alone (then left to the exact path by edit())
+            for (uint32_t s0 = 0; s0 < fw.nrec;) {
+                const uint32_t i = s0 + (uint32_t)lane;
+                const bool v = i < fw.nrec;
+                const uint32_t r = v ? REL[i] : 0u, r1 = v ? REL[i + 1] : 0u;
+                const uint32_t rs = REL[s0];
+                const uint64_t t0 = fw.ws + rs;
+                const bool fits = v && TE_CONTIG_FITS_IN((uint32_t)(t0 & 15), r1 - rs, (uint32_t)TB);
+                const unsigned long long brk = __ballot(lane > 0 && (!v || !fits));
+                const uint32_t len = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+                te_tile_t tl;
+                tl.span_off = t0;
+                tl.scratch_off = TE_NO_SCRATCH;
+                tl.first_pkt = 0;
+                tl.npkt = len;
+                tl.span_len = REL[s0 + len] - rs;
+                tl.flags = 0;
+                const uint32_t my_rel = (uint32_t)lane < len ? r - rs : REL[s0 + len - 1] - rs;
+                // the tile's image: its span start at S + LDS_FRONT + (span_off & 15)
+                S = IMG + (uint32_t)((t0 & ~15ull) - fw.A0);
+                WK_LANES_SYNC();
+                edit(k, tl, my_rel, 0u, false);
+                WK_LANES_SYNC();
+                s0 += len;
+            }
+        }
+    } else {
     Span RA, RB;
     if (w0 < n_tiles) issue(RA, tiles[w0]);
     if (DEPTH == 2 && w0 + W < n_tiles) issue(RB, tiles[w0 + W]);
@@ -1892,6 +1998,7 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
             if (t + W >= n_tiles) break;
             step(t + W, RB, RA);
         }
+    }
     }
 #undef WK_EACH
 #if TE_WK_STAMPS
@@ -1911,6 +2018,41 @@ __global__ void __launch_bounds__(WKB, WkCfg<F>::blocks) te_wave_tiles(FastArgs 
         for (int w = 0; w < WK_NW; ++w) s += red[w][tid];
         a.slots[4 * blockIdx.x + tid] = s;
     }
+}
+
+// ---------------------------------------------------------------------------
+// te_win_check: the window mode's cross-window chain check, one thread a window: a window's
+// first record must be where the chain left the nearest earlier window a record starts in
+// (the first window's, the known first record), and a window without one must be passed
+// over whole; a chain end, an empty record or a miss sends the batch to the exact path.
+// The chain's end (the next pipeline chunk's first record) is the largest exit.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long long *tot) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.nwin) return;
+    const uint64_t entry = a.win_entry_ptr ? *(const volatile uint64_t *)a.win_entry_ptr - a.win_entry_sub
+                                           : a.win_entry;
+    const uint32_t kE = (uint32_t)((entry - a.win_base) / WIN_WN);
+    if (k < kE) return;
+    const uint64_t went = a.w_entry[k];
+    bool bad = a.w_flags[k] != 0;
+    if (k == kE) {
+        bad |= went != entry;
+    } else {
+        uint32_t j = k - 1, steps = 0;
+        while (j > kE && a.w_entry[j] == IDX_NONE && ++steps < 4096) --j;
+        const uint64_t xj = a.w_exit[j];
+        if (a.w_entry[j] == IDX_NONE) {
+            bad = true;
+        } else if (went != IDX_NONE) {
+            bad |= xj != went;
+        } else {
+            const uint64_t qe = a.win_base + (uint64_t)(k + 1) * WIN_WN;
+            bad |= xj < (qe < a.win_limit ? qe : a.win_limit);
+        }
+    }
+    if (bad) atomicOr(a.win_bad, 1u);
+    if (went != IDX_NONE) atomicMax(&tot[0], (unsigned long long)a.w_exit[k]);
 }
 
 // ===========================================================================
@@ -2273,6 +2415,10 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
     X(TE_FF_ALL, 1, SZ_GROW) X(TE_FF_ALLH, 1, SZ_GROW) X(TE_FF_ALLX, 1, SZ_GROW)                      \
     X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)
+#define TE_WIN_INSTANCES(X)                                                                           \
+    X(0u, 1, SZ_NONE) X(TE_FF_SEED, 1, SZ_NONE) X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE)             \
+    X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE) X(TE_FF_SEED | TE_FF_INCR, 1, SZ_NONE)          \
+    X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE) X(TE_FF_ALLX, 1, SZ_NONE)
 static struct {
     uint32_t feat;
     int sz;
@@ -2282,6 +2428,17 @@ static struct {
 #define TE_WI(f, d, g) {f, g, (const void *)te_wave_tiles<f, d, g>, 0},
     TE_WAVE_INSTANCES(TE_WI)
 #undef TE_WI
+};
+
+// window-mode instances: the size-preserving ones
+static struct {
+    uint32_t feat;
+    const void *fn;
+    int grid;
+} win_inst[] = {
+#define TE_WW(f, d, g) {f, (const void *)te_wave_tiles<f, d, g, true>, 0},
+    TE_WIN_INSTANCES(TE_WW)
+#undef TE_WW
 };
 
 static uint32_t fast_feat(const te_dev_cfg_t *c);
@@ -2535,6 +2692,69 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     hipError_t e;
     const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink) &&
                       L->n_tiles > 0;
+    if (L->win) {  // window mode: the wave lane finds its records; then the chain check
+        if (!L->cfg_host || L->in_swapped || L->in_nsec || L->dirbits || L->nwin == 0) return -1;
+        FastArgs f;
+        memset(&f, 0, sizeof f);
+        f.cfg = L->cfg;
+        f.portlut = L->portlut;
+        f.in = L->in;
+        f.out = L->out;
+        f.status = L->status;
+        f.list_cnt_next = L->list_cnt + 1;
+        f.counters_next = (unsigned long long *)L->counters_next;
+        f.ws_zero = (unsigned long long *)L->ws_zero;
+        f.out_base = L->out_base;
+        f.rec0 = L->rec0;
+        f.fixed_dir = L->fixed_dir;
+        f.v6_ok = (uint32_t)L->fast_v6;
+        f.stream = (uint32_t)L->stream;
+        f.slots = (unsigned long long *)L->slots;
+        const te_dev_cfg_t *ch = L->cfg_host;
+        f.seed_sw = __builtin_bswap32(ch->seed);
+        f.seed_on = ch->seed != 0;
+        f.skip_bcast = ch->skip_broadcast != 0;
+        f.win_len = L->win_len;
+        f.win_entry = L->win_entry;
+        f.win_entry_ptr = L->win_entry_ptr;
+        f.win_entry_sub = L->win_entry_sub;
+        f.win_base = L->win_base;
+        f.win_limit = L->win_limit;
+        f.nwin = L->nwin;
+        f.w_entry = L->w_entry;
+        f.w_exit = L->w_exit;
+        f.w_flags = L->w_flags;
+        f.win_bad = L->win_bad;
+        const uint32_t want = fast_feat(ch);
+        int wk = -1;
+        for (int k = 0; k < (int)(sizeof(win_inst) / sizeof(win_inst[0])) && wk < 0; ++k)
+            if ((want & ~win_inst[k].feat) == 0 && ((want ^ win_inst[k].feat) & TE_FF_INCR) == 0) wk = k;
+        if (wk < 0) return -1;
+        if (!win_inst[wk].grid) {
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, win_inst[wk].fn, WKB, 0) != hipSuccess ||
+                per_cu < 1)
+                per_cu = 1;
+            win_inst[wk].grid = cu_count() * per_cu;
+        }
+        int grid = win_inst[wk].grid;
+        const uint32_t need = (L->nwin + WK_NW - 1) / WK_NW;
+        if ((uint32_t)grid > need) grid = (int)need;
+        if (grid < 1 || ((L->out_base - L->rec0) & 15)) return -1;
+        if (hipMemsetAsync(L->win_bad, 0, 4, stream) != hipSuccess ||
+            hipMemsetAsync(L->win_tot, 0, 8, stream) != hipSuccess)
+            return -1;
+        if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
+        {
+            void *args[] = {&f};
+            if (hipLaunchKernel(win_inst[wk].fn, dim3(grid), dim3(WKB), args, 0, stream) != hipSuccess) return -1;
+        }
+        hipLaunchKernelGGL(te_win_check, dim3((L->nwin + 255) / 256), dim3(256), 0, stream, f,
+                           (unsigned long long *)L->win_tot);
+        if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
+        L->out_fgrid = grid;
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (fast && !L->generic_only) {
         // the fast kernel zeroes the generic kernel's words itself: no memset launch
         FastArgs f;
@@ -2649,6 +2869,8 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
 }
+
+extern "C" uint32_t te_win_bytes(void) { return (uint32_t)WIN_WN; }
 
 extern "C" int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream) {
     hipLaunchKernelGGL(te_packet_server, dim3(1), dim3(BLOCK), 0, stream, *S);

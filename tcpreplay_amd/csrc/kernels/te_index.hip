@@ -37,17 +37,13 @@
 #include <stdint.h>
 
 #include "te_index.h"
+#include "te_window.hpp"
 
 namespace {
-typedef uint8_t u8;
-typedef uint16_t u16;
-typedef uint32_t u32;
-typedef uint64_t u64;
+using namespace tew;
 
-constexpr int IW = 64;                       // lanes (sub-windows) per window
 constexpr int IB = 256;                      // threads per block: 4 windows in flight
 constexpr int IWAVES = IB / IW;
-constexpr u32 MAXCAP = 262144u;
 constexpr int REC_BITS = 36;                 // a window's (records | tiles << 36)
 constexpr u64 REC_MASK = (1ull << REC_BITS) - 1;
 
@@ -63,71 +59,6 @@ struct WinLds {
     u64 pfx;                                 // the window's exclusive (records | tiles) prefix
 };
 
-__device__ __forceinline__ u32 lds_u32(const u32 *img, u32 p) {  // unaligned LDS dword
-    const u32 a = img[p >> 2], b = img[(p >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(b, a, p & 3u);
-}
-__device__ __forceinline__ u32 sw32(u32 v, bool sw) { return sw ? __builtin_bswap32(v) : v; }
-// a byte's zero mask over a dword: bit 8i+7 set iff byte i == 0 (exact)
-__device__ __forceinline__ u32 zero_bytes(u32 x) {
-    const u32 y = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
-    return ~(y | x | 0x7f7f7f7fu);
-}
-__device__ __forceinline__ u32 nib(u32 z) {  // 4 zero flags of a dword -> 4 bits
-    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-
-// one lane's walk over the records that start in [from, se), headers from LDS
-struct LaneWalk {
-    u64 exit;  // first record start >= se, or where the chain ended
-    u32 n;     // records taken
-    u32 stop;  // 0 goes on, IDX_STOP oversize, IDX_ERROR len > 262144, IDX_END truncated / no bytes
-};
-__device__ __forceinline__ LaneWalk walk_lds(const IdxArgs &a, const u32 *img, u64 A0, u64 from, u64 se) {
-    LaneWalk w{from, 0, 0};
-    u64 off = from;
-    while (off < se) {
-        if (off + 16 > a.len) {
-            w.stop = IDX_END;
-            break;
-        }
-        const u32 p = (u32)(off - A0);
-        const u32 cl = sw32(lds_u32(img, p + 8), a.sw), pl = sw32(lds_u32(img, p + 12), a.sw);
-        if (cl > MAXCAP) {
-            w.stop = IDX_STOP;
-            break;
-        }
-        if (off + 16 + cl > a.len) {
-            w.stop = IDX_END;
-            break;
-        }
-        if (pl > MAXCAP) {
-            w.stop = IDX_ERROR;
-            break;
-        }
-        ++w.n;
-        off += 16 + (u64)cl;
-    }
-    w.exit = off;
-    return w;
-}
-
-// a candidate's strength: 0 no header here, 1 a header whose successor is not staged (or
-// past the image), 2 a header followed by a staged acceptable one (or ending the image)
-__device__ __forceinline__ int strength(const IdxArgs &a, const u32 *img, u64 A0, u64 staged_end, u64 p) {
-    const u32 lim = a.nsec ? 1000000000u : 1000000u;
-    if (p + 16 > a.len) return 0;
-    u32 q = (u32)(p - A0);
-    u32 frac = sw32(lds_u32(img, q + 4), a.sw), cl = sw32(lds_u32(img, q + 8), a.sw), pl = sw32(lds_u32(img, q + 12), a.sw);
-    if (cl > MAXCAP || pl > MAXCAP || frac >= lim || p + 16 + cl > a.len) return 0;
-    p += 16 + (u64)cl;
-    if (p == a.len) return 2;
-    if (p + 16 > a.len || p + 16 > staged_end) return 1;
-    q = (u32)(p - A0);
-    frac = sw32(lds_u32(img, q + 4), a.sw), cl = sw32(lds_u32(img, q + 8), a.sw), pl = sw32(lds_u32(img, q + 12), a.sw);
-    return (cl > MAXCAP || pl > MAXCAP || frac >= lim || p + 16 + cl > a.len) ? 0 : 2;
-}
-
 // Window geometry: window k owns the record starts in [ws, we), ws = base + k WN.  Its wave
 // stages [ws - O, we + 16): the O = OL S bytes before the window are the first OL lanes'
 // sub-windows, whose only job is to establish the chain entering ws (a guess there that is
@@ -140,226 +71,11 @@ struct Facts {
 };
 template <int S, int OL>
 __device__ __forceinline__ Facts count_window(const IdxArgs &a, WinLds<S> &M, u32 k) {
-    constexpr int W = IW * S;       // staged sub-window bytes
-    constexpr int O = OL * S;       // overlap before the window
-    constexpr int WN = W - O;       // bytes a window owns
-    static_assert(S % 16 == 0 && S <= 128, "sub-window: whole 16-byte chunks, <= two 64-bit masks");
     const int lane = threadIdx.x & 63;
-
-    // the first record: known to the host (a.entry), or where the previous pipeline chunk's
-    // chain ended (read on the device: that chunk's index ran before this one on the stream)
-    const u64 entry = a.entry_ptr ? *(const volatile u64 *)a.entry_ptr - a.entry_sub : a.entry;
-    const u64 base = a.base;         // the window grid (16-aligned, <= entry)
-    const u64 limit = a.limit;       // records starting here or later are not this image's
-    const u32 kE = (u32)((entry - base) / WN);                     // the window of the first record
-    const int laneE = OL + (int)(((entry - base) % WN) / S);       // ... and its lane
-    const u64 ws = base + (u64)k * WN;
-    const u64 we = ws + WN < limit ? ws + WN : limit;
-    const u64 A0 = ws - O;          // lane l's sub-window starts at A0 + l S (window 0: none before base)
-    const u64 lo_stage = k ? A0 : base;
-    const u64 staged_end = we + 16;  // bytes [lo_stage, staged_end) are in LDS (past a.len: garbage)
-
-    // ---- stage the window: 16-byte chunks, all loads in flight before the LDS stores ----
-    {
-        const u32 c0 = (u32)((lo_stage - A0) >> 4);
-        const u32 nch = (u32)((staged_end - A0 + 15) >> 4);
-        const uint4 *g = (const uint4 *)(a.img + A0);
-        constexpr int K = (W + 48 + 16 * IW - 1) / (16 * IW);
-        uint4 v[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const u32 c = lane + i * IW;
-            v[i] = (c >= c0 && c < nch) ? g[c] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const u32 c = lane + i * IW;
-            if (c < nch && c < (u32)((W + 48) / 16)) *(uint4 *)&M.img[4 * c] = v[i];
-        }
-    }
-    // one wave's LDS accesses are performed in order; the empty asm keeps the compiler from
-    // moving a lane's reads of other lanes' stores across them (no block barrier: the
-    // block's waves work on their own windows and may have left already)
-    asm volatile("" ::: "memory");
-
-    // ---- this lane's guess: the first strong candidate in its sub-window, else the first weak ----
-    const u64 lo = A0 + (u64)lane * S, hi_raw = lo + S;
-    const u64 hi = hi_raw < we ? hi_raw : we;
-    const bool active = lo >= lo_stage && lo < we && (k > kE || (k == kE && lane > laneE));
-    u64 e = IDX_NONE;
-    if (k == kE && lane == laneE) {
-        e = entry;  // the first record is known
-    } else if (active) {
-        // zero flags of bytes [lo, lo + S + 16): dword d of the sub-window holds bytes 4d..4d+3
-        const u32 q0 = (u32)(lo - A0);  // lane S: a multiple of 16
-        u64 z[3] = {0, 0, 0};
-#pragma unroll
-        for (int d = 0; d < S / 4 + 4; ++d) {
-            const u64 f = (u64)nib(zero_bytes(M.img[(q0 >> 2) + d])) << ((4 * d) & 63);
-            z[(4 * d) >> 6] |= f;
-        }
-        auto bits_at = [&](int h, int sh) -> unsigned long long {  // bits 64h + j (j < 64) of z >> sh
-            return sh == 0 ? z[h] : (z[h] >> sh) | (z[h + 1] << (64 - sh));
-        };
-        // a header has a zero byte at +11 and +15 (caplen, len <= 262144), and at +7 when the
-        // fraction counts microseconds (< 10^6) -- the high bytes: +8, +12 and +4 in a
-        // big-endian capture
-        const bool us = !a.nsec;
-        const int zc = a.sw ? 8 : 11, zl = a.sw ? 12 : 15, zf = a.sw ? 4 : 7;
-        u64 weak = IDX_NONE;
-#pragma unroll
-        for (int h = 0; h < (S + 63) / 64; ++h) {
-            if (e != IDX_NONE) break;
-            unsigned long long m = bits_at(h, zc) & bits_at(h, zl) & (us ? bits_at(h, zf) : ~0ull);
-            const int span = S - 64 * h;
-            if (span < 64) m &= (1ull << span) - 1ull;
-            while (m) {
-                const int j = __builtin_ctzll(m);
-                m &= m - 1;
-                const u64 c = lo + 64 * h + j;
-                if (c >= hi) break;
-                const int st = strength(a, M.img, A0, staged_end, c);
-                if (st == 2) {
-                    e = c;
-                    break;
-                }
-                if (st == 1 && weak == IDX_NONE) weak = c;
-            }
-        }
-        if (e == IDX_NONE) e = weak;
-    }
-    LaneWalk w = e != IDX_NONE ? walk_lds(a, M.img, A0, e, hi) : LaneWalk{0, 0, 0};
-    bool has = e != IDX_NONE;
-
-    // ---- where the chain starts: the first guess the next guess confirms (its walk ends
-    // exactly there, or at a strong candidate).  A guess that is not a record start jumps by a garbage length, so it is
-    // confirmed only when it lands on the chain anyway (and then the chain is right from
-    // there on); window 0's known first record needs no confirmation ----
-    {
-        int nsrc = has ? lane : 64;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_down(nsrc, o, 64);
-            if (lane + o < 64 && y < nsrc) nsrc = y;
-        }
-        int nxt = __shfl_down(nsrc, 1, 64);
-        if (lane == 63) nxt = 64;
-        const u64 ng = __shfl(e, nxt < 64 ? nxt : 0);
-        // (or its walk ends at a strong candidate inside the window: a wrong guess next to a
-        // record start would otherwise hide the record start's confirmation)
-        const bool confirmed = has && !w.stop &&
-                               ((nxt < 64 && w.exit == ng) ||
-                                (w.exit < we && strength(a, M.img, A0, staged_end, w.exit) == 2));
-        const u64 cm = __ballot(confirmed), hm0 = __ballot(has);
-        const int start = k == kE ? laneE : (cm ? __builtin_ctzll(cm) : (hm0 ? __builtin_ctzll(hm0) : 64));
-        if (lane < start) {
-            has = false;
-            e = IDX_NONE;
-        }
-    }
-
-    // ---- the exact chain: the chain's first guess is trusted (the overlap lanes' chain, or window 0's
-    // known first record); after it, lane l's first record must be where the nearest earlier
-    // guessing lane's walk ended (P), and no lane the chain passes over may keep a guess.
-    // Jacobi rounds, each fixing at least the first inconsistent lane, until every lane agrees
-    // (in practice one or two); the serial lane loop after 8 rounds ----
-    bool settled = false;
-    for (int round = 0; round < 8; ++round) {
-        int src = has ? lane : -1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(src, o, 64);
-            if (lane >= o && y > src) src = y;
-        }
-        int prev = __shfl_up(src, 1, 64);
-        if (lane == 0) prev = -1;
-        const u64 P = __shfl(w.exit, prev < 0 ? 0 : prev);
-        const u32 pstop = (u32)__shfl((int)w.stop, prev < 0 ? 0 : prev);
-        bool change = false;
-        if (prev >= 0 && active) {
-            if (pstop) {  // the chain ended before this lane
-                change = has;
-                has = false;
-            } else if (P < lo) {  // (an earlier lane without a guess takes it first)
-            } else if (P < hi) {  // the chain enters this sub-window at P
-                if (!has || e != P) {
-                    e = P;
-                    w = walk_lds(a, M.img, A0, P, hi);
-                    has = true;
-                    change = true;
-                }
-            } else if (has) {  // the chain passes over it
-                has = false;
-                change = true;
-            }
-        }
-        if (!__ballot(change)) {
-            settled = true;
-            break;
-        }
-    }
-    if (!settled) {  // the serial lane loop (exact)
-        u64 cur = IDX_NONE;
-        u32 ended = 0;
-        for (u32 l = 0; l < IW; ++l) {
-            const u64 ll = A0 + (u64)l * S, lh = ll + S < we ? ll + S : we;
-            const bool act = ll >= lo_stage && ll < we && (k > kE || (k == kE && (int)l >= laneE));
-            const bool hl = __shfl((int)has, (int)l) != 0;
-            if (!act || ended) {
-                if (lane == (int)l) has = false;
-                continue;
-            }
-            if (cur == IDX_NONE) {
-                if (hl) {
-                    cur = __shfl(w.exit, (int)l);
-                    ended = (u32)__shfl((int)w.stop, (int)l);
-                }
-                continue;
-            }
-            if (cur >= lh) {
-                if (lane == (int)l) has = false;
-                continue;
-            }
-            if (lane == (int)l && (!has || e != cur)) {
-                e = cur;
-                w = walk_lds(a, M.img, A0, cur, lh);
-                has = true;
-            }
-            cur = __shfl(w.exit, (int)l);
-            ended = (u32)__shfl((int)w.stop, (int)l);
-        }
-    }
-    // only the window's own lanes' records count (the overlap's are window k - 1's)
-    if (lane < OL) has = false;
-    // the window's entry, exit and how the chain ends here
-    const u64 hm = __ballot(has);
-    const int fl = hm ? __builtin_ctzll(hm) : 0, ll = hm ? 63 - __builtin_clzll(hm) : 0;
-    const u64 went = hm ? __shfl(e, fl) : IDX_NONE;
-    const u64 wexit = hm ? __shfl(w.exit, ll) : IDX_NONE;
-    const u32 wstop = hm ? (u32)__shfl((int)w.stop, ll) : 0u;
-    // ---- the window's records: positions (wave scan), offsets into LDS ----
-    const u32 n = has ? w.n : 0;
-    u32 pos = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = __shfl_up(pos, o, 64);
-        if (lane >= o) pos += y;
-    }
-    const u32 nrec = __shfl(pos, 63);
-    pos -= n;
-    bool zero = false;
-    if (has) {
-        u64 off = e;
-        for (u32 i = 0; i < w.n; ++i) {
-            M.rel[pos + i] = (u32)(off - ws);
-            const u32 cl = sw32(lds_u32(M.img, (u32)(off - A0) + 8), a.sw);
-            zero |= cl == 0;
-            off += 16 + (u64)cl;
-            if (pos + i + 1 == nrec) M.rel[nrec] = (u32)(off - ws);  // the last record's end
-        }
-    }
-    const bool anyzero = __ballot(zero) != 0;
-    asm volatile("" ::: "memory");
+    const tew::Found fw = tew::find_window<S, OL>(a, M.img, M.rel, k);
+    const u64 ws = fw.ws, went = fw.went, wexit = fw.wexit;
+    const u32 wstop = fw.wstop, nrec = fw.nrec;
+    const bool anyzero = fw.anyzero;
 
     // ---- the tile cut: one ballot per tile ----
     u32 ntile = 0;
