@@ -61,7 +61,12 @@ ETH_LINES = [
 
 @pytest.fixture(scope="module")
 def emu(built):
-    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "emu")])
+    # one build at a time (pytest -n: every worker asks for it), under a lock file
+    import fcntl
+    os.makedirs(os.path.dirname(EMU), exist_ok=True)
+    with open(EMU + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "emu")])
     return EMU
 
 
