@@ -289,6 +289,17 @@ int tcpedit_fuzz_skip(tcpedit_t *tcpedit, uint64_t draws);
  * tcpedit_set_l2carry: seed the context with the nearest earlier shard's value. */
 int tcpedit_batch_l2carry_out(tcpedit_t *tcpedit, tcpedit_batch_t *b);
 int tcpedit_set_l2carry(tcpedit_t *tcpedit, int value);
+
+/* DLT_JUNIPER_ETHER across shards (jnpr_ether.c:269-272: a frame whose extensions are not
+ * Ethernet is encoded with the decoder state the last whole inner decode left): the state
+ * the batch's last whole decode leaves, TCPEDIT_JNPR_STATE_BYTES into `state` -- 1 when
+ * the batch has one, 0 when not (or a config without the carry), found before any edit;
+ * and seeding a context with an earlier shard's (NULL: the capture's start; unknown = 1:
+ * not known, a frame that needs it then fails loudly).  Exchange these before the Q18
+ * carry-out (tcpedit_batch_l2carry_out reads the seeded state). */
+#define TCPEDIT_JNPR_STATE_BYTES 48
+int tcpedit_batch_jnpr_out(tcpedit_t *tcpedit, tcpedit_batch_t *b, void *state, size_t len);
+int tcpedit_set_jnpr_state(tcpedit_t *tcpedit, const void *state, size_t len, int unknown);
 /* tcpedit_batch_run with the record discovery fused into the edit (the window mode of the
  * wave lane): no index pass or tiles, each wave finds the records of a byte window of the
  * image and edits them in place, the chain checked across windows after.  Batches it does

@@ -192,6 +192,9 @@ typedef struct {
     uint32_t vlan_offset;
     uint16_t vlan_tag, vlan_pri, vlan_cfi, vlan_proto;
     bool src_modified, dst_modified;
+    /* DLT_JUNIPER_ETHER: a whole inner decode has been copied in (the encoder's extra is
+       the en10mb sub-decoder's from then on, dlt_utils.c:261-263) */
+    bool jnpr_sub;
 } ostate_t;
 
 typedef struct {
@@ -1662,10 +1665,30 @@ static int jnpr_decode(ostate_t *s, const uint8_t *pkt, int pktlen)
         seterr("packet DLT %d and encapsulation type %u not supported", dlt, encap);
         return TCPEDIT_WARN;
     }
-    /* the sub-decoder (an en10mb context of its own: its l2offset is not copied back) */
-    if (en10mb_decode(s, pkt + hl, pktlen - hl) == TCPEDIT_ERROR)
+    /* the sub-decoder: an en10mb context of its own (config->subctx, jnpr_ether.c:135-136,276)
+       whose state is copied into ours only after a whole decode (:280, dlt_utils.c:249-271:
+       addresses, proto, the extra by pointer, the l2lens added; not its l2offset) -- a decode
+       that fails part-way leaves ours as the last whole one left it, which is what a later
+       TCPEDIT_WARN frame encodes with.  Until the first whole decode the encoder's extra is
+       our own zeroed one; from it on it is the sub-decoder's, whose dst_modified/src_modified
+       no encode has written yet (en10mb_decode never writes them). */
+    ostate_t sub = *s;
+    if (en10mb_decode(&sub, pkt + hl, pktlen - hl) == TCPEDIT_ERROR)
         return TCPEDIT_ERROR;
-    s->l2len += hl;
+    memcpy(s->dstaddr, sub.dstaddr, 6);
+    memcpy(s->srcaddr, sub.srcaddr, 6);
+    s->proto = sub.proto;
+    s->vlan = sub.vlan;
+    s->vlan_offset = sub.vlan_offset;
+    s->vlan_tag = sub.vlan_tag;
+    s->vlan_pri = sub.vlan_pri;
+    s->vlan_cfi = sub.vlan_cfi;
+    s->vlan_proto = sub.vlan_proto;
+    if (!s->jnpr_sub) {
+        s->jnpr_sub = true;
+        s->dst_modified = s->src_modified = false;
+    }
+    s->l2len = hl + sub.l2len;
     s->l2offset = 0;
     return TCPEDIT_OK;
 }

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("TCPEDIT_HIP_LIB") or os.path.join(HERE, "lib", "libtc
 
 TCPEDIT_SOFT_ERROR, TCPEDIT_ERROR, TCPEDIT_OK, TCPEDIT_WARN = -2, -1, 0, 1
 TCPR_DIR_NOSEND, TCPR_DIR_C2S, TCPR_DIR_S2C = 0, 1, 2
+JNPR_STATE_BYTES = 48  # TCPEDIT_JNPR_STATE_BYTES
 
 
 class ST:
@@ -93,6 +94,8 @@ def load():
         "tcpedit_fuzz_skip": (c_int, [vp, u64]),
         "tcpedit_batch_l2carry_out": (c_int, [vp, vp]),
         "tcpedit_set_l2carry": (c_int, [vp, c_int]),
+        "tcpedit_batch_jnpr_out": (c_int, [vp, vp, vp, ctypes.c_size_t]),
+        "tcpedit_set_jnpr_state": (c_int, [vp, vp, ctypes.c_size_t, c_int]),
         "tcpedit_batch_device_output": (vp, [vp]),
         "tcpedit_batch_input_bytes": (u64, [vp]),
         "tcpedit_rewrite_pcap": (c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(sz)]),
@@ -245,6 +248,14 @@ class TcpEdit:
         """seed the en10mb encoder's dst_modified carry as an earlier shard
         left it (tcpedit_set_l2carry)"""
         if self._L.tcpedit_set_l2carry(self._ctx, int(value)) < 0:
+            raise RuntimeError(self.geterr())
+
+    def set_jnpr_state(self, state=None, unknown: bool = False):
+        """seed the Juniper decoder state (the state a frame whose extensions are not Ethernet
+        is encoded with, jnpr_ether.c:269-272) as an earlier shard left it (Batch.jnpr_out);
+        None: the capture's start (tcpedit_set_jnpr_state)"""
+        buf = ctypes.create_string_buffer(bytes(state), JNPR_STATE_BYTES) if state is not None else None
+        if self._L.tcpedit_set_jnpr_state(self._ctx, buf, JNPR_STATE_BYTES, 1 if unknown else 0) < 0:
             raise RuntimeError(self.geterr())
 
     def packet(self, hdr, data: bytearray, direction=TCPR_DIR_C2S):
@@ -451,6 +462,15 @@ class Batch:
         if v < 0:
             raise RuntimeError(self._te.geterr())
         return int(v)
+
+    def jnpr_out(self):
+        """(has one, state bytes): the Juniper decoder state this batch's last whole inner
+        decode leaves (tcpedit_batch_jnpr_out), found before any edit"""
+        buf = ctypes.create_string_buffer(JNPR_STATE_BYTES)
+        v = self._L.tcpedit_batch_jnpr_out(self._te._ctx, self._b, buf, JNPR_STATE_BYTES)
+        if v < 0:
+            raise RuntimeError(self._te.geterr())
+        return v == 1, buf.raw
 
     def time(self, iters):
         ms = ctypes.c_double()

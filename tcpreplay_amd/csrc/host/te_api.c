@@ -110,6 +110,10 @@ struct tcpedit_batch_s {
     uint64_t l2carry_cap;
     void *d_l2tmp;           /* ... and the scan's scratch */
     size_t l2tmp_bytes;
+    uint8_t *d_jnpr;         /* DLT_JUNIPER_ETHER: (jnpr_cap + 1) x {scan, key, 32-byte state} */
+    uint64_t jnpr_cap;
+    void *d_jtmp;
+    size_t jtmp_bytes;
     uint32_t *d_fuzz;        /* --fuzz-seed: per-record RNG states, then a word per 1024 records */
     uint64_t fuzz_cap;       /* records d_fuzz has room for */
     int fuzz_probe_only;     /* the next launch only counts records reaching the fuzz step */
@@ -859,6 +863,8 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_tile_list);
     hipFree(b->d_fuzz);
     hipFree(b->d_l2carry);
+    hipFree(b->d_jnpr);
+    hipFree(b->d_jtmp);
     hipFree(b->d_l2tmp);
     b->d_l2carry = NULL;
     b->d_l2tmp = NULL;
@@ -1178,6 +1184,56 @@ static int launch(tcpedit_batch_t *b, int fixed_dir)
 
 /* the dst_modified carry's buffers for a launch over b (the context's word,
  * zeroed when first allocated: the reference's zeroed en10mb extra) */
+/* DLT_JUNIPER_ETHER into an encoder that reads the decoder state (en10mb, user, hdlc; the
+ * Juniper plugin's own encoder refuses every record, pppserial passes it through) */
+static int jnpr_carry_cfg(const te_dev_cfg_t *c)
+{
+    return c->decoder == TE_DEC_JNPR &&
+           (c->encoder == TE_ENC_EN10MB || c->encoder == TE_ENC_USER || c->encoder == TE_ENC_HDLC);
+}
+
+static int jctx_ready(tcpedit_t *t)
+{
+    if (t->d_jctx)
+        return 0;
+    if (hipMalloc((void **)&t->d_jctx, sizeof(te_jctx_t)) != hipSuccess ||
+        hipMemsetAsync(t->d_jctx, 0, sizeof(te_jctx_t), t->stream) != hipSuccess) { /* TE_JC_NONE */
+        t->d_jctx = NULL;
+        te_seterr(t, "out of device memory (Juniper decoder state)");
+        return -1;
+    }
+    return 0;
+}
+
+/* the Juniper decoder-state scan's buffers for a launch over b */
+static int jnpr_bufs(tcpedit_t *t, tcpedit_batch_t *b, te_launch_t *L)
+{
+    if (b->n_pkts >= 0xffffffffull || jctx_ready(t) < 0)
+        return -1;
+    if (b->jnpr_cap < b->n_pkts) {
+        hipFree(b->d_jnpr);
+        hipFree(b->d_jtmp);
+        b->d_jnpr = NULL;
+        b->d_jtmp = NULL;
+        b->jnpr_cap = 0;
+        b->jtmp_bytes = te_l2carry_temp_bytes((uint32_t)b->n_pkts);
+        if (!b->jtmp_bytes || hipMalloc((void **)&b->d_jnpr, 48 * (b->n_pkts + 1)) != hipSuccess ||
+            hipMalloc(&b->d_jtmp, b->jtmp_bytes) != hipSuccess) {
+            te_seterr(t, "out of device memory (Juniper decoder state)");
+            return -1;
+        }
+        b->jnpr_cap = b->n_pkts;
+    }
+    L->n_pkts = (uint32_t)b->n_pkts;
+    L->jscan = (uint64_t *)b->d_jnpr;
+    L->jkeys = L->jscan + b->jnpr_cap + 1;
+    L->jstates = (te_jstate_t *)(L->jkeys + b->jnpr_cap + 1);
+    L->jctx = t->d_jctx;
+    L->jtmp = b->d_jtmp;
+    L->jtmp_bytes = b->jtmp_bytes;
+    return 0;
+}
+
 static int l2carry_bufs(tcpedit_t *t, tcpedit_batch_t *b, te_launch_t *L)
 {
     if (b->n_pkts >= 0xffffffffull)
@@ -1318,6 +1374,8 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     }
     if (c->l2carry && !L.fast && b->n_pkts && l2carry_bufs(t, b, &L) < 0)
         return -1;
+    if (jnpr_carry_cfg(c) && !L.fast && b->n_pkts && jnpr_bufs(t, b, &L) < 0)
+        return -1;
     L.any_dec = c->decoder != TE_DEC_EN10MB || c->encoder == TE_ENC_NOENC || c->encoder == TE_ENC_PPP;
     if (b->win_req) { /* window mode: the wave lane finds the records (no tiles, no index) */
         const te_win_req_t *q = b->win_req;
@@ -1408,6 +1466,13 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
         L.fuzz_states = b->d_fuzz;
     if (t->cfg.l2carry && !b->last_fast)
         L.l2carry = b->d_l2carry; /* the last launch's scan: each replayed record's carried value */
+    if (jnpr_carry_cfg(&t->cfg) && !b->last_fast && b->d_jnpr && b->jnpr_cap >= b->n_pkts) {
+        /* ... and each replayed record's Juniper decoder state (the context's word now holds
+           the launch's last: a record with none before it in the launch is not replayed) */
+        L.jscan = (uint64_t *)b->d_jnpr;
+        L.jstates = (te_jstate_t *)(L.jscan + 2 * (b->jnpr_cap + 1));
+        L.jctx = t->d_jctx;
+    }
     if (te_launch_q8(&L, st) != 0) {
         te_seterr(t, "stale-buffer replay launch failed: %s", hipGetErrorString(hipGetLastError()));
         return -1;
@@ -1676,7 +1741,7 @@ int tcpedit_batch_l2carry_out(tcpedit_t *t, tcpedit_batch_t *b)
     L.n_tiles = (uint32_t)b->n_tiles;
     L.in_swapped = (uint32_t)b->swapped;
     L.in_nsec = (uint32_t)b->nsec;
-    if (l2carry_bufs(t, b, &L) < 0)
+    if (l2carry_bufs(t, b, &L) < 0 || (jnpr_carry_cfg(&t->cfg) && jnpr_bufs(t, b, &L) < 0))
         return TCPEDIT_ERROR;
     if (te_launch_l2carry(&L, t->stream) != 0) {
         te_seterr(t, "dst_modified carry launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1701,6 +1766,82 @@ int tcpedit_set_l2carry(tcpedit_t *t, int value)
         HIPCHK(t, hipMalloc((void **)&t->d_l2word, sizeof(uint32_t)));
     const uint32_t w = (uint32_t)value;
     HIPCHK(t, hipMemcpyAsync(t->d_l2word, &w, sizeof(w), hipMemcpyHostToDevice, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    return TCPEDIT_OK;
+fail:
+    return TCPEDIT_ERROR;
+}
+
+/* DLT_JUNIPER_ETHER across shards: the decoder state the batch's last whole inner decode
+ * leaves (TCPEDIT_JNPR_STATE_BYTES into `state`), found by the state scan before any edit;
+ * 1 when the batch has such a decode, 0 when none (the carry passes through), also for a
+ * config without the carry.  A whole decode reads no carried state, so the ranks of a
+ * sharded job can exchange these first and seed each context with the nearest earlier
+ * shard's (tcpedit_set_jnpr_state) before the Q18 carry-out, which reads it. */
+int tcpedit_batch_jnpr_out(tcpedit_t *t, tcpedit_batch_t *b, void *state, size_t len)
+{
+    if (!t || !b || !state || len < sizeof(te_jctx_t))
+        return TCPEDIT_ERROR;
+    memset(state, 0, sizeof(te_jctx_t));
+    if (te_upload_cfg(t) < 0)
+        return TCPEDIT_ERROR;
+    if (!jnpr_carry_cfg(&t->cfg) || !b->n_pkts)
+        return 0;
+    te_launch_t L;
+    memset(&L, 0, sizeof(L));
+    L.cfg = t->d_cfg;
+    L.cfg_host = &t->cfg;
+    L.dirbits = b->d_dirbits;
+    L.dirbits_len = b->dirbits_len;
+    L.pkt_base = b->pkt_base;
+    L.fixed_dir = -1;
+    L.in = b->d_in;
+    L.tiles = b->d_tiles;
+    L.pkt_rel = b->d_pkt_rel;
+    L.n_tiles = (uint32_t)b->n_tiles;
+    L.in_swapped = (uint32_t)b->swapped;
+    L.in_nsec = (uint32_t)b->nsec;
+    te_jctx_t *d_out = NULL;
+    te_jctx_t h;
+    if (jnpr_bufs(t, b, &L) < 0)
+        return TCPEDIT_ERROR;
+    HIPCHK(t, hipMalloc((void **)&d_out, sizeof(te_jctx_t)));
+    if (te_launch_jnpr(&L, d_out, t->stream) != 0) {
+        te_seterr(t, "Juniper decoder-state launch failed: %s", hipGetErrorString(hipGetLastError()));
+        hipFree(d_out);
+        return TCPEDIT_ERROR;
+    }
+    HIPCHK(t, hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(t, hipStreamSynchronize(t->stream));
+    hipFree(d_out);
+    memcpy(state, &h, sizeof(h));
+    return h.valid == TE_JC_VALID ? 1 : 0;
+fail:
+    hipFree(d_out);
+    return TCPEDIT_ERROR;
+}
+
+/* seed the context's Juniper decoder state as an earlier shard left it: `state` from
+ * tcpedit_batch_jnpr_out (1 returned there), or NULL for none before (the capture's start);
+ * unknown = 1 marks it not known (a frame that needs it then fails loudly) */
+int tcpedit_set_jnpr_state(tcpedit_t *t, const void *state, size_t len, int unknown)
+{
+    if (!t || (state && len < sizeof(te_jctx_t)))
+        return TCPEDIT_ERROR;
+    if (te_upload_cfg(t) < 0 || jctx_ready(t) < 0)
+        return TCPEDIT_ERROR;
+    te_jctx_t h;
+    memset(&h, 0, sizeof(h));
+    if (state) {
+        memcpy(&h, state, sizeof(h));
+        if (h.valid != TE_JC_VALID && h.valid != TE_JC_NONE) {
+            te_seterr(t, "not a Juniper decoder state");
+            return TCPEDIT_ERROR;
+        }
+    }
+    if (unknown)
+        h.valid = TE_JC_UNKNOWN;
+    HIPCHK(t, hipMemcpyAsync(t->d_jctx, &h, sizeof(h), hipMemcpyHostToDevice, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
     return TCPEDIT_OK;
 fail:
@@ -3832,7 +3973,8 @@ static int packet_via_server(tcpedit_t *t, struct pcap_pkthdr *h, unsigned char 
     if (!srv_enabled() || (t->srv && t->srv->broken))
         return TE_SRV_DECLINED;
     const te_dev_cfg_t *c = &t->cfg;
-    if (c->fuzz_seed || (TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB && !(c->mac_mask & TE_MASK_DMAC1)))
+    if (c->fuzz_seed || (TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB && !(c->mac_mask & TE_MASK_DMAC1)) ||
+        jnpr_carry_cfg(c)) /* (the Juniper decoder state: the launch path carries it) */
         return TE_SRV_DECLINED;
     const uint32_t caplen = h->caplen;
     uint64_t data = caplen;
@@ -3983,6 +4125,7 @@ int tcpedit_close(tcpedit_t **tp)
     hipFree(t->d_portlut);
     hipFree(t->d_fuzz_words);
     hipFree(t->d_l2word);
+    hipFree(t->d_jctx);
     hipFree(t->d_q8_scratch);
     te_pipe_free(t);
     if (t->stream)

@@ -599,7 +599,8 @@ int te_decoder_l2len(int dec)
     case TE_DEC_NULL:
     case TE_DEC_PPP:
     case TE_DEC_CHDLC: return 4;
-    case TE_DEC_JNPR: return 20;     /* the 6-byte Juniper header and the inner Ethernet, at least */
+    case TE_DEC_JNPR: return 6;      /* the 6-byte Juniper header alone: a frame whose extensions
+                                        are not Ethernet (TCPEDIT_WARN) decodes to just it */
     case TE_DEC_80211: return 24;    /* ieee80211_hdr_t, at least */
     case TE_DEC_RADIOTAP: return 24; /* (never encoded: every record is a soft error) */
     default: return 14;

@@ -79,6 +79,7 @@ struct tcpedit_s {
     uint32_t *d_fuzz_words;       /* --fuzz-seed: [0] the running RNG state (te_launch_t.fuzz_words) */
     uint8_t *d_q8_scratch;        /* te_q8_replay's emulated static buffers (allocated on first use) */
     uint32_t *d_l2word;           /* the en10mb encoder's dst_modified after the last launch */
+    te_jctx_t *d_jctx;            /* DLT_JUNIPER_ETHER: the decoder state the last whole inner decode left */
     int dev_dirty;                /* cfg changed since last upload */
     uint32_t cfg_gen;             /* uploads so far (batches key cached launch hints to it) */
     tcpedit_batch_t *one;         /* reusable one-record batch for tcpedit_packet() */

@@ -67,6 +67,32 @@ extern "C" {
     ((((uint32_t)(head) + (uint32_t)(g) + 16u + (uint32_t)(data) + (uint32_t)TE_TAIL_BYTES) + 15u) & ~15u)
 #define TE_SLOT_BYTES_OF(g, data) TE_SLOT_BYTES_OF_H(TE_HEAD, g, data)
 
+/* DLT_JUNIPER_ETHER: the decoder state a whole inner decode leaves in the encoder's
+ * context (tcpedit_dlt_copy_decoder_state, dlt_utils.c:249-271: addresses, proto, and by
+ * the extra pointer the en10mb sub-decoder's VLAN fields), which a later frame whose
+ * extensions are not Ethernet -- the reference's TCPEDIT_WARN, jnpr_ether.c:269-272 --
+ * is encoded with */
+typedef struct {
+    uint8_t dstaddr[6], srcaddr[6];
+    uint16_t proto;
+    uint16_t vlan_tag, vlan_pri, vlan_cfi, vlan_proto;
+    uint16_t pad0_;
+    uint32_t vlan_offset;
+    uint8_t vlan;
+    uint8_t pad1_[3];
+} te_jstate_t;
+/* the context's carried state: TE_JC_NONE no whole decode yet (the encoder's own zeroed
+ * extra), TE_JC_VALID the state in .st, TE_JC_UNKNOWN not known here (a shard that starts
+ * mid-capture before its carry-in was set: such a frame fails loudly) */
+typedef struct {
+    te_jstate_t st;
+    uint32_t valid;
+    uint32_t pad_[3];
+} te_jctx_t;
+#define TE_JC_NONE 0u
+#define TE_JC_VALID 1u
+#define TE_JC_UNKNOWN 2u
+
 /* A tile = a run of consecutive pcap records processed by one block. */
 typedef struct {
     uint64_t span_off;    /* HBM offset of the first record (its 16-byte header) */
@@ -160,6 +186,15 @@ typedef struct {
     uint32_t *l2carry_word;   /* device: the context's value after its last launch */
     void *l2carry_tmp;        /* device: te_l2carry_temp_bytes(n_pkts) of scan scratch */
     size_t l2carry_tmp_bytes;
+    /* DLT_JUNIPER_ETHER into an encoder that reads the decoder state: each record's last
+       whole inner decode before it (te_jnpr_mark + an inclusive max scan: jscan[j] = i + 1
+       for record i, 0 = none in the launch, then *jctx).  NULL: none */
+    uint64_t *jscan;          /* device: n_pkts + 1 scan results */
+    uint64_t *jkeys;          /* device: n_pkts + 1 keys */
+    te_jstate_t *jstates;     /* device: n_pkts + 1 states (entry i + 1: record i's) */
+    te_jctx_t *jctx;          /* device: the context's carried state */
+    void *jtmp;               /* device: te_l2carry_temp_bytes(n_pkts) of scan scratch */
+    size_t jtmp_bytes;
     int any_dec;              /* a non-Ethernet decoder or a non-encoding / pppserial encoder: the
                                  generic kernel's instance that carries them */
     /* window mode (te_launch_edit with win set): the wave lane finds the records itself, no
@@ -226,6 +261,8 @@ uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz);
 int te_launch_edit(te_launch_t *L, hipStream_t stream);
 int te_launch_q8(te_launch_t *L, hipStream_t stream);
 int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
+/* the Juniper state scan alone, and the state the launch leaves in *out (a shard's carry-out) */
+int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream);
 int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);

@@ -68,6 +68,11 @@ struct Pkt {
                    // Tracked across every move of the record, so the two encodes of a fuzzed
                    // record (tcpedit.c:89,250-258) are bounded together, not each on its own
     u8 l2carry = 0;  // the en10mb encoder's dst_modified as the last C2S record left it (Q18)
+    // DLT_JUNIPER_ETHER: the decoder state the last whole inner decode before this record
+    // left (jc), or none yet (jnone: zeros, the encoder's own extra) -- what a frame whose
+    // extensions are not Ethernet is encoded with.  Neither: not at hand (fails loudly)
+    const te_jstate_t *jc = nullptr;
+    bool jnone = false;
     // the generic lane's tile (LDS) path: do_checksum leaves the L4 payload sum to the block
     // (all 256 threads sum every record's L4 bytes in 64-byte pieces) and records the job;
     // the lane writes the field once the block has summed (tile_body)
@@ -1065,6 +1070,29 @@ DI int w80211_proto(Pkt &pk) {
     return RC_PROTO_SOFT;
 }
 
+// dlt_jnpr_ether_decode's header checks (jnpr_ether.c:215-273): RC_ERROR, JNPR_WARN (the
+// extensions do not say Ethernet: media type 1 and encapsulation 14) or RC_OK; hl = the
+// Juniper header's length (set for a warning too)
+constexpr int JNPR_WARN = 1;
+DI int jnpr_header(const u8 *d, u32 n, u32 &hl) {
+    if (n < 6) return RC_ERROR;
+    if (d[0] != 0x4d || d[1] != 0x47 || d[2] != 0x43) return RC_ERROR;  // JUNIPER_ETHER_MAGIC
+    if (!(d[3] & 0x80)) return RC_ERROR;                                 // no L2 header
+    hl = ((u32)d[4] << 8 | d[5]) + 6u;
+    if (n < hl + 14) return RC_ERROR;
+    // the extension TLVs: media type (3) and encapsulation (6), first byte of each value
+    u32 ext = 6, dlt = 0, enc = 0;
+    while (ext + 2 < hl) {
+        const u32 el = d[ext + 1];
+        if (d[ext] == 3) dlt = d[ext + 2];
+        else if (d[ext] == 6) enc = d[ext + 2];
+        if (dlt && enc) break;
+        ext += el + 2;
+    }
+    if (ext > hl) return RC_ERROR;
+    return dlt != 1 || enc != 14 ? JNPR_WARN : RC_OK;
+}
+
 // the decoder's proto (tcpedit_dlt_proto on the source DLT, tcpedit.c:96): the ethertype
 // as the little-endian u16 of its network-order bytes, or < 0
 DI int decoder_proto(Pkt &pk, const te_dev_cfg_t &cfg) {
@@ -1143,32 +1171,48 @@ DI int foreign_decode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
         s.l2len = 4;
         return RC_OK;
     case TE_DEC_JNPR: {  // dlt_jnpr_ether_decode (jnpr_ether.c:201-282)
-        if (n < 6) return RC_ERROR;
-        if (d[0] != 0x4d || d[1] != 0x47 || d[2] != 0x43) return RC_ERROR;  // JUNIPER_ETHER_MAGIC
-        if (!(d[3] & 0x80)) return RC_ERROR;                                 // no L2 header
-        const u32 hl = ((u32)d[4] << 8 | d[5]) + 6u;
-        if (n < hl + 14) return RC_ERROR;
-        // the extension TLVs: media type (3) and encapsulation (6), first byte of each value
-        u32 ext = 6, dlt = 0, enc = 0;
-        while (ext + 2 < hl) {
-            const u32 el = d[ext + 1];
-            if (d[ext] == 3) dlt = d[ext + 2];
-            else if (d[ext] == 6) enc = d[ext + 2];
-            if (dlt && enc) break;
-            ext += el + 2;
+        u32 hl = 0;
+        const int h = jnpr_header(d, n, hl);
+        if (h == RC_ERROR) return RC_ERROR;
+        if (h == JNPR_WARN) {
+            // TCPEDIT_WARN (:269-272): the header length is set, and the frame is encoded
+            // with the state the last whole inner decode left in the context (the copied
+            // addresses and proto, the sub-decoder's extra by pointer)
+            if (pk.jc) {
+                const te_jstate_t &c = *pk.jc;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    s.dstaddr[i] = c.dstaddr[i];
+                    s.srcaddr[i] = c.srcaddr[i];
+                }
+                s.proto = c.proto;
+                s.vlan = c.vlan;
+                s.vlan_offset = c.vlan_offset;
+                s.vlan_tag = c.vlan_tag;
+                s.vlan_pri = c.vlan_pri;
+                s.vlan_cfi = c.vlan_cfi;
+                s.vlan_proto = c.vlan_proto;
+            } else if (pk.jnone) {  // no whole decode yet: the zeroed context and extra
+                s.proto = 0;
+            } else {  // the carried state is not at hand: the record fails the run loudly
+                stale(pk, (int)NEED_NEVER);
+                return RC_ERROR;
+            }
+            s.l2len = (int)hl;
+            return RC_OK;
         }
-        if (ext > hl) return RC_ERROR;
-        // TCPEDIT_WARN: the reference encodes this frame with the previous frame's decoded
-        // state (the decode left it); not reproduced here -- the record fails the run loudly
-        if (dlt != 1 || enc != 14) {
-            stale(pk, (int)NEED_NEVER);
-            return RC_ERROR;
-        }
-        // the en10mb sub-decoder (tcpedit_dlt_copy_decoder_state, dlt_utils.c:249-271: its
-        // addresses, proto and extra; the l2lens add; ctx->l2offset stays 0)
-        if (en10mb_decode(d + hl, (int)(n - hl), s) == RC_ERROR) return RC_ERROR;
-        s.l2len += (int)hl;
-        s.l2offset = 0;
+        // the en10mb sub-decoder works on a context of its own (jnpr_ether.c:135-136,276):
+        // a decode that fails part-way leaves ours as it was; a whole one is copied in
+        // (tcpedit_dlt_copy_decoder_state, dlt_utils.c:249-271: its addresses, proto and
+        // extra; the l2lens add; ctx->l2offset stays 0)
+        Dec t = s;
+        if (en10mb_decode(d + hl, (int)(n - hl), t) == RC_ERROR) return RC_ERROR;
+        t.l2len += (int)hl;
+        t.l2offset = 0;
+        // the first whole decode makes the sub-decoder's extra the encoder's: a fresh
+        // dst_modified (en10mb_decode never writes it)
+        if (pk.jnone) t.dst_modified = false;
+        s = t;
         return RC_OK;
     }
     case TE_DEC_80211: {  // dlt_ieee80211_decode (ieee80211.c:184-224)
@@ -1619,6 +1663,17 @@ again:  // :89 -- after the fuzz step the packet goes through L2 and the L3 edit
         pktlen = (int)pk.caplen;
         s.l2offset = 0;
     } else {
+        if constexpr (FZ && ANYDEC) {
+            // the second decode of a fuzzed record (tcpedit.c:89,250-258) by the Juniper
+            // decoder: a header it takes would write the carried state, or a warning read the
+            // one this record's first decode wrote -- neither is what the state scan saw
+            u32 hl = 0;
+            if (cfg.decoder == TE_DEC_JNPR && fz_mode == TE_FUZZ_APPLY && !fuzz_once &&
+                jnpr_header(pk.d, pk.caplen, hl) != RC_ERROR) {
+                stale(pk, (int)NEED_NEVER);
+                return RC_SOFT;
+            }
+        }
         if ((ANYDEC && cfg.decoder != TE_DEC_EN10MB ? foreign_decode(pk, cfg, s)
                                                     : en10mb_decode(pk.d, (int)pk.caplen, s)) == RC_ERROR)
             return RC_SOFT;

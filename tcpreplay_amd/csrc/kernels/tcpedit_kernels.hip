@@ -96,7 +96,27 @@ struct LaunchArgs {
     // per record (launch-relative index), the last C2S record's dst_modified
     // ((position << 1) | value, 0 = none yet): te_l2carry_mark + an inclusive max scan
     const unsigned long long *l2carry;
+    // DLT_JUNIPER_ETHER: per record the last whole inner decode before it (te_jnpr_mark +
+    // an inclusive max scan: i + 1 for record i, 0 = none in the launch, then *jctx), and
+    // the states (entry i + 1: record i's); null: no carry
+    const unsigned long long *jscan;
+    const te_jstate_t *jstates;
+    const te_jctx_t *jctx;
 };
+
+// the Juniper decoder state record j (launch-relative) is encoded with, should its frame
+// be a TCPEDIT_WARN one (jnpr_ether.c:269-272)
+__device__ __forceinline__ void jnpr_carry(const LaunchArgs &a, uint64_t j, Pkt &pk) {
+    if (!a.jscan) return;
+    const unsigned long long i = a.jscan[j];
+    if (i) {
+        pk.jc = &a.jstates[i];
+    } else {
+        const uint32_t v = a.jctx->valid;
+        if (v == TE_JC_VALID) pk.jc = &a.jctx->st;
+        else if (v == TE_JC_NONE) pk.jnone = true;
+    }
+}
 
 __device__ __forceinline__ uint32_t ld_hdr32(const uint8_t *p, bool swapped) {
     uint32_t v = ld32(p);
@@ -384,6 +404,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         // contiguous span has no byte before a record that is the record's own
         pk.room = MODE == MODE_SLOT ? r0 - (slot_end - my_slot) : 0u;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[tile.first_pkt + tid] & 1u) : 0;
+        if constexpr (AD) jnpr_carry(a, tile.first_pkt + tid, pk);
         pk.defer = kDefer;
         int rc = RC_OK;
         bool warned = false;
@@ -1285,6 +1306,10 @@ constexpr int wk_nch(int tb) { return tb / 16 + 2; }
 constexpr int WIN_S = 64, WIN_OL = 7;
 constexpr int WIN_W = 64 * WIN_S, WIN_WN = WIN_W - WIN_OL * WIN_S;
 constexpr int WIN_TAIL = 2048;
+// staged with the window past its end + 16 (five 1 KiB wave loads in all): the last
+// record reaching past the window is in LDS without a second, dependent load unless longer
+constexpr int WIN_PRE = 5 * 1024 - WIN_W - 48;
+static_assert(WIN_PRE >= 0 && WIN_PRE <= WIN_TAIL, "window pre-staging within the tail room");
 constexpr int WIN_IMG = LDS_FRONT + WIN_W + 48 + WIN_TAIL + 128;
 constexpr int WIN_REL = 4 * WIN_S + 1;
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
@@ -1934,7 +1959,8 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks
         uint8_t *const IMG = SB[wid];       // the staged window at IMG + LDS_FRONT
         uint32_t *const REL = RELB[WIN ? wid : 0];
         for (uint32_t k = w0; k < a.nwin; k += W) {
-            const tew::Found fw = tew::find_window<WIN_S, WIN_OL>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+            const tew::Found fw = tew::find_window<WIN_S, WIN_OL, WIN_PRE>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+            WK_STAMP(0)  // (window mode: the record discovery)
             const uint32_t wfl = fw.wstop | (fw.anyzero ? (uint32_t)IDX_ZERO : 0u);
             if (lane == 0) {
                 a.w_entry[k] = fw.went;
@@ -1957,6 +1983,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks
                     *(uint4 *)(IMG + LDS_FRONT + c) = *(g_cu4 *)(gin + fw.A0 + c);
                 WK_LANES_SYNC();
             }
+            WK_STAMP(5)  // (window mode: the tail load)
             // the tile cut walk_range makes: <= 64 records whose span fits the budget, a
             // record too large for it alone (then left to the exact path by edit())
             for (uint32_t s0 = 0; s0 < fw.nrec;) {
@@ -1981,6 +2008,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks
                 WK_LANES_SYNC();
                 edit(k, tl, my_rel, 0u, false);
                 WK_LANES_SYNC();
+                WK_STAMP(4)  // (window mode: the edit's stores)
                 s0 += len;
             }
         }
@@ -2178,7 +2206,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         if (caplen > MAX_SNAPLEN) { Q8_DBG(2); return Q8_FAIL; }
         for (uint32_t x = 0; x < caplen; ++x) buf[x] = rec[16 + x];  // tcprewrite.c:301
         if (caplen > V) V = caplen;
-        if (j < 0 && (a.l2carry || (FZ && a.fuzz_mode == TE_FUZZ_APPLY)))
+        if (j < 0 && (a.l2carry || a.jscan || (FZ && a.fuzz_mode == TE_FUZZ_APPLY)))
             { Q8_DBG(3); return Q8_FAIL; }  // (a staged record's carried state is not at hand)
         const uint64_t pktno = a.pkt_base + (uint64_t)j;
         int dir = TE_DIR_C2S;
@@ -2209,6 +2237,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         pk.strict = true;
         pk.room = Q8_HEAD - 16;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[j] & 1u) : 0;
+        jnpr_carry(a, (uint64_t)j, pk);
         bool warned = false;
         const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
         const int rc = tcpedit_packet<FZ, true>(pk, cfg, a.portlut, dir, warned, a.fuzz_mode, fzs);
@@ -2540,6 +2569,9 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.q8_list = (uint4 *)L->q8_list;
     a.q8_cap = L->q8_cap;
     a.l2carry = (const unsigned long long *)L->l2carry;
+    a.jscan = (const unsigned long long *)L->jscan;
+    a.jstates = L->jstates;
+    a.jctx = L->jctx;
 }
 
 // ===========================================================================
@@ -2585,18 +2617,111 @@ __global__ __launch_bounds__(256) void te_l2carry_mark(LaunchArgs a, unsigned lo
     pk.unsupported = false;
     pk.need = 0;
     pk.strict = false;
-    bool writer = dir == TE_DIR_C2S && decoder_proto(pk, cfg) >= 0;
+    // (a Juniper frame that is a TCPEDIT_WARN one decodes to the carried state, jnpr_carry)
+    jnpr_carry(a, j, pk);
     Dec s;
     s.dst_modified = false;
-    if (writer) writer = foreign_decode(pk, cfg, s) != RC_ERROR;
+    const bool decoded = dir != TE_DIR_NOSEND && decoder_proto(pk, cfg) >= 0 && foreign_decode(pk, cfg, s) != RC_ERROR;
     const int pktlen = (int)caplen;
-    if (writer) writer = pktlen >= 14 && pktlen >= s.l2len && pktlen + 14 - s.l2len <= (int)MAXPACKET;
+    const bool writer = decoded && dir == TE_DIR_C2S && pktlen >= 14 && pktlen >= s.l2len &&
+                        pktlen + 14 - s.l2len <= (int)MAXPACKET;
     // dst_modified: the frame's first 6 bytes (the encoder's memmove leaves them) against
     // the decoded destination (en10mb.c:612-615)
     bool nz = false;
     if (writer)
         for (int i = 0; i < 6; ++i) nz |= pk.d[i] != s.dstaddr[i];
-    key[j + 1] = writer ? ((unsigned long long)(j + 1) << 1 | (nz ? 1u : 0u)) : 0ull;
+    // the first whole Juniper inner decode makes the sub-decoder's extra the encoder's
+    // (dlt_utils.c:261-263): the records after it read its dst_modified, false until a C2S
+    // record writes it -- a writer of false unless it writes itself
+    uint32_t hl = 0;
+    const bool first = decoded && pk.jnone && cfg.decoder == TE_DEC_JNPR && jnpr_header(pk.d, caplen, hl) == RC_OK;
+    key[j + 1] = writer ? ((unsigned long long)(j + 1) << 1 | (nz ? 1u : 0u))
+                        : first ? (unsigned long long)(j + 1) << 1 : 0ull;
+}
+
+// ===========================================================================
+// DLT_JUNIPER_ETHER into an encoder that reads the decoder state (en10mb, user, hdlc): a
+// frame whose extensions are not Ethernet is a TCPEDIT_WARN (jnpr_ether.c:269-272) and is
+// encoded with the state the last whole inner decode left in the context -- its addresses
+// and proto (dlt_utils.c:249-271) and, by the extra pointer, the en10mb sub-decoder's VLAN
+// fields.  te_jnpr_mark keys each record that decodes whole (the decoder's proto and
+// decode succeed, tcpedit.c:96, dlt_plugins.c:210-238) with its position and stores its
+// state; an inclusive max scan gives each record the last such record before it, and
+// te_jnpr_save leaves the launch's last state in the context for the next launch.
+// ===========================================================================
+__global__ __launch_bounds__(256) void te_jnpr_mark(LaunchArgs a, unsigned long long *key, te_jstate_t *states) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) key[0] = 0;
+    const te_tile_t tile = a.tiles[blockIdx.x];
+    if (threadIdx.x >= tile.npkt) return;
+    const uint32_t j = tile.first_pkt + threadIdx.x;
+    const te_dev_cfg_t &cfg = *a.cfg;
+    const bool swp = a.in_swapped != 0;
+    const uint8_t *rec = a.in + tile.span_off + a.pkt_rel[j];
+    uint32_t caplen = ld_hdr32(rec + 8, swp);
+    const uint32_t len = ld_hdr32(rec + 12, swp);
+    if (cfg.efcs && len > 4 && caplen == len) caplen -= 4;  // tcpedit.c:78-84
+    int dir = TE_DIR_C2S;
+    if (a.fixed_dir >= 0) {
+        dir = a.fixed_dir;
+    } else if (a.dirbits) {
+        const uint64_t pktno = a.pkt_base + j;
+        const uint64_t idx = pktno >> 2;
+        const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
+        const uint8_t b = idx < a.dirbits_len ? a.dirbits[idx] : 0;
+        dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+    }
+    Pkt pk;
+    pk.d = const_cast<uint8_t *>(rec + 16);
+    pk.caplen = caplen;
+    pk.len = len;
+    pk.phys = pk.avail = pk.ext = caplen;
+    pk.unsupported = false;
+    pk.need = 0;
+    pk.strict = false;
+    uint32_t hl = 0;
+    Dec s;
+    s.dst_modified = false;
+    const bool whole = dir != TE_DIR_NOSEND && decoder_proto(pk, cfg) >= 0 &&
+                       jnpr_header(pk.d, caplen, hl) == RC_OK && foreign_decode(pk, cfg, s) == RC_OK;
+    if (whole) {
+        te_jstate_t st;
+        for (int i = 0; i < 6; ++i) {
+            st.dstaddr[i] = s.dstaddr[i];
+            st.srcaddr[i] = s.srcaddr[i];
+        }
+        st.proto = (uint16_t)s.proto;
+        st.vlan_tag = s.vlan_tag;
+        st.vlan_pri = s.vlan_pri;
+        st.vlan_cfi = s.vlan_cfi;
+        st.vlan_proto = s.vlan_proto;
+        st.pad0_ = 0;
+        st.vlan_offset = s.vlan_offset;
+        st.vlan = (uint8_t)s.vlan;
+        st.pad1_[0] = st.pad1_[1] = st.pad1_[2] = 0;
+        states[j + 1] = st;
+    }
+    key[j + 1] = whole ? (unsigned long long)(j + 1) : 0ull;
+}
+
+// the launch's last whole decode (if any) becomes the context's carried state
+__global__ void te_jnpr_save(const unsigned long long *scan, const te_jstate_t *states, uint32_t n, te_jctx_t *ctx,
+                             te_jctx_t *out) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long i = scan[n];
+    te_jctx_t c;
+    if (out) {  // the launch's own: none unless it has a whole decode
+        c.valid = TE_JC_NONE;
+        for (int k = 0; k < 3; ++k) c.pad_[k] = 0;
+        c.st = te_jstate_t{};
+    } else {
+        c = *ctx;
+    }
+    if (i) {
+        c.st = states[i];
+        c.valid = TE_JC_VALID;
+    }
+    if (out) *out = c;
+    else *ctx = c;
 }
 
 __global__ void te_l2carry_save(const unsigned long long *scan, uint32_t n, uint32_t *word) {
@@ -2631,12 +2756,40 @@ static int l2carry_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stre
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the Juniper state keys and scan before the edit (and before the fuzz reach pass: a
+// warning frame's encode decides whether it reaches the fuzz step)
+static int jnpr_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stream) {
+    if (!L->jscan) return 0;
+    if (!L->jkeys || !L->jstates || !L->jctx || !L->jtmp || L->n_tiles == 0) return -1;
+    hipLaunchKernelGGL(te_jnpr_mark, dim3(L->n_tiles), dim3(256), 0, stream, a, (unsigned long long *)L->jkeys,
+                       L->jstates);
+    size_t tb = L->jtmp_bytes;
+    if (hipcub::DeviceScan::InclusiveScan(L->jtmp, tb, (const unsigned long long *)L->jkeys,
+                                          (unsigned long long *)L->jscan, MaxU64(), (int)L->n_pkts + 1,
+                                          stream) != hipSuccess)
+        return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // the keys and the scan alone (tcpedit_batch_l2carry_out: a shard's carry-out before any
-// shard edits, so the ranks can exchange them)
+// shard edits, so the ranks can exchange them); the Juniper state scan first (a warning
+// frame's destination is the carried one)
 extern "C" int te_launch_l2carry(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     fill_args(a, L);
+    if (jnpr_prepare(L, a, stream) != 0) return -1;
     return l2carry_prepare(L, a, stream);
+}
+
+// the Juniper state scan alone and the state the launch would leave (a shard's carry-out:
+// it does not depend on the carry-in, a whole decode reads none)
+extern "C" int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream) {
+    LaunchArgs a;
+    fill_args(a, L);
+    if (!L->jscan || jnpr_prepare(L, a, stream) != 0) return -1;
+    hipLaunchKernelGGL(te_jnpr_save, dim3(1), dim3(64), 0, stream, (const unsigned long long *)L->jscan, L->jstates,
+                       L->n_pkts, L->jctx, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" uint64_t te_q8_slot_bytes(void) { return Q8_SLOT; }
@@ -2838,6 +2991,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     const int res = resident_blocks(L->slot_layout);
     int grid = L->grid > 0 && L->grid < res ? L->grid : res;
     if ((uint32_t)grid > L->n_tiles) grid = (int)L->n_tiles;
+    if (!fast && jnpr_prepare(L, a, stream) != 0) return -1;
     if (L->fuzz_states && !fast) {
         // --fuzz-seed: reach pass, per-record RNG states, then the edit pass below
         if (!L->fuzz_blk || !L->fuzz_words || L->n_pkts == 0) return -1;
@@ -2866,6 +3020,9 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     if (!fast && L->l2carry)  // the last record's value, for the next launch (the Q8 replay reads the array)
         hipLaunchKernelGGL(te_l2carry_save, dim3(1), dim3(64), 0, stream, (const unsigned long long *)L->l2carry,
                            L->n_pkts, L->l2carry_word);
+    if (!fast && L->jscan)  // the launch's last whole Juniper decode, for the next launch
+        hipLaunchKernelGGL(te_jnpr_save, dim3(1), dim3(64), 0, stream, (const unsigned long long *)L->jscan,
+                           L->jstates, L->n_pkts, L->jctx, (te_jctx_t *)nullptr);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : -1;
 }

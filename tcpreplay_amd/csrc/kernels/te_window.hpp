@@ -103,8 +103,10 @@ struct Found {
     u32 wstop, nrec;
     bool anyzero;     // a record with caplen 0
 };
-// img: (W + 48) / 4 dwords at least (W = 64 S); rel: 4 S + 1 entries
-template <int S, int OL>
+// img: (W + 48 + PRE) / 4 dwords at least (W = 64 S); rel: 4 S + 1 entries.  PRE: bytes
+// staged past the window's end + 16 (the fused edit's last record reaching past the window:
+// in LDS with the window, no second dependent load for it)
+template <int S, int OL, int PRE = 0>
 __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *rel, u32 k) {
     constexpr int W = IW * S;       // staged sub-window bytes
     constexpr int O = OL * S;       // overlap before the window
@@ -123,14 +125,15 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     const u64 we = ws + WN < limit ? ws + WN : limit;
     const u64 A0 = ws - O;          // lane l's sub-window starts at A0 + l S (window 0: none before base)
     const u64 lo_stage = k ? A0 : base;
-    const u64 staged_end = we + 16;  // bytes [lo_stage, staged_end) are in LDS (past a.len: garbage)
+    // bytes [lo_stage, staged_end) are in LDS (past a.len: garbage; never more than 16 past it)
+    const u64 staged_end = PRE == 0 ? we + 16 : (we + 16 + PRE < a.len + 16 ? we + 16 + PRE : (we > a.len ? we : a.len) + 16);
 
     // ---- stage the window: 16-byte chunks, all loads in flight before the LDS stores ----
     {
         const u32 c0 = (u32)((lo_stage - A0) >> 4);
         const u32 nch = (u32)((staged_end - A0 + 15) >> 4);
         const uint4 *g = (const uint4 *)(a.img + A0);
-        constexpr int K = (W + 48 + 16 * IW - 1) / (16 * IW);
+        constexpr int K = (W + 48 + PRE + 16 * IW - 1) / (16 * IW);
         uint4 v[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
@@ -140,7 +143,7 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             const u32 c = lane + i * IW;
-            if (c < nch && c < (u32)((W + 48) / 16)) *(uint4 *)&img[4 * c] = v[i];
+            if (c < nch && c < (u32)((W + 48 + PRE) / 16)) *(uint4 *)&img[4 * c] = v[i];
         }
     }
     // one wave's LDS accesses are performed in order; the empty asm keeps the compiler from

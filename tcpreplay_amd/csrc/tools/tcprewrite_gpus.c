@@ -40,6 +40,9 @@ typedef struct {
     int opened, rc;
     int64_t reach;
     int carry;
+    int jnpr;                                 /* DLT_JUNIPER_ETHER: the decoder-state exchange runs */
+    int jvalid;                               /* this shard has a whole inner decode ... */
+    uint8_t jstate[TCPEDIT_JNPR_STATE_BYTES]; /* ... and the state its last one leaves */
     tcpedit_batch_result_t r;
     uint64_t seg;
     const uint8_t *status;
@@ -99,8 +102,12 @@ static void *shard_main(void *arg)
     }
     if (S->b) {
         S->reach = tcpedit_batch_fuzz_reach(S->te, S->b);
-        S->carry = tcpedit_batch_l2carry_out(S->te, S->b);
-        S->opened = S->reach >= 0 && S->carry >= 0;
+        /* DLT_JUNIPER_ETHER: the shards' decoder states go round first (below); the
+           dst_modified carry-out reads the seeded state, so it waits for it */
+        S->jnpr = J->dlt == 178;
+        S->jvalid = S->jnpr ? tcpedit_batch_jnpr_out(S->te, S->b, S->jstate, sizeof S->jstate) : 0;
+        S->carry = S->jnpr ? 2 : tcpedit_batch_l2carry_out(S->te, S->b);
+        S->opened = S->reach >= 0 && S->carry >= 0 && S->jvalid >= 0;
         if (!S->opened)
             snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
     }
@@ -121,6 +128,21 @@ static void *shard_main(void *arg)
     int carry_in = 0;
     for (int j = 0; j < J->n; j++)
         all_open &= J->sh[j].opened;
+    if (all_open && J->dlt == 178) {
+        /* the nearest earlier shard's Juniper decoder state, then this shard's carry-out */
+        const uint8_t *src = NULL;
+        for (int j = k - 1; j >= 0 && !src; j--)
+            if (J->sh[j].jvalid == 1)
+                src = J->sh[j].jstate;
+        if (tcpedit_set_jnpr_state(S->te, src, TCPEDIT_JNPR_STATE_BYTES, 0) < 0 ||
+            (S->carry = tcpedit_batch_l2carry_out(S->te, S->b)) < 0) {
+            snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
+            S->opened = 0;
+        }
+        pthread_barrier_wait(&J->bar);
+        for (int j = 0; j < J->n; j++)
+            all_open &= J->sh[j].opened;
+    }
     for (int j = 0; j < k; j++)
         skip += (uint64_t)J->sh[j].reach;
     for (int j = k - 1; j >= 0; j--)

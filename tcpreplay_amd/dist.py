@@ -126,19 +126,42 @@ def gpu_editor(image, args, cache: Optional[bytes], pkt_base: int, device: int,
         sh.close()
 
 
-def _pre_edit(dist, cdev, ok: bool, reach: int, carry: int):
-    """The one exchange before the edit, on every rank: (shard opened, fuzz reach,
-    dst_modified carry-out) per rank.  Returns (ranks that failed, fuzz draws of the
-    earlier ranks, the dst_modified value the nearest earlier writing shard left, or 0:
-    the reference's zeroed en10mb extra)."""
+def _pre_edit(dist, cdev, sh):
+    """The exchange before the edit, on every rank: (shard opened, fuzz reach,
+    dst_modified carry-out) per rank -- for a Juniper capture the shards' decoder states
+    first, then the carry-outs they decide (a second all-gather).  `sh`: this rank's
+    _DeviceShard or None (it failed to open).  Returns (ranks that failed, fuzz draws of the
+    earlier ranks, the dst_modified value the nearest earlier writing shard left, or 0: the
+    reference's zeroed en10mb extra)."""
+    import struct
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
-    mine = torch.tensor([1 if ok else 0, reach, carry], dtype=torch.int64, device=cdev)
+    ok = sh is not None
+    jnpr = bool(ok and sh.jnpr)
+    jv, jst = sh.jstate if ok else (False, bytes(48))
+    words = list(struct.unpack("<6q", bytes(jst)[:48]))
+    mine = torch.tensor([1 if ok else 0, sh.reach if ok else 0, sh.carry if ok else 2, 1 if jnpr else 0,
+                         1 if jv else 0] + words, dtype=torch.int64, device=cdev)
     allv = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allv, mine)
     rows = [[int(x) for x in v.tolist()] for v in allv]
     bad = [r for r in range(world) if not rows[r][0]]
     skip = sum(rows[r][1] for r in range(rank))
+    if not bad and any(rows[r][3] for r in range(world)):
+        # the nearest earlier shard with a whole Juniper decode seeds this one's state
+        src = next((r for r in range(rank - 1, -1, -1) if rows[r][4]), None)
+        err = ""
+        try:
+            sh.seed_jnpr(struct.pack("<6q", *rows[src][5:11]) if src is not None else None)
+        except Exception as e:  # noqa: BLE001 -- every rank raises after the exchange
+            err = str(e)
+        mine = torch.tensor([0 if err else 1, sh.carry if not err else 2], dtype=torch.int64, device=cdev)
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        for r in range(world):
+            rows[r][2] = int(allc[r][1].item())
+            if not int(allc[r][0].item()):
+                bad.append(r)
     carry_in = next((rows[r][2] for r in range(rank - 1, -1, -1) if rows[r][2] in (0, 1)), 0)
     return bad, skip, carry_in
 
@@ -179,7 +202,7 @@ def rewrite_distributed(pcap: bytes, args, cache: Optional[bytes] = None, out_pa
                               dev, prefix=memoryview(pcap)[PCAP_HDR_LEN:p.offsets[rank]] if rank else None)
         except Exception as e:  # noqa: BLE001 -- every rank raises after the exchange
             err = f"rank {rank}: {e}"
-        bad, skip, carry_in = _pre_edit(dist, cdev, sh is not None, sh.reach if sh else 0, sh.carry if sh else 2)
+        bad, skip, carry_in = _pre_edit(dist, cdev, sh)
         if bad:
             if sh is not None:
                 sh.close()
@@ -246,11 +269,22 @@ class _DeviceShard:
                 self.prefix = prefix
                 self.b.set_prefix(prefix)
             self.reach = self.b.fuzz_reach() if fuzz_enabled(args) else 0
-            self.carry = self.b.l2carry_out()
+            # DLT_JUNIPER_ETHER: the decoder state this shard's last whole inner decode
+            # leaves goes round first; the dst_modified carry-out reads the seeded state
+            # (a warning frame's destination is the carried one), so it waits for it
+            self.jnpr = capture_dlt(hdr if hdr is not None else seg) == 178
+            self.jstate = self.b.jnpr_out() if self.jnpr else (False, bytes(48))
+            self.carry = 2 if self.jnpr else self.b.l2carry_out()
         except Exception:
             self.close()
             raise
         self.rc, self.counters, self.seg_len, self.error = None, [0] * len(COUNTER_NAMES), 0, ""
+
+    def seed_jnpr(self, state):
+        """the nearest earlier shard's Juniper decoder state (None: none before), then this
+        shard's dst_modified carry-out, which reads it"""
+        self.te.set_jnpr_state(state)
+        self.carry = self.b.l2carry_out()
 
     def run(self, fuzz_skip: int, carry_in: Optional[int]):
         """the edit, after the earlier shards' fuzz draws and with their carry"""
@@ -361,8 +395,7 @@ def rewrite_file_distributed(in_path: str, args, out_path: str, cache_path: Opti
             except Exception as e:  # noqa: BLE001 -- travels in the exchange below
                 err = f"rank {rank}: {e}"
             # every rank, opened or not: no rank is left waiting in a collective
-            bad, skip, carry_in = _pre_edit(dist, cdev, sh is not None, sh.reach if sh else 0,
-                                            sh.carry if sh else 2)
+            bad, skip, carry_in = _pre_edit(dist, cdev, sh)
             if sh is not None:
                 try:
                     if bad:

@@ -75,6 +75,10 @@ int main(int argc, char **argv) {
     if (img.size() < 24) return 2;
     std::vector<uint8_t> out(img.begin(), img.begin() + 24);
     uint32_t fstate = cfg.fuzz_seed;  // fuzzing_init (fuzzing.c:12-20)
+    // DLT_JUNIPER_ETHER: the decoder state the last whole inner decode left (what a frame
+    // whose extensions are not Ethernet is encoded with), as te_jnpr_mark + its scan give it
+    te_jstate_t jst{};
+    bool jvalid = false;
     uint64_t recs = 0, written = 0, unsup = 0;
     int error = 0;
     size_t off = 24;
@@ -97,6 +101,40 @@ int main(int argc, char **argv) {
             const uint32_t bit = (uint32_t)((pktno & 3) * 2) + 1;
             const uint8_t b = idx < dirbits.size() ? dirbits[idx] : 0;
             dir = !(b & (1u << bit)) ? TE_DIR_NOSEND : ((b & (1u << (bit - 1))) ? TE_DIR_C2S : TE_DIR_S2C);
+        }
+        // this record's first decode, on its input bytes (te_jnpr_mark): whole or not
+        bool jwhole = false;
+        te_jstate_t jnext{};
+        if (cfg.decoder == TE_DEC_JNPR && dir != TE_DIR_NOSEND) {
+            std::vector<uint8_t> tmp(rec + 16, rec + 16 + caplen);
+            tmp.resize(caplen + 64);
+            Pkt q;
+            q.d = tmp.data();
+            q.caplen = caplen;
+            if (cfg.efcs && len > 4 && caplen == len) q.caplen -= 4;
+            q.len = len;
+            q.phys = q.avail = q.ext = q.caplen;
+            q.unsupported = false;
+            q.need = 0;
+            q.strict = false;
+            uint32_t hl = 0;
+            Dec ds;
+            ds.dst_modified = false;
+            jwhole = decoder_proto(q, cfg) >= 0 && jnpr_header(q.d, q.caplen, hl) == RC_OK &&
+                     foreign_decode(q, cfg, ds) == RC_OK;
+            if (jwhole) {
+                for (int i = 0; i < 6; ++i) {
+                    jnext.dstaddr[i] = ds.dstaddr[i];
+                    jnext.srcaddr[i] = ds.srcaddr[i];
+                }
+                jnext.proto = (uint16_t)ds.proto;
+                jnext.vlan_tag = ds.vlan_tag;
+                jnext.vlan_pri = ds.vlan_pri;
+                jnext.vlan_cfi = ds.vlan_cfi;
+                jnext.vlan_proto = ds.vlan_proto;
+                jnext.vlan_offset = ds.vlan_offset;
+                jnext.vlan = (uint8_t)ds.vlan;
+            }
         }
         bool reached = false;
         int rc = RC_OK;
@@ -123,6 +161,8 @@ int main(int argc, char **argv) {
             pk.room = r0;
             pk.l2carry = 0;
             pk.defer = false;
+            pk.jc = jvalid ? &jst : nullptr;
+            pk.jnone = !jvalid;
             if (dir == TE_DIR_NOSEND) break;  // tcprewrite.c:314-315: written unedited
             const uint32_t mode = !fz ? TE_FUZZ_OFF : pass == 0 ? TE_FUZZ_PROBE : TE_FUZZ_APPLY;
             const uint32_t st = pass == 1 && reached ? fstate : 0u;
@@ -133,6 +173,10 @@ int main(int argc, char **argv) {
             if (pass == 0) reached = rc == RC_REACHED;
         }
         if (reached) tcpr_random_dev(fstate);  // the record's draw (fuzzing.c:88)
+        if (jwhole) {
+            jst = jnext;
+            jvalid = true;
+        }
         ++recs;
         bool write = true;
         if (rc == RC_ERROR) {

@@ -355,6 +355,25 @@ def test_two_rank_gpu_rewrite_equals_oracle(built, case):
     assert out == exp
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("line", ["q18_cache", "hdlc"])
+def test_gpu_ranks_carry_the_jnpr_decoder_state(built, world, line):
+    """Juniper warning frames (encoded with the last whole inner decode's state) across
+    shard cuts: the ranks all-gather their shards' last states, seed their contexts with
+    the nearest earlier one, then exchange the SURVEY Q18 carry-outs (which read it)"""
+    import test_dlt_wireless as W
+    pcap, _ = W._jnpr_warn(6000, seed=31, every=5, lead=40)
+    if line == "q18_cache":
+        args, cache = ["--dlt=enet", "--fixcsum"], S.tcpprep_cache(6000, seed=31, nosend_every=9)
+    else:
+        args, cache = ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"], None
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    out, res = run_world(pcap, args, cache, world=world, use_gpu=True)
+    assert rc_o == 0 and all(r[1] == 0 for r in res)
+    assert out == exp
+
+
 def _q8_across_the_cut(world=2):
     """IPv6 records, one overstating its payload just after the shard cut, its donor (a
     longer record) just before it: the replay of shard 1's record walks back into shard 0"""

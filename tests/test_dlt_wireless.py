@@ -15,8 +15,12 @@ the oracle, bit-exact.  Reference behaviours kept:
   * Juniper: the inner Ethernet frame's en10mb decode supplies addresses, proto and the
     VLAN fields (by the extra pointer), so --enet-vlan=del writes the inner type and a
     tagged inner frame without --enet-vlan gets its TCI written at offset 14 of the new
-    frame; a frame whose extensions are not Ethernet is a TCPEDIT_WARN that re-uses the
-    previous frame's decoded state -- the device refuses such a record loudly."""
+    frame; a frame whose extensions are not Ethernet is a TCPEDIT_WARN (jnpr_ether.c:269-272)
+    that is encoded with the state the last whole inner decode left in the context (its
+    addresses and proto, dlt_utils.c:249-271, and by the extra pointer the sub-decoder's
+    VLAN fields) -- zeros before the first, whose sub-decoder extra then becomes the
+    encoder's (a fresh dst_modified).  The device carries it with a mark + max scan over
+    the records (te_jnpr_mark), across launches, pipeline chunks and shards."""
 import pytest
 
 import oracle_lib as O
@@ -182,22 +186,97 @@ def test_gpu_dst_modified_carries_across_s2c_records(built, kind):
     _gpu_vs_oracle(pcap, args, DLT_OF[kind], cache)
 
 
+def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
+    """a Juniper capture whose records lead, lead + 1, ... (the first `lead` records, then
+    every `every`-th) carry encapsulation 15 (not Ethernet: TCPEDIT_WARN); every 4th inner
+    frame is 802.1Q-tagged (S.reframe), so the carried VLAN fields change along the way"""
+    recs = S.records(S.reframe(_base(n, seed=seed), "jnpr"))
+    warn = set(range(lead)) | {i for i in range(len(recs)) if i % every == 2}
+    for i in sorted(warn):
+        ts, tu, cl, ln, d = recs[i]
+        d = bytearray(d)
+        k = d.find(b"\x06\x01\x0e")
+        d[k + 2] = 0x0f
+        recs[i] = (ts, tu, cl, ln, bytes(d))
+    return S.build_pcap(recs, 178), warn
+
+
+def test_oracle_jnpr_warning_frames_encode_with_the_carried_state(built):
+    """--dlt=hdlc: a warning frame becomes {address, control, the carried proto} + the
+    frame after its Juniper header (only that header is its l2len); the proto is the last
+    whole decode's inner ethertype, zero before the first"""
+    pcap, warn = _jnpr_warn(200)
+    args = ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3"]
+    rc, out = O.rewrite(pcap, args)
+    assert rc == 0
+    prev = b"\x00\x00"
+    for i, (r_in, r_out) in enumerate(zip(S.records(pcap), S.records(out))):
+        d, o = r_in[4], r_out[4]
+        hl = 6 + (d[4] << 8 | d[5])
+        inner = d[hl:]
+        if i in warn:
+            assert o == bytes([15, 3]) + prev + inner, i
+            continue
+        typ = inner[12:14]  # (en10mb.c:431: the outer type, 0x8100 for a tagged frame)
+        assert o[:4] == bytes([15, 3]) + typ, i
+        prev = typ
+
+
+# the option lines of the Juniper warning frames: the en10mb encoder with both MACs, with a
+# VLAN pop (the carried inner type), without MACs (the carried addresses, SURVEY Q18 with a
+# cache), the user and hdlc encoders, --fuzz-seed behind it
+JNPR_LINES = [
+    ["--dlt=enet"] + MACS + ["--fixcsum"],
+    ["--dlt=enet", "--enet-vlan=del", "--seed=3"] + MACS,
+    ["--dlt=enet", "--fixcsum"],
+    ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--ttl=9"],
+    ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
+    ["--dlt=enet", "--fuzz-seed=3", "--fuzz-factor=2", "--fixcsum"] + MACS,
+]
+
+
 @pytest.mark.gpu
-def test_gpu_jnpr_non_ethernet_extension_is_refused(built):
-    """a Juniper frame whose extensions are not Ethernet (TCPEDIT_WARN: the reference
-    encodes it with the previous frame's decoded state) fails the run loudly on the device"""
-    recs = S.records(S.reframe(_base(200, seed=4), "jnpr"))
-    ts, tu, cl, ln, d = recs[50]
-    d = bytearray(d)
-    k = d.find(b"\x06\x01\x0e")
-    d[k + 2] = 0x0f  # encapsulation 15
-    recs[50] = (ts, tu, cl, ln, bytes(d))
-    pcap = S.build_pcap(recs, 178)
-    rc_o, exp = O.rewrite(pcap, ["--dlt=enet"] + MACS)
-    assert rc_o == 0
+@pytest.mark.parametrize("k", range(len(JNPR_LINES)))
+def test_gpu_jnpr_warning_frames_match_oracle(built, k):
+    """batch (one launch), pipelined (64 KiB chunks: the state crosses chunk cuts) and a
+    tcpprep cache (NOSEND records decode nothing, S2C records keep Q18's value)"""
+    pcap, _ = _jnpr_warn(3000, seed=k + 5)
+    _gpu_vs_oracle(pcap, JNPR_LINES[k], 178)
+    if "--fuzz-seed=3" not in JNPR_LINES[k]:
+        cache = S.tcpprep_cache(3000, seed=k + 5, nosend_every=9)
+        _gpu_vs_oracle(pcap, JNPR_LINES[k], 178, cache)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [0, 2, 4])
+def test_gpu_jnpr_warning_frames_per_packet(built, k):
+    """tcpedit_packet record by record (the launch path: the server declines this config):
+    the state carries from one call to the next"""
+    pcap, _ = _jnpr_warn(150, seed=11)
+    args = JNPR_LINES[k]
+    rc_o, exp = O.rewrite(pcap, args)
+    te = TA.TcpEdit(args, dlt=178)
+    try:
+        got = []
+        for ts, tu, cl, ln, d in S.records(pcap):
+            buf = bytearray(d) + bytearray(262166)
+            rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf, 1)
+            assert rc != -1, te.geterr()
+            got.append((h["ts_sec"], h["ts_usec"], h["caplen"], h["len"], bytes(buf[:h["caplen"]])))
+        assert got == S.records(exp)
+    finally:
+        te.close()
+
+
+@pytest.mark.gpu
+def test_gpu_jnpr_state_unknown_fails_loudly(built):
+    """a context told its carried state is not known (a shard seeded with unknown = 1)
+    fails the run at a warning frame before the shard's first whole decode"""
+    pcap, _ = _jnpr_warn(200, seed=4)
     te = TA.TcpEdit(["--dlt=enet"] + MACS, dlt=178)
     try:
+        te.set_jnpr_state(None, unknown=True)
         rc, out = te.rewrite(pcap)
-        assert rc == -1 and "record 51" in te.geterr()  # (1-based, as the reference counts)
+        assert rc == -1 and "record 1" in te.geterr()
     finally:
         te.close()

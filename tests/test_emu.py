@@ -28,7 +28,7 @@ from tcpreplay_amd import synth as S
 HERE = os.path.dirname(os.path.abspath(__file__))
 EMU = os.path.join(HERE, "emu", "_build", "te_emu")
 DLT_OF = {"sll": 113, "sll2": 276, "raw": 12, "raw12": 12, "null": 0, "loop": 108, "ppp": 50, "chdlc": 104}
-DEC_L2 = {1: 14, 113: 16, 276: 20, 12: 0, 0: 4, 108: 4, 50: 4, 104: 4, 178: 20, 105: 24, 127: 24}
+DEC_L2 = {1: 14, 113: 16, 276: 20, 12: 0, 0: 4, 108: 4, 50: 4, 104: 4, 178: 6, 105: 24, 127: 24}
 MACS = ["--enet-smac=00:11:22:33:44:55,00:aa:bb:cc:dd:ee", "--enet-dmac=00:66:77:88:99:aa,00:12:34:56:78:9a"]
 USER14 = ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1"]
 USER40 = ["--dlt=user", "--user-dlink=" + ",".join("%02x" % (b + 0x40) for b in range(38)) + ",08,00",
@@ -154,6 +154,16 @@ def test_emu_ethernet(emu, tmp_path, k):
     --fixlen=pad and --mtu-trunc, and into a 40-byte user header (headroom 2 x 26)"""
     pcap = S.pcap_imix(1500, seed=k + 5)
     _check(emu, str(tmp_path), pcap, ETH_LINES[k], 1)
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_emu_jnpr_warning_frames(emu, tmp_path, k):
+    """Juniper frames whose extensions are not Ethernet (TCPEDIT_WARN), encoded with the
+    carried decoder state -- plain and fuzzed lines, into en10mb, user and hdlc"""
+    import test_dlt_wireless as W
+    lines = [W.JNPR_LINES[0], W.JNPR_LINES[1], W.JNPR_LINES[3], W.JNPR_LINES[4], W.JNPR_LINES[5]]
+    pcap, _ = W._jnpr_warn(1500, seed=k + 41)
+    _check(emu, str(tmp_path), pcap, lines[k], 178)
 
 
 def test_emu_headroom_holds_two_encodes(emu, tmp_path):
