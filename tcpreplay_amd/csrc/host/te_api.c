@@ -2572,6 +2572,9 @@ struct te_pipe_s {
        index totals), ~0 when not */
     uint64_t early[TE_PIPE_SLOTS];
     uint32_t early_miss, early_n; /* (trace: early copies done again, early copies) */
+    /* the window-mode pipeline: the call's device accumulator {packets, bytes, edited,
+       chain verdict} and its pinned landing area (+ the last chunk's chain end) */
+    uint64_t *d_wacc, *h_wacc;
 };
 
 /* a chunk's first record at file offset off: an anchor for later prefixes */
@@ -2623,6 +2626,8 @@ void te_pipe_free(tcpedit_t *t)
         hipFree(P->d_idx[s]);
         hipHostFree(P->h_tot[s]);
     }
+    hipFree(P->d_wacc);
+    hipHostFree(P->h_wacc);
     if (P->s_h2d)
         hipStreamDestroy(P->s_h2d);
     if (P->s_d2h)
@@ -3143,6 +3148,127 @@ fail:
     return -1;
 }
 
+static int win_pipe_off(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_PIPE_NO_WIN");
+    return e && *e && *e != '0';
+}
+
+/* The window-mode pipeline, for the wave lane's size-preserving configs without a tcpprep
+ * cache (what tcpedit_batch_run_fused carries): chunk k is the file bytes [cst_k, cst_k+1)
+ * uploaded with the next TE_PIPE_MARGIN bytes and edited in window mode -- the wave lane
+ * finds its records itself, the first where the previous chunk's chain ended (read on the
+ * device).  Records keep their file offsets, so the chunk's output image, completed with
+ * the previous chunk's last record (te_win_head), goes down as the same file range.  No
+ * host wait per chunk: the block totals and the chain verdicts gather on the device and
+ * are read once at the end.  Returns 0 (*pos_io: the output's end), 1 (a chunk missed the
+ * chain, a chain end or a record the window mode leaves to the exact path: the caller runs
+ * the exact pipeline over the whole capture; the same bytes), or -1. */
+static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t in_len, uint8_t *dst, size_t out_cap,
+                        uint64_t *pos_io, int trace)
+{
+    const uint64_t C = P->chunk;
+    int nch = (int)((in_len - 24 + C - 1) / C);
+    if (nch < 1)
+        nch = 1;
+    if (in_len > out_cap || in_len < 24 + 16)
+        return 1; /* (the copies move whole file ranges) */
+    const double t0 = te_now();
+    if (!P->d_wacc) {
+        HIPCHK(t, hipMalloc((void **)&P->d_wacc, 64));
+        HIPCHK(t, hipHostMalloc((void **)&P->h_wacc, 64, 0));
+    }
+    const uint64_t limit_max = 24 + C;
+    const uint32_t nwin_max = (uint32_t)((limit_max - 16 + te_win_bytes() - 1) / te_win_bytes());
+    for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+        tcpedit_batch_t *b = P->slot[s];
+        b->out_cap = C + TE_PIPE_MARGIN + 24;
+        if (win_ready(t, b, nwin_max) < 0 || pipe_grow(t, P, s) < 0)
+            return -1;
+    }
+    HIPCHK(t, hipMemsetAsync(P->d_wacc, 0, 32, t->stream));
+    int last = 0;
+    for (int k = 0; k < nch; k++) {
+        const int s = k % TE_PIPE_SLOTS, ps = (k + TE_PIPE_SLOTS - 1) % TE_PIPE_SLOTS;
+        tcpedit_batch_t *b = P->slot[s], *pb = P->slot[ps];
+        const uint64_t f0 = 24 + (uint64_t)k * C, f1 = f0 + C < in_len ? f0 + C : in_len;
+        const uint64_t fe = f1 + TE_PIPE_MARGIN < in_len ? f1 + TE_PIPE_MARGIN : in_len;
+        /* upload (the slot's last window kernel has read its input) */
+        if (k >= TE_PIPE_SLOTS)
+            HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s], 0));
+        HIPCHK(t, hipMemcpyAsync(b->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));
+        HIPCHK(t, hipMemcpyAsync(b->d_in + 24, img + f0, fe - f0, hipMemcpyHostToDevice, P->s_h2d));
+        HIPCHK(t, hipEventRecord(P->h2d_done[s], P->s_h2d));
+        b->in_len = 24 + (fe - f0);
+        b->n_tiles = 0;
+        b->rec0 = b->out_base = 24; /* records keep their image offsets */
+        b->launches = 0;
+        b->gen_hint_ok = 0;
+        te_win_req_t q;
+        memset(&q, 0, sizeof q);
+        q.len = b->in_len;
+        q.entry = 24;
+        q.base = 16;
+        q.limit = f1 >= in_len ? b->in_len : 24 + (f1 - f0);
+        q.nwin = (uint32_t)((q.limit - q.base + te_win_bytes() - 1) / te_win_bytes());
+        const uint64_t *prev_tot =
+            k ? (const uint64_t *)(pb->d_win + ((20ull * pb->win_cap + 8 + 7) & ~7ull)) : NULL;
+        q.entry_ptr = prev_tot;
+        q.entry_sub = k ? C : 0; /* the previous chunk's image is C bytes earlier */
+        /* the window kernel: after the upload, and after the slot's last output copy */
+        HIPCHK(t, hipStreamWaitEvent(t->stream, P->h2d_done[s], 0));
+        HIPCHK(t, hipStreamWaitEvent(t->stream, P->d2h_done[s], 0));
+        b->win_req = &q;
+        const int lr = launch(b, -1);
+        b->win_req = NULL;
+        if (lr != 0) {
+            te_seterr(t, "window-mode launch failed: %s", hipGetErrorString(hipGetLastError()));
+            goto fail;
+        }
+        if (k && te_launch_win_tail(pb->d_out, b->d_out, prev_tot, C, 24 + TE_PIPE_MARGIN, t->stream) != 0)
+            goto fail;
+        if (te_launch_win_acc((const uint64_t *)(b->d_ws + WS_SLOTS(0)), (uint32_t)b->last_fgrid,
+                              (const uint32_t *)(b->d_win + 20ull * b->win_cap), P->d_wacc, t->stream) != 0)
+            goto fail;
+        HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
+        /* the chunk's file range down, behind its edit */
+        HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
+        HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + 24, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
+        HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+        last = s;
+    }
+    {
+        tcpedit_batch_t *b = P->slot[last];
+        HIPCHK(t, hipMemcpyAsync(P->h_wacc, P->d_wacc, 32, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(P->h_wacc + 4, b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull), 8,
+                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+        HIPCHK(t, hipStreamSynchronize(P->s_d2h));
+    }
+    if (trace)
+        fprintf(stderr, "pipe (window mode): %d chunks, %.3f ms, verdict %llu\n", nch, (te_now() - t0) * 1e3,
+                (unsigned long long)P->h_wacc[3]);
+    if (P->h_wacc[3])
+        return 1;
+    {
+        const uint64_t *acc = P->h_wacc;
+        const uint64_t f0 = 24 + (uint64_t)(nch - 1) * C;
+        const uint64_t end = f0 + acc[4] - 24; /* the last chunk's chain end, as a file offset */
+        if (acc[1] != end - 24 || end > in_len)
+            return 1; /* (the records and the chain must agree) */
+        *pos_io = end;
+        t->pub.runtime.packetnum += acc[0];
+        t->pub.runtime.total_bytes += acc[1];
+        t->pub.runtime.pkts_edited += acc[2];
+    }
+    return 0;
+fail:
+    hipStreamSynchronize(P->s_h2d);
+    hipStreamSynchronize(t->stream);
+    hipStreamSynchronize(P->s_d2h);
+    return -1;
+}
+
 int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, const void *cache, size_t cache_len,
                                    void *out, size_t out_cap, size_t *out_len, size_t chunk_bytes)
 {
@@ -3244,6 +3370,19 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             te_walk_t proto;
             cut_setup(t, bs, &proto);
             dix &= bs->cut_device_ok;
+        }
+        if (dix && b0->fast_kind == TE_FAST_WAVE && !b0->slot_layout && !d_dirbits && !b0->swapped && !b0->nsec &&
+            static_capable(&t->cfg) && fast_capable(&t->cfg) && !fast_lane_off() && !win_pipe_off()) {
+            /* the window mode: no index passes and no host wait per chunk */
+            const int r = pipe_run_win(t, P, img, in_len, dst, out_cap, &pos, trace);
+            if (r < 0)
+                goto fail;
+            if (r == 0) {
+                *out_len = pos;
+                rc = TCPEDIT_OK;
+                goto out;
+            }
+            pos = 24; /* (the exact pipeline below redoes the capture) */
         }
         if (dix && b0->fast_kind == TE_FAST_WAVE) {
             /* scratch for huge records, sized for the worst chunk (the index places them) */

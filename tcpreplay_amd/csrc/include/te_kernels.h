@@ -263,6 +263,13 @@ int te_launch_q8(te_launch_t *L, hipStream_t stream);
 int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
 /* the Juniper state scan alone, and the state the launch leaves in *out (a shard's carry-out) */
 int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream);
+/* the window-mode pipeline: a chunk image's bytes before its first record from the previous
+   chunk's output image (sub: the chunks' file distance), and a chunk's block totals and
+   chain verdict added to the call's accumulator {packets, bytes, edited, bad} */
+int te_launch_win_tail(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr, uint64_t sub,
+                       uint64_t max_e, hipStream_t stream);
+int te_launch_win_acc(const uint64_t *slots, uint32_t nblk, const uint32_t *win_bad, uint64_t *acc,
+                      hipStream_t stream);
 int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);

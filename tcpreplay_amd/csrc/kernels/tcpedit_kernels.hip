@@ -3029,6 +3029,61 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
 
 extern "C" uint32_t te_win_bytes(void) { return (uint32_t)WIN_WN; }
 
+// ---------------------------------------------------------------------------
+// the window-mode pipeline (tcpedit_rewrite_pcap_pipelined for the wave lane's
+// size-preserving configs): chunk images hold fixed byte ranges of the file, so a chunk's
+// output image holds its file range's bytes at the same offsets once the bytes before its
+// first record -- the previous chunk's last record, edited there -- are copied over from
+// the previous chunk's output (te_win_head).  te_win_acc adds a chunk's block totals and
+// its chain verdict to the call's accumulator on the device: no host wait per chunk.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void te_win_head(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr,
+                                                   uint64_t sub, uint64_t max_e) {
+    // this chunk's first record (image offset): where the previous chunk's chain ended (a
+    // chunk whose chain broke leaves no such position: the call's verdict sends the capture
+    // to the exact path, and nothing is copied here)
+    const uint64_t e = *(const volatile uint64_t *)entry_ptr - sub;
+    if (e < 24 || e > max_e) return;
+    const uint64_t t = blockIdx.x * 256ull + threadIdx.x, nt = gridDim.x * 256ull;
+    // bytes [24, e) of this image are the previous image's [24 + sub, e + sub) (sub: a
+    // multiple of 16, so both sides share their 16-byte phase)
+    if (t < 8 && 24 + t < e) out[24 + t] = prev_out[24 + sub + t];
+    const uint64_t c1 = e & ~15ull;
+    for (uint64_t c = 32 + 16 * t; c < c1; c += 16 * nt)
+        *(uint4 *)(out + c) = *(const uint4 *)(prev_out + c + sub);
+    if (t < 16 && c1 >= 32 && c1 + t < e) out[c1 + t] = prev_out[c1 + sub + t];
+}
+
+__global__ __launch_bounds__(256) void te_win_acc(const unsigned long long *slots, uint32_t nblk,
+                                                  const uint32_t *win_bad, unsigned long long *acc) {
+    unsigned long long p = 0, b = 0, e = 0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
+        p += slots[4 * i];
+        b += slots[4 * i + 1];
+        e += slots[4 * i + 2];
+    }
+    if (p) atomicAdd(&acc[0], p);
+    if (b) atomicAdd(&acc[1], b);
+    if (e) atomicAdd(&acc[2], e);
+    if (threadIdx.x == 0) {
+        const uint32_t w = *win_bad;
+        if (w) atomicOr(&acc[3], (unsigned long long)w);
+    }
+}
+
+extern "C" int te_launch_win_tail(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr, uint64_t sub,
+                                  uint64_t max_e, hipStream_t stream) {
+    hipLaunchKernelGGL(te_win_head, dim3(64), dim3(256), 0, stream, prev_out, out, entry_ptr, sub, max_e);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int te_launch_win_acc(const uint64_t *slots, uint32_t nblk, const uint32_t *win_bad, uint64_t *acc,
+                                 hipStream_t stream) {
+    hipLaunchKernelGGL(te_win_acc, dim3(1), dim3(256), 0, stream, (const unsigned long long *)slots, nblk, win_bad,
+                       (unsigned long long *)acc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream) {
     hipLaunchKernelGGL(te_packet_server, dim3(1), dim3(BLOCK), 0, stream, *S);
     return hipGetLastError() == hipSuccess ? 0 : -1;

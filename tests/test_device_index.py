@@ -145,10 +145,13 @@ def _pipe(pcap, args, cache=None, chunk=1 << 20, env=None):
     ("mixed", lambda: F.build(F.mixed(8000, seed=25)), ["--seed=7", "--fixcsum"]),
 ], ids=lambda x: x if isinstance(x, str) else "")
 def test_pipeline_device_index_matches_the_oracle(built, name, gen, args):
-    """the pipelined path with the record index built on the device: fixed 1 MiB chunks
-    (records straddle every cut; the next chunk starts where the previous chain ended,
-    read on the device)"""
-    _pipe(gen(), args)
+    """the pipelined path: fixed 1 MiB chunks (records straddle every cut; the next chunk
+    starts where the previous chain ended, read on the device) -- in window mode (the
+    wave lane finds each chunk's records itself) where the config is size-preserving, and
+    with the device record index (TCPEDIT_HIP_PIPE_NO_WIN)"""
+    pcap = gen()
+    _pipe(pcap, args)
+    _pipe(pcap, args, env={"TCPEDIT_HIP_PIPE_NO_WIN": "1"})
 
 
 def test_pipeline_device_index_edges(built):
@@ -179,5 +182,20 @@ def test_pipeline_device_index_edges(built):
         d[42:42 + len(fake)] = fake
         fooled.append((ts, tu, cl, ln, bytes(d)))
     _pipe(S.build_pcap(fooled), args)
-    # the host walk in the pipeline (A/B): the same bytes
+    # the host walk in the pipeline (A/B) and the device index without the window mode:
+    # the same bytes
     _pipe(S.build_pcap(recs), args, env={"TCPEDIT_HIP_PIPE_INDEX": "host"})
+    _pipe(S.build_pcap(recs), args, env={"TCPEDIT_HIP_PIPE_NO_WIN": "1"})
+    _pipe(over, args, env={"TCPEDIT_HIP_PIPE_NO_WIN": "1"})
+
+
+def test_window_pipeline_chunk_cuts(built):
+    """the window-mode pipeline over 1 MiB chunks: 64-byte records (the last record of
+    every chunk straddles its cut, te_win_head completes the next image), 1,514-byte
+    records, a capture one chunk long, and a capture whose last record is cut short (the
+    chain ends early: the exact pipeline redoes the capture)"""
+    args = ["--seed=42", "--fixcsum"]
+    for pcap in (S.pcap_fixed(40_000, 64, seed=41), S.pcap_mixed_v4v6(3_000, 1514, seed=42),
+                 S.pcap_fixed(5_000, 64, seed=43)):
+        _pipe(pcap, args)
+        _pipe(pcap[:-7], args)
