@@ -1174,6 +1174,12 @@ typedef struct te_win_req_s {
     uint64_t len, entry, entry_sub, base, limit;
     const uint64_t *entry_ptr;
     uint32_t nwin;
+    /* the window-mode pipeline: the call's accumulator, the previous chunk's output image,
+       the output image's device address when it is not the batch's (host-mapped) */
+    uint64_t *acc;
+    const uint8_t *prev_out;
+    uint64_t head_max;
+    uint8_t *out;
 } te_win_req_t;
 /* the window workspace layout of d_win for `cap` windows: entries | exits | flags | bad | tot */
 #define WIN_WS_BYTES(cap) (16ull * (cap) + 4ull * (cap) + 64)
@@ -1392,6 +1398,11 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.w_flags = (uint32_t *)(L.w_exit + b->win_cap);
         L.win_bad = L.w_flags + b->win_cap;
         L.win_tot = (uint64_t *)(b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull));
+        L.win_acc = q->acc;
+        L.win_prev_out = q->prev_out;
+        L.win_head_max = q->head_max;
+        if (q->out)
+            L.out = q->out;
         L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
         L.stream = (b->in_len + b->out_cap) > ((uint64_t)256 << 20);
     }
@@ -1907,6 +1918,7 @@ static int fused_capable(const tcpedit_t *t, const tcpedit_batch_t *b)
 
 static int win_ready(tcpedit_t *t, tcpedit_batch_t *b, uint64_t nwin)
 {
+    nwin = (nwin + 1) & ~1ull; /* (even: the verdict and chain-end words adjacent, one memset) */
     if (b->win_cap >= nwin)
         return 0;
     hipFree(b->d_win);
@@ -3154,45 +3166,115 @@ static int win_pipe_off(void)
     return e && *e && *e != '0';
 }
 
+/* the window-mode pipeline's chunk starts: C/4 and C/2 (at least 1 MiB) to fill the
+   pipeline, C-sized chunks, then halving pieces to drain it -- every chunk but the last a
+   multiple of 16 bytes (the head copy moves 16-byte pieces) */
+static uint64_t *win_plan(size_t in_len, uint64_t C, int *n_out)
+{
+    const uint64_t MIN = (uint64_t)1 << 20;
+    const int cap = (int)((in_len / MIN) + 16);
+    uint64_t *st = malloc(sizeof(uint64_t) * (size_t)cap);
+    if (!st)
+        return NULL;
+    int n = 0;
+    uint64_t at = 24;
+    st[n++] = at;
+    while (at < in_len && n < cap - 1) {
+        const uint64_t rem = in_len - at;
+        uint64_t sz;
+        if (n == 1)
+            sz = C / 4;
+        else if (n == 2)
+            sz = C / 2;
+        else
+            sz = rem > C + C / 2 ? C : rem / 2; /* (the drain halves what is left) */
+        if (sz < MIN)
+            sz = MIN;
+        if (sz > C)
+            sz = C;
+        sz &= ~15ull;
+        if (sz >= rem)
+            sz = rem;
+        st[n++] = (at += sz);
+    }
+    st[n - 1] = in_len;
+    *n_out = n - 1;
+    return st;
+}
+
+/* bytes past a window-mode chunk uploaded with it: a record starting in the chunk may end
+   there; one that ends further out breaks the chain (the exact pipeline redoes the capture) */
+#define TE_PIPE_WIN_MARGIN ((uint64_t)65536)
+
 /* The window-mode pipeline, for the wave lane's size-preserving configs without a tcpprep
  * cache (what tcpedit_batch_run_fused carries): chunk k is the file bytes [cst_k, cst_k+1)
- * uploaded with the next TE_PIPE_MARGIN bytes and edited in window mode -- the wave lane
+ * uploaded with the next TE_PIPE_WIN_MARGIN bytes and edited in window mode -- the wave lane
  * finds its records itself, the first where the previous chunk's chain ended (read on the
  * device).  Records keep their file offsets, so the chunk's output image, completed with
- * the previous chunk's last record (te_win_head), goes down as the same file range.  No
- * host wait per chunk: the block totals and the chain verdicts gather on the device and
- * are read once at the end.  Returns 0 (*pos_io: the output's end), 1 (a chunk missed the
- * chain, a chain end or a record the window mode leaves to the exact path: the caller runs
- * the exact pipeline over the whole capture; the same bytes), or -1. */
+ * the previous chunk's last record (the check launch copies it), goes down as the same file
+ * range.  No host wait per chunk beyond keeping two chunks ahead: the block totals and
+ * chain verdicts gather on the device, read once at the end.  Returns 0 (*pos_io: the
+ * output's end), 1 (a chunk missed the chain, a chain end or a record the window mode
+ * leaves to the exact path: the caller runs the exact pipeline over the whole capture;
+ * the same bytes), or -1. */
 static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t in_len, uint8_t *dst, size_t out_cap,
                         uint64_t *pos_io, int trace)
 {
     const uint64_t C = P->chunk;
-    int nch = (int)((in_len - 24 + C - 1) / C);
-    if (nch < 1)
-        nch = 1;
     if (in_len > out_cap || in_len < 24 + 16)
         return 1; /* (the copies move whole file ranges) */
+    int nch = 0;
+    uint64_t *cst = win_plan(in_len, C, &nch);
+    if (!cst) {
+        te_seterr(t, "out of memory");
+        return -1;
+    }
     const double t0 = te_now();
     if (!P->d_wacc) {
         HIPCHK(t, hipMalloc((void **)&P->d_wacc, 64));
         HIPCHK(t, hipHostMalloc((void **)&P->h_wacc, 64, 0));
     }
-    const uint64_t limit_max = 24 + C;
-    const uint32_t nwin_max = (uint32_t)((limit_max - 16 + te_win_bytes() - 1) / te_win_bytes());
-    for (int s = 0; s < TE_PIPE_SLOTS; s++) {
-        tcpedit_batch_t *b = P->slot[s];
-        b->out_cap = C + TE_PIPE_MARGIN + 24;
-        if (win_ready(t, b, nwin_max) < 0 || pipe_grow(t, P, s) < 0)
-            return -1;
+    {
+        const uint64_t limit_max = 24 + C;
+        const uint32_t nwin_max = (uint32_t)((limit_max - 16 + te_win_bytes() - 1) / te_win_bytes());
+        for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+            tcpedit_batch_t *b = P->slot[s];
+            b->out_cap = C + TE_PIPE_WIN_MARGIN + 24;
+            if (win_ready(t, b, nwin_max) < 0 || pipe_grow(t, P, s) < 0)
+                goto fail;
+        }
     }
     HIPCHK(t, hipMemsetAsync(P->d_wacc, 0, 32, t->stream));
     int last = 0;
+    /* TCPEDIT_HIP_PIPE_ZC=1 (A/B): the output written by the kernel straight into the
+       caller's page-locked buffer over PCIe (its device address) -- no D2H copies, and a
+       chunk's last record is written whole by its own launch, so no head copy either.  On
+       C2 the kernel's PCIe writes ran at ~34 GB/s and the call took 2.35 ms against 2.18
+       with the copies, so the copies stay the default */
+    uint8_t *zc = NULL;
+    {
+        const char *e = getenv("TCPEDIT_HIP_PIPE_ZC");
+        void *dp = NULL;
+        /* (the stores reach up to 15 bytes past the last record: room for them) */
+        if (e && *e == '1' && out_cap >= in_len + 16 && hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp)
+            zc = (uint8_t *)dp;
+        (void)hipGetLastError();
+    }
+    /* chunks enqueued ahead of the oldest unfinished edit (TCPEDIT_HIP_PIPE_WIN_AHEAD, A/B):
+       the host keeps the streams' cross waits few instead of queueing the whole capture */
+    int ahead = 2;
+    {
+        const char *e = getenv("TCPEDIT_HIP_PIPE_WIN_AHEAD");
+        if (e && *e)
+            ahead = atoi(e);
+    }
     for (int k = 0; k < nch; k++) {
         const int s = k % TE_PIPE_SLOTS, ps = (k + TE_PIPE_SLOTS - 1) % TE_PIPE_SLOTS;
         tcpedit_batch_t *b = P->slot[s], *pb = P->slot[ps];
-        const uint64_t f0 = 24 + (uint64_t)k * C, f1 = f0 + C < in_len ? f0 + C : in_len;
-        const uint64_t fe = f1 + TE_PIPE_MARGIN < in_len ? f1 + TE_PIPE_MARGIN : in_len;
+        if (ahead > 0 && ahead < TE_PIPE_SLOTS && k >= ahead)
+            HIPCHK(t, hipEventSynchronize(P->edit_done[(k - ahead) % TE_PIPE_SLOTS]));
+        const uint64_t f0 = cst[k], f1 = cst[k + 1];
+        const uint64_t fe = f1 + TE_PIPE_WIN_MARGIN < in_len ? f1 + TE_PIPE_WIN_MARGIN : in_len;
         /* upload (the slot's last window kernel has read its input) */
         if (k >= TE_PIPE_SLOTS)
             HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s], 0));
@@ -3211,13 +3293,16 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         q.base = 16;
         q.limit = f1 >= in_len ? b->in_len : 24 + (f1 - f0);
         q.nwin = (uint32_t)((q.limit - q.base + te_win_bytes() - 1) / te_win_bytes());
-        const uint64_t *prev_tot =
-            k ? (const uint64_t *)(pb->d_win + ((20ull * pb->win_cap + 8 + 7) & ~7ull)) : NULL;
-        q.entry_ptr = prev_tot;
-        q.entry_sub = k ? C : 0; /* the previous chunk's image is C bytes earlier */
+        q.entry_ptr = k ? (const uint64_t *)(pb->d_win + ((20ull * pb->win_cap + 8 + 7) & ~7ull)) : NULL;
+        q.entry_sub = k ? f0 - cst[k - 1] : 0; /* the previous chunk's image is that much earlier */
+        q.acc = P->d_wacc;
+        q.prev_out = k && !zc ? pb->d_out : NULL;
+        q.head_max = 24 + TE_PIPE_WIN_MARGIN;
+        q.out = zc ? zc + (f0 - 24) : NULL; /* (image offset x is file offset f0 + x - 24) */
         /* the window kernel: after the upload, and after the slot's last output copy */
         HIPCHK(t, hipStreamWaitEvent(t->stream, P->h2d_done[s], 0));
-        HIPCHK(t, hipStreamWaitEvent(t->stream, P->d2h_done[s], 0));
+        if (!zc)
+            HIPCHK(t, hipStreamWaitEvent(t->stream, P->d2h_done[s], 0));
         b->win_req = &q;
         const int lr = launch(b, -1);
         b->win_req = NULL;
@@ -3225,16 +3310,12 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             te_seterr(t, "window-mode launch failed: %s", hipGetErrorString(hipGetLastError()));
             goto fail;
         }
-        if (k && te_launch_win_tail(pb->d_out, b->d_out, prev_tot, C, 24 + TE_PIPE_MARGIN, t->stream) != 0)
-            goto fail;
-        if (te_launch_win_acc((const uint64_t *)(b->d_ws + WS_SLOTS(0)), (uint32_t)b->last_fgrid,
-                              (const uint32_t *)(b->d_win + 20ull * b->win_cap), P->d_wacc, t->stream) != 0)
-            goto fail;
         HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
-        /* the chunk's file range down, behind its edit */
-        HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
-        HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + 24, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
-        HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+        if (!zc) { /* the chunk's file range down, behind its edit */
+            HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
+            HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + 24, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
+            HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+        }
         last = s;
     }
     {
@@ -3246,15 +3327,14 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipStreamSynchronize(P->s_d2h));
     }
     if (trace)
-        fprintf(stderr, "pipe (window mode): %d chunks, %.3f ms, verdict %llu\n", nch, (te_now() - t0) * 1e3,
-                (unsigned long long)P->h_wacc[3]);
-    if (P->h_wacc[3])
-        return 1;
+        fprintf(stderr, "pipe (window mode%s): %d chunks, %.3f ms, verdict %llu\n", zc ? ", output over PCIe" : "",
+                nch, (te_now() - t0) * 1e3, (unsigned long long)P->h_wacc[3]);
     {
         const uint64_t *acc = P->h_wacc;
-        const uint64_t f0 = 24 + (uint64_t)(nch - 1) * C;
+        const uint64_t f0 = cst[nch - 1];
         const uint64_t end = f0 + acc[4] - 24; /* the last chunk's chain end, as a file offset */
-        if (acc[1] != end - 24 || end > in_len)
+        free(cst);
+        if (acc[3] || acc[1] != end - 24 || end > in_len)
             return 1; /* (the records and the chain must agree) */
         *pos_io = end;
         t->pub.runtime.packetnum += acc[0];
@@ -3266,6 +3346,7 @@ fail:
     hipStreamSynchronize(P->s_h2d);
     hipStreamSynchronize(t->stream);
     hipStreamSynchronize(P->s_d2h);
+    free(cst);
     return -1;
 }
 

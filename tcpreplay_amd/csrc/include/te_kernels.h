@@ -210,6 +210,13 @@ typedef struct {
     uint32_t *win_bad;           /* device word, zeroed by the launch: bit 0 the chain missed or
                                     stopped, bit 1 a record left to the exact path */
     uint64_t *win_tot;           /* device: [0] the chain's end (image offset), zeroed by the launch */
+    /* the window-mode pipeline's per-chunk steps, in the check's launch: the call's device
+       accumulator {packets, bytes, edited, verdict} (or NULL), and the previous chunk's output
+       image whose bytes before this chunk's first record are copied in (or NULL; a first
+       record past win_head_max is no chain's: nothing copied) */
+    uint64_t *win_acc;
+    const uint8_t *win_prev_out;
+    uint64_t win_head_max;
 } te_launch_t;
 /* bytes a window of the window mode owns */
 uint32_t te_win_bytes(void);
@@ -263,13 +270,7 @@ int te_launch_q8(te_launch_t *L, hipStream_t stream);
 int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
 /* the Juniper state scan alone, and the state the launch leaves in *out (a shard's carry-out) */
 int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream);
-/* the window-mode pipeline: a chunk image's bytes before its first record from the previous
-   chunk's output image (sub: the chunks' file distance), and a chunk's block totals and
-   chain verdict added to the call's accumulator {packets, bytes, edited, bad} */
-int te_launch_win_tail(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr, uint64_t sub,
-                       uint64_t max_e, hipStream_t stream);
-int te_launch_win_acc(const uint64_t *slots, uint32_t nblk, const uint32_t *win_bad, uint64_t *acc,
-                      hipStream_t stream);
+
 int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);

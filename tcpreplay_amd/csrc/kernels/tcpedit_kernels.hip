@@ -1588,7 +1588,13 @@ __device__ __forceinline__ void vdel_view(uint32_t (&H)[fl::NW], const uint32_t 
 // it for te_win_check; a record the lane cannot finish sets win_bad, and the caller then runs
 // the exact path (index + tiles) instead.
 template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
-__global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
+#ifndef TE_WIN_PREFETCH
+#define TE_WIN_PREFETCH 0
+#endif
+#ifndef TE_WIN_BLOCKS
+#define TE_WIN_BLOCKS TE_WK_MIN_BLOCKS  // window mode: blocks per CU (its VGPR budget)
+#endif
+__global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
@@ -1958,8 +1964,17 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks
         ia.nsec = 0;
         uint8_t *const IMG = SB[wid];       // the staged window at IMG + LDS_FRONT
         uint32_t *const REL = RELB[WIN ? wid : 0];
+        // TE_WIN_PREFETCH: the next window's staging in flight in registers while this one
+        // is edited (A/B: on C2 it cost more in registers -- spills at 4 blocks/CU, or a
+        // quarter of the occupancy at 3 -- than the overlap won)
+        tew::Staging<WIN_S, WIN_OL, WIN_PRE> stg;
+        if (TE_WIN_PREFETCH && w0 < a.nwin) tew::stage_load(ia, w0, stg);
         for (uint32_t k = w0; k < a.nwin; k += W) {
-            const tew::Found fw = tew::find_window<WIN_S, WIN_OL, WIN_PRE>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+            if (!TE_WIN_PREFETCH) tew::stage_load(ia, k, stg);
+            tew::stage_store(ia, k, stg, (uint32_t *)(IMG + LDS_FRONT));
+            const tew::Found fw =
+                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+            if (TE_WIN_PREFETCH && k + W < a.nwin) tew::stage_load(ia, k + W, stg);
             WK_STAMP(0)  // (window mode: the record discovery)
             const uint32_t wfl = fw.wstop | (fw.anyzero ? (uint32_t)IDX_ZERO : 0u);
             if (lane == 0) {
@@ -2055,7 +2070,65 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WK_MIN_BLOCKS : WkCfg<F>::blocks
 // over whole; a chain end, an empty record or a miss sends the batch to the exact path.
 // The chain's end (the next pipeline chunk's first record) is the largest exit.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long long *tot) {
+// The window-mode pipeline's per-chunk steps ride in the same launch (WinTail): one block
+// adds the chunk's block totals and the edit's verdict bits to the call's accumulator
+// {packets, bytes, edited, verdict} (the check blocks OR their own verdict in too), and
+// WIN_HEAD_BLOCKS blocks copy the bytes before the chunk's first record -- the previous
+// chunk's last record, edited there -- from the previous chunk's output image, so the
+// chunk's output image holds its whole file range.
+struct WinTail {
+    unsigned long long *acc;  // null: a batch, no accumulator
+    const unsigned long long *slots;
+    uint32_t nslots, ncheck;   // the edit's blocks; the check's blocks
+    const uint8_t *prev_out;   // null: no head copy (the first chunk, a batch)
+    uint8_t *out;
+    uint64_t head_max;         // a first record further in is no chain's: nothing copied
+};
+constexpr uint32_t WIN_HEAD_BLOCKS = 64;
+
+__device__ void win_head_copy(const FastArgs &a, const WinTail &w, uint32_t blk) {
+    const uint64_t sub = a.win_entry_sub;
+    // this chunk's first record (image offset): where the previous chunk's chain ended (a
+    // chunk whose chain broke leaves no such position: the call's verdict sends the capture
+    // to the exact path, and nothing is copied here)
+    const uint64_t e = *(const volatile uint64_t *)a.win_entry_ptr - sub;
+    if (e < 24 || e > w.head_max) return;
+    const uint64_t t = blk * 256ull + threadIdx.x, nt = WIN_HEAD_BLOCKS * 256ull;
+    if (sub & 15) {  // (a chunk size that is not a multiple of 16: byte by byte)
+        for (uint64_t x = 24 + t; x < e; x += nt) w.out[x] = w.prev_out[x + sub];
+        return;
+    }
+    // bytes [24, e) of this image are the previous image's [24 + sub, e + sub); both sides
+    // share their 16-byte phase
+    if (t < 8 && 24 + t < e) w.out[24 + t] = w.prev_out[24 + sub + t];
+    const uint64_t c1 = e & ~15ull;
+    for (uint64_t c = 32 + 16 * t; c < c1; c += 16 * nt)
+        *(uint4 *)(w.out + c) = *(const uint4 *)(w.prev_out + c + sub);
+    if (t < 16 && c1 >= 32 && c1 + t < e) w.out[c1 + t] = w.prev_out[c1 + sub + t];
+}
+
+__global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long long *tot, WinTail w) {
+    if (blockIdx.x >= w.ncheck) {
+        const uint32_t b = blockIdx.x - w.ncheck;
+        if (w.acc && b == 0) {  // the chunk's totals and the edit's verdict bits
+            unsigned long long p = 0, by = 0, e = 0;
+            for (uint32_t i = threadIdx.x; i < w.nslots; i += 256) {
+                p += w.slots[4 * i];
+                by += w.slots[4 * i + 1];
+                e += w.slots[4 * i + 2];
+            }
+            if (p) atomicAdd(&w.acc[0], p);
+            if (by) atomicAdd(&w.acc[1], by);
+            if (e) atomicAdd(&w.acc[2], e);
+            if (threadIdx.x == 0) {
+                const uint32_t v = *a.win_bad & 2u;  // (the edit is done: its bits are all in)
+                if (v) atomicOr(&w.acc[3], (unsigned long long)v);
+            }
+        } else if (w.prev_out) {
+            win_head_copy(a, w, b - (w.acc ? 1u : 0u));
+        }
+        return;
+    }
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= a.nwin) return;
     const uint64_t entry = a.win_entry_ptr ? *(const volatile uint64_t *)a.win_entry_ptr - a.win_entry_sub
@@ -2079,7 +2152,10 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
             bad |= xj < (qe < a.win_limit ? qe : a.win_limit);
         }
     }
-    if (bad) atomicOr(a.win_bad, 1u);
+    if (bad) {
+        atomicOr(a.win_bad, 1u);
+        if (w.acc) atomicOr(&w.acc[3], 1ull);
+    }
     if (went != IDX_NONE) atomicMax(&tot[0], (unsigned long long)a.w_exit[k]);
 }
 
@@ -2894,16 +2970,28 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         const uint32_t need = (L->nwin + WK_NW - 1) / WK_NW;
         if ((uint32_t)grid > need) grid = (int)need;
         if (grid < 1 || ((L->out_base - L->rec0) & 15)) return -1;
-        if (hipMemsetAsync(L->win_bad, 0, 4, stream) != hipSuccess ||
-            hipMemsetAsync(L->win_tot, 0, 8, stream) != hipSuccess)
+        if ((uint8_t *)L->win_tot == (uint8_t *)L->win_bad + 8) {  // (one memset: adjacent words)
+            if (hipMemsetAsync(L->win_bad, 0, 16, stream) != hipSuccess) return -1;
+        } else if (hipMemsetAsync(L->win_bad, 0, 4, stream) != hipSuccess ||
+                   hipMemsetAsync(L->win_tot, 0, 8, stream) != hipSuccess) {
             return -1;
+        }
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
         {
             void *args[] = {&f};
             if (hipLaunchKernel(win_inst[wk].fn, dim3(grid), dim3(WKB), args, 0, stream) != hipSuccess) return -1;
         }
-        hipLaunchKernelGGL(te_win_check, dim3((L->nwin + 255) / 256), dim3(256), 0, stream, f,
-                           (unsigned long long *)L->win_tot);
+        WinTail wt;
+        wt.acc = (unsigned long long *)L->win_acc;
+        wt.slots = (const unsigned long long *)L->slots;
+        wt.nslots = (uint32_t)grid;
+        wt.ncheck = (L->nwin + 255) / 256;
+        wt.prev_out = L->win_prev_out && L->win_entry_ptr ? L->win_prev_out : nullptr;
+        wt.out = L->out;
+        wt.head_max = L->win_head_max;
+        const uint32_t nx = (wt.acc ? 1u : 0u) + (wt.prev_out ? WIN_HEAD_BLOCKS : 0u);
+        hipLaunchKernelGGL(te_win_check, dim3(wt.ncheck + nx), dim3(256), 0, stream, f,
+                           (unsigned long long *)L->win_tot, wt);
         if (L->ev_k1 && hipEventRecord((hipEvent_t)L->ev_k1, stream) != hipSuccess) return -1;
         L->out_fgrid = grid;
         return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -3029,60 +3117,6 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
 
 extern "C" uint32_t te_win_bytes(void) { return (uint32_t)WIN_WN; }
 
-// ---------------------------------------------------------------------------
-// the window-mode pipeline (tcpedit_rewrite_pcap_pipelined for the wave lane's
-// size-preserving configs): chunk images hold fixed byte ranges of the file, so a chunk's
-// output image holds its file range's bytes at the same offsets once the bytes before its
-// first record -- the previous chunk's last record, edited there -- are copied over from
-// the previous chunk's output (te_win_head).  te_win_acc adds a chunk's block totals and
-// its chain verdict to the call's accumulator on the device: no host wait per chunk.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void te_win_head(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr,
-                                                   uint64_t sub, uint64_t max_e) {
-    // this chunk's first record (image offset): where the previous chunk's chain ended (a
-    // chunk whose chain broke leaves no such position: the call's verdict sends the capture
-    // to the exact path, and nothing is copied here)
-    const uint64_t e = *(const volatile uint64_t *)entry_ptr - sub;
-    if (e < 24 || e > max_e) return;
-    const uint64_t t = blockIdx.x * 256ull + threadIdx.x, nt = gridDim.x * 256ull;
-    // bytes [24, e) of this image are the previous image's [24 + sub, e + sub) (sub: a
-    // multiple of 16, so both sides share their 16-byte phase)
-    if (t < 8 && 24 + t < e) out[24 + t] = prev_out[24 + sub + t];
-    const uint64_t c1 = e & ~15ull;
-    for (uint64_t c = 32 + 16 * t; c < c1; c += 16 * nt)
-        *(uint4 *)(out + c) = *(const uint4 *)(prev_out + c + sub);
-    if (t < 16 && c1 >= 32 && c1 + t < e) out[c1 + t] = prev_out[c1 + sub + t];
-}
-
-__global__ __launch_bounds__(256) void te_win_acc(const unsigned long long *slots, uint32_t nblk,
-                                                  const uint32_t *win_bad, unsigned long long *acc) {
-    unsigned long long p = 0, b = 0, e = 0;
-    for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
-        p += slots[4 * i];
-        b += slots[4 * i + 1];
-        e += slots[4 * i + 2];
-    }
-    if (p) atomicAdd(&acc[0], p);
-    if (b) atomicAdd(&acc[1], b);
-    if (e) atomicAdd(&acc[2], e);
-    if (threadIdx.x == 0) {
-        const uint32_t w = *win_bad;
-        if (w) atomicOr(&acc[3], (unsigned long long)w);
-    }
-}
-
-extern "C" int te_launch_win_tail(const uint8_t *prev_out, uint8_t *out, const uint64_t *entry_ptr, uint64_t sub,
-                                  uint64_t max_e, hipStream_t stream) {
-    hipLaunchKernelGGL(te_win_head, dim3(64), dim3(256), 0, stream, prev_out, out, entry_ptr, sub, max_e);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-extern "C" int te_launch_win_acc(const uint64_t *slots, uint32_t nblk, const uint32_t *win_bad, uint64_t *acc,
-                                 hipStream_t stream) {
-    hipLaunchKernelGGL(te_win_acc, dim3(1), dim3(256), 0, stream, (const unsigned long long *)slots, nblk, win_bad,
-                       (unsigned long long *)acc);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 extern "C" int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream) {
     hipLaunchKernelGGL(te_packet_server, dim3(1), dim3(BLOCK), 0, stream, *S);

@@ -103,10 +103,65 @@ struct Found {
     u32 wstop, nrec;
     bool anyzero;     // a record with caplen 0
 };
+// a window's staging: its 16-byte chunks [c0, nch) from A0, in registers (K a lane) until
+// stored to LDS -- issued one window ahead by the fused edit, so the loads are in flight
+// while it edits the window before
+template <int S, int OL, int PRE>
+struct Staging {
+    static constexpr int W = IW * S, O = OL * S, WN = W - O;
+    static constexpr int K = (W + 48 + PRE + 16 * IW - 1) / (16 * IW);
+    uint4 v[K];
+};
+
+// window k's byte range: [ws, we) owned, staged [lo_stage, staged_end) from A0
+template <int S, int OL, int PRE>
+__device__ __forceinline__ void window_range(const IdxArgs &a, u32 k, u64 &ws, u64 &we, u64 &A0, u64 &lo_stage,
+                                             u64 &staged_end) {
+    constexpr int W = IW * S, O = OL * S, WN = W - O;
+    ws = a.base + (u64)k * WN;
+    we = ws + WN < a.limit ? ws + WN : a.limit;
+    A0 = ws - O;  // lane l's sub-window starts at A0 + l S (window 0: none before base)
+    lo_stage = k ? A0 : a.base;
+    // bytes [lo_stage, staged_end) are in LDS (past a.len: garbage; never more than 16 past it)
+    staged_end = PRE == 0 ? we + 16 : (we + 16 + PRE < a.len + 16 ? we + 16 + PRE : (we > a.len ? we : a.len) + 16);
+}
+
+// the loads of window k's staging (in flight until stage_store)
+template <int S, int OL, int PRE>
+__device__ __forceinline__ void stage_load(const IdxArgs &a, u32 k, Staging<S, OL, PRE> &st) {
+    u64 ws, we, A0, lo_stage, staged_end;
+    window_range<S, OL, PRE>(a, k, ws, we, A0, lo_stage, staged_end);
+    const int lane = threadIdx.x & 63;
+    const u32 c0 = (u32)((lo_stage - A0) >> 4);
+    const u32 nch = (u32)((staged_end - A0 + 15) >> 4);
+    const uint4 *g = (const uint4 *)(a.img + A0);
+#pragma unroll
+    for (int i = 0; i < Staging<S, OL, PRE>::K; ++i) {
+        const u32 c = lane + i * IW;
+        st.v[i] = (c >= c0 && c < nch) ? g[c] : make_uint4(0, 0, 0, 0);
+    }
+}
+
+// the staging into LDS (waits for its loads)
+template <int S, int OL, int PRE>
+__device__ __forceinline__ void stage_store(const IdxArgs &a, u32 k, const Staging<S, OL, PRE> &st, u32 *img) {
+    constexpr int W = IW * S;
+    u64 ws, we, A0, lo_stage, staged_end;
+    window_range<S, OL, PRE>(a, k, ws, we, A0, lo_stage, staged_end);
+    const int lane = threadIdx.x & 63;
+    const u32 nch = (u32)((staged_end - A0 + 15) >> 4);
+#pragma unroll
+    for (int i = 0; i < Staging<S, OL, PRE>::K; ++i) {
+        const u32 c = lane + i * IW;
+        if (c < nch && c < (u32)((W + 48 + PRE) / 16)) *(uint4 *)&img[4 * c] = st.v[i];
+    }
+}
+
 // img: (W + 48 + PRE) / 4 dwords at least (W = 64 S); rel: 4 S + 1 entries.  PRE: bytes
 // staged past the window's end + 16 (the fused edit's last record reaching past the window:
-// in LDS with the window, no second dependent load for it)
-template <int S, int OL, int PRE = 0>
+// in LDS with the window, no second dependent load for it).  STAGED: the caller has stored
+// window k's staging into img already (stage_load / stage_store)
+template <int S, int OL, int PRE = 0, bool STAGED = false>
 __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *rel, u32 k) {
     constexpr int W = IW * S;       // staged sub-window bytes
     constexpr int O = OL * S;       // overlap before the window
@@ -129,7 +184,7 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     const u64 staged_end = PRE == 0 ? we + 16 : (we + 16 + PRE < a.len + 16 ? we + 16 + PRE : (we > a.len ? we : a.len) + 16);
 
     // ---- stage the window: 16-byte chunks, all loads in flight before the LDS stores ----
-    {
+    if constexpr (!STAGED) {
         const u32 c0 = (u32)((lo_stage - A0) >> 4);
         const u32 nch = (u32)((staged_end - A0 + 15) >> 4);
         const uint4 *g = (const uint4 *)(a.img + A0);
@@ -201,25 +256,24 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     bool has = e != IDX_NONE;
 
     // ---- where the chain starts: the first guess the next guess confirms (its walk ends
-    // exactly there, or at a strong candidate).  A guess that is not a record start jumps by a garbage length, so it is
-    // confirmed only when it lands on the chain anyway (and then the chain is right from
-    // there on); window 0's known first record needs no confirmation ----
+    // exactly there, or at a strong candidate).  A guess that is not a record start jumps by
+    // a garbage length, so it is confirmed only when it lands on the chain anyway (and then
+    // the chain is right from there on); window 0's known first record needs no
+    // confirmation.  Lane sets are ballots: the next guessing lane is a bit search, not a
+    // wave scan; offsets travel relative to A0 in 32 bits (a walk ends < 2^20 bytes on) ----
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < this one
     {
-        int nsrc = has ? lane : 64;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_down(nsrc, o, 64);
-            if (lane + o < 64 && y < nsrc) nsrc = y;
-        }
-        int nxt = __shfl_down(nsrc, 1, 64);
-        if (lane == 63) nxt = 64;
-        const u64 ng = __shfl(e, nxt < 64 ? nxt : 0);
+        const unsigned long long hm0 = __ballot(has);
+        const unsigned long long after = hm0 & ~below & ~(1ull << lane);
+        const int nxt = after ? __builtin_ctzll(after) : 64;
+        const u32 ngr = (u32)__shfl((int)(has ? (u32)(e - A0) : 0u), nxt < 64 ? nxt : 0);
+        const u64 ng = A0 + ngr;
         // (or its walk ends at a strong candidate inside the window: a wrong guess next to a
         // record start would otherwise hide the record start's confirmation)
         const bool confirmed = has && !w.stop &&
                                ((nxt < 64 && w.exit == ng) ||
                                 (w.exit < we && strength(a, img, A0, staged_end, w.exit) == 2));
-        const u64 cm = __ballot(confirmed), hm0 = __ballot(has);
+        const unsigned long long cm = __ballot(confirmed);
         const int start = k == kE ? laneE : (cm ? __builtin_ctzll(cm) : (hm0 ? __builtin_ctzll(hm0) : 64));
         if (lane < start) {
             has = false;
@@ -231,19 +285,15 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     // known first record); after it, lane l's first record must be where the nearest earlier
     // guessing lane's walk ended (P), and no lane the chain passes over may keep a guess.
     // Jacobi rounds, each fixing at least the first inconsistent lane, until every lane agrees
-    // (in practice one or two); the serial lane loop after 8 rounds ----
+    // (in practice one or two); the serial lane loop after 8 rounds.  The nearest earlier
+    // guessing lane is a bit search on the ballot; its exit and stop come in one shuffle ----
     bool settled = false;
     for (int round = 0; round < 8; ++round) {
-        int src = has ? lane : -1;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(src, o, 64);
-            if (lane >= o && y > src) src = y;
-        }
-        int prev = __shfl_up(src, 1, 64);
-        if (lane == 0) prev = -1;
-        const u64 P = __shfl(w.exit, prev < 0 ? 0 : prev);
-        const u32 pstop = (u32)__shfl((int)w.stop, prev < 0 ? 0 : prev);
+        const unsigned long long hb = __ballot(has) & below;
+        const int prev = hb ? 63 - __builtin_clzll(hb) : -1;
+        const u32 xs = (u32)__shfl((int)((((u32)(w.exit - A0)) << 3) | w.stop), prev < 0 ? 0 : prev);
+        const u64 P = A0 + (xs >> 3);
+        const u32 pstop = xs & 7u;
         bool change = false;
         if (prev >= 0 && active) {
             if (pstop) {  // the chain ended before this lane
@@ -300,22 +350,22 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     }
     // only the window's own lanes' records count (the overlap's are window k - 1's)
     if (lane < OL) has = false;
-    // the window's entry, exit and how the chain ends here
-    const u64 hm = __ballot(has);
+    // the window's entry, exit and how the chain ends here (wave-uniform lanes: readlane)
+    const unsigned long long hm = __ballot(has);
     const int fl = hm ? __builtin_ctzll(hm) : 0, ll = hm ? 63 - __builtin_clzll(hm) : 0;
-    const u64 went = hm ? __shfl(e, fl) : IDX_NONE;
-    const u64 wexit = hm ? __shfl(w.exit, ll) : IDX_NONE;
-    const u32 wstop = hm ? (u32)__shfl((int)w.stop, ll) : 0u;
-    // ---- the window's records: positions (wave scan), offsets into LDS ----
+    const u64 went = hm ? A0 + (u32)__builtin_amdgcn_readlane((int)(u32)(e - A0), fl) : IDX_NONE;
+    const u32 xl = (u32)__builtin_amdgcn_readlane((int)((((u32)(w.exit - A0)) << 3) | w.stop), ll);
+    const u64 wexit = hm ? A0 + (xl >> 3) : IDX_NONE;
+    const u32 wstop = hm ? (xl & 7u) : 0u;
+    // ---- the window's records: positions, offsets into LDS.  A lane takes at most S / 16
+    // records (< 8): its count's three bits are three ballots, its position their popcounts
+    // below it ----
+    static_assert(S / 16 < 8, "a lane's record count fits three bits");
     const u32 n = has ? w.n : 0;
-    u32 pos = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = __shfl_up(pos, o, 64);
-        if (lane >= o) pos += y;
-    }
-    const u32 nrec = __shfl(pos, 63);
-    pos -= n;
+    const unsigned long long n0 = __ballot(n & 1u), n1 = __ballot(n & 2u), n2 = __ballot(n & 4u);
+    const u32 pos = (u32)(__builtin_popcountll(n0 & below) + 2 * __builtin_popcountll(n1 & below) +
+                          4 * __builtin_popcountll(n2 & below));
+    const u32 nrec = (u32)(__builtin_popcountll(n0) + 2 * __builtin_popcountll(n1) + 4 * __builtin_popcountll(n2));
     bool zero = false;
     if (has) {
         u64 off = e;

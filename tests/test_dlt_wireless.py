@@ -197,6 +197,11 @@ def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
         d = bytearray(d)
         k = d.find(b"\x06\x01\x0e")
         d[k + 2] = 0x0f
+        # the warning frame's l2len is the Juniper header alone, so an encoder takes the inner
+        # Ethernet header for the L3 bytes; a first byte of 0x45 keeps them an IPv4 header
+        # (version 4 is what --fixcsum demands, edit_packet.c:73-79: else the run stops there)
+        hl = 6 + (d[4] << 8 | d[5])
+        d[hl] = 0x45
         recs[i] = (ts, tu, cl, ln, bytes(d))
     return S.build_pcap(recs, 178), warn
 
