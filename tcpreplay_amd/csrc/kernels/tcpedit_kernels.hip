@@ -1650,6 +1650,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
 #if TE_WK_STAMPS
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
+    unsigned long long fph[5] = {0, 0, 0, 0, 0};  // (window mode: inside the record discovery)
 #endif
 
     // loads of a tile's span (its chunks, record offsets and cache bytes) into R
@@ -1972,8 +1973,15 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
         for (uint32_t k = w0; k < a.nwin; k += W) {
             if (!TE_WIN_PREFETCH) tew::stage_load(ia, k, stg);
             tew::stage_store(ia, k, stg, (uint32_t *)(IMG + LDS_FRONT));
+#if TE_WK_STAMPS
+            WK_STAMP(5)  // (window mode: the staging)
+            const tew::Found fw =
+                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k, fph);
+            last_ = __builtin_amdgcn_s_memtime();
+#else
             const tew::Found fw =
                 tew::find_window<WIN_S, WIN_OL, WIN_PRE, true>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+#endif
             if (TE_WIN_PREFETCH && k + W < a.nwin) tew::stage_load(ia, k + W, stg);
             WK_STAMP(0)  // (window mode: the record discovery)
             const uint32_t wfl = fw.wstop | (fw.anyzero ? (uint32_t)IDX_ZERO : 0u);
@@ -1998,7 +2006,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                     *(uint4 *)(IMG + LDS_FRONT + c) = *(g_cu4 *)(gin + fw.A0 + c);
                 WK_LANES_SYNC();
             }
-            WK_STAMP(5)  // (window mode: the tail load)
+            WK_STAMP(5)  // (window mode: the tail load, with the staging)
             // the tile cut walk_range makes: <= 64 records whose span fits the budget, a
             // record too large for it alone (then left to the exact path by edit())
             for (uint32_t s0 = 0; s0 < fw.nrec;) {
@@ -2048,6 +2056,11 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     if (lane == 0 && wid == 0 && (blockIdx.x % 128) == 0)
         printf("wstamps block %u tiles %llu: top %llu phaseA %llu prefix %llu phaseB %llu store %llu fill %llu\n",
                blockIdx.x, ntl, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+    if constexpr (WIN) {
+        if (lane == 0 && wid == 0 && (blockIdx.x % 128) == 0)
+            printf("fstamps block %u: cand %llu walk %llu confirm %llu jacobi %llu positions %llu\n", blockIdx.x,
+                   fph[0], fph[1], fph[2], fph[3], fph[4]);
+    }
 #endif
     if (lane == 0) {
         red[wid][0] = c_pkts;

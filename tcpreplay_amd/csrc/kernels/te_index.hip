@@ -49,7 +49,7 @@ constexpr u64 REC_MASK = (1ull << REC_BITS) - 1;
 
 // one wave's LDS: the staged window, its record offsets, per-record tile starts, tile starts
 template <int S>
-struct WinLds {
+struct alignas(16) WinLds {
     static constexpr int W = IW * S;
     static constexpr int MAXR = W / 16;      // records starting in a window, at most
     u32 img[(W + 48) / 4];                   // bytes [A0, A0 + W + 48): A0 = window start & ~15

@@ -161,8 +161,18 @@ __device__ __forceinline__ void stage_store(const IdxArgs &a, u32 k, const Stagi
 // staged past the window's end + 16 (the fused edit's last record reaching past the window:
 // in LDS with the window, no second dependent load for it).  STAGED: the caller has stored
 // window k's staging into img already (stage_load / stage_store)
+// ts: (diagnostic builds) s_memtime per phase added to ts[0..4]: candidates, walks,
+// confirmation, Jacobi rounds, positions -- or null
 template <int S, int OL, int PRE = 0, bool STAGED = false>
-__device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *rel, u32 k) {
+__device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *rel, u32 k,
+                                             unsigned long long *ts = nullptr) {
+    unsigned long long tl_ = ts ? __builtin_amdgcn_s_memtime() : 0ull;
+#define TEW_STAMP(i)                                                    \
+    if (ts) {                                                           \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+        ts[i] += now_ - tl_;                                            \
+        tl_ = now_;                                                     \
+    }
     constexpr int W = IW * S;       // staged sub-window bytes
     constexpr int O = OL * S;       // overlap before the window
     constexpr int WN = W - O;       // bytes a window owns
@@ -217,10 +227,17 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
         // zero flags of bytes [lo, lo + S + 16): dword d of the sub-window holds bytes 4d..4d+3
         const u32 q0 = (u32)(lo - A0);  // lane S: a multiple of 16
         u64 z[3] = {0, 0, 0};
+        // (16-byte LDS reads: the sub-window starts 16-aligned)
 #pragma unroll
-        for (int d = 0; d < S / 4 + 4; ++d) {
-            const u64 f = (u64)nib(zero_bytes(img[(q0 >> 2) + d])) << ((4 * d) & 63);
-            z[(4 * d) >> 6] |= f;
+        for (int c = 0; c < S / 16 + 1; ++c) {
+            const uint4 q = *(const uint4 *)&img[(q0 >> 2) + 4 * c];
+            const u32 dw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int d = 4 * c + j;
+                const u64 f = (u64)nib(zero_bytes(dw[j])) << ((4 * d) & 63);
+                z[(4 * d) >> 6] |= f;
+            }
         }
         auto bits_at = [&](int h, int sh) -> unsigned long long {  // bits 64h + j (j < 64) of z >> sh
             return sh == 0 ? z[h] : (z[h] >> sh) | (z[h + 1] << (64 - sh));
@@ -231,12 +248,19 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
         const bool us = !a.nsec;
         const int zc = a.sw ? 8 : 11, zl = a.sw ? 12 : 15, zf = a.sw ? 4 : 7;
         u64 weak = IDX_NONE;
+        unsigned long long mh[(S + 63) / 64];
+#pragma unroll
+        for (int h = 0; h < (S + 63) / 64; ++h) {
+            mh[h] = bits_at(h, zc) & bits_at(h, zl) & (us ? bits_at(h, zf) : ~0ull);
+            const int span = S - 64 * h;
+            if (span < 64) mh[h] &= (1ull << span) - 1ull;
+        }
+        // (one candidate at a time: batching the first four's header reads -- two LDS round
+        // trips instead of two each -- ran slower, the lane is issue-bound here)
 #pragma unroll
         for (int h = 0; h < (S + 63) / 64; ++h) {
             if (e != IDX_NONE) break;
-            unsigned long long m = bits_at(h, zc) & bits_at(h, zl) & (us ? bits_at(h, zf) : ~0ull);
-            const int span = S - 64 * h;
-            if (span < 64) m &= (1ull << span) - 1ull;
+            unsigned long long m = mh[h];
             while (m) {
                 const int j = __builtin_ctzll(m);
                 m &= m - 1;
@@ -252,8 +276,10 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
         }
         if (e == IDX_NONE) e = weak;
     }
+    TEW_STAMP(0)
     LaneWalk w = e != IDX_NONE ? walk_lds(a, img, A0, e, hi) : LaneWalk{0, 0, 0};
     bool has = e != IDX_NONE;
+    TEW_STAMP(1)
 
     // ---- where the chain starts: the first guess the next guess confirms (its walk ends
     // exactly there, or at a strong candidate).  A guess that is not a record start jumps by
@@ -280,6 +306,7 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
             e = IDX_NONE;
         }
     }
+    TEW_STAMP(2)
 
     // ---- the exact chain: the chain's first guess is trusted (the overlap lanes' chain, or window 0's
     // known first record); after it, lane l's first record must be where the nearest earlier
@@ -348,6 +375,7 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
             ended = (u32)__shfl((int)w.stop, (int)l);
         }
     }
+    TEW_STAMP(3)
     // only the window's own lanes' records count (the overlap's are window k - 1's)
     if (lane < OL) has = false;
     // the window's entry, exit and how the chain ends here (wave-uniform lanes: readlane)
@@ -379,6 +407,8 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     }
     const bool anyzero = __ballot(zero) != 0;
     asm volatile("" ::: "memory");
+    TEW_STAMP(4)
+#undef TEW_STAMP
     return Found{ws, we, A0, staged_end, went, wexit, wstop, nrec, anyzero};
 }
 }  // namespace tew
