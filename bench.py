@@ -569,9 +569,10 @@ def main():
                 return {"mpkt_s": round(n / sec / 1e6, 2), "ms": round(sec * 1e3, 3),
                         "gbps_in": round(len(pcap) / sec / 1e9, 2), "path": path}
             result["end_to_end"] = dict(
-                rate(p_s, "page-locked host capture -> chunks of whole records (the default: a tenth of the "
-                          "capture, 8-32 MiB), device record index | edit | D2H on three streams -> page-locked "
-                          "host output (median of 5)"),
+                rate(p_s, "page-locked host capture -> byte-range chunks (the default: a tenth of the capture, "
+                          "8-32 MiB; C/4 and C/2 first, halving last), H2D | window-mode edit (records found "
+                          "on the device, chain verdict gathered on the device) | D2H on three streams -> "
+                          "page-locked host output (median of 5)"),
                 pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 5)"),
                 one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
                                    "pageable copies (median of 3)"))

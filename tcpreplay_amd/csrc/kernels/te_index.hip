@@ -3,34 +3,32 @@
 //
 // libpcap reads a capture as a chain of records, each header saying where the next one
 // starts (tcprewrite.c:289 pcap_next).  The host walks that chain (te_api.c walk_range);
-// here it is found in parallel, speculatively, and checked exactly, in ONE pass over the
-// bytes:
-//   * the capture is cut into windows of W = 64 S bytes, one wave each (windows taken in
-//     order from an atomic ticket), and every window into 64 sub-windows of S bytes, one
-//     lane each.  The wave stages its window (+ 16 bytes) into LDS with coalesced 16-byte
-//     loads; every later read is an LDS read;
-//   * a lane guesses the first record start in its sub-window: a record header has a zero
-//     byte at +11 (caplen <= 262144) and +15 (len <= 262144), and at +7 for a microsecond
-//     capture (fraction < 10^6), so the lane builds the sub-window's zero-byte mask from
-//     its dwords and tests only the offsets the mask allows -- the header's ranges, and
-//     the next header's when it is staged;
-//   * each lane walks the records that start in its sub-window from its guess; the guesses
-//     are then checked exactly: a lane's guess must be where the nearest earlier lane's
-//     walk ended, and no sub-window the chain enters may be without a guess (ballots; a
-//     miss re-walks the window lane by lane from where the chain is);
-//   * the window's records are cut into wave-lane tiles as walk_range cuts them (byte
-//     budget, 64 records, solo and huge records) by a ballot per tile; a tile never spans
-//     two windows;
-//   * a decoupled look-back over windows (records | tiles in one 64-bit granule) gives the
-//     window's first record and tile numbers, and the wave writes its tiles and record
-//     offsets in place;
-//   * once its look-back has seen every earlier window's granule, a window checks its first
-//     record against where the chain left the nearest earlier window with a record (window
-//     kE starts at the known first record) and reports a miss as the first bad window;
-//     te_index_finish (one lane, the next launch) compares the first bad window with the
-//     first stop, finds where the chain ends and writes the totals.  A guess that was wrong
-//     across windows sets IDX_T_BAD: the caller keeps the host walk's index, which is exact.
-//     (A serial finishing loop over every window cost ~50 ns a window: 0.84 ms on C2.)
+// here it is found in parallel, speculatively, and checked exactly, in four launches with
+// no window ever waiting on another:
+//   * te_index_count, a wave per window: the capture is cut into windows of W = 64 S bytes
+//     (each owning W - OL S bytes, the first OL sub-windows being the previous window's),
+//     every window into 64 sub-windows of S bytes, one lane each.  The record discovery is
+//     te_window.hpp find_window (shared with the edit's window mode): the wave stages its
+//     window into LDS with coalesced 16-byte loads; a lane guesses the first record start
+//     in its sub-window from the zero-byte mask of its dwords (a header has zero bytes at
+//     +11 and +15 -- caplen, len <= 262144 -- and at +7 for a microsecond capture) and the
+//     header behind the guess, walks its records, and the guesses are reconciled exactly (a
+//     lane's guess must be where the nearest earlier guessing lane's walk ended: ballots and
+//     bit searches, Jacobi rounds, a serial lane loop as the last resort).  The wave cuts
+//     its records into wave-lane tiles as walk_range cuts them (byte budget, 64 records,
+//     solo and huge records; a tile never spans two windows) and writes its facts (entry,
+//     exit, chain flags, records | tiles, huge-record scratch bytes) and its cut to a
+//     per-window scratch area;
+//   * te_index_part (a block of 1,024 windows) and te_index_scan (one block): exclusive
+//     scans of (records | tiles), scratch bytes and the last window with a record, libpcap's
+//     first stop, the totals;
+//   * te_index_write, a wave per window: the window's tiles and record offsets at its global
+//     bases, and the chain check -- a window's first record must be where the chain left the
+//     nearest earlier window a record starts in (window kE starts at the known first record),
+//     and a window without one must be passed over whole.  A miss sets IDX_T_BAD and the
+//     caller keeps the host walk's index, which is exact.
+//   (A single-pass version with a decoupled look-back over windows and a serial finishing
+//   check cost ~50 ns a window: 0.84 ms on C2.)
 // libpcap's ends are kept: an oversize record (caplen > 262144) or a truncated one ends
 // the chain; a len > 262144 record ends it with the reference's error (tcprewrite.c:296).
 #include <hip/hip_runtime.h>
