@@ -1303,12 +1303,18 @@ constexpr int wk_nch(int tb) { return tb / 16 + 2; }
 // window mode: sub-window bytes per lane and lookback lanes of the discovery (te_window.hpp),
 // the bytes a window's last record may reach past the staged window (a longer one is left to
 // the exact path), and the window image: front pad, the staged window, that tail, slack
-constexpr int WIN_S = 64, WIN_OL = 7;
+#ifndef TE_WIN_S
+#define TE_WIN_S 64  // bytes a lane scans: a window is 64 of them
+#endif
+#ifndef TE_WIN_OL
+#define TE_WIN_OL 7  // of which the first TE_WIN_OL lanes' are the previous window's
+#endif
+constexpr int WIN_S = TE_WIN_S, WIN_OL = TE_WIN_OL;
 constexpr int WIN_W = 64 * WIN_S, WIN_WN = WIN_W - WIN_OL * WIN_S;
 constexpr int WIN_TAIL = 2048;
 // staged with the window past its end + 16 (five 1 KiB wave loads in all): the last
 // record reaching past the window is in LDS without a second, dependent load unless longer
-constexpr int WIN_PRE = 5 * 1024 - WIN_W - 48;
+constexpr int WIN_PRE = 1024 * ((WIN_W + 48 + 900 + 1023) / 1024) - WIN_W - 48;
 static_assert(WIN_PRE >= 0 && WIN_PRE <= WIN_TAIL, "window pre-staging within the tail room");
 constexpr int WIN_IMG = LDS_FRONT + WIN_W + 48 + WIN_TAIL + 128;
 constexpr int WIN_REL = 4 * WIN_S + 1;

@@ -388,12 +388,14 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     // ---- the window's records: positions, offsets into LDS.  A lane takes at most S / 16
     // records (< 8): its count's three bits are three ballots, its position their popcounts
     // below it ----
-    static_assert(S / 16 < 8, "a lane's record count fits three bits");
+    static_assert(S / 16 < 16, "a lane's record count fits four bits");
     const u32 n = has ? w.n : 0;
-    const unsigned long long n0 = __ballot(n & 1u), n1 = __ballot(n & 2u), n2 = __ballot(n & 4u);
+    const unsigned long long n0 = __ballot(n & 1u), n1 = __ballot(n & 2u), n2 = __ballot(n & 4u),
+                             n3 = S / 16 >= 8 ? __ballot(n & 8u) : 0ull;
     const u32 pos = (u32)(__builtin_popcountll(n0 & below) + 2 * __builtin_popcountll(n1 & below) +
-                          4 * __builtin_popcountll(n2 & below));
-    const u32 nrec = (u32)(__builtin_popcountll(n0) + 2 * __builtin_popcountll(n1) + 4 * __builtin_popcountll(n2));
+                          4 * __builtin_popcountll(n2 & below) + 8 * __builtin_popcountll(n3 & below));
+    const u32 nrec = (u32)(__builtin_popcountll(n0) + 2 * __builtin_popcountll(n1) + 4 * __builtin_popcountll(n2) +
+                           8 * __builtin_popcountll(n3));
     bool zero = false;
     if (has) {
         u64 off = e;
