@@ -1180,6 +1180,7 @@ typedef struct te_win_req_s {
     const uint8_t *prev_out;
     uint64_t head_max;
     uint8_t *out;
+    uint64_t org;
 } te_win_req_t;
 /* the window workspace layout of d_win for `cap` windows: entries | exits | flags | bad | tot */
 #define WIN_WS_BYTES(cap) (16ull * (cap) + 4ull * (cap) + 64)
@@ -1401,6 +1402,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.win_acc = q->acc;
         L.win_prev_out = q->prev_out;
         L.win_head_max = q->head_max;
+        L.win_org = q->org;
         if (q->out)
             L.out = q->out;
         L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
@@ -3169,9 +3171,9 @@ static int win_pipe_off(void)
 /* the window-mode pipeline's chunk starts: C/4 and C/2 (at least 1 MiB) to fill the
    pipeline, C-sized chunks, then halving pieces to drain it -- every chunk but the last a
    multiple of 16 bytes (the head copy moves 16-byte pieces) */
-static uint64_t *win_plan(size_t in_len, uint64_t C, int *n_out)
+static uint64_t *win_plan(size_t in_len, uint64_t C, uintptr_t addr, int *n_out)
 {
-    const uint64_t MIN = (uint64_t)1 << 20;
+    const uint64_t MIN = (uint64_t)1 << 20, A = 256;
     const int cap = (int)((in_len / MIN) + 16);
     uint64_t *st = malloc(sizeof(uint64_t) * (size_t)cap);
     if (!st)
@@ -3192,7 +3194,9 @@ static uint64_t *win_plan(size_t in_len, uint64_t C, int *n_out)
             sz = MIN;
         if (sz > C)
             sz = C;
-        sz &= ~15ull;
+        /* chunk starts 256-byte aligned in the caller's buffer after the first (the copies
+           run slower from and to misaligned addresses) */
+        sz = n == 1 ? ((addr + at + sz) & ~(uintptr_t)(A - 1)) - (addr + at) : sz & ~(A - 1);
         if (sz >= rem)
             sz = rem;
         st[n++] = (at += sz);
@@ -3224,7 +3228,11 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     if (in_len > out_cap || in_len < 24 + 16)
         return 1; /* (the copies move whole file ranges) */
     int nch = 0;
-    uint64_t *cst = win_plan(in_len, C, &nch);
+    /* a chunk's bytes sit at image offset ORG (the file header is not in the image: the
+       window mode starts from the chunk's first record), 256-byte aligned on the device as
+       the chunk starts are in the caller's buffers (win_plan) */
+    const uint64_t ORG = 256;
+    uint64_t *cst = win_plan(in_len, C, (uintptr_t)img, &nch);
     if (!cst) {
         te_seterr(t, "out of memory");
         return -1;
@@ -3235,11 +3243,11 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipHostMalloc((void **)&P->h_wacc, 64, 0));
     }
     {
-        const uint64_t limit_max = 24 + C;
-        const uint32_t nwin_max = (uint32_t)((limit_max - 16 + te_win_bytes() - 1) / te_win_bytes());
+        const uint64_t limit_max = ORG + C + 256;
+        const uint32_t nwin_max = (uint32_t)((limit_max - ORG + te_win_bytes() - 1) / te_win_bytes());
         for (int s = 0; s < TE_PIPE_SLOTS; s++) {
             tcpedit_batch_t *b = P->slot[s];
-            b->out_cap = C + TE_PIPE_WIN_MARGIN + 24;
+            b->out_cap = C + 256 + TE_PIPE_WIN_MARGIN + ORG;
             if (win_ready(t, b, nwin_max) < 0 || pipe_grow(t, P, s) < 0)
                 goto fail;
         }
@@ -3278,27 +3286,27 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         /* upload (the slot's last window kernel has read its input) */
         if (k >= TE_PIPE_SLOTS)
             HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s], 0));
-        HIPCHK(t, hipMemcpyAsync(b->d_in, P->hdr, 24, hipMemcpyHostToDevice, P->s_h2d));
-        HIPCHK(t, hipMemcpyAsync(b->d_in + 24, img + f0, fe - f0, hipMemcpyHostToDevice, P->s_h2d));
+        HIPCHK(t, hipMemcpyAsync(b->d_in + ORG, img + f0, fe - f0, hipMemcpyHostToDevice, P->s_h2d));
         HIPCHK(t, hipEventRecord(P->h2d_done[s], P->s_h2d));
-        b->in_len = 24 + (fe - f0);
+        b->in_len = ORG + (fe - f0);
         b->n_tiles = 0;
-        b->rec0 = b->out_base = 24; /* records keep their image offsets */
+        b->rec0 = b->out_base = ORG; /* records keep their image offsets */
         b->launches = 0;
         b->gen_hint_ok = 0;
         te_win_req_t q;
         memset(&q, 0, sizeof q);
         q.len = b->in_len;
-        q.entry = 24;
-        q.base = 16;
-        q.limit = f1 >= in_len ? b->in_len : 24 + (f1 - f0);
+        q.entry = ORG;
+        q.base = ORG;
+        q.limit = f1 >= in_len ? b->in_len : ORG + (f1 - f0);
         q.nwin = (uint32_t)((q.limit - q.base + te_win_bytes() - 1) / te_win_bytes());
         q.entry_ptr = k ? (const uint64_t *)(pb->d_win + ((20ull * pb->win_cap + 8 + 7) & ~7ull)) : NULL;
         q.entry_sub = k ? f0 - cst[k - 1] : 0; /* the previous chunk's image is that much earlier */
         q.acc = P->d_wacc;
         q.prev_out = k && !zc ? pb->d_out : NULL;
-        q.head_max = 24 + TE_PIPE_WIN_MARGIN;
-        q.out = zc ? zc + (f0 - 24) : NULL; /* (image offset x is file offset f0 + x - 24) */
+        q.head_max = ORG + TE_PIPE_WIN_MARGIN;
+        q.org = ORG;
+        q.out = zc ? zc + f0 - ORG : NULL; /* (image offset x is file offset f0 + x - ORG) */
         /* the window kernel: after the upload, and after the slot's last output copy */
         HIPCHK(t, hipStreamWaitEvent(t->stream, P->h2d_done[s], 0));
         if (!zc)
@@ -3313,7 +3321,7 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
         if (!zc) { /* the chunk's file range down, behind its edit */
             HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
-            HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + 24, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
+            HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + ORG, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
             HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
         }
         last = s;
@@ -3332,7 +3340,7 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     {
         const uint64_t *acc = P->h_wacc;
         const uint64_t f0 = cst[nch - 1];
-        const uint64_t end = f0 + acc[4] - 24; /* the last chunk's chain end, as a file offset */
+        const uint64_t end = f0 + acc[4] - ORG; /* the last chunk's chain end, as a file offset */
         free(cst);
         if (acc[3] || acc[1] != end - 24 || end > in_len)
             return 1; /* (the records and the chain must agree) */

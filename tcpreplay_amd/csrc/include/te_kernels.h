@@ -217,6 +217,7 @@ typedef struct {
     uint64_t *win_acc;
     const uint8_t *win_prev_out;
     uint64_t win_head_max;
+    uint64_t win_org;            /* image offset of the chunk's first file byte (0: 24) */
 } te_launch_t;
 /* bytes a window of the window mode owns */
 uint32_t te_win_bytes(void);

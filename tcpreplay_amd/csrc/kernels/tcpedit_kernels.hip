@@ -2102,28 +2102,27 @@ struct WinTail {
     const uint8_t *prev_out;   // null: no head copy (the first chunk, a batch)
     uint8_t *out;
     uint64_t head_max;         // a first record further in is no chain's: nothing copied
+    uint64_t org;              // the image offset of the chunk's first file byte
 };
 constexpr uint32_t WIN_HEAD_BLOCKS = 64;
 
 __device__ void win_head_copy(const FastArgs &a, const WinTail &w, uint32_t blk) {
-    const uint64_t sub = a.win_entry_sub;
+    const uint64_t sub = a.win_entry_sub, org = w.org;
     // this chunk's first record (image offset): where the previous chunk's chain ended (a
     // chunk whose chain broke leaves no such position: the call's verdict sends the capture
     // to the exact path, and nothing is copied here)
     const uint64_t e = *(const volatile uint64_t *)a.win_entry_ptr - sub;
-    if (e < 24 || e > w.head_max) return;
+    if (e < org || e > w.head_max) return;
     const uint64_t t = blk * 256ull + threadIdx.x, nt = WIN_HEAD_BLOCKS * 256ull;
-    if (sub & 15) {  // (a chunk size that is not a multiple of 16: byte by byte)
-        for (uint64_t x = 24 + t; x < e; x += nt) w.out[x] = w.prev_out[x + sub];
+    if ((sub | org) & 15) {  // (not 16-byte pieces on both sides: byte by byte)
+        for (uint64_t x = org + t; x < e; x += nt) w.out[x] = w.prev_out[x + sub];
         return;
     }
-    // bytes [24, e) of this image are the previous image's [24 + sub, e + sub); both sides
-    // share their 16-byte phase
-    if (t < 8 && 24 + t < e) w.out[24 + t] = w.prev_out[24 + sub + t];
+    // bytes [org, e) of this image are the previous image's [org + sub, e + sub)
     const uint64_t c1 = e & ~15ull;
-    for (uint64_t c = 32 + 16 * t; c < c1; c += 16 * nt)
+    for (uint64_t c = org + 16 * t; c < c1; c += 16 * nt)
         *(uint4 *)(w.out + c) = *(const uint4 *)(w.prev_out + c + sub);
-    if (t < 16 && c1 >= 32 && c1 + t < e) w.out[c1 + t] = w.prev_out[c1 + sub + t];
+    if (t < 16 && c1 >= org && c1 + t < e) w.out[c1 + t] = w.prev_out[c1 + sub + t];
 }
 
 __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long long *tot, WinTail w) {
@@ -3008,6 +3007,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         wt.prev_out = L->win_prev_out && L->win_entry_ptr ? L->win_prev_out : nullptr;
         wt.out = L->out;
         wt.head_max = L->win_head_max;
+        wt.org = L->win_org ? L->win_org : 24;
         const uint32_t nx = (wt.acc ? 1u : 0u) + (wt.prev_out ? WIN_HEAD_BLOCKS : 0u);
         hipLaunchKernelGGL(te_win_check, dim3(wt.ncheck + nx), dim3(256), 0, stream, f,
                            (unsigned long long *)L->win_tot, wt);
