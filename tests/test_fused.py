@@ -49,6 +49,13 @@ def _run(pcap, args, cache=None, fused=True):
     ("macs", lambda: S.pcap_imix(30_000, seed=6), ["--enet-smac=00:11:22:33:44:55,00:aa:bb:cc:dd:ee",
                                                    "--enet-dmac=00:66:77:88:99:aa,00:12:34:56:78:9a",
                                                    "--ttl=+3", "--tos=7", "--fixcsum"]),
+    # the incremental-checksum instances (no --fixcsum)
+    ("seed-incr", lambda: S.pcap_fixed(40_000, 64, seed=7), ["--seed=42"]),
+    ("hdr-incr", lambda: S.pcap_imix(30_000, seed=8), ["--ttl=+1", "--tos=7"]),
+    ("all-incr", lambda: S.pcap_imix(30_000, seed=9), ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353",
+                                                       "--enet-dmac=00:66:77:88:99:aa,00:12:34:56:78:9a",
+                                                       "--ttl=9"]),
+    ("v6", lambda: S.pcap_fixed(20_000, 200, ipv6=True, proto=6, seed=10), ["--seed=5", "--fixcsum"]),
 ], ids=lambda x: x if isinstance(x, str) else "")
 def test_fused_matches_the_oracle(built, name, gen, args):
     _run(gen(), args)
@@ -116,6 +123,19 @@ def test_fused_not_carried(built, args, cache):
     pcap = S.pcap_imix(10_000, seed=14)
     c = S.tcpprep_cache(10_000, seed=14, nosend_every=7) if cache else None
     _run(pcap, args, c, fused=False)
+
+
+def test_fused_not_carried_inputs(built):
+    """big-endian and nanosecond captures run the exact path (the window mode reads native
+    microsecond headers only)"""
+    recs = S.records(S.pcap_imix(8_000, seed=17))
+    for magic in (0xA1B23C4D, 0xD4C3B2A1):
+        sw = magic == 0xD4C3B2A1
+        e = ">" if sw else "<"
+        hdr = struct.pack(e + "IHHiIII", 0xA1B2C3D4 if sw else magic, 2, 4, 0, 0, 65535, 1)
+        body = b"".join(struct.pack(e + "IIII", ts, tu * (1000 if magic == 0xA1B23C4D else 1), cl, ln) + d
+                        for ts, tu, cl, ln, d in recs)
+        _run(hdr + body, ["--seed=5", "--fixcsum"], fused=False)
 
 
 def test_fused_small_and_empty(built):
