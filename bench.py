@@ -62,10 +62,11 @@ WORKLOADS = {
              "--efcs --fixcsum on IMIX 68/574/1518 7:4:1 frames captured with their FCS (every record -4 bytes)"),
     "macseed": ("pcap_imix", dict(), ["--enet-mac-seed=42", "--fixcsum"],
                 "--enet-mac-seed=42 --fixcsum on IMIX 64/570/1514 7:4:1 (MAC seed masks, en10mb.c:674-689)"),
-    # the generic lane (te_edit_tiles): a size change that differs by record
+    # a size change that differs by record: the wave lane's SZ_MTU instances, tiles placed by the
+    # device-predicted cuts (te_mtu_cuts; TCPEDIT_HIP_NO_MTU_FAST=1: the generic lane's scan + look-back)
     "mtu": ("pcap_imix", dict(), ["--mtu=1000", "--mtu-trunc", "--fixcsum"],
             "--mtu=1000 --mtu-trunc --fixcsum on IMIX 64/570/1514 7:4:1 (1514 B records cut to 1014 B: "
-            "per-record sizes, block scan + look-back placement on the generic lane)"),
+            "per-record sizes; wave lane, tiles at the predicted cuts' prefix)"),
 }
 PER_RANK_PACKETS = {"c2": 10_000_000}  # N > 1 per-rank shard (HBM-resident)
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,

@@ -53,6 +53,13 @@ struct tcpedit_batch_s {
     int last_grow;           /* the last launch placed records by static_grow (+4) or static_shrink (-4) */
     int grow_never;          /* pipelined chunk slots: no rerun on a violation, so always scan */
     uint32_t grow_bad;       /* its violation word, read back */
+    int mtu_fast;            /* tiles were cut for the wave lane's --mtu-trunc instances */
+    int last_mtu;            /* the last launch placed tiles by the --mtu-trunc prediction */
+    long long *d_tcut;       /* the prediction: n_tiles + 1 prefix (te_mtu_cuts), ... */
+    int32_t *d_tcut_raw;     /* ... from per-tile cuts */
+    uint64_t tcut_cap;       /* tiles d_tcut holds */
+    int tcut_ok;             /* d_tcut is this tile cut's, for tcut_mtu (0 after any re-cut) */
+    int32_t tcut_mtu;
     int fast_tiles;          /* tiles were cut for the fast lane ... */
     int fast_kind;           /* ... of this kind (TE_FAST_BLOCK / TE_FAST_WAVE budgets) */
     uint64_t launches;       /* parity selects the fast lane's tile-list count */
@@ -239,6 +246,25 @@ static int static_shrink_kind(const te_dev_cfg_t *c)
 static int fast_capable_shrink(const te_dev_cfg_t *c)
 {
     return static_shrink_kind(c) != TE_SZ_NONE && !c->fixhdrlen && cidr_inline(c);
+}
+
+/* --mtu-trunc as the only size change, on the wave lane: records keep their order and
+ * lose only their tails, so tile t's output sits at its input offset less the bytes the
+ * records before it lose -- a prefix the device predicts from the record headers
+ * (te_mtu_cuts) and every tile checks.  (mtu >= 128: a cut packet keeps its whole
+ * header window, fast_lane.hpp.) */
+static int fast_capable_mtu(const te_dev_cfg_t *c)
+{
+    return c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && c->mtu_truncate &&
+           c->mtu >= 128 && c->mtu <= 65535 && c->vlan == TE_VLAN_OFF && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
+           !c->skip_soft_errors && !c->fuzz_seed && !c->fixhdrlen && cidr_inline(c);
+}
+
+/* TCPEDIT_HIP_NO_MTU_FAST=1 keeps --mtu-trunc on the generic lane (A/B checks) */
+static int mtu_fast_off(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_NO_MTU_FAST");
+    return e && *e == '1';
 }
 
 /* IPv6 rewrites with a non-octet target mask keep the reference's stray write
@@ -604,13 +630,17 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
                        fast_kind_pref() == TE_FAST_WAVE;
     /* ... and a VLAN pop or --efcs (native-order microsecond input only) */
     const int shrink_fast = !proto->slot_mode && fast_capable_shrink(&t->cfg) && !b->swapped && !b->nsec;
-    b->fast_tiles = (!proto->slot_mode && fast_capable(&t->cfg)) || proto->grow_fast || shrink_fast;
+    /* ... and --mtu-trunc (native-order microsecond input, the wave lane only) */
+    b->mtu_fast = !proto->slot_mode && fast_capable_mtu(&t->cfg) && !b->swapped && !b->nsec &&
+                  fast_kind_pref() == TE_FAST_WAVE && !mtu_fast_off();
+    b->fast_tiles = (!proto->slot_mode && fast_capable(&t->cfg)) || proto->grow_fast || shrink_fast || b->mtu_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
     if (shrink_fast && !proto->grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
         b->fast_tiles = 0, b->fast_kind = 0;
     proto->wave = b->fast_kind == TE_FAST_WAVE;
     proto->budget = proto->wave      ? te_wave_tile_bytes(&t->cfg, proto->grow_fast ? TE_SZ_GROW
                                                                    : shrink_fast     ? static_shrink_kind(&t->cfg)
+                                                                   : b->mtu_fast     ? TE_SZ_MTU
                                                                                      : TE_SZ_NONE)
                     : b->fast_tiles ? TE_FK_TILE_BYTES
                                     : TE_SLOT_BYTES;
@@ -837,7 +867,9 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     b->cut_tiles = m->n_tiles;
     b->n_pkts = m->n_pkts;
     if (!rc && proto.wave && !proto.slot_mode && !b->idx_pinned)
-        balance_tiles(b, te_wave_waves(&t->cfg, proto.shrink_fast ? static_shrink_kind(&t->cfg) : TE_SZ_NONE),
+        balance_tiles(b, te_wave_waves(&t->cfg, proto.shrink_fast ? static_shrink_kind(&t->cfg)
+                                                : b->mtu_fast      ? TE_SZ_MTU
+                                                                   : TE_SZ_NONE),
                       proto.budget, proto.max_pkts);
     b->out_cap = 24 + 64 + m->rec_bytes;
     b->scratch_bytes = m->scratch_bytes;
@@ -860,6 +892,12 @@ static void batch_free_dev(tcpedit_batch_t *b)
     hipFree(b->d_tiles);
     hipFree(b->d_pkt_rel);
     hipFree(b->d_ws);
+    hipFree(b->d_tcut);
+    hipFree(b->d_tcut_raw);
+    b->d_tcut = NULL;
+    b->d_tcut_raw = NULL;
+    b->tcut_cap = 0;
+    b->tcut_ok = 0;
     hipFree(b->d_tile_list);
     hipFree(b->d_fuzz);
     hipFree(b->d_l2carry);
@@ -1087,6 +1125,7 @@ static tcpedit_batch_t *batch_open(tcpedit_t *t, const uint8_t *hdr, const uint8
         HIPCHK(t, hipMalloc((void **)&b->d_scratch, b->scratch_bytes));
     HIPCHK(t, hipMalloc((void **)&b->d_tiles, sizeof(te_tile_t) * (b->n_tiles + 1)));
     HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice, t->stream));
+    b->tcut_ok = 0;
     HIPCHK(t, hipMalloc((void **)&b->d_pkt_rel, sizeof(uint16_t) * (b->n_pkts + 1)));
     HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
                              t->stream));
@@ -1278,6 +1317,32 @@ static int l2carry_bufs(tcpedit_t *t, tcpedit_batch_t *b, te_launch_t *L)
 
 /* generic_only: the generic pass over what the last (wave-lane) launch listed, under
  * that launch's parity -- for a run whose generic pass was left out by the hint */
+/* the --mtu-trunc placement prediction for this tile cut (te_mtu_cuts), computed on the
+   batch's stream the first time a cut is launched with this MTU; 0 when ready */
+static int mtu_cuts_ready(tcpedit_batch_t *b, int32_t mtu)
+{
+    tcpedit_t *t = b->ctx;
+    if (b->tcut_ok && b->tcut_mtu == mtu)
+        return 0;
+    if (b->tcut_cap < b->n_tiles + 1) {
+        hipFree(b->d_tcut);
+        hipFree(b->d_tcut_raw);
+        b->d_tcut = NULL;
+        b->d_tcut_raw = NULL;
+        b->tcut_cap = 0;
+        if (hipMalloc((void **)&b->d_tcut, sizeof(long long) * (b->n_tiles + 1)) != hipSuccess ||
+            hipMalloc((void **)&b->d_tcut_raw, sizeof(int32_t) * (b->n_tiles + 1)) != hipSuccess)
+            return -1;
+        b->tcut_cap = b->n_tiles + 1;
+    }
+    if (te_mtu_cuts(b->d_in, b->d_tiles, b->d_pkt_rel, (uint32_t)b->n_tiles, (uint32_t)mtu, b->d_tcut_raw, b->d_tcut,
+                    t->stream) != 0)
+        return -1;
+    b->tcut_ok = 1;
+    b->tcut_mtu = mtu;
+    return 0;
+}
+
 static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_t k1, int generic_only)
 {
     tcpedit_t *t = b->ctx;
@@ -1327,9 +1392,17 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
                           : TE_SZ_NONE;
     L.grow_bad = (uint32_t *)(b->d_ws + WS_GROW_BAD);
     b->last_grow = L.static_grow ? 4 : L.static_shrink ? -4 : 0;
+    /* --mtu-trunc on the wave lane: tiles placed by the predicted cuts (fast_capable_mtu) */
+    L.static_mtu = b->mtu_fast && b->fast_kind == TE_FAST_WAVE && fast_capable_mtu(c) && !b->slot_layout &&
+                   !b->has_zero_cap && !b->swapped && !b->nsec && !b->dirbits_len && b->n_tiles > 0 &&
+                   !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env() &&
+                   !fast_lane_off() && mtu_cuts_ready(b, c->mtu) == 0;
+    L.tcut = L.static_mtu ? b->d_tcut : NULL;
+    L.mtu = (uint32_t)c->mtu;
+    b->last_mtu = L.static_mtu;
     L.fast = b->fast_tiles && !fast_lane_off() &&
              ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)) ||
-              (L.static_shrink && fast_capable_shrink(c)));
+              (L.static_shrink && fast_capable_shrink(c)) || L.static_mtu);
     L.fast_v6 = fast_v6_ok(c);
     /* a batch whose input + output outgrow the 256 MiB Infinity Cache streams through it:
        nontemporal loads and stores (TCPEDIT_HIP_STREAM=0/1 overrides, for A/B runs) */
@@ -1610,7 +1683,7 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
                                  hipMemcpyDeviceToHost, t->stream));
     }
-    if (b->last_grow)
+    if (b->last_grow || b->last_mtu)
         HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
@@ -1625,15 +1698,16 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
-        if (b->last_grow) /* the listed tiles can break static placement too */
+        if (b->last_grow || b->last_mtu) /* the listed tiles can break static placement too */
             HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                      t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
         b->last_skipped = 0;
     }
-    if (b->last_grow && b->grow_bad) {
-        /* a record did not grow by exactly 4 bytes: place this batch by scan + look-back
-           from now on, and run it again that way */
+    if ((b->last_grow || b->last_mtu) && b->grow_bad) {
+        /* a record did not grow by exactly 4 bytes (a tile's --mtu-trunc cut was not the
+           predicted one): place this batch by scan + look-back from now on, and run it again
+           that way */
         b->grow_off = 1;
         b->grow_off_gen = t->cfg_gen;
         b->grow_bad = 0;
@@ -1663,7 +1737,8 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
-        b->counters[TE_CNT_BYTES_OUT] += v[1] + (uint64_t)((int64_t)b->last_grow * (int64_t)v[0]); /* +- 4 a record */
+        b->counters[TE_CNT_BYTES_OUT] += v[1] + (uint64_t)((int64_t)b->last_grow * (int64_t)v[0]) /* +- 4 a record */
+                                         - v[3];                                                /* the MTU cuts */
         b->counters[TE_CNT_EDITED] += v[2];
     }
     if (b->last_fast) { /* same batch + same config lists the same tiles next time */
@@ -2377,6 +2452,7 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
         }
         hipFree(b->d_tiles);
         b->d_tiles = d_tiles;
+        b->tcut_ok = 0;
         d_tiles = NULL;
         hipFree(b->d_pkt_rel);
         b->d_pkt_rel = d_rel;
@@ -3047,6 +3123,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             b->out_cap += 16; /* (out_base) */
             HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice,
                                      t->stream));
+            b->tcut_ok = 0;
             HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
                                      t->stream));
             P->h_tot[s][IDX_T_END] = b->walk_end;
@@ -3547,6 +3624,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
                D2H of the chunk this slot held before ---- */
         HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice,
                                  P->s_h2d));
+        b->tcut_ok = 0;
         HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t) * b->n_pkts, hipMemcpyHostToDevice,
                                  P->s_h2d));
         HIPCHK(t, hipMemsetAsync(b->d_ws, 0, WS_STATE, P->s_h2d)); /* err, ticket, both counter sets */
@@ -4290,6 +4368,7 @@ int tcpedit_packet(tcpedit_t *t, struct pcap_pkthdr **pkthdr, unsigned char **pk
     HIPCHK(t, hipMemcpyAsync(b->d_in, img, img_len, hipMemcpyHostToDevice, t->stream));
     HIPCHK(t, hipMemcpyAsync(b->d_tiles, b->tiles, sizeof(te_tile_t) * b->n_tiles, hipMemcpyHostToDevice, t->stream));
     HIPCHK(t, hipMemcpyAsync(b->d_pkt_rel, b->pkt_rel, sizeof(uint16_t), hipMemcpyHostToDevice, t->stream));
+    b->tcut_ok = 0;
     HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream));
     if (batch_run_dir(t, b, (int)direction) != TCPEDIT_OK)
         goto out;

@@ -42,6 +42,7 @@ extern "C" {
 #define TE_SZ_GROW 1           /* --enet-vlan=add: +4 per record */
 #define TE_SZ_VDEL 2           /* --enet-vlan=del over tagged records: -4 */
 #define TE_SZ_EFCS 3           /* --efcs: -4 */
+#define TE_SZ_MTU 4            /* --mtu-trunc: a record longer than the MTU loses its tail */
 /* option groups of the fast lane: a te_wave_tiles instance compiles in the groups of
    its mask, and te_launch_edit launches the smallest instance covering the config */
 #define TE_FF_MAC 1u     /* --enet-dmac / --enet-smac */
@@ -139,6 +140,12 @@ typedef struct {
                                  bytes (a VLAN pop, or --efcs, as the only size change): record i sits
                                  at its input offset - 4 i; a record that breaks it sets *grow_bad */
     uint32_t *grow_bad;       /* device word, zeroed with the error words */
+    int static_mtu;           /* --mtu-trunc as the only size change: tile t's output starts at its
+                                 input offset - tcut[t], the predicted bytes --mtu-trunc removes from
+                                 the records before it (te_mtu_cuts); a tile whose output differs
+                                 from the prediction sets *grow_bad */
+    const long long *tcut;    /* device: n_tiles + 1 exclusive prefix of the predicted cuts */
+    uint32_t mtu;             /* static_mtu: the MTU (cfg.mtu) */
     /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
        only the listed tiles */
@@ -273,6 +280,11 @@ int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
 int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream);
 
 int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
+/* --mtu-trunc placement: cut[t] = bytes tile t's records lose to the truncation, predicted
+   from each record's header and type field (len > mtu + l2len: caplen becomes l2len + mtu),
+   and pre = their exclusive prefix (n_tiles + 1 entries) */
+int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n_tiles, uint32_t mtu,
+                int32_t *cut, long long *pre, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
 /* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */

@@ -171,10 +171,16 @@ struct State {
 // k = (caplen + 2) / 4 < NW, the rest zeroed; 0 when there is none), which the
 // caller reads from the unedited image.  It is always L4 payload: a packet on
 // this lane has its whole L4 header inside caplen, and the header dwords are whole.
+//
+// `tcap` (--mtu-trunc, SZ_MTU instances; 0 otherwise): the packet is classified with its
+// captured caplen/len, then cut to tcap = 14 + mtu bytes as untrunc_packet does
+// (edit_packet.c:596-611, after the header edits and before the address edits, tcpedit.c:
+// 261-265): caplen = len = tcap, IPv4 total length = mtu, IPv6 payload length = mtu - 40,
+// and the checksums cover the cut packet.  `part` is then the cut packet's.
 // ---------------------------------------------------------------------------
 template <u32 F>
 DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_dev_cfg_t &cfg, const Knobs &kn,
-                bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st) {
+                bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st, u32 tcap = 0) {
     // ---- classify: Ethernet II + IPv4 (IHL 5, no fragment, ip_len == caplen - 14) or
     // IPv6 (payload length == caplen - 54), then TCP or UDP with a whole header ----
     const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
@@ -183,10 +189,13 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
                      (ip_len >= 20) & ((bs16(hi16(H[5])) & 0x3fffu) == 0);                    // and fragments: generic
     const u32 plen_raw = lo16(H[5]), l4len6 = bs16(plen_raw);
     const bool v6 = et == 0xDD86u;  // ETHERTYPE_IP6
+    // (--mtu-trunc: edit_packet.c:167 sees the cut packet's payload length)
+    const u32 plen_chk = tcap != 0 ? bs16(tcap - 54u) : plen_raw;
     const bool ok6 = v6 & v6_ok & (((H[4] >> 4) & 0xfu) == 6u) & (caplen >= 54) & (l4len6 == caplen - 54) &
-                     !((caplen > 56) & (plen_raw < 40));  // raw network-order compare (edit_packet.c:167)
+                     !((caplen > 56) & (plen_chk < 40));  // raw network-order compare (edit_packet.c:167)
     const u32 proto = v6 ? (H[5] >> 16) & 0xffu : (H[6] >> 8) & 0xffu;
-    const u32 l4len = v6 ? l4len6 : ip_len - 20;
+    const bool cut = tcap != 0;
+    const u32 l4len = cut ? tcap - (v6 ? 54u : 34u) : (v6 ? l4len6 : ip_len - 20);
     const bool tcp = proto == 6;
     const bool ok = (caplen == len) & ((dir == TE_DIR_C2S) | (dir == TE_DIR_S2C)) & (ok4 | ok6) &
                     (tcp ? l4len >= 20 : ((proto == 17) & (l4len >= 8)));
@@ -276,6 +285,12 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
         dirty |= v6 ? 1u << 4 : 0u;
     }
 
+    // ---- --mtu-trunc: the IP length fields of the cut packet (a full recompute follows:
+    // untrunc_packet's 1 is a needtorecalc) ----
+    // (selects, not a branch on the lane's cut: see the note above phase_a)
+    H[4] = (cut & !v6) ? with_hi16(H[4], bs16(tcap - 14u)) : H[4];
+    H[5] = (cut & v6) ? with_lo16(H[5], bs16(tcap - 54u)) : H[5];
+    dirty |= cut ? (v6 ? 1u << 5 : 1u << 4) : 0u;
     // L4 header (20 bytes) at packet offset 34 (v4) or 54 (v6)
     // bitwise selects, not `v6 ? H[14+i] : H[9+i]`: the compiler folds the
     // latter into one dynamically indexed access, which moves H to scratch
@@ -510,9 +525,10 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     // L4 bytes [L4S, min(caplen, WEND)) inside the window: the whole dwords
     // (4i + 2 <= caplen) and the partly valid one.  Relative offsets 4i - 2 are
     // even, so each dword's halves are packet-pairing 16-bit words.
+    const u32 ecap = cut ? tcap : caplen;  // the bytes the checksums cover
 #pragma unroll
     for (int i = 9; i < NW; ++i) {
-        const bool whole = caplen >= (u32)(4 * i + 2) && (i >= 14 || !v6);
+        const bool whole = ecap >= (u32)(4 * i + 2) && (i >= 14 || !v6);
         sum = wsum_acc(whole ? H[i] : 0u, sum);
     }
     sum = wsum_acc(part, sum);  // < 2^16 * 32 overall
@@ -534,12 +550,12 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     }
 
     st.l4sum = sum;
-    st.end = caplen;
+    st.end = ecap;
     st.dirty = dirty;
     st.v6 = v6;
     st.tcp = tcp;
     st.do_l4 = do_l4;
-    st.tail = do_l4 && caplen > (u32)WEND;
+    st.tail = do_l4 && ecap > (u32)WEND;
     return ok;
 }
 

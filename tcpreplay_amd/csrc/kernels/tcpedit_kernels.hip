@@ -80,6 +80,10 @@ struct LaunchArgs {
     uint32_t static_grow;            // output offset = input offset + 4 x record index (VLAN add)
     uint32_t static_shrink;          // output offset = input offset - 4 x record index (VLAN pop, --efcs)
     uint32_t *grow_bad;              // set when a record breaks static_grow's placement
+    // --mtu-trunc (te_launch_t.static_mtu): tile t's output at its input offset - tcut[t], the
+    // predicted bytes the records before it lose; a tile whose total differs sets *grow_bad
+    const long long *tcut;
+    uint32_t static_mtu;
     // after te_fast_tiles: only the listed tiles are edited here, and the last
     // block folds the fast kernel's per-block counters into `counters`
     const uint32_t *tile_list;
@@ -556,6 +560,12 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if (tid == 0)
             sh.out_excl = tile.span_off - a.rec0 +
                           (shrink ? -4ull * tile.first_pkt : (grow ? 4ull * tile.first_pkt : 0ull));
+    } else if (a.static_mtu) {  // the predicted placement, checked by the tile's total
+        if (tid == 0) {
+            const long long c0 = a.tcut[t], c1 = a.tcut[t + 1];
+            sh.out_excl = (unsigned long long)((long long)(tile.span_off - a.rec0) - c0);
+            if ((long long)tile_total != (long long)tile.span_len - (c1 - c0)) atomicOr(a.grow_bad, 1u);
+        }
     } else if (tid < 64) {
         const unsigned long long e = lookback(a.tile_state, t, tile_total, a.err);
         if (tid == 0) sh.out_excl = e;
@@ -874,6 +884,9 @@ struct FastArgs {
     uint32_t in_swapped, in_nsec, v6_ok;
     uint32_t seed_sw, seed_on, skip_bcast;  // te_wave_tiles' phase-A knobs (fl::Knobs), in SGPRs
     uint32_t vlan_tag_word;                 // GROW: the 4 pushed bytes {TPID, TCI} as a LE dword
+    uint32_t mtu;                           // SZ_MTU: --mtu; tile t's output at input offset - tcut[t]
+    const long long *tcut;
+    uint32_t *grow_bad;                     // SZ_MTU: a tile whose cut differs from tcut's
     uint32_t stream;                        // nontemporal span loads and output stores (a batch larger
                                             // than the 256 MiB Infinity Cache: read once, written once)
     // window mode (te_wave_tiles<..., WIN>: the record discovery fused into the edit)
@@ -1357,7 +1370,7 @@ __device__ __forceinline__ bool wk_solo(const te_tile_t &tl, uint32_t tb) {
 }
 
 // size-changing instances (SZ): the one length change every record takes
-enum : int { SZ_NONE = TE_SZ_NONE, SZ_GROW = TE_SZ_GROW, SZ_VDEL = TE_SZ_VDEL, SZ_EFCS = TE_SZ_EFCS };
+enum : int { SZ_NONE = TE_SZ_NONE, SZ_GROW = TE_SZ_GROW, SZ_VDEL = TE_SZ_VDEL, SZ_EFCS = TE_SZ_EFCS, SZ_MTU = TE_SZ_MTU };
 
 // caplen and len of the record header at LDS byte h (any alignment) + delta: the VLAN
 // push's +4 (tcpedit.c:112-113), the VLAN pop's or --efcs's -4 (tcpedit.c:78-84)
@@ -1375,6 +1388,22 @@ __device__ __forceinline__ void hdr_add4(uint8_t *S, uint32_t h, uint32_t delta)
         w[0] = (q0 & lo) | (cap << s8);
         w[1] = (cap >> (32u - s8)) | (len << s8);
         w[2] = (q2 & ~lo) | (len >> (32u - s8));
+    }
+}
+
+// caplen = len = v in the record header at LDS byte h (any alignment): --mtu-trunc's cut
+// (edit_packet.c:599)
+__device__ __forceinline__ void hdr_put(uint8_t *S, uint32_t h, uint32_t v) {
+    const uint32_t h8 = h + 8, al = h8 & ~3u, s8 = 8u * (h8 & 3u);
+    uint32_t *w = (uint32_t *)(S + al);
+    if (s8 == 0) {
+        w[0] = v;
+        w[1] = v;
+    } else {
+        const uint32_t lo = (1u << s8) - 1u, q0 = w[0], q2 = w[2];
+        w[0] = (q0 & lo) | (v << s8);
+        w[1] = (v >> (32u - s8)) | (v << s8);
+        w[2] = (q2 & ~lo) | (v >> (32u - s8));
     }
 }
 
@@ -1566,6 +1595,100 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
     gout[q] = img[(uint32_t)(q - OS)];
 }
 
+// --mtu-trunc stores (SZ_MTU).  Record j keeps its first 16 + caplen'_j bytes; the records
+// sit back to back from the tile's output offset OS, record j at tile-relative output
+// offset op_j (a wave scan of the kept sizes) and input offset rel_j.  Per output chunk the
+// map K names the record holding its first byte (one mark per record + a prefix max, as
+// wk_chunk_map); bit 15 marks a chunk a record starts inside of.  Pass 1 stores every
+// other chunk as one unaligned 16-byte LDS read of its record (the cut moves records by
+// any byte count: five dwords, four funnel shifts).  Pass 2: each record's lane builds the
+// chunk it starts inside of from the previous record's tail and its own head.  The leading
+// bytes (OS up to the first 16-byte boundary) and the trailing ones (the last boundary up
+// to the tile's output end) go a byte a lane, so a tile writes only its own output bytes:
+// the next tile's first record header, which the last chunk would carry, is not known here.
+// P: K in u16 [0, 512), the record table {rel_j | op_j << 16} in u32 [256, 320).
+template <int NK>
+__device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
+                                             uint32_t out_len, uint32_t npkt, uint32_t my_rel, uint32_t my_op,
+                                             bool on, int lane, bool stream) {
+    const uint64_t C0 = (OS + 15) & ~15ull;
+    const uint32_t o0 = (uint32_t)(C0 - OS);
+    const uint32_t nfull = (out_len - o0) >> 4;  // >= 2: a record here is >= 50 bytes
+    uint16_t *K = (uint16_t *)P;
+    uint32_t *T = P + 256;
+    *(uint4 *)(K + 8 * lane) = make_uint4(0, 0, 0, 0);
+    if (on) T[lane] = my_rel | (my_op << 16);
+    WK_LANES_SYNC();
+    if (on) {  // the first chunk starting at or after op_j (record 0: chunk 0)
+        const uint32_t cj = my_op <= o0 ? 0u : (my_op - o0 + 15u) >> 4;
+        if (cj <= nfull) K[cj] = (uint16_t)(lane + 1);
+    }
+    WK_LANES_SYNC();
+    {  // prefix max over K, 8 entries a lane
+        const uint4 q = *(const uint4 *)(K + 8 * lane);
+        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
+                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+#pragma unroll
+        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
+        const uint32_t excl = wave_prev(wave_scan_max(e[7]));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
+        *(uint4 *)(K + 8 * lane) =
+            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+    }
+    WK_LANES_SYNC();
+    // record j > 0 starting inside a chunk: K there already names record j - 1 (value j)
+    const uint32_t x = (on && lane > 0) ? my_op - o0 : 16u, c1 = x >> 4, t1 = x & 15u;
+    if (t1 != 0 && c1 < nfull) K[c1] = (uint16_t)(lane | 0x8000);
+    WK_LANES_SYNC();
+    uint32_t kv[NK], w[NK][4];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nfull - 1u)];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {  // lanes past the output repeat its last full chunk
+        const uint32_t cc = umin32((uint32_t)lane + 64u * k, nfull - 1u);
+        const uint32_t e = T[(kv[k] & 0x7fu) - 1u];
+        const uint4 v = read16(S, ib + (e & 0xffffu) + o0 + 16u * cc - (e >> 16));
+        w[k][0] = v.x;
+        w[k][1] = v.y;
+        w[k][2] = v.z;
+        w[k][3] = v.w;
+    }
+    WK_LANES_SYNC();
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+        if ((kv[k] >> 15) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
+    {  // pass 2: the chunk record j starts inside of (the previous record's {rel, op} from T:
+       // a DPP shift of my_op came back unshifted here -- the compiler folded it away)
+        const uint32_t ep = T[lane > 0 ? lane - 1 : 0], prel = ep & 0xffffu, pop = ep >> 16;
+        const uint32_t q = o0 + 16u * c1;
+        const bool p2 = t1 != 0 && c1 < nfull;  // (lane 0, off lanes: x = 16, so t1 = 0)
+        // (the lanes that store nothing read the image start: every address stays in it)
+        const uint4 va = read16(S, p2 ? ib + prel + (q - pop) : ib);
+        const uint4 vb = read16(S, p2 ? ib + my_rel - t1 : ib);
+        const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
+        uint32_t m[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t mk = fl::bmask(0, (int)t1 - 4 * i);
+            m[i] = (A[i] & mk) | (B[i] & ~mk);
+        }
+        WK_LANES_SYNC();
+        if (p2) wk_put16(gout, C0 + 16ull * c1, m, stream);
+    }
+    {  // the trailing bytes [o0 + 16 nfull, out_len), a byte a lane
+        const uint32_t q0t = o0 + 16u * nfull, ntr = out_len - q0t;
+        const uint32_t qb = q0t + umin32((uint32_t)lane, ntr ? ntr - 1u : 0u);
+        const uint32_t j = (K[nfull] & 0x7fu) - 1u;
+        const uint32_t e1 = T[umin32(j + 1u, npkt - 1u)];
+        const uint32_t e = (j + 1u < npkt && qb >= (e1 >> 16)) ? e1 : T[j];
+        const uint8_t v = S[ib + (e & 0xffffu) + qb - (e >> 16)];
+        if ((uint32_t)lane < ntr) gout[OS + qb] = v;
+    }
+    // the leading bytes: record 0's (rel 0, op 0)
+    if ((uint32_t)lane < o0) gout[OS + (uint32_t)lane] = S[ib + (uint32_t)lane];
+}
+
 // big-endian / nanosecond input: a record header in host order and microseconds
 __device__ __forceinline__ void conv_hdr(uint8_t *rec, bool swp, bool nsec) {
     const uint32_t ts_sec = ld_hdr32(rec, swp), cl = ld_hdr32(rec + 8, swp), ln = ld_hdr32(rec + 12, swp);
@@ -1605,6 +1728,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
+    constexpr bool MTU = SZ == SZ_MTU;
     // VLAN pop: the window reaches 4 input bytes further (the packet' view skips the tag)
     constexpr int XW = VDEL ? 1 : 0;
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
@@ -1612,7 +1736,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     // per-run tables: copied only by instances whose option groups read them
     __shared__ __attribute__((aligned(16))) uint8_t cfg_raw[WkCfg<F>::reads ? sizeof(te_dev_cfg_t) : 16];
     const te_dev_cfg_t &cfg = *(const te_dev_cfg_t *)cfg_raw;
-    __shared__ unsigned long long red[WK_NW][3];
+    __shared__ unsigned long long red[WK_NW][4];
     __shared__ uint32_t RELB[WIN ? WK_NW : 1][WIN ? WIN_REL : 1];  // window mode: record offsets
     const int tid = threadIdx.x;
     int lane = tid & 63;
@@ -1632,7 +1756,8 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     const bool swp = a.in_swapped != 0, nsec = a.in_nsec != 0, conv = swp || nsec;
     const bool explicit_dir = a.fixed_dir >= 0;
     // the next record's header rides along (conversion; GROW / SHRINK: its caplen/len +- 4)
-    const uint32_t extra = (conv || SZ != SZ_NONE) ? 16u : 0u;
+    // (--mtu-trunc: a tile stores only its own output bytes, so nothing rides along)
+    const uint32_t extra = (conv || (SZ != SZ_NONE && !MTU)) ? 16u : 0u;
     g_cu8 *gin = (g_cu8 *)a.in;
     g_u8 *gout = (g_u8 *)a.out + ((int64_t)a.out_base - (int64_t)a.rec0);
     const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
@@ -1654,7 +1779,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     const uint32_t W = gridDim.x * WK_NW;
     const uint32_t w0 = blockIdx.x * WK_NW + wid;
     const uint32_t n_tiles = a.n_tiles;
-    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0;
+    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0, c_cut = 0;
 #if TE_WK_STAMPS
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
     unsigned long long fph[5] = {0, 0, 0, 0, 0};  // (window mode: inside the record discovery)
@@ -1736,7 +1861,12 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
             uint32_t H[fl::NW], d0;
             // SHRINK: the packet's caplen/len after the pop or the FCS strip (a record whose
             // caplen != len keeps its caplen under --efcs: phase A defers it)
-            const uint32_t ecap = SHRINK ? caplen - 4u : caplen, elen = SHRINK ? len - 4u : len;
+            // MTU: untrunc_packet's cut (edit_packet.c:596-611): a packet longer than l2len + mtu
+            // keeps that many bytes (l2len 14 on this lane; phase A classifies the packet as
+            // captured and checksums the cut one)
+            const bool mcut = MTU && len > a.mtu + 14u;
+            const uint32_t ecap = SHRINK ? caplen - 4u : (mcut ? a.mtu + 14u : caplen);
+            const uint32_t elen = SHRINK ? len - 4u : (mcut ? a.mtu + 14u : len);
             bool tagged = true;  // VDEL: a single 802.1Q / 802.1ad / QinQ-TPID tag at offset 12
             {
                 const uint32_t A4 = wa & ~3u, sh = wa & 3u;
@@ -1788,7 +1918,8 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 nosend = true;
             }
 #else
-            bool ok = fl::phase_a<F>(H, ecap, elen, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
+            bool ok = MTU ? fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st, mcut ? ecap : 0u)
+                          : fl::phase_a<F>(H, ecap, elen, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
             if constexpr (VDEL) ok = ok && tagged;
             ok = ok || !edit;
             // GROW / SHRINK: a record written unedited keeps its size; the scan placement takes it
@@ -1879,6 +2010,9 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 // after the write-back, which rewrote len's bytes
                 if constexpr (GROW) hdr_add4(S, r0, 4u);
                 if constexpr (SHRINK) hdr_add4(S, r0, (uint32_t)-4);
+                if constexpr (MTU) {
+                    if (mcut) hdr_put(S, r0, ecap);
+                }
                 // (window mode: no record numbers; every record it finishes is status 0, which
                 // the caller writes for the whole batch)
                 if (!WIN) ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
@@ -1899,6 +2033,17 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
                 wk_store_sized<false>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
                                       Dj - 4u * (uint32_t)lane, on, 0u, lane, stream && WK_SIZED_STREAM);
+            } else if constexpr (MTU) {
+                // the kept sizes -> output offsets; the tile's output at input offset - tcut[t]
+                const uint32_t osz = on ? 16u + ecap : 0u;
+                const uint32_t incl = wave_scan_add(osz);
+                const uint32_t out_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                const long long k0 = a.tcut[t], k1 = a.tcut[t + 1];
+                const uint32_t cut = tile.span_len - out_len;
+                if (lane == 0 && (long long)cut != k1 - k0) atomicOr(a.grow_bad, 1u);  // (a stale prediction)
+                c_cut += cut;
+                wk_store_mtu<WK_KL + 1>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len, npkt,
+                                        my_rel, incl - osz, on, lane, stream && WK_SIZED_STREAM);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -2073,9 +2218,10 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
         red[wid][0] = c_pkts;
         red[wid][1] = c_bytes;
         red[wid][2] = c_edited;
+        red[wid][3] = c_cut;
     }
     __syncthreads();
-    if (tid < 3) {  // this block's totals; the generic kernel's block 0 adds them up
+    if (tid < 4) {  // this block's totals; the generic kernel's block 0 adds them up
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < WK_NW; ++w) s += red[w][tid];
@@ -2538,7 +2684,8 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE)         \
     X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
     X(TE_FF_ALL, 1, SZ_GROW) X(TE_FF_ALLH, 1, SZ_GROW) X(TE_FF_ALLX, 1, SZ_GROW)                      \
-    X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)
+    X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)  \
+    X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)
 #define TE_WIN_INSTANCES(X)                                                                           \
     X(0u, 1, SZ_NONE) X(TE_FF_SEED, 1, SZ_NONE) X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE)             \
     X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE) X(TE_FF_SEED | TE_FF_INCR, 1, SZ_NONE)          \
@@ -2572,6 +2719,7 @@ static int wave_pick(uint32_t want, int sz) {
     static const uint32_t feat_env =
         getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
     want |= feat_env;
+    if (sz == SZ_MTU) want &= ~TE_FF_INCR;  // (--mtu-trunc recomputes every IP packet's checksums)
     for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k)
         if (wave_inst[k].sz == sz && (want & ~wave_inst[k].feat) == 0 && ((want ^ wave_inst[k].feat) & TE_FF_INCR) == 0)
             return k;
@@ -2656,6 +2804,8 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.static_grow = (uint32_t)L->static_grow;
     a.static_shrink = (uint32_t)L->static_shrink;
     a.grow_bad = L->grow_bad;
+    a.tcut = (const long long *)L->tcut;
+    a.static_mtu = (uint32_t)L->static_mtu;
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
@@ -2934,11 +3084,71 @@ static void launch_generic(bool fz, bool ad, bool slot, int grid, hipStream_t st
 #undef TE_GL
 }
 
+// --mtu-trunc placement (te_launch_t.static_mtu): the bytes each tile's records lose, as
+// untrunc_packet cuts them (edit_packet.c:596-611): len > mtu + l2len -> caplen = len =
+// l2len + mtu.  l2len is predicted from the frame's type field (14; 18 behind one
+// 802.1Q / 802.1ad / QinQ tag).  The prediction only places the tiles: every tile checks
+// its actual output total against it, and a mismatch (another L2 shape, an error, a
+// record written unedited) sets *grow_bad and the host places the batch by scan instead.
+__global__ void te_mtu_tile_cut(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n,
+                                uint32_t mtu, int32_t *cut) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const te_tile_t tl = tiles[t];
+    int32_t s = 0;
+    for (uint32_t k = 0; k < tl.npkt; ++k) {
+        const uint8_t *r = in + tl.span_off + pkt_rel[tl.first_pkt + k];
+        const uint32_t cap = ld32(r + 8), len = ld32(r + 12);
+        uint32_t l2 = 14;
+        if (cap >= 14) {
+            const uint32_t et = ((uint32_t)r[28] << 8) | r[29];
+            if (et == 0x8100u || et == 0x88a8u || et == 0x9100u) l2 = 18;
+        }
+        if (len > mtu + l2) s += (int32_t)cap - (int32_t)(l2 + mtu);
+    }
+    cut[t] = s;
+}
+
+// exclusive prefix of the tile cuts (pre[n] = the total): one block, a stretch a thread
+__global__ void __launch_bounds__(1024) te_mtu_cut_scan(const int32_t *cut, uint32_t n, long long *pre) {
+    __shared__ long long part[1024];
+    const uint32_t per = (n + 1023u) / 1024u, b = threadIdx.x * per, e = min(n, b + per);
+    long long s = 0;
+    for (uint32_t i = b; i < e; ++i) s += cut[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long acc = 0;
+        for (int i = 0; i < 1024; ++i) {
+            const long long v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        pre[n] = acc;
+    }
+    __syncthreads();
+    long long acc = part[threadIdx.x];
+    for (uint32_t i = b; i < e; ++i) {
+        pre[i] = acc;
+        acc += cut[i];
+    }
+}
+
+extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n_tiles,
+                           uint32_t mtu, int32_t *cut, long long *pre, hipStream_t stream) {
+    if (n_tiles == 0) return -1;
+    hipLaunchKernelGGL(te_mtu_tile_cut, dim3((n_tiles + 255) / 256), dim3(256), 0, stream, in, tiles, pkt_rel, n_tiles,
+                       mtu, cut);
+    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, (const int32_t *)cut, n_tiles, pre);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     fill_args(a, L);
     hipError_t e;
-    const bool fast = L->fast && ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink) &&
+    const bool fast = L->fast &&
+                      ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink || L->static_mtu) &&
                       L->n_tiles > 0;
     if (L->win) {  // window mode: the wave lane finds its records; then the chain check
         if (!L->cfg_host || L->in_swapped || L->in_nsec || L->dirbits || L->nwin == 0) return -1;
@@ -3058,8 +3268,12 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         } else {
             f.vlan_tag_word = 0;
         }
+        f.mtu = L->static_mtu ? L->mtu : 0u;
+        f.tcut = (const long long *)L->tcut;
+        f.grow_bad = L->grow_bad;
+        if (L->static_mtu && (!L->tcut || L->fast_kind != TE_FAST_WAVE)) return -1;
         const void *wfn = nullptr;
-        const int wk = wave_pick(fast_feat(ch), grow ? SZ_GROW : L->static_shrink);
+        const int wk = wave_pick(fast_feat(ch), grow ? SZ_GROW : L->static_mtu ? SZ_MTU : L->static_shrink);
         if (wk < 0) return -1;
         wfn = wave_inst[wk].fn;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
