@@ -1454,6 +1454,9 @@ __device__ __forceinline__ uint32_t wave_prev(uint32_t v) {
 #ifndef WK_SIZED_STREAM
 #define WK_SIZED_STREAM 0
 #endif
+#ifndef WK_MTU_STREAM
+#define WK_MTU_STREAM 0  // SZ_MTU: nontemporal chunk stores on batches past the Infinity Cache
+#endif
 #ifndef WK_PLAIN_STREAM
 #define WK_PLAIN_STREAM 1
 #endif
@@ -1659,7 +1662,7 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
     for (int k = 0; k < NK; ++k)
         if ((kv[k] >> 15) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
     {  // pass 2: the chunk record j starts inside of (the previous record's {rel, op} from T:
-       // a DPP shift of my_op came back unshifted here -- the compiler folded it away)
+       // taken with wave_prev DPP shifts instead, the first bytes came from the wrong place)
         const uint32_t ep = T[lane > 0 ? lane - 1 : 0], prel = ep & 0xffffu, pop = ep >> 16;
         const uint32_t q = o0 + 16u * c1;
         const bool p2 = t1 != 0 && c1 < nfull;  // (lane 0, off lanes: x = 16, so t1 = 0)
@@ -2043,7 +2046,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 if (lane == 0 && (long long)cut != k1 - k0) atomicOr(a.grow_bad, 1u);  // (a stale prediction)
                 c_cut += cut;
                 wk_store_mtu<WK_KL + 1>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len, npkt,
-                                        my_rel, incl - osz, on, lane, stream && WK_SIZED_STREAM);
+                                        my_rel, incl - osz, on, lane, stream && WK_MTU_STREAM);
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -3109,29 +3112,45 @@ __global__ void te_mtu_tile_cut(const uint8_t *in, const te_tile_t *tiles, const
     cut[t] = s;
 }
 
-// exclusive prefix of the tile cuts (pre[n] = the total): one block, a stretch a thread
+// exclusive prefix of the tile cuts (pre[n] = the total): one block walks the cuts 4096 at a
+// time, four consecutive a thread (coalesced), a block scan of the threads' sums per step
+// (a stretch per thread made every load a dependent, uncoalesced one: 0.64 ms for 62K tiles)
 __global__ void __launch_bounds__(1024) te_mtu_cut_scan(const int32_t *cut, uint32_t n, long long *pre) {
-    __shared__ long long part[1024];
-    const uint32_t per = (n + 1023u) / 1024u, b = threadIdx.x * per, e = min(n, b + per);
-    long long s = 0;
-    for (uint32_t i = b; i < e; ++i) s += cut[i];
-    part[threadIdx.x] = s;
+    __shared__ long long wsum[16];
+    __shared__ long long carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    if (tid == 0) carry = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        long long acc = 0;
-        for (int i = 0; i < 1024; ++i) {
-            const long long v = part[i];
-            part[i] = acc;
-            acc += v;
+    for (uint32_t base = 0; base < n; base += 4096u) {
+        long long v[4], s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + 4u * tid + (uint32_t)k;
+            v[k] = i < n ? (long long)cut[i] : 0ll;
+            s += v[k];
         }
-        pre[n] = acc;
+        long long x = s;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_up(x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        long long before = carry;
+        for (uint32_t q = 0; q < w; ++q) before += wsum[q];
+        before += x - s;  // this thread's exclusive prefix
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + 4u * tid + (uint32_t)k;
+            if (i < n) pre[i] = before;
+            before += v[k];
+        }
+        __syncthreads();
+        if (tid == 1023) carry = before;  // (the last thread's running total is the step's end)
+        __syncthreads();
     }
-    __syncthreads();
-    long long acc = part[threadIdx.x];
-    for (uint32_t i = b; i < e; ++i) {
-        pre[i] = acc;
-        acc += cut[i];
-    }
+    if (tid == 0) pre[n] = carry;
 }
 
 extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n_tiles,
