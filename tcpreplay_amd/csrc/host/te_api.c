@@ -56,7 +56,7 @@ struct tcpedit_batch_s {
     int mtu_fast;            /* tiles were cut for the wave lane's --mtu-trunc instances */
     int last_mtu;            /* the last launch placed tiles by the --mtu-trunc prediction */
     long long *d_tcut;       /* the prediction: n_tiles + 1 prefix (te_mtu_cuts), ... */
-    int32_t *d_tcut_raw;     /* ... from per-tile cuts */
+    long long *d_tcut_raw;   /* ... from per-64-tile sums (scratch) */
     uint64_t tcut_cap;       /* tiles d_tcut holds */
     int tcut_ok;             /* d_tcut is this tile cut's, for tcut_mtu (0 after any re-cut) */
     int32_t tcut_mtu;
@@ -1331,7 +1331,7 @@ static int mtu_cuts_ready(tcpedit_batch_t *b, int32_t mtu)
         b->d_tcut_raw = NULL;
         b->tcut_cap = 0;
         if (hipMalloc((void **)&b->d_tcut, sizeof(long long) * (b->n_tiles + 1)) != hipSuccess ||
-            hipMalloc((void **)&b->d_tcut_raw, sizeof(int32_t) * (b->n_tiles + 1)) != hipSuccess)
+            hipMalloc((void **)&b->d_tcut_raw, sizeof(long long) * ((b->n_tiles + 63) / 64 + 1)) != hipSuccess)
             return -1;
         b->tcut_cap = b->n_tiles + 1;
     }

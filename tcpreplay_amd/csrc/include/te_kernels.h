@@ -280,11 +280,12 @@ int te_launch_l2carry(te_launch_t *L, hipStream_t stream);
 int te_launch_jnpr(te_launch_t *L, te_jctx_t *out, hipStream_t stream);
 
 int te_launch_packet_server(const te_srv_launch_t *S, hipStream_t stream);
-/* --mtu-trunc placement: cut[t] = bytes tile t's records lose to the truncation, predicted
-   from each record's header and type field (len > mtu + l2len: caplen becomes l2len + mtu),
-   and pre = their exclusive prefix (n_tiles + 1 entries) */
+/* --mtu-trunc placement: pre = the exclusive prefix (n_tiles + 1 entries) of the bytes each
+   tile's records lose to the truncation, predicted from each record's header and type field
+   (len > mtu + l2len: caplen becomes l2len + mtu); bsum: (n_tiles + 63) / 64 + 1 entries of
+   scratch (per-64-tile sums) */
 int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n_tiles, uint32_t mtu,
-                int32_t *cut, long long *pre, hipStream_t stream);
+                long long *bsum, long long *pre, hipStream_t stream);
 #endif
 uint64_t te_q8_slot_bytes(void);
 /* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */

@@ -3093,29 +3093,52 @@ static void launch_generic(bool fz, bool ad, bool slot, int grid, hipStream_t st
 // 802.1Q / 802.1ad / QinQ tag).  The prediction only places the tiles: every tile checks
 // its actual output total against it, and a mismatch (another L2 shape, an error, a
 // record written unedited) sets *grow_bad and the host places the batch by scan instead.
-__global__ void te_mtu_tile_cut(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n,
-                                uint32_t mtu, int32_t *cut) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const te_tile_t tl = tiles[t];
-    int32_t s = 0;
-    for (uint32_t k = 0; k < tl.npkt; ++k) {
-        const uint8_t *r = in + tl.span_off + pkt_rel[tl.first_pkt + k];
-        const uint32_t cap = ld32(r + 8), len = ld32(r + 12);
-        uint32_t l2 = 14;
-        if (cap >= 14) {
-            const uint32_t et = ((uint32_t)r[28] << 8) | r[29];
-            if (et == 0x8100u || et == 0x88a8u || et == 0x9100u) l2 = 18;
+// One wave per tile, its lanes over the tile's records (a thread walking a whole tile made
+// ~100 dependent header loads per thread: 150 us for 4M IMIX records); each block takes 64
+// tiles and leaves their block-local exclusive prefix in pre[] and their total in bsum[b].
+__global__ void __launch_bounds__(256) te_mtu_tile_cut(const uint8_t *in, const te_tile_t *tiles,
+                                                       const uint16_t *pkt_rel, uint32_t n, uint32_t mtu,
+                                                       long long *pre, long long *bsum) {
+    __shared__ long long c[64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t0 = blockIdx.x * 64u;
+    for (uint32_t j = w; j < 64u; j += 4u) {
+        const uint32_t t = t0 + j;
+        long long s = 0;
+        if (t < n) {
+            const te_tile_t tl = tiles[t];
+            for (uint32_t k = lane; k < tl.npkt; k += 64u) {
+                const uint8_t *r = in + tl.span_off + pkt_rel[tl.first_pkt + k];
+                const uint32_t cap = ld32(r + 8), len = ld32(r + 12);
+                uint32_t l2 = 14;
+                if (cap >= 14) {
+                    const uint32_t et = ((uint32_t)r[28] << 8) | r[29];
+                    if (et == 0x8100u || et == 0x88a8u || et == 0x9100u) l2 = 18;
+                }
+                if (len > mtu + l2) s += (long long)cap - (long long)(l2 + mtu);
+            }
         }
-        if (len > mtu + l2) s += (int32_t)cap - (int32_t)(l2 + mtu);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) c[j] = s;
     }
-    cut[t] = s;
+    __syncthreads();
+    if (w == 0) {
+        const long long v = c[lane];
+        long long x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_up(x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (t0 + lane < n) pre[t0 + lane] = x - v;
+        if (lane == 63) bsum[blockIdx.x] = x;
+    }
 }
 
-// exclusive prefix of the tile cuts (pre[n] = the total): one block walks the cuts 4096 at a
-// time, four consecutive a thread (coalesced), a block scan of the threads' sums per step
-// (a stretch per thread made every load a dependent, uncoalesced one: 0.64 ms for 62K tiles)
-__global__ void __launch_bounds__(1024) te_mtu_cut_scan(const int32_t *cut, uint32_t n, long long *pre) {
+// exclusive prefix of the block sums, in place (pre[n] = the total): one block walks them 4096
+// at a time, four consecutive a thread (coalesced), a block scan of the threads' sums per step
+__global__ void __launch_bounds__(1024) te_mtu_cut_scan(long long *pre, uint32_t n) {
     __shared__ long long wsum[16];
     __shared__ long long carry;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
@@ -3126,7 +3149,7 @@ __global__ void __launch_bounds__(1024) te_mtu_cut_scan(const int32_t *cut, uint
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t i = base + 4u * tid + (uint32_t)k;
-            v[k] = i < n ? (long long)cut[i] : 0ll;
+            v[k] = i < n ? pre[i] : 0ll;
             s += v[k];
         }
         long long x = s;  // inclusive scan over the wave
@@ -3153,12 +3176,22 @@ __global__ void __launch_bounds__(1024) te_mtu_cut_scan(const int32_t *cut, uint
     if (tid == 0) pre[n] = carry;
 }
 
+// the block prefixes into the tiles' local prefixes; pre[n] = the batch total
+__global__ void te_mtu_cut_add(long long *pre, const long long *bpre, uint32_t n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) pre[t] += bpre[t >> 6];
+    else if (t == n) pre[n] = bpre[(n + 63u) >> 6];
+}
+
+// bsum: (n_tiles + 63) / 64 + 1 entries of scratch
 extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel, uint32_t n_tiles,
-                           uint32_t mtu, int32_t *cut, long long *pre, hipStream_t stream) {
+                           uint32_t mtu, long long *bsum, long long *pre, hipStream_t stream) {
     if (n_tiles == 0) return -1;
-    hipLaunchKernelGGL(te_mtu_tile_cut, dim3((n_tiles + 255) / 256), dim3(256), 0, stream, in, tiles, pkt_rel, n_tiles,
-                       mtu, cut);
-    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, (const int32_t *)cut, n_tiles, pre);
+    const uint32_t nb = (n_tiles + 63u) / 64u;
+    hipLaunchKernelGGL(te_mtu_tile_cut, dim3(nb), dim3(256), 0, stream, in, tiles, pkt_rel, n_tiles, mtu, pre, bsum);
+    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    hipLaunchKernelGGL(te_mtu_cut_add, dim3((n_tiles + 1u + 255u) / 256u), dim3(256), 0, stream, pre,
+                       (const long long *)bsum, n_tiles);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
