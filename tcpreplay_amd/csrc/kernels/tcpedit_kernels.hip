@@ -2650,12 +2650,13 @@ __global__ void __launch_bounds__(FZ_BLOCK) te_fuzz_states(const uint8_t *st, ui
     uint32_t f[FZ_PER_THREAD], tot;
     const uint32_t i0 = blockIdx.x * FZ_PER_BLOCK + threadIdx.x * FZ_PER_THREAD;
     const uint32_t c = fz_flags(st, n, i0, f);
-    uint32_t rank = blk[blockIdx.x] + block_exscan<FZ_BLOCK>(c, wsum, tot);
-    const uint32_t s0 = words[1];
+    const uint32_t rank = blk[blockIdx.x] + block_exscan<FZ_BLOCK>(c, wsum, tot);
+    // one jump to the thread's first record, then one draw (three steps) per reaching record
+    uint32_t x = lcg_jump(words[1], 3ull * rank);
 #pragma unroll
     for (int k = 0; k < FZ_PER_THREAD; ++k) {
-        if (i0 + k < n) states[i0 + k] = lcg_jump(s0, 3ull * rank);
-        rank += f[k];
+        if (i0 + k < n) states[i0 + k] = x;
+        if (f[k]) x = ((x * 1103515245u + 12345u) * 1103515245u + 12345u) * 1103515245u + 12345u;
     }
 }
 
