@@ -1,4 +1,5 @@
 # A/B of the mtu bench line: product library vs a variant (argument: variant name), twice each
+# (the variant is built by tools/build_variants.sh; lift the ./tcpreplay_amd/lib/var line of .gpurunignore for the call)
 set -o pipefail
 mkdir -p gpurun_out
 V=$PWD/tcpreplay_amd/lib/var/libtcpedit_hip_$1.so
