@@ -37,6 +37,11 @@ size_t tcpreplay_hip_output_bound(tcpreplay_hip_t *ctx, size_t len);
    unique-ip edit failed (stats->failed) */
 int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *ctx, const uint8_t *pcap, size_t len, uint8_t *out, size_t cap,
                                      uint64_t *failed);
+/* 1 when the last tcpreplay_hip_replay_to_pcap ended where safe_pcap_next exit(-1)s
+   (send_packets.c:955,985 -> src/common/utils.c:136-156: a record with len > MAX_SNAPLEN
+   or a zero len or caplen): its output is what tcpreplay wrote before exiting, and
+   geterr names the record; 0 otherwise */
+int tcpreplay_hip_reader_exited(tcpreplay_hip_t *ctx);
 #ifdef __cplusplus
 }
 #endif

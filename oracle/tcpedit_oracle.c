@@ -3262,15 +3262,27 @@ int oracle_rewrite_mem_base(const uint8_t *in, size_t in_len, const uint8_t *cac
         if (caplen > MAX_SNAPLEN)
             break; /* libpcap's reader refuses the record ("invalid packet capture length"):
                       pcap_next returns NULL and tcprewrite's loop ends (tcprewrite.c:289) */
-        if (len > MAX_SNAPLEN) { /* tcprewrite.c:296-297 errx() */
-            seterr("Frame too big");
+        /* safe_pcap_next (tcprewrite.c:289 -> src/common/utils.c:131-169): a len past
+           MAX_SNAPLEN (:136-145) or a zero len or caplen (:147-156) exit(-1)s, so the
+           output keeps the records before this one; tcprewrite.c:293-296's errx()s are
+           never reached after it */
+        if (len > MAX_SNAPLEN) {
+            seterr("safe_pcap_next ERROR: Invalid packet length: %u is greater than maximum %u", len, MAX_SNAPLEN);
             rc = -1;
             break;
         }
+        if (!len || !caplen) {
+            seterr("safe_pcap_next ERROR: Invalid packet length: packet length=%u capture length=%u", len, caplen);
+            rc = -1;
+            break;
+        }
+        const size_t file_cap = caplen;
+        if (len < caplen) /* utils.c:159-162: caplen = len before the copy and the edit */
+            caplen = len;
         uint32_t ts_sec = rh[0], ts_usec = nsec ? rh[1] / 1000 : rh[1];
         packetnum++;
-        memcpy(buf, in + ip_ + 16, caplen);
-        ip_ += 16 + caplen;
+        memcpy(buf, in + ip_ + 16, caplen); /* tcprewrite.c:301: the trimmed caplen */
+        ip_ += 16 + file_cap;               /* libpcap moved past the record as stored */
         int dir = DIR_C2S;
         if (cdata)
             dir = check_cache(cdata, cdata_len, pkt_base + packetnum);

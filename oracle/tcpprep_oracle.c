@@ -410,6 +410,26 @@ static uint32_t tpo_rd32(const uint8_t *p, int sw)
     return sw ? __builtin_bswap32(v) : v;
 }
 
+/* tcpprep.c:353's read: libpcap's pcap_next (an oversize or truncated record ends the
+ * file), then safe_pcap_next (src/common/utils.c:131-169): len > MAX_SNAPLEN or a zero
+ * len or caplen exit(-1)s -- before write_cache (tcpprep.c:194), so no cache is written --
+ * and len < caplen trims caplen to len.  Returns 1 with the record's data offset and its
+ * (trimmed) caplen, 0 at the end, -5 at the reader's exit; *off moves past the record. */
+static int tpo_next(const uint8_t *pcap, size_t len, int sw, size_t *off, size_t *data, uint32_t *caplen)
+{
+    if (*off + 16 > len)
+        return 0;
+    const uint32_t cl = tpo_rd32(pcap + *off + 8, sw), pl = tpo_rd32(pcap + *off + 12, sw);
+    if (cl > 262144u || *off + 16 + cl > len)
+        return 0;
+    if (pl > 262144u || !pl || !cl)
+        return -5;
+    *data = *off + 16;
+    *caplen = pl < cl ? pl : cl;
+    *off += 16 + cl;
+    return 1;
+}
+
 
 /* ---- auto modes: tree.c's host table (RB tree there, open addressing here) ---- */
 typedef struct {
@@ -596,12 +616,13 @@ static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, in
     tpo_nodes = calloc(tpo_cap, sizeof(tpo_node_t));
     if (!tpo_nodes)
         return -4;
-    for (size_t off = 24; off + 16 <= len;) {
-        uint32_t caplen = tpo_rd32(pcap + off + 8, sw);
-        if (caplen > 262144u || off + 16 + caplen > len)
-            break;
-        const uint8_t *d = pcap + off + 16;
-        off += 16 + caplen;
+    size_t off = 24, dat = 0;
+    uint32_t caplen = 0;
+    int nx;
+    while ((nx = tpo_next(pcap, len, sw, &off, &dat, &caplen)) != 0) {
+        if (nx < 0)
+            return -5;
+        const uint8_t *d = pcap + dat;
         uint16_t proto = 0;
         uint32_t l2len = 0;
         int res = caplen ? tpo_l2(d, caplen, &proto, &l2len) : -1;
@@ -670,7 +691,9 @@ static int tpo_check_tree(const tpo_opt_t *o, int fam, const uint8_t *src)
 /*
  * tcpprep_oracle_run: classify a whole pcap image and write the cache file
  * (header + comment + packed 2-bit entries) into `out`.  Returns the cache
- * size, or -1 on an option error, -2 on a bad pcap, -3 if `cap` is too small.
+ * size, or -1 on an option error, -2 on a bad pcap, -3 if `cap` is too small,
+ * -4 on the reference's errx() paths, -5 when safe_pcap_next exits on a record
+ * (tpo_next: no cache is written).
  */
 static uint64_t tpo_pkt_base, tpo_last_entries;
 
@@ -705,15 +728,13 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
         return -4; /* errx "Unsupported pcap DLT type" */
     if (tpo_dlt != 1 && o.mode == TPO_MAC)
         return -4; /* err "MAC mode splitting is only supported by DLT_EN10MB packet captures." */
-    if (tpo_dlt == 178)
-        for (size_t off = 24; off + 16 <= len;) {
-            uint32_t cl = tpo_rd32(pcap + off + 8, sw);
-            if (cl > 262144u || off + 16 + cl > len)
-                break;
-            if (cl >= 4 && !memcmp(pcap + off + 16, "MGC", 3) && (pcap[off + 16 + 3] & 0x02))
+    if (tpo_dlt == 178) {
+        size_t off = 24, d = 0;
+        uint32_t cl = 0;
+        while (tpo_next(pcap, len, sw, &off, &d, &cl) > 0)
+            if (cl >= 4 && !memcmp(pcap + d, "MGC", 3) && (pcap[d + 3] & 0x02))
                 return -4;
-            off += 16 + cl;
-        }
+    }
     size_t clen = strlen(o.comment);
     size_t hdr = 24 + clen;
     if (cap < hdr)
@@ -721,25 +742,26 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
     memset(out, 0, cap);
     if (o.mode == TPO_AUTO) {
         uint64_t recs = 0;
-        for (size_t off = 24; off + 16 <= len;) {
-            uint32_t cl = tpo_rd32(pcap + off + 8, sw);
-            if (cl > 262144u || off + 16 + cl > len)
-                break;
-            recs++;
-            off += 16 + cl;
+        {
+            size_t off = 24, d = 0;
+            uint32_t cl = 0;
+            while (tpo_next(pcap, len, sw, &off, &d, &cl) > 0)
+                recs++;
         }
-        if (tpo_tree_pass(&o, pcap, len, sw, recs) < 0)
-            return -4;
+        const int tr = tpo_tree_pass(&o, pcap, len, sw, recs);
+        if (tr < 0)
+            return tr == -5 ? -5 : -4;
     }
     uint64_t packetnum = 0, entries = 0;
     static uint8_t pkt[MAXPACKET + 64];
-    for (size_t off = 24; off + 16 <= len;) {
-        uint32_t caplen = tpo_rd32(pcap + off + 8, sw);
-        if (caplen > 262144u || off + 16 + caplen > len)
-            break; /* libpcap stops */
+    size_t off = 24, dat = 0;
+    uint32_t caplen = 0;
+    int nx;
+    while ((nx = tpo_next(pcap, len, sw, &off, &dat, &caplen)) != 0) {
+        if (nx < 0)
+            return -5; /* safe_pcap_next's exit(-1): the cache file stays empty */
         memset(pkt, 0, caplen + 64);
-        memcpy(pkt, pcap + off + 16, caplen);
-        off += 16 + caplen;
+        memcpy(pkt, pcap + dat, caplen);
         packetnum++;
         int send = 1, dir = 0, add = 1; /* dir: 1 = C2S */
         if (o.nlist && !!(o.xx_mode & XX_EXCLUDE) == tpo_check_list(&o, tpo_pkt_base + packetnum)) {

@@ -150,6 +150,10 @@ static int tro_listed_out(const tro_list_t *l, int exclude, uint64_t packetnum)
     return (rule_set && exclude) || (!rule_set && !exclude);
 }
 
+/* 1 when the last run ended at safe_pcap_next's exit(-1) (its length: the records before) */
+static int g_replay_exit;
+int tcpreplay_oracle_exited(void) { return g_replay_exit; }
+
 /* returns the output length, or -1 bad options, -2 not a pcap, -3 out too small */
 long tcpreplay_oracle_run_list(const uint8_t *pcap, size_t len, int loops, int unique_ip, double unique_loops,
                                int preload, const char *list, int exclude, uint8_t *out, size_t cap,
@@ -198,17 +202,25 @@ long tcpreplay_oracle_run_list(const uint8_t *pcap, size_t len, int loops, int u
     static uint8_t pkt[MAXPACKET + 64];
     uint64_t iteration = 0, uniq = 0, last_uniq = 0;
     *failed = 0;
+    g_replay_exit = 0;
     for (int pass = 0; pass < loops; pass++) {
         uint64_t packetnum = 0;
-        for (size_t off = 24; off + 16 <= len;) {
-            const uint32_t ts = tpo_rd32(pcap + off, sw), frac = tpo_rd32(pcap + off + 4, sw);
-            const uint32_t caplen = tpo_rd32(pcap + off + 8, sw), plen = tpo_rd32(pcap + off + 12, sw);
-            if (caplen > 262144u || off + 16 + caplen > len)
-                break; /* libpcap stops */
-            uint8_t *data = preload ? cache + off + 16 : pkt;
+        size_t off = 24, dat = 0;
+        uint32_t caplen = 0;
+        int nx;
+        /* get_next_packet (send_packets.c:955,985): safe_pcap_next's reader rules (tpo_next);
+           its exit(-1) comes in the first pass, with the records sent so far in the file */
+        while ((nx = tpo_next(pcap, len, sw, &off, &dat, &caplen)) != 0) {
+            if (nx < 0) {
+                g_replay_exit = 1;
+                free(cache);
+                return (long)o;
+            }
+            const uint32_t ts = tpo_rd32(pcap + dat - 16, sw), frac = tpo_rd32(pcap + dat - 12, sw);
+            const uint32_t plen = tpo_rd32(pcap + dat - 4, sw);
+            uint8_t *data = preload ? cache + dat : pkt;
             if (!preload)
-                memcpy(pkt, pcap + off + 16, caplen);
-            off += 16 + caplen;
+                memcpy(pkt, pcap + dat, caplen);
             if (tro_listed_out(list ? &lst : NULL, exclude, ++packetnum))
                 continue;
             if (unique_ip && uniq && uniq > last_uniq && tro_fast_edit(data, caplen, uniq - 1, preload) == -1) {
@@ -334,15 +346,17 @@ int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int p
         memcpy(out, hdr, 24);
     }
     buf = calloc(1, MAXPACKET + 65536); /* libpcap's read buffer (a fresh mapping: zero) */
-    /* the records (libpcap's walk) */
-    for (size_t p = 24; p + 16 <= in_len; nrec++) {
-        uint32_t cl;
-        memcpy(&cl, in + p + 8, 4);
-        if (swap)
-            cl = bswap32_(cl);
-        if (cl > MAX_SNAPLEN || p + 16 + cl > in_len)
-            break;
-        p += 16 + cl;
+    /* the records (libpcap's walk, then safe_pcap_next, send_packets.c:955,985 ->
+       src/common/utils.c:131-169): a record with len > MAX_SNAPLEN or a zero len or caplen
+       exit(-1)s when the first pass reaches it */
+    int reader_exit = 0;
+    {
+        size_t p = 24, d = 0;
+        uint32_t cl = 0;
+        int nx;
+        while ((nx = tpo_next(in, in_len, swap, &p, &d, &cl)) > 0)
+            nrec++;
+        reader_exit = nx < 0;
     }
     if (preload) {
         cache = calloc(nrec ? nrec : 1, sizeof(*cache));
@@ -362,17 +376,15 @@ int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int p
             if (swap)
                 for (int q = 0; q < 4; q++)
                     rh[q] = bswap32_(rh[q]);
-            if (rh[3] > MAX_SNAPLEN) { /* safe_pcap_next's errx (tcpreplay too) */
-                seterr("Frame too big");
-                rc = -1;
-                break;
-            }
+            const uint32_t file_cap = rh[2];
+            if (rh[3] < rh[2]) /* utils.c:159-162: caplen = len */
+                rh[2] = rh[3];
             uint8_t *data;
             ohdr_t h = {rh[2], rh[3]};
             if (!preload || pass == 0) {
                 memcpy(buf, in + p + 16, rh[2]);
                 data = buf;
-                if (preload) { /* the unedited copy and header the later passes use */
+                if (preload) { /* the unedited copy and header the later passes use (:973-977) */
                     cache[i] = calloc(1, (size_t)rh[2] + 512 + 4096);
                     memcpy(cache[i], in + p + 16, rh[2]);
                     memcpy(chdr + 4 * i, rh, 16);
@@ -382,7 +394,7 @@ int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int p
                 h.caplen = chdr[4 * i + 2];
                 h.len = chdr[4 * i + 3];
             }
-            p += 16 + rh[2];
+            p += 16 + file_cap;
             if (listed_out)
                 continue; /* read (and cached under -K), not edited, not sent */
             int warned = 0;
@@ -414,6 +426,10 @@ int tcpreplay_edit_oracle_run(const uint8_t *in, size_t in_len, int loops, int p
             memcpy(out + op, orh, 16);
             memcpy(out + op + 16, data, h.caplen);
             op += 16 + h.caplen;
+        }
+        if (rc == 0 && pass == 0 && reader_exit) {
+            seterr("safe_pcap_next ERROR: Invalid packet length: packet %llu", (unsigned long long)(nrec + 1));
+            rc = -1;
         }
         /* increment_iteration (send_packets.c:362-372) */
         last_uniq = uniq;

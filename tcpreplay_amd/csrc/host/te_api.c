@@ -23,6 +23,10 @@
         }                                                                                 \
     } while (0)
 
+/* safe_pcap_next's exit (src/common/utils.c:136-156): a record with len > MAX_SNAPLEN or a
+   zero len or caplen ends the run; the output keeps the records before it */
+#define TE_READER_ERR "safe_pcap_next ERROR: Invalid packet length: packet %lld"
+
 static __thread int g_device = -1; /* per thread: one host thread may drive each device */
 
 int tcpedit_set_device(int device)
@@ -47,7 +51,7 @@ struct tcpedit_batch_s {
     int status_valid;
     int64_t stop_error_pkt;  /* a record the reader refuses (len > MAX_SNAPLEN): hard error */
     int slot_layout;
-    int has_zero_cap;        /* some input record has caplen 0 (written nowhere: sizes shift) */
+    int has_trim;            /* some input record has len < caplen: the reader trims it (sizes shift) */
     int grow_off;            /* a run found a record that broke static_grow placement ... */
     uint32_t grow_off_gen;   /* ... under this cfg_gen: place by scan from then on */
     int last_grow;           /* the last launch placed records by static_grow (+4) or static_shrink (-4) */
@@ -324,7 +328,7 @@ typedef struct {
     int fixed;               /* the arrays cannot grow (a pipeline slot's pinned index) */
     uint64_t rec_bytes;      /* sum of 16 + data + 4 (output room) */
     uint64_t scratch_bytes;
-    int has_zero_cap;
+    int has_trim;
     int64_t stop_error_pkt;  /* stretch-relative, or -1 */
     int walk_stop;           /* 0 ran out / reached stop_at, 1 oversize, 2 hard error */
     size_t end;              /* offset of the first record not taken */
@@ -374,14 +378,15 @@ static void walk_range(te_walk_t *w)
         }
         if (off + 16 + caplen > len)
             break; /* ... and at a truncated one (or a pipeline chunk ends here) */
-        if (plen > 262144u) {
-            /* tcprewrite.c:296-297 errx()s here: the output keeps earlier records */
+        if (plen > 262144u || plen == 0 || caplen == 0) {
+            /* safe_pcap_next (tcprewrite.c:289 -> src/common/utils.c:136-156) exit(-1)s
+               here: the output keeps the earlier records */
             w->stop_error_pkt = (int64_t)w->n_pkts;
             w->walk_stop = 2;
             break;
         }
-        if (caplen == 0)
-            w->has_zero_cap = 1;
+        if (plen < caplen) /* utils.c:159-162: the edit sees caplen = len (sizes shift) */
+            w->has_trim = 1;
         uint32_t data = w->pad && plen > caplen ? plen : caplen;
         uint32_t g = (uint32_t)(off & 15);
         uint32_t slot = TE_SLOT_BYTES_OF_H(w->head, g, data);
@@ -790,7 +795,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         m->n_pkts += x->n_pkts;
         m->rec_bytes += x->rec_bytes;
         m->scratch_bytes += x->scratch_bytes;
-        m->has_zero_cap |= x->has_zero_cap;
+        m->has_trim |= x->has_trim;
         m->walk_stop = x->walk_stop;
         m->end = x->end;
         m->stop_at = x->stop_at;
@@ -841,7 +846,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         m->n_pkts += rest.n_pkts;
         m->rec_bytes += rest.rec_bytes;
         m->scratch_bytes += rest.scratch_bytes;
-        m->has_zero_cap |= rest.has_zero_cap;
+        m->has_trim |= rest.has_trim;
         m->walk_stop = rest.walk_stop;
         m->end = rest.end;
         m->fail = rest.fail;
@@ -874,7 +879,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     b->out_cap = 24 + 64 + m->rec_bytes;
     b->scratch_bytes = m->scratch_bytes;
     b->stop_error_pkt = m->stop_error_pkt;
-    b->has_zero_cap = m->has_zero_cap;
+    b->has_trim = m->has_trim;
     b->walk_stop = m->walk_stop;
     b->walk_end = m->end;
     b->in_len = len;
@@ -1375,18 +1380,18 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.slot_layout = b->slot_layout;
     /* size-preserving config: no edit step can change a record's length or drop
        it (efcs, VLAN add/del, fixlen, MTU truncation, skipped soft errors, and
-       zero-length records are the only ways), so outputs sit at input offsets */
+       the reader's len < caplen trim are the only ways), so outputs sit at input offsets */
     const te_dev_cfg_t *c = &t->cfg;
-    L.static_off = !b->slot_layout && static_capable(c) && !b->has_zero_cap;
+    L.static_off = !b->slot_layout && static_capable(c) && !b->has_trim;
     L.rec0 = b->rec0 ? b->rec0 : 24;
     /* VLAN add as the only size change: every record grows by 4 bytes or is a hard error
        (dlt_en10mb_encode, en10mb.c:520-575), so outputs sit at input offset + 4 x index */
     L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
-                    !c->mtu_truncate && !c->skip_soft_errors && !b->has_zero_cap && !c->fuzz_seed &&
+                    !c->mtu_truncate && !c->skip_soft_errors && !b->has_trim && !c->fuzz_seed &&
                     !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env();
     /* a VLAN pop or --efcs as the only size change: outputs at input offset - 4 x index
        (checked record by record like static_grow) */
-    L.static_shrink = !b->slot_layout && !b->has_zero_cap && !b->swapped && !b->nsec &&
+    L.static_shrink = !b->slot_layout && !b->has_trim && !b->swapped && !b->nsec &&
                               !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env()
                           ? static_shrink_kind(c)
                           : TE_SZ_NONE;
@@ -1394,7 +1399,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     b->last_grow = L.static_grow ? 4 : L.static_shrink ? -4 : 0;
     /* --mtu-trunc on the wave lane: tiles placed by the predicted cuts (fast_capable_mtu) */
     L.static_mtu = b->mtu_fast && b->fast_kind == TE_FAST_WAVE && fast_capable_mtu(c) && !b->slot_layout &&
-                   !b->has_zero_cap && !b->swapped && !b->nsec && !b->dirbits_len && b->n_tiles > 0 &&
+                   !b->has_trim && !b->swapped && !b->nsec && !b->dirbits_len && b->n_tiles > 0 &&
                    !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env() &&
                    !fast_lane_off() && mtu_cuts_ready(b, c->mtu) == 0;
     L.tcut = L.static_mtu ? b->d_tcut : NULL;
@@ -1988,7 +1993,7 @@ fail:
 static int fused_capable(const tcpedit_t *t, const tcpedit_batch_t *b)
 {
     return b->fast_tiles && b->fast_kind == TE_FAST_WAVE && !b->slot_layout && static_capable(&t->cfg) &&
-           fast_capable(&t->cfg) && !b->has_zero_cap &&
+           fast_capable(&t->cfg) && !b->has_trim &&
            !b->swapped && !b->nsec && !b->d_dirbits && !b->pre_host && !fast_lane_off() &&
            b->stop_error_pkt < 0 && !b->walk_stop && b->n_pkts && !getenv("TCPEDIT_HIP_NO_FUSED");
 }
@@ -2165,9 +2170,12 @@ int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
                   (long long)(first + 1 + (int64_t)b->pkt_base));
         return TCPEDIT_ERROR;
     }
-    if (b->err[0] != ~0ull || b->stop_error_pkt >= 0) {
-        int64_t e = b->err[0] != ~0ull ? (int64_t)b->err[0] : b->stop_error_pkt;
-        te_seterr(t, "Error rewriting packets: packet %lld", (long long)(e + 1 + (int64_t)b->pkt_base));
+    if (b->err[0] != ~0ull) {
+        te_seterr(t, "Error rewriting packets: packet %lld", (long long)(b->err[0] + 1 + b->pkt_base));
+        return TCPEDIT_ERROR;
+    }
+    if (b->stop_error_pkt >= 0) {
+        te_seterr(t, TE_READER_ERR, (long long)(b->stop_error_pkt + 1 + (int64_t)b->pkt_base));
         return TCPEDIT_ERROR;
     }
     return TCPEDIT_OK;
@@ -2459,7 +2467,7 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
         d_rel = NULL;
         b->n_tiles = nt;
     }
-    b->has_zero_cap = tot[IDX_T_ZERO] != 0;
+    b->has_trim = tot[IDX_T_TRIM] != 0;
     b->walk_end = tot[IDX_T_END];
     b->walk_stop = tot[IDX_T_STOP] == IDX_STOP ? 1 : tot[IDX_T_STOP] == IDX_ERROR ? 2 : 0;
     b->stop_error_pkt = tot[IDX_T_ERR_REC] == ~0ull ? -1 : (int64_t)tot[IDX_T_ERR_REC];
@@ -2870,11 +2878,13 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     const uint64_t ob = b->out_base ? b->out_base : 24;
     uint64_t bytes = b->counters[TE_CNT_BYTES_OUT];
     int64_t err_pkt = -1;
+    int reader_err = 0;
     if (b->err[0] != ~0ull) { /* a hard error truncates the output at the failing record */
         bytes = b->err[1] - ob;
         err_pkt = (int64_t)(pkt_base + b->err[0]);
     } else if (b->stop_error_pkt >= 0) {
         err_pkt = (int64_t)(pkt_base + (uint64_t)b->stop_error_pkt);
+        reader_err = 1;
     }
     if (*pos + bytes > out_cap) {
         te_seterr(t, "output buffer too small (%llu bytes needed so far)", (unsigned long long)(*pos + bytes));
@@ -2896,7 +2906,7 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     t->pub.runtime.total_bytes += b->counters[TE_CNT_BYTES_OUT];
     t->pub.runtime.pkts_edited += b->counters[TE_CNT_EDITED];
     if (err_pkt >= 0) {
-        te_seterr(t, "Error rewriting packets: packet %lld", (long long)(err_pkt + 1));
+        te_seterr(t, reader_err ? TE_READER_ERR : "Error rewriting packets: packet %lld", (long long)(err_pkt + 1));
         t->pipe_err = 1;
         *stopped = 2;
     }
@@ -3132,7 +3142,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         } else {
             b->n_pkts = T[IDX_T_RECS];
             b->n_tiles = T[IDX_T_TILES];
-            b->has_zero_cap = T[IDX_T_ZERO] != 0;
+            b->has_trim = T[IDX_T_TRIM] != 0;
             b->walk_end = T[IDX_T_END];
             b->walk_stop = T[IDX_T_STOP] == IDX_STOP ? 1 : T[IDX_T_STOP] == IDX_ERROR ? 2 : 0;
             b->stop_error_pkt = T[IDX_T_ERR_REC] == ~0ull ? -1 : (int64_t)T[IDX_T_ERR_REC];
@@ -3147,8 +3157,8 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         entry_file = file0[s] + b->walk_end - 24;
         if (b->n_pkts == 0) {
             if (b->stop_error_pkt >= 0) { /* the chunk's first record is the hard error: the
-                                             output ends with the chunks before (tcprewrite.c:296) */
-                te_seterr(t, "Error rewriting packets: packet %llu", (unsigned long long)(pkts + 1));
+                                             output ends with the chunks before (utils.c:136-156) */
+                te_seterr(t, TE_READER_ERR, (long long)(pkts + 1));
                 t->pipe_err = 1;
             }
             stopped = 1;
@@ -3178,7 +3188,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
                output is its records' bytes: start their D2H behind the edit now, without the
                host's round trip for the results (pipe_finish_chunk checks them and copies
                again only when a replay changed the bytes) */
-            if (!b->slot_layout && static_capable(&t->cfg) && !b->has_zero_cap && b->stop_error_pkt < 0 &&
+            if (!b->slot_layout && static_capable(&t->cfg) && !b->has_trim && b->stop_error_pkt < 0 &&
                 !getenv("TCPEDIT_HIP_PIPE_NO_EARLY") &&
                 pos_early + (b->walk_end - entry_img) <= out_cap) {
                 const uint64_t ob_ = b->out_base ? b->out_base : 24, nb_ = b->walk_end - entry_img;
@@ -3607,7 +3617,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         if (b->n_pkts == 0) { /* the walk stopped at the chunk's first record */
             stopped = 1;
             if (b->stop_error_pkt >= 0) {
-                te_seterr(t, "Error rewriting packets: packet %llu", (unsigned long long)(pkts + 1));
+                te_seterr(t, TE_READER_ERR, (long long)(pkts + 1));
                 goto fail_drain;
             }
             break;
@@ -4038,13 +4048,25 @@ static int te_srv_atexit_done;
    sync its stream.  A kernel that never leaves (a broken server, stuck in its tile body)
    is reported and its stream is not synced -- tcpedit_close and exit must not hang on it;
    its mappings are then leaked, not freed under it (srv_free) */
+/* (tests: the path of a kernel that never leaves; read once) */
+static int srv_test_stuck(void)
+{
+    static int v = -1;
+    if (v < 0)
+        v = getenv("TCPEDIT_HIP_SRV_TEST_STUCK") != NULL;
+    return v;
+}
+
 static int srv_stop(te_srv_t *S)
 {
     if (!S->running)
         return 0;
+    if (S->stuck) /* it did not leave the last time: do not wait for it again */
+        return -1;
     __atomic_store_n(&S->ctl->stop, 1u, __ATOMIC_RELEASE);
     const double t0 = te_now();
-    while (__atomic_load_n(&S->ctl->alive, __ATOMIC_ACQUIRE) && !getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) {
+    const int test_stuck = srv_test_stuck();
+    while (!test_stuck && __atomic_load_n(&S->ctl->alive, __ATOMIC_ACQUIRE)) {
         if (te_now() - t0 > 2.0) {
             fprintf(stderr, "tcpedit: the packet server kernel did not leave in 2 s; its buffers are leaked\n");
             S->stuck = 1;
@@ -4052,7 +4074,7 @@ static int srv_stop(te_srv_t *S)
         }
         __builtin_ia32_pause();
     }
-    if (getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) { /* (tests: the path of a kernel that never leaves) */
+    if (test_stuck) {
         fprintf(stderr, "tcpedit: the packet server kernel did not leave in 2 s; its buffers are leaked\n");
         S->stuck = 1;
         return -1;
@@ -4221,7 +4243,7 @@ static int srv_call(tcpedit_t *t, te_srv_t *S)
             hipStreamSynchronize(S->stream);
             if (srv_launch(t, S, q - 1) < 0)
                 return -1;
-        } else if (te_now() - t0 > 5.0 || getenv("TCPEDIT_HIP_SRV_TEST_STUCK")) {
+        } else if (te_now() - t0 > 5.0 || srv_test_stuck()) {
             te_seterr(t, "packet server did not answer in 5 s");
             srv_stop(S); /* bounded: a kernel that does not leave is left running, unsynced */
             return -1;

@@ -89,8 +89,13 @@ tcpedit_replay_t *tcpedit_replay_open(tcpedit_t *t, const void *pcap, size_t len
         goto fail;
     memcpy(r->img, pcap, len);
     for (size_t p = 24; p + 16 <= len; r->nrec++) { /* libpcap's walk */
-        const uint32_t cl = rp32(r->img + p + 8, r->swapped);
+        const uint32_t cl = rp32(r->img + p + 8, r->swapped), pl = rp32(r->img + p + 12, r->swapped);
         if (cl > 262144u || p + 16 + cl > len)
+            break;
+        /* safe_pcap_next (send_packets.c:955,985 -> src/common/utils.c:136-156) exits at
+           this record: the batch stops there too (its first pass then fails after the
+           records before it were sent) */
+        if (pl > 262144u || !pl || !cl)
             break;
         p += 16 + cl;
     }
@@ -321,8 +326,8 @@ int tcpedit_replay_pass(tcpedit_t *t, tcpedit_replay_t *r, void *out, size_t cap
             return TCPEDIT_ERROR;
         }
     }
-    /* the records as sent: every record edited (a zero-length one too: pcap_dump writes it,
-       where tcprewrite drops it, tcprewrite.c:367), its fraction as the dump writes it */
+    /* the records as sent: every record edited (one the edit emptied too: pcap_dump writes
+       it, where tcprewrite drops it, tcprewrite.c:367), its fraction as the dump writes it */
     size_t ip = 24, op = 24, w = 0;
     uint64_t ku = 0;
     int err = 0;
@@ -340,14 +345,12 @@ int tcpedit_replay_pass(tcpedit_t *t, tcpedit_replay_t *r, void *out, size_t cap
         }
         uint32_t h[4];
         if (st[i] & TE_ST_ZEROCAP) {
-            /* a record with caplen 0 after its edit (the batch output leaves it out): read
-               that way, tcpedit_packet's only change is --efcs's trim of len (tcpedit.c:78-84)
-               before the L2 parse fails (a soft error); emptied by the edit, it is the fuzz
-               step's drop (fuzzing.c:37-60: caplen = len = 0) */
-            const uint32_t ln = rp32(src + ip + 12, r->swapped);
+            /* a record with caplen 0 after its edit (the batch output leaves it out): no
+               record is read that way (safe_pcap_next exits, utils.c:147-156), so the edit
+               emptied it -- the fuzz step's drop (fuzzing.c:37-60: caplen = len = 0) */
             h[0] = rp32(src + ip, r->swapped);
             h[2] = 0;
-            h[3] = cl0 ? 0u : (((const tcpedit_ref_t *)t)->efcs && ln > 4 ? ln - 4 : ln);
+            h[3] = 0;
         } else {
             if (op + 16 > olen) { /* (the batch wrote fewer records than it edited) */
                 err = 1;

@@ -383,7 +383,8 @@ typedef struct {
     uint64_t n, records;
 } tp_index_t;
 
-/* the record walk: libpcap's pcap_next stops at an oversize or truncated record.
+/* the record walk: libpcap's pcap_next stops at an oversize or truncated record, and
+   safe_pcap_next's rules follow (an exit, or caplen trimmed to len).
    MAC mode leaves records shorter than an Ethernet header out of the cache
    (tcpprep.c:465-468 `break`s before add_cache), so they get no entry -- unless
    the include/exclude packet list, checked first (:362-375), gives them DONT_SEND. */
@@ -416,9 +417,17 @@ static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index
         return tp_err(t, "out of memory");
     int mac = t->cfg.mode == TP_MODE_MAC, gaps = 0;
     for (size_t off = 24; off + 16 <= len;) {
-        uint32_t caplen = rd32(img + off + 8, sw);
-        if (caplen > 262144u || off + 16 + caplen > len)
+        const uint32_t fcap = rd32(img + off + 8, sw), plen = rd32(img + off + 12, sw);
+        if (fcap > 262144u || off + 16 + fcap > len)
             break;
+        /* safe_pcap_next (tcpprep.c:353 -> src/common/utils.c:131-169): a len past
+           MAX_SNAPLEN or a zero len or caplen exit(-1)s before write_cache (no cache file);
+           len < caplen trims caplen to len */
+        if (plen > 262144u || !plen || !fcap)
+            return tp_err(t, "safe_pcap_next ERROR: Invalid packet length: packet %llu: packet length=%u capture "
+                             "length=%u",
+                          (unsigned long long)(x->records + 1), plen, fcap);
+        const uint32_t caplen = plen < fcap ? plen : fcap;
         x->records++;
         if (dlt == 178 && caplen >= 4 && !memcmp(img + off + 16, "MGC", 3) && (img[off + 16 + 3] & 0x02))
             /* JUNIPER_FLAG_NO_L2: get_l2len_protocol leaves l2len 0 with l2offset past it, and
@@ -443,7 +452,7 @@ static int index_pcap(tcpprep_hip_t *t, const uint8_t *img, size_t len, tp_index
                 x->pktnum[x->n] = (uint32_t)x->records;
             x->n++;
         }
-        off += 16 + caplen;
+        off += 16 + fcap;
     }
     if (x->records > 0xffffffffull)
         return tp_err(t, "more than 2^32 records");

@@ -4,7 +4,10 @@
  * The host side of send_packets (src/send_packets.c:379-646) for file output: the record
  * walk libpcap's reader makes (a record past MAX_SNAPLEN or past the end stops it), the
  * pass loop with increment_iteration (:362-372) deciding which passes edit, and the
- * pcap_dump header (sendpacket.c:945-968: pcap_open_dead(DLT_EN10MB, MAX_SNAPLEN)).  Each
+ * pcap_dump header (sendpacket.c:945-968: pcap_open_dead(DLT_EN10MB, MAX_SNAPLEN)).
+ * safe_pcap_next's rules (src/common/utils.c:131-169) hold on the walk: a zero len or
+ * caplen (or len > MAX_SNAPLEN) ends the run after the first pass's earlier records, and
+ * the kernels trim caplen to len.  Each
  * pass runs on the device (tcpreplay_kernels.hip) and lands in one device output buffer.
  */
 #include <hip/hip_runtime_api.h>
@@ -22,8 +25,11 @@ struct tcpreplay_hip_s {
     int unique_ip, preload;
     double unique_loops;
     tr_list_t list;     /* --include / --exclude (n = 0: none) */
+    int reader_exit;    /* the last replay ended at safe_pcap_next's exit */
     char err[512];
 };
+
+int tcpreplay_hip_reader_exited(tcpreplay_hip_t *t) { return t ? t->reader_exit : 0; }
 
 /* parse_list (src/common/list.c:61-130): ',' tokens (strtok_r drops empty ones), each
    "^[0-9]+(-([0-9]+|\s*))?$"; add_to_list (:36-50) takes min by strtoull(.., 0), max = min
@@ -230,13 +236,22 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
         return tr_err(t, "--unique-ip is served for DLT_EN10MB captures only");
     if (cap < tcpreplay_hip_output_bound(t, len))
         return tr_err(t, "output buffer smaller than tcpreplay_hip_output_bound");
-    /* libpcap's walk: a record past MAX_SNAPLEN or past the end stops the read */
+    t->reader_exit = 0;
+    /* libpcap's walk: a record past MAX_SNAPLEN or past the end stops the read; then
+       safe_pcap_next (send_packets.c:955,985 -> src/common/utils.c:131-169): a len past
+       MAX_SNAPLEN or a zero len or caplen exit(-1)s in the first pass, after the records
+       before it were sent (the kernels trim len < caplen) */
     uint64_t n = 0, ncap = 1024;
     uint64_t *off = malloc(ncap * sizeof *off);
+    int reader_exit = 0;
     for (size_t o = 24; off && o + 16 <= len;) {
-        const uint32_t cl = rd32(pcap + o + 8, sw);
+        const uint32_t cl = rd32(pcap + o + 8, sw), pl = rd32(pcap + o + 12, sw);
         if (cl > 262144u || o + 16 + cl > len)
             break;
+        if (pl > 262144u || !pl || !cl) {
+            reader_exit = 1;
+            break;
+        }
         if (n == ncap) {
             uint64_t *g = realloc(off, 2 * ncap * sizeof *off);
             if (!g) {
@@ -285,7 +300,7 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
         memcpy(out, hdr, 24);
     }
     uint64_t o = 24, iteration = 0, uniq = 0, last_uniq = 0, fails = 0;
-    for (uint32_t pass = 0; pass < t->loops && n; pass++) {
+    for (uint32_t pass = 0; pass < (reader_exit ? 1u : t->loops) && n; pass++) {
         TrPass p;
         memset(&p, 0, sizeof p);
         p.img = d_img;
@@ -330,6 +345,10 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
     }
     *failed = fails;
     rc = (int64_t)o;
+    if (reader_exit) { /* the output holds the first pass's records before it */
+        t->reader_exit = 1;
+        tr_err(t, "safe_pcap_next ERROR: Invalid packet length: packet %llu", (unsigned long long)(n + 1));
+    }
 fail:
     hipFree(d_img);
     hipFree(d_cache);

@@ -17,9 +17,9 @@
 #define IDX_NONE 0xffffffffffffffffull
 /* how the chain ends in a window (w_flags) */
 #define IDX_STOP 1u   /* oversize record: libpcap stops (walk_stop 1) */
-#define IDX_ERROR 2u  /* len > 262144: the reference's error (walk_stop 2) */
+#define IDX_ERROR 2u  /* len > 262144, len 0 or caplen 0: safe_pcap_next exits (walk_stop 2) */
 #define IDX_END 4u    /* a truncated record or the bytes ran out */
-#define IDX_ZERO 8u   /* a record with caplen 0 */
+#define IDX_TRIM 8u   /* a record with len < caplen: safe_pcap_next trims it (utils.c:159-162) */
 /* totals[] */
 #define IDX_T_RECS 0
 #define IDX_T_TILES 1
@@ -29,7 +29,7 @@
 #define IDX_T_WINDOWS 5 /* windows up to the chain's end */
 #define IDX_T_STOP 6    /* IDX_STOP / IDX_ERROR / IDX_END, or 0 */
 #define IDX_T_END 7     /* offset of the first record not taken */
-#define IDX_T_ZERO 8
+#define IDX_T_TRIM 8
 #define IDX_T_ERR_REC 9 /* the record with the len error, or ~0 */
 #define IDX_T_OVERFLOW 10 /* the tiles or records outgrew tile_cap / rec_cap */
 #define IDX_T_BADWIN 11 /* diagnostics: the first window whose guess missed the chain */

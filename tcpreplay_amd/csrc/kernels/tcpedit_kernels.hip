@@ -380,9 +380,13 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         if constexpr (MODE == MODE_SLOT)  // zero the room after the data (chunk stores spilled into it)
             for (uint32_t i = r0 + 16 + my_cap; i < slot_end; ++i) S[i] = 0;
         uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp);
-        uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
+        const uint32_t fcap = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
         if (a.in_nsec) ts_frac /= 1000;  // libpcap opens at us precision
-        c_in = 16 + (unsigned long long)caplen;
+        c_in = 16 + (unsigned long long)fcap;
+        // safe_pcap_next (src/common/utils.c:159-162): len < caplen -> caplen = len before
+        // tcprewrite.c:301's copy, so the bytes past it are not the record's (a read there
+        // is a stale static-buffer read, Q8)
+        const uint32_t caplen = len < fcap ? len : fcap;
         const uint64_t pktno = a.pkt_base + tile.first_pkt + tid;  // 0-based
         int dir = TE_DIR_C2S;
         const bool explicit_dir = a.fixed_dir >= 0;
@@ -398,7 +402,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         pk.d = rec + 16;
         pk.caplen = caplen;
         pk.len = len;
-        pk.phys = my_cap;
+        pk.phys = my_cap < caplen ? my_cap : caplen;
         pk.avail = slot_end - (r0 + 16);
         pk.unsupported = false;
         pk.need = 0;
@@ -448,7 +452,7 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             st32(orec, ts_sec);
             st32(orec + 4, ts_frac);
         }
-        if (swp || pk.caplen != caplen || pk.len != len || pk.d != rec + 16) {
+        if (swp || pk.caplen != fcap || pk.len != len || pk.d != rec + 16) {
             st32(orec + 8, pk.caplen);
             st32(orec + 12, pk.len);
         }
@@ -898,7 +902,7 @@ struct FastArgs {
                                             //   are not the image's
     uint32_t nwin;
     uint64_t *w_entry, *w_exit;             // per window: where the chain enters and leaves it
-    uint32_t *w_flags;                      // per window: IDX_STOP / IDX_ERROR / IDX_END / IDX_ZERO
+    uint32_t *w_flags;                      // per window: IDX_STOP / IDX_ERROR / IDX_END / IDX_TRIM
     uint32_t *win_bad;                      // bit 1: a window left a record to the exact path
 };
 
@@ -2139,7 +2143,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
 #endif
             if (TE_WIN_PREFETCH && k + W < a.nwin) tew::stage_load(ia, k + W, stg);
             WK_STAMP(0)  // (window mode: the record discovery)
-            const uint32_t wfl = fw.wstop | (fw.anyzero ? (uint32_t)IDX_ZERO : 0u);
+            const uint32_t wfl = fw.wstop | (fw.anytrim ? (uint32_t)IDX_TRIM : 0u);
             if (lane == 0) {
                 a.w_entry[k] = fw.went;
                 a.w_exit[k] = fw.wexit;
@@ -2401,7 +2405,9 @@ __device__ int64_t q8_chain(const Q8Args &q, int64_t pos, uint32_t need) {
     uint32_t steps = 0;
     for (int64_t j = pos - 1; j >= -(int64_t)q.npre; --j) {
         if (++steps > Q8_MAX_CHAIN) return Q8_TOOLONG;
-        const uint32_t cl = ld_hdr32(q8_recp(q, j) + 8, swp);
+        const uint8_t *rh = q8_recp(q, j);
+        const uint32_t fc = ld_hdr32(rh + 8, swp), pl = ld_hdr32(rh + 12, swp);
+        const uint32_t cl = pl < fc ? pl : fc;  // the bytes tcprewrite.c:301 copied (the trimmed caplen)
         if (cl > cov) {
             cov = cl;
             j0 = j;
@@ -2446,8 +2452,9 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
     for (int64_t j = j0; j <= (int64_t)i; ++j) {
         const uint8_t *rec = q8_recp(q, j);
         const uint32_t ts_sec = ld_hdr32(rec, swp), ts_frac = ld_hdr32(rec + 4, swp) / (a.in_nsec ? 1000u : 1u);
-        const uint32_t caplen = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
-        if (caplen > MAX_SNAPLEN) { Q8_DBG(2); return Q8_FAIL; }
+        const uint32_t fcap = ld_hdr32(rec + 8, swp), len = ld_hdr32(rec + 12, swp);
+        if (fcap > MAX_SNAPLEN) { Q8_DBG(2); return Q8_FAIL; }
+        const uint32_t caplen = len < fcap ? len : fcap;  // safe_pcap_next's trim (utils.c:159-162)
         for (uint32_t x = 0; x < caplen; ++x) buf[x] = rec[16 + x];  // tcprewrite.c:301
         if (caplen > V) V = caplen;
         if (j < 0 && (a.l2carry || a.jscan || (FZ && a.fuzz_mode == TE_FUZZ_APPLY)))
@@ -2844,6 +2851,7 @@ __global__ __launch_bounds__(256) void te_l2carry_mark(LaunchArgs a, unsigned lo
     const uint8_t *rec = a.in + tile.span_off + a.pkt_rel[j];
     uint32_t caplen = ld_hdr32(rec + 8, swp);
     const uint32_t len = ld_hdr32(rec + 12, swp);
+    if (len < caplen) caplen = len;                         // safe_pcap_next (utils.c:159-162)
     if (cfg.efcs && len > 4 && caplen == len) caplen -= 4;  // tcpedit.c:78-84
     int dir = TE_DIR_C2S;
     if (a.fixed_dir >= 0) {
@@ -2908,6 +2916,7 @@ __global__ __launch_bounds__(256) void te_jnpr_mark(LaunchArgs a, unsigned long 
     const uint8_t *rec = a.in + tile.span_off + a.pkt_rel[j];
     uint32_t caplen = ld_hdr32(rec + 8, swp);
     const uint32_t len = ld_hdr32(rec + 12, swp);
+    if (len < caplen) caplen = len;                         // safe_pcap_next (utils.c:159-162)
     if (cfg.efcs && len > 4 && caplen == len) caplen -= 4;  // tcpedit.c:78-84
     int dir = TE_DIR_C2S;
     if (a.fixed_dir >= 0) {

@@ -30,6 +30,13 @@ __device__ __forceinline__ u32 be32at(const u8 *p) {
 }
 
 // fast_edit_packet: the new source / destination (host order) and where they go, or -1
+// a record's caplen as get_next_packet returns it: safe_pcap_next (send_packets.c:955,985 ->
+// src/common/utils.c:159-162) trims it to len (the host walk stopped at a zero len or caplen)
+__device__ __forceinline__ u32 rd_cap(const u8 *rec, bool sw) {
+    const u32 cl = rd32(rec + 8, sw), pl = rd32(rec + 12, sw);
+    return pl < cl ? pl : cl;
+}
+
 __device__ int fast_edit(const u8 *pkt, u32 caplen, uint64_t iteration, bool cached, u32 &src, u32 &dst,
                          u32 &at_s, u32 &at_d) {
     te::L2 r;
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(256) void tr_mark(TrPass a) {
     if (j >= a.n) return;
     const uint64_t off = a.off[j];
     const u8 *rec = (a.cache ? a.cache : a.img) + off;
-    const u32 caplen = rd32(rec + 8, a.swapped != 0);
+    const u32 caplen = rd_cap(rec, a.swapped != 0);
     u32 keep = 1, at_s = 0, src = 0, dst = 0, at_d = 0;
     if (a.list && listed_out(a.list, a.nlist, a.exclude != 0, j + 1)) {
         keep = 0;  // skipped before anything else: not edited, not sent, not counted failed
@@ -118,9 +125,9 @@ __global__ __launch_bounds__(256) void tr_write(TrPass a) {
     const u8 *rec = (a.cache ? a.cache : a.img) + a.off[j];
     u8 *o = a.out + a.pos[j];
     const bool sw = a.swapped != 0;
-    const u32 caplen = rd32(rec + 8, sw);
+    const u32 caplen = rd_cap(rec, sw);
     if (lane < 4) {  // ts_sec, the fraction (x1000 for a microsecond capture), caplen, len
-        u32 v = rd32(rec + 4 * lane, sw);
+        u32 v = lane == 2 ? caplen : rd32(rec + 4 * lane, sw);
         if (lane == 1 && !a.nsec) v *= 1000u;
         for (int k = 0; k < 4; ++k) o[4 * lane + k] = (u8)(v >> (8 * k));
     }

@@ -30,7 +30,8 @@
 //   (A single-pass version with a decoupled look-back over windows and a serial finishing
 //   check cost ~50 ns a window: 0.84 ms on C2.)
 // libpcap's ends are kept: an oversize record (caplen > 262144) or a truncated one ends
-// the chain; a len > 262144 record ends it with the reference's error (tcprewrite.c:296).
+// the chain; a record with len > 262144, len 0 or caplen 0 ends it with safe_pcap_next's
+// exit (src/common/utils.c:136-156).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,7 +74,7 @@ __device__ __forceinline__ Facts count_window(const IdxArgs &a, WinLds<S> &M, u3
     const tew::Found fw = tew::find_window<S, OL>(a, M.img, M.rel, k);
     const u64 ws = fw.ws, went = fw.went, wexit = fw.wexit;
     const u32 wstop = fw.wstop, nrec = fw.nrec;
-    const bool anyzero = fw.anyzero;
+    const bool anytrim = fw.anytrim;
 
     // ---- the tile cut: one ballot per tile ----
     u32 ntile = 0;
@@ -116,7 +117,7 @@ __device__ __forceinline__ Facts count_window(const IdxArgs &a, WinLds<S> &M, u3
     for (int o = 32; o > 0; o >>= 1) scr += __shfl_xor(scr, o, 64);
     for (u32 i = lane; i < nrec; i += IW)
         if (i < (u32)IDX_MAXR) a.t_prel[(u64)k * IDX_MAXR + i] = (u16)(M.rel[i] - M.rel[M.tsi[i]]);
-    return Facts{went, wexit, scr, nrec, ntile, wstop | (anyzero ? IDX_ZERO : 0u)};
+    return Facts{went, wexit, scr, nrec, ntile, wstop | (anytrim ? IDX_TRIM : 0u)};
 }
 
 // ---- the scan, in two levels: te_index_part (a block of SB windows, one a thread) leaves
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(SB) void te_index_scan(IdxArgs a) {
     // set by the write pass, window by window
     a.totals[IDX_T_BAD] = 0;
     a.totals[IDX_T_BADWIN] = 0xffffffffull;
-    a.totals[IDX_T_ZERO] = 0;
+    a.totals[IDX_T_TRIM] = 0;
 }
 
 // ---- the write pass: a wave per window puts its tiles and record offsets at its bases ----
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(IB) void te_index_write(IdxArgs a) {
             atomicOr((unsigned long long *)&T[IDX_T_BAD], 1ull);
             atomicMin((unsigned long long *)&T[IDX_T_BADWIN], (unsigned long long)k);
         }
-        if (wfl & IDX_ZERO) atomicOr((unsigned long long *)&T[IDX_T_ZERO], 1ull);
+        if (wfl & IDX_TRIM) atomicOr((unsigned long long *)&T[IDX_T_TRIM], 1ull);
     }
     if (ovf) return;
     const u64 ws = a.base + (u64)k * WN;

@@ -12,8 +12,8 @@
 // cross-window chain is checked by the caller (the index's write pass, the fused edit's
 // validation kernel): a window's first record must be where the chain left the nearest
 // earlier window with a record.  libpcap's ends are kept: an oversize record (caplen >
-// 262144) or a truncated one ends the chain; len > 262144 ends it with the reference's error
-// (tcprewrite.c:296).
+// 262144) or a truncated one ends the chain; len > 262144, len 0 or caplen 0 ends it with
+// safe_pcap_next's exit (src/common/utils.c:131-169).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -47,7 +47,7 @@ __device__ __forceinline__ u32 nib(u32 z) {  // 4 zero flags of a dword -> 4 bit
 struct LaneWalk {
     u64 exit;  // first record start >= se, or where the chain ended
     u32 n;     // records taken
-    u32 stop;  // 0 goes on, IDX_STOP oversize, IDX_ERROR len > 262144, IDX_END truncated / no bytes
+    u32 stop;  // 0 goes on, IDX_STOP oversize, IDX_ERROR the reader's exit, IDX_END truncated / no bytes
 };
 __device__ __forceinline__ LaneWalk walk_lds(const IdxArgs &a, const u32 *img, u64 A0, u64 from, u64 se) {
     LaneWalk w{from, 0, 0};
@@ -67,7 +67,7 @@ __device__ __forceinline__ LaneWalk walk_lds(const IdxArgs &a, const u32 *img, u
             w.stop = IDX_END;
             break;
         }
-        if (pl > MAXCAP) {
+        if (pl > MAXCAP || pl == 0 || cl == 0) {  // safe_pcap_next exits (utils.c:136-156)
             w.stop = IDX_ERROR;
             break;
         }
@@ -101,7 +101,7 @@ struct Found {
     u64 ws, we, A0, staged_end;
     u64 went, wexit;  // IDX_NONE: no record starts here
     u32 wstop, nrec;
-    bool anyzero;     // a record with caplen 0
+    bool anytrim;     // a record with len < caplen (safe_pcap_next trims it, utils.c:159-162)
 };
 // a window's staging: its 16-byte chunks [c0, nch) from A0, in registers (K a lane) until
 // stored to LDS -- issued one window ahead by the fused edit, so the loads are in flight
@@ -401,16 +401,17 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
         u64 off = e;
         for (u32 i = 0; i < w.n; ++i) {
             rel[pos + i] = (u32)(off - ws);
-            const u32 cl = sw32(lds_u32(img, (u32)(off - A0) + 8), a.sw);
-            zero |= cl == 0;
+            const u32 cl = sw32(lds_u32(img, (u32)(off - A0) + 8), a.sw),
+                      pl = sw32(lds_u32(img, (u32)(off - A0) + 12), a.sw);
+            zero |= pl < cl;  // safe_pcap_next trims it: the exact path places it by scan
             off += 16 + (u64)cl;
             if (pos + i + 1 == nrec) rel[nrec] = (u32)(off - ws);  // the last record's end
         }
     }
-    const bool anyzero = __ballot(zero) != 0;
+    const bool anytrim = __ballot(zero) != 0;
     asm volatile("" ::: "memory");
     TEW_STAMP(4)
 #undef TEW_STAMP
-    return Found{ws, we, A0, staged_end, went, wexit, wstop, nrec, anyzero};
+    return Found{ws, we, A0, staged_end, went, wexit, wstop, nrec, anytrim};
 }
 }  // namespace tew

@@ -38,6 +38,7 @@ typedef struct {
     tcpedit_t *te;
     tcpedit_batch_t *b;
     int opened, rc;
+    int jfail;          /* the Juniper state seeding failed (read by all after the inner barrier) */
     int64_t reach;
     int carry;
     int jnpr;                                 /* DLT_JUNIPER_ETHER: the decoder-state exchange runs */
@@ -129,19 +130,26 @@ static void *shard_main(void *arg)
     for (int j = 0; j < J->n; j++)
         all_open &= J->sh[j].opened;
     if (all_open && J->dlt == 178) {
-        /* the nearest earlier shard's Juniper decoder state, then this shard's carry-out */
+        /* the nearest earlier shard's Juniper decoder state, then this shard's carry-out.
+           A failure here goes to jfail, not opened: the other threads may still be reading
+           every shard's opened flag above, and all of them fold jfail in only
+           after the barrier, so they agree on all_open and on joining the all-reduce */
         const uint8_t *src = NULL;
         for (int j = k - 1; j >= 0 && !src; j--)
             if (J->sh[j].jvalid == 1)
                 src = J->sh[j].jstate;
-        if (tcpedit_set_jnpr_state(S->te, src, TCPEDIT_JNPR_STATE_BYTES, 0) < 0 ||
+        const char *inj = getenv("TCPREWRITE_GPUS_FAIL_JNPR"); /* (tests: this shard's seeding fails) */
+        if ((inj && *inj && atoi(inj) == k) || tcpedit_set_jnpr_state(S->te, src, TCPEDIT_JNPR_STATE_BYTES, 0) < 0 ||
             (S->carry = tcpedit_batch_l2carry_out(S->te, S->b)) < 0) {
-            snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
-            S->opened = 0;
+            snprintf(S->err, sizeof S->err, "device %d: %s", k,
+                     inj && *inj && atoi(inj) == k ? "Juniper state seeding failed (injected)" : tcpedit_geterr(S->te));
+            S->jfail = 1;
         }
         pthread_barrier_wait(&J->bar);
         for (int j = 0; j < J->n; j++)
-            all_open &= J->sh[j].opened;
+            all_open &= !J->sh[j].jfail;
+        if (S->jfail)
+            S->opened = 0; /* (no thread reads opened again before the placement barrier) */
     }
     for (int j = 0; j < k; j++)
         skip += (uint64_t)J->sh[j].reach;

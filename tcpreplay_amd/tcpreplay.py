@@ -29,7 +29,8 @@ def _lib():
                 ("tcpreplay_hip_set_preload_pcap", c_int, [vp, ctypes.c_bool]),
                 ("tcpreplay_hip_output_bound", sz, [vp, sz]),
                 ("tcpreplay_hip_replay_to_pcap", ctypes.c_int64,
-                 [vp, ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(ctypes.c_uint64)])):
+                 [vp, ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(ctypes.c_uint64)]),
+                ("tcpreplay_hip_reader_exited", c_int, [vp])):
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         _SIG_DONE = True
@@ -63,6 +64,12 @@ class TcpReplay:
         if n < 0:
             raise RuntimeError(self.geterr())
         return out.raw[:n], int(failed.value)
+
+    @property
+    def reader_exited(self) -> bool:
+        """the last replay ended at safe_pcap_next's exit (src/common/utils.c:136-156): its
+        output is what tcpreplay wrote before exiting"""
+        return bool(self._L.tcpreplay_hip_reader_exited(self._ctx))
 
     def close(self):
         if self._ctx:

@@ -261,7 +261,7 @@ static int rewrite_packets(tcpedit_t *ctx, const uint8_t *img, size_t len, FILE 
         pktdata_buff = calloc(1, MAXPACKET);
     pktdata = &pktdata_buff;
     size_t off = 24;
-    while (off + 16 <= len) { /* safe_pcap_next */
+    while (off + 16 <= len) { /* pcap_next, then safe_pcap_next (src/common/utils.c:131-169) */
         pkthdr.ts.tv_sec = rd32(img + off, sw);
         pkthdr.ts.tv_usec = rd32(img + off + 4, sw) / (nsec ? 1000 : 1);
         pkthdr.caplen = rd32(img + off + 8, sw);
@@ -270,11 +270,21 @@ static int rewrite_packets(tcpedit_t *ctx, const uint8_t *img, size_t len, FILE 
             break;
         const uint8_t *pktconst = img + off + 16;
         off += 16 + pkthdr.caplen;
-        packetnum++;
         if (pkthdr.len > MAX_SNAPLEN) {
-            fprintf(stderr, "Frame too big, len %d exceeds %d\n", pkthdr.len, MAX_SNAPLEN);
+            fprintf(stderr, "safe_pcap_next ERROR: Invalid packet length: %u is greater than maximum %u\n",
+                    pkthdr.len, MAX_SNAPLEN);
+            fflush(out);
             exit(255);
         }
+        if (!pkthdr.len || !pkthdr.caplen) {
+            fprintf(stderr, "safe_pcap_next ERROR: Invalid packet length: packet length=%u capture length=%u\n",
+                    pkthdr.len, pkthdr.caplen);
+            fflush(out);
+            exit(255);
+        }
+        if (pkthdr.len < pkthdr.caplen)
+            pkthdr.caplen = pkthdr.len;
+        packetnum++;
         memcpy(*pktdata, pktconst, pkthdr.caplen);
         if (cachedata)
             cache_result = check_cache(cachedata, packetnum);

@@ -56,24 +56,29 @@ def test_device_index_with_a_tcpprep_cache(built):
     _run(pcap, args, cache)
 
 
-def test_tiny_huge_and_zero_length_records(built):
-    """caplen 0..20 records (the fast lane defers them), records larger than a wave tile
-    (solo) and than a generic slot (huge: HBM scratch), between ordinary ones"""
+def test_tiny_huge_and_trimmed_records(built):
+    """caplen 1..21 records (the fast lane defers them), records larger than a wave tile
+    (solo) and than a generic slot (huge: HBM scratch), and len < caplen records (the
+    reader trims caplen to len, src/common/utils.c:159-162), between ordinary ones"""
     base = S.records(S.pcap_fixed(3000, 90, seed=9))
     big = S.records(S.pcap_fixed(3, 9000, seed=10)) + S.records(S.pcap_fixed(2, 40000, seed=11))
     recs = []
     for i, r in enumerate(base):
         recs.append(r)
         if i % 97 == 0:
-            recs.append((1, i, i % 21, i % 21, bytes(i % 21)))
+            recs.append((1, i, 1 + i % 21, 1 + i % 21, bytes(1 + i % 21)))
+        if i % 89 == 5:
+            ts, tu, cl, ln, d = r
+            recs.append((ts, tu, cl, cl - 1 - i % 40, d))
         if i % 701 == 0:
             recs.append(big[(i // 701) % len(big)])
     _run(S.build_pcap(recs), ["--seed=3", "--fixcsum"])
 
 
 def test_the_chain_ends_as_libpcap_ends_it(built):
-    """a truncated last record, an oversize record mid-capture (libpcap stops there) and a
-    len > 262144 record (the reference's error; the output keeps the records before it)"""
+    """a truncated last record, an oversize record mid-capture (libpcap stops there), and a
+    len > 262144 or zero len / caplen record (safe_pcap_next's exit; the output keeps the
+    records before it)"""
     recs = S.records(S.pcap_fixed(20_000, 80, seed=12))
     pcap = S.build_pcap(recs)
     _run(pcap[:-30], ["--fixcsum"])
@@ -83,6 +88,9 @@ def test_the_chain_ends_as_libpcap_ends_it(built):
     _run(over, ["--fixcsum"])
     err = S.build_pcap(recs[:9_999] + [(ts, tu, cl, 400_000, d)] + recs[10_000:])
     _run(err, ["--fixcsum"])
+    # safe_pcap_next's exit (src/common/utils.c:147-156): caplen 0, len 0, or both
+    for zc, zl in ((0, 0), (0, 80), (cl, 0)):
+        _run(S.build_pcap(recs[:7_777] + [(ts, tu, zc, zl, d[:zc])] + recs[7_778:]), ["--fixcsum"])
 
 
 def test_record_like_payloads_fall_back_or_match(built):
@@ -164,7 +172,10 @@ def test_pipeline_device_index_edges(built):
     for i, r in enumerate(base):
         recs.append(r)
         if i % 97 == 0:
-            recs.append((1, i, i % 21, i % 21, bytes(i % 21)))
+            recs.append((1, i, 1 + i % 21, 1 + i % 21, bytes(1 + i % 21)))
+        if i % 89 == 5:
+            ts, tu, cl, ln, d = r
+            recs.append((ts, tu, cl, cl - 1 - i % 40, d))
         if i % 3001 == 0:
             recs.append(big[(i // 3001) % len(big)])
     args = ["--seed=3", "--fixcsum"]

@@ -266,6 +266,29 @@ def test_tcprewrite_gpus_counter_setup_failure_ends_cleanly(built, tmp_path):
     assert b"no device buffer for the counter all-reduce" in r.stderr
 
 
+@pytest.mark.gpu
+def test_tcprewrite_gpus_jnpr_seeding_failure_ends_cleanly(built, tmp_path):
+    """a shard whose Juniper decoder-state seeding fails: every shard folds that failure in
+    only after the exchange's barrier, so all agree to skip the edit and the all-reduce --
+    the job ends with the message, exit 255, no hang"""
+    import subprocess
+    import test_dlt_wireless as W
+    pcap, _ = W._jnpr_warn(600, seed=31, every=5, lead=4)
+    inp, out = tmp_path / "in.pcap", tmp_path / "out.pcap"
+    inp.write_bytes(pcap)
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tcpreplay_amd", "bin",
+                        "tcprewrite")
+    env = dict(os.environ, TCPREWRITE_GPUS_FAIL_JNPR="0")
+    r = subprocess.run([tool, "--gpus", "1", "-i", str(inp), "-o", str(out), "--dlt=enet", "--fixcsum"],
+                       capture_output=True, timeout=120, env=env)
+    assert r.returncode == 255
+    assert b"Juniper state seeding failed" in r.stderr
+    env.pop("TCPREWRITE_GPUS_FAIL_JNPR")
+    r = subprocess.run([tool, "--gpus", "1", "-i", str(inp), "-o", str(out), "--dlt=enet", "--fixcsum"],
+                       capture_output=True, timeout=120, env=env)
+    assert r.returncode == 0 and out.read_bytes() == O.rewrite(pcap, ["--dlt=enet", "--fixcsum"])[1]
+
+
 # ---------------------------------------------------------------- gloo world_size 2 (oracle-edited shards)
 @pytest.mark.parametrize("case", ["fixcsum", "c4_cache", "seed_imix", "fuzz_golden", "fuzz_imix"])
 def test_two_rank_rewrite_equals_single_process(built, case):

@@ -85,8 +85,10 @@ def test_fused_records_larger_than_a_window(built):
 
 
 def test_fused_chain_ends(built):
-    """a truncated last record, an oversize record (libpcap stops), a len > 262144 record
-    (the reference's error) and caplen-0 records: all taken by the exact path"""
+    """a truncated last record, an oversize record (libpcap stops), a len > 262144 record and
+    records with caplen 0, len 0 or both (safe_pcap_next's exit, src/common/utils.c:136-156:
+    the output ends before them, rc -1), and a len < caplen record (the reader trims its
+    caplen to len, utils.c:159-162): all taken by the exact path"""
     recs = S.records(S.pcap_fixed(20_000, 80, seed=12))
     pcap = S.build_pcap(recs)
     _run(pcap[:-30], ["--fixcsum"], fused=None)
@@ -96,8 +98,11 @@ def test_fused_chain_ends(built):
     _run(over, ["--fixcsum"], fused=False)
     err = S.build_pcap(recs[:9_999] + [(ts, tu, cl, 400_000, d)] + recs[10_000:])
     _run(err, ["--fixcsum"], fused=False)
-    zero = S.build_pcap(recs[:5000] + [(ts, tu, 0, 0, b"")] + recs[5000:])
-    _run(zero, ["--fixcsum"], fused=False)
+    for zc, zl in ((0, 0), (0, 80), (cl, 0)):
+        zero = S.build_pcap(recs[:5000] + [(ts, tu, zc, zl, d[:zc])] + recs[5000:])
+        _run(zero, ["--fixcsum"], fused=False)
+    trim = S.build_pcap(recs[:7000] + [(ts, tu, cl, cl - 9, d)] + recs[7000:])
+    _run(trim, ["--fixcsum"], fused=False)
 
 
 def test_fused_record_like_payloads(built):

@@ -219,3 +219,18 @@ def test_per_packet_api_reads_the_callers_buffer(built):
     finally:
         te.close()
     assert got == S.records(exp)
+
+
+def test_trimmed_records_bound_the_stale_extent(built):
+    """a len < caplen record is copied as len bytes (safe_pcap_next's trim, utils.c:159-162,
+    then tcprewrite.c:301): the stale bytes a later overstated IPv6 record reads are the
+    older record's past that, not the trimmed record's stored tail"""
+    ts, tu, cl, ln, d = S.records(S.pcap_fixed(1, 200, ipv6=True, proto=17, seed=3))[0]
+    v6 = _overstate([(ts, tu, cl, ln, d)], [0])[0]
+    big = S.records(S.pcap_fixed(1, 1200, seed=4))[0]
+    recs = []
+    for k in range(40):
+        keep = 120 + 7 * k
+        tail = big[4][:keep] + bytes([0xE0 + (k & 15)]) * (1200 - keep)
+        recs += [big, (ts, tu, 1200, keep, tail), v6]
+    _check(S.build_pcap(recs), ["--fixcsum"], min_stale=40)

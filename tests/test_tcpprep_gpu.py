@@ -20,18 +20,22 @@ def test_gpu_matches_reference_cache(name):
 
 def _adversarial(seed=7, copies=6):
     """test.pcap's records (VLAN, MPLS, EoMPLS, IPv6, ARP, 802.3, padded frames) plus
-    mutated copies: truncated captures (caplen 0..70), ethertypes flipped to
-    VLAN/QinQ/IPv6/IPv4, random IP header bytes and v6 next-header chains."""
+    mutated copies: truncated captures (caplen 1..70), len < caplen (the reader trims caplen
+    to len, src/common/utils.c:159-162), ethertypes flipped to VLAN/QinQ/IPv6/IPv4, random IP
+    header bytes and v6 next-header chains."""
     rng = np.random.default_rng(seed)
     base = synth.records(T.test_pcap())
     recs = list(base)
     for _ in range(copies):
         for ts, tu, cl, ln, data in base:
             d = bytearray(data)
-            k = rng.integers(0, 6)
+            k = rng.integers(0, 7)
             if k == 0 and cl:
-                cl = int(rng.integers(0, min(cl, 70) + 1))
+                cl = int(rng.integers(1, min(cl, 70) + 1))
                 d = d[:cl]
+            elif k == 6 and cl > 1:
+                recs.append((ts, tu, cl, int(rng.integers(1, cl)), bytes(d)))
+                continue
             elif k == 1 and cl >= 14:
                 d[12:14] = [(0x81, 0x00), (0x88, 0xa8), (0x86, 0xdd), (0x08, 0x00), (0x91, 0x00)][rng.integers(0, 5)]
             elif k == 2 and cl > 40:
@@ -101,7 +105,7 @@ def test_gpu_matches_oracle_adversarial(line):
 @pytest.mark.parametrize("mode", ["bridge", "client", "server", "first", "router"])
 def test_gpu_auto_matches_oracle_without_short_tcp(mode):
     """the adversarial corpus minus the truncations that make packet2tree abort"""
-    recs = [r for r in synth.records(_adversarial(seed=11)) if r[2] >= 74]
+    recs = [r for r in synth.records(_adversarial(seed=11)) if min(r[2], r[3]) >= 74]  # (as trimmed)
     pcap = synth.build_pcap(recs)
     got, exp = _both(pcap, [f"--auto={mode}"])
     assert got == exp and got != "error"
@@ -114,6 +118,23 @@ def test_gpu_auto_reports_len_error_like_the_reference():
     recs[3] = (0, 0, 40, 40, bytes(d))
     pcap = synth.build_pcap(recs)
     assert _both(pcap, ["--auto=bridge"]) == ("error", "error")
+
+
+@pytest.mark.parametrize("zc,zl", [(0, 0), (0, 60), (60, 0), (60, 300_000)])
+@pytest.mark.parametrize("args", [["--port"], ["--cidr=96.17.211.0/24", "--include=P:3-90"], ["--auto=bridge"],
+                                  ["--mac=00:1f:f3:3c:e1:13"]])
+def test_reader_exit_writes_no_cache(zc, zl, args):
+    """safe_pcap_next (tcpprep.c:353 -> src/common/utils.c:136-156) exit(-1)s at a record with
+    a zero len or caplen or len > MAX_SNAPLEN, before write_cache (tcpprep.c:194): no cache,
+    on the GPU as in the oracle -- and the records before it do not matter"""
+    recs = synth.records(T.test_pcap())
+    ts, tu, cl, ln, d = recs[50]
+    recs[50] = (ts, tu, zc, zl, d[:zc])
+    pcap = synth.build_pcap(recs)
+    with pytest.raises(ValueError):
+        oracle_lib.tcpprep(pcap, args)
+    with pytest.raises(RuntimeError, match="safe_pcap_next"):
+        TP.cache(pcap, args)
 
 
 def test_gpu_matches_oracle_full_size_imix():

@@ -106,6 +106,36 @@ def test_gpu_nanosecond_and_big_endian_input(built):
         assert TR.replay(pcap, ["--unique-ip", "--loop=3"]) == O.replay(pcap, ["--unique-ip", "--loop=3"])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["--unique-ip", "--loop=4"], ["--unique-ip", "--loop=3", "-K"], ["--loop=2"]],
+                         ids=["loop4", "preload", "no-unique"])
+def test_gpu_reader_rules_match_oracle(built, args):
+    """safe_pcap_next's rules (send_packets.c:955,985 -> src/common/utils.c:131-169): len <
+    caplen records are sent as len bytes; a zero len or caplen record ends the run after the
+    first pass's earlier records (tcpreplay_hip_reader_exited, geterr names it)"""
+    import ctypes
+    from tcpreplay_amd import tcpreplay as TR
+    lib = O.load()
+    lib.tcpreplay_oracle_exited.restype = ctypes.c_int
+    recs = S.records(_edge_pcap(400, seed=11))
+    for i in range(3, len(recs), 37):
+        ts, tu, cl, ln, d = recs[i]
+        recs[i] = (ts, tu, cl, max(1, cl - 1 - i % 30), d)
+    pcap = S.build_pcap(recs)
+    t = TR.TcpReplay(args)
+    try:
+        assert t.replay(pcap) == O.replay(pcap, args)
+        assert not t.reader_exited and lib.tcpreplay_oracle_exited() == 0
+        for zc, zl in ((0, 0), (0, 70), (70, 0)):
+            ts, tu, cl, ln, d = recs[250]
+            bad = S.build_pcap(recs[:250] + [(ts, tu, zc, zl, d[:zc])] + recs[251:])
+            got = t.replay(bad)
+            assert t.reader_exited and "safe_pcap_next" in t.geterr()
+            assert got == O.replay(bad, args) and lib.tcpreplay_oracle_exited() == 1
+    finally:
+        t.close()
+
+
 def test_unserved_options_are_refused(built):
     from tcpreplay_amd import tcpreplay as TR
     for bad in (["--unique-ip-loops=2"], ["--loop=0"], ["--mbps=10"], ["--unique-ip", "--unique-ip-loops=0"]):
