@@ -192,6 +192,32 @@ def _pcap_shards(pcap, parts):
     return [hdr + pcap[a:b] for a, b in zip(cuts, cuts[1:]) if b > a]
 
 
+def copy_floor(src_addr, n_in, dst_addr, n_out, reps=5):
+    """The box's PCIe floor for the end-to-end path: the capture up and its output down, one
+    hipMemcpyAsync each on two streams at once, from and to the same page-locked buffers the
+    pipelined run uses (median ms).  No edit can beat it; end_to_end.ms is read against it."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    din, dout, s1, s2 = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    if hip.hipMalloc(ctypes.byref(din), ctypes.c_size_t(n_in)) or hip.hipMalloc(ctypes.byref(dout),
+                                                                                 ctypes.c_size_t(n_out)):
+        return None
+    hip.hipStreamCreateWithFlags(ctypes.byref(s1), 1)
+    hip.hipStreamCreateWithFlags(ctypes.byref(s2), 1)
+    ts = []
+    for _ in range(reps + 1):
+        hip.hipDeviceSynchronize()
+        t0 = time.perf_counter()
+        hip.hipMemcpyAsync(din, ctypes.c_void_p(src_addr), ctypes.c_size_t(n_in), 1, s1)
+        hip.hipMemcpyAsync(ctypes.c_void_p(dst_addr), dout, ctypes.c_size_t(n_out), 2, s2)
+        hip.hipDeviceSynchronize()
+        ts.append(time.perf_counter() - t0)
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
+    hip.hipFree(din)
+    hip.hipFree(dout)
+    return sorted(ts[1:])[reps // 2] * 1e3
+
+
 def cpu_baseline(pcap, args, n_pkts, budget_s=10.0, threads=1):
     """The oracle (C restatement of tcpedit_packet) on the same workload: only the C call
     is timed, over preallocated buffers; with threads > 1 each thread rewrites its own
@@ -556,6 +582,8 @@ def main():
 
             p_s = e2e(pin_in.view, pin_out.view)
             g_s = e2e(src, bytearray(bound))
+            floor_ms = copy_floor(ctypes.addressof(ctypes.c_char.from_buffer(pin_in.view)), len(pcap),
+                                  ctypes.addressof(ctypes.c_char.from_buffer(pin_out.view)), len(out3))
             one = []
             for _ in range(3):
                 t1 = time.perf_counter()
@@ -574,6 +602,10 @@ def main():
                           "8-32 MiB; C/4 and C/2 first, halving last), H2D | window-mode edit (records found "
                           "on the device, chain verdict gathered on the device) | D2H on three streams -> "
                           "page-locked host output (median of 5)"),
+                copy_floor_ms=round(floor_ms, 3) if floor_ms else None,
+                frac_of_copy_floor=round(floor_ms / (p_s * 1e3), 4) if floor_ms else None,
+                copy_floor="this box's PCIe floor: the capture up and the output down at once, one copy each on "
+                           "two streams, same page-locked buffers, no edit (median of 5)",
                 pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 5)"),
                 one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
                                    "pageable copies (median of 3)"))

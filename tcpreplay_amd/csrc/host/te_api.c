@@ -2599,8 +2599,11 @@ static double te_now(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-/* page-locked host memory (hipHostMalloc) for callers that read a capture straight into
- * it: the pipelined rewrite then skips hipHostRegister for that buffer */
+/* page-locked host memory for callers that read a capture straight into it: the
+ * pipelined rewrite then skips hipHostRegister for that buffer */
+/* (hipHostMalloc puts the pages on the device's NUMA node; pages on the other node, or
+   malloc'd and hipHostRegister'ed, or the non-coherent and coherent flags measured the same
+   on MI355X boxes: profiles/r05_e2e_ab.txt) */
 void *tcpedit_host_alloc(size_t bytes)
 {
     void *p = NULL;
@@ -3260,6 +3263,8 @@ static int win_pipe_off(void)
    multiple of 16 bytes (the head copy moves 16-byte pieces) */
 static uint64_t *win_plan(size_t in_len, uint64_t C, uintptr_t addr, int *n_out)
 {
+    /* (chunk starts 256-byte aligned: 4 KiB and 64 KiB alignment measured the same,
+       profiles/r05_e2e_ab.txt) */
     const uint64_t MIN = (uint64_t)1 << 20, A = 256;
     const int cap = (int)((in_len / MIN) + 16);
     uint64_t *st = malloc(sizeof(uint64_t) * (size_t)cap);
@@ -3363,18 +3368,34 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         if (e && *e)
             ahead = atoi(e);
     }
+    /* TCPEDIT_HIP_PIPE_TIMELINE=1 (diagnostics): timing events per chunk -- upload start and
+       end, edit end, download start and end -- printed relative to the first upload */
+    enum { TL_H0, TL_H1, TL_E1, TL_D0, TL_D1, TL_N };
+    const int tl_on = getenv("TCPEDIT_HIP_PIPE_TIMELINE") != NULL && nch <= 64;
+    hipEvent_t tl[64][TL_N];
+    double tl_host[64];
+    if (tl_on)
+        for (int k = 0; k < nch; k++)
+            for (int e = 0; e < TL_N; e++)
+                HIPCHK(t, hipEventCreate(&tl[k][e]));
     for (int k = 0; k < nch; k++) {
         const int s = k % TE_PIPE_SLOTS, ps = (k + TE_PIPE_SLOTS - 1) % TE_PIPE_SLOTS;
         tcpedit_batch_t *b = P->slot[s], *pb = P->slot[ps];
         if (ahead > 0 && ahead < TE_PIPE_SLOTS && k >= ahead)
             HIPCHK(t, hipEventSynchronize(P->edit_done[(k - ahead) % TE_PIPE_SLOTS]));
+        if (tl_on)
+            tl_host[k] = te_now() - t0;
         const uint64_t f0 = cst[k], f1 = cst[k + 1];
         const uint64_t fe = f1 + TE_PIPE_WIN_MARGIN < in_len ? f1 + TE_PIPE_WIN_MARGIN : in_len;
         /* upload (the slot's last window kernel has read its input) */
         if (k >= TE_PIPE_SLOTS)
             HIPCHK(t, hipStreamWaitEvent(P->s_h2d, P->edit_done[s], 0));
+        if (tl_on)
+            HIPCHK(t, hipEventRecord(tl[k][TL_H0], P->s_h2d));
         HIPCHK(t, hipMemcpyAsync(b->d_in + ORG, img + f0, fe - f0, hipMemcpyHostToDevice, P->s_h2d));
         HIPCHK(t, hipEventRecord(P->h2d_done[s], P->s_h2d));
+        if (tl_on)
+            HIPCHK(t, hipEventRecord(tl[k][TL_H1], P->s_h2d));
         b->in_len = ORG + (fe - f0);
         b->n_tiles = 0;
         b->rec0 = b->out_base = ORG; /* records keep their image offsets */
@@ -3406,10 +3427,16 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             goto fail;
         }
         HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
+        if (tl_on)
+            HIPCHK(t, hipEventRecord(tl[k][TL_E1], t->stream));
         if (!zc) { /* the chunk's file range down, behind its edit */
             HIPCHK(t, hipStreamWaitEvent(P->s_d2h, P->edit_done[s], 0));
+            if (tl_on)
+                HIPCHK(t, hipEventRecord(tl[k][TL_D0], P->s_d2h));
             HIPCHK(t, hipMemcpyAsync(dst + f0, b->d_out + ORG, f1 - f0, hipMemcpyDeviceToHost, P->s_d2h));
             HIPCHK(t, hipEventRecord(P->d2h_done[s], P->s_d2h));
+            if (tl_on)
+                HIPCHK(t, hipEventRecord(tl[k][TL_D1], P->s_d2h));
         }
         last = s;
     }
@@ -3424,6 +3451,20 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     if (trace)
         fprintf(stderr, "pipe (window mode%s): %d chunks, %.3f ms, verdict %llu\n", zc ? ", output over PCIe" : "",
                 nch, (te_now() - t0) * 1e3, (unsigned long long)P->h_wacc[3]);
+    if (tl_on) {
+        for (int k = 0; k < nch; k++) {
+            float v[TL_N] = {0};
+            for (int e = 0; e < TL_N; e++)
+                if (!zc || e < TL_D0)
+                    (void)hipEventElapsedTime(&v[e], tl[0][TL_H0], tl[k][e]);
+            fprintf(stderr, "tl chunk %2d %6.2f MiB: host %.3f | up %.3f-%.3f | edit end %.3f | down %.3f-%.3f ms\n",
+                    k, (cst[k + 1] - cst[k]) / 1048576.0, tl_host[k] * 1e3, v[TL_H0], v[TL_H1], v[TL_E1], v[TL_D0],
+                    v[TL_D1]);
+        }
+        for (int k = 0; k < nch; k++)
+            for (int e = 0; e < TL_N; e++)
+                hipEventDestroy(tl[k][e]);
+    }
     {
         const uint64_t *acc = P->h_wacc;
         const uint64_t f0 = cst[nch - 1];
