@@ -570,18 +570,20 @@ def main():
             pin_in, pin_out = TA.PinnedBuffer(len(pcap)), TA.PinnedBuffer(bound)
             pin_in.view[:] = pcap
 
-            def e2e(si, so, reps=5):
-                ts = []
+            def e2e(kinds, reps=9):
+                """median seconds per buffer kind; the kinds' runs interleaved, so a slow spell
+                of the box's copies (seen for seconds at a time: DESIGN 6) hits them alike"""
+                ts = [[] for _ in kinds]
                 for _ in range(reps):
-                    t1 = time.perf_counter()
-                    rc, view = te3.rewrite_pipelined(si, out=so)
-                    ts.append(time.perf_counter() - t1)
-                    if rc != 0 or view != out3:
-                        raise RuntimeError("pipelined end-to-end run differs from its first run")
-                return sorted(ts)[reps // 2]
+                    for i, (si, so) in enumerate(kinds):
+                        t1 = time.perf_counter()
+                        rc, view = te3.rewrite_pipelined(si, out=so)
+                        ts[i].append(time.perf_counter() - t1)
+                        if rc != 0 or view != out3:
+                            raise RuntimeError("pipelined end-to-end run differs from its first run")
+                return [sorted(t)[reps // 2] for t in ts]
 
-            p_s = e2e(pin_in.view, pin_out.view)
-            g_s = e2e(src, bytearray(bound))
+            p_s, g_s = e2e([(pin_in.view, pin_out.view), (src, bytearray(bound))])
             floor_ms = copy_floor(ctypes.addressof(ctypes.c_char.from_buffer(pin_in.view)), len(pcap),
                                   ctypes.addressof(ctypes.c_char.from_buffer(pin_out.view)), len(out3))
             one = []
@@ -601,12 +603,12 @@ def main():
                 rate(p_s, "page-locked host capture -> byte-range chunks (the default: a tenth of the capture, "
                           "8-32 MiB; C/4 and C/2 first, halving last), H2D | window-mode edit (records found "
                           "on the device, chain verdict gathered on the device) | D2H on three streams -> "
-                          "page-locked host output (median of 5)"),
+                          "page-locked host output (median of 9, interleaved with the pageable runs)"),
                 copy_floor_ms=round(floor_ms, 3) if floor_ms else None,
                 frac_of_copy_floor=round(floor_ms / (p_s * 1e3), 4) if floor_ms else None,
                 copy_floor="this box's PCIe floor: the capture up and the output down at once, one copy each on "
                            "two streams, same page-locked buffers, no edit (median of 5)",
-                pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 5)"),
+                pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 9)"),
                 one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
                                    "pageable copies (median of 3)"))
         if not opt.no_cpu_baseline and opt.workload not in CACHED:
