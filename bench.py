@@ -6,8 +6,8 @@ BASELINE configs[1]: `--seed=42 --fixcsum` over 1M x 64 B synthetic UDP
 records.  A "step" is one pass of the whole device pipeline (one kernel:
 parse + edit + checksum + scan + compaction) over that batch, inputs already
 resident in HBM.  With --gpus N (one process per GPU, torch.distributed over
-RCCL) every rank rewrites its own 10M-record shard (HBM-resident; N = 1's
-`c2x10` side line is the same per-GPU workload) -- packets are independent, so
+RCCL) every rank rewrites its own shard of the N = 1 workload (1M x 64 B: weak
+scaling, like with like) -- packets are independent, so
 there is no data-path collective, only one all-reduce of the counters per job
 -- and `value` is the aggregate packets/s over the max-over-ranks time; a
 `strong_c4` side line runs BASELINE configs[3] (100M records split over the
@@ -68,7 +68,10 @@ WORKLOADS = {
             "--mtu=1000 --mtu-trunc --fixcsum on IMIX 64/570/1514 7:4:1 (1514 B records cut to 1014 B: "
             "per-record sizes; wave lane, tiles at the predicted cuts' prefix)"),
 }
-PER_RANK_PACKETS = {"c2": 10_000_000}  # N > 1 per-rank shard (HBM-resident)
+# every rank's share at N > 1: the N = 1 workload itself (BASELINE configs[1]'s 1M x 64 B
+# for c2), so the driver's 1/2/4/8 curve weak-scales like with like; the
+# HBM-resident 10M-record form is the c2x10 side line (--packets 10000000 at any N)
+PER_RANK_PACKETS = {}
 DEFAULT_PACKETS = {"c2": 1_000_000, "c3": 10_000_000, "c5": 1_000_000, "c4": 12_500_000, "c2x10": 10_000_000,
                    "fz": 10_000_000, "seed": 1_000_000, "hdr": 4_000_000, "vdel": 4_000_000, "efcs": 4_000_000, "macseed": 4_000_000,
                    "mtu": 4_000_000}
@@ -352,10 +355,8 @@ def main():
                                                verify=not opt.no_verify and n <= STRONG_VERIFY_MAX)
         del share
     else:
-        # N = 1: BASELINE configs[1] (1M x 64 B).  N > 1: every rank weak-scales a
-        # 10M-record shard of the same config (1.6 GB moved per pass, so the curve measures
-        # HBM, not the 256 MiB Infinity Cache a 1M shard sits in; N = 1's c2x10 side line
-        # is the same per-GPU workload)
+        # N = 1: BASELINE configs[1] (1M x 64 B); N > 1: every rank the same 1M-record
+        # workload (weak scaling, like with like)
         n = opt.packets or (PER_RANK_PACKETS.get(opt.workload, DEFAULT_PACKETS[opt.workload]) if world > 1
                             else DEFAULT_PACKETS[opt.workload])
         te, b, r, pcap, checked = run_workload(opt.workload, n, opt.steps, opt.warmup, seed=1 + rank,
