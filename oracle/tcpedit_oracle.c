@@ -1978,24 +1978,42 @@ static int user_encode(const ocfg_t *c, const ostate_t *s, uint8_t *packet, int 
 }
 
 /* dlt_hdlc_encode: plugins/dlt_hdlc/hdlc.c:223-290 -- a 4-byte Cisco HDLC header
- * {address, control, protocol}; an Ethernet decode leaves no HDLC fields to fall back on */
+ * {address, control, protocol}.  Without --hdlc-address / --hdlc-control the fields come
+ * from `extra->hdlc` (:273, :283): the first int of the context's decoded extra, which no
+ * decoder writes as such -- the en10mb decoder's extra begins with its `vlan` flag (1 for
+ * a tagged frame, en10mb_types.h:30, en10mb.c:452,466), every other decoder's extra is
+ * zeroed and never written there (the HDLC decoder sets only address/control, :212-213).
+ * A 0 fails the encode after the memmove (and after the address, when only the control is
+ * missing): tcpedit.c:104-108 then writes the record as that left it, a soft error. */
 static int hdlc_encode(const ocfg_t *c, const ostate_t *s, uint8_t *packet, int pktlen)
 {
     if (pktlen < 4)
         return TCPEDIT_ERROR;
-    if (s->l2len != 4)
+    /* :237-238: after a whole Juniper inner decode the context's decoded extra is the en10mb
+       sub-decoder's (dlt_utils.c:262-263), smaller than an hdlc_extra_t: an error before
+       anything moves */
+    if (c->decoder == DEC_JNPR && s->jnpr_sub)
+        return TCPEDIT_ERROR;
+    if (s->l2len != 4) /* :241-248 (the l2len < 4 copy writes past pktlen, into the buffer) */
         memmove(packet + 4, packet + s->l2len, (size_t)(pktlen - s->l2len));
     const int newpktlen = pktlen + 4 - s->l2len;
-    if (c->hdlc_address >= 65535) {
+    const int fb = c->decoder == DEC_EN10MB ? s->vlan : 0; /* extra->hdlc */
+    if (c->hdlc_address < 65535)
+        packet[0] = (uint8_t)c->hdlc_address;
+    else if (fb)
+        packet[0] = (uint8_t)fb;
+    else {
         seterr("Non-HDLC packet requires --hdlc-address");
         return TCPEDIT_ERROR;
     }
-    packet[0] = (uint8_t)c->hdlc_address;
-    if (c->hdlc_control >= 65535) {
+    if (c->hdlc_control < 65535)
+        packet[1] = (uint8_t)c->hdlc_control;
+    else if (fb)
+        packet[1] = (uint8_t)fb;
+    else {
         seterr("Non-HDLC packet requires --hdlc-control");
         return TCPEDIT_ERROR;
     }
-    packet[1] = (uint8_t)c->hdlc_control;
     st16(packet + 2, (uint16_t)s->proto); /* hdlc->protocol = ctx->proto */
     return newpktlen;
 }

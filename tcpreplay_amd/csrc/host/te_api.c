@@ -194,7 +194,8 @@ static int l2_growth(const te_dev_cfg_t *c)
     const int dl = te_decoder_l2len(c->decoder);
     return c->encoder == TE_ENC_USER                                     ? c->user_length - dl
            : c->encoder == TE_ENC_HDLC                                   ? 4 - dl
-           : c->encoder == TE_ENC_EN10MB && c->decoder != TE_DEC_EN10MB ? 14 - dl /* another DLT -> Ethernet */
+           : c->encoder == TE_ENC_EN10MB && c->decoder != TE_DEC_EN10MB
+               ? (c->vlan == TE_VLAN_ADD ? 18 : 14) - dl /* another DLT -> Ethernet (en10mb.c:545-549) */
                                                                          : 0;
 }
 static uint32_t rec_growth(const te_dev_cfg_t *c)
@@ -1386,7 +1387,8 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.rec0 = b->rec0 ? b->rec0 : 24;
     /* VLAN add as the only size change: every record grows by 4 bytes or is a hard error
        (dlt_en10mb_encode, en10mb.c:520-575), so outputs sit at input offset + 4 x index */
-    L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
+    L.static_grow = b->slot_layout && c->vlan == TE_VLAN_ADD && c->encoder == TE_ENC_EN10MB &&
+                    c->decoder == TE_DEC_EN10MB && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
                     !c->mtu_truncate && !c->skip_soft_errors && !b->has_trim && !c->fuzz_seed &&
                     !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never && !grow_off_env();
     /* a VLAN pop or --efcs as the only size change: outputs at input offset - 4 x index

@@ -616,21 +616,13 @@ int te_check_decoder_cfg(tcpedit_t *t, int s2c)
     const int eth_addr = c->decoder == TE_DEC_EN10MB || TE_DEC_ETH_ADDR(c->decoder);
     c->l2carry = TE_DEC_ETH_ADDR(c->decoder) && c->encoder == TE_ENC_EN10MB &&
                  !(c->mac_mask & TE_MASK_DMAC1);
-    if (foreign && c->encoder == TE_ENC_EN10MB) {
-        if (c->vlan == TE_VLAN_ADD) {
-            /* en10mb.c:696-715 writes the tag at the never-set vlan_offset 0 of another decoder */
-            te_seterr(t, "--enet-vlan=add on DLT %d input is not served by this build", t->dlt);
-            return -1;
-        }
-        /* en10mb.c:592-659: a decoder without Ethernet addresses needs both MACs, or every
-           packet fails after the encoder's memmove (written half-moved): not served */
-        const int need = TE_MASK_SMAC1 | TE_MASK_DMAC1 | (s2c ? TE_MASK_SMAC2 | TE_MASK_DMAC2 : 0);
-        if (!eth_addr && (c->mac_mask & need) != need) {
-            te_seterr(t, "DLT %d input into --dlt=enet needs --enet-smac and --enet-dmac%s", t->dlt,
-                      s2c ? " for both directions" : "");
-            return -1;
-        }
-    }
+    /* (served: --enet-vlan=add behind another decoder -- the tag lands at the decoder extra's
+       never-set vlan_offset 0, en10mb.c:696-715 -- and a decoder without Ethernet addresses
+       into --dlt=enet without both MACs -- every packet fails after the encoder's memmove and
+       is written half-moved, en10mb.c:567-619: edit_pkt.hpp en10mb_encode_foreign) */
+    (void)foreign;
+    (void)eth_addr;
+    (void)s2c;
     /* --fuzz-seed behind any decoder and into any encoder: a fuzzed record goes back to
        `again:` and is decoded by the input decoder and encoded a second time (tcpedit.c:89,
        250-258); the slot headroom holds both encodes (te_slot_head).  Not served: the
@@ -950,14 +942,9 @@ int te_derive_cfg(tcpedit_t *t)
             return -1;
         }
     }
-    if (c->encoder == TE_ENC_HDLC && (!t->have[OPT_HDLC_ADDRESS] || !t->have[OPT_HDLC_CONTROL]) &&
-        te_decoder_l2len(c->decoder) != 4) {
-        /* dlt_hdlc_encode (hdlc.c:270-288) fails every packet without them (no decoder marks
-           the HDLC extra filled), after its memmove: the reference writes those soft errors
-           half-moved.  A 4-byte decoded header is not moved (its packets fail cleanly). */
-        te_seterr(t, "--dlt=hdlc needs --hdlc-address and --hdlc-control for this input");
-        return -1;
-    }
+    /* (without --hdlc-address / --hdlc-control dlt_hdlc_encode falls back on the decoded
+       extra's first int, hdlc.c:270-288: a tagged Ethernet frame's vlan flag, else a soft
+       error written as its memmove left it -- served on the device, edit_pkt.hpp hdlc_encode) */
     { /* dlt_hdlc_parse_opts (hdlc.c:156-180) */
         long v;
         if (t->have[OPT_HDLC_CONTROL]) {

@@ -116,6 +116,9 @@ struct Dec {  // tcpeditdlt_t + en10mb_extra_t fields the encode/merge steps rea
     u32 vlan_offset;
     u16 vlan_tag, vlan_pri, vlan_cfi, vlan_proto;
     bool dst_modified;   // en10mb_extra_t.dst_modified (read by the multicast MAC update)
+    // DLT_JUNIPER_ETHER: the context's decoded extra is the en10mb sub-decoder's (a whole
+    // inner decode copied it in, dlt_utils.c:262-263) -- too small for dlt_hdlc_encode
+    bool jsub = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -1180,6 +1183,7 @@ DI int foreign_decode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
             // addresses and proto, the sub-decoder's extra by pointer)
             if (pk.jc) {
                 const te_jstate_t &c = *pk.jc;
+                s.jsub = true;
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
                     s.dstaddr[i] = c.dstaddr[i];
@@ -1212,6 +1216,8 @@ DI int foreign_decode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
         // the first whole decode makes the sub-decoder's extra the encoder's: a fresh
         // dst_modified (en10mb_decode never writes it)
         if (pk.jnone) t.dst_modified = false;
+        t.jsub = true;
+        t.proto_vlan_tag = s.proto_vlan_tag;  // (the sub-context's: not copied, dlt_utils.c:254-263)
         s = t;
         return RC_OK;
     }
@@ -1280,6 +1286,7 @@ DI void en10mb_mac_rules(const te_dev_cfg_t &cfg, u8 *dh, u8 *sh) {
 }
 
 DI bool l2_replace(Pkt &pk, int l2len, int n);
+DI void l2_half_move(Pkt &pk, int oldl2, int newl2, int pktlen);
 
 // dlt_en10mb_encode for another decoder (en10mb.c:544-548 and on): a 14-byte Ethernet
 // header replaces the decoded one (the host refuses VLAN add here, and the configs where
@@ -1289,22 +1296,42 @@ DI bool l2_replace(Pkt &pk, int l2len, int n);
 // --enet-dmac sets dst_modified (its old first 6 bytes against that zero destination).
 DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktlen, int dir) {
     if (pktlen < 14) return RC_ERROR;
-    if (pktlen + 14 - s.l2len > MAXPACKET) return RC_ERROR;
+    // :518-521 (before anything moves): a tag to push, or the decoder's tagged frame
+    if (cfg.vlan == TE_VLAN_ADD && !s.vlan && cfg.vlan_tag == 65535) return RC_ERROR;
+    const int newl2 = cfg.vlan == TE_VLAN_ADD ? 18 : 14;  // :545-549
+    if (pktlen < newl2 || pktlen + newl2 - s.l2len > MAXPACKET) return RC_ERROR;
     if (pktlen < s.l2len) return RC_ERROR;
     if (dir != TE_DIR_C2S && dir != TE_DIR_S2C) return RC_ERROR;
     const bool eth_addr = TE_DEC_ETH_ADDR(cfg.decoder);
     const bool c2s = dir == TE_DIR_C2S;
     const int sm = c2s ? TE_MASK_SMAC1 : TE_MASK_SMAC2, dm = c2s ? TE_MASK_DMAC1 : TE_MASK_DMAC2;
-    if (!eth_addr && (!(cfg.mac_mask & sm) || !(cfg.mac_mask & dm))) return RC_ERROR;
+    const u8 *smac = c2s ? cfg.intf1_smac : cfg.intf2_smac;
+    const u8 *dmac = c2s ? cfg.intf1_dmac : cfg.intf2_dmac;
+    if (!eth_addr && (!(cfg.mac_mask & sm) || !(cfg.mac_mask & dm))) {
+        // no address to fall back on (:599-602, :616-619): an error after the memmove, the
+        // source address written first when only the destination is missing
+        l2_half_move(pk, s.l2len, newl2, pktlen);
+        if (cfg.mac_mask & sm)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) pk.d[6 + i] = smac[i];
+        return RC_ERROR;
+    }
     bool old_nz = false;  // memcmp(eth->ether_dhost, ctx->dstaddr, 6) before the writes
 #pragma unroll
     for (int i = 0; i < 6; ++i) old_nz |= pk.d[i] != s.dstaddr[i];
-    if (!l2_replace(pk, s.l2len, 14)) return RC_ERROR;
-    pktlen += 14 - s.l2len;
+    // a VLAN push's bytes [14, 18) are the packet's before the memmove (:577 writes from
+    // byte 18 on; pktlen >= 18 here) unless the tag lands there
+    u8 pre[4];
+    if (cfg.vlan == TE_VLAN_ADD)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pre[i] = pk.d[14 + i];
+    if (!l2_replace(pk, s.l2len, newl2)) return RC_ERROR;
+    if (cfg.vlan == TE_VLAN_ADD)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk.d[14 + i] = pre[i];
+    pktlen += newl2 - s.l2len;
     u8 *dh = pk.d, *sh = pk.d + 6;
     const bool l2skip = cfg.l2_skip_broadcast;
-    const u8 *smac = c2s ? cfg.intf1_smac : cfg.intf2_smac;
-    const u8 *dmac = c2s ? cfg.intf1_dmac : cfg.intf2_dmac;
     const bool use_s = (cfg.mac_mask & sm) && (!eth_addr || !l2skip || is_unicast_ethernet(s.srcaddr));
     const bool use_d = (cfg.mac_mask & dm) && (!eth_addr || !l2skip || is_unicast_ethernet(s.dstaddr));
 #pragma unroll
@@ -1314,17 +1341,26 @@ DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktle
     }
     if (c2s && !(cfg.mac_mask & dm)) s.dst_modified = old_nz;
     en10mb_mac_rules(cfg, dh, sh);
-    st16(pk.d + 12, (u16)s.proto);
-    // the VLAN fields of the decoder's extra: zero (never set) but for the Juniper decoder,
-    // whose inner frame's en10mb decode filled them (en10mb.c:696-732)
-    if (cfg.vlan == TE_VLAN_OFF && s.vlan) {  // the TCI written at the inner frame's tag offset
-        if ((int)s.vlan_offset + 2 > pktlen) {
+    if (newl2 == 14) st16(pk.d + 12, (u16)s.proto);  // :691-694
+    // the VLAN fields of the decoder's extra (en10mb.c:696-732): zero (never set) but for the
+    // Juniper decoder, whose inner frame's en10mb decode filled them -- so behind any other
+    // decoder a pushed tag's {TCI, inner type} land at byte 0, over the destination address,
+    // and the inner type is the context's never-set proto_vlan_tag: 0
+    if (cfg.vlan == TE_VLAN_ADD || (cfg.vlan == TE_VLAN_OFF && s.vlan)) {
+        if ((int)s.vlan_offset + (cfg.vlan == TE_VLAN_ADD ? 4 : 2) > pktlen) {
             stale(pk, (int)NEED_NEVER);  // (past the new frame: the static buffer)
         } else {
             u8 *vh = pk.d + s.vlan_offset;
-            st16(vh, bswap16((u16)((cfg.vlan_tag < 65535 ? (u16)cfg.vlan_tag & 0x0fff : s.vlan_tag))));
-            st16(vh, (u16)(ld16(vh) + bswap16(cfg.vlan_pri < 255 ? (u16)(cfg.vlan_pri << 13) : s.vlan_pri)));
-            st16(vh, (u16)(ld16(vh) + bswap16(cfg.vlan_cfi < 255 ? (u16)(cfg.vlan_cfi << 12) : s.vlan_cfi)));
+            if (cfg.vlan == TE_VLAN_ADD) {
+                st16(pk.d + 12, bswap16((u16)cfg.vlan_proto));
+                st16(vh + 2, bswap16((u16)s.proto_vlan_tag));
+            }
+            if (cfg.vlan_tag < 65535) st16(vh, bswap16((u16)cfg.vlan_tag & 0x0fff));
+            else if (s.vlan) st16(vh, bswap16(s.vlan_tag));
+            if (cfg.vlan_pri < 255) st16(vh, (u16)(ld16(vh) + bswap16((u16)(cfg.vlan_pri << 13))));
+            else if (s.vlan) st16(vh, (u16)(ld16(vh) + bswap16(s.vlan_pri)));
+            if (cfg.vlan_cfi < 255) st16(vh, (u16)(ld16(vh) + bswap16((u16)(cfg.vlan_cfi << 12))));
+            else if (s.vlan) st16(vh, (u16)(ld16(vh) + bswap16(s.vlan_cfi)));
         }
     } else if (cfg.vlan == TE_VLAN_DEL) {
         st16(pk.d + 12, bswap16((u16)s.vlan_proto));  // htons(extra->vlan_proto)
@@ -1464,17 +1500,43 @@ DI int user_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen, i
     return pktlen + n - s.l2len;
 }
 
-// dlt_hdlc_encode (plugins/dlt_hdlc/hdlc.c:223-290): {address, control, protocol}; no
-// decoder marks its HDLC extra filled, so without --hdlc-address and --hdlc-control the
-// reference fails every packet (the host refuses that unless the decoded L2 is 4 bytes)
+// An encoder's memmove that a later step of the same encode fails (dlt_hdlc_encode,
+// hdlc.c:240-248 then :276/:286; dlt_en10mb_encode from another DLT, en10mb.c:567-578 then
+// :600/:617/:634/:650): the payload at byte oldl2 moved to byte newl2 in place, the caplen
+// unchanged -- the soft error writes the record so (tcpedit.c:104-108).  A move to a later
+// byte also pushes the payload's last newl2 - oldl2 bytes past the record, into the buffer
+// (written where the slot has room: only a later stale read would see them).
+DI void l2_half_move(Pkt &pk, int oldl2, int newl2, int pktlen) {
+    u8 *d = pk.d;
+    if (oldl2 > newl2) {
+        for (int i = newl2; i < pktlen - oldl2 + newl2; ++i) d[i] = d[i + oldl2 - newl2];
+    } else if (oldl2 < newl2) {
+        const int sh = newl2 - oldl2, end = pktlen + sh <= (int)pk.avail ? pktlen + sh : pktlen;
+        for (int i = end - 1; i >= newl2; --i) d[i] = d[i - sh];
+        if (end > (int)pk.ext) pk.ext = (u32)end;
+    }
+}
+
+// dlt_hdlc_encode (plugins/dlt_hdlc/hdlc.c:223-290): {address, control, protocol}.
+// Without --hdlc-address / --hdlc-control a field comes from `extra->hdlc` (:273, :283),
+// the first int of the context's decoded extra: the en10mb decoder's `vlan` flag (1 for a
+// tagged frame, en10mb_types.h:30), 0 behind every other decoder (zeroed, never written
+// there); a 0 fails the encode after the memmove (l2_half_move)
 DI int hdlc_encode(Pkt &pk, const te_dev_cfg_t &cfg, const Dec &s, int pktlen) {
     if (pktlen < 4) return RC_ERROR;
+    // :237-238: behind a whole Juniper inner decode the decoded extra is too small
+    if (s.jsub) return RC_ERROR;
+    const int fb = cfg.decoder == TE_DEC_EN10MB ? s.vlan : 0;
+    const bool aok = cfg.hdlc_address < 65535 || fb, cok = cfg.hdlc_control < 65535 || fb;
+    const int addr = cfg.hdlc_address < 65535 ? (int)(u8)cfg.hdlc_address : (int)(u8)fb;
+    if (!aok || !cok) {  // (the address byte goes in before the control field fails)
+        l2_half_move(pk, s.l2len, 4, pktlen);
+        if (aok) pk.d[0] = (u8)addr;
+        return RC_ERROR;
+    }
     if (!l2_replace(pk, s.l2len, 4)) return RC_ERROR;
-    // no option and no filled HDLC extra: an error (the host refuses it where the
-    // reference's memmove above would have moved the packet first)
-    if (cfg.hdlc_address >= 65535 || cfg.hdlc_control >= 65535) return RC_ERROR;
-    pk.d[0] = (u8)cfg.hdlc_address;
-    pk.d[1] = (u8)cfg.hdlc_control;
+    pk.d[0] = (u8)addr;
+    pk.d[1] = cfg.hdlc_control < 65535 ? (u8)cfg.hdlc_control : (u8)fb;
     st16(pk.d + 2, (u16)s.proto);  // hdlc->protocol = ctx->proto
     return pktlen + 4 - s.l2len;
 }

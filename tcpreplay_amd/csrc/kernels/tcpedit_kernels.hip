@@ -25,6 +25,7 @@
 #include "edit_pkt.hpp"
 #include "te_kernels.h"
 #include "te_window.hpp"
+#include "wave_dpp.hpp"
 
 using namespace te;
 
@@ -1355,18 +1356,6 @@ static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES
 #define WK_STAMP(i)
 #endif
 
-// OR over the wave's 64 lanes, in VALU: DPP row shifts leave each 16-lane row's OR in
-// its lane 15, and four readlanes combine the rows (__shfl_xor would be six dependent
-// ds_bpermute round trips through the LDS pipe)
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
-    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
-    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 15) | __builtin_amdgcn_readlane((int)v, 31) |
-                      __builtin_amdgcn_readlane((int)v, 47) | __builtin_amdgcn_readlane((int)v, 63));
-}
-
 __device__ __forceinline__ bool wk_solo(const te_tile_t &tl, uint32_t tb) {
     // (the last test: a span the image cannot hold never reaches the lane, whatever the cut)
     return (tl.flags & TE_TILE_SOLO) != 0 || tl.scratch_off != TE_NO_SCRATCH ||
@@ -1411,32 +1400,8 @@ __device__ __forceinline__ void hdr_put(uint8_t *S, uint32_t h, uint32_t v) {
     }
 }
 
-// inclusive scans over the wave's 64 lanes in VALU: DPP row shifts scan each 16-lane row,
-// two row broadcasts carry the rows' totals on (GFX9 DPP; __shfl_up would be six
-// ds_bpermute round trips through the LDS pipe)
-__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
-    return v;
-}
-// the previous lane's value (0 in lane 0): DPP wave_shr:1
-__device__ __forceinline__ uint32_t wave_prev(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, true);
-}
-
+// inclusive wave scans and the previous lane's value: wave_dpp.hpp (call them where every
+// lane of the wave is active -- tests/test_dpp.py)
 // Size-changing stores (GROW: a 4-byte tag pushed into every record; SHRINK: 4 bytes
 // dropped from every record).  Record j's change sits at tile-relative input offset D_j,
 // and consecutive changes are >= 58 bytes apart, so a 16-byte output chunk meets at most
@@ -1602,6 +1567,9 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
     gout[q] = img[(uint32_t)(q - OS)];
 }
 
+#ifndef WK_MTU_PREV_DPP
+#define WK_MTU_PREV_DPP 0
+#endif
 // --mtu-trunc stores (SZ_MTU).  Record j keeps its first 16 + caplen'_j bytes; the records
 // sit back to back from the tile's output offset OS, record j at tile-relative output
 // offset op_j (a wave scan of the kept sizes) and input offset rel_j.  Per output chunk the
@@ -1618,6 +1586,9 @@ template <int NK>
 __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
                                              uint32_t out_len, uint32_t npkt, uint32_t my_rel, uint32_t my_op,
                                              bool on, int lane, bool stream) {
+#if WK_MTU_PREV_DPP == 5
+    const uint32_t prel_e = wave_prev(my_rel), pop_e = wave_prev(my_op);
+#endif
     const uint64_t C0 = (OS + 15) & ~15ull;
     const uint32_t o0 = (uint32_t)(C0 - OS);
     const uint32_t nfull = (out_len - o0) >> 4;  // >= 2: a record here is >= 50 bytes
@@ -1667,9 +1638,29 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
         if ((kv[k] >> 15) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
     {  // pass 2: the chunk record j starts inside of (the previous record's {rel, op} from T:
        // taken with wave_prev DPP shifts instead, the first bytes came from the wrong place)
-        const uint32_t ep = T[lane > 0 ? lane - 1 : 0], prel = ep & 0xffffu, pop = ep >> 16;
+#if WK_MTU_PREV_DPP == 1  // (diagnostic variants: the previous record's {rel, op} by wave_prev, every lane)
+        const uint32_t prel = wave_prev(my_rel), pop = wave_prev(my_op);
+#elif WK_MTU_PREV_DPP == 3  // (... with wait states before the DPP reads)
+        asm volatile("s_nop 7\n s_nop 7" ::: "memory");
+        const uint32_t prel = wave_prev(my_rel), pop = wave_prev(my_op);
+#elif WK_MTU_PREV_DPP == 4  // (... through ds_bpermute instead of DPP)
+        const uint32_t prel = (uint32_t)__shfl_up((int)my_rel, 1), pop = (uint32_t)__shfl_up((int)my_op, 1);
+#elif WK_MTU_PREV_DPP == 5  // (... taken on entry, before the chunk map)
+        const uint32_t prel = prel_e, pop = pop_e;
+#else
+        const uint32_t ep = T[lane > 0 ? lane - 1 : 0], prel0 = ep & 0xffffu, pop0 = ep >> 16;
+#endif
         const uint32_t q = o0 + 16u * c1;
         const bool p2 = t1 != 0 && c1 < nfull;  // (lane 0, off lanes: x = 16, so t1 = 0)
+#if WK_MTU_PREV_DPP == 2  // (... or by wave_prev in the lanes that store a pass-2 chunk only)
+        uint32_t prel = 0, pop = 0;
+        if (p2) {
+            prel = wave_prev(my_rel);
+            pop = wave_prev(my_op);
+        }
+#elif WK_MTU_PREV_DPP == 0
+        const uint32_t prel = prel0, pop = pop0;
+#endif
         // (the lanes that store nothing read the image start: every address stays in it)
         const uint4 va = read16(S, p2 ? ib + prel + (q - pop) : ib);
         const uint4 vb = read16(S, p2 ? ib + my_rel - t1 : ib);

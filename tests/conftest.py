@@ -19,4 +19,5 @@ def built():
     import subprocess
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tcpreplay_amd", "csrc")])
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "dpp")])
     return True

@@ -95,13 +95,65 @@ def test_oracle_cooked_source_address_and_zero_destination(built):
 
 def test_unserved_combinations_are_refused(built):
     te = TA.TcpEdit
-    for dlt, args in [(12, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
-                      (12, ["--dlt=enet"]), (0, ["--dlt=enet", "--enet-smac=00:11:22:33:44:55"]),
-                      (113, ["--fuzz-seed=3", "--dlt=enet"]), (113, ["--dlt=hdlc"]), (1, ["--dlt=tokenring"])]:
+    for dlt, args in [(113, ["--fuzz-seed=3", "--dlt=enet"]), (1, ["--dlt=tokenring"])]:
         with pytest.raises(Exception):
             te(args, dlt=dlt)
     with pytest.raises(Exception):
         te(["--fixcsum"], dlt=9)  # DLT_PPP: the reference has no plugin for it either
+
+
+@pytest.mark.parametrize("kind", ["raw", "null", "ppp", "chdlc"])
+def test_oracle_failing_encodes_write_the_half_moved_record(built, kind):
+    """decoders without Ethernet addresses: --dlt=enet without --enet-dmac fails every packet
+    after the encoder's memmove of the payload from the decoded l2len to byte 14 (en10mb.c:
+    567-578) and after the source address (:586-619); --dlt=hdlc without its fields after the
+    memmove to byte 4 (hdlc.c:240-288).  The soft error writes the record as that left it,
+    its caplen unchanged (tcpedit.c:104-108); a record the decoder refuses is written as read"""
+    pcap = S.reframe(_base(300, seed=31), kind, odd_every=7)
+    hl = {"raw": 0, "null": 4, "ppp": 4, "chdlc": 4}[kind]
+    smac = bytes.fromhex("001122334455")
+    rc, out = O.rewrite(pcap, ["--dlt=enet", "--enet-smac=00:11:22:33:44:55"])
+    assert rc == 0
+    for r_in, r_out in zip(S.records(pcap), S.records(out)):
+        d, o = r_in[4], r_out[4]
+        assert r_out[2:4] == r_in[2:4]
+        if _eth_of(kind, r_in, b"", b"") is None:  # (the decoder's soft error: as read)
+            assert o == d
+            continue
+        moved = bytearray(d) + bytes(14 - hl)
+        moved[14:14 + len(d) - hl] = d[hl:]
+        moved[6:12] = smac
+        assert o == bytes(moved[:len(d)])
+    rc, out = O.rewrite(pcap, ["--dlt=hdlc", "--hdlc-address=9"])
+    assert rc == 0
+    for r_in, r_out in zip(S.records(pcap), S.records(out)):
+        d, o = r_in[4], r_out[4]
+        if _eth_of(kind, r_in, b"", b"") is None:
+            assert o == d
+            continue
+        moved = bytearray(d) + bytes(4)
+        moved[4:4 + len(d) - hl] = d[hl:]
+        moved[0] = 9  # the address goes in before the control field fails
+        assert r_out[2:4] == r_in[2:4] and o == bytes(moved[:len(d)])
+
+
+@pytest.mark.parametrize("kind", ["raw", "sll"])
+def test_oracle_vlan_push_behind_another_decoder(built, kind):
+    """--enet-vlan=add with both MACs: an 18-byte header from 14 + 4 (en10mb.c:547), the TCI at
+    the decoder extra's never-set vlan_offset 0 over the destination address, the inner type
+    the context's never-set proto_vlan_tag 0 (:696-715), bytes [14, 18) the packet's own"""
+    pcap = S.reframe(_base(200, seed=33), kind, odd_every=9)
+    hl = {"raw": 0, "sll": 16}[kind]
+    rc, out = O.rewrite(pcap, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=45", "--enet-vlan-pri=5"] + MACS)
+    for r_in, r_out in zip(S.records(pcap), S.records(out)):
+        d, o = r_in[4], r_out[4]
+        if _eth_of(kind, r_in, b"", b"") is None:
+            assert o == d
+            continue
+        tci = (45 | 5 << 13).to_bytes(2, "big")
+        exp = tci + b"\x00\x00" + bytes.fromhex("99aa") + bytes.fromhex("001122334455") + b"\x81\x00" + \
+            d[14:18] + d[hl:]
+        assert rc == 0 and o == exp
 
 
 # ------------------------------------------------------------------------- GPU
@@ -125,6 +177,16 @@ ARGSETS = [
      "--fuzz-seed=11", "--fuzz-factor=1", "--fixcsum"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--fuzz-seed=9", "--fuzz-factor=2"],
     ["--fuzz-seed=3", "--fuzz-factor=1"],
+    # round 5, the reference's failing encodes written half-moved (soft errors): the hdlc
+    # encoder without its fields (hdlc.c:240-288), en10mb without addresses (en10mb.c:567-619),
+    # and a VLAN push behind another decoder (the tag at byte 0, en10mb.c:696-715)
+    ["--dlt=hdlc"],
+    ["--dlt=hdlc", "--hdlc-address=15", "--seed=2"],
+    ["--dlt=enet", "--fixcsum"],
+    ["--dlt=enet", "--enet-smac=00:11:22:33:44:55", "--seed=6"],
+    ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=45", "--enet-vlan-pri=5", "--enet-vlan-cfi=1", "--fixcsum"] +
+    MACS,
+    ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=7", "--fuzz-seed=4", "--fuzz-factor=2"] + MACS,
 ]
 
 

@@ -117,8 +117,7 @@ def test_oracle_jnpr_into_ethernet_strips_header_and_tag(built):
 
 def test_unserved_combinations_are_refused(built):
     # (--fuzz-seed with the en10mb encoder's dst_modified carry, SURVEY Q18: no --enet-dmac)
-    for dlt, args in [(178, ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=5"] + MACS),
-                      (105, ["--fuzz-seed=3", "--dlt=enet"]), (178, ["--fuzz-seed=3", "--dlt=enet"])]:
+    for dlt, args in [(105, ["--fuzz-seed=3", "--dlt=enet"]), (178, ["--fuzz-seed=3", "--dlt=enet"])]:
         with pytest.raises(Exception):
             TA.TcpEdit(args, dlt=dlt)
 
@@ -139,6 +138,8 @@ ARGSETS = [
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--fuzz-seed=5",
      "--fuzz-factor=1"],
     ["--fuzz-seed=4", "--fuzz-factor=1"],
+    ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=9", "--fixcsum"] + MACS,
+    ["--dlt=hdlc", "--seed=8"],
 ]
 
 
@@ -207,11 +208,11 @@ def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
 
 
 def test_oracle_jnpr_warning_frames_encode_with_the_carried_state(built):
-    """--dlt=hdlc: a warning frame becomes {address, control, the carried proto} + the
-    frame after its Juniper header (only that header is its l2len); the proto is the last
-    whole decode's inner ethertype, zero before the first"""
+    """--dlt=enet with both MACs: a warning frame gets a new Ethernet header in place of its
+    Juniper header (only that header is its l2len), whose type is the carried proto -- the
+    last whole decode's inner ethertype, zero before the first"""
     pcap, warn = _jnpr_warn(200)
-    args = ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3"]
+    args = ["--dlt=enet"] + MACS
     rc, out = O.rewrite(pcap, args)
     assert rc == 0
     prev = b"\x00\x00"
@@ -220,11 +221,28 @@ def test_oracle_jnpr_warning_frames_encode_with_the_carried_state(built):
         hl = 6 + (d[4] << 8 | d[5])
         inner = d[hl:]
         if i in warn:
-            assert o == bytes([15, 3]) + prev + inner, i
+            # (a carried tagged decode also writes its TCI at offset 14)
+            assert o[12:14] == prev and (prev == b"\x81\x00" or o[14:] == inner), i
             continue
-        typ = inner[12:14]  # (en10mb.c:431: the outer type, 0x8100 for a tagged frame)
-        assert o[:4] == bytes([15, 3]) + typ, i
-        prev = typ
+        prev = inner[12:14]  # (en10mb.c:431: the outer type, 0x8100 for a tagged frame)
+
+
+def test_oracle_jnpr_into_hdlc_fails_after_the_first_whole_decode(built):
+    """--dlt=hdlc: before the first whole inner decode a warning frame becomes {address,
+    control, proto 0} + the frame after its Juniper header; from that decode on the context's
+    decoded extra is the en10mb sub-decoder's (dlt_utils.c:262-263), smaller than the
+    hdlc_extra_t dlt_hdlc_encode demands (hdlc.c:237-238): every record is a soft error,
+    written as read (tcpedit.c:104-108)"""
+    pcap, warn = _jnpr_warn(200, lead=3)
+    rc, out = O.rewrite(pcap, ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3"])
+    assert rc == 0
+    for i, (r_in, r_out) in enumerate(zip(S.records(pcap), S.records(out))):
+        d, o = r_in[4], r_out[4]
+        if i < 3:
+            hl = 6 + (d[4] << 8 | d[5])
+            assert o == bytes([15, 3, 0, 0]) + d[hl:], i
+        else:
+            assert r_out == r_in, i
 
 
 # the option lines of the Juniper warning frames: the en10mb encoder with both MACs, with a
@@ -237,6 +255,10 @@ JNPR_LINES = [
     ["--dlt=user", "--user-dlink=01,02,03,04,05,06,07,08,09,0a,0b,0c,08,00", "--user-dlt=1", "--ttl=9"],
     ["--dlt=hdlc", "--hdlc-address=15", "--hdlc-control=3", "--seed=5"],
     ["--dlt=enet", "--fuzz-seed=3", "--fuzz-factor=2", "--fixcsum"] + MACS,
+    # round 5: a VLAN push behind the Juniper decoder (the tag at the inner frame's
+    # vlan_offset, en10mb.c:696-715) and the hdlc encoder without its fields
+    ["--dlt=enet", "--enet-vlan=add", "--enet-vlan-tag=12", "--enet-vlan-pri=2", "--fixcsum"] + MACS,
+    ["--dlt=hdlc", "--hdlc-control=3"],
 ]
 
 

@@ -103,6 +103,9 @@ OPTION_POOL = [c[3] for c in G.IN_SCOPE if c[2] is None] + [
     # non-octet IPv6 masks: remap_ipv6's stray write on the generic lane
     ["--pnat=[::/0]:[2001:db8:aaaa::/36]", "--fixcsum"], ["--srcipmap=[::/0]:[2001:db8::/20]", "--seed=5"],
     ["--pnat=10.0.0.0/8:192.168.0.0/20,[::/0]:[fd00::/9]"],
+    # the hdlc encoder's fallback fields on Ethernet: a tagged frame's vlan flag (1), else a
+    # soft error written half-moved (hdlc.c:240-288)
+    ["--dlt=hdlc"], ["--dlt=hdlc", "--hdlc-control=9", "--fixcsum"],
 ]
 
 

@@ -188,3 +188,27 @@ def test_gpu_reproduces_reference_quirk(built, check):
         return rc, out
 
     check(gpu)
+
+
+def test_hdlc_encoder_falls_back_on_the_decoded_vlan_flag(built):
+    """--dlt=hdlc without --hdlc-address/--hdlc-control on Ethernet: dlt_hdlc_encode reads
+    `extra->hdlc`, the first int of the decoded extra -- the en10mb decoder's `vlan` flag
+    (en10mb_types.h:30): a tagged frame gets address = control = 1 and the proto, an untagged
+    one fails after the memmove of its payload to byte 4 (hdlc.c:240-288) and is written as
+    that left it (a soft error, caplen unchanged).  Parity unpinned: no reference fixture."""
+    import tcpreplay_amd.synth as S
+    base = S.records(S.pcap_fixed(6, 90, seed=4))
+    recs = []
+    for i, (ts, tu, cl, ln, d) in enumerate(base):
+        if i % 2:
+            d = d[:12] + b"\x81\x00\x20\x05" + d[12:]
+            cl, ln = cl + 4, ln + 4
+        recs.append((ts, tu, cl, ln, d))
+    rc, out = O.rewrite(S.build_pcap(recs), ["--dlt=hdlc"])
+    assert rc == 0
+    for i, (r_in, r_out) in enumerate(zip(recs, S.records(out))):
+        d = r_in[4]
+        if i % 2:  # {1, 1, ctx->proto}: the outer type, 0x8100 (en10mb.c:431) + the L3 bytes
+            assert r_out[4] == b"\x01\x01\x81\x00" + d[18:] and r_out[2] == r_in[2] - 14
+        else:      # d[0:4] + the payload moved to byte 4 + the last 10 bytes as they were
+            assert r_out[2:4] == r_in[2:4] and r_out[4] == d[:4] + d[14:] + d[-10:]
