@@ -59,6 +59,10 @@ struct tcpedit_batch_s {
     uint32_t grow_bad;       /* its violation word, read back */
     int mtu_fast;            /* tiles were cut for the wave lane's --mtu-trunc instances */
     int last_mtu;            /* the last launch placed tiles by the --mtu-trunc prediction */
+    int fz_fast;             /* tiles were cut for the wave lane's --fuzz-seed instances */
+    int last_fz;             /* the last launch fuzzed on the wave lane (static_fz placement) */
+    uint32_t *d_fzlist;      /* static_fz: the reach list (n_tiles + 1 words) */
+    uint64_t fzlist_cap;
     long long *d_tcut;       /* the prediction: n_tiles + 1 prefix (te_mtu_cuts), ... */
     long long *d_tcut_raw;   /* ... from per-64-tile sums (scratch) */
     uint64_t tcut_cap;       /* tiles d_tcut holds */
@@ -155,7 +159,7 @@ struct tcpedit_batch_s {
 #define WS_COUNTERS1 128 /* counter set 1: the fast lane alternates sets by launch parity */
 #define WS_STATE 256
 #define WS_LIST_CNT(n_tiles) (WS_STATE + 8 * ((n_tiles) + 1))
-#define WS_SLOTS(n_tiles) ((WS_LIST_CNT(n_tiles) + 8 + 15) & ~(uint64_t)15) /* wave lane: 32 B per block */
+#define WS_SLOTS(n_tiles) ((WS_LIST_CNT(n_tiles) + 8 + 15) & ~(uint64_t)15) /* wave lane: TE_WK_SLOT_WORDS a block */
 
 /* no edit step can change a record's length or drop it: efcs, VLAN add/del,
  * fixlen, MTU truncation and skipped soft errors are the only ways (plus
@@ -263,6 +267,25 @@ static int fast_capable_mtu(const te_dev_cfg_t *c)
     return c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && c->mtu_truncate &&
            c->mtu >= 128 && c->mtu <= 65535 && c->vlan == TE_VLAN_OFF && !c->efcs && c->fixlen == TE_FIXLEN_OFF &&
            !c->skip_soft_errors && !c->fuzz_seed && !c->fixhdrlen && cidr_inline(c);
+}
+
+/* --fuzz-seed on the wave lane: no edit before the fuzz step but the en10mb decode and
+ * re-encode (so fuzzing() sees the input bytes and each record's cut is predictable from
+ * them, te_fuzz_tile_cut), no other size change, no skipped soft errors (a cut record is a
+ * soft error that stays in the output) */
+static int fast_capable_fuzz(const te_dev_cfg_t *c)
+{
+    return c->fuzz_seed && c->encoder == TE_ENC_EN10MB && c->decoder == TE_DEC_EN10MB && c->vlan == TE_VLAN_OFF &&
+           !c->efcs && c->fixlen == TE_FIXLEN_OFF && !c->mtu_truncate && !c->skip_soft_errors && !c->fixhdrlen &&
+           !c->l2carry && cidr_inline(c) && !(c->mac_mask || c->n_subs || c->random_set) && !c->has_portmap &&
+           c->tos < 0 && c->ttl_mode == TE_TTL_OFF && c->tclass < 0 && c->flowlabel < 0 && !c->tcp_sequence_enable;
+}
+
+/* TCPEDIT_HIP_NO_FUZZ_FAST=1 keeps --fuzz-seed on the generic lane (A/B checks) */
+static int fuzz_fast_off(void)
+{
+    const char *e = getenv("TCPEDIT_HIP_NO_FUZZ_FAST");
+    return e && *e == '1';
 }
 
 /* TCPEDIT_HIP_NO_MTU_FAST=1 keeps --mtu-trunc on the generic lane (A/B checks) */
@@ -639,7 +662,11 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
     /* ... and --mtu-trunc (native-order microsecond input, the wave lane only) */
     b->mtu_fast = !proto->slot_mode && fast_capable_mtu(&t->cfg) && !b->swapped && !b->nsec &&
                   fast_kind_pref() == TE_FAST_WAVE && !mtu_fast_off();
-    b->fast_tiles = (!proto->slot_mode && fast_capable(&t->cfg)) || proto->grow_fast || shrink_fast || b->mtu_fast;
+    /* ... and --fuzz-seed (native-order microsecond input, the wave lane only) */
+    b->fz_fast = !proto->slot_mode && fast_capable_fuzz(&t->cfg) && !b->swapped && !b->nsec &&
+                 fast_kind_pref() == TE_FAST_WAVE && !fuzz_fast_off();
+    b->fast_tiles = (!proto->slot_mode && fast_capable(&t->cfg)) || proto->grow_fast || shrink_fast || b->mtu_fast ||
+                    b->fz_fast;
     b->fast_kind = b->fast_tiles ? fast_kind_pref() : 0;
     if (shrink_fast && !proto->grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
         b->fast_tiles = 0, b->fast_kind = 0;
@@ -647,6 +674,7 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
     proto->budget = proto->wave      ? te_wave_tile_bytes(&t->cfg, proto->grow_fast ? TE_SZ_GROW
                                                                    : shrink_fast     ? static_shrink_kind(&t->cfg)
                                                                    : b->mtu_fast     ? TE_SZ_MTU
+                                                                   : b->fz_fast      ? TE_SZ_FUZZ
                                                                                      : TE_SZ_NONE)
                     : b->fast_tiles ? TE_FK_TILE_BYTES
                                     : TE_SLOT_BYTES;
@@ -875,6 +903,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     if (!rc && proto.wave && !proto.slot_mode && !b->idx_pinned)
         balance_tiles(b, te_wave_waves(&t->cfg, proto.shrink_fast ? static_shrink_kind(&t->cfg)
                                                 : b->mtu_fast      ? TE_SZ_MTU
+                                                : b->fz_fast       ? TE_SZ_FUZZ
                                                                    : TE_SZ_NONE),
                       proto.budget, proto.max_pkts);
     b->out_cap = 24 + 64 + m->rec_bytes;
@@ -906,6 +935,9 @@ static void batch_free_dev(tcpedit_batch_t *b)
     b->tcut_ok = 0;
     hipFree(b->d_tile_list);
     hipFree(b->d_fuzz);
+    hipFree(b->d_fzlist);
+    b->d_fzlist = NULL;
+    b->fzlist_cap = 0;
     hipFree(b->d_l2carry);
     hipFree(b->d_jnpr);
     hipFree(b->d_jtmp);
@@ -1137,7 +1169,7 @@ static tcpedit_batch_t *batch_open(tcpedit_t *t, const uint8_t *hdr, const uint8
                              t->stream));
     b->ws_bytes = WS_SLOTS(b->n_tiles) + 64;
     if (b->fast_kind == TE_FAST_WAVE)
-        b->ws_bytes += 32 * (uint64_t)te_wave_grid();
+        b->ws_bytes += 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid();
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
     HIPCHK(t, hipMemsetAsync(b->d_ws, 0, b->ws_bytes, t->stream)); /* the list count starts at 0 */
     if (b->fast_tiles)
@@ -1325,11 +1357,9 @@ static int l2carry_bufs(tcpedit_t *t, tcpedit_batch_t *b, te_launch_t *L)
  * that launch's parity -- for a run whose generic pass was left out by the hint */
 /* the --mtu-trunc placement prediction for this tile cut (te_mtu_cuts), computed on the
    batch's stream the first time a cut is launched with this MTU; 0 when ready */
-static int mtu_cuts_ready(tcpedit_batch_t *b, int32_t mtu)
+/* room for a placement prediction of this tile cut (d_tcut, d_tcut_raw) */
+static int tcut_bufs(tcpedit_batch_t *b)
 {
-    tcpedit_t *t = b->ctx;
-    if (b->tcut_ok && b->tcut_mtu == mtu)
-        return 0;
     if (b->tcut_cap < b->n_tiles + 1) {
         hipFree(b->d_tcut);
         hipFree(b->d_tcut_raw);
@@ -1341,6 +1371,16 @@ static int mtu_cuts_ready(tcpedit_batch_t *b, int32_t mtu)
             return -1;
         b->tcut_cap = b->n_tiles + 1;
     }
+    return 0;
+}
+
+static int mtu_cuts_ready(tcpedit_batch_t *b, int32_t mtu)
+{
+    tcpedit_t *t = b->ctx;
+    if (b->tcut_ok && b->tcut_mtu == mtu)
+        return 0;
+    if (tcut_bufs(b) < 0)
+        return -1;
     if (te_mtu_cuts(b->d_in, b->d_tiles, b->d_pkt_rel, (uint32_t)b->n_tiles, (uint32_t)mtu, b->d_tcut_raw, b->d_tcut,
                     t->stream) != 0)
         return -1;
@@ -1407,9 +1447,30 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
     L.tcut = L.static_mtu ? b->d_tcut : NULL;
     L.mtu = (uint32_t)c->mtu;
     b->last_mtu = L.static_mtu;
+    /* --fuzz-seed on the wave lane: tiles placed by the predicted cuts, which the launch
+       computes after drawing the states (fast_capable_fuzz) */
+    L.static_fz = b->fz_fast && b->fast_kind == TE_FAST_WAVE && fast_capable_fuzz(c) && !b->slot_layout &&
+                  !b->has_trim && !b->swapped && !b->nsec && !b->d_dirbits && b->n_tiles > 0 && b->n_pkts > 0 &&
+                  !b->fuzz_probe_only && !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never &&
+                  !grow_off_env() && !fast_lane_off() && tcut_bufs(b) == 0;
+    if (L.static_fz) {
+        if (b->fzlist_cap < b->n_tiles) {
+            hipFree(b->d_fzlist);
+            b->d_fzlist = NULL;
+            b->fzlist_cap = 0;
+            if (hipMalloc((void **)&b->d_fzlist, 4 * (b->n_tiles + 1)) != hipSuccess)
+                return -1;
+            b->fzlist_cap = b->n_tiles;
+        }
+        L.tcut = b->d_tcut;
+        L.tcut_raw = b->d_tcut_raw;
+        L.fz_list = b->d_fzlist;
+        b->tcut_ok = 0; /* (d_tcut now holds this launch's fuzz cuts) */
+    }
+    b->last_fz = L.static_fz;
     L.fast = b->fast_tiles && !fast_lane_off() &&
              ((L.static_off && fast_capable(c)) || (L.static_grow && fast_capable_grow(c)) ||
-              (L.static_shrink && fast_capable_shrink(c)) || L.static_mtu);
+              (L.static_shrink && fast_capable_shrink(c)) || L.static_mtu || L.static_fz);
     L.fast_v6 = fast_v6_ok(c);
     /* a batch whose input + output outgrow the 256 MiB Infinity Cache streams through it:
        nontemporal loads and stores (TCPEDIT_HIP_STREAM=0/1 overrides, for A/B runs) */
@@ -1440,7 +1501,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
                      b->gen_hint_gen == t->cfg_gen && b->last_listed == 0;
     if (generic_only)
         L.grid = b->last_listed ? (int)b->last_listed : 1;
-    if (c->fuzz_seed && !L.fast && b->n_pkts) {
+    if (c->fuzz_seed && (!L.fast || L.static_fz) && b->n_pkts) {
         /* --fuzz-seed: room for a state per record and a word per 1024 records */
         const uint64_t need = b->n_pkts;
         if (b->fuzz_cap < need) {
@@ -1555,7 +1616,7 @@ static int run_q8(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir, int file_star
         L.q8_npre = b->npre;
         L.q8_pre_file_start = b->pre_file_start;
     }
-    if (t->cfg.fuzz_seed && b->d_fuzz && !b->last_fast)
+    if (t->cfg.fuzz_seed && b->d_fuzz && (!b->last_fast || b->last_fz))
         L.fuzz_states = b->d_fuzz;
     if (t->cfg.l2carry && !b->last_fast)
         L.l2carry = b->d_l2carry; /* the last launch's scan: each replayed record's carried value */
@@ -1686,11 +1747,11 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
                                  sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
     if (b->last_fgrid) {
         if (!b->slots_host)
-            b->slots_host = malloc(32 * (size_t)te_wave_grid());
-        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
-                                 hipMemcpyDeviceToHost, t->stream));
+            b->slots_host = malloc(8 * TE_WK_SLOT_WORDS * (size_t)te_wave_grid());
+        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles),
+                                 8 * TE_WK_SLOT_WORDS * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
     }
-    if (b->last_grow || b->last_mtu)
+    if (b->last_grow || b->last_mtu || b->last_fz)
         HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
@@ -1705,16 +1766,20 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
         HIPCHK(t, hipMemcpyAsync(b->counters, b->d_ws + b->last_cnt_off, sizeof(b->counters),
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipMemcpyAsync(b->err, b->d_ws + WS_ERR, sizeof(b->err), hipMemcpyDeviceToHost, t->stream));
-        if (b->last_grow || b->last_mtu) /* the listed tiles can break static placement too */
+        if (b->last_grow || b->last_mtu || b->last_fz) /* the listed tiles can break static placement too */
             HIPCHK(t, hipMemcpyAsync(&b->grow_bad, b->d_ws + WS_GROW_BAD, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                      t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
         b->last_skipped = 0;
     }
-    if ((b->last_grow || b->last_mtu) && b->grow_bad) {
-        /* a record did not grow by exactly 4 bytes (a tile's --mtu-trunc cut was not the
-           predicted one): place this batch by scan + look-back from now on, and run it again
-           that way */
+    if ((b->last_grow || b->last_mtu || b->last_fz) && b->grow_bad) {
+        /* a record did not grow by exactly 4 bytes (a tile's --mtu-trunc or fuzz cut was not
+           the predicted one): place this batch by scan + look-back from now on, and run it
+           again that way -- from the RNG state this run started at (te_fuzz_scan kept it in
+           words[1]) */
+        if (b->last_fz)
+            HIPCHK(t, hipMemcpyAsync(t->d_fuzz_words, t->d_fuzz_words + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                     t->stream));
         b->grow_off = 1;
         b->grow_off_gen = t->cfg_gen;
         b->grow_bad = 0;
@@ -1740,13 +1805,14 @@ static int batch_run_dir(tcpedit_t *t, tcpedit_batch_t *b, int fixed_dir)
             return TCPEDIT_ERROR;
     }
     for (int i = 0; i < b->last_fgrid; i++) { /* the wave lane's per-block totals */
-        const uint64_t *v = b->slots_host + 4 * (size_t)i;
+        const uint64_t *v = b->slots_host + TE_WK_SLOT_WORDS * (size_t)i;
         b->counters[TE_CNT_PACKETS] += v[0];
-        b->counters[TE_CNT_WRITTEN] += v[0];
+        b->counters[TE_CNT_WRITTEN] += v[0] - v[4]; /* (fuzz drops) */
         b->counters[TE_CNT_BYTES_IN] += v[1];
         b->counters[TE_CNT_BYTES_OUT] += v[1] + (uint64_t)((int64_t)b->last_grow * (int64_t)v[0]) /* +- 4 a record */
-                                         - v[3];                                                /* the MTU cuts */
+                                         - v[3];                                        /* the MTU / fuzz cuts */
         b->counters[TE_CNT_EDITED] += v[2];
+        b->counters[TE_CNT_SOFT] += v[5];
     }
     if (b->last_fast) { /* same batch + same config lists the same tiles next time */
         b->gen_hint_ok = 1;
@@ -2050,14 +2116,14 @@ static int fused_once(tcpedit_t *t, tcpedit_batch_t *b)
     HIPCHK(t, hipMemcpyAsync(&tot, b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull), 8, hipMemcpyDeviceToHost,
                              t->stream));
     if (!b->slots_host)
-        b->slots_host = malloc(32 * (size_t)te_wave_grid());
+        b->slots_host = malloc(8 * TE_WK_SLOT_WORDS * (size_t)te_wave_grid());
     if (b->last_fgrid)
-        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles), 32 * (size_t)b->last_fgrid,
-                                 hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipMemcpyAsync(b->slots_host, b->d_ws + WS_SLOTS(b->n_tiles),
+                                 8 * TE_WK_SLOT_WORDS * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
     memset(b->counters, 0, sizeof(b->counters));
     for (int i = 0; i < b->last_fgrid; i++) {
-        const uint64_t *v = b->slots_host + 4 * (size_t)i;
+        const uint64_t *v = b->slots_host + TE_WK_SLOT_WORDS * (size_t)i;
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
@@ -2457,7 +2523,7 @@ int tcpedit_batch_index_device(tcpedit_t *t, tcpedit_batch_t *b, int iters, doub
             hipFree(b->d_ws);
             b->d_ws = NULL;
             HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (nt + 1)));
-            b->ws_bytes = WS_SLOTS(nt) + 64 + (b->fast_kind == TE_FAST_WAVE ? 32 * (uint64_t)te_wave_grid() : 0);
+            b->ws_bytes = WS_SLOTS(nt) + 64 + (b->fast_kind == TE_FAST_WAVE ? 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid() : 0);
             HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
         }
         hipFree(b->d_tiles);
@@ -2760,8 +2826,8 @@ static tcpedit_batch_t *pipe_slot_open(tcpedit_t *t, size_t chunk)
     HIPCHK(t, hipMalloc((void **)&b->d_tile_list, sizeof(uint32_t) * (b->idx_cap_tiles + 1)));
     b->q8_cap = (uint32_t)(b->idx_cap_pkts < TE_Q8_CAP ? b->idx_cap_pkts : TE_Q8_CAP);
     HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * (size_t)b->q8_cap));
-    HIPCHK(t, hipMalloc((void **)&b->d_ws, WS_SLOTS(b->idx_cap_tiles) + 64 + 32 * (uint64_t)te_wave_grid()));
-    HIPCHK(t, hipHostMalloc((void **)&b->res_pinned, TE_RES_SLOTS + 32 * (uint64_t)te_wave_grid(), 0));
+    HIPCHK(t, hipMalloc((void **)&b->d_ws, WS_SLOTS(b->idx_cap_tiles) + 64 + 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid()));
+    HIPCHK(t, hipHostMalloc((void **)&b->res_pinned, TE_RES_SLOTS + 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid(), 0));
     HIPCHK(t, hipEventCreate(&b->ev0));
     HIPCHK(t, hipEventCreate(&b->ev1));
     return b;
@@ -2862,7 +2928,7 @@ static int pipe_finish_chunk(tcpedit_t *t, te_pipe_t *P, int s, uint64_t pkt_bas
     }
     memcpy(b->err, b->res_pinned + WS_ERR, sizeof(b->err));
     for (int i = 0; i < b->last_fgrid; i++) {
-        const uint64_t *v = (const uint64_t *)(b->res_pinned + TE_RES_SLOTS) + 4 * (size_t)i;
+        const uint64_t *v = (const uint64_t *)(b->res_pinned + TE_RES_SLOTS) + TE_WK_SLOT_WORDS * (size_t)i;
         b->counters[TE_CNT_PACKETS] += v[0];
         b->counters[TE_CNT_WRITTEN] += v[0];
         b->counters[TE_CNT_BYTES_IN] += v[1];
@@ -3172,7 +3238,7 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
                 stopped = 1; /* libpcap's end, or the bytes ran out */
             b->dirbits_len = dirbits_len;
             b->d_dirbits = d_dirbits;
-            b->ws_bytes = WS_SLOTS(b->n_tiles) + 64 + 32 * (uint64_t)te_wave_grid();
+            b->ws_bytes = WS_SLOTS(b->n_tiles) + 64 + 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid();
             if (pipe_grow(t, P, s) < 0)
                 goto fail;
             HIPCHK(t, hipMemsetAsync(b->d_ws, 0, WS_STATE, t->stream)); /* err, ticket, both counter sets */
@@ -3187,7 +3253,8 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
             HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws, WS_STATE, hipMemcpyDeviceToHost, t->stream));
             if (b->last_fgrid)
                 HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
-                                         32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
+                                         8 * TE_WK_SLOT_WORDS * (size_t)b->last_fgrid, hipMemcpyDeviceToHost,
+                                         t->stream));
             HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
             /* a size-preserving config writes each record at its input offset, so the chunk's
                output is its records' bytes: start their D2H behind the edit now, without the
@@ -3669,7 +3736,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             stopped = 1;
         b->dirbits_len = dirbits_len;
         b->d_dirbits = d_dirbits;
-        b->ws_bytes = WS_SLOTS(b->n_tiles) + 64 + 32 * (uint64_t)te_wave_grid();
+        b->ws_bytes = WS_SLOTS(b->n_tiles) + 64 + 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid();
         if (pipe_grow(t, P, s) < 0)
             goto fail_drain;
         const size_t rec_bytes = (size_t)(b->walk_end - 24);
@@ -3697,7 +3764,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         HIPCHK(t, hipMemcpyAsync(b->res_pinned, b->d_ws, WS_STATE, hipMemcpyDeviceToHost, t->stream));
         if (b->last_fgrid)
             HIPCHK(t, hipMemcpyAsync(b->res_pinned + TE_RES_SLOTS, b->d_ws + WS_SLOTS(b->n_tiles),
-                                     32 * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
+                                     8 * TE_WK_SLOT_WORDS * (size_t)b->last_fgrid, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipEventRecord(P->edit_done[s], t->stream));
         inflight[s] = 1;
         chunk_pkt_base[s] = pkts;
@@ -4044,7 +4111,7 @@ static tcpedit_batch_t *one_ready(tcpedit_t *t)
     b->q8_defer = 1;
     HIPCHK(t, hipMalloc((void **)&b->d_q8, 16 * 2));
     HIPCHK(t, hipMalloc((void **)&b->d_q8_init, 262144 + 64));
-    b->ws_bytes = WS_SLOTS(1) + 64 + 32 * (uint64_t)te_wave_grid();
+    b->ws_bytes = WS_SLOTS(1) + 64 + 8 * TE_WK_SLOT_WORDS * (uint64_t)te_wave_grid();
     HIPCHK(t, hipMalloc((void **)&b->d_ws, b->ws_bytes));
     HIPCHK(t, hipEventCreate(&b->ev0));
     HIPCHK(t, hipEventCreate(&b->ev1));

@@ -43,6 +43,10 @@ extern "C" {
 #define TE_SZ_VDEL 2           /* --enet-vlan=del over tagged records: -4 */
 #define TE_SZ_EFCS 3           /* --efcs: -4 */
 #define TE_SZ_MTU 4            /* --mtu-trunc: a record longer than the MTU loses its tail */
+#define TE_SZ_FUZZ 5           /* --fuzz-seed: a picked record may be cut (DROP / REDUCE) */
+/* the wave lane's per-block totals: {records, bytes in, records edited, bytes cut, records
+   dropped (not written), soft errors, -, -} */
+#define TE_WK_SLOT_WORDS 8
 /* option groups of the fast lane: a te_wave_tiles instance compiles in the groups of
    its mask, and te_launch_edit launches the smallest instance covering the config */
 #define TE_FF_MAC 1u     /* --enet-dmac / --enet-smac */
@@ -146,13 +150,19 @@ typedef struct {
                                  from the prediction sets *grow_bad */
     const long long *tcut;    /* device: n_tiles + 1 exclusive prefix of the predicted cuts */
     uint32_t mtu;             /* static_mtu: the MTU (cfg.mtu) */
+    int static_fz;            /* --fuzz-seed on the wave lane: the launch finds the reaching records
+                                 (te_fuzz_reach + the generic reach pass over the tiles it lists),
+                                 draws the states, predicts each tile's cut into tcut (written
+                                 here, not read) and places tiles by it like static_mtu */
+    long long *tcut_raw;      /* static_fz: device scratch, (n_tiles + 63) / 64 + 1 words */
+    uint32_t *fz_list;        /* static_fz: device, n_tiles + 1 words (the reach list, its count) */
     /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
        only the listed tiles */
     int fast;
     int fast_kind;            /* TE_FAST_BLOCK or TE_FAST_WAVE (how the tiles were cut) */
-    uint64_t *slots;          /* device: wave lane's per-block {packets, bytes, edited, -}; the host
-                                 adds them to this launch's counters */
+    uint64_t *slots;          /* device: wave lane's per-block totals (TE_WK_SLOT_WORDS words); the
+                                 host adds them to this launch's counters */
     int skip_generic;         /* wave lane: leave out the generic pass (no tile will be listed) */
     int generic_only;         /* run only the generic pass over the tiles the last fast launch listed */
     int out_fgrid;            /* set by te_launch_edit: blocks of the fast-lane launch (slots written) */

@@ -1570,11 +1570,12 @@ DI void en10mb_merge_layer3(Pkt &pk, const Dec &s, const u8 *ip, const u8 *ip6) 
 
 // the encoder's L2 length (plugin_l2len): en10mb's parse (en10mb.c:917-943),
 // user.c:325-342, hdlc.c:355-366
-DI int encoder_l2len(const Pkt &pk, const te_dev_cfg_t &cfg) {
+DI int encoder_l2len_d(const u8 *d, u32 caplen, const te_dev_cfg_t &cfg) {
     return cfg.encoder == TE_ENC_USER                                   ? cfg.user_length
-           : (cfg.encoder == TE_ENC_HDLC || cfg.encoder == TE_ENC_PPP) ? (pk.caplen < 4 ? -1 : 4)  // pppserial.c:335-343
-                                                                       : en10mb_l2len(pk.d, (int)pk.caplen);
+           : (cfg.encoder == TE_ENC_HDLC || cfg.encoder == TE_ENC_PPP) ? (caplen < 4 ? -1 : 4)  // pppserial.c:335-343
+                                                                       : en10mb_l2len(d, (int)caplen);
 }
+DI int encoder_l2len(const Pkt &pk, const te_dev_cfg_t &cfg) { return encoder_l2len_d(pk.d, pk.caplen, cfg); }
 
 // ---------------------------------------------------------------------------
 // --fuzz-seed: fuzzing() (src/tcpedit/fuzzing.c:62-297) for one packet.  The
@@ -1614,31 +1615,89 @@ DI void fuzz_fill(Pkt &pk, int from, int n, int how, u8 x) {  // how: 0 = 0x00, 
     }
 }
 
-DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
-    u32 r = tcpr_random_dev(state);
-    if (r % cfg.fuzz_factor) return 0;
-    const int caplen = (int)pk.caplen;
-    const int l2len = encoder_l2len(pk, cfg);
+// What fuzzing() does to a record it picked (fuzzing.c:133-199), from the draw r and the
+// payload's place (l4off = l4data - packet, l4len as the reference computes it): a size cut
+// (DROP / REDUCE: caplen = len = nl) or a byte run [from, from + n) set to 0x00 / 0xff or
+// XORed with x (how 0 / 1 / 2), and fuzzing()'s return (chksum_update_required).  Reads
+// nothing: the wave lane plans its records with it, and fuzz_plan below the others.
+struct FzPlan {
+    int ret = 0;
+    bool cut = false;
+    u32 nl = 0;
+    int from = 0, n = 0, how = 0;
+    u8 x = 0;
+    int stale_at = 0;  // > 0: the IP protocol byte was read at or past `phys` (fuzz_plan)
+};
+DI FzPlan fuzz_plan_l4(u32 r, int l4off, int l4len, u32 caplen, u32 len) {
+    FzPlan f;
+    if (l4len <= 1 || l4off > (int)caplen) return f;
+    r ^= r >> 16;
+    const u32 act = r % 11u;  // fuzzing.h: DROP, REDUCE, START_{0,R,FF}, MID_{0,R,FF}, END_{0,R,FF}
+    f.x = (u8)(r >> 4);
+    if (act <= 1) {  // fuzz_reduce_packet_size (fuzzing.c:37-60): DROP returns 0, REDUCE 1
+        const u32 nl = act == 0 ? 0u : r % (u32)(l4len - 1) + 1u;
+        if (len < caplen || nl > caplen) return f;
+        f.ret = (int)act;
+        f.cut = nl != caplen;
+        f.nl = nl;
+        return f;
+    }
+    if (act <= 4) {  // START_*
+        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);
+        if (!sgt && act != 2) return f;
+        f.from = l4off;
+        f.n = sgt;
+        f.how = act == 2 ? 0 : act == 4 ? 1 : 2;
+        f.ret = 1;
+        return f;
+    }
+    if (act <= 7) {  // MID_*
+        if (act != 6 && l4len <= 2) return f;
+        const u32 off = ((r >> 16) % (u32)(l4len - 1)) + 1u;
+        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len - off);
+        if (!sgt || (act == 6 && sgt > l4len)) return f;
+        f.from = l4off + (int)off;
+        f.n = sgt;
+        f.how = act == 5 ? 0 : act == 7 ? 1 : 2;
+        f.ret = 1;
+        return f;
+    }
+    const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);  // END_*
+    if (!sgt || sgt > l4len) return f;
+    f.from = l4off + l4len - sgt;
+    f.n = sgt;
+    f.how = act == 8 ? 0 : act == 10 ? 1 : 2;
+    f.ret = 1;
+    return f;
+}
+
+// fuzzing() for a picked record d[0, caplen) as the encoder left it (fuzzing.c:89-131:
+// the encoder's l2len and protocol, the L4 header's place); `phys`: the bytes from d
+// that are the record's (a read past them is a stale static-buffer read, Q8)
+DI FzPlan fuzz_plan(const u8 *d, u32 caplen_u, u32 len, u32 phys, const te_dev_cfg_t &cfg, u32 r) {
+    const int caplen = (int)caplen_u;
+    const int l2len = encoder_l2len_d(d, caplen_u, cfg);
     int proto = -1;  // plugin_proto: en10mb.c:741-762, user.c:271-279 (always an error), hdlc.c:300-312
     if (cfg.encoder == TE_ENC_HDLC) {
-        if (caplen >= 4) proto = ld16(pk.d + 2);
+        if (caplen >= 4) proto = ld16(d + 2);
     } else if (cfg.encoder == TE_ENC_EN10MB && caplen >= 14) {
         L2 q;
-        if (get_l2len_protocol(pk.d, pk.caplen, q) != -1) proto = bswap16(q.protocol);
+        if (get_l2len_protocol(d, caplen_u, q) != -1) proto = bswap16(q.protocol);
     }
     const u16 l2proto = bswap16((u16)proto);
-    if (l2len == -1 || caplen < l2len || caplen <= l2len) return 0;  // :95-109, dlt_utils.c:195
+    if (l2len == -1 || caplen < l2len || caplen <= l2len) return FzPlan{};  // :95-109, dlt_utils.c:195
     int l4off, l4len;  // l4data - packet, and the reference's l4len
     u8 l4proto;
+    int stale_at = 0;
     if (l2proto == 0x0800 || l2proto == 0x86DD) {
-        const u8 *ip = pk.d + l2len;
+        const u8 *ip = d + l2len;
         const bool v4 = l2proto == 0x0800;
         const int l4 = v4 ? l4_v4(ip, caplen - l2len) : l4_v6(ip, 0, caplen - l2len);
-        if (l4 < 0) return 0;
+        if (l4 < 0) return FzPlan{};
         l4off = l2len + l4;
         l4len = l4off;  // an offset, as the reference has it (fuzzing.c:118,127)
         const int pb = l2len + (v4 ? 9 : 6);
-        if (pb >= (int)pk.phys) stale(pk, pb + 1);
+        if (pb >= (int)phys) stale_at = pb + 1;
         l4proto = ip[v4 ? 9 : 6];
     } else {
         l4len = caplen - l2len;
@@ -1652,35 +1711,19 @@ DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
         l4len -= 8;
         l4off += 8;
     }
-    if (l4len <= 1 || l4off > caplen) return 0;
-    r ^= r >> 16;
-    const u32 act = r % 11u;  // fuzzing.h: DROP, REDUCE, START_{0,R,FF}, MID_{0,R,FF}, END_{0,R,FF}
-    const u8 x = (u8)(r >> 4);
-    if (act <= 1) {  // fuzz_reduce_packet_size (fuzzing.c:37-60)
-        const u32 nl = act == 0 ? 0u : r % (u32)(l4len - 1) + 1u;
-        if (pk.len < pk.caplen || nl > pk.caplen) return 0;
-        if (nl == pk.caplen) return act;
-        pk.len = pk.caplen = nl;
-        return act;
-    }
-    if (act <= 4) {  // START_*
-        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);
-        if (!sgt && act != 2) return 0;
-        fuzz_fill(pk, l4off, sgt, act == 2 ? 0 : act == 4 ? 1 : 2, x);
-        return 1;
-    }
-    if (act <= 7) {  // MID_*
-        if (act != 6 && l4len <= 2) return 0;
-        const u32 off = ((r >> 16) % (u32)(l4len - 1)) + 1u;
-        const int sgt = (int)fuzz_sgt_size(r, (u32)l4len - off);
-        if (!sgt || (act == 6 && sgt > l4len)) return 0;
-        fuzz_fill(pk, l4off + (int)off, sgt, act == 5 ? 0 : act == 7 ? 1 : 2, x);
-        return 1;
-    }
-    const int sgt = (int)fuzz_sgt_size(r, (u32)l4len);  // END_*
-    if (!sgt || sgt > l4len) return 0;
-    fuzz_fill(pk, l4off + l4len - sgt, sgt, act == 8 ? 0 : act == 10 ? 1 : 2, x);
-    return 1;
+    FzPlan f = fuzz_plan_l4(r, l4off, l4len, caplen_u, len);
+    f.stale_at = stale_at;
+    return f;
+}
+
+DI int fuzz_packet(Pkt &pk, const te_dev_cfg_t &cfg, u32 state) {
+    const u32 r = tcpr_random_dev(state);
+    if (r % cfg.fuzz_factor) return 0;
+    const FzPlan f = fuzz_plan(pk.d, pk.caplen, pk.len, pk.phys, cfg, r);
+    if (f.stale_at) stale(pk, f.stale_at);
+    if (f.cut) pk.len = pk.caplen = f.nl;
+    if (f.n) fuzz_fill(pk, f.from, f.n, f.how, f.x);
+    return f.ret;
 }
 
 // ---------------------------------------------------------------------------

@@ -177,10 +177,13 @@ struct State {
 // (edit_packet.c:596-611, after the header edits and before the address edits, tcpedit.c:
 // 261-265): caplen = len = tcap, IPv4 total length = mtu, IPv6 payload length = mtu - 40,
 // and the checksums cover the cut packet.  `part` is then the cut packet's.
+//
+// `force` (SZ_FUZZ instances): fuzzing() changed the packet (its 1 is a needtorecalc,
+// tcpedit.c:252-256), so an F_INCR run checksums it from scratch too.
 // ---------------------------------------------------------------------------
 template <u32 F>
 DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_dev_cfg_t &cfg, const Knobs &kn,
-                bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st, u32 tcap = 0) {
+                bool v6_ok, const TE_AS_GLOBAL uint16_t *lut, State &st, u32 tcap = 0, bool force = false) {
     // ---- classify: Ethernet II + IPv4 (IHL 5, no fragment, ip_len == caplen - 14) or
     // IPv6 (payload length == caplen - 54), then TCP or UDP with a whole header ----
     const u32 et = hi16(H[3]);  // bytes 12,13 as a raw LE u16
@@ -501,7 +504,7 @@ DI bool phase_a(u32 (&H)[NW], u32 caplen, u32 len, u32 part, int dir, const te_d
     // caplen == len, not a fragment, lengths consistent: the L4 sum always runs,
     // except on a UDP field that is (still) 0 (checksum.c:115).  F_INCR: only for a
     // packet an edit asked to recompute; the others keep the incremental fields.
-    const bool full = !kIncr || recalc;
+    const bool full = !kIncr || recalc || force;
     const bool do_l4 = full && (tcp || ucs != 0);
     L[4] = (do_l4 && tcp) ? with_lo16(L[4], 0) : ((kIncr && !full && tcp) ? with_lo16(L[4], tcs) : L[4]);
     ucs = (do_l4 && !tcp) ? 0u : ucs;                     // uh_sum (L4 + 6)

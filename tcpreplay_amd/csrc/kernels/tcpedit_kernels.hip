@@ -880,7 +880,7 @@ struct FastArgs {
     uint32_t *list_cnt;  // this launch's count; list_cnt_next is zeroed for the next launch
     uint32_t *list_cnt_next;
     unsigned long long *counters;  // this launch's counter set (zeroed by the previous launch)
-    unsigned long long *slots;     // te_wave_tiles: per-block totals (4 words a block), summed by the host
+    unsigned long long *slots;     // te_wave_tiles: per-block totals (TE_WK_SLOT_WORDS a block), summed by the host
     unsigned long long *counters_next;  // te_wave_tiles: the other parity's counter set, zeroed for the next launch
     unsigned long long *ws_zero;
     uint64_t out_base, rec0;
@@ -891,7 +891,9 @@ struct FastArgs {
     uint32_t vlan_tag_word;                 // GROW: the 4 pushed bytes {TPID, TCI} as a LE dword
     uint32_t mtu;                           // SZ_MTU: --mtu; tile t's output at input offset - tcut[t]
     const long long *tcut;
-    uint32_t *grow_bad;                     // SZ_MTU: a tile whose cut differs from tcut's
+    uint32_t *grow_bad;                     // SZ_MTU / SZ_FUZZ: a tile whose cut differs from tcut's
+    const uint32_t *fz_state;               // SZ_FUZZ: each record's RNG state (te_fuzz_states)
+    uint32_t fz_factor;                     // SZ_FUZZ: --fuzz-factor
     uint32_t stream;                        // nontemporal span loads and output stores (a batch larger
                                             // than the 256 MiB Infinity Cache: read once, written once)
     // window mode (te_wave_tiles<..., WIN>: the record discovery fused into the edit)
@@ -1363,7 +1365,14 @@ __device__ __forceinline__ bool wk_solo(const te_tile_t &tl, uint32_t tb) {
 }
 
 // size-changing instances (SZ): the one length change every record takes
-enum : int { SZ_NONE = TE_SZ_NONE, SZ_GROW = TE_SZ_GROW, SZ_VDEL = TE_SZ_VDEL, SZ_EFCS = TE_SZ_EFCS, SZ_MTU = TE_SZ_MTU };
+enum : int {
+    SZ_NONE = TE_SZ_NONE,
+    SZ_GROW = TE_SZ_GROW,
+    SZ_VDEL = TE_SZ_VDEL,
+    SZ_EFCS = TE_SZ_EFCS,
+    SZ_MTU = TE_SZ_MTU,
+    SZ_FUZZ = TE_SZ_FUZZ
+};
 
 // caplen and len of the record header at LDS byte h (any alignment) + delta: the VLAN
 // push's +4 (tcpedit.c:112-113), the VLAN pop's or --efcs's -4 (tcpedit.c:78-84)
@@ -1567,39 +1576,49 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
     gout[q] = img[(uint32_t)(q - OS)];
 }
 
-#ifndef WK_MTU_PREV_DPP
-#define WK_MTU_PREV_DPP 0
-#endif
-// --mtu-trunc stores (SZ_MTU).  Record j keeps its first 16 + caplen'_j bytes; the records
-// sit back to back from the tile's output offset OS, record j at tile-relative output
-// offset op_j (a wave scan of the kept sizes) and input offset rel_j.  Per output chunk the
-// map K names the record holding its first byte (one mark per record + a prefix max, as
-// wk_chunk_map); bit 15 marks a chunk a record starts inside of.  Pass 1 stores every
-// other chunk as one unaligned 16-byte LDS read of its record (the cut moves records by
-// any byte count: five dwords, four funnel shifts).  Pass 2: each record's lane builds the
-// chunk it starts inside of from the previous record's tail and its own head.  The leading
-// bytes (OS up to the first 16-byte boundary) and the trailing ones (the last boundary up
-// to the tile's output end) go a byte a lane, so a tile writes only its own output bytes:
-// the next tile's first record header, which the last chunk would carry, is not known here.
-// P: K in u16 [0, 512), the record table {rel_j | op_j << 16} in u32 [256, 320).
-template <int NK>
+// --mtu-trunc and --fuzz-seed stores (SZ_MTU, SZ_FUZZ).  A kept record j keeps its first
+// 16 + caplen'_j bytes (keep false: a record that keeps nothing, a fuzz DROP); the kept
+// records sit back to back from the tile's output offset OS, record j at tile-relative
+// output offset op_j (a wave scan of the kept sizes) and input offset rel_j.  The kept
+// records are numbered 0.. in order (ballot + popcount) and only they take part: per output
+// chunk the map K names the kept record holding its first byte (one mark per record + a
+// prefix max, as wk_chunk_map); bit 15 marks a chunk a record starts inside of.  Pass 1
+// stores every other chunk as one unaligned 16-byte LDS read of its record (the cut moves
+// records by any byte count: five dwords, four funnel shifts).  Pass 2: each record's lane
+// builds the chunk it starts inside of from the previous kept record's tail and its own
+// head.  The leading bytes (OS up to the first 16-byte boundary) and the trailing ones (the
+// last boundary up to the tile's output end) go a byte a lane, so a tile writes only its
+// own output bytes: the next tile's first record header, which the last chunk would carry,
+// is not known here.  A kept record is >= 17 bytes, so a chunk meets at most two of them,
+// and the leading / trailing bytes lie in at most two.
+// P: K in u16 [0, 512), the kept-record table {rel_j | op_j << 16} in u32 [256, 320).
+// (The previous record's {rel, op} came from wave_prev DPP shifts once, under the EXEC mask
+// of the pass-2 branch: wrong bytes -- wave_dpp.hpp, DESIGN.md 4.13.  It is read from T.)
+// DROPS (SZ_FUZZ): records may keep nothing and a record may be as short as 17 bytes, so
+// the kept ones are numbered apart from their lanes and a tile may have no whole chunk;
+// without it (SZ_MTU) the kept records are lanes [0, npkt) and each is >= 50 bytes.
+template <int NK, bool DROPS>
 __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
                                              uint32_t out_len, uint32_t npkt, uint32_t my_rel, uint32_t my_op,
-                                             bool on, int lane, bool stream) {
-#if WK_MTU_PREV_DPP == 5
-    const uint32_t prel_e = wave_prev(my_rel), pop_e = wave_prev(my_op);
-#endif
+                                             bool keep, int lane, bool stream) {
+    if (DROPS && out_len == 0) return;  // (wave-uniform: every record dropped)
+    uint32_t ci = (uint32_t)lane, nk = npkt;  // this record's kept number; the kept records
+    if constexpr (DROPS) {
+        const unsigned long long km = __ballot(keep);
+        ci = (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+        nk = (uint32_t)__popcll(km);
+    }
     const uint64_t C0 = (OS + 15) & ~15ull;
     const uint32_t o0 = (uint32_t)(C0 - OS);
-    const uint32_t nfull = (out_len - o0) >> 4;  // >= 2: a record here is >= 50 bytes
+    const uint32_t nfull = (out_len - o0) >> 4;  // (out_len >= 17 > o0; MTU: nfull >= 2)
     uint16_t *K = (uint16_t *)P;
     uint32_t *T = P + 256;
     *(uint4 *)(K + 8 * lane) = make_uint4(0, 0, 0, 0);
-    if (on) T[lane] = my_rel | (my_op << 16);
+    if (keep) T[ci] = my_rel | (my_op << 16);
     WK_LANES_SYNC();
-    if (on) {  // the first chunk starting at or after op_j (record 0: chunk 0)
+    if (keep) {  // the first chunk starting at or after op_j (the first kept record: chunk 0)
         const uint32_t cj = my_op <= o0 ? 0u : (my_op - o0 + 15u) >> 4;
-        if (cj <= nfull) K[cj] = (uint16_t)(lane + 1);
+        if (cj <= nfull) K[cj] = (uint16_t)(ci + 1);
     }
     WK_LANES_SYNC();
     {  // prefix max over K, 8 entries a lane
@@ -1615,52 +1634,34 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
             make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
     }
     WK_LANES_SYNC();
-    // record j > 0 starting inside a chunk: K there already names record j - 1 (value j)
-    const uint32_t x = (on && lane > 0) ? my_op - o0 : 16u, c1 = x >> 4, t1 = x & 15u;
-    if (t1 != 0 && c1 < nfull) K[c1] = (uint16_t)(lane | 0x8000);
+    // kept record j > 0 starting inside a chunk: K there already names kept record j - 1 (value j)
+    const uint32_t x = (keep && ci > 0) ? my_op - o0 : 16u, c1 = x >> 4, t1 = x & 15u;
+    if (t1 != 0 && c1 < nfull) K[c1] = (uint16_t)(ci | 0x8000);
     WK_LANES_SYNC();
-    uint32_t kv[NK], w[NK][4];
+    if (!DROPS || nfull) {  // (wave-uniform)
+        uint32_t kv[NK], w[NK][4];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nfull - 1u)];
+        for (int k = 0; k < NK; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nfull - 1u)];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) {  // lanes past the output repeat its last full chunk
-        const uint32_t cc = umin32((uint32_t)lane + 64u * k, nfull - 1u);
-        const uint32_t e = T[(kv[k] & 0x7fu) - 1u];
-        const uint4 v = read16(S, ib + (e & 0xffffu) + o0 + 16u * cc - (e >> 16));
-        w[k][0] = v.x;
-        w[k][1] = v.y;
-        w[k][2] = v.z;
-        w[k][3] = v.w;
-    }
-    WK_LANES_SYNC();
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-        if ((kv[k] >> 15) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
-    {  // pass 2: the chunk record j starts inside of (the previous record's {rel, op} from T:
-       // taken with wave_prev DPP shifts instead, the first bytes came from the wrong place)
-#if WK_MTU_PREV_DPP == 1  // (diagnostic variants: the previous record's {rel, op} by wave_prev, every lane)
-        const uint32_t prel = wave_prev(my_rel), pop = wave_prev(my_op);
-#elif WK_MTU_PREV_DPP == 3  // (... with wait states before the DPP reads)
-        asm volatile("s_nop 7\n s_nop 7" ::: "memory");
-        const uint32_t prel = wave_prev(my_rel), pop = wave_prev(my_op);
-#elif WK_MTU_PREV_DPP == 4  // (... through ds_bpermute instead of DPP)
-        const uint32_t prel = (uint32_t)__shfl_up((int)my_rel, 1), pop = (uint32_t)__shfl_up((int)my_op, 1);
-#elif WK_MTU_PREV_DPP == 5  // (... taken on entry, before the chunk map)
-        const uint32_t prel = prel_e, pop = pop_e;
-#else
-        const uint32_t ep = T[lane > 0 ? lane - 1 : 0], prel0 = ep & 0xffffu, pop0 = ep >> 16;
-#endif
-        const uint32_t q = o0 + 16u * c1;
-        const bool p2 = t1 != 0 && c1 < nfull;  // (lane 0, off lanes: x = 16, so t1 = 0)
-#if WK_MTU_PREV_DPP == 2  // (... or by wave_prev in the lanes that store a pass-2 chunk only)
-        uint32_t prel = 0, pop = 0;
-        if (p2) {
-            prel = wave_prev(my_rel);
-            pop = wave_prev(my_op);
+        for (int k = 0; k < NK; ++k) {  // lanes past the output repeat its last full chunk
+            const uint32_t cc = umin32((uint32_t)lane + 64u * k, nfull - 1u);
+            const uint32_t e = T[(kv[k] & 0x7fu) - 1u];
+            const uint4 v = read16(S, ib + (e & 0xffffu) + o0 + 16u * cc - (e >> 16));
+            w[k][0] = v.x;
+            w[k][1] = v.y;
+            w[k][2] = v.z;
+            w[k][3] = v.w;
         }
-#elif WK_MTU_PREV_DPP == 0
-        const uint32_t prel = prel0, pop = pop0;
-#endif
+        WK_LANES_SYNC();
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+            if ((kv[k] >> 15) == 0u)
+                wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
+    }
+    {  // pass 2: the chunk kept record j starts inside of (the previous one's {rel, op} from T)
+        const uint32_t ep = T[ci > 0 ? ci - 1 : 0], prel = ep & 0xffffu, pop = ep >> 16;
+        const uint32_t q = o0 + 16u * c1;
+        const bool p2 = t1 != 0 && c1 < nfull;  // (the first kept record, the others: x = 16, t1 = 0)
         // (the lanes that store nothing read the image start: every address stays in it)
         const uint4 va = read16(S, p2 ? ib + prel + (q - pop) : ib);
         const uint4 vb = read16(S, p2 ? ib + my_rel - t1 : ib);
@@ -1678,13 +1679,13 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
         const uint32_t q0t = o0 + 16u * nfull, ntr = out_len - q0t;
         const uint32_t qb = q0t + umin32((uint32_t)lane, ntr ? ntr - 1u : 0u);
         const uint32_t j = (K[nfull] & 0x7fu) - 1u;
-        const uint32_t e1 = T[umin32(j + 1u, npkt - 1u)];
-        const uint32_t e = (j + 1u < npkt && qb >= (e1 >> 16)) ? e1 : T[j];
+        const uint32_t e1 = T[umin32(j + 1u, nk - 1u)];
+        const uint32_t e = (j + 1u < nk && qb >= (e1 >> 16)) ? e1 : T[j];
         const uint8_t v = S[ib + (e & 0xffffu) + qb - (e >> 16)];
         if ((uint32_t)lane < ntr) gout[OS + qb] = v;
     }
-    // the leading bytes: record 0's (rel 0, op 0)
-    if ((uint32_t)lane < o0) gout[OS + (uint32_t)lane] = S[ib + (uint32_t)lane];
+    // the leading bytes: the first kept record's (op 0; MTU: record 0, rel 0)
+    if ((uint32_t)lane < o0) gout[OS + (uint32_t)lane] = S[ib + (DROPS ? T[0] & 0xffffu : 0u) + (uint32_t)lane];
 }
 
 // big-endian / nanosecond input: a record header in host order and microseconds
@@ -1722,11 +1723,15 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 #ifndef TE_WIN_BLOCKS
 #define TE_WIN_BLOCKS TE_WK_MIN_BLOCKS  // window mode: blocks per CU (its VGPR budget)
 #endif
-__global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
+// (SZ_FUZZ: 4 blocks per CU, 3 with the address maps -- at the lean instances' 5 / the others'
+//  4 the fuzz step's registers spill)
+__global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
+                                       : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_MIN_BLOCKS - 1 : TE_WK_MIN_BLOCKS)
+                                                       : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
-    constexpr bool MTU = SZ == SZ_MTU;
+    constexpr bool MTU = SZ == SZ_MTU, FUZZ = SZ == SZ_FUZZ;
     // VLAN pop: the window reaches 4 input bytes further (the packet' view skips the tag)
     constexpr int XW = VDEL ? 1 : 0;
     __shared__ __attribute__((aligned(16))) uint8_t SB[WK_NW][WK_IMG];
@@ -1734,7 +1739,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     // per-run tables: copied only by instances whose option groups read them
     __shared__ __attribute__((aligned(16))) uint8_t cfg_raw[WkCfg<F>::reads ? sizeof(te_dev_cfg_t) : 16];
     const te_dev_cfg_t &cfg = *(const te_dev_cfg_t *)cfg_raw;
-    __shared__ unsigned long long red[WK_NW][4];
+    __shared__ unsigned long long red[WK_NW][6];
     __shared__ uint32_t RELB[WIN ? WK_NW : 1][WIN ? WIN_REL : 1];  // window mode: record offsets
     const int tid = threadIdx.x;
     int lane = tid & 63;
@@ -1754,8 +1759,8 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     const bool swp = a.in_swapped != 0, nsec = a.in_nsec != 0, conv = swp || nsec;
     const bool explicit_dir = a.fixed_dir >= 0;
     // the next record's header rides along (conversion; GROW / SHRINK: its caplen/len +- 4)
-    // (--mtu-trunc: a tile stores only its own output bytes, so nothing rides along)
-    const uint32_t extra = (conv || (SZ != SZ_NONE && !MTU)) ? 16u : 0u;
+    // (--mtu-trunc, --fuzz-seed: a tile stores only its own output bytes, so nothing rides along)
+    const uint32_t extra = (conv || (SZ != SZ_NONE && !MTU && !FUZZ)) ? 16u : 0u;
     g_cu8 *gin = (g_cu8 *)a.in;
     g_u8 *gout = (g_u8 *)a.out + ((int64_t)a.out_base - (int64_t)a.rec0);
     const TE_AS_GLOBAL uint16_t *lut = (const TE_AS_GLOBAL uint16_t *)a.portlut;
@@ -1771,13 +1776,14 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
         te_tile_t tl;
         uint4 v0, v1, v2, v3, v4, v5, v6, v7;
         uint32_t rel, dirb;
-        bool dirv;  // (the cache byte exists: idx < dirbits_len)
+        bool dirv;     // (the cache byte exists: idx < dirbits_len)
+        uint32_t fzs;  // FUZZ: the record's RNG state
     };
 #define WK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
     const uint32_t W = gridDim.x * WK_NW;
     const uint32_t w0 = blockIdx.x * WK_NW + wid;
     const uint32_t n_tiles = a.n_tiles;
-    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0, c_cut = 0;
+    unsigned long long c_pkts = 0, c_bytes = 0, c_edited = 0, c_cut = 0, c_drop = 0, c_soft = 0;
 #if TE_WK_STAMPS
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, last_ = __builtin_amdgcn_s_memtime(), ntl = 0;
     unsigned long long fph[5] = {0, 0, 0, 0, 0};  // (window mode: inside the record discovery)
@@ -1802,6 +1808,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
 #undef WK_LD
         const uint32_t k_ = tl.first_pkt + umin32((uint32_t)lane, tl.npkt - 1u);
         R.rel = pkt_rel[k_];
+        R.fzs = FUZZ ? a.fz_state[k_] : 0u;
         if (a.dirbits) {  // in flight with the span (no consumer here: its wait would drain the span)
             const uint64_t ix_ = (a.pkt_base + k_) >> 2;
             R.dirb = a.dirbits[ix_ < a.dirbits_len ? ix_ : 0];
@@ -1822,7 +1829,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
     // edit and store tile t, whose span is in the LDS image; a tile the lane cannot
     // finish is listed for the generic lane and stores nothing
     auto edit = [&](const uint32_t t, const te_tile_t &tile, const uint32_t my_rel, const uint32_t my_dirb,
-                    const bool my_dirv) __attribute__((always_inline)) {
+                    const bool my_dirv, const uint32_t my_fzs) __attribute__((always_inline)) {
             const uint32_t npkt = tile.npkt;
             const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
             const uint32_t g0 = (uint32_t)(G0 - A0);
@@ -1853,6 +1860,36 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                     caplen = bswap32(caplen);
                     len = bswap32(len);
                 }
+            }
+            // --fuzz-seed (SZ_FUZZ): fuzzing() for a record its draw picks (tcpedit.c:250-258,
+            // fuzzing.c:80-199), before the window is read.  The lane plans it for the header
+            // shape phase A takes (Ethernet II, IPv4 IHL 5 or IPv6, TCP or UDP: a packet of
+            // another shape sends the tile to the generic lane, which plans it itself).  A byte
+            // run lands in the image (a changed record is checksummed from scratch: fuzzing()'s
+            // 1 is a needtorecalc); a cut (DROP / REDUCE) fails the second decode (a soft error,
+            // tcpedit.c:95-99), so the record is written unedited at its first nl bytes.
+            bool fz_cut = false, fz_recalc = false;
+            uint32_t fz_nl = 0;
+            if constexpr (FUZZ) {
+                uint32_t s_ = my_fzs;
+                const uint32_t r = tcpr_random_dev(s_);
+                if (on && r % a.fz_factor == 0u) {
+                    const bool v6 = S[p + 12] == 0x86u && S[p + 13] == 0xDDu;
+                    const uint32_t proto = v6 ? S[p + 20] : S[p + 23];
+                    const int l3 = v6 ? 54 : 34, l4h = proto == 6u ? 20 : 8;
+                    const FzPlan f = fuzz_plan_l4(r, l3 + l4h, l3 - l4h, caplen, len);
+                    for (int i = 0; i < f.n; ++i) {  // (bytes past caplen: the reference's buffer, never output)
+                        const uint32_t j = (uint32_t)(f.from + i);
+                        if (j < caplen) {
+                            uint8_t &b = S[p + j];
+                            b = f.how == 0 ? (uint8_t)0 : f.how == 1 ? (uint8_t)0xff : (uint8_t)(b ^ f.x);
+                        }
+                    }
+                    fz_cut = f.cut;
+                    fz_recalc = f.ret != 0 && !f.cut;
+                    fz_nl = f.nl;
+                }
+                WK_LANES_SYNC();  // the window reads below see every lane's run
             }
             // 21 dword-aligned reads (paired into ds_read2_b32) and a funnel shift align
             // the window to packet offset -2; each H[i] can take d[i]'s register
@@ -1905,7 +1942,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
             st.dirty = 0;
             // phase A runs on every lane (it has no divergent branches); only lanes that edit
             // a packet keep its verdict and state
-            const bool edit = on && !nosend;
+            const bool edit = on && !nosend && !fz_cut;
 #if TE_WK_EXP == 2  // diagnostics only: window reads, no edit
             bool ok = true;
             {
@@ -1917,9 +1954,9 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
             }
 #else
             bool ok = MTU ? fl::phase_a<F>(H, caplen, len, part, dir, cfg, kn, a.v6_ok != 0, lut, st, mcut ? ecap : 0u)
-                          : fl::phase_a<F>(H, ecap, elen, part, dir, cfg, kn, a.v6_ok != 0, lut, st);
+                          : fl::phase_a<F>(H, ecap, elen, part, dir, cfg, kn, a.v6_ok != 0, lut, st, 0u, fz_recalc);
             if constexpr (VDEL) ok = ok && tagged;
-            ok = ok || !edit;
+            ok = ok || !(edit || fz_cut);  // (a cut record's plan assumed the shape too)
             // GROW / SHRINK: a record written unedited keeps its size; the scan placement takes it
             if constexpr (SZ != SZ_NONE) ok = ok && !nosend;
             st.tail = st.tail && edit;
@@ -1965,7 +2002,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
             // below are scalar branches.  A lane that did not change such a dword rewrites
             // it with its own packet's bytes (never past caplen), which is harmless.
             uint32_t todo = 0;
-            if (on && !nosend) {
+            if (edit) {
                 todo = st.dirty;
                 // VLAN pop: packet' dword i >= 4 is input dword i + 1; input dword 4 (the popped
                 // TCI and the inner type field, unchanged) is never dirty
@@ -1974,10 +2011,10 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
             }
             todo = wave_or(todo);
             // every written dword ends by packet offset 78 <= caplen + 16: no per-dword test
-            const bool wide = !__ballot(on && !nosend && ecap < (uint32_t)fl::WEND - 16);
+            const bool wide = !__ballot(edit && ecap < (uint32_t)fl::WEND - 16);
             // ---- phase B + write-back of the dwords phase A touched ----
             if (on) {
-                if (!nosend) {
+                if (edit) {
                     uint32_t tail = 0;
                     if (st.tail) {
                         const uint32_t pv = p + (VDEL ? 4u : 0u);  // packet' byte x is LDS byte pv + x
@@ -2011,9 +2048,15 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 if constexpr (MTU) {
                     if (mcut) hdr_put(S, r0, ecap);
                 }
+                if constexpr (FUZZ) {
+                    if (fz_cut && fz_nl) hdr_put(S, r0, fz_nl);
+                }
                 // (window mode: no record numbers; every record it finishes is status 0, which
                 // the caller writes for the whole batch)
-                if (!WIN) ((g_u8 *)a.status)[tile.first_pkt + lane] = nosend ? (uint8_t)TE_ST_NOSEND : (uint8_t)0;
+                const uint8_t stb = nosend   ? (uint8_t)TE_ST_NOSEND
+                                    : fz_cut ? (uint8_t)(TE_ST_RC_SOFT | (fz_nl ? 0 : TE_ST_ZEROCAP))
+                                             : (uint8_t)0;
+                if (!WIN) ((g_u8 *)a.status)[tile.first_pkt + lane] = stb;
             }
             if (conv && lane == (int)(npkt & 63u)) conv_hdr(S + LDS_FRONT + g0 + tile.span_len, swp, nsec);
             if (GROW && lane == (int)(npkt & 63u)) hdr_add4(S, LDS_FRONT + g0 + tile.span_len, 4u);
@@ -2031,17 +2074,22 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
                 wk_store_sized<false>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
                                       Dj - 4u * (uint32_t)lane, on, 0u, lane, stream && WK_SIZED_STREAM);
-            } else if constexpr (MTU) {
+            } else if constexpr (MTU || FUZZ) {
                 // the kept sizes -> output offsets; the tile's output at input offset - tcut[t]
-                const uint32_t osz = on ? 16u + ecap : 0u;
+                // (FUZZ: a dropped record keeps nothing, not even its header)
+                const uint32_t osz = !on ? 0u : !FUZZ ? 16u + ecap : !fz_cut ? 16u + caplen : fz_nl ? 16u + fz_nl : 0u;
                 const uint32_t incl = wave_scan_add(osz);
                 const uint32_t out_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 const long long k0 = a.tcut[t], k1 = a.tcut[t + 1];
                 const uint32_t cut = tile.span_len - out_len;
                 if (lane == 0 && (long long)cut != k1 - k0) atomicOr(a.grow_bad, 1u);  // (a stale prediction)
                 c_cut += cut;
-                wk_store_mtu<WK_KL + 1>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len, npkt,
-                                        my_rel, incl - osz, on, lane, stream && WK_MTU_STREAM);
+                wk_store_mtu<WK_KL + 1, FUZZ>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len,
+                                              npkt, my_rel, incl - osz, osz != 0u, lane, stream && WK_MTU_STREAM);
+                if constexpr (FUZZ) {
+                    c_drop += (unsigned long long)__popcll(__ballot(on && fz_cut && fz_nl == 0u));
+                    c_soft += (unsigned long long)__popcll(__ballot(on && fz_cut));
+                }
             } else {
                 const uint64_t C0 = (G0 + 15) & ~15ull;
                 const uint32_t nown = (uint32_t)((((E + 15) & ~15ull) - C0) >> 4);  // >= 1 (a 16-byte header)
@@ -2073,10 +2121,10 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
 #if TE_WK_STAMPS
             ++ntl;
 #endif
-            const uint32_t n_nosend = (uint32_t)__popcll(__ballot(nosend));
+            const uint32_t n_noedit = (uint32_t)__popcll(__ballot(on && !edit));
             c_pkts += npkt;
             c_bytes += tile.span_len;
-            c_edited += npkt - n_nosend;
+            c_edited += npkt - n_noedit;
     };
     // one tile with DEPTH spans in flight.  Rf holds tile t's descriptor and per-lane
     // values (its chunks are in LDS already) and is reloaded with tile t + DEPTH * W;
@@ -2089,12 +2137,12 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
         asm volatile("" : "+v"(lane));
 #endif
         const te_tile_t tile = Rf.tl;
-        const uint32_t my_rel = Rf.rel, my_dirb = Rf.dirb;
+        const uint32_t my_rel = Rf.rel, my_dirb = Rf.dirb, my_fzs = Rf.fzs;
         const bool my_dirv = Rf.dirv;
         if (t + DEPTH * W < n_tiles) issue(Rf, dpre);  // in flight while this tile is edited and stored
         if (t + (DEPTH + 1) * W < n_tiles) dpre = tiles[t + (DEPTH + 1) * W];
         WK_STAMP(0)  // loop top + loads issued
-        edit(t, tile, my_rel, my_dirb, my_dirv);
+        edit(t, tile, my_rel, my_dirb, my_dirv, my_fzs);
         WK_STAMP(4)  // stores issued
         if (t + W < n_tiles) fill(Rn);
         WK_LANES_SYNC();  // the next tile's lanes read what every lane filled
@@ -2179,7 +2227,7 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
                 // the tile's image: its span start at S + LDS_FRONT + (span_off & 15)
                 S = IMG + (uint32_t)((t0 & ~15ull) - fw.A0);
                 WK_LANES_SYNC();
-                edit(k, tl, my_rel, 0u, false);
+                edit(k, tl, my_rel, 0u, false, 0u);
                 WK_LANES_SYNC();
                 WK_STAMP(4)  // (window mode: the edit's stores)
                 s0 += len;
@@ -2217,13 +2265,17 @@ __global__ void __launch_bounds__(WKB, WIN ? TE_WIN_BLOCKS : WkCfg<F>::blocks) t
         red[wid][1] = c_bytes;
         red[wid][2] = c_edited;
         red[wid][3] = c_cut;
+        red[wid][4] = c_drop;
+        red[wid][5] = c_soft;
     }
     __syncthreads();
-    if (tid < 4) {  // this block's totals; the generic kernel's block 0 adds them up
+    if (tid < TE_WK_SLOT_WORDS) {  // this block's totals (the host adds them up)
         unsigned long long s = 0;
+        if (tid < 6) {
 #pragma unroll
-        for (int w = 0; w < WK_NW; ++w) s += red[w][tid];
-        a.slots[4 * blockIdx.x + tid] = s;
+            for (int w = 0; w < WK_NW; ++w) s += red[w][tid];
+        }
+        a.slots[TE_WK_SLOT_WORDS * blockIdx.x + tid] = s;
     }
 }
 
@@ -2276,9 +2328,9 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
         if (w.acc && b == 0) {  // the chunk's totals and the edit's verdict bits
             unsigned long long p = 0, by = 0, e = 0;
             for (uint32_t i = threadIdx.x; i < w.nslots; i += 256) {
-                p += w.slots[4 * i];
-                by += w.slots[4 * i + 1];
-                e += w.slots[4 * i + 2];
+                p += w.slots[TE_WK_SLOT_WORDS * i];
+                by += w.slots[TE_WK_SLOT_WORDS * i + 1];
+                e += w.slots[TE_WK_SLOT_WORDS * i + 2];
             }
             if (p) atomicAdd(&w.acc[0], p);
             if (by) atomicAdd(&w.acc[1], by);
@@ -2687,7 +2739,9 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
     X(TE_FF_ALL, 1, SZ_GROW) X(TE_FF_ALLH, 1, SZ_GROW) X(TE_FF_ALLX, 1, SZ_GROW)                      \
     X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)  \
-    X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)
+    X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)                                                          \
+    X(TE_FF_INCR, 1, SZ_FUZZ) X(0u, 1, SZ_FUZZ) X(TE_FF_RWIP | TE_FF_INCR, 1, SZ_FUZZ)                  \
+    X(TE_FF_RWIP, 1, SZ_FUZZ)
 #define TE_WIN_INSTANCES(X)                                                                           \
     X(0u, 1, SZ_NONE) X(TE_FF_SEED, 1, SZ_NONE) X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE)             \
     X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE) X(TE_FF_SEED | TE_FF_INCR, 1, SZ_NONE)          \
@@ -2807,7 +2861,7 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.static_shrink = (uint32_t)L->static_shrink;
     a.grow_bad = L->grow_bad;
     a.tcut = (const long long *)L->tcut;
-    a.static_mtu = (uint32_t)L->static_mtu;
+    a.static_mtu = (uint32_t)(L->static_mtu || L->static_fz);  // (placement by tcut)
     a.tile_list = nullptr;
     a.list_cnt = nullptr;
     a.counters_next = nullptr;
@@ -3196,12 +3250,125 @@ extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ===========================================================================
+// --fuzz-seed on the wave lane (te_launch_t.static_fz).  A record's RNG draw depends on how
+// many records before it reach the fuzz step (te_fuzz_states), so the launch finds them
+// first.  te_fuzz_reach reads each record's header (one wave per tile, a lane per record)
+// and marks the records of the shape the wave lane edits -- Ethernet II, IPv4 with IHL 5 or
+// IPv6 with TCP or UDP next, the network header captured: under the configs static_fz takes
+// (no edit before the fuzz step but the en10mb decode and re-encode) such a record always
+// reaches it (tcpedit.c:89-248: decode, encode, the IP header and L4 checks).  A tile holding
+// any other record is listed, and the generic kernel's reach pass decides that tile.  It
+// also zeroes the ticket that reach pass takes.
+// ===========================================================================
+__global__ void __launch_bounds__(256) te_fuzz_reach(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel,
+                                                     uint32_t n, uint8_t *status, uint32_t *list, uint32_t *list_cnt,
+                                                     unsigned int *ticket) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (t >= n) return;  // (wave-uniform)
+    const te_tile_t tl = tiles[t];
+    bool open = false;
+    for (uint32_t k = lane; k < tl.npkt; k += 64u) {
+        const uint8_t *r = in + tl.span_off + pkt_rel[tl.first_pkt + k];
+        const uint32_t cap = ld32(r + 8);
+        const uint8_t *d = r + 16;
+        const uint32_t et = cap >= 14 ? ((uint32_t)d[12] << 8) | d[13] : 0u;
+        const bool v4 = et == 0x0800u && cap >= 34 && d[14] == 0x45u;
+        const bool v6 = et == 0x86DDu && cap >= 54 && (d[20] == 6u || d[20] == 17u);
+        if (v4 || v6) status[tl.first_pkt + k] = 1;
+        else open = true;
+    }
+    if (__ballot(open) && lane == 0) list[atomicAdd(list_cnt, 1u)] = t;
+}
+
+// the bytes each tile's records lose to fuzzing() (DROP: the whole record; REDUCE: its tail),
+// from the reach flags and RNG states, as te_mtu_tile_cut lays them out.  With no edit before
+// the fuzz step but the en10mb decode and re-encode, fuzzing() sees the input bytes, so
+// fuzz_plan on them is its choice (every tile checks its output total against this).
+__global__ void __launch_bounds__(256) te_fuzz_tile_cut(const uint8_t *in, const te_tile_t *tiles,
+                                                        const uint16_t *pkt_rel, uint32_t n, const uint8_t *status,
+                                                        const uint32_t *states, const te_dev_cfg_t *cfg,
+                                                        long long *pre, long long *bsum) {
+    __shared__ long long c[64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t0 = blockIdx.x * 64u;
+    const uint32_t factor = cfg->fuzz_factor;
+    for (uint32_t j = w; j < 64u; j += 4u) {
+        const uint32_t t = t0 + j;
+        long long s = 0;
+        if (t < n) {
+            const te_tile_t tl = tiles[t];
+            for (uint32_t k = lane; k < tl.npkt; k += 64u) {
+                const uint32_t i = tl.first_pkt + k;
+                if (!(status[i] & 1u)) continue;
+                uint32_t st = states[i];
+                const uint32_t r = tcpr_random_dev(st);
+                if (r % factor) continue;
+                const uint8_t *rec = in + tl.span_off + pkt_rel[i];
+                const uint32_t cap = ld32(rec + 8), len = ld32(rec + 12);
+                const FzPlan f = fuzz_plan(rec + 16, cap, len, cap, *cfg, r);
+                if (f.cut) s += f.nl ? (long long)(cap - f.nl) : 16ll + cap;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) c[j] = s;
+    }
+    __syncthreads();
+    if (w == 0) {
+        const long long v = c[lane];
+        long long x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_up(x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (t0 + lane < n) pre[t0 + lane] = x - v;
+        if (lane == 63) bsum[blockIdx.x] = x;
+    }
+}
+
+// static_fz's prelude: the reach (header kernel + the generic reach pass over the tiles it
+// listed), the RNG states, the placement prediction (tcut)
+static int fuzz_wave_prelude(const te_launch_t *L, const LaunchArgs &a, hipStream_t stream) {
+    if (!L->fuzz_states || !L->fuzz_blk || !L->fuzz_words || !L->fz_list || !L->tcut || !L->tcut_raw ||
+        L->n_pkts == 0 || L->n_tiles == 0)
+        return -1;
+    uint32_t *cnt = L->fz_list + L->n_tiles;
+    if (hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+    hipLaunchKernelGGL(te_fuzz_reach, dim3((L->n_tiles + 3u) / 4u), dim3(256), 0, stream, L->in, L->tiles,
+                       L->pkt_rel, L->n_tiles, L->status, L->fz_list, cnt, L->ticket);
+    LaunchArgs pa = a;
+    pa.tile_list = L->fz_list;
+    pa.list_cnt = cnt;
+    pa.counters_next = nullptr;
+    pa.fuzz_mode = TE_FUZZ_PROBE;
+    launch_generic(true, false, false, resident_blocks(0), stream, pa);
+    const uint32_t nblk = (L->n_pkts + FZ_PER_BLOCK - 1) / FZ_PER_BLOCK;
+    hipLaunchKernelGGL(te_fuzz_count, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status, L->n_pkts,
+                       L->fuzz_blk);
+    hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words, 1);
+    hipLaunchKernelGGL(te_fuzz_states, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status, L->n_pkts,
+                       (const uint32_t *)L->fuzz_blk, (const uint32_t *)L->fuzz_words, L->fuzz_states);
+    const uint32_t nb = (L->n_tiles + 63u) / 64u;
+    long long *pre = (long long *)L->tcut, *bsum = (long long *)L->tcut_raw;
+    hipLaunchKernelGGL(te_fuzz_tile_cut, dim3(nb), dim3(256), 0, stream, L->in, L->tiles, L->pkt_rel, L->n_tiles,
+                       (const uint8_t *)L->status, (const uint32_t *)L->fuzz_states, L->cfg, pre, bsum);
+    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    hipLaunchKernelGGL(te_mtu_cut_add, dim3((L->n_tiles + 1u + 255u) / 256u), dim3(256), 0, stream, pre,
+                       (const long long *)bsum, L->n_tiles);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
     LaunchArgs a;
     fill_args(a, L);
     hipError_t e;
     const bool fast = L->fast &&
-                      ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink || L->static_mtu) &&
+                      ((L->static_off && !L->slot_layout) || L->static_grow || L->static_shrink || L->static_mtu ||
+                       L->static_fz) &&
                       L->n_tiles > 0;
     if (L->win) {  // window mode: the wave lane finds its records; then the chain check
         if (!L->cfg_host || L->in_swapped || L->in_nsec || L->dirbits || L->nwin == 0) return -1;
@@ -3280,6 +3447,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (fast && !L->generic_only) {
+        if (L->static_fz && fuzz_wave_prelude(L, a, stream) != 0) return -1;
         // the fast kernel zeroes the generic kernel's words itself: no memset launch
         FastArgs f;
         f.cfg = L->cfg;
@@ -3324,9 +3492,14 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.mtu = L->static_mtu ? L->mtu : 0u;
         f.tcut = (const long long *)L->tcut;
         f.grow_bad = L->grow_bad;
-        if (L->static_mtu && (!L->tcut || L->fast_kind != TE_FAST_WAVE)) return -1;
+        f.fz_state = L->static_fz ? L->fuzz_states : nullptr;
+        f.fz_factor = ch->fuzz_factor ? ch->fuzz_factor : 1u;
+        if ((L->static_mtu || L->static_fz) && (!L->tcut || L->fast_kind != TE_FAST_WAVE)) return -1;
         const void *wfn = nullptr;
-        const int wk = wave_pick(fast_feat(ch), grow ? SZ_GROW : L->static_mtu ? SZ_MTU : L->static_shrink);
+        const int wk = wave_pick(fast_feat(ch), grow            ? SZ_GROW
+                                                : L->static_mtu ? SZ_MTU
+                                                : L->static_fz  ? SZ_FUZZ
+                                                                : L->static_shrink);
         if (wk < 0) return -1;
         wfn = wave_inst[wk].fn;
         const bool wave = L->fast_kind == TE_FAST_WAVE;
@@ -3355,6 +3528,10 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         a.tile_list = L->tile_list;
         a.list_cnt = L->list_cnt + (L->parity & 1);
         a.counters_next = (unsigned long long *)L->counters_next;
+        if (L->static_fz) {  // ... fuzzing them with the states the prelude drew
+            a.fuzz_mode = TE_FUZZ_APPLY;
+            a.fuzz_state = L->fuzz_states;
+        }
     } else {
         // one memset per launch: error words, ticket, counters, look-back granules
         e = hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream);

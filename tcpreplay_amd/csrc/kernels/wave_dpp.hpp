@@ -6,11 +6,16 @@
 //
 // Call these where every lane of the wave is active (wave-uniform control flow).  A DPP
 // operand read from a lane that EXEC has switched off does not return that lane's value:
-// with bound_ctrl (as here) it reads 0 -- measured on MI355X by tests/test_dpp.py, whose
-// probe kernels (tests/dpp/dpp_probe.hip) run these helpers under full and divergent EXEC
-// against an LDS shift.  (The first wk_store_mtu read the previous record's {rel, op}
-// with wave_prev; its pass-2 chunks took their first bytes from byte 0 of the tile image,
-// what a 0 from a switched-off source lane gives -- the values now come from an LDS table.)
+// with bound_ctrl (as here) it reads 0.  A DPP op right behind the SALU write of EXEC that
+// ends a divergent branch reads the lanes the new EXEC has on (no wait states needed).
+//
+// The product builds with the compiler's DPP combine off (-mllvm -amdgpu-dpp-combine=false,
+// tcpreplay_amd/csrc/Makefile): the combine folds a DPP mov into the VALU op that uses it,
+// and on MI355X a folded "reversed" VOP2 op applies the DPP lane pattern to src1 instead of
+// src0 -- v_subrev_u32_dpp d, a, b wave_shr:1 gives prev(b) - a, not b - prev(a), and
+// v_lshlrev_b32_dpp likewise (tests/test_dpp.py, the probe kernels in tests/dpp/).  That was
+// the first wk_store_mtu's wrong output: its pass-2 `q - pop` with pop = wave_prev(my_op)
+// became v_subrev_u32_dpp, and the chunks took their first bytes from the wrong place.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 while [ $# -ge 2 ]; do
     name=$1; flags=$2; shift 2
     make -s -j8 -C "$CS" OBJDIR="$CS/build/var_$name/" LIB="$OUT/libtcpedit_hip_$name.so" \
-        HIPFLAGS="-O3 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-parameter $flags" \
+        HIPFLAGS="-O3 -gline-tables-only -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-parameter -mllvm -amdgpu-dpp-combine=false $flags" \
         CFLAGS="-O2 -g -std=gnu11 -fPIC -D__HIP_PLATFORM_AMD__ -Wno-unused-parameter $flags" \
         "$OUT/libtcpedit_hip_$name.so"
     echo "built $OUT/libtcpedit_hip_$name.so ($flags)"
