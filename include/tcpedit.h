@@ -357,6 +357,12 @@ int tcpedit_rewrite_pcap(tcpedit_t *tcpedit, const void *in, size_t in_len, cons
  * page-locked for the call.  Same output bytes and return codes as tcpedit_rewrite_pcap. */
 int tcpedit_rewrite_pcap_pipelined(tcpedit_t *tcpedit, const void *in, size_t in_len, const void *cache,
                                    size_t cache_len, void *out, size_t out_cap, size_t *out_len, size_t chunk_bytes);
+/* pipelined calls of this context whose window mode (records found on the device) missed --
+ * a chunk's chain miss, a zero-length record, a record reaching more than 64 KiB past its
+ * chunk, a record left to the generic lane -- so the call redid the capture on the exact
+ * (device-index) pipeline: same output, about twice the time (TCPEDIT_HIP_PIPE_TRACE names
+ * the verdict) */
+uint64_t tcpedit_pipeline_fallbacks(tcpedit_t *tcpedit);
 /* worst-case output image size of `in` under the context's options (host-only walk) */
 size_t tcpedit_output_bound(tcpedit_t *tcpedit, const void *in, size_t in_len);
 /* page-locked host buffers (a capture read straight into one needs no per-call locking) */

@@ -78,6 +78,7 @@ def load():
         "tcpedit_batch_run_fused": (c_int, [vp, vp]),
         "tcpedit_batch_time_fused": (c_int, [vp, vp, c_int, ctypes.POINTER(ctypes.c_double)]),
         "tcpedit_batch_fused_fallbacks": (ctypes.c_uint64, [vp]),
+        "tcpedit_pipeline_fallbacks": (ctypes.c_uint64, [vp]),
         "tcpedit_batch_update_input": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_set_prefix": (c_int, [vp, vp, vp, sz]),
         "tcpedit_batch_result": (c_int, [vp, ctypes.POINTER(BatchResult)]),

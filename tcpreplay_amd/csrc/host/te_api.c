@@ -61,8 +61,8 @@ struct tcpedit_batch_s {
     int last_mtu;            /* the last launch placed tiles by the --mtu-trunc prediction */
     int fz_fast;             /* tiles were cut for the wave lane's --fuzz-seed instances */
     int last_fz;             /* the last launch fuzzed on the wave lane (static_fz placement) */
-    uint32_t *d_fzlist;      /* static_fz: the reach list (n_tiles + 1 words) */
-    uint64_t fzlist_cap;
+    uint32_t *d_fzlist;      /* static_fz: the reach list, its count, a word a record */
+    uint64_t fzlist_cap;     /* (words) */
     long long *d_tcut;       /* the prediction: n_tiles + 1 prefix (te_mtu_cuts), ... */
     long long *d_tcut_raw;   /* ... from per-64-tile sums (scratch) */
     uint64_t tcut_cap;       /* tiles d_tcut holds */
@@ -1454,13 +1454,14 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
                   !b->fuzz_probe_only && !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never &&
                   !grow_off_env() && !fast_lane_off() && tcut_bufs(b) == 0;
     if (L.static_fz) {
-        if (b->fzlist_cap < b->n_tiles) {
+        const uint64_t words = b->n_tiles + 1 + b->n_pkts; /* the reach list, its count, a word a record */
+        if (b->fzlist_cap < words) {
             hipFree(b->d_fzlist);
             b->d_fzlist = NULL;
             b->fzlist_cap = 0;
-            if (hipMalloc((void **)&b->d_fzlist, 4 * (b->n_tiles + 1)) != hipSuccess)
+            if (hipMalloc((void **)&b->d_fzlist, 4 * words) != hipSuccess)
                 return -1;
-            b->fzlist_cap = b->n_tiles;
+            b->fzlist_cap = words;
         }
         L.tcut = b->d_tcut;
         L.tcut_raw = b->d_tcut_raw;
@@ -2216,6 +2217,7 @@ fail:
 }
 
 uint64_t tcpedit_batch_fused_fallbacks(tcpedit_batch_t *b) { return b ? b->win_fallbacks : 0; }
+uint64_t tcpedit_pipeline_fallbacks(tcpedit_t *t) { return t ? t->pipe_fallbacks : 0; }
 
 int tcpedit_batch_run(tcpedit_t *t, tcpedit_batch_t *b)
 {
@@ -3539,8 +3541,14 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         const uint64_t f0 = cst[nch - 1];
         const uint64_t end = f0 + acc[4] - ORG; /* the last chunk's chain end, as a file offset */
         free(cst);
-        if (acc[3] || acc[1] != end - 24 || end > in_len)
-            return 1; /* (the records and the chain must agree) */
+        if (acc[3] || acc[1] != end - 24 || end > in_len) { /* (the records and the chain must agree) */
+            if (trace)
+                fprintf(stderr, "pipe (window mode): missed -- verdict %llu, chain end %llu, records end %llu of %zu;"
+                                " the exact pipeline redoes the capture\n",
+                        (unsigned long long)acc[3], (unsigned long long)end, (unsigned long long)(acc[1] + 24),
+                        in_len);
+            return 1;
+        }
         *pos_io = end;
         t->pub.runtime.packetnum += acc[0];
         t->pub.runtime.total_bytes += acc[1];
@@ -3668,6 +3676,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
                 rc = TCPEDIT_OK;
                 goto out;
             }
+            t->pipe_fallbacks++;
             pos = 24; /* (the exact pipeline below redoes the capture) */
         }
         if (dix && b0->fast_kind == TE_FAST_WAVE) {

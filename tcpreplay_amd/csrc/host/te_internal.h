@@ -86,6 +86,7 @@ struct tcpedit_s {
     struct te_pipe_s *pipe;       /* tcpedit_rewrite_pcap_pipelined's slots and streams (kept) */
     struct te_srv_s *srv;         /* tcpedit_packet's resident server (te_packet_server), or NULL */
     int pipe_err;                 /* that call hit a hard error */
+    uint64_t pipe_fallbacks;      /* pipelined calls whose window mode missed (redone exactly) */
 };
 
 #define TE_ERR(t) ((t)->pub.runtime.errstr)

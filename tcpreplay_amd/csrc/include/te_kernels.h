@@ -155,7 +155,8 @@ typedef struct {
                                  draws the states, predicts each tile's cut into tcut (written
                                  here, not read) and places tiles by it like static_mtu */
     long long *tcut_raw;      /* static_fz: device scratch, (n_tiles + 63) / 64 + 1 words */
-    uint32_t *fz_list;        /* static_fz: device, n_tiles + 1 words (the reach list, its count) */
+    uint32_t *fz_list;        /* static_fz: device, n_tiles + 1 + n_pkts words (the reach list, its
+                                 count, a word per record for the cut prediction) */
     /* fast lane (static_off configs the register-resident lane carries): te_fast_tiles edits
        every tile it can, appends the rest to tile_list, and the generic kernel then redoes
        only the listed tiles */

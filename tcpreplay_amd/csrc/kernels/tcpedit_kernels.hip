@@ -1723,10 +1723,13 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 #ifndef TE_WIN_BLOCKS
 #define TE_WIN_BLOCKS TE_WK_MIN_BLOCKS  // window mode: blocks per CU (its VGPR budget)
 #endif
-// (SZ_FUZZ: 4 blocks per CU, 3 with the address maps -- at the lean instances' 5 / the others'
-//  4 the fuzz step's registers spill)
+// (SZ_FUZZ: TE_WK_FUZZ_BLOCKS per CU, one fewer with the address maps -- at the lean
+//  instances' 5 / the others' 4 the fuzz step's registers spill)
+#ifndef TE_WK_FUZZ_BLOCKS
+#define TE_WK_FUZZ_BLOCKS TE_WK_MIN_BLOCKS
+#endif
 __global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
-                                       : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_MIN_BLOCKS - 1 : TE_WK_MIN_BLOCKS)
+                                       : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_FUZZ_BLOCKS - 1 : TE_WK_FUZZ_BLOCKS)
                                                        : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
@@ -1878,11 +1881,23 @@ __global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
                     const uint32_t proto = v6 ? S[p + 20] : S[p + 23];
                     const int l3 = v6 ? 54 : 34, l4h = proto == 6u ? 20 : 8;
                     const FzPlan f = fuzz_plan_l4(r, l3 + l4h, l3 - l4h, caplen, len);
-                    for (int i = 0; i < f.n; ++i) {  // (bytes past caplen: the reference's buffer, never output)
-                        const uint32_t j = (uint32_t)(f.from + i);
-                        if (j < caplen) {
-                            uint8_t &b = S[p + j];
-                            b = f.how == 0 ? (uint8_t)0 : f.how == 1 ? (uint8_t)0xff : (uint8_t)(b ^ f.x);
+                    // the run [from, from + n) (<= 15 bytes), cut at caplen (past it lies the
+                    // reference's buffer, never output, and here the next record), as five
+                    // aligned dwords read together and written back under byte masks (a byte
+                    // loop waited out the LDS latency per byte); records' runs are >= 58 bytes
+                    // apart, so no other lane writes these dwords now
+                    const uint32_t lo = p + (uint32_t)f.from, hi = p + umin32((uint32_t)(f.from + f.n), caplen);
+                    if (f.n > 0 && hi > lo) {
+                        const uint32_t a4 = lo & ~3u;
+                        uint32_t q[5];
+#pragma unroll
+                        for (int k = 0; k < 5; ++k) q[k] = *(const uint32_t *)(S + a4 + 4 * k);
+                        const uint32_t xv = 0x01010101u * f.x;
+#pragma unroll
+                        for (int k = 0; k < 5; ++k) {
+                            const uint32_t m = fl::bmask((int)lo - (int)(a4 + 4 * k), (int)hi - (int)(a4 + 4 * k));
+                            const uint32_t v = f.how == 0 ? 0u : f.how == 1 ? 0xffffffffu : (q[k] ^ xv);
+                            if (m) *(uint32_t *)(S + a4 + 4 * k) = (q[k] & ~m) | (v & m);
                         }
                     }
                     fz_cut = f.cut;
@@ -3253,81 +3268,140 @@ extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint
 // ===========================================================================
 // --fuzz-seed on the wave lane (te_launch_t.static_fz).  A record's RNG draw depends on how
 // many records before it reach the fuzz step (te_fuzz_states), so the launch finds them
-// first.  te_fuzz_reach reads each record's header (one wave per tile, a lane per record)
-// and marks the records of the shape the wave lane edits -- Ethernet II, IPv4 with IHL 5 or
-// IPv6 with TCP or UDP next, the network header captured: under the configs static_fz takes
-// (no edit before the fuzz step but the en10mb decode and re-encode) such a record always
-// reaches it (tcpedit.c:89-248: decode, encode, the IP header and L4 checks).  A tile holding
-// any other record is listed, and the generic kernel's reach pass decides that tile.  It
-// also zeroes the ticket that reach pass takes.
+// first.  te_fuzz_reach reads each record's header and marks the records of the shape the
+// wave lane edits -- Ethernet II with IPv4 IHL 5 or with IPv6 and TCP or UDP next, the
+// network header captured: under the configs static_fz takes (no edit before the fuzz step
+// but the en10mb decode and re-encode) such a record always reaches it (tcpedit.c:89-248:
+// decode, encode, the IP header and L4 checks).  A tile holding any other record is listed,
+// and the generic kernel's reach pass decides that tile.  For a marked record it also keeps
+// what fuzzing() will look at (fuzzing.c:89-131) in one word, so the cut prediction reads no
+// header again: caplen (bits 0-18), len < caplen (19), IPv6 (20), TCP (21), UDP (22), valid (31).
+//
+// Both kernels walk consecutive tiles a wave with every lane on a record (an IMIX tile of
+// the lean budget holds ~14 records): the tiles' first records and span offsets go to LDS,
+// and a lane finds its record's tile by a binary search there.  The reach kernel takes 16
+// tiles a wave (a latency-bound gather: more waves in flight), the cut kernel 64 (its
+// output is the per-64-tile layout te_mtu_cut_scan reads).
 // ===========================================================================
+constexpr uint32_t FZ_REACH_TILES = 16;
+constexpr uint32_t FZD_VALID = 1u << 31, FZD_LT = 1u << 19, FZD_V6 = 1u << 20, FZD_TCP = 1u << 21,
+                   FZD_UDP = 1u << 22;
+
+struct FzTiles {  // one wave's 64 tiles
+    uint32_t fp[65];  // first record of each, and the end
+    unsigned long long so[64];
+};
+
+// loads tiles [t0, t0 + G) into T (lane j: tile t0 + j); returns how many exist
+template <uint32_t G = 64>
+__device__ __forceinline__ uint32_t fz_load_tiles(const te_tile_t *tiles, uint32_t n, uint32_t t0, FzTiles &T,
+                                                  uint32_t lane) {
+    const uint32_t nt = n - t0 < G ? n - t0 : G;
+    if (lane < nt) {
+        const te_tile_t tl = tiles[t0 + lane];
+        T.fp[lane] = tl.first_pkt;
+        T.so[lane] = tl.span_off;
+        if (lane == nt - 1) T.fp[nt] = tl.first_pkt + tl.npkt;
+    }
+    WK_LANES_SYNC();
+    return nt;
+}
+// the tile (of the wave's nt) holding record r
+__device__ __forceinline__ uint32_t fz_tile_of(const FzTiles &T, uint32_t nt, uint32_t r) {
+    uint32_t lo = 0, hi = nt - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (T.fp[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 __global__ void __launch_bounds__(256) te_fuzz_reach(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_rel,
-                                                     uint32_t n, uint8_t *status, uint32_t *list, uint32_t *list_cnt,
-                                                     unsigned int *ticket) {
+                                                     uint32_t n, uint8_t *status, uint32_t *desc, uint32_t *list,
+                                                     uint32_t *list_cnt, unsigned int *ticket) {
+    __shared__ FzTiles TS[4];
+    __shared__ uint32_t openb[4][2];
     if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (t >= n) return;  // (wave-uniform)
-    const te_tile_t tl = tiles[t];
-    bool open = false;
-    for (uint32_t k = lane; k < tl.npkt; k += 64u) {
-        const uint8_t *r = in + tl.span_off + pkt_rel[tl.first_pkt + k];
-        const uint32_t cap = ld32(r + 8);
-        const uint8_t *d = r + 16;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t t0 = (blockIdx.x * 4u + w) * FZ_REACH_TILES;
+    if (t0 >= n) return;  // (wave-uniform)
+    FzTiles &T = TS[w];
+    if (lane < 2) openb[w][lane] = 0;
+    const uint32_t nt = fz_load_tiles<FZ_REACH_TILES>(tiles, n, t0, T, lane);
+    const uint32_t r0 = T.fp[0], r1 = T.fp[nt];
+    for (uint32_t r = r0 + lane; r < r1; r += 64u) {
+        const uint32_t j = fz_tile_of(T, nt, r);
+        const uint8_t *rec = in + T.so[j] + pkt_rel[r];
+        const uint32_t cap = ld32(rec + 8), len = ld32(rec + 12);
+        const uint8_t *d = rec + 16;
         const uint32_t et = cap >= 14 ? ((uint32_t)d[12] << 8) | d[13] : 0u;
         const bool v4 = et == 0x0800u && cap >= 34 && d[14] == 0x45u;
         const bool v6 = et == 0x86DDu && cap >= 54 && (d[20] == 6u || d[20] == 17u);
-        if (v4 || v6) status[tl.first_pkt + k] = 1;
-        else open = true;
+        if (v4 || v6) {
+            const uint32_t pr = v6 ? d[20] : d[23];
+            status[r] = 1;
+            desc[r] = FZD_VALID | cap | (len < cap ? FZD_LT : 0u) | (v6 ? FZD_V6 : 0u) | (pr == 6u ? FZD_TCP : 0u) |
+                      (pr == 17u ? FZD_UDP : 0u);
+        } else {
+            desc[r] = 0u;
+            atomicOr(&openb[w][j >> 5], 1u << (j & 31u));
+        }
     }
-    if (__ballot(open) && lane == 0) list[atomicAdd(list_cnt, 1u)] = t;
+    WK_LANES_SYNC();
+    if (lane < nt && ((openb[w][lane >> 5] >> (lane & 31u)) & 1u)) list[atomicAdd(list_cnt, 1u)] = t0 + lane;
 }
 
 // the bytes each tile's records lose to fuzzing() (DROP: the whole record; REDUCE: its tail),
-// from the reach flags and RNG states, as te_mtu_tile_cut lays them out.  With no edit before
-// the fuzz step but the en10mb decode and re-encode, fuzzing() sees the input bytes, so
-// fuzz_plan on them is its choice (every tile checks its output total against this).
+// from the reach flags, the RNG states and te_fuzz_reach's words (the records of a listed tile
+// read their headers), laid out as te_mtu_tile_cut's: per 64 tiles a local exclusive prefix in
+// pre[] and the total in bsum[].  With no edit before the fuzz step but the en10mb decode and
+// re-encode, fuzzing() sees the input bytes, so this is its choice (every tile checks its
+// output total against it).
 __global__ void __launch_bounds__(256) te_fuzz_tile_cut(const uint8_t *in, const te_tile_t *tiles,
                                                         const uint16_t *pkt_rel, uint32_t n, const uint8_t *status,
-                                                        const uint32_t *states, const te_dev_cfg_t *cfg,
-                                                        long long *pre, long long *bsum) {
-    __shared__ long long c[64];
+                                                        const uint32_t *states, const uint32_t *desc,
+                                                        const te_dev_cfg_t *cfg, long long *pre, long long *bsum) {
+    __shared__ FzTiles TS[4];
+    __shared__ uint32_t cut[4][64];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t t0 = blockIdx.x * 64u;
+    const uint32_t g = blockIdx.x * 4u + w, t0 = g * 64u;
+    if (t0 >= n) return;  // (wave-uniform)
+    FzTiles &T = TS[w];
+    cut[w][lane] = 0;
+    const uint32_t nt = fz_load_tiles(tiles, n, t0, T, lane);
     const uint32_t factor = cfg->fuzz_factor;
-    for (uint32_t j = w; j < 64u; j += 4u) {
-        const uint32_t t = t0 + j;
-        long long s = 0;
-        if (t < n) {
-            const te_tile_t tl = tiles[t];
-            for (uint32_t k = lane; k < tl.npkt; k += 64u) {
-                const uint32_t i = tl.first_pkt + k;
-                if (!(status[i] & 1u)) continue;
-                uint32_t st = states[i];
-                const uint32_t r = tcpr_random_dev(st);
-                if (r % factor) continue;
-                const uint8_t *rec = in + tl.span_off + pkt_rel[i];
-                const uint32_t cap = ld32(rec + 8), len = ld32(rec + 12);
-                const FzPlan f = fuzz_plan(rec + 16, cap, len, cap, *cfg, r);
-                if (f.cut) s += f.nl ? (long long)(cap - f.nl) : 16ll + cap;
-            }
+    const uint32_t r0 = T.fp[0], r1 = T.fp[nt];
+    for (uint32_t r = r0 + lane; r < r1; r += 64u) {
+        if (!(status[r] & 1u)) continue;
+        uint32_t st = states[r];
+        const uint32_t rnd = tcpr_random_dev(st);
+        if (rnd % factor) continue;
+        const uint32_t dw = desc[r];
+        FzPlan f;
+        uint32_t cap;
+        if (dw & FZD_VALID) {
+            cap = dw & 0x7ffffu;
+            const int l3 = (dw & FZD_V6) ? 54 : 34, adj = (dw & FZD_TCP) ? 20 : (dw & FZD_UDP) ? 8 : 0;
+            f = fuzz_plan_l4(rnd, l3 + adj, l3 - adj, cap, (dw & FZD_LT) ? 0u : cap);
+        } else {
+            const uint32_t j = fz_tile_of(T, nt, r);
+            const uint8_t *rec = in + T.so[j] + pkt_rel[r];
+            cap = ld32(rec + 8);
+            f = fuzz_plan(rec + 16, cap, ld32(rec + 12), cap, *cfg, rnd);
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (lane == 0) c[j] = s;
+        if (f.cut) atomicAdd(&cut[w][fz_tile_of(T, nt, r)], f.nl ? cap - f.nl : 16u + cap);
     }
-    __syncthreads();
-    if (w == 0) {
-        const long long v = c[lane];
-        long long x = v;
+    WK_LANES_SYNC();
+    const long long v = lane < nt ? (long long)cut[w][lane] : 0ll;
+    long long x = v;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const long long y = __shfl_up(x, o, 64);
-            if ((int)lane >= o) x += y;
-        }
-        if (t0 + lane < n) pre[t0 + lane] = x - v;
-        if (lane == 63) bsum[blockIdx.x] = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o, 64);
+        if ((int)lane >= o) x += y;
     }
+    if (lane < nt) pre[t0 + lane] = x - v;
+    if (lane == 63) bsum[g] = x;
 }
 
 // static_fz's prelude: the reach (header kernel + the generic reach pass over the tiles it
@@ -3336,10 +3410,12 @@ static int fuzz_wave_prelude(const te_launch_t *L, const LaunchArgs &a, hipStrea
     if (!L->fuzz_states || !L->fuzz_blk || !L->fuzz_words || !L->fz_list || !L->tcut || !L->tcut_raw ||
         L->n_pkts == 0 || L->n_tiles == 0)
         return -1;
-    uint32_t *cnt = L->fz_list + L->n_tiles;
+    uint32_t *cnt = L->fz_list + L->n_tiles, *desc = cnt + 1;
+    const uint32_t ng = (L->n_tiles + 63u) / 64u;  // groups of 64 tiles, a wave each
+    const uint32_t nr = (L->n_tiles + FZ_REACH_TILES - 1) / FZ_REACH_TILES;  // the reach kernel's groups
     if (hipMemsetAsync(cnt, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
-    hipLaunchKernelGGL(te_fuzz_reach, dim3((L->n_tiles + 3u) / 4u), dim3(256), 0, stream, L->in, L->tiles,
-                       L->pkt_rel, L->n_tiles, L->status, L->fz_list, cnt, L->ticket);
+    hipLaunchKernelGGL(te_fuzz_reach, dim3((nr + 3u) / 4u), dim3(256), 0, stream, L->in, L->tiles, L->pkt_rel,
+                       L->n_tiles, L->status, desc, L->fz_list, cnt, L->ticket);
     LaunchArgs pa = a;
     pa.tile_list = L->fz_list;
     pa.list_cnt = cnt;
@@ -3352,11 +3428,11 @@ static int fuzz_wave_prelude(const te_launch_t *L, const LaunchArgs &a, hipStrea
     hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words, 1);
     hipLaunchKernelGGL(te_fuzz_states, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status, L->n_pkts,
                        (const uint32_t *)L->fuzz_blk, (const uint32_t *)L->fuzz_words, L->fuzz_states);
-    const uint32_t nb = (L->n_tiles + 63u) / 64u;
     long long *pre = (long long *)L->tcut, *bsum = (long long *)L->tcut_raw;
-    hipLaunchKernelGGL(te_fuzz_tile_cut, dim3(nb), dim3(256), 0, stream, L->in, L->tiles, L->pkt_rel, L->n_tiles,
-                       (const uint8_t *)L->status, (const uint32_t *)L->fuzz_states, L->cfg, pre, bsum);
-    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    hipLaunchKernelGGL(te_fuzz_tile_cut, dim3((ng + 3u) / 4u), dim3(256), 0, stream, L->in, L->tiles, L->pkt_rel,
+                       L->n_tiles, (const uint8_t *)L->status, (const uint32_t *)L->fuzz_states,
+                       (const uint32_t *)desc, L->cfg, pre, bsum);
+    hipLaunchKernelGGL(te_mtu_cut_scan, dim3(1), dim3(1024), 0, stream, bsum, ng);
     hipLaunchKernelGGL(te_mtu_cut_add, dim3((L->n_tiles + 1u + 255u) / 256u), dim3(256), 0, stream, pre,
                        (const long long *)bsum, L->n_tiles);
     return hipGetLastError() == hipSuccess ? 0 : -1;

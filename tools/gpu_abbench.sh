@@ -1,13 +1,14 @@
 #!/bin/bash
 # bench.py at full size for library variants (diagnostic): AB_VARIANTS (names under
-# tcpreplay_amd/lib/var, "base" = the in-tree library), AB_WLS workloads
+# tcpreplay_amd/lib/abvar -- copy them there from lib/var, which no GPU run receives;
+# "base" = the in-tree library), AB_WLS workloads
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 F="--steps 20 --warmup 3 --extra= --no-cpu-baseline --no-e2e --no-device-index --no-packet-latency"
 for v in ${AB_VARIANTS:-base}; do
   for w in ${AB_WLS:-c4}; do
-    if [ "$v" = base ]; then L=tcpreplay_amd/lib/libtcpedit_hip.so; else L=tcpreplay_amd/lib/var/libtcpedit_hip_$v.so; fi
+    if [ "$v" = base ]; then L=tcpreplay_amd/lib/libtcpedit_hip.so; else L=tcpreplay_amd/lib/abvar/libtcpedit_hip_$v.so; fi
     TCPEDIT_HIP_LIB=$L timeout -k 10 300 python3 bench.py --workload $w $F > gpurun_out/abb_${v}_$w.json 2> gpurun_out/abb_${v}_$w.err || { tail -5 gpurun_out/abb_${v}_$w.err; exit 1; }
     python3 -c "import json,sys; j=json.load(open(sys.argv[1])); r=j['roofline']; print(sys.argv[2], sys.argv[3], 'frac', r['frac'], 'kernel_ms', r['kernel_ms'], 'pipe_ms', r['pipeline_ms'])" gpurun_out/abb_${v}_$w.json $v $w
     if [ -n "$AB_PMC" ]; then
