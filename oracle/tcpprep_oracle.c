@@ -290,10 +290,8 @@ static int tpo_parse(tpo_opt_t *o, int argc, char **argv)
     }
     if (!o->mode)
         return -1;
-    if (o->mode == TPO_AUTO && o->xx_mode)
-        return -1;
     if (o->min_mask <= o->max_mask)
-        return -1; /* tcpprep_api.c:204-208 */ /* the first pass would add_cache() the filtered packets a second time */
+        return -1; /* tcpprep_api.c:204-208 */
     /* tcpprep_post_args, tcpprep_api.c:160-197: "args\ncomment" */
     char full[8192] = "";
     if (!o->nocomment && args[0]) {
@@ -605,10 +603,18 @@ static int tpo_packet2tree(const uint8_t *d, uint32_t caplen)
     return -1;
 }
 
+static uint64_t tpo_pkt_base; /* a shard's first global record number (0-based) */
+
 /* the first pass of auto mode (tcpprep.c:480-496, tree.c:333-538) and tree_calculate
-   (tree.c:540-565); returns 0, or -4 on the reference's errx() paths */
-static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, int sw, uint64_t records)
+   (tree.c:540-565); returns 0, or -4 on the reference's errx() paths.  The include/exclude
+   filters run in this pass too (tcpprep.c:362-375, 413-428): a filtered record adds a
+   DONT_SEND entry to the cache here -- before the second pass adds every record's entry
+   again -- and stays out of the tree; *dont_send counts those entries. */
+static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, int sw, uint64_t records,
+                         uint64_t *dont_send)
 {
+    *dont_send = 0;
+    uint64_t packetnum = 0;
     tpo_cap = 16;
     while (tpo_cap < 4 * records + 16)
         tpo_cap <<= 1;
@@ -622,6 +628,11 @@ static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, in
     while ((nx = tpo_next(pcap, len, sw, &off, &dat, &caplen)) != 0) {
         if (nx < 0)
             return -5;
+        packetnum++;
+        if (o->nlist && !!(o->xx_mode & XX_EXCLUDE) == tpo_check_list(o, tpo_pkt_base + packetnum)) {
+            (*dont_send)++;
+            continue;
+        }
         const uint8_t *d = pcap + dat;
         uint16_t proto = 0;
         uint32_t l2len = 0;
@@ -630,6 +641,10 @@ static int tpo_tree_pass(const tpo_opt_t *o, const uint8_t *pcap, size_t len, in
         int v6 = !v4 && res != -1 && l2len + 40 <= caplen && proto == 0x86DD;
         if (!v4 && !v6)
             continue;
+        if (o->nxx_cidr && o->xx_mode && !tpo_xx_cidr(o, d + l2len, v6)) {
+            (*dont_send)++;
+            continue;
+        }
         int fam = v4 ? 4 : 6, ins = 0;
         const uint8_t *src = d + l2len + (v4 ? 12 : 8), *dst = d + l2len + (v4 ? 16 : 24);
         if (o->automode == TPA_FIRST) { /* add_tree_first_ipv4/ipv6: first sighting wins */
@@ -695,7 +710,7 @@ static int tpo_check_tree(const tpo_opt_t *o, int fam, const uint8_t *src)
  * -4 on the reference's errx() paths, -5 when safe_pcap_next exits on a record
  * (tpo_next: no cache is written).
  */
-static uint64_t tpo_pkt_base, tpo_last_entries;
+static uint64_t tpo_last_entries;
 
 /* a shard's first global record number (0-based): P: lists keep global numbers */
 void tcpprep_oracle_set_pkt_base(uint64_t base) { tpo_pkt_base = base; }
@@ -740,6 +755,7 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
     if (cap < hdr)
         return -3;
     memset(out, 0, cap);
+    uint64_t entries = 0;
     if (o.mode == TPO_AUTO) {
         uint64_t recs = 0;
         {
@@ -748,11 +764,13 @@ long tcpprep_oracle_run(int argc, char **argv, const uint8_t *pcap, size_t len, 
             while (tpo_next(pcap, len, sw, &off, &d, &cl) > 0)
                 recs++;
         }
-        const int tr = tpo_tree_pass(&o, pcap, len, sw, recs);
+        const int tr = tpo_tree_pass(&o, pcap, len, sw, recs, &entries); /* (its DONT_SEND entries: zeros) */
         if (tr < 0)
             return tr == -5 ? -5 : -4;
+        if (hdr + entries / 4 >= cap && entries)
+            return -3;
     }
-    uint64_t packetnum = 0, entries = 0;
+    uint64_t packetnum = 0;
     static uint8_t pkt[MAXPACKET + 64];
     size_t off = 24, dat = 0;
     uint32_t caplen = 0;

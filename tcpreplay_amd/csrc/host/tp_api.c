@@ -328,9 +328,6 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
     if (t->min_mask <= t->max_mask) /* tcpprep_api.c:204-208 */
         return tp_err(t, "Min network mask len (%d) must be less then max network mask len (%d)", t->min_mask,
                       t->max_mask);
-    if (c->mode == TP_MODE_AUTO && c->xx_mode)
-        return tp_err(t, "--include/--exclude with --auto are not served (the reference's first pass "
-                         "would add the filtered records to the cache a second time)");
     /* tcpprep_post_args (tcpprep_api.c:160-197): "args\ncomment" */
     char full[sizeof t->comment] = "";
     if (!t->nocomment && args[0]) {
@@ -349,7 +346,8 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
 
 size_t tcpprep_cache_bound(tcpprep_hip_t *t, size_t pcap_len)
 {
-    return 24 + (t ? strlen(t->comment) : 0) + (pcap_len / 16) / 4 + 1;
+    /* (--auto with --include/--exclude: up to two entries a record, see tcpprep_cache_pcap) */
+    return 24 + (t ? strlen(t->comment) : 0) + (pcap_len / 16) / 2 + 1;
 }
 
 static uint32_t rd32(const uint8_t *p, int sw)
@@ -666,8 +664,19 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
         index_free(&x);
         return tp_err(t, "No packets were processed.  Filter too limiting?");
     }
+    /* --auto with --include/--exclude: the reference's first pass (tcpprep.c:362-375, 413-428)
+       adds a DONT_SEND entry for each record a filter drops, and the second pass then adds
+       every record's entry after them: the file holds those entries first (the header still
+       counts the records).  In the second pass only the filters give DONT_SEND, so they are
+       the body's zero entries; the body is shifted by their count below. */
+    const int filt_auto = t->cfg.mode == TP_MODE_AUTO && t->cfg.xx_mode;
+    if (filt_auto && (t->merged || t->cfg.pkt_base)) {
+        index_free(&x);
+        return tp_err(t, "--include/--exclude with --auto on shards are not served (the first pass's "
+                         "entries of every shard come before the second pass's)");
+    }
     size_t clen = strlen(t->comment), hdr = 24 + clen, body = (x.n + 3) / 4;
-    if (out_cap < hdr + body) {
+    if (out_cap < hdr + (filt_auto ? (2 * x.n + 3) / 4 : body)) {
         index_free(&x);
         return tp_err(t, "cache buffer too small (%zu < %zu)", out_cap, hdr + body);
     }
@@ -698,6 +707,25 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
         index_free(&x);
         return tp_err(t, "classification kernel failed");
     }
+    uint64_t entries = x.n;
+    if (filt_auto) { /* the first pass's DONT_SEND entries, then the body's */
+        uint8_t *b = out + hdr;
+        uint64_t f = 0;
+        for (uint64_t i = 0; i < x.n; i++)
+            f += ((b[i / 4] >> (2 * (i % 4))) & 3u) == 0;
+        if (f) {
+            memset(b + body, 0, (x.n + f + 3) / 4 - body); /* (the bytes the shift extends into) */
+            for (uint64_t i = x.n; i-- > 0;) { /* back to front: the shift moves entries on */
+                const unsigned e = (b[i / 4] >> (2 * (i % 4))) & 3u;
+                const uint64_t k = i + f;
+                b[k / 4] = (uint8_t)((b[k / 4] & ~(3u << (2 * (k % 4)))) | (e << (2 * (k % 4))));
+            }
+            for (uint64_t k = 0; k < f; k++)
+                b[k / 4] &= (uint8_t)~(3u << (2 * (k % 4)));
+        }
+        entries = x.n + f;
+        body = (entries + 3) / 4;
+    }
     /* tcpr_cache_file_hdr_t (cache.h:63-72), big-endian counts */
     memcpy(out, "tcpprep\0", 8);
     memcpy(out + 8, "04\0\0", 4);
@@ -708,7 +736,7 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
     out[22] = (uint8_t)(clen >> 8);
     out[23] = (uint8_t)clen;
     memcpy(out + 24, t->comment, clen);
-    t->last_entries = x.n;
+    t->last_entries = entries;
     index_free(&x);
     return (int64_t)(hdr + body);
 }

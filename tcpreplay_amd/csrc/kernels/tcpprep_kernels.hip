@@ -225,9 +225,16 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
                                                      uint64_t base, tp_tree_t t, const tp_dev_cfg_t *cfg) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
+    const tp_dev_cfg_t &c = *cfg;
+    // the include/exclude filters skip a record before the tree (tcpprep.c:362-375, 413-428;
+    // that first pass's DONT_SEND entries are the host's, tcpprep_cache_pcap)
+    if (c.nlist && check_list(c, c.pkt_base + j + 1) == ((c.xx_mode & TP_XX_EXCLUDE) != 0)) {
+        t.slot[j] = 0xffffffffu;
+        return;
+    }
     const u8 *d = img + off[j];
     const u32 cl = caplen[j];
-    const int dlt = cfg->dlt;
+    const int dlt = c.dlt;
     L2 r;
     const int res = cl ? tp_l2(d, cl, dlt, r) : -1;
     const bool v4 = res != -1 && r.l2len + 20 <= cl && r.protocol == 0x0800;
@@ -237,6 +244,10 @@ __global__ __launch_bounds__(256) void tp_tree_build(const u8 *__restrict__ img,
         return;
     }
     const u8 *ip = d + r.l2len;
+    if (c.nxx_cidr && c.xx_mode && !xx_cidr(c, ip, v6)) {
+        t.slot[j] = 0xffffffffu;
+        return;
+    }
     const uint32_t s = tree_insert(t, node_key(v6, ip + (v6 ? 8 : 12)));
     t.slot[j] = s;
     if (s == 0xffffffffu) {

@@ -174,8 +174,7 @@ def test_mac_mode_short_records_get_no_entry():
 
 
 def test_rejects_unsupported_modes_loudly():
-    for args in (["--auto=bogus"], ["--auto=router", "--minmask=8", "--maxmask=16"], ["--regex=(96"], ["--port", "--include=F:tcp"], [],
-                 ["--auto=bridge", "--include=P:1-5"]):
+    for args in (["--auto=bogus"], ["--auto=router", "--minmask=8", "--maxmask=16"], ["--regex=(96"], ["--port", "--include=F:tcp"], []):
         with pytest.raises(ValueError):
             TP.TcpPrep(args)
 
@@ -223,3 +222,19 @@ def test_regex_over_every_ipv6_text_shape(pattern):
     pcap = synth.build_pcap(recs)
     args = ["--no-arg-comment", "--regex=" + pattern]
     assert TP.cache(pcap, args) == oracle_lib.tcpprep(pcap, args)
+
+
+AUTO_FILTERS = [["--include=P:5-60"], ["--exclude=P:1-9,30-31,100-"], ["--include=S:172.16.0.0/12"],
+                ["--exclude=D:10.0.0.0/8"], ["--include=B:0.0.0.0/0"], ["--exclude=E:96.17.211.0/24"]]
+
+
+@pytest.mark.parametrize("mode", ["bridge", "client", "server", "first", "router"])
+@pytest.mark.parametrize("filt", range(len(AUTO_FILTERS)))
+def test_gpu_auto_with_include_exclude(mode, filt):
+    """--auto with --include/--exclude (tcpprep.c:362-375, 413-428 in both passes): the first
+    pass's DONT_SEND entries of the filtered records, then every record's entry -- GPU ==
+    oracle, on the reference's test.pcap and on an IMIX capture"""
+    args = ["--no-arg-comment", f"--auto={mode}"] + AUTO_FILTERS[filt]
+    for pcap in (T.test_pcap(), synth.pcap_imix(3000, seed=filt)):
+        got, exp = _both(pcap, args)
+        assert got == exp and got != "error"
