@@ -132,6 +132,7 @@ struct tcpedit_batch_s {
     uint32_t *d_fuzz;        /* --fuzz-seed: per-record RNG states, then a word per 1024 records */
     uint64_t fuzz_cap;       /* records d_fuzz has room for */
     int fuzz_probe_only;     /* the next launch only counts records reaching the fuzz step */
+    int q18_only;            /* the next launch only finds the Q18 carry (--fuzz-seed: after the states) */
     uint64_t ws_bytes;
     hipEvent_t ev0, ev1;
     /* window mode (tcpedit_batch_run_fused): its per-window workspace, and the window
@@ -1451,7 +1452,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
        computes after drawing the states (fast_capable_fuzz) */
     L.static_fz = b->fz_fast && b->fast_kind == TE_FAST_WAVE && fast_capable_fuzz(c) && !b->slot_layout &&
                   !b->has_trim && !b->swapped && !b->nsec && !b->d_dirbits && b->n_tiles > 0 && b->n_pkts > 0 &&
-                  !b->fuzz_probe_only && !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never &&
+                  !b->fuzz_probe_only && !b->q18_only && !(b->grow_off && b->grow_off_gen == t->cfg_gen) && !b->grow_never &&
                   !grow_off_env() && !fast_lane_off() && tcut_bufs(b) == 0;
     if (L.static_fz) {
         const uint64_t words = b->n_tiles + 1 + b->n_pkts; /* the reach list, its count, a word a record */
@@ -1520,6 +1521,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.fuzz_words = t->d_fuzz_words;
         L.n_pkts = (uint32_t)b->n_pkts;
         L.fuzz_probe_only = b->fuzz_probe_only;
+        L.q18_only = b->q18_only;
     }
     if (c->l2carry && !L.fast && b->n_pkts && l2carry_bufs(t, b, &L) < 0)
         return -1;
@@ -1889,6 +1891,26 @@ int tcpedit_batch_l2carry_out(tcpedit_t *t, tcpedit_batch_t *b)
         return TCPEDIT_ERROR;
     if (!t->cfg.l2carry || !b->n_pkts)
         return 2;
+    uint64_t last = 0;
+    if (t->cfg.fuzz_seed) {
+        /* a fuzzed record's second encode writes the carry too: the fuzz states first (from
+           the context's running start -- the earlier shards' draws skipped already), then
+           the carry's mark run of the edit and its scan (te_launch_edit, q18_only) */
+        b->q18_only = 1;
+        const int rc = launch(b, -1);
+        b->q18_only = 0;
+        if (rc != 0) {
+            te_seterr(t, "dst_modified carry launch failed: %s", hipGetErrorString(hipGetLastError()));
+            return TCPEDIT_ERROR;
+        }
+        HIPCHK(t, hipMemcpyAsync(&last, b->d_l2carry + b->n_pkts, sizeof(last), hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(t, hipStreamSynchronize(t->stream));
+        if (last >> 63) {
+            te_seterr(t, "dst_modified carry: a fuzzed record's second encode read stale buffer bytes (not served)");
+            return TCPEDIT_ERROR;
+        }
+        return (last >> 1) ? (int)(last & 1u) : 2;
+    }
     te_launch_t L;
     memset(&L, 0, sizeof(L));
     L.cfg = t->d_cfg;
@@ -1909,7 +1931,6 @@ int tcpedit_batch_l2carry_out(tcpedit_t *t, tcpedit_batch_t *b)
         te_seterr(t, "dst_modified carry launch failed: %s", hipGetErrorString(hipGetLastError()));
         return TCPEDIT_ERROR;
     }
-    uint64_t last = 0;
     HIPCHK(t, hipMemcpyAsync(&last, L.l2carry + b->n_pkts, sizeof(last), hipMemcpyDeviceToHost, t->stream));
     HIPCHK(t, hipStreamSynchronize(t->stream));
     return (last >> 1) ? (int)(last & 1u) : 2; /* position 0 is the context's own word */
@@ -2699,8 +2720,14 @@ static int host_locked(const void *p)
 /* device slots a pipelined run rotates through: chunk k is finished (results read, a
    stale-buffer replay retried with the earlier chunks as prefix) while chunk k + 1 is
    indexed and edited and chunk k + 2 uploads -- into a third slot, so chunk k's input and
-   index stand until it is finished */
-#define TE_PIPE_SLOTS 3
+   index stand until it is finished.  The edit of chunk k writes its slot's output buffer
+   once chunk k - SLOTS's download has left it: with three slots the last chunks' edits
+   waited on downloads three chunks back (the download stream trails the uploads), so there
+   are more (TE_PIPE_SLOTS_N overrides, A/B) */
+#ifndef TE_PIPE_SLOTS_N
+#define TE_PIPE_SLOTS_N 6
+#endif
+#define TE_PIPE_SLOTS TE_PIPE_SLOTS_N
 #define TE_PIPE_ANCHORS 64 /* chunk starts kept (chunks are >= 8 MiB: >= 512 MiB of anchors) */
 /* the default chunk: a tenth of the capture, 8-32 MiB (measured on MI355X, tools/e2e_probe.py:
    C2's 80 MB runs best at 8 MiB -- pipeline fill and drain are one chunk each -- and 2M IMIX

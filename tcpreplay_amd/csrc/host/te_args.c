@@ -625,14 +625,9 @@ int te_check_decoder_cfg(tcpedit_t *t, int s2c)
     (void)s2c;
     /* --fuzz-seed behind any decoder and into any encoder: a fuzzed record goes back to
        `again:` and is decoded by the input decoder and encoded a second time (tcpedit.c:89,
-       250-258); the slot headroom holds both encodes (te_slot_head).  Not served: the
-       en10mb encoder's dst_modified carry together with it, whose writers the
-       carry's mark pass finds from the first encode only */
-    if (c->fuzz_seed && c->l2carry) {
-        te_seterr(t, "--fuzz-seed with DLT %d input into --dlt=enet without --enet-dmac is not served by this "
-                     "build", t->dlt);
-        return -1;
-    }
+       250-258); the slot headroom holds both encodes (te_slot_head).  With the en10mb
+       encoder's dst_modified carry the second encode writes the carry too: its
+       mark runs the edit itself (te_launch_edit, LaunchArgs.q18_keys) */
     return 0;
 }
 

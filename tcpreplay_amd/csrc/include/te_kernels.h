@@ -182,6 +182,8 @@ typedef struct {
                                  [2] records of the launch that reached the fuzz step */
     uint32_t n_pkts;          /* records in the launch */
     int fuzz_probe_only;      /* count the reaching records (words[2]) and stop: no edit, no state change */
+    int q18_only;             /* --fuzz-seed with the Q18 carry: the states (from the running start, which
+                                 stays) and the carry's mark run and scan, then stop: no edit */
     /* stale static-buffer reads: the edit lists such written records here as
        {record, bytes needed, output offset lo, hi}; te_launch_q8 replays them */
     void *q8_list;            /* device: q8_cap x 16 bytes, or NULL */

@@ -68,6 +68,10 @@ struct Pkt {
                    // Tracked across every move of the record, so the two encodes of a fuzzed
                    // record (tcpedit.c:89,250-258) are bounded together, not each on its own
     u8 l2carry = 0;  // the en10mb encoder's dst_modified as the last C2S record left it (Q18)
+    // Q18 under --fuzz-seed (the carry's mark run, LaunchArgs.q18_keys): this record's last
+    // write of dst_modified -- bit 1 written, bit 0 the value -- and bit 2 once the record
+    // went back to `again:` after the fuzz step (tcpedit.c:255)
+    u8 q18ev = 0;
     // DLT_JUNIPER_ETHER: the decoder state the last whole inner decode before this record
     // left (jc), or none yet (jnone: zeros, the encoder's own extra) -- what a frame whose
     // extensions are not Ethernet is encoded with.  Neither: not at hand (fails loudly)
@@ -1215,7 +1219,10 @@ DI int foreign_decode(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s) {
         t.l2offset = 0;
         // the first whole decode makes the sub-decoder's extra the encoder's: a fresh
         // dst_modified (en10mb_decode never writes it)
-        if (pk.jnone) t.dst_modified = false;
+        if (pk.jnone) {
+            t.dst_modified = false;
+            pk.q18ev = (u8)((pk.q18ev & 4u) | 2u);
+        }
         t.jsub = true;
         t.proto_vlan_tag = s.proto_vlan_tag;  // (the sub-context's: not copied, dlt_utils.c:254-263)
         s = t;
@@ -1339,7 +1346,10 @@ DI int en10mb_encode_foreign(Pkt &pk, const te_dev_cfg_t &cfg, Dec &s, int pktle
         sh[i] = use_s ? smac[i] : s.srcaddr[i];
         dh[i] = use_d ? dmac[i] : s.dstaddr[i];
     }
-    if (c2s && !(cfg.mac_mask & dm)) s.dst_modified = old_nz;
+    if (c2s && !(cfg.mac_mask & dm)) {
+        s.dst_modified = old_nz;
+        pk.q18ev = (u8)((pk.q18ev & 4u) | 2u | (old_nz ? 1u : 0u));
+    }
     en10mb_mac_rules(cfg, dh, sh);
     if (newl2 == 14) st16(pk.d + 12, (u16)s.proto);  // :691-694
     // the VLAN fields of the decoder's extra (en10mb.c:696-732): zero (never set) but for the
@@ -1898,6 +1908,7 @@ again:  // :89 -- after the fuzz step the packet goes through L2 and the L3 edit
             fuzz_once = false;
             retval = fuzz_packet(pk, cfg, fz_state);
             needtorecalc += retval;
+            pk.q18ev |= 4u;
             goto again;
         }
     }

@@ -101,6 +101,10 @@ struct LaunchArgs {
     // per record (launch-relative index), the last C2S record's dst_modified
     // ((position << 1) | value, 0 = none yet): te_l2carry_mark + an inclusive max scan
     const unsigned long long *l2carry;
+    // Q18 under --fuzz-seed: the carry's mark run (an edit pass before the edit) writes each
+    // edited record's key from its own edit -- a fuzzed record's second encode writes
+    // dst_modified again (tcpedit.c:89,250-258) -- over te_l2carry_mark's; null otherwise
+    unsigned long long *q18_keys;
     // DLT_JUNIPER_ETHER: per record the last whole inner decode before it (te_jnpr_mark +
     // an inclusive max scan: i + 1 for record i, 0 = none in the launch, then *jctx), and
     // the states (entry i + 1: record i's); null: no carry
@@ -413,6 +417,8 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
         // contiguous span has no byte before a record that is the record's own
         pk.room = MODE == MODE_SLOT ? r0 - (slot_end - my_slot) : 0u;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[tile.first_pkt + tid] & 1u) : 0;
+        if (FZ && AD && a.l2carry && (a.l2carry[tile.first_pkt + tid] >> 63))
+            stale(pk, (int)NEED_NEVER);  // a poisoned carry (q18_keys): fails loudly
         if constexpr (AD) jnpr_carry(a, tile.first_pkt + tid, pk);
         pk.defer = kDefer;
         int rc = RC_OK;
@@ -423,6 +429,15 @@ __device__ __forceinline__ void tile_body(const LaunchArgs &a, const te_tile_t &
             const uint32_t fzs = a.fuzz_mode == TE_FUZZ_APPLY ? a.fuzz_state[tile.first_pkt + tid] : 0u;
             rc = tcpedit_packet<FZ, AD>(pk, cfg, (const TE_AS_GLOBAL uint16_t *)a.portlut, dir, warned,
                                         a.fuzz_mode, fzs);
+            if (FZ && AD && a.q18_keys) {  // (the carry's decoders are the ANYDEC instance's)
+                // the record's last dst_modified write; a stale read before a write in its
+                // second pass poisons the carry from here on (bit 63: the edit run fails
+                // those records loudly rather than guess what the bytes would have decided)
+                const uint32_t j = tile.first_pkt + tid;
+                unsigned long long k = (pk.q18ev & 2u) ? ((unsigned long long)(j + 1) << 1 | (pk.q18ev & 1u)) : 0ull;
+                if (pk.unsupported && (pk.q18ev & 6u) == 6u) k |= 1ull << 63;
+                a.q18_keys[j + 1] = k;
+            }
         }
         if (FZ && a.fuzz_mode == TE_FUZZ_PROBE) st = rc == RC_REACHED ? 1 : 0;
         if (warned) st |= TE_ST_WARNED;
@@ -2546,6 +2561,7 @@ __device__ int q8_replay_from(const Q8Args &q, const te_dev_cfg_t &cfg, int64_t 
         pk.strict = true;
         pk.room = Q8_HEAD - 16;
         pk.l2carry = a.l2carry ? (uint8_t)(a.l2carry[j] & 1u) : 0;
+        if (a.l2carry && (a.l2carry[j] >> 63)) { Q8_DBG(6); return Q8_FAIL; }  // (a poisoned carry, q18_keys)
         jnpr_carry(a, (uint64_t)j, pk);
         bool warned = false;
         const uint32_t fzs = (FZ && a.fuzz_mode == TE_FUZZ_APPLY) ? a.fuzz_state[j] : 0u;
@@ -2687,7 +2703,8 @@ __global__ void __launch_bounds__(FZ_BLOCK) te_fuzz_count(const uint8_t *st, uin
 }
 
 // one block: exclusive scan of the block counts in place, then the state words
-// (words[2] = reaching records; advance = 0 leaves the running state alone)
+// (words[2] = reaching records; advance = 0 leaves the running state alone, 2 takes the
+// states' start from it and leaves it: the Q18 carry-out of a shard before its edit)
 __global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nblk, uint32_t *words, int advance) {
     __shared__ uint32_t wsum[1024 / 64];
     uint64_t carry = 0;
@@ -2702,10 +2719,8 @@ __global__ void __launch_bounds__(1024) te_fuzz_scan(uint32_t *blk, uint32_t nbl
     if (threadIdx.x == 0) {
         const uint32_t s0 = words[0];
         words[2] = (uint32_t)carry;
-        if (advance) {
-            words[1] = s0;
-            words[0] = lcg_jump(s0, 3ull * carry);
-        }
+        if (advance) words[1] = s0;
+        if (advance == 1) words[0] = lcg_jump(s0, 3ull * carry);
     }
 }
 
@@ -2885,6 +2900,7 @@ static void fill_args(LaunchArgs &a, const te_launch_t *L) {
     a.q8_list = (uint4 *)L->q8_list;
     a.q8_cap = L->q8_cap;
     a.l2carry = (const unsigned long long *)L->l2carry;
+    a.q18_keys = nullptr;
     a.jscan = (const unsigned long long *)L->jscan;
     a.jstates = L->jstates;
     a.jctx = L->jctx;
@@ -3060,12 +3076,27 @@ extern "C" size_t te_l2carry_temp_bytes(uint32_t n_pkts) {
     return t;
 }
 
-// the keys and the scan before the edit (the edit then reads L->l2carry)
-static int l2carry_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stream) {
+static void launch_generic(bool fz, bool anydec, bool slot, int grid, hipStream_t stream, const LaunchArgs &a);
+
+// the keys and the scan before the edit (the edit then reads L->l2carry).  Under
+// --fuzz-seed (a.fuzz_mode APPLY, the states drawn) a fuzzed record decodes and encodes a
+// second time, so its last write is known only from its edit: a mark run of the edit
+// writes the keys of the records it edits over te_l2carry_mark's (its output, counters and
+// look-back words are the real run's to redo: `grid` blocks, then the zeroed region again)
+static int l2carry_prepare(te_launch_t *L, const LaunchArgs &a, hipStream_t stream, int grid = 0) {
     if (!L->l2carry) return 0;
     if (!L->l2carry_keys || !L->l2carry_word || !L->l2carry_tmp || L->n_tiles == 0) return -1;
     hipLaunchKernelGGL(te_l2carry_mark, dim3(L->n_tiles), dim3(256), 0, stream, a,
                        (unsigned long long *)L->l2carry_keys, (const uint32_t *)L->l2carry_word);
+    if (a.fuzz_mode == TE_FUZZ_APPLY) {
+        if (grid < 1) return -1;
+        LaunchArgs m = a;
+        m.q18_keys = (unsigned long long *)L->l2carry_keys;
+        m.l2carry = nullptr;
+        m.q8_list = nullptr;
+        launch_generic(true, L->any_dec != 0, L->slot_layout != 0, grid, stream, m);
+        if (hipMemsetAsync(L->zero_region, 0, L->zero_bytes, stream) != hipSuccess) return -1;
+    }
     size_t tb = L->l2carry_tmp_bytes;
     if (hipcub::DeviceScan::InclusiveScan(L->l2carry_tmp, tb, (const unsigned long long *)L->l2carry_keys,
                                           (unsigned long long *)L->l2carry, MaxU64(), (int)L->n_pkts + 1,
@@ -3629,7 +3660,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         hipLaunchKernelGGL(te_fuzz_count, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
                            L->n_pkts, L->fuzz_blk);
         hipLaunchKernelGGL(te_fuzz_scan, dim3(1), dim3(1024), 0, stream, L->fuzz_blk, nblk, L->fuzz_words,
-                           L->fuzz_probe_only ? 0 : 1);
+                           L->fuzz_probe_only ? 0 : L->q18_only ? 2 : 1);
         if (L->fuzz_probe_only) return hipGetLastError() == hipSuccess ? 0 : -1;
         hipLaunchKernelGGL(te_fuzz_states, dim3(nblk), dim3(FZ_BLOCK), 0, stream, (const uint8_t *)L->status,
                            L->n_pkts, (const uint32_t *)L->fuzz_blk, (const uint32_t *)L->fuzz_words,
@@ -3640,7 +3671,8 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         a.fuzz_mode = TE_FUZZ_APPLY;
         a.fuzz_state = L->fuzz_states;
     }
-    if (!fast && l2carry_prepare(L, a, stream) != 0) return -1;
+    if (!fast && l2carry_prepare(L, a, stream, grid) != 0) return -1;
+    if (L->q18_only) return L->fuzz_states && L->l2carry && hipGetLastError() == hipSuccess ? 0 : -1;
     const bool ev = !fast && L->ev_k0;  // without the fast lane this kernel is the edit kernel
     if (ev && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
     launch_generic(a.fuzz_mode != TE_FUZZ_OFF, L->any_dec != 0, L->slot_layout != 0, grid, stream, a);

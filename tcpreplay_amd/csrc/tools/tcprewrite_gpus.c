@@ -39,6 +39,7 @@ typedef struct {
     tcpedit_batch_t *b;
     int opened, rc;
     int jfail;          /* the Juniper state seeding failed (read by all after the inner barrier) */
+    int ffail, skipped; /* the fuzz skip (and the carry-out after it) failed / was applied */
     int64_t reach;
     int carry;
     int jnpr;                                 /* DLT_JUNIPER_ETHER: the decoder-state exchange runs */
@@ -153,6 +154,25 @@ static void *shard_main(void *arg)
     }
     for (int j = 0; j < k; j++)
         skip += (uint64_t)J->sh[j].reach;
+    int any_fz = 0;
+    for (int j = 0; j < J->n; j++)
+        any_fz |= J->sh[j].reach > 0;
+    if (all_open && any_fz) {
+        /* --fuzz-seed: this shard's RNG stream starts after the earlier shards' draws; with the
+           dst_modified carry a fuzzed record's second encode writes it, so a
+           shard that fuzzes after earlier draws finds its carry-out again from there */
+        if ((skip && tcpedit_fuzz_skip(S->te, skip) < 0) ||
+            (S->reach > 0 && skip && (S->carry = tcpedit_batch_l2carry_out(S->te, S->b)) < 0)) {
+            snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
+            S->ffail = 1;
+        }
+        S->skipped = 1;
+        pthread_barrier_wait(&J->bar);
+        for (int j = 0; j < J->n; j++)
+            all_open &= !J->sh[j].ffail;
+        if (S->ffail)
+            S->opened = 0;
+    }
     for (int j = k - 1; j >= 0; j--)
         if (J->sh[j].carry == 0 || J->sh[j].carry == 1) {
             carry_in = J->sh[j].carry;
@@ -161,7 +181,7 @@ static void *shard_main(void *arg)
     S->rc = TCPEDIT_ERROR;
     uint64_t cnt[NCNT] = {0};
     if (all_open) {
-        if ((skip && tcpedit_fuzz_skip(S->te, skip) < 0) || tcpedit_set_l2carry(S->te, carry_in) < 0) {
+        if ((skip && !S->skipped && tcpedit_fuzz_skip(S->te, skip) < 0) || tcpedit_set_l2carry(S->te, carry_in) < 0) {
             snprintf(S->err, sizeof S->err, "device %d: %s", k, tcpedit_geterr(S->te));
         } else {
             S->rc = tcpedit_batch_run(S->te, S->b);

@@ -142,17 +142,23 @@ def _pre_edit(dist, cdev, sh):
     words = list(struct.unpack("<6q", bytes(jst)[:48]))
     mine = torch.tensor([1 if ok else 0, sh.reach if ok else 0, sh.carry if ok else 2, 1 if jnpr else 0,
                          1 if jv else 0] + words, dtype=torch.int64, device=cdev)
+    # (--fuzz-seed with the dst_modified carry: a fuzzed record's second encode writes it, so
+    # a shard that fuzzes after earlier shards' draws finds its carry-out again from there)
     allv = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allv, mine)
     rows = [[int(x) for x in v.tolist()] for v in allv]
     bad = [r for r in range(world) if not rows[r][0]]
     skip = sum(rows[r][1] for r in range(rank))
-    if not bad and any(rows[r][3] for r in range(world)):
-        # the nearest earlier shard with a whole Juniper decode seeds this one's state
-        src = next((r for r in range(rank - 1, -1, -1) if rows[r][4]), None)
+    any_j = any(rows[r][3] for r in range(world))
+    any_fz = any(rows[r][1] for r in range(world))
+    if not bad and (any_j or any_fz):
         err = ""
         try:
-            sh.seed_jnpr(struct.pack("<6q", *rows[src][5:11]) if src is not None else None)
+            if any_j:  # the nearest earlier shard with a whole Juniper decode seeds this one's state
+                src = next((r for r in range(rank - 1, -1, -1) if rows[r][4]), None)
+                sh.seed_jnpr(struct.pack("<6q", *rows[src][5:11]) if src is not None else None)
+            if any_fz:
+                sh.skip_fuzz(skip)
         except Exception as e:  # noqa: BLE001 -- every rank raises after the exchange
             err = str(e)
         mine = torch.tensor([0 if err else 1, sh.carry if not err else 2], dtype=torch.int64, device=cdev)
@@ -261,6 +267,7 @@ class _DeviceShard:
         from . import Batch, TcpEdit
         self.te = TcpEdit(args, dlt=capture_dlt(hdr if hdr is not None else seg), device=device)
         self.b, self.prefix = None, None
+        self.fz_skipped = False
         try:
             self.b = Batch(self.te, seg, cache, pkt_base=pkt_base, hdr=hdr)
             if prefix is not None and len(prefix):
@@ -286,9 +293,19 @@ class _DeviceShard:
         self.te.set_jnpr_state(state)
         self.carry = self.b.l2carry_out()
 
+    def skip_fuzz(self, skip: int):
+        """the earlier shards' fuzz draws (the RNG stream is run-wide); a shard that fuzzes
+        after them finds its dst_modified carry-out again (a fuzzed record's second encode
+        writes it)"""
+        if skip:
+            self.te.fuzz_skip(skip)
+        self.fz_skipped = True
+        if self.reach and skip:
+            self.carry = self.b.l2carry_out()
+
     def run(self, fuzz_skip: int, carry_in: Optional[int]):
         """the edit, after the earlier shards' fuzz draws and with their carry"""
-        if fuzz_skip:
+        if fuzz_skip and not self.fz_skipped:
             self.te.fuzz_skip(fuzz_skip)
         if carry_in is not None:
             self.te.set_l2carry(carry_in)

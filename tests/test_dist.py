@@ -512,6 +512,16 @@ def _cache_of(dirs):
 
 
 def q18_job(kind="sll"):
+    if kind == "80211fz":
+        # --fuzz-seed: a fuzzed record's second encode writes the carry too, and shard 1's RNG
+        # stream starts after shard 0's draws (the reach exchange, then its carry-out again)
+        import test_dlt_wireless as W
+        pcap, cache, _ = W.q18_fuzz_capture(1200, seed=8)
+        return pcap, W.Q18_FZ_ARGS[:2] + ["--fuzz-factor=3"], cache, 105
+    return _q18_job(kind)
+
+
+def _q18_job(kind):
     """SURVEY Q18 across a shard cut: a cooked capture whose IPv4 destinations are all
     multicast; every record before the 2-rank cut is C2S (the last one sets the en10mb
     encoder's dst_modified: its cooked header's first bytes are not the zero destination),
@@ -545,7 +555,7 @@ def _q18_worker(rank, world, port, kind, use_file, d, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,use_file", [("sll", False), ("sll2", True)])
+@pytest.mark.parametrize("kind,use_file", [("sll", False), ("sll2", True), ("80211fz", False), ("80211fz", True)])
 def test_two_rank_gpu_q18_carry_crosses_the_cut(built, kind, use_file):
     """the dst_modified carry of the last C2S record of shard 0 reaches shard
     1's first S2C records (the pre-edit exchange), as the single-process reference run has it"""

@@ -95,7 +95,7 @@ def test_oracle_cooked_source_address_and_zero_destination(built):
 
 def test_unserved_combinations_are_refused(built):
     te = TA.TcpEdit
-    for dlt, args in [(113, ["--fuzz-seed=3", "--dlt=enet"]), (1, ["--dlt=tokenring"])]:
+    for dlt, args in [(1, ["--dlt=tokenring"])]:
         with pytest.raises(Exception):
             te(args, dlt=dlt)
     with pytest.raises(Exception):

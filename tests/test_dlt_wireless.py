@@ -21,6 +21,8 @@ the oracle, bit-exact.  Reference behaviours kept:
     VLAN fields) -- zeros before the first, whose sub-decoder extra then becomes the
     encoder's (a fresh dst_modified).  The device carries it with a mark + max scan over
     the records (te_jnpr_mark), across launches, pipeline chunks and shards."""
+import struct
+
 import pytest
 
 import oracle_lib as O
@@ -115,11 +117,87 @@ def test_oracle_jnpr_into_ethernet_strips_header_and_tag(built):
     assert S.records(out) == exp
 
 
-def test_unserved_combinations_are_refused(built):
-    # (--fuzz-seed with the en10mb encoder's dst_modified carry, SURVEY Q18: no --enet-dmac)
+def test_fuzz_with_the_dst_modified_carry_is_served(built):
+    # (--fuzz-seed with the en10mb encoder's dst_modified carry, SURVEY Q18: no --enet-dmac;
+    # refused through round 4, served by the carry's mark run of the edit since round 5)
     for dlt, args in [(105, ["--fuzz-seed=3", "--dlt=enet"]), (178, ["--fuzz-seed=3", "--dlt=enet"])]:
-        with pytest.raises(Exception):
-            TA.TcpEdit(args, dlt=dlt)
+        TA.TcpEdit(args, dlt=dlt).close()
+
+
+# ------------------------------------------- Q18 under --fuzz-seed: the second encode writes
+def _cache_of(dirs):
+    """a tcpprep v04 cache (cache.h:63-72) from per-record directions (1 C2S, 2 S2C)"""
+    body = bytearray((len(dirs) + 3) // 4)
+    for i, d in enumerate(dirs):
+        body[i // 4] |= (0b11 if d == 1 else 0b10) << (2 * (i % 4))
+    return b"tcpprep\0" + b"04\0\0" + struct.pack(">QHH", len(dirs), 4, 0) + bytes(body)
+
+
+def q18_fuzz_capture(n=1500, seed=5):
+    """802.11 data frames (ToDS = FromDS = 0: destination = addr3, tcpedit's
+    ieee80211_get_dst) around IPv4/UDP, in four kinds, with their directions:
+      A  C2S; addr3 = the frame's first 6 bytes (FC, duration, addr1[0:2]), so the first
+         encode writes dst_modified = 0; the IP checksum is 0xAAAA, so the second decode
+         (tcpedit.c:89: the re-encoded Ethernet frame read as 802.11 -- its destination
+         08:00:.. a data frame control word, SNAP at the IP checksum) succeeds and the second
+         encode writes dst_modified = 1 (en10mb.c:614)
+      B  C2S as A but an ordinary checksum: the second decode fails, the carry stays 0
+      C  S2C, second decode as A, the UDP payload's bytes 6..9 a multicast address that the
+         second pass reads as the IPv4 destination: its multicast MAC update (en10mb.c:
+         868-873) shows the carried value
+      D  C2S, addr3 not the first 6 bytes (dst_modified = 1), second decode fails
+    Every record reaches the fuzz step, so every one goes through the second pass; a high
+    --fuzz-factor fuzzes few of them."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    recs, dirs, kinds = [], [], []
+    for i in range(n):
+        k = "ABCD"[int(rng.integers(0, 4))] if i else "A"
+        plen = int(rng.integers(16, 120))
+        pay = bytearray(rng.integers(0, 256, plen, dtype=np.uint8).tobytes())
+        pay[6:10] = bytes([224 + i % 16, 1, 2, 3])
+        ulen = 8 + plen
+        udp = struct.pack(">HHHH", int(rng.integers(1024, 65535)), 53, ulen, 0x12FD)
+        dst_ip = bytes([8, 0, 0x45, int(rng.integers(0, 256))])
+        csum = b"\xaa\xaa" if k in "AC" else b"\x12\x34"
+        ip = (bytes([0x45, 0]) + struct.pack(">HH", 20 + ulen, i & 0xFFFF) + b"\x40\x00\x40\x11" + csum +
+              bytes([10, 1, int(rng.integers(0, 256)), int(rng.integers(0, 256))]) + dst_ip)
+        dur = rng.integers(0, 256, 2, dtype=np.uint8).tobytes()
+        a1 = rng.integers(0, 256, 6, dtype=np.uint8).tobytes()
+        a2 = bytes([2]) + rng.integers(0, 256, 5, dtype=np.uint8).tobytes()
+        a3 = b"\x08\x00" + dur + a1[:2]
+        if k == "D":
+            a3 = b"\x08\x00" + bytes([dur[0] ^ 0x5A]) + a3[3:]
+        frame = b"\x08\x00" + dur + a1 + a2 + a3 + b"\x10\x00" + b"\xaa\xaa\x03\x00\x00\x00\x08\x00" + ip + udp + bytes(pay)
+        recs.append((1600000000 + i // 1000, i % 1000 * 1000, len(frame), len(frame), frame))
+        dirs.append(2 if k == "C" else 1)
+        kinds.append(k)
+    return S.build_pcap(recs, 105), _cache_of(dirs), kinds
+
+
+Q18_FZ_ARGS = ["--dlt=enet", "--fuzz-seed=9", "--fuzz-factor=64"]
+
+
+def test_oracle_second_encode_writes_the_carry(built):
+    """the restatement keeps the second encode's dst_modified write: an S2C record after an
+    A (first encode 0, second 1) skips the multicast MAC update, one after a B (0, no second
+    encode) takes it -- so a carry found from the first encodes alone would be wrong"""
+    pcap, cache, kinds = q18_fuzz_capture()
+    # (a factor no draw divides: no record is fuzzed, every one goes through the second pass)
+    rc, out = O.rewrite(pcap, Q18_FZ_ARGS[:2] + ["--fuzz-factor=1000000000"], cache)
+    assert rc == 0
+    got = S.records(out)
+    assert len(got) == len(kinds)
+    last, seen = None, {"A": 0, "B": 0}
+    for k, (_, _, _, _, d) in zip(kinds, got):
+        if k in "ABD":
+            last = k
+            continue
+        if last in ("A", "B"):
+            upd = d[:3] == b"\x01\x00\x5e"
+            assert upd == (last == "B"), (last, d[:6].hex())
+            seen[last] += 1
+    assert seen["A"] > 20 and seen["B"] > 20
 
 
 # ------------------------------------------------------------------------- GPU
@@ -185,6 +263,23 @@ def test_gpu_dst_modified_carries_across_s2c_records(built, kind):
     cache = S.tcpprep_cache(len(base), seed=5, nosend_every=9)
     args = ["--dlt=enet", "--fixcsum"]
     _gpu_vs_oracle(pcap, args, DLT_OF[kind], cache)
+
+
+@pytest.mark.gpu
+def test_gpu_second_encode_writes_the_carry(built):
+    """SURVEY Q18 under --fuzz-seed: the carry's mark run of the edit finds each record's
+    last dst_modified write, the second encode's included -- batch and 16 KiB pipeline
+    chunks equal the oracle"""
+    pcap, cache, _ = q18_fuzz_capture()
+    _gpu_vs_oracle(pcap, Q18_FZ_ARGS[:2] + ["--fuzz-factor=1000000000"], 105, cache)
+    _gpu_vs_oracle(pcap, Q18_FZ_ARGS, 105, cache)
+    rc_o, exp = O.rewrite(pcap, Q18_FZ_ARGS, cache)
+    te = TA.TcpEdit(Q18_FZ_ARGS, dlt=105)
+    try:
+        rc, out = te.rewrite_pipelined(pcap, cache, chunk_bytes=1 << 14)
+        assert (rc, out) == (rc_o, exp)
+    finally:
+        te.close()
 
 
 def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
