@@ -336,7 +336,8 @@ int tcpprep_parse_args(tcpprep_hip_t *t, int argc, char **argv)
     }
     if (t->has_comment) {
         size_t l = strlen(full);
-        snprintf(full + l, sizeof full - l, "\n%s", t->comment);
+        if (snprintf(full + l, sizeof full - l, "\n%s", t->comment) >= (int)(sizeof full - l))
+            full[sizeof full - 1] = 0; /* (cut at the comment's bound, as the copy below is) */
     }
     memcpy(t->comment, full, sizeof full);
     if (strlen(t->comment) > 65535)

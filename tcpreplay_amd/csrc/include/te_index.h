@@ -11,7 +11,7 @@
 #define TE_IDX_S 80     /* sub-window bytes per lane: a wave stages 64 x TE_IDX_S bytes */
 #endif
 #ifndef TE_IDX_OL
-#define TE_IDX_OL 7     /* of which the first TE_IDX_OL sub-windows are the previous window's
+#define TE_IDX_OL 2     /* of which the first TE_IDX_OL sub-windows are the previous window's
                            last bytes (they establish the chain entering the window) */
 #endif
 #define IDX_NONE 0xffffffffffffffffull

@@ -1339,20 +1339,27 @@ constexpr int wk_nch(int tb) { return tb / 16 + 2; }
 // the bytes a window's last record may reach past the staged window (a longer one is left to
 // the exact path), and the window image: front pad, the staged window, that tail, slack
 #ifndef TE_WIN_S
-#define TE_WIN_S 64  // bytes a lane scans: a window is 64 of them
+#define TE_WIN_S 80  // bytes a lane scans: a window is 64 of them
 #endif
 #ifndef TE_WIN_OL
-#define TE_WIN_OL 7  // of which the first TE_WIN_OL lanes' are the previous window's
+#define TE_WIN_OL 2  // of which the first TE_WIN_OL lanes' are the previous window's
 #endif
 constexpr int WIN_S = TE_WIN_S, WIN_OL = TE_WIN_OL;
 constexpr int WIN_W = 64 * WIN_S, WIN_WN = WIN_W - WIN_OL * WIN_S;
-constexpr int WIN_TAIL = 2048;
+#ifndef TE_WIN_TAIL
+#define TE_WIN_TAIL 2048
+#endif
+constexpr int WIN_TAIL = TE_WIN_TAIL;
 // staged with the window past its end + 16 (five 1 KiB wave loads in all): the last
 // record reaching past the window is in LDS without a second, dependent load unless longer
-constexpr int WIN_PRE = 1024 * ((WIN_W + 48 + 900 + 1023) / 1024) - WIN_W - 48;
+#ifndef TE_WIN_PRE
+#define TE_WIN_PRE (-1)  // (A/B: the bytes staged past a window's end + 16; -1: fill the last 1 KiB load)
+#endif
+constexpr int WIN_PRE = TE_WIN_PRE >= 0 ? TE_WIN_PRE : 1024 * ((WIN_W + 48 + 900 + 1023) / 1024) - WIN_W - 48;
 static_assert(WIN_PRE >= 0 && WIN_PRE <= WIN_TAIL, "window pre-staging within the tail room");
 constexpr int WIN_IMG = LDS_FRONT + WIN_W + 48 + WIN_TAIL + 128;
 constexpr int WIN_REL = 4 * WIN_S + 1;
+static_assert(WIN_W + 48 + WIN_TAIL < 65536, "record offsets from a window's start fit 16 bits");
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
 static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
 static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
@@ -1738,12 +1745,15 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 #ifndef TE_WIN_BLOCKS
 #define TE_WIN_BLOCKS TE_WK_MIN_BLOCKS  // window mode: blocks per CU (its VGPR budget)
 #endif
+#ifndef TE_WIN_LEAN_BLOCKS
+#define TE_WIN_LEAN_BLOCKS TE_WIN_BLOCKS  // ... for the lean instances (no cfg copy in LDS)
+#endif
 // (SZ_FUZZ: TE_WK_FUZZ_BLOCKS per CU, one fewer with the address maps -- at the lean
 //  instances' 5 / the others' 4 the fuzz step's registers spill)
 #ifndef TE_WK_FUZZ_BLOCKS
 #define TE_WK_FUZZ_BLOCKS TE_WK_MIN_BLOCKS
 #endif
-__global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
+__global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_WIN_BLOCKS : TE_WIN_LEAN_BLOCKS)
                                        : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_FUZZ_BLOCKS - 1 : TE_WK_FUZZ_BLOCKS)
                                                        : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
@@ -1758,7 +1768,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
     __shared__ __attribute__((aligned(16))) uint8_t cfg_raw[WkCfg<F>::reads ? sizeof(te_dev_cfg_t) : 16];
     const te_dev_cfg_t &cfg = *(const te_dev_cfg_t *)cfg_raw;
     __shared__ unsigned long long red[WK_NW][6];
-    __shared__ uint32_t RELB[WIN ? WK_NW : 1][WIN ? WIN_REL : 1];  // window mode: record offsets
+    __shared__ uint16_t RELB[WIN ? WK_NW : 1][WIN ? WIN_REL : 1];  // window mode: record offsets
     const int tid = threadIdx.x;
     int lane = tid & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
@@ -2192,7 +2202,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
         ia.sw = 0;
         ia.nsec = 0;
         uint8_t *const IMG = SB[wid];       // the staged window at IMG + LDS_FRONT
-        uint32_t *const REL = RELB[WIN ? wid : 0];
+        uint16_t *const REL = RELB[WIN ? wid : 0];
         // TE_WIN_PREFETCH: the next window's staging in flight in registers while this one
         // is edited (A/B: on C2 it cost more in registers -- spills at 4 blocks/CU, or a
         // quarter of the occupancy at 3 -- than the overlap won)
@@ -2204,11 +2214,11 @@ __global__ void __launch_bounds__(WKB, WIN              ? TE_WIN_BLOCKS
 #if TE_WK_STAMPS
             WK_STAMP(5)  // (window mode: the staging)
             const tew::Found fw =
-                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k, fph);
+                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true, uint16_t>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k, fph);
             last_ = __builtin_amdgcn_s_memtime();
 #else
             const tew::Found fw =
-                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
+                tew::find_window<WIN_S, WIN_OL, WIN_PRE, true, uint16_t>(ia, (uint32_t *)(IMG + LDS_FRONT), REL, k);
 #endif
             if (TE_WIN_PREFETCH && k + W < a.nwin) tew::stage_load(ia, k + W, stg);
             WK_STAMP(0)  // (window mode: the record discovery)

@@ -157,14 +157,15 @@ __device__ __forceinline__ void stage_store(const IdxArgs &a, u32 k, const Stagi
     }
 }
 
-// img: (W + 48 + PRE) / 4 dwords at least (W = 64 S); rel: 4 S + 1 entries.  PRE: bytes
+// img: (W + 48 + PRE) / 4 dwords at least (W = 64 S); rel: 4 S + 1 entries (R: u16 when
+// every offset from ws fits, the fused edit's LDS budget).  PRE: bytes
 // staged past the window's end + 16 (the fused edit's last record reaching past the window:
 // in LDS with the window, no second dependent load for it).  STAGED: the caller has stored
 // window k's staging into img already (stage_load / stage_store)
 // ts: (diagnostic builds) s_memtime per phase added to ts[0..4]: candidates, walks,
 // confirmation, Jacobi rounds, positions -- or null
-template <int S, int OL, int PRE = 0, bool STAGED = false>
-__device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *rel, u32 k,
+template <int S, int OL, int PRE = 0, bool STAGED = false, typename R = u32>
+__device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, R *rel, u32 k,
                                              unsigned long long *ts = nullptr) {
     unsigned long long tl_ = ts ? __builtin_amdgcn_s_memtime() : 0ull;
 #define TEW_STAMP(i)                                                    \
@@ -400,12 +401,12 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, u32 *re
     if (has) {
         u64 off = e;
         for (u32 i = 0; i < w.n; ++i) {
-            rel[pos + i] = (u32)(off - ws);
+            rel[pos + i] = (R)(off - ws);
             const u32 cl = sw32(lds_u32(img, (u32)(off - A0) + 8), a.sw),
                       pl = sw32(lds_u32(img, (u32)(off - A0) + 12), a.sw);
             zero |= pl < cl;  // safe_pcap_next trims it: the exact path places it by scan
             off += 16 + (u64)cl;
-            if (pos + i + 1 == nrec) rel[nrec] = (u32)(off - ws);  // the last record's end
+            if (pos + i + 1 == nrec) rel[nrec] = (R)(off - ws);  // the last record's end
         }
     }
     const bool anytrim = __ballot(zero) != 0;
