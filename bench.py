@@ -495,7 +495,7 @@ def main():
                 "ms": round(fms, 5), "mpkt_s": round(r.packets / (fms * 1e-3) / 1e6, 1),
                 "frac_hbm_peak": round(alg_bytes / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "same_bytes_as_exact_path": bool(same),
-                "path": "window mode: each wave stages 4 KiB windows of the raw capture, finds the records "
+                "path": "window mode: each wave stages 5 KiB windows of the raw capture, finds the records "
                         "(speculative boundary guesses checked along the chain), edits them in LDS and "
                         "stores them; te_win_check verifies the chain across windows"}
             if not same:
