@@ -282,6 +282,26 @@ def test_gpu_second_encode_writes_the_carry(built):
         te.close()
 
 
+@pytest.mark.gpu
+def test_gpu_second_encode_carry_per_packet(built):
+    """the same through tcpedit_packet, record by record with each record's direction: the
+    carry and the RNG state cross the calls in the context (launch per call)"""
+    pcap, cache, kinds = q18_fuzz_capture(400, seed=6)
+    args = Q18_FZ_ARGS[:2] + ["--fuzz-factor=1000000000"]
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    te = TA.TcpEdit(args, dlt=105)
+    try:
+        got = []
+        for k, (ts, tu, cl, ln, d) in zip(kinds, S.records(pcap)):
+            buf = bytearray(d) + bytearray(262166)
+            rc, h = te.packet({"ts_sec": ts, "ts_usec": tu, "caplen": cl, "len": ln}, buf, 2 if k == "C" else 1)
+            assert rc != -1, te.geterr()
+            got.append((h["ts_sec"], h["ts_usec"], h["caplen"], h["len"], bytes(buf[:h["caplen"]])))
+        assert got == S.records(exp)
+    finally:
+        te.close()
+
+
 def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
     """a Juniper capture whose records lead, lead + 1, ... (the first `lead` records, then
     every `every`-th) carry encapsulation 15 (not Ethernet: TCPEDIT_WARN); every 4th inner
