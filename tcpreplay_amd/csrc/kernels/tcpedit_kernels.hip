@@ -1316,11 +1316,20 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_LEAN_TILE_BYTES
 #define TE_WK_LEAN_TILE_BYTES 5120
 #endif
-template <uint32_t F>
+// The lean size-preserving instances of the exact path (tiles from the host index) cut tiles
+// to TE_WK_BIG_TILE_BYTES at 4 blocks/CU: a 1,514-byte record's tile then holds five records,
+// not three (C5 0.585 -> 0.627 of peak, C2 and c2x10 unchanged: 64 records cap a C2 tile
+// either way; A/B on one box, tools/gpu_abbench.sh).  Window mode and the sized
+// instances keep TE_WK_LEAN_TILE_BYTES (their LDS budgets hold 4 and 5 blocks/CU).
+#ifndef TE_WK_BIG_TILE_BYTES
+#define TE_WK_BIG_TILE_BYTES 8192
+#endif
+template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
-    static constexpr int blocks = reads ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
-    static constexpr int tile = reads ? TE_WK_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
+    static constexpr bool big = !reads && SZ == 0 && !WIN;
+    static constexpr int blocks = reads || big ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
+    static constexpr int tile = reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
 };
 #ifndef TE_WK_STORE_BARRIER
 #define TE_WK_STORE_BARRIER 1
@@ -1755,8 +1764,8 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 #endif
 __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_WIN_BLOCKS : TE_WIN_LEAN_BLOCKS)
                                        : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_FUZZ_BLOCKS - 1 : TE_WK_FUZZ_BLOCKS)
-                                                       : WkCfg<F>::blocks) te_wave_tiles(FastArgs a) {
-    constexpr int TB = WkCfg<F>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
+                                                       : (WkCfg<F, SZ, WIN>::blocks)) te_wave_tiles(FastArgs a) {
+    constexpr int TB = WkCfg<F, SZ, WIN>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
     constexpr bool MTU = SZ == SZ_MTU, FUZZ = SZ == SZ_FUZZ;
@@ -2848,6 +2857,7 @@ extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz) {
     const int k = wave_pick(fast_feat(c), sz);
     if (k < 0) return TE_WK_TILE_BYTES;
     return (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) ? TE_WK_TILE_BYTES
+           : wave_inst[k].sz == SZ_NONE                                                 ? TE_WK_BIG_TILE_BYTES
                                                                                        : TE_WK_LEAN_TILE_BYTES;
 }
 
