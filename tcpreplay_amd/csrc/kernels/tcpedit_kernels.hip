@@ -1371,6 +1371,10 @@ constexpr int WIN_REL = 4 * WIN_S + 1;
 static_assert(WIN_W + 48 + WIN_TAIL < 65536, "record offsets from a window's start fit 16 bits");
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
 static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
+// the sized stores (VLAN push / pop, --efcs: the instances that read the cfg) map a tile's
+// output chunks in 512 16-bit entries, laid out for 6 KiB tiles; 7 and 8 KiB builds wrote
+// wrong C4 bytes (A/B builds, round 5), so the budget is pinned
+static_assert(TE_WK_TILE_BYTES == 6144, "the sized stores' chunk map is laid out for 6 KiB tiles");
 static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
 static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
 
