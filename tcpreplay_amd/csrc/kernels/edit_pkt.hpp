@@ -77,6 +77,10 @@ struct Pkt {
     // extensions are not Ethernet is encoded with.  Neither: not at hand (fails loudly)
     const te_jstate_t *jc = nullptr;
     bool jnone = false;
+    // ... and as this record's own first pass leaves it (its whole decode, else the same):
+    // what the second decode of a fuzzed record reads when it is a warning frame
+    const te_jstate_t *jc2 = nullptr;
+    bool jnone2 = false;
     // the generic lane's tile (LDS) path: do_checksum leaves the L4 payload sum to the block
     // (all 256 threads sum every record's L4 bytes in 64-byte pieces) and records the job;
     // the lane writes the field once the block has summed (tile_body)
@@ -1780,13 +1784,17 @@ again:  // :89 -- after the fuzz step the packet goes through L2 and the L3 edit
     } else {
         if constexpr (FZ && ANYDEC) {
             // the second decode of a fuzzed record (tcpedit.c:89,250-258) by the Juniper
-            // decoder: a header it takes would write the carried state, or a warning read the
-            // one this record's first decode wrote -- neither is what the state scan saw
+            // decoder: a warning frame reads the state this record's first pass left (its own
+            // whole decode, else the carried one: the scan's next entry); a whole decode
+            // would write state the scan did not see -- not served (fails loudly)
             u32 hl = 0;
-            if (cfg.decoder == TE_DEC_JNPR && fz_mode == TE_FUZZ_APPLY && !fuzz_once &&
-                jnpr_header(pk.d, pk.caplen, hl) != RC_ERROR) {
-                stale(pk, (int)NEED_NEVER);
-                return RC_SOFT;
+            if (cfg.decoder == TE_DEC_JNPR && fz_mode == TE_FUZZ_APPLY && !fuzz_once) {
+                pk.jc = pk.jc2;
+                pk.jnone = pk.jnone2;
+                if (jnpr_header(pk.d, pk.caplen, hl) == RC_OK) {
+                    stale(pk, (int)NEED_NEVER);
+                    return RC_SOFT;
+                }
             }
         }
         if ((ANYDEC && cfg.decoder != TE_DEC_EN10MB ? foreign_decode(pk, cfg, s)

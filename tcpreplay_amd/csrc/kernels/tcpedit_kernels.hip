@@ -115,15 +115,23 @@ struct LaunchArgs {
 
 // the Juniper decoder state record j (launch-relative) is encoded with, should its frame
 // be a TCPEDIT_WARN one (jnpr_ether.c:269-272)
+// (and, for a fuzzed record's second decode, the state after its own first pass: the
+// inclusive scan's next entry, j + 1 -- the scan has n + 1 entries)
 __device__ __forceinline__ void jnpr_carry(const LaunchArgs &a, uint64_t j, Pkt &pk) {
     if (!a.jscan) return;
-    const unsigned long long i = a.jscan[j];
+    const unsigned long long i = a.jscan[j], i2 = a.jscan[j + 1];
+    const uint32_t v = a.jctx->valid;
     if (i) {
         pk.jc = &a.jstates[i];
     } else {
-        const uint32_t v = a.jctx->valid;
         if (v == TE_JC_VALID) pk.jc = &a.jctx->st;
         else if (v == TE_JC_NONE) pk.jnone = true;
+    }
+    if (i2) {
+        pk.jc2 = &a.jstates[i2];
+    } else {
+        if (v == TE_JC_VALID) pk.jc2 = &a.jctx->st;
+        else if (v == TE_JC_NONE) pk.jnone2 = true;
     }
 }
 

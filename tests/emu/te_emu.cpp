@@ -163,6 +163,9 @@ int main(int argc, char **argv) {
             pk.defer = false;
             pk.jc = jvalid ? &jst : nullptr;
             pk.jnone = !jvalid;
+            // (a fuzzed record's second decode: the state after its own first pass)
+            pk.jc2 = jwhole ? &jnext : pk.jc;
+            pk.jnone2 = !jwhole && !jvalid;
             if (dir == TE_DIR_NOSEND) break;  // tcprewrite.c:314-315: written unedited
             const uint32_t mode = !fz ? TE_FUZZ_OFF : pass == 0 ? TE_FUZZ_PROBE : TE_FUZZ_APPLY;
             const uint32_t st = pass == 1 && reached ? fstate : 0u;

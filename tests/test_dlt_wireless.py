@@ -322,6 +322,40 @@ def _jnpr_warn(n=600, seed=4, every=7, lead=3, cut=None):
     return S.build_pcap(recs, 178), warn
 
 
+JMAGIC_DMAC = "4d:47:43:80:00:00"  # the Juniper magic + L2-present flag + no extensions
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q18", [False, True])
+def test_gpu_second_decode_is_a_juniper_warning_frame(built, q18):
+    """--fuzz-seed behind the Juniper decoder into --dlt=enet, where the re-encoded frame
+    starts with the Juniper magic (its destination 4d:47:43:80:00:00: a header of 6 bytes and
+    no extensions), so every record's second decode (tcpedit.c:89,250-258) is a TCPEDIT_WARN
+    frame, encoded with the state its own first pass left (its whole inner decode, else the
+    carried one).  q18: the destination is the inner frame's own (no --enet-dmac), so the
+    dst_modified carry's mark run goes through those second encodes too.  Refused through
+    round 4; parity is unpinned (no reference capture), the oracle restates the sequence."""
+    pcap, _ = _jnpr_warn(700, seed=12)
+    if q18:
+        recs = []
+        for ts, tu, cl, ln, d in S.records(pcap):
+            d = bytearray(d)
+            hl = 6 + (d[4] << 8 | d[5])
+            if hl + 6 <= len(d):
+                d[hl:hl + 6] = bytes.fromhex(JMAGIC_DMAC.replace(":", ""))
+            recs.append((ts, tu, cl, ln, bytes(d)))
+        pcap = S.build_pcap(recs, 178)
+        args = ["--dlt=enet", "--enet-smac=00:11:22:33:44:55", "--fuzz-seed=3", "--fuzz-factor=4"]
+        cache = _cache_of([1 + (i % 3 == 1) for i in range(len(recs))])
+    else:
+        args = ["--dlt=enet", "--enet-dmac=" + JMAGIC_DMAC, "--enet-smac=00:11:22:33:44:55", "--fuzz-seed=5",
+                "--fuzz-factor=3"]
+        cache = None
+    rc_o, exp = O.rewrite(pcap, args, cache)
+    assert rc_o == 0
+    _gpu_vs_oracle(pcap, args, 178, cache)
+
+
 def test_oracle_jnpr_warning_frames_encode_with_the_carried_state(built):
     """--dlt=enet with both MACs: a warning frame gets a new Ethernet header in place of its
     Juniper header (only that header is its l2len), whose type is the carried proto -- the

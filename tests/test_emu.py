@@ -166,6 +166,18 @@ def test_emu_jnpr_warning_frames(emu, tmp_path, k):
     _check(emu, str(tmp_path), pcap, lines[k], 178)
 
 
+@pytest.mark.parametrize("k", range(2))
+def test_emu_jnpr_second_decode_is_a_warning_frame(emu, tmp_path, k):
+    """a fuzzed record's second decode taken by the Juniper decoder as a warning frame (the
+    re-encoded frame starts with the Juniper magic: --enet-dmac 4d:47:43:80:00:00) reads the
+    state its own first pass left (tests/test_dlt_wireless.py, GPU)"""
+    import test_dlt_wireless as W
+    pcap, _ = W._jnpr_warn(1200, seed=k + 61)
+    args = ["--dlt=enet", "--enet-dmac=" + W.JMAGIC_DMAC, "--enet-smac=00:11:22:33:44:55",
+            "--fuzz-seed=%d" % (k + 5), "--fuzz-factor=%d" % (k + 2)]
+    _check(emu, str(tmp_path), pcap, args, 178)
+
+
 def test_emu_headroom_holds_two_encodes(emu, tmp_path):
     """the config's headroom covers both encodes of a fuzzed record (te_slot_head)"""
     cfg, _ = _cfg(USER40 + ["--fuzz-seed=1"], 12)
