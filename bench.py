@@ -301,6 +301,76 @@ def strong_side(opt, world, rank, local, barrier):
                     "path is checked at N=1"}
 
 
+def e2e_line(opt):
+    """the end_to_end line: host pcap bytes -> host output bytes through the pipelined path,
+    run by `bench.py --e2e-child` in a process of its own (main() starts it)"""
+    import tcpreplay_amd as TA
+    n = opt.packets or DEFAULT_PACKETS[opt.workload]
+    pcap = make_pcap(opt.workload, n, seed=1)
+    # PCIe-inclusive rates (never `value`), host pcap bytes -> host output bytes,
+    # through the pipelined path (chunks of whole records, H2D | edit | D2H on three
+    # streams; median of 5 after a sizing run):
+    #   pinned:   capture and output in page-locked memory (as bin/tcprewrite reads
+    #             the file straight into it) -- the main figure;
+    #   pageable: ordinary buffers, page-locked by the library for each call;
+    #   one_shot: tcpedit_rewrite_pcap (device allocation, synchronous copies).
+    te3 = TA.TcpEdit(WORKLOADS[opt.workload][2], device=0)
+    src = bytearray(pcap)
+    rc3, out3 = te3.rewrite_pipelined(src)  # sizes the device slots
+    if not opt.no_verify:  # the pipelined path's output is the oracle's too
+        check_output_bytes(pcap, WORKLOADS[opt.workload][2], None, out3)
+    bound = te3.output_bound(src)
+    pin_in, pin_out = TA.PinnedBuffer(len(pcap)), TA.PinnedBuffer(bound)
+    pin_in.view[:] = pcap
+
+    def e2e(si, so, reps=9):
+        """median seconds of `reps` back-to-back runs, after 0.5 s of them: a fresh
+        context's first ~0.2 s of pipelined runs copy at about half speed (3.8-4.1 ms
+        against 2.09-2.14, every host-buffer kind alike, tools/e2e_host_ab.py)"""
+        t_warm = time.perf_counter() + 0.5
+        while time.perf_counter() < t_warm:
+            te3.rewrite_pipelined(si, out=so)
+        ts = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            rc, view = te3.rewrite_pipelined(si, out=so)
+            ts.append(time.perf_counter() - t1)
+            if rc != 0 or view != out3:
+                raise RuntimeError("pipelined end-to-end run differs from its first run")
+        return sorted(ts)[reps // 2]
+
+    p_s = e2e(pin_in.view, pin_out.view)
+    g_s = e2e(src, bytearray(bound))
+    floor_ms = copy_floor(ctypes.addressof(ctypes.c_char.from_buffer(pin_in.view)), len(pcap),
+                          ctypes.addressof(ctypes.c_char.from_buffer(pin_out.view)), len(out3))
+    one = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        rc3, _out = te3.rewrite(pcap)
+        one.append(time.perf_counter() - t1)
+    pin_in.close()
+    pin_out.close()
+    te3.close()
+    o_s = sorted(one)[1]
+
+    def rate(sec, path):
+        return {"mpkt_s": round(n / sec / 1e6, 2), "ms": round(sec * 1e3, 3),
+                "gbps_in": round(len(pcap) / sec / 1e9, 2), "path": path}
+    return dict(
+        rate(p_s, "page-locked host capture -> byte-range chunks (the default: a tenth of the capture, "
+                  "8-32 MiB; C/4 and C/2 first, halving last), H2D | window-mode edit (records found "
+                  "on the device, chain verdict gathered on the device) | D2H on three streams -> "
+                  "page-locked host output (median of 9 back-to-back runs after 0.5 s of them)"),
+        copy_floor_ms=round(floor_ms, 3) if floor_ms else None,
+        frac_of_copy_floor=round(floor_ms / (p_s * 1e3), 4) if floor_ms else None,
+        copy_floor="this box's PCIe floor: the capture up and the output down at once, one copy each on "
+                   "two streams, same page-locked buffers, no edit (median of 5)",
+        pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 9 "
+                           "back-to-back runs after 0.5 s of them, timed after the page-locked block)"),
+        one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
+                           "pageable copies (median of 3)"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -318,6 +388,7 @@ def main():
                     "(default: the CPUs this process may run on, at most 16 -- the GPU box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
+    ap.add_argument("--e2e-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of every workload's "
                     "first run (on by default: the bench line is parity evidence)")
     ap.add_argument("--no-strong-side", action="store_true", help="N > 1: skip the BASELINE configs[3] line "
@@ -328,6 +399,9 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="--strong: the job's total records "
                     "(default 100M for c4, else the config's size)")
     opt = ap.parse_args()
+    if opt.e2e_child:  # (main() of the parent process starts this)
+        print(json.dumps(e2e_line(opt)), flush=True)
+        return
     if opt.strong:  # one big job: the per-config side lines measure other things
         opt.extra, opt.no_e2e, opt.no_cpu_baseline = "", True, True
         opt.no_device_index = opt.no_packet_latency = True
@@ -555,72 +629,17 @@ def main():
         if extra:
             result["extra_configs"] = extra
         if not opt.no_e2e:
-            # PCIe-inclusive rates (never `value`), host pcap bytes -> host output bytes,
-            # through the pipelined path (chunks of whole records, H2D | edit | D2H on three
-            # streams; median of 5 after a sizing run):
-            #   pinned:   capture and output in page-locked memory (as bin/tcprewrite reads
-            #             the file straight into it) -- the main figure;
-            #   pageable: ordinary buffers, page-locked by the library for each call;
-            #   one_shot: tcpedit_rewrite_pcap (device allocation, synchronous copies).
-            te3 = TA.TcpEdit(WORKLOADS[opt.workload][2], device=0)
-            src = bytearray(pcap)
-            rc3, out3 = te3.rewrite_pipelined(src)  # sizes the device slots
-            if not opt.no_verify:  # the pipelined path's output is the oracle's too
-                check_output_bytes(pcap, WORKLOADS[opt.workload][2], None, out3)
-            bound = te3.output_bound(src)
-            pin_in, pin_out = TA.PinnedBuffer(len(pcap)), TA.PinnedBuffer(bound)
-            pin_in.view[:] = pcap
-
-            def e2e(kinds, reps=9):
-                """median seconds per buffer kind; the kinds' runs interleaved, so a slow spell
-                of the box's copies (seen for seconds at a time: DESIGN 6) hits them alike"""
-                ts = [[] for _ in kinds]
-                for _ in range(reps):
-                    for i, (si, so) in enumerate(kinds):
-                        t1 = time.perf_counter()
-                        rc, view = te3.rewrite_pipelined(si, out=so)
-                        ts[i].append(time.perf_counter() - t1)
-                        if rc != 0 or view != out3:
-                            raise RuntimeError("pipelined end-to-end run differs from its first run")
-                return [sorted(t)[reps // 2] for t in ts]
-
-            # warm the copy path first: a fresh context's first ~0.2 s of pipelined runs copy at
-            # about half speed (3.8-4.1 ms against 2.09-2.14 for every host-buffer kind alike,
-            # tools/e2e_host_ab.py, DESIGN 6) -- steady state is what the line reports
-            g_out = bytearray(bound)
-            t_warm = time.perf_counter() + 1.0
-            while time.perf_counter() < t_warm:
-                te3.rewrite_pipelined(pin_in.view, out=pin_out.view)
-                te3.rewrite_pipelined(src, out=g_out)
-            p_s, g_s = e2e([(pin_in.view, pin_out.view), (src, g_out)])
-            floor_ms = copy_floor(ctypes.addressof(ctypes.c_char.from_buffer(pin_in.view)), len(pcap),
-                                  ctypes.addressof(ctypes.c_char.from_buffer(pin_out.view)), len(out3))
-            one = []
-            for _ in range(3):
-                t1 = time.perf_counter()
-                rc3, _out = te3.rewrite(pcap)
-                one.append(time.perf_counter() - t1)
-            pin_in.close()
-            pin_out.close()
-            te3.close()
-            o_s = sorted(one)[1]
-
-            def rate(sec, path):
-                return {"mpkt_s": round(n / sec / 1e6, 2), "ms": round(sec * 1e3, 3),
-                        "gbps_in": round(len(pcap) / sec / 1e9, 2), "path": path}
-            result["end_to_end"] = dict(
-                rate(p_s, "page-locked host capture -> byte-range chunks (the default: a tenth of the capture, "
-                          "8-32 MiB; C/4 and C/2 first, halving last), H2D | window-mode edit (records found "
-                          "on the device, chain verdict gathered on the device) | D2H on three streams -> "
-                          "page-locked host output (median of 9, interleaved with the pageable runs, after 1 s "
-                          "of both to warm the copy path)"),
-                copy_floor_ms=round(floor_ms, 3) if floor_ms else None,
-                frac_of_copy_floor=round(floor_ms / (p_s * 1e3), 4) if floor_ms else None,
-                copy_floor="this box's PCIe floor: the capture up and the output down at once, one copy each on "
-                           "two streams, same page-locked buffers, no edit (median of 5)",
-                pageable=rate(g_s, "the same from ordinary host buffers, page-locked per call (median of 9)"),
-                one_shot=rate(o_s, "tcpedit_rewrite_pcap: device allocation, record index, synchronous "
-                                   "pageable copies (median of 3)"))
+            # PCIe-inclusive rates (never `value`): measured in a child process of their own
+            # (e2e_line), as a tcprewrite run has the device to itself -- inside this process,
+            # after the lines above, the same runs scattered over 2.3-2.9 ms against a steady
+            # 2.1 in a fresh one (tools/e2e_host_ab.py, tools/gpu_e2e_bench_ab.sh)
+            import subprocess
+            cmd = [sys.executable, os.path.abspath(__file__), "--e2e-child", "--workload", opt.workload,
+                   "--packets", str(n)] + (["--no-verify"] if opt.no_verify else [])
+            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            if cp.returncode != 0:
+                raise RuntimeError("end-to-end child failed: " + cp.stderr[-2000:])
+            result["end_to_end"] = json.loads(cp.stdout.strip().splitlines()[-1])
         if not opt.no_cpu_baseline and opt.workload not in CACHED:
             wl_args = WORKLOADS[opt.workload][2]
             v1, runs1, el1, _ = cpu_baseline(pcap, wl_args, n, opt.cpu_seconds / 2)

@@ -16,6 +16,18 @@ hip = ctypes.CDLL("libamdhip64.so")
 hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
 hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
 
+if "torch" in sys.argv[2:]:  # torch's HIP context first, as bench.py has it
+    import torch
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
+if "big" in sys.argv[2:]:  # a C4-sized batch first, as bench.py runs before its e2e lines
+    big = S.pcap_imix(12_500_000, seed=1)
+    te0 = TA.TcpEdit(["--seed=3", "--fixcsum"])
+    b0 = TA.Batch(te0, big)
+    b0.run()
+    b0.close()
+    te0.close()
+    del big
 pcap = S.pcap_fixed(1_000_000, 64, seed=1)
 te = TA.TcpEdit(["--seed=42", "--fixcsum"])
 rc, ref = te.rewrite_pipelined(pcap)
