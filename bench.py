@@ -343,6 +343,7 @@ def e2e_line(opt):
     g_s = e2e(src, bytearray(bound))
     floor_ms = copy_floor(ctypes.addressof(ctypes.c_char.from_buffer(pin_in.view)), len(pcap),
                           ctypes.addressof(ctypes.c_char.from_buffer(pin_out.view)), len(out3))
+    te3.rewrite(pcap)  # (its first call in a process allocates the one-shot buffers)
     one = []
     for _ in range(3):
         t1 = time.perf_counter()
