@@ -18,7 +18,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "te_index.h"
+
+#ifndef TE_WIN_CAND3
+#define TE_WIN_CAND3 1  // candidate masks from three dword zero-masks (0: per-byte flag nibbles, A/B)
+#endif
 
 namespace tew {
 typedef uint8_t u8;
@@ -225,8 +231,55 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, R *rel,
     if (k == kE && lane == laneE) {
         e = entry;  // the first record is known
     } else if (active) {
-        // zero flags of bytes [lo, lo + S + 16): dword d of the sub-window holds bytes 4d..4d+3
         const u32 q0 = (u32)(lo - A0);  // lane S: a multiple of 16
+        const bool us = !a.nsec;
+        u64 weak = IDX_NONE;
+        unsigned long long mh[(S + 63) / 64];
+#if TE_WIN_CAND3
+        // a header has a zero byte at +11 and +15 (caplen, len <= 262144), and at +7 when the
+        // fraction counts microseconds (< 10^6) -- +8, +12 and +4 in a big-endian capture:
+        // three bytes 4 apart, so the same byte lane of three consecutive dwords.  Candidate p
+        // = 4 D + b - zf for byte lane b of M_D = Z_D & Z_{D+1} & Z_{D+2} (Z: a dword's
+        // zero-byte flags), each M_D's four flags gathered into a nibble by one multiply
+        // (no per-dword nibble of every byte's flag, no 64-bit realignment of three masks)
+        {
+            constexpr int ND = S / 4 + 4;  // dwords of bytes [lo, lo + S + 16)
+            u32 Z[ND];
+#pragma unroll
+            for (int c = 0; c < ND / 4; ++c) {
+                const uint4 q = *(const uint4 *)&img[(q0 >> 2) + 4 * c];
+                Z[4 * c] = zero_bytes(q.x);
+                Z[4 * c + 1] = zero_bytes(q.y);
+                Z[4 * c + 2] = zero_bytes(q.z);
+                Z[4 * c + 3] = zero_bytes(q.w);
+            }
+            auto gather = [&](auto zfc) {
+                constexpr int ZF = decltype(zfc)::value;
+#pragma unroll
+                for (int h = 0; h < (S + 63) / 64; ++h) mh[h] = 0;
+#pragma unroll
+                for (int D = 1; D + 2 < ND; ++D) {
+                    const u32 M = (us ? Z[D] : 0xffffffffu) & Z[D + 1] & Z[D + 2];
+                    const u64 n = (u64)((((M >> 7) & 0x01010101u) * 0x01020408u) >> 24);  // flags of bytes 0..3
+                    const int sh = 4 * D - ZF;  // bit of byte lane 0's candidate (unrolled: constants)
+                    if (sh < 0) {
+                        mh[0] |= n >> (-sh);
+                    } else if (sh < S) {
+                        mh[sh >> 6] |= n << (sh & 63);
+                        if ((sh & 63) > 60 && (sh >> 6) + 1 < (S + 63) / 64) mh[(sh >> 6) + 1] |= n >> (64 - (sh & 63));
+                    }
+                }
+            };
+            if (a.sw) gather(std::integral_constant<int, 4>{});
+            else gather(std::integral_constant<int, 7>{});
+#pragma unroll
+            for (int h = 0; h < (S + 63) / 64; ++h) {
+                const int span = S - 64 * h;
+                if (span < 64) mh[h] &= (1ull << span) - 1ull;
+            }
+        }
+#else
+        // zero flags of bytes [lo, lo + S + 16): dword d of the sub-window holds bytes 4d..4d+3
         u64 z[3] = {0, 0, 0};
         // (16-byte LDS reads: the sub-window starts 16-aligned)
 #pragma unroll
@@ -246,16 +299,14 @@ __device__ __forceinline__ Found find_window(const IdxArgs &a, u32 *img, R *rel,
         // a header has a zero byte at +11 and +15 (caplen, len <= 262144), and at +7 when the
         // fraction counts microseconds (< 10^6) -- the high bytes: +8, +12 and +4 in a
         // big-endian capture
-        const bool us = !a.nsec;
         const int zc = a.sw ? 8 : 11, zl = a.sw ? 12 : 15, zf = a.sw ? 4 : 7;
-        u64 weak = IDX_NONE;
-        unsigned long long mh[(S + 63) / 64];
 #pragma unroll
         for (int h = 0; h < (S + 63) / 64; ++h) {
             mh[h] = bits_at(h, zc) & bits_at(h, zl) & (us ? bits_at(h, zf) : ~0ull);
             const int span = S - 64 * h;
             if (span < 64) mh[h] &= (1ull << span) - 1ull;
         }
+#endif
         // (one candidate at a time: batching the first four's header reads -- two LDS round
         // trips instead of two each -- ran slower, the lane is issue-bound here)
 #pragma unroll
