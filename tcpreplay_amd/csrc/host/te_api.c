@@ -1262,6 +1262,10 @@ typedef struct te_win_req_s {
 } te_win_req_t;
 /* the window workspace layout of d_win for `cap` windows: entries | exits | flags | bad | tot */
 #define WIN_WS_BYTES(cap) (16ull * (cap) + 4ull * (cap) + 64)
+/* the verdict word and the chain end, adjacent and 16-aligned: one 16-byte zeroing a launch
+   (a fill that is not 16-aligned ran as two fill kernels, ~5 us each: a tenth of a C2 run) */
+#define WIN_BAD_OFF(cap) ((20ull * (cap) + 15) & ~15ull)
+#define WIN_TOT_OFF(cap) (WIN_BAD_OFF(cap) + 8)
 static int launch(tcpedit_batch_t *b, int fixed_dir)
 {
     return launch_ev(b, fixed_dir, NULL, NULL, 0);
@@ -1541,8 +1545,8 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.w_entry = (uint64_t *)b->d_win;
         L.w_exit = L.w_entry + b->win_cap;
         L.w_flags = (uint32_t *)(L.w_exit + b->win_cap);
-        L.win_bad = L.w_flags + b->win_cap;
-        L.win_tot = (uint64_t *)(b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull));
+        L.win_bad = (uint32_t *)(b->d_win + WIN_BAD_OFF(b->win_cap));
+        L.win_tot = (uint64_t *)(b->d_win + WIN_TOT_OFF(b->win_cap));
         L.win_acc = q->acc;
         L.win_prev_out = q->prev_out;
         L.win_head_max = q->head_max;
@@ -2133,9 +2137,9 @@ static int fused_once(tcpedit_t *t, tcpedit_batch_t *b)
     HIPCHK(t, hipEventRecord(b->ev1, t->stream));
     uint32_t bad = 0;
     uint64_t tot = 0;
-    const uint8_t *wb = b->d_win + 20ull * b->win_cap;
+    const uint8_t *wb = b->d_win + WIN_BAD_OFF(b->win_cap);
     HIPCHK(t, hipMemcpyAsync(&bad, wb, 4, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(t, hipMemcpyAsync(&tot, b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull), 8, hipMemcpyDeviceToHost,
+    HIPCHK(t, hipMemcpyAsync(&tot, b->d_win + WIN_TOT_OFF(b->win_cap), 8, hipMemcpyDeviceToHost,
                              t->stream));
     if (!b->slots_host)
         b->slots_host = malloc(8 * TE_WK_SLOT_WORDS * (size_t)te_wave_grid());
@@ -3506,7 +3510,7 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         q.base = ORG;
         q.limit = f1 >= in_len ? b->in_len : ORG + (f1 - f0);
         q.nwin = (uint32_t)((q.limit - q.base + te_win_bytes() - 1) / te_win_bytes());
-        q.entry_ptr = k ? (const uint64_t *)(pb->d_win + ((20ull * pb->win_cap + 8 + 7) & ~7ull)) : NULL;
+        q.entry_ptr = k ? (const uint64_t *)(pb->d_win + WIN_TOT_OFF(pb->win_cap)) : NULL;
         q.entry_sub = k ? f0 - cst[k - 1] : 0; /* the previous chunk's image is that much earlier */
         q.acc = P->d_wacc;
         q.prev_out = k && !zc ? pb->d_out : NULL;
@@ -3541,7 +3545,7 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     {
         tcpedit_batch_t *b = P->slot[last];
         HIPCHK(t, hipMemcpyAsync(P->h_wacc, P->d_wacc, 32, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(t, hipMemcpyAsync(P->h_wacc + 4, b->d_win + ((20ull * b->win_cap + 8 + 7) & ~7ull), 8,
+        HIPCHK(t, hipMemcpyAsync(P->h_wacc + 4, b->d_win + WIN_TOT_OFF(b->win_cap), 8,
                                  hipMemcpyDeviceToHost, t->stream));
         HIPCHK(t, hipStreamSynchronize(t->stream));
         HIPCHK(t, hipStreamSynchronize(P->s_d2h));

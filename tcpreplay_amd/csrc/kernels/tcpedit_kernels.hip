@@ -928,8 +928,10 @@ struct FastArgs {
                                             //   are not the image's
     uint32_t nwin;
     uint64_t *w_entry, *w_exit;             // per window: where the chain enters and leaves it
-    uint32_t *w_flags;                      // per window: IDX_STOP / IDX_ERROR / IDX_END / IDX_TRIM
-    uint32_t *win_bad;                      // bit 1: a window left a record to the exact path
+    uint32_t *w_flags;                      // per window: IDX_STOP / IDX_ERROR / IDX_END / IDX_TRIM, WIN_F_EDIT
+    uint32_t *win_bad;                      // the verdict (te_win_check): bit 0 the chain, bit 1 a
+                                            //   record left to the exact path; zeroed here
+    unsigned long long *win_tot;            // the chain's end (te_win_check); zeroed here
 };
 
 // the window's partly valid dword for fl::phase_a: packet bytes [4k - 2, caplen), k =
@@ -1376,6 +1378,12 @@ constexpr int WIN_PRE = TE_WIN_PRE >= 0 ? TE_WIN_PRE : 1024 * ((WIN_W + 48 + 900
 static_assert(WIN_PRE >= 0 && WIN_PRE <= WIN_TAIL, "window pre-staging within the tail room");
 constexpr int WIN_IMG = LDS_FRONT + WIN_W + 48 + WIN_TAIL + 128;
 constexpr int WIN_REL = 4 * WIN_S + 1;
+// a window's flags word (w_flags): the discovery's chain stops (IDX_*), and this bit when
+// the edit left one of its records to the exact path -- te_win_check turns either into the
+// batch's verdict, so nothing writes the verdict words during the window kernel, which
+// zeroes them itself (no fill launch a run)
+constexpr uint32_t WIN_F_EDIT = 0x100u;
+static_assert((WIN_F_EDIT & (IDX_STOP | IDX_ERROR | IDX_END | IDX_TRIM)) == 0, "a flag bit of its own");
 static_assert(WIN_W + 48 + WIN_TAIL < 65536, "record offsets from a window's start fit 16 bits");
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
 static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
@@ -1884,7 +1892,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
             const uint32_t g0 = (uint32_t)(G0 - A0);
             if (wk_solo(tile, TB)) {  // a record larger than the image: the generic lane
                 if (WIN) {
-                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                    if (lane == 0) atomicOr(&a.w_flags[t], WIN_F_EDIT);
                 } else if (lane == 0) {
                     a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
                 }
@@ -2024,7 +2032,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
 #endif
             if (__ballot(!ok)) {  // a packet for the generic lane: it redoes this tile
                 if (WIN) {  // (window mode: the exact path redoes the batch)
-                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                    if (lane == 0) atomicOr(&a.w_flags[t], WIN_F_EDIT);
                 } else if (lane == 0) {
                     a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
                 }
@@ -2212,6 +2220,10 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
 
     if constexpr (WIN) {
         // ---- window mode: wave w takes windows w, w + W, ... ----
+        if (blockIdx.x == 0 && threadIdx.x == 0) {  // te_win_check, next on the stream, writes them
+            *a.win_bad = 0u;
+            *a.win_tot = 0ull;
+        }
         IdxArgs ia;
         ia.img = a.in;
         ia.len = a.win_len;
@@ -2257,7 +2269,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
             const uint64_t need = fw.wexit + 16;
             if (need > fw.staged_end) {
                 if (need - fw.A0 > (uint64_t)(WIN_W + 48 + WIN_TAIL)) {
-                    if (lane == 0) atomicOr(a.win_bad, 2u);
+                    if (lane == 0) atomicOr(&a.w_flags[k], WIN_F_EDIT);
                     continue;
                 }
                 const uint64_t c0 = (fw.staged_end & ~15ull) - fw.A0, c1 = ((need + 15) & ~15ull) - fw.A0;
@@ -2396,43 +2408,57 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
             if (p) atomicAdd(&w.acc[0], p);
             if (by) atomicAdd(&w.acc[1], by);
             if (e) atomicAdd(&w.acc[2], e);
-            if (threadIdx.x == 0) {
-                const uint32_t v = *a.win_bad & 2u;  // (the edit is done: its bits are all in)
-                if (v) atomicOr(&w.acc[3], (unsigned long long)v);
-            }
+
         } else if (w.prev_out) {
             win_head_copy(a, w, b - (w.acc ? 1u : 0u));
         }
         return;
     }
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= a.nwin) return;
-    const uint64_t entry = a.win_entry_ptr ? *(const volatile uint64_t *)a.win_entry_ptr - a.win_entry_sub
-                                           : a.win_entry;
-    const uint32_t kE = (uint32_t)((entry - a.win_base) / WIN_WN);
-    if (k < kE) return;
-    const uint64_t went = a.w_entry[k];
-    bool bad = a.w_flags[k] != 0;
-    if (k == kE) {
-        bad |= went != entry;
-    } else {
-        uint32_t j = k - 1, steps = 0;
-        while (j > kE && a.w_entry[j] == IDX_NONE && ++steps < 4096) --j;
-        const uint64_t xj = a.w_exit[j];
-        if (a.w_entry[j] == IDX_NONE) {
-            bad = true;
-        } else if (went != IDX_NONE) {
-            bad |= xj != went;
-        } else {
-            const uint64_t qe = a.win_base + (uint64_t)(k + 1) * WIN_WN;
-            bad |= xj < (qe < a.win_limit ? qe : a.win_limit);
+    unsigned long long ex = 0;  // this window's exit (its last record's end), for the chain's end
+    if (k < a.nwin) {
+        const uint64_t entry = a.win_entry_ptr ? *(const volatile uint64_t *)a.win_entry_ptr - a.win_entry_sub
+                                               : a.win_entry;
+        const uint32_t kE = (uint32_t)((entry - a.win_base) / WIN_WN);
+        if (k >= kE) {
+            const uint64_t went = a.w_entry[k];
+            const uint32_t wf = a.w_flags[k];
+            bool bad = (wf & ~WIN_F_EDIT) != 0;
+            if (wf & WIN_F_EDIT) {  // a record left to the exact path
+                atomicOr(a.win_bad, 2u);
+                if (w.acc) atomicOr(&w.acc[3], 2ull);
+            }
+            if (k == kE) {
+                bad |= went != entry;
+            } else {
+                uint32_t j = k - 1, steps = 0;
+                while (j > kE && a.w_entry[j] == IDX_NONE && ++steps < 4096) --j;
+                const uint64_t xj = a.w_exit[j];
+                if (a.w_entry[j] == IDX_NONE) {
+                    bad = true;
+                } else if (went != IDX_NONE) {
+                    bad |= xj != went;
+                } else {
+                    const uint64_t qe = a.win_base + (uint64_t)(k + 1) * WIN_WN;
+                    bad |= xj < (qe < a.win_limit ? qe : a.win_limit);
+                }
+            }
+            if (bad) {
+                atomicOr(a.win_bad, 1u);
+                if (w.acc) atomicOr(&w.acc[3], 1ull);
+            }
+            if (went != IDX_NONE) ex = a.w_exit[k];
         }
     }
-    if (bad) {
-        atomicOr(a.win_bad, 1u);
-        if (w.acc) atomicOr(&w.acc[3], 1ull);
+    // the chain's end: one atomic a wave on its windows' largest exit (one a window put
+    // ~16K atomics on one address for C2's 1M records)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)ex, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(ex >> 32), o);
+        const unsigned long long v = (unsigned long long)hi << 32 | lo;
+        ex = v > ex ? v : ex;
     }
-    if (went != IDX_NONE) atomicMax(&tot[0], (unsigned long long)a.w_exit[k]);
+    if ((threadIdx.x & 63) == 0 && ex) atomicMax(&tot[0], ex);
 }
 
 // ===========================================================================
@@ -3542,6 +3568,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.w_exit = L->w_exit;
         f.w_flags = L->w_flags;
         f.win_bad = L->win_bad;
+        f.win_tot = (unsigned long long *)L->win_tot;
         const uint32_t want = fast_feat(ch);
         int wk = -1;
         for (int k = 0; k < (int)(sizeof(win_inst) / sizeof(win_inst[0])) && wk < 0; ++k)
@@ -3558,12 +3585,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         const uint32_t need = (L->nwin + WK_NW - 1) / WK_NW;
         if ((uint32_t)grid > need) grid = (int)need;
         if (grid < 1 || ((L->out_base - L->rec0) & 15)) return -1;
-        if ((uint8_t *)L->win_tot == (uint8_t *)L->win_bad + 8) {  // (one memset: adjacent words)
-            if (hipMemsetAsync(L->win_bad, 0, 16, stream) != hipSuccess) return -1;
-        } else if (hipMemsetAsync(L->win_bad, 0, 4, stream) != hipSuccess ||
-                   hipMemsetAsync(L->win_tot, 0, 8, stream) != hipSuccess) {
-            return -1;
-        }
+        // (the verdict words: zeroed by the window kernel itself, which never writes them)
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
         {
             void *args[] = {&f};
