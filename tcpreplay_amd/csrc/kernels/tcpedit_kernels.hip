@@ -2417,12 +2417,16 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     unsigned long long ex = 0;  // this window's exit (its last record's end), for the chain's end
     if (k < a.nwin) {
+        // every load this window's check may need, issued together (the usual path reads
+        // its own entry, exit and flags and the previous window's entry and exit; one
+        // dependent walk back only past windows without a record)
+        const uint64_t went = a.w_entry[k], wexit = a.w_exit[k];
+        const uint32_t wf = a.w_flags[k];
+        const uint64_t pent = k ? a.w_entry[k - 1] : IDX_NONE, pexit = k ? a.w_exit[k - 1] : 0ull;
         const uint64_t entry = a.win_entry_ptr ? *(const volatile uint64_t *)a.win_entry_ptr - a.win_entry_sub
                                                : a.win_entry;
         const uint32_t kE = (uint32_t)((entry - a.win_base) / WIN_WN);
         if (k >= kE) {
-            const uint64_t went = a.w_entry[k];
-            const uint32_t wf = a.w_flags[k];
             bool bad = (wf & ~WIN_F_EDIT) != 0;
             if (wf & WIN_F_EDIT) {  // a record left to the exact path
                 atomicOr(a.win_bad, 2u);
@@ -2432,9 +2436,13 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
                 bad |= went != entry;
             } else {
                 uint32_t j = k - 1, steps = 0;
-                while (j > kE && a.w_entry[j] == IDX_NONE && ++steps < 4096) --j;
-                const uint64_t xj = a.w_exit[j];
-                if (a.w_entry[j] == IDX_NONE) {
+                uint64_t ej = pent, xj = pexit;
+                if (ej == IDX_NONE && j > kE) {  // (rare: windows without a record before this one)
+                    while (j > kE && a.w_entry[j] == IDX_NONE && ++steps < 4096) --j;
+                    ej = a.w_entry[j];
+                    xj = a.w_exit[j];
+                }
+                if (ej == IDX_NONE) {
                     bad = true;
                 } else if (went != IDX_NONE) {
                     bad |= xj != went;
@@ -2447,7 +2455,7 @@ __global__ __launch_bounds__(256) void te_win_check(FastArgs a, unsigned long lo
                 atomicOr(a.win_bad, 1u);
                 if (w.acc) atomicOr(&w.acc[3], 1ull);
             }
-            if (went != IDX_NONE) ex = a.w_exit[k];
+            if (went != IDX_NONE) ex = wexit;
         }
     }
     // the chain's end: one atomic a wave on its windows' largest exit (one a window put
