@@ -34,7 +34,10 @@ int tcpreplay_hip_set_preload_pcap(tcpreplay_hip_t *ctx, bool value);       /* t
 size_t tcpreplay_hip_output_bound(tcpreplay_hip_t *ctx, size_t len);
 /* every pass over the classic pcap image (host memory) on the GPU; writes the -w file
    into out (cap bytes) and returns its length, or -1 (geterr); *failed = records whose
-   unique-ip edit failed (stats->failed) */
+   unique-ip edit failed (stats->failed).  TCPREPLAY_HIP_READER_EXIT when the run ended
+   where safe_pcap_next exit(-1)s (below): out then holds what tcpreplay wrote before
+   exiting, tcpreplay_hip_output_len() bytes, and geterr names the record */
+#define TCPREPLAY_HIP_READER_EXIT (-2)
 int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *ctx, const uint8_t *pcap, size_t len, uint8_t *out, size_t cap,
                                      uint64_t *failed);
 /* 1 when the last tcpreplay_hip_replay_to_pcap ended where safe_pcap_next exit(-1)s
@@ -42,6 +45,9 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *ctx, const uint8_t *pcap, 
    or a zero len or caplen): its output is what tcpreplay wrote before exiting, and
    geterr names the record; 0 otherwise */
 int tcpreplay_hip_reader_exited(tcpreplay_hip_t *ctx);
+/* the -w file's length the last tcpreplay_hip_replay_to_pcap wrote (its return value on
+   success; on TCPREPLAY_HIP_READER_EXIT the bytes written before the exit; 0 after -1) */
+int64_t tcpreplay_hip_output_len(tcpreplay_hip_t *ctx);
 #ifdef __cplusplus
 }
 #endif

@@ -192,6 +192,12 @@ class TcpEdit:
     def geterr(self):
         return self._L.tcpedit_geterr(self._ctx).decode(errors="replace")
 
+    @property
+    def pipeline_fallbacks(self) -> int:
+        """pipelined calls whose window mode missed and that redid the capture the exact way
+        (tcpedit_pipeline_fallbacks)"""
+        return int(self._L.tcpedit_pipeline_fallbacks(self._ctx))
+
     def close(self):
         if self._ctx:
             self._L.tcpedit_close(ctypes.byref(self._ctx))

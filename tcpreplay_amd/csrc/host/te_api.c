@@ -60,6 +60,7 @@ struct tcpedit_batch_s {
     int mtu_fast;            /* tiles were cut for the wave lane's --mtu-trunc instances */
     int last_mtu;            /* the last launch placed tiles by the --mtu-trunc prediction */
     int fz_fast;             /* tiles were cut for the wave lane's --fuzz-seed instances */
+    int wk_small;            /* tiles were cut for the wave lane's TE_FF_SMALL instances */
     int last_fz;             /* the last launch fuzzed on the wave lane (static_fz placement) */
     uint32_t *d_fzlist;      /* static_fz: the reach list, its count, a word a record */
     uint64_t fzlist_cap;     /* (words) */
@@ -642,9 +643,33 @@ static void pool_wait(int *pending)
 
 #define TE_WALK_PART_MIN ((size_t)2 << 20) /* bytes per stretch of a parallel walk, at least */
 
-/* The tile cut a config and capture (b->swapped, b->nsec) get: the lane (wave, block or
- * generic), the slot layout, the tile budget; *proto is the walk's prototype. */
-static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
+/* a capture of small records: its first (up to) 256 records average at most
+   TE_SMALL_REC_BYTES with their headers, so 64 of them -- the wave tile's record cap -- fill
+   the 5 KiB tiles of the TE_FF_SMALL instances (C2's 80-byte records: 63), which run a block
+   more per CU than the 8 KiB ones (TCPEDIT_HIP_NO_SMALL=1: never, for A/B) */
+#define TE_SMALL_REC_BYTES 84u
+static int small_records(const uint8_t *recs, size_t len, int sw)
+{
+    static int off_env = -1;
+    if (off_env < 0) {
+        const char *e = getenv("TCPEDIT_HIP_NO_SMALL");
+        off_env = e && *e && *e != '0';
+    }
+    uint64_t off = 0, n = 0;
+    while (recs && !off_env && n < 256 && off + 16 <= len) {
+        const uint32_t cl = rd32(recs + off + 8, sw);
+        if (cl > 262144u || off + 16 + cl > len)
+            break;
+        off += 16 + cl;
+        n++;
+    }
+    return n >= 16 && off <= n * TE_SMALL_REC_BYTES;
+}
+
+/* The tile cut a config and capture (b->swapped, b->nsec; its records recs[0, len) for the
+ * small-record test) get: the lane (wave, block or generic), the slot layout, the tile
+ * budget; *proto is the walk's prototype. */
+static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto, const uint8_t *recs, size_t len)
 {
     memset(proto, 0, sizeof(*proto));
     proto->swapped = b->swapped;
@@ -672,11 +697,13 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto)
     if (shrink_fast && !proto->grow_fast && b->fast_kind != TE_FAST_WAVE) /* (the block lane has no shrink) */
         b->fast_tiles = 0, b->fast_kind = 0;
     proto->wave = b->fast_kind == TE_FAST_WAVE;
+    b->wk_small = proto->wave && !proto->grow_fast && !shrink_fast && !b->mtu_fast && !b->fz_fast &&
+                  small_records(recs, len, b->swapped);
     proto->budget = proto->wave      ? te_wave_tile_bytes(&t->cfg, proto->grow_fast ? TE_SZ_GROW
                                                                    : shrink_fast     ? static_shrink_kind(&t->cfg)
                                                                    : b->mtu_fast     ? TE_SZ_MTU
                                                                    : b->fz_fast      ? TE_SZ_FUZZ
-                                                                                     : TE_SZ_NONE)
+                                                                                     : TE_SZ_NONE, b->wk_small)
                     : b->fast_tiles ? TE_FK_TILE_BYTES
                                     : TE_SLOT_BYTES;
     proto->max_pkts = proto->wave ? TE_WK_PKTS : b->fast_tiles ? TE_FK_BLOCK : TE_MAX_PKTS;
@@ -716,7 +743,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     }
     b->linktype = te_linktype_dlt(rd32(hdr + 20, b->swapped) & 0x03ffffffu);
     te_walk_t proto;
-    cut_setup(t, b, &proto);
+    cut_setup(t, b, &proto, recs, len > 24 ? len - 24 : 0);
     proto.recs = recs;
     proto.len = len;
 
@@ -905,7 +932,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
         balance_tiles(b, te_wave_waves(&t->cfg, proto.shrink_fast ? static_shrink_kind(&t->cfg)
                                                 : b->mtu_fast      ? TE_SZ_MTU
                                                 : b->fz_fast       ? TE_SZ_FUZZ
-                                                                   : TE_SZ_NONE),
+                                                                   : TE_SZ_NONE, b->wk_small),
                       proto.budget, proto.max_pkts);
     b->out_cap = 24 + 64 + m->rec_bytes;
     b->scratch_bytes = m->scratch_bytes;
@@ -1485,6 +1512,7 @@ static int launch_ev(tcpedit_batch_t *b, int fixed_dir, hipEvent_t k0, hipEvent_
         L.stream = e && *e ? atoi(e) != 0 : (b->in_len + b->out_cap) > ((uint64_t)256 << 20);
     }
     L.fast_kind = b->fast_kind;
+    L.wk_small = b->wk_small;
     L.slots = (uint64_t *)(b->d_ws + WS_SLOTS(b->n_tiles));
     if (L.fast && b->gen_hint_ok && b->gen_hint_gen == t->cfg_gen)
         L.grid = b->last_listed ? (int)b->last_listed : 1; /* the generic kernel's grid after the fast lane */
@@ -2777,6 +2805,11 @@ struct te_pipe_s {
     /* the window-mode pipeline: the call's device accumulator {packets, bytes, edited,
        chain verdict} and its pinned landing area (+ the last chunk's chain end) */
     uint64_t *d_wacc, *h_wacc;
+    /* slots opened so far: a call opens only as many as its capture can have chunks in
+       flight (pipe_ready), later calls open more -- each slot is ~7x its chunk bytes of
+       device memory (input, output, huge-record scratch, per-record index arrays: ~230 MB
+       at a 32 MiB chunk) and its index arrays ~2x the chunk in page-locked host memory */
+    int nopen;
 };
 
 /* a chunk's first record at file offset off: an anchor for later prefixes */
@@ -2869,22 +2902,33 @@ fail:
     return NULL;
 }
 
-static int pipe_ready(tcpedit_t *t, size_t chunk)
+/* the pipeline for `chunk`-byte chunks with at least `want` slots open (the chunks a capture
+   of in_len bytes can be cut into, at most TE_PIPE_SLOTS: pipe_want) */
+static int pipe_ready(tcpedit_t *t, size_t chunk, int want)
 {
     te_pipe_t *P = t->pipe;
-    if (P && P->chunk == chunk)
+    if (want > TE_PIPE_SLOTS)
+        want = TE_PIPE_SLOTS;
+    if (want < 1)
+        want = 1;
+    if (P && P->chunk == chunk && P->nopen >= want)
         return 0;
-    te_pipe_free(t);
-    P = t->pipe = calloc(1, sizeof(*P));
-    if (P)
+    if (!P || P->chunk != chunk) {
+        te_pipe_free(t);
+        P = t->pipe = calloc(1, sizeof(*P));
+        if (!P) {
+            te_seterr(t, "out of memory");
+            return -1;
+        }
         for (int j = 0; j < TE_PIPE_SLOTS; j++)
             P->early[j] = ~0ull;
-    P->chunk = chunk;
-    HIPCHK(t, hipStreamCreateWithFlags(&P->s_h2d, hipStreamNonBlocking));
-    HIPCHK(t, hipStreamCreateWithFlags(&P->s_d2h, hipStreamNonBlocking));
-    HIPCHK(t, hipHostMalloc((void **)&P->hdr, 64, 0));
-    P->idx_nwin = idx_nwin(16, 24 + chunk + TE_PIPE_MARGIN);
-    for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+        P->chunk = chunk;
+        HIPCHK(t, hipStreamCreateWithFlags(&P->s_h2d, hipStreamNonBlocking));
+        HIPCHK(t, hipStreamCreateWithFlags(&P->s_d2h, hipStreamNonBlocking));
+        HIPCHK(t, hipHostMalloc((void **)&P->hdr, 64, 0));
+        P->idx_nwin = idx_nwin(16, 24 + chunk + TE_PIPE_MARGIN);
+    }
+    for (int s = P->nopen; s < want; s++, P->nopen++) {
         if (!(P->slot[s] = pipe_slot_open(t, chunk)))
             goto fail;
         HIPCHK(t, hipEventCreateWithFlags(&P->h2d_done[s], hipEventDisableTiming));
@@ -3134,6 +3178,11 @@ static int pipe_run_dix(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         for (int j = 0; j < nch; j++)
             cst[j] = 24 + (uint64_t)j * C;
         cst[nch] = in_len;
+    }
+    if (nch > P->nopen && P->nopen < TE_PIPE_SLOTS) { /* (pipe_ready's bound on the chunks) */
+        te_seterr(t, "pipeline: %d chunks over %d open slots", nch, P->nopen);
+        free(cst);
+        return -1;
     }
     uint64_t pos = *pos_io, pkts = 0, chunk_pkt_base[TE_PIPE_SLOTS] = {0};
     int inflight[TE_PIPE_SLOTS] = {0}, stopped = 0, k = 0, fallbacks = 0;
@@ -3431,6 +3480,11 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
         te_seterr(t, "out of memory");
         return -1;
     }
+    if (nch > P->nopen && P->nopen < TE_PIPE_SLOTS) { /* (pipe_ready's bound on the chunks) */
+        te_seterr(t, "pipeline: %d chunks over %d open slots", nch, P->nopen);
+        free(cst);
+        return -1;
+    }
     const double t0 = te_now();
     if (!P->d_wacc) {
         HIPCHK(t, hipMalloc((void **)&P->d_wacc, 64));
@@ -3439,7 +3493,7 @@ static int pipe_run_win(tcpedit_t *t, te_pipe_t *P, const uint8_t *img, size_t i
     {
         const uint64_t limit_max = ORG + C + 256;
         const uint32_t nwin_max = (uint32_t)((limit_max - ORG + te_win_bytes() - 1) / te_win_bytes());
-        for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+        for (int s = 0; s < P->nopen; s++) {
             tcpedit_batch_t *b = P->slot[s];
             b->out_cap = C + 256 + TE_PIPE_WIN_MARGIN + ORG;
             if (win_ready(t, b, nwin_max) < 0 || pipe_grow(t, P, s) < 0)
@@ -3634,7 +3688,10 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
     if (chunk_bytes < ((size_t)1 << 20))
         chunk_bytes = (size_t)1 << 20; /* >= any record (16 + 262144 B) */
     chunk_bytes = (chunk_bytes + 15) & ~(size_t)15;
-    if (te_upload_cfg(t) < 0 || pipe_ready(t, chunk_bytes) < 0)
+    /* the chunks the capture can be cut into: every chunk but the last holds >= 1 MiB of the
+       window plan or >= chunk - one largest record of a record-cut plan (>= 1 MiB - 262,160) */
+    const int want = (int)((in_len > 24 ? in_len - 24 : 0) / (((size_t)1 << 20) - 262160u) + 2);
+    if (te_upload_cfg(t) < 0 || pipe_ready(t, chunk_bytes, want) < 0)
         return TCPEDIT_ERROR;
     te_pipe_t *P = t->pipe;
     {
@@ -3688,12 +3745,12 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         uint32_t magic;
         memcpy(&magic, img, 4);
         int dix = !pipe_index_host_env();
-        for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+        for (int s = 0; s < P->nopen; s++) {
             tcpedit_batch_t *bs = P->slot[s];
             bs->swapped = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
             bs->nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
             te_walk_t proto;
-            cut_setup(t, bs, &proto);
+            cut_setup(t, bs, &proto, img + 24, in_len - 24);
             dix &= bs->cut_device_ok;
         }
         if (dix && b0->fast_kind == TE_FAST_WAVE && !b0->slot_layout && !d_dirbits && !b0->swapped && !b0->nsec &&
@@ -3712,7 +3769,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         }
         if (dix && b0->fast_kind == TE_FAST_WAVE) {
             /* scratch for huge records, sized for the worst chunk (the index places them) */
-            for (int s = 0; s < TE_PIPE_SLOTS; s++) {
+            for (int s = 0; s < P->nopen; s++) {
                 const uint64_t need = (uint64_t)chunk_bytes + TE_PIPE_MARGIN + (chunk_bytes + TE_PIPE_MARGIN) / 8 + 65536;
                 if (P->d_scratch_alloc[s] < need) {
                     hipFree(P->slot[s]->d_scratch);
@@ -3745,6 +3802,10 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
         }
         if (stopped || off + 16 > in_len)
             break;
+        if (!b) { /* (pipe_ready's bound on the chunks) */
+            te_seterr(t, "pipeline: chunk %d over %d open slots", k, P->nopen);
+            goto fail_drain;
+        }
         /* ---- index the next chunk into the slot (its pinned arrays are free once the
                H2D that read them is done) ---- */
         HIPCHK(t, hipEventSynchronize(P->h2d_done[s]));

@@ -677,9 +677,11 @@ int64_t tcpprep_cache_pcap(tcpprep_hip_t *t, const void *pcap, size_t len, void 
                          "entries of every shard come before the second pass's)");
     }
     size_t clen = strlen(t->comment), hdr = 24 + clen, body = (x.n + 3) / 4;
-    if (out_cap < hdr + (filt_auto ? (2 * x.n + 3) / 4 : body)) {
+    /* (--auto with filters: up to one first-pass entry per record before the body) */
+    const size_t need = hdr + (filt_auto ? (2 * x.n + 3) / 4 : body);
+    if (out_cap < need) {
         index_free(&x);
-        return tp_err(t, "cache buffer too small (%zu < %zu)", out_cap, hdr + body);
+        return tp_err(t, "cache buffer too small (%zu < %zu)", out_cap, need);
     }
     tp_dev_t d;
     if (stage(t, pcap, len, &x, &d) < 0) {

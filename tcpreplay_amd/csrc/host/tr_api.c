@@ -26,10 +26,12 @@ struct tcpreplay_hip_s {
     double unique_loops;
     tr_list_t list;     /* --include / --exclude (n = 0: none) */
     int reader_exit;    /* the last replay ended at safe_pcap_next's exit */
+    int64_t out_len;    /* the bytes the last replay wrote */
     char err[512];
 };
 
 int tcpreplay_hip_reader_exited(tcpreplay_hip_t *t) { return t ? t->reader_exit : 0; }
+int64_t tcpreplay_hip_output_len(tcpreplay_hip_t *t) { return t ? t->out_len : 0; }
 
 /* parse_list (src/common/list.c:61-130): ',' tokens (strtok_r drops empty ones), each
    "^[0-9]+(-([0-9]+|\s*))?$"; add_to_list (:36-50) takes min by strtoull(.., 0), max = min
@@ -237,6 +239,7 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
     if (cap < tcpreplay_hip_output_bound(t, len))
         return tr_err(t, "output buffer smaller than tcpreplay_hip_output_bound");
     t->reader_exit = 0;
+    t->out_len = 0;
     /* libpcap's walk: a record past MAX_SNAPLEN or past the end stops the read; then
        safe_pcap_next (send_packets.c:955,985 -> src/common/utils.c:131-169): a len past
        MAX_SNAPLEN or a zero len or caplen exit(-1)s in the first pass, after the records
@@ -344,10 +347,13 @@ int64_t tcpreplay_hip_replay_to_pcap(tcpreplay_hip_t *t, const uint8_t *pcap, si
         fails = nf;
     }
     *failed = fails;
+    t->out_len = (int64_t)o;
     rc = (int64_t)o;
-    if (reader_exit) { /* the output holds the first pass's records before it */
+    if (reader_exit) { /* the output holds the first pass's records before it: a return no
+                          caller can take for a whole run (tcpreplay exit(-1)s there) */
         t->reader_exit = 1;
         tr_err(t, "safe_pcap_next ERROR: Invalid packet length: packet %llu", (unsigned long long)(n + 1));
+        rc = TCPREPLAY_HIP_READER_EXIT;
     }
 fail:
     hipFree(d_img);

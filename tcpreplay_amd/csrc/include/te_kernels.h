@@ -58,6 +58,9 @@ extern "C" {
 #define TE_FF_INCR 32u   /* no --fixcsum: checksums follow the incremental updates (RFC 1624)
                             unless the packet needs a recompute (needtorecalc, tcpedit.c:338) */
 #define TE_FF_ALLX 63u
+#define TE_FF_SMALL 64u  /* a mode, not an option group: the lean size-preserving instances cut to
+                            5 KiB tiles at 5 blocks/CU, for batches of small records (64 of them, the
+                            tile's record cap, fit): te_wave_small(); others take 8 KiB at 3-4 */
 
 /* bytes a record needs in a slot: g = its HBM address mod 16, data = bytes of
  * packet data to materialise (caplen, or max(caplen, len) under --fixlen=pad) */
@@ -150,6 +153,7 @@ typedef struct {
                                  from the prediction sets *grow_bad */
     const long long *tcut;    /* device: n_tiles + 1 exclusive prefix of the predicted cuts */
     uint32_t mtu;             /* static_mtu: the MTU (cfg.mtu) */
+    int wk_small;             /* the batch's tiles were cut for the TE_FF_SMALL instances */
     int static_fz;            /* --fuzz-seed on the wave lane: the launch finds the reaching records
                                  (te_fuzz_reach + the generic reach pass over the tiles it lists),
                                  draws the states, predicts each tile's cut into tcut (written
@@ -283,7 +287,7 @@ size_t te_l2carry_temp_bytes(uint32_t n_pkts);
 /* blocks of te_fast_tiles / te_wave_tiles resident on the current device */
 int te_fast_grid(void);
 int te_wave_grid(void);
-uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz);
+uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz, int small);
 
 #ifdef __HIP_PLATFORM_AMD__
 int te_launch_edit(te_launch_t *L, hipStream_t stream);
@@ -302,7 +306,7 @@ int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint16_t *pkt_r
 #endif
 uint64_t te_q8_slot_bytes(void);
 /* tile budget of the wave-lane instance the config launches (sz: TE_SZ_*) */
-uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz);
+uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small);
 
 #ifdef __cplusplus
 }

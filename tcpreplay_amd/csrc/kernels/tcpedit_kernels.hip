@@ -1334,10 +1334,13 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_BIG_TILE_BYTES
 #define TE_WK_BIG_TILE_BYTES 8192
 #endif
+// (TE_FF_SMALL instances keep TE_WK_LEAN_TILE_BYTES at 5 blocks/CU: a batch of C2's 80-byte
+// records fills 63 of them into 5 KiB, so the 8 KiB image buys nothing but a block per CU --
+// C2 0.626 -> 0.678 of peak, seed 0.685 -> 0.70, A/B on one box, round 6)
 template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
-    static constexpr bool big = !reads && SZ == 0 && !WIN;
+    static constexpr bool big = !reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
     static constexpr int blocks = reads || big ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
     static constexpr int tile = reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
 };
@@ -2829,6 +2832,8 @@ extern "C" int te_fast_grid(void) {
 #define TE_FF_ALLH (TE_FF_ALL | TE_FF_HDR)
 #define TE_WAVE_INSTANCES(X)                                                                         \
     X(0u, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, SZ_NONE)                          \
+    X(TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED | TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE)    \
+    X(TE_FF_SEED | TE_FF_INCR | TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE)                                \
     X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE) X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE)       \
     X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE)         \
     X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
@@ -2866,20 +2871,31 @@ static struct {
 static uint32_t fast_feat(const te_dev_cfg_t *c);
 // the first (smallest) instance covering the config's option groups and size change;
 // TCPEDIT_HIP_WAVE_FEAT=<mask> adds groups to the choice (A/B runs)
+// (TE_FF_SMALL in `want`: the small-tile instance of the same groups if there is one, else the
+//  other; the INCR and SMALL modes match exactly)
 static int wave_pick(uint32_t want, int sz) {
     static const uint32_t feat_env =
         getenv("TCPEDIT_HIP_WAVE_FEAT") ? (uint32_t)atoi(getenv("TCPEDIT_HIP_WAVE_FEAT")) : 0u;
     want |= feat_env;
     if (sz == SZ_MTU) want &= ~TE_FF_INCR;  // (--mtu-trunc recomputes every IP packet's checksums)
-    for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k)
-        if (wave_inst[k].sz == sz && (want & ~wave_inst[k].feat) == 0 && ((want ^ wave_inst[k].feat) & TE_FF_INCR) == 0)
-            return k;
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t w = pass ? want & ~TE_FF_SMALL : want;
+        for (int k = 0; k < (int)(sizeof(wave_inst) / sizeof(wave_inst[0])); ++k)
+            if (wave_inst[k].sz == sz && (w & ~wave_inst[k].feat) == 0 &&
+                ((w ^ wave_inst[k].feat) & (TE_FF_INCR | TE_FF_SMALL)) == 0)
+                return k;
+        if (!(want & TE_FF_SMALL)) break;
+    }
     return -1;
 }
 
+// (--seed sets rewrite_ip too, tcpedit parse_args.c:218-238, but rewrite_ipv4l3 /
+// rewrite_ipv6l3 with no map change nothing and return 0, edit_packet.c:787-878: a seed-only
+// config runs the lean SEED instance, not the cfg-reading address-map one)
 static uint32_t fast_feat(const te_dev_cfg_t *c) {
+    const bool maps = c->n_srcipmap || c->n_dstipmap || c->n_cidrmap1 || c->n_cidrmap2;
     return ((c->mac_mask || c->n_subs || c->random_set) ? TE_FF_MAC : 0u) | (c->has_portmap ? TE_FF_PORTMAP : 0u) |
-           (c->rewrite_ip ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u) |
+           ((c->rewrite_ip && maps) ? TE_FF_RWIP : 0u) | (c->seed ? TE_FF_SEED : 0u) |
            ((c->tos >= 0 || c->ttl_mode != TE_TTL_OFF || c->tclass >= 0 || c->flowlabel >= 0 ||
              c->tcp_sequence_enable)
                 ? TE_FF_HDR
@@ -2899,18 +2915,18 @@ static int wave_inst_grid(int k) {
 
 // the tile budget of the wave-lane instance a config launches (the host cuts tiles to it)
 static int wave_pick(uint32_t want, int sz);
-extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz) {
-    const int k = wave_pick(fast_feat(c), sz);
+extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small) {
+    const int k = wave_pick(fast_feat(c) | (small ? TE_FF_SMALL : 0u), sz);
     if (k < 0) return TE_WK_TILE_BYTES;
     return (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) ? TE_WK_TILE_BYTES
-           : wave_inst[k].sz == SZ_NONE                                                 ? TE_WK_BIG_TILE_BYTES
-                                                                                       : TE_WK_LEAN_TILE_BYTES;
+           : wave_inst[k].sz == SZ_NONE && !(wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_BIG_TILE_BYTES
+                                                                            : TE_WK_LEAN_TILE_BYTES;
 }
 
 // the waves a config's wave-lane launch runs (its instance's resident grid x 4): the host
 // balances a small batch's tile cut to a whole number of rounds of them
-extern "C" uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz) {
-    const int k = wave_pick(fast_feat(c), sz);
+extern "C" uint32_t te_wave_waves(const te_dev_cfg_t *c, int sz, int small) {
+    const int k = wave_pick(fast_feat(c) | (small ? TE_FF_SMALL : 0u), sz);
     return k < 0 ? 0u : (uint32_t)wave_inst_grid(k) * (uint32_t)WK_NW;
 }
 
@@ -3665,7 +3681,7 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         f.fz_factor = ch->fuzz_factor ? ch->fuzz_factor : 1u;
         if ((L->static_mtu || L->static_fz) && (!L->tcut || L->fast_kind != TE_FAST_WAVE)) return -1;
         const void *wfn = nullptr;
-        const int wk = wave_pick(fast_feat(ch), grow            ? SZ_GROW
+        const int wk = wave_pick(fast_feat(ch) | (L->wk_small ? TE_FF_SMALL : 0u), grow ? SZ_GROW
                                                 : L->static_mtu ? SZ_MTU
                                                 : L->static_fz  ? SZ_FUZZ
                                                                 : L->static_shrink);

@@ -30,16 +30,30 @@ def _lib():
                 ("tcpreplay_hip_output_bound", sz, [vp, sz]),
                 ("tcpreplay_hip_replay_to_pcap", ctypes.c_int64,
                  [vp, ctypes.c_char_p, sz, vp, sz, ctypes.POINTER(ctypes.c_uint64)]),
-                ("tcpreplay_hip_reader_exited", c_int, [vp])):
+                ("tcpreplay_hip_reader_exited", c_int, [vp]),
+                ("tcpreplay_hip_output_len", ctypes.c_int64, [vp])):
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         _SIG_DONE = True
     return L
 
 
+READER_EXIT = -2  # TCPREPLAY_HIP_READER_EXIT
+
+
+class ReaderExit(RuntimeError):
+    """the replay ended where safe_pcap_next exit(-1)s (src/common/utils.c:136-156): `output`
+    is the -w file tcpreplay wrote before exiting, `failed` its failed unique-ip edits"""
+
+    def __init__(self, msg, output, failed):
+        super().__init__(msg)
+        self.output, self.failed = output, failed
+
+
 class TcpReplay:
     """tcpreplay_hip_init + tcpreplay_hip_parse_args; replay(pcap) -> (the -w file bytes,
-    the records whose unique-ip edit failed: stats->failed)"""
+    the records whose unique-ip edit failed: stats->failed); a run that ends at
+    safe_pcap_next's exit raises ReaderExit (its partial output attached)"""
 
     def __init__(self, args):
         self._L = _lib()
@@ -61,6 +75,8 @@ class TcpReplay:
         out = ctypes.create_string_buffer(max(cap, 1))
         failed = ctypes.c_uint64()
         n = self._L.tcpreplay_hip_replay_to_pcap(self._ctx, pcap, len(pcap), out, cap, ctypes.byref(failed))
+        if n == READER_EXIT:
+            raise ReaderExit(self.geterr(), out.raw[:self._L.tcpreplay_hip_output_len(self._ctx)], int(failed.value))
         if n < 0:
             raise RuntimeError(self.geterr())
         return out.raw[:n], int(failed.value)

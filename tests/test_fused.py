@@ -4,6 +4,7 @@ into the edit -- each wave stages a byte window of the capture, finds its record
 them where they lie; te_win_check then checks the chain across windows.  Every case must
 write the oracle's bytes; a batch the window mode does not carry, or one where the
 speculation misses the chain, runs the exact path (tcpedit_batch_run) instead."""
+import ctypes
 import struct
 
 import pytest
@@ -163,5 +164,85 @@ def test_fused_runs_repeat(built):
             assert b.run_fused() == rc_o and b.output() == exp
         assert b.fused_fallbacks == 0
         b.close()
+    finally:
+        te.close()
+
+
+def _udp_frame(size, payload_at=None, payload=b""):
+    """an Ethernet II / IPv4 / UDP frame of `size` bytes (checksums left to --fixcsum), with
+    `payload` written at frame offset payload_at and 0xEE filler elsewhere in the UDP payload
+    (no zero bytes: nothing there looks like a record header to the discovery)"""
+    f = bytearray(b"\xee" * size)
+    f[0:14] = bytes.fromhex("001122334455" "00667788 99aa".replace(" ", "")) + b"\x08\x00"
+    f[14:34] = struct.pack(">BBHHHBBH4s4s", 0x45, 0, size - 14, 1, 0x4000, 64, 17, 0, bytes([10, 1, 2, 3]),
+                           bytes([172, 16, 0, 9]))
+    f[34:42] = struct.pack(">HHHH", 4000, 53, size - 34, 0)
+    if payload_at is not None:
+        f[payload_at:payload_at + len(payload)] = payload
+    return bytes(f)
+
+
+def _fake_chain():
+    """pcap records as payload bytes: five 64-byte UDP records, an ARP record (a shape the
+    wave lane leaves to the exact path) and the header of a 6,000-byte record (past the
+    window's staged tail: also left to the exact path)"""
+    parts = []
+    for i in range(5):
+        parts.append(struct.pack("<IIII", 1700000000, 1000 + i, 64, 64) + _udp_frame(64))
+    arp = bytes.fromhex("ffffffffffff" "00667788 99aa".replace(" ", "")) + b"\x08\x06" + b"\x00\x01" * 23
+    parts.append(struct.pack("<IIII", 1700000000, 2000, len(arp), len(arp)) + arp)
+    parts.append(struct.pack("<IIII", 1700000000, 3000, 6000, 6000))
+    return b"".join(parts)
+
+
+def test_window_pipeline_false_records_before_the_chain_entry(built):
+    """in the window-mode pipeline the windows before a chunk's chain entry (kE)
+    hold the tail of the previous chunk's last record; what the discovery finds there is not
+    a record, the edit's writes there are overwritten by the head copy, and a record it
+    leaves to the exact path (WIN_F_EDIT) must not send the capture to the fallback.  Here the
+    record straddling the first chunk cut is a 5,050-byte UDP frame (the lean window tile
+    holds it) whose payload past the cut carries a fake record chain with a deferred ARP
+    record and an over-long record: the output is the oracle's and no call falls back."""
+    args = ["--seed=42", "--fixcsum"]
+    n_total = (3 << 20) + 4096
+    buf = bytearray(n_total)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    # te_api.c win_plan: the first chunk cut at a 256-byte boundary of the caller's buffer
+    # 1 MiB past the first record (1 MiB chunks)
+    cut1 = ((addr + 24 + (1 << 20)) & ~255) - addr
+    # the jumbo: 16 + J + 16 within the 5,120-byte lean window tile; its bytes past the cut,
+    # 16 + J - 100 = 4,966, put the next chunk's chain entry in its window 1 (kE = 1).  (Its
+    # chunk-0 window offset is 1,660-1,916 for any buffer address: the window's staging plus
+    # its tail load hold the whole record.)
+    J = 5050
+    jstart = cut1 - 100
+    recs, off, i = [], 24, 0
+    while off < jstart:
+        gap = jstart - off
+        size = 64 if gap >= 80 + 76 or gap == 80 else gap - 16  # (the last filler 60..139 bytes)
+        recs.append((1600000000, i, size, size, _udp_frame(size)))
+        off += 16 + size
+        i += 1
+    assert off == jstart
+    fake = _fake_chain()
+    # chunk-1 offset 200 is jumbo data offset 200 + 84
+    recs.append((1600000001, 0, J, J, _udp_frame(J, 284, fake)))
+    off += 16 + J
+    while off + 80 <= n_total:
+        recs.append((1600000002, i, 64, 64, _udp_frame(64)))
+        off += 80
+        i += 1
+    pcap = S.build_pcap(recs)
+    assert len(pcap) <= n_total
+    buf[:len(pcap)] = pcap  # (in place: the address the cut was computed for)
+    src = memoryview(buf)[:len(pcap)]
+    rc_o, exp = O.rewrite(pcap, args)
+    te = TA.TcpEdit(args)
+    try:
+        rc, out = te.rewrite_pipelined(src, chunk_bytes=1 << 20)
+        assert rc == rc_o == 0
+        assert out == exp
+        assert te.pipeline_fallbacks == 0
+        src.release()
     finally:
         te.close()

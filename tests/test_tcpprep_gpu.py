@@ -246,3 +246,25 @@ def test_gpu_auto_with_include_exclude(mode, filt):
     for pcap in (T.test_pcap(), synth.pcap_imix(3000, seed=filt)):
         got, exp = _both(pcap, args)
         assert got == exp and got != "error"
+
+
+def test_gpu_auto_filter_buffer_size_message_is_the_size_needed():
+    """--auto with a filter: the cache can hold a first-pass entry per filtered record before
+    the body, so tcpprep_cache_pcap needs hdr + (2n + 3) / 4 bytes -- and a too-small buffer's
+    error names that size, which then succeeds"""
+    import ctypes
+    import re
+    pcap = synth.pcap_imix(3000, seed=3)
+    p = TP.TcpPrep(["--no-arg-comment", "--auto=bridge", "--exclude=P:1-9,30-31,100-"])
+    try:
+        L = p._L
+        small = ctypes.create_string_buffer(24 + (3000 + 3) // 4)
+        assert L.tcpprep_cache_pcap(p._ctx, pcap, len(pcap), small, len(small)) < 0
+        m = re.search(r"too small \((\d+) < (\d+)\)", p.geterr())
+        need = int(m.group(2))
+        assert need == 24 + (2 * 3000 + 3) // 4
+        buf = ctypes.create_string_buffer(need)
+        n = L.tcpprep_cache_pcap(p._ctx, pcap, len(pcap), buf, need)
+        assert n > 0 and buf.raw[:n] == p.cache(pcap)
+    finally:
+        p.close()

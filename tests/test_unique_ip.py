@@ -112,7 +112,8 @@ def test_gpu_nanosecond_and_big_endian_input(built):
 def test_gpu_reader_rules_match_oracle(built, args):
     """safe_pcap_next's rules (send_packets.c:955,985 -> src/common/utils.c:131-169): len <
     caplen records are sent as len bytes; a zero len or caplen record ends the run after the
-    first pass's earlier records (tcpreplay_hip_reader_exited, geterr names it)"""
+    first pass's earlier records (TCPREPLAY_HIP_READER_EXIT: ReaderExit carries that output,
+    geterr names the record)"""
     import ctypes
     from tcpreplay_amd import tcpreplay as TR
     lib = O.load()
@@ -129,9 +130,10 @@ def test_gpu_reader_rules_match_oracle(built, args):
         for zc, zl in ((0, 0), (0, 70), (70, 0)):
             ts, tu, cl, ln, d = recs[250]
             bad = S.build_pcap(recs[:250] + [(ts, tu, zc, zl, d[:zc])] + recs[251:])
-            got = t.replay(bad)
-            assert t.reader_exited and "safe_pcap_next" in t.geterr()
-            assert got == O.replay(bad, args) and lib.tcpreplay_oracle_exited() == 1
+            with pytest.raises(TR.ReaderExit) as ex:
+                t.replay(bad)
+            assert t.reader_exited and "safe_pcap_next" in str(ex.value)
+            assert (ex.value.output, ex.value.failed) == O.replay(bad, args) and lib.tcpreplay_oracle_exited() == 1
     finally:
         t.close()
 

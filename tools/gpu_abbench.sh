@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-F="--steps 20 --warmup 3 --extra= --no-cpu-baseline --no-e2e --no-device-index --no-packet-latency"
+F="--steps 20 --warmup 3 --extra= --no-cpu-baseline --no-e2e --no-device-index --no-packet-latency ${AB_NOVERIFY:+--no-verify}"
 for v in ${AB_VARIANTS:-base}; do
   for w in ${AB_WLS:-c4}; do
     if [ "$v" = base ]; then L=tcpreplay_amd/lib/libtcpedit_hip.so; else L=tcpreplay_amd/lib/abvar/libtcpedit_hip_$v.so; fi
