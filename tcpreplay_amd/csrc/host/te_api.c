@@ -646,8 +646,11 @@ static void pool_wait(int *pending)
 /* a capture of small records: its first (up to) 256 records average at most
    TE_SMALL_REC_BYTES with their headers, so 64 of them -- the wave tile's record cap -- fill
    the 5 KiB tiles of the TE_FF_SMALL instances (C2's 80-byte records: 63), which run a block
-   more per CU than the 8 KiB ones (TCPEDIT_HIP_NO_SMALL=1: never, for A/B) */
+   more per CU than the 8 KiB ones -- for a batch the Infinity Cache holds (in + out <= 256
+   MiB): from HBM the 8 KiB tiles' bytes in flight count for more (c2x10 0.645 vs 0.636 of
+   peak, C2 0.623 vs 0.679; TCPEDIT_HIP_NO_SMALL=1: never, for A/B) */
 #define TE_SMALL_REC_BYTES 84u
+#define TE_SMALL_MAX_BATCH ((uint64_t)128 << 20)
 static int small_records(const uint8_t *recs, size_t len, int sw)
 {
     static int off_env = -1;
@@ -669,7 +672,8 @@ static int small_records(const uint8_t *recs, size_t len, int sw)
 /* The tile cut a config and capture (b->swapped, b->nsec; its records recs[0, len) for the
  * small-record test) get: the lane (wave, block or generic), the slot layout, the tile
  * budget; *proto is the walk's prototype. */
-static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto, const uint8_t *recs, size_t len)
+static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto, const uint8_t *recs, size_t len,
+                      uint64_t batch_bytes)
 {
     memset(proto, 0, sizeof(*proto));
     proto->swapped = b->swapped;
@@ -698,7 +702,7 @@ static void cut_setup(tcpedit_t *t, tcpedit_batch_t *b, te_walk_t *proto, const 
         b->fast_tiles = 0, b->fast_kind = 0;
     proto->wave = b->fast_kind == TE_FAST_WAVE;
     b->wk_small = proto->wave && !proto->grow_fast && !shrink_fast && !b->mtu_fast && !b->fz_fast &&
-                  small_records(recs, len, b->swapped);
+                  batch_bytes <= TE_SMALL_MAX_BATCH && small_records(recs, len, b->swapped);
     proto->budget = proto->wave      ? te_wave_tile_bytes(&t->cfg, proto->grow_fast ? TE_SZ_GROW
                                                                    : shrink_fast     ? static_shrink_kind(&t->cfg)
                                                                    : b->mtu_fast     ? TE_SZ_MTU
@@ -743,7 +747,7 @@ static int index_image(tcpedit_t *t, tcpedit_batch_t *b, const uint8_t *hdr, con
     }
     b->linktype = te_linktype_dlt(rd32(hdr + 20, b->swapped) & 0x03ffffffu);
     te_walk_t proto;
-    cut_setup(t, b, &proto, recs, len > 24 ? len - 24 : 0);
+    cut_setup(t, b, &proto, recs, len > 24 ? len - 24 : 0, len);
     proto.recs = recs;
     proto.len = len;
 
@@ -3750,7 +3754,7 @@ int tcpedit_rewrite_pcap_pipelined(tcpedit_t *t, const void *in, size_t in_len, 
             bs->swapped = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
             bs->nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
             te_walk_t proto;
-            cut_setup(t, bs, &proto, img + 24, in_len - 24);
+            cut_setup(t, bs, &proto, img + 24, in_len - 24, P->chunk);
             dix &= bs->cut_device_ok;
         }
         if (dix && b0->fast_kind == TE_FAST_WAVE && !b0->slot_layout && !d_dirbits && !b0->swapped && !b0->nsec &&

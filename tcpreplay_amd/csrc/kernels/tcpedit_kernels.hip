@@ -1347,6 +1347,11 @@ struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupan
 #ifndef TE_WK_STORE_BARRIER
 #define TE_WK_STORE_BARRIER 1
 #endif
+// the size-preserving store fills the next tile's span into LDS between its LDS reads and
+// its global stores (0: after the stores, as before round 6)
+#ifndef TE_WK_FILL_EARLY
+#define TE_WK_FILL_EARLY 1
+#endif
 #ifndef TE_WK_LANE_OPAQUE
 #define TE_WK_LANE_OPAQUE 1
 #endif
@@ -1787,6 +1792,7 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 #endif
 __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_WIN_BLOCKS : TE_WIN_LEAN_BLOCKS)
                                        : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_FUZZ_BLOCKS - 1 : TE_WK_FUZZ_BLOCKS)
+                                       : DEPTH == 2    ? TE_WK_MIN_BLOCKS  // (two spans in flight: 128 VGPRs)
                                                        : (WkCfg<F, SZ, WIN>::blocks)) te_wave_tiles(FastArgs a) {
     constexpr int TB = WkCfg<F, SZ, WIN>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
@@ -1885,11 +1891,19 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
     if constexpr (k < WK_KL) *(uint4 *)(S + LDS_FRONT + (((uint32_t)lane + k * 64u) << 4)) = R.v##k;
         WK_EACH(WK_ST)
 #undef WK_ST
+        // the span's per-lane loads (issued after its chunks) are taken here too, on every path
+        // that fills: otherwise the loop's copy of them waits at the back edge, where the paths
+        // merge with different store counts, for every store of the tile just done (vmcnt(0))
+        asm volatile("" ::"v"(R.rel), "v"(R.dirb), "v"(R.fzs));
     };
     // edit and store tile t, whose span is in the LDS image; a tile the lane cannot
     // finish is listed for the generic lane and stores nothing
+    // pre_store(): called by the size-preserving store between its LDS reads and its global
+    // stores -- the step puts the next tile's span into LDS there (TE_WK_FILL_EARLY), so the
+    // wait for that span's loads no longer covers this tile's stores (vmcnt counts both, in
+    // issue order); returns whether it ran
     auto edit = [&](const uint32_t t, const te_tile_t &tile, const uint32_t my_rel, const uint32_t my_dirb,
-                    const bool my_dirv, const uint32_t my_fzs) __attribute__((always_inline)) {
+                    const bool my_dirv, const uint32_t my_fzs, auto &&pre_store) __attribute__((always_inline)) -> bool {
             const uint32_t npkt = tile.npkt;
             const uint64_t G0 = tile.span_off, A0 = G0 & ~15ull, E = G0 + tile.span_len;
             const uint32_t g0 = (uint32_t)(G0 - A0);
@@ -1899,7 +1913,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 } else if (lane == 0) {
                     a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
                 }
-                return;
+                return false;
             }
 
             // ---- phase A: one lane per packet ----
@@ -2039,7 +2053,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 } else if (lane == 0) {
                     a.tile_list[atomicAdd(a.list_cnt, 1u)] = t;
                 }
-                return;
+                return false;
             }
 
             WK_STAMP(1)  // phase A
@@ -2137,6 +2151,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
             WK_LANES_SYNC();  // the store reads what every lane wrote back
             WK_STAMP(3)  // phase B
             // ---- store: the chunks that start in the span, then the leading bytes ----
+            bool filled = false;
             if constexpr (GROW) {
                 // record j's tag at output offset rel_j + 28 + 4 j (its input byte rel_j + 28 on)
                 wk_store_sized<true>(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0,
@@ -2180,15 +2195,22 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 *dk = w##k;                                                                                \
         }
                 WK_EACH(WK_RD)
+                const uint32_t nlead = (uint32_t)(C0 - G0);
+                const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
+                const uint8_t lead = S[LDS_FRONT + (uint32_t)(q - A0)];
+                // (the instances that read the cfg keep the fill after the stores: their
+                //  registers spill with the span and the store data live together)
+                if constexpr (TE_WK_FILL_EARLY && !WkCfg<F>::reads) {
+                    WK_LANES_SYNC();  // (the image's reads before the next span's writes)
+                    filled = pre_store();
+                }
 #if TE_WK_STORE_BARRIER
                 __builtin_amdgcn_sched_barrier(0);
 #endif
                 WK_EACH(WK_WR)  // lanes past the span repeat its last chunk (same bytes)
 #undef WK_RD
 #undef WK_WR
-                const uint32_t nlead = (uint32_t)(C0 - G0);
-                const uint64_t q = (uint32_t)lane < nlead ? G0 + (uint32_t)lane : C0;  // others repeat byte C0
-                gout[q] = S[LDS_FRONT + (uint32_t)(q - A0)];
+                gout[q] = lead;
             }
 #if TE_WK_STAMPS
             ++ntl;
@@ -2197,6 +2219,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
             c_pkts += npkt;
             c_bytes += tile.span_len;
             c_edited += npkt - n_noedit;
+            return filled;
     };
     // one tile with DEPTH spans in flight.  Rf holds tile t's descriptor and per-lane
     // values (its chunks are in LDS already) and is reloaded with tile t + DEPTH * W;
@@ -2214,9 +2237,12 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
         if (t + DEPTH * W < n_tiles) issue(Rf, dpre);  // in flight while this tile is edited and stored
         if (t + (DEPTH + 1) * W < n_tiles) dpre = tiles[t + (DEPTH + 1) * W];
         WK_STAMP(0)  // loop top + loads issued
-        edit(t, tile, my_rel, my_dirb, my_dirv, my_fzs);
+        const bool filled = edit(t, tile, my_rel, my_dirb, my_dirv, my_fzs, [&]() __attribute__((always_inline)) {
+            if (t + W < n_tiles) fill(Rn);
+            return true;
+        });
         WK_STAMP(4)  // stores issued
-        if (t + W < n_tiles) fill(Rn);
+        if (!filled && t + W < n_tiles) fill(Rn);
         WK_LANES_SYNC();  // the next tile's lanes read what every lane filled
         WK_STAMP(5)  // next span -> LDS (waits for its loads)
     };
@@ -2303,7 +2329,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 // the tile's image: its span start at S + LDS_FRONT + (span_off & 15)
                 S = IMG + (uint32_t)((t0 & ~15ull) - fw.A0);
                 WK_LANES_SYNC();
-                edit(k, tl, my_rel, 0u, false, 0u);
+                edit(k, tl, my_rel, 0u, false, 0u, []() { return false; });
                 WK_LANES_SYNC();
                 WK_STAMP(4)  // (window mode: the edit's stores)
                 s0 += len;
@@ -2827,13 +2853,16 @@ extern "C" int te_fast_grid(void) {
 #ifndef TE_WK_DEPTH_LEAN
 #define TE_WK_DEPTH_LEAN 1
 #endif
+#ifndef TE_WK_DEPTH_SMALL
+#define TE_WK_DEPTH_SMALL 1
+#endif
 // (TE_FF_INCR is a mode, not an option group: an instance with it keeps the incremental
 // checksums of a run without --fixcsum, so a launch takes one whose INCR bit matches)
 #define TE_FF_ALLH (TE_FF_ALL | TE_FF_HDR)
 #define TE_WAVE_INSTANCES(X)                                                                         \
     X(0u, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, SZ_NONE)                          \
-    X(TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED | TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE)    \
-    X(TE_FF_SEED | TE_FF_INCR | TE_FF_SMALL, TE_WK_DEPTH_LEAN, SZ_NONE)                                \
+    X(TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE) X(TE_FF_SEED | TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE)  \
+    X(TE_FF_SEED | TE_FF_INCR | TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE)                               \
     X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE) X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE)       \
     X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE)         \
     X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
