@@ -1337,12 +1337,36 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 // (TE_FF_SMALL instances keep TE_WK_LEAN_TILE_BYTES at 5 blocks/CU: a batch of C2's 80-byte
 // records fills 63 of them into 5 KiB, so the 8 KiB image buys nothing but a block per CU --
 // C2 0.626 -> 0.678 of peak, seed 0.685 -> 0.70, A/B on one box, round 6)
+// the size-preserving exact-path instances that read the cfg: their tile budget and blocks/CU
+// (8 KiB at 3 blocks/CU: an IMIX tile holds ~22 records, not ~16, and the per-tile phases
+//  edit a third more records a pass -- C3 0.607 -> 0.623, hdr 0.624 -> 0.645, macseed
+//  0.623 -> 0.641 of peak, A/B on one box, round 6; 6 KiB at 4 blocks before)
+#ifndef TE_WK_READS_TILE_BYTES
+#define TE_WK_READS_TILE_BYTES 8192
+#endif
+#ifndef TE_WK_READS_BLOCKS
+#define TE_WK_READS_BLOCKS 3
+#endif
+// the static +-4 instances (VLAN push / pop, --efcs: wk_store_sized) likewise: C4 0.564 ->
+// 0.581, vdel 0.589 -> 0.595, efcs 0.591 -> 0.595 (their chunk map sized by the budget)
+#ifndef TE_WK_SIZED_TILE_BYTES
+#define TE_WK_SIZED_TILE_BYTES 8192
+#endif
+#ifndef TE_WK_SIZED_BLOCKS
+#define TE_WK_SIZED_BLOCKS 3
+#endif
 template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     static constexpr bool big = !reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
-    static constexpr int blocks = reads || big ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
-    static constexpr int tile = reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
+    static constexpr bool rbig = reads && SZ == 0 && !WIN;
+    static constexpr bool sized = reads && (SZ == TE_SZ_GROW || SZ == TE_SZ_VDEL || SZ == TE_SZ_EFCS);
+    static constexpr int blocks = rbig    ? TE_WK_READS_BLOCKS
+                                  : sized ? TE_WK_SIZED_BLOCKS
+                                  : reads || big ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
+    static constexpr int tile = rbig    ? TE_WK_READS_TILE_BYTES
+                                : sized ? TE_WK_SIZED_TILE_BYTES
+                                : reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
 };
 #ifndef TE_WK_STORE_BARRIER
 #define TE_WK_STORE_BARRIER 1
@@ -1398,7 +1422,7 @@ static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "who
 // the sized stores (VLAN push / pop, --efcs: the instances that read the cfg) map a tile's
 // output chunks in 512 16-bit entries, laid out for 6 KiB tiles; 7 and 8 KiB builds wrote
 // wrong C4 bytes (A/B builds, round 5), so the budget is pinned
-static_assert(TE_WK_TILE_BYTES == 6144, "the sized stores' chunk map is laid out for 6 KiB tiles");
+static_assert(TE_WK_SIZED_TILE_BYTES <= 8192, "the sized stores' chunk map: at most 1,024 entries");
 static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
 static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
 
@@ -1499,10 +1523,14 @@ __device__ __forceinline__ void hdr_put(uint8_t *S, uint32_t h, uint32_t v) {
 #endif
 #define WK_LANES_SYNC() asm volatile("" ::: "memory")
 
+// (NE: map entries a lane, 8 for tiles up to 6 KiB -- 512 entries -- 16 past them)
+template <int NE>
 __device__ __forceinline__ void wk_chunk_map(uint32_t *P, uint32_t nown, uint32_t o0, uint32_t X, bool on,
                                              bool grow, int lane) {
-    uint16_t *K = (uint16_t *)P;  // 512 entries
-    *(uint4 *)(K + 8 * lane) = make_uint4(0, 0, 0, 0);
+    static_assert(NE == 8 || NE == 16, "whole uint4s of entries a lane");
+    uint16_t *K = (uint16_t *)P;  // 64 NE entries
+#pragma unroll
+    for (int h = 0; h < NE / 8; ++h) *(uint4 *)(K + NE * lane + 8 * h) = make_uint4(0, 0, 0, 0);
     // the first chunk that change j lies wholly before (GROW: the tag [X, X + 4) has ended;
     // SHRINK: the boundary X is at or before the chunk start)
     const uint32_t wb = grow ? X + 4u : X;
@@ -1511,17 +1539,25 @@ __device__ __forceinline__ void wk_chunk_map(uint32_t *P, uint32_t nown, uint32_
         if (cj < nown) K[cj] = (uint16_t)(lane + 1);
     }
     WK_LANES_SYNC();
-    {  // prefix max over K, 8 entries a lane
-        const uint4 q = *(const uint4 *)(K + 8 * lane);
-        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
-                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+    {  // prefix max over K, NE entries a lane
+        uint32_t e[NE];
 #pragma unroll
-        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
-        const uint32_t excl = wave_prev(wave_scan_max(e[7]));
+        for (int h = 0; h < NE / 8; ++h) {
+            const uint4 q = *(const uint4 *)(K + NE * lane + 8 * h);
+            e[8 * h + 0] = q.x & 0xffffu, e[8 * h + 1] = q.x >> 16, e[8 * h + 2] = q.y & 0xffffu;
+            e[8 * h + 3] = q.y >> 16, e[8 * h + 4] = q.z & 0xffffu, e[8 * h + 5] = q.z >> 16;
+            e[8 * h + 6] = q.w & 0xffffu, e[8 * h + 7] = q.w >> 16;
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
-        *(uint4 *)(K + 8 * lane) =
-            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+        for (int i = 1; i < NE; ++i) e[i] = max(e[i], e[i - 1]);
+        const uint32_t excl = wave_prev(wave_scan_max(e[NE - 1]));
+#pragma unroll
+        for (int i = 0; i < NE; ++i) e[i] = max(e[i], excl);
+#pragma unroll
+        for (int h = 0; h < NE / 8; ++h)
+            *(uint4 *)(K + NE * lane + 8 * h) =
+                make_uint4(e[8 * h] | (e[8 * h + 1] << 16), e[8 * h + 2] | (e[8 * h + 3] << 16),
+                           e[8 * h + 4] | (e[8 * h + 5] << 16), e[8 * h + 6] | (e[8 * h + 7] << 16));
     }
     WK_LANES_SYNC();
     // the chunks change j meets (whose m is j): where
@@ -1575,24 +1611,28 @@ __device__ __forceinline__ void wk_put16(g_u8 *gout, uint64_t at, const uint32_t
 // meets and stores them over the first pass's bytes (one wave's stores to an address are
 // performed in order).  (Mixing in the chunk pass costs every chunk the VALU work
 // of the few that need it: C4 spent a third of its kernel there.)
-template <bool GROW>
+// (TB: the tile budget; the output chunks of a tile number <= (TB + 256) / 16 + 1: NK rounds
+//  of 64, a map of NE entries a lane)
+template <bool GROW, int TB>
 __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_u8 *gout, uint64_t OS,
                                                uint32_t span_len, uint32_t npkt, uint32_t g0, uint32_t X,
                                                bool on, uint32_t tag, int lane, bool stream) {
+    constexpr int NK = ((TB + 256) / 16 + 1 + 63) / 64, NE = NK <= 8 ? 8 : 16;
+    static_assert(NE * 64 * 2 <= wk_nch(TB) * 4, "the chunk map fits the chunk-prefix array");
     const uint64_t OE = GROW ? OS + span_len + 4ull * npkt : OS + span_len - 4ull * npkt;
     const uint64_t C0 = (OS + 15) & ~15ull;
     const uint32_t o0 = (uint32_t)(C0 - OS);
-    const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);  // <= 403
-    wk_chunk_map(P, nown, o0, X, on, GROW, lane);
+    const uint32_t nown = (uint32_t)((((OE + 15) & ~15ull) - C0) >> 4);  // <= 64 NK
+    wk_chunk_map<NE>(P, nown, o0, X, on, GROW, lane);
     const uint16_t *K = (const uint16_t *)P;
     const uint8_t *img = S + LDS_FRONT + g0;  // input byte x of the tile
     // every read in flight before the first store (a store under its own branch would
     // otherwise pull its reads in after it and wait them out one chunk at a time)
-    uint32_t kv[7], w[7][4];
+    uint32_t kv[NK], w[NK][4];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nown - 1u)];
+    for (int k = 0; k < NK; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nown - 1u)];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {  // lanes past the output repeat its last chunk (same bytes)
+    for (int k = 0; k < NK; ++k) {  // lanes past the output repeat its last chunk (same bytes)
         const uint32_t cc = umin32((uint32_t)lane + 64u * k, nown - 1u);
         const uint32_t m = kv[k] & 127u;
         const uint32_t o = o0 + 16u * cc;
@@ -1606,11 +1646,11 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
     // and overwriting; WK_SKIP_TOUCHED=0 restores the unconditional form)
 #if WK_SKIP_TOUCHED
 #pragma unroll
-    for (int k = 0; k < 7; ++k)
+    for (int k = 0; k < NK; ++k)
         if ((kv[k] >> 7) == 0u) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
 #else
 #pragma unroll
-    for (int k = 0; k < 7; ++k) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
+    for (int k = 0; k < NK; ++k) wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nown - 1u), w[k], stream);
 #endif
     // the chunks this lane's change meets: both built on every lane (reads in flight
     // together), stored where they exist
@@ -2154,12 +2194,12 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
             bool filled = false;
             if constexpr (GROW) {
                 // record j's tag at output offset rel_j + 28 + 4 j (its input byte rel_j + 28 on)
-                wk_store_sized<true>(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0,
+                wk_store_sized<true, TB>(S, P, gout, G0 + 4ull * tile.first_pkt, tile.span_len, npkt, g0,
                                      my_rel + 28u + 4u * (uint32_t)lane, on, a.vlan_tag_word, lane,
                                      stream && WK_SIZED_STREAM);
             } else if constexpr (SHRINK) {
                 const uint32_t Dj = my_rel + (VDEL ? 28u : 16u + ecap);
-                wk_store_sized<false>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
+                wk_store_sized<false, TB>(S, P, gout, G0 - 4ull * tile.first_pkt, tile.span_len, npkt, g0,
                                       Dj - 4u * (uint32_t)lane, on, 0u, lane, stream && WK_SIZED_STREAM);
             } else if constexpr (MTU || FUZZ) {
                 // the kept sizes -> output offsets; the tile's output at input offset - tcut[t]
@@ -2947,7 +2987,11 @@ static int wave_pick(uint32_t want, int sz);
 extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small) {
     const int k = wave_pick(fast_feat(c) | (small ? TE_FF_SMALL : 0u), sz);
     if (k < 0) return TE_WK_TILE_BYTES;
-    return (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) ? TE_WK_TILE_BYTES
+    const bool reads = (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
+    const int sz_ = wave_inst[k].sz;
+    return reads ? (sz_ == SZ_NONE                                          ? TE_WK_READS_TILE_BYTES
+                    : sz_ == SZ_GROW || sz_ == SZ_VDEL || sz_ == SZ_EFCS ? TE_WK_SIZED_TILE_BYTES
+                                                                         : TE_WK_TILE_BYTES)
            : wave_inst[k].sz == SZ_NONE && !(wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_BIG_TILE_BYTES
                                                                             : TE_WK_LEAN_TILE_BYTES;
 }
