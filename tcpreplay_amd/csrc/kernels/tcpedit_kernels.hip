@@ -1323,6 +1323,9 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #endif
 // The lean instances also cut tiles to TE_WK_LEAN_TILE_BYTES: 63 C2 records (80 B) fill five
 // 16-byte chunk loads per lane exactly, where 64 records and the next header need six.
+#ifndef TE_WK_SMALL_BLOCKS
+#define TE_WK_SMALL_BLOCKS TE_WK_LEAN_BLOCKS  // (the TE_FF_SMALL instances)
+#endif
 #ifndef TE_WK_LEAN_TILE_BYTES
 #define TE_WK_LEAN_TILE_BYTES 5120
 #endif
@@ -1355,6 +1358,16 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_SIZED_BLOCKS
 #define TE_WK_SIZED_BLOCKS 3
 #endif
+// the per-record cut instances (--mtu-trunc, --fuzz-seed: wk_store_mtu): their tile budget
+// for the lean and the cfg-reading instances
+// (8 KiB at 3 blocks/CU, a map of 16 entries a lane: mtu 0.547 -> 0.587, fz 0.365 -> 0.412 of
+//  peak, A/B on one box, round 6; the lean 5 KiB / cfg 6 KiB budgets before -- 0 restores them)
+#ifndef TE_WK_CUT_TILE_BYTES
+#define TE_WK_CUT_TILE_BYTES 8192
+#endif
+#ifndef TE_WK_CUT_BLOCKS
+#define TE_WK_CUT_BLOCKS 3  // (0: as the other lean / cfg instances; --fuzz-seed: TE_WK_FUZZ_BLOCKS)
+#endif
 template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
@@ -1363,9 +1376,13 @@ struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupan
     static constexpr bool sized = reads && (SZ == TE_SZ_GROW || SZ == TE_SZ_VDEL || SZ == TE_SZ_EFCS);
     static constexpr int blocks = rbig    ? TE_WK_READS_BLOCKS
                                   : sized ? TE_WK_SIZED_BLOCKS
-                                  : reads || big ? TE_WK_MIN_BLOCKS : TE_WK_LEAN_BLOCKS;
+                                  : SZ == TE_SZ_MTU && TE_WK_CUT_BLOCKS ? TE_WK_CUT_BLOCKS
+                                  : reads || big ? TE_WK_MIN_BLOCKS
+                                  : (F & TE_FF_SMALL) && SZ == 0 && !WIN ? TE_WK_SMALL_BLOCKS : TE_WK_LEAN_BLOCKS;
+    static constexpr bool cut = SZ == TE_SZ_MTU || SZ == TE_SZ_FUZZ;
     static constexpr int tile = rbig    ? TE_WK_READS_TILE_BYTES
                                 : sized ? TE_WK_SIZED_TILE_BYTES
+                                : cut && TE_WK_CUT_TILE_BYTES ? TE_WK_CUT_TILE_BYTES
                                 : reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
 };
 #ifndef TE_WK_STORE_BARRIER
@@ -1696,10 +1713,14 @@ __device__ __forceinline__ void wk_store_sized(const uint8_t *S, uint32_t *P, g_
 // DROPS (SZ_FUZZ): records may keep nothing and a record may be as short as 17 bytes, so
 // the kept ones are numbered apart from their lanes and a tile may have no whole chunk;
 // without it (SZ_MTU) the kept records are lanes [0, npkt) and each is >= 50 bytes.
-template <int NK, bool DROPS>
+// (NE: map entries a lane -- 8, or 16 for tiles past 8 KiB of output chunks -- the record
+//  table T then starts at u32 32 NE: P holds >= 32 NE + 64 words, wk_mtu_nch)
+template <int NK, bool DROPS, int NE = 8>
 __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
                                              uint32_t out_len, uint32_t npkt, uint32_t my_rel, uint32_t my_op,
                                              bool keep, int lane, bool stream) {
+    static_assert(NE == 8 || NE == 16, "whole uint4s of entries a lane");
+    static_assert(NK <= NE, "the map covers the full chunks");
     if (DROPS && out_len == 0) return;  // (wave-uniform: every record dropped)
     uint32_t ci = (uint32_t)lane, nk = npkt;  // this record's kept number; the kept records
     if constexpr (DROPS) {
@@ -1711,8 +1732,9 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
     const uint32_t o0 = (uint32_t)(C0 - OS);
     const uint32_t nfull = (out_len - o0) >> 4;  // (out_len >= 17 > o0; MTU: nfull >= 2)
     uint16_t *K = (uint16_t *)P;
-    uint32_t *T = P + 256;
-    *(uint4 *)(K + 8 * lane) = make_uint4(0, 0, 0, 0);
+    uint32_t *T = P + 32 * NE;
+#pragma unroll
+    for (int h = 0; h < NE / 8; ++h) *(uint4 *)(K + NE * lane + 8 * h) = make_uint4(0, 0, 0, 0);
     if (keep) T[ci] = my_rel | (my_op << 16);
     WK_LANES_SYNC();
     if (keep) {  // the first chunk starting at or after op_j (the first kept record: chunk 0)
@@ -1720,17 +1742,25 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
         if (cj <= nfull) K[cj] = (uint16_t)(ci + 1);
     }
     WK_LANES_SYNC();
-    {  // prefix max over K, 8 entries a lane
-        const uint4 q = *(const uint4 *)(K + 8 * lane);
-        uint32_t e[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16,
-                         q.z & 0xffffu, q.z >> 16, q.w & 0xffffu, q.w >> 16};
+    {  // prefix max over K, NE entries a lane
+        uint32_t e[NE];
 #pragma unroll
-        for (int i = 1; i < 8; ++i) e[i] = max(e[i], e[i - 1]);
-        const uint32_t excl = wave_prev(wave_scan_max(e[7]));
+        for (int h = 0; h < NE / 8; ++h) {
+            const uint4 q = *(const uint4 *)(K + NE * lane + 8 * h);
+            e[8 * h + 0] = q.x & 0xffffu, e[8 * h + 1] = q.x >> 16, e[8 * h + 2] = q.y & 0xffffu;
+            e[8 * h + 3] = q.y >> 16, e[8 * h + 4] = q.z & 0xffffu, e[8 * h + 5] = q.z >> 16;
+            e[8 * h + 6] = q.w & 0xffffu, e[8 * h + 7] = q.w >> 16;
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = max(e[i], excl);
-        *(uint4 *)(K + 8 * lane) =
-            make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+        for (int i = 1; i < NE; ++i) e[i] = max(e[i], e[i - 1]);
+        const uint32_t excl = wave_prev(wave_scan_max(e[NE - 1]));
+#pragma unroll
+        for (int i = 0; i < NE; ++i) e[i] = max(e[i], excl);
+#pragma unroll
+        for (int h = 0; h < NE / 8; ++h)
+            *(uint4 *)(K + NE * lane + 8 * h) =
+                make_uint4(e[8 * h] | (e[8 * h + 1] << 16), e[8 * h + 2] | (e[8 * h + 3] << 16),
+                           e[8 * h + 4] | (e[8 * h + 5] << 16), e[8 * h + 6] | (e[8 * h + 7] << 16));
     }
     WK_LANES_SYNC();
     // kept record j > 0 starting inside a chunk: K there already names kept record j - 1 (value j)
@@ -1828,13 +1858,20 @@ template <uint32_t F, int DEPTH, int SZ, bool WIN = false>
 // (SZ_FUZZ: TE_WK_FUZZ_BLOCKS per CU, one fewer with the address maps -- at the lean
 //  instances' 5 / the others' 4 the fuzz step's registers spill)
 #ifndef TE_WK_FUZZ_BLOCKS
-#define TE_WK_FUZZ_BLOCKS TE_WK_MIN_BLOCKS
+#define TE_WK_FUZZ_BLOCKS (TE_WK_CUT_TILE_BYTES > 6144 ? 3 : TE_WK_MIN_BLOCKS)
 #endif
 __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_WIN_BLOCKS : TE_WIN_LEAN_BLOCKS)
-                                       : SZ == SZ_FUZZ ? (WkCfg<F>::reads ? TE_WK_FUZZ_BLOCKS - 1 : TE_WK_FUZZ_BLOCKS)
-                                       : DEPTH == 2    ? TE_WK_MIN_BLOCKS  // (two spans in flight: 128 VGPRs)
+                                       : SZ == SZ_FUZZ ? (WkCfg<F>::reads && TE_WK_CUT_TILE_BYTES <= 6144 ? TE_WK_FUZZ_BLOCKS - 1
+                                                                                                    : TE_WK_FUZZ_BLOCKS)
+                                       : (DEPTH == 2 && (WkCfg<F, SZ, WIN>::blocks) > TE_WK_MIN_BLOCKS)
+                                                       ? TE_WK_MIN_BLOCKS  // (two spans in flight: >= 128 VGPRs)
                                                        : (WkCfg<F, SZ, WIN>::blocks)) te_wave_tiles(FastArgs a) {
-    constexpr int TB = WkCfg<F, SZ, WIN>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB), WK_NCH = wk_nch(TB);
+    constexpr int TB = WkCfg<F, SZ, WIN>::tile, WK_KL = wk_kl(TB), WK_IMG = WIN ? WIN_IMG : wk_img(TB);
+    // (--mtu-trunc / --fuzz-seed stores: a map of MTU_NE entries a lane and a 64-word record
+    //  table after it, in the chunk-prefix array)
+    constexpr int MTU_NE = WK_KL + 1 <= 8 ? 8 : 16;
+    constexpr int WK_NCH = (SZ == SZ_MTU || SZ == SZ_FUZZ) && 32 * MTU_NE + 64 > wk_nch(TB) ? 32 * MTU_NE + 64
+                                                                                         : wk_nch(TB);
     static_assert(!WIN || SZ == SZ_NONE, "window mode: size-preserving instances");
     constexpr bool GROW = SZ == SZ_GROW, VDEL = SZ == SZ_VDEL, EFCS = SZ == SZ_EFCS, SHRINK = VDEL || EFCS;
     constexpr bool MTU = SZ == SZ_MTU, FUZZ = SZ == SZ_FUZZ;
@@ -2211,7 +2248,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 const uint32_t cut = tile.span_len - out_len;
                 if (lane == 0 && (long long)cut != k1 - k0) atomicOr(a.grow_bad, 1u);  // (a stale prediction)
                 c_cut += cut;
-                wk_store_mtu<WK_KL + 1, FUZZ>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len,
+                wk_store_mtu<WK_KL + 1, FUZZ, MTU_NE>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len,
                                               npkt, my_rel, incl - osz, osz != 0u, lane, stream && WK_MTU_STREAM);
                 if constexpr (FUZZ) {
                     c_drop += (unsigned long long)__popcll(__ballot(on && fz_cut && fz_nl == 0u));
@@ -2898,16 +2935,20 @@ extern "C" int te_fast_grid(void) {
 #endif
 // (TE_FF_INCR is a mode, not an option group: an instance with it keeps the incremental
 // checksums of a run without --fixcsum, so a launch takes one whose INCR bit matches)
+#ifndef TE_WK_DEPTH_READS
+#define TE_WK_DEPTH_READS 1
+#endif
 #define TE_FF_ALLH (TE_FF_ALL | TE_FF_HDR)
+#define DR TE_WK_DEPTH_READS
 #define TE_WAVE_INSTANCES(X)                                                                         \
     X(0u, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, SZ_NONE)                          \
     X(TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE) X(TE_FF_SEED | TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE)  \
     X(TE_FF_SEED | TE_FF_INCR | TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE)                               \
-    X(TE_FF_PORTMAP | TE_FF_RWIP, 1, SZ_NONE) X(TE_FF_ALL, 1, SZ_NONE) X(TE_FF_ALLH, 1, SZ_NONE)       \
-    X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, 1, SZ_NONE)         \
-    X(TE_FF_ALLX, 1, SZ_NONE)                                                                         \
-    X(TE_FF_ALL, 1, SZ_GROW) X(TE_FF_ALLH, 1, SZ_GROW) X(TE_FF_ALLX, 1, SZ_GROW)                      \
-    X(TE_FF_ALLH, 1, SZ_VDEL) X(TE_FF_ALLX, 1, SZ_VDEL) X(TE_FF_ALLH, 1, SZ_EFCS) X(TE_FF_ALLX, 1, SZ_EFCS)  \
+    X(TE_FF_PORTMAP | TE_FF_RWIP, DR, SZ_NONE) X(TE_FF_ALL, DR, SZ_NONE) X(TE_FF_ALLH, DR, SZ_NONE)    \
+    X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, DR, SZ_NONE)        \
+    X(TE_FF_ALLX, DR, SZ_NONE)                                                                        \
+    X(TE_FF_ALL, DR, SZ_GROW) X(TE_FF_ALLH, DR, SZ_GROW) X(TE_FF_ALLX, DR, SZ_GROW)                   \
+    X(TE_FF_ALLH, DR, SZ_VDEL) X(TE_FF_ALLX, DR, SZ_VDEL) X(TE_FF_ALLH, DR, SZ_EFCS) X(TE_FF_ALLX, DR, SZ_EFCS)  \
     X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)                                                          \
     X(TE_FF_INCR, 1, SZ_FUZZ) X(0u, 1, SZ_FUZZ) X(TE_FF_RWIP | TE_FF_INCR, 1, SZ_FUZZ)                  \
     X(TE_FF_RWIP, 1, SZ_FUZZ)
@@ -2989,6 +3030,7 @@ extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small)
     if (k < 0) return TE_WK_TILE_BYTES;
     const bool reads = (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     const int sz_ = wave_inst[k].sz;
+    if ((sz_ == SZ_MTU || sz_ == SZ_FUZZ) && TE_WK_CUT_TILE_BYTES) return TE_WK_CUT_TILE_BYTES;
     return reads ? (sz_ == SZ_NONE                                          ? TE_WK_READS_TILE_BYTES
                     : sz_ == SZ_GROW || sz_ == SZ_VDEL || sz_ == SZ_EFCS ? TE_WK_SIZED_TILE_BYTES
                                                                          : TE_WK_TILE_BYTES)
