@@ -1339,7 +1339,8 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #endif
 // (TE_FF_SMALL instances keep TE_WK_LEAN_TILE_BYTES at 5 blocks/CU: a batch of C2's 80-byte
 // records fills 63 of them into 5 KiB, so the 8 KiB image buys nothing but a block per CU --
-// C2 0.626 -> 0.678 of peak, seed 0.685 -> 0.70, A/B on one box, round 6)
+// C2 0.626 -> 0.678 of peak, seed 0.685 -> 0.70, A/B on one box, round 6; the cfg-reading
+// ones TE_WK_TILE_BYTES at 4 blocks/CU: 1M x 64 B under --pnat --portmap 0.50 -> 0.58)
 // the size-preserving exact-path instances that read the cfg: their tile budget and blocks/CU
 // (8 KiB at 3 blocks/CU: an IMIX tile holds ~22 records, not ~16, and the per-tile phases
 //  edit a third more records a pass -- C3 0.607 -> 0.623, hdr 0.624 -> 0.645, macseed
@@ -1372,7 +1373,7 @@ template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     static constexpr bool big = !reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
-    static constexpr bool rbig = reads && SZ == 0 && !WIN;
+    static constexpr bool rbig = reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
     static constexpr bool sized = reads && (SZ == TE_SZ_GROW || SZ == TE_SZ_VDEL || SZ == TE_SZ_EFCS);
     static constexpr int blocks = rbig    ? TE_WK_READS_BLOCKS
                                   : sized ? TE_WK_SIZED_BLOCKS
@@ -2947,6 +2948,9 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_PORTMAP | TE_FF_RWIP, DR, SZ_NONE) X(TE_FF_ALL, DR, SZ_NONE) X(TE_FF_ALLH, DR, SZ_NONE)    \
     X(TE_FF_SEED | TE_FF_INCR, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR, DR, SZ_NONE)        \
     X(TE_FF_ALLX, DR, SZ_NONE)                                                                        \
+    X(TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_SMALL, 1, SZ_NONE) X(TE_FF_ALL | TE_FF_SMALL, 1, SZ_NONE)      \
+    X(TE_FF_ALLH | TE_FF_SMALL, 1, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR | TE_FF_SMALL, 1, SZ_NONE)         \
+    X(TE_FF_ALLX | TE_FF_SMALL, 1, SZ_NONE)                                                           \
     X(TE_FF_ALL, DR, SZ_GROW) X(TE_FF_ALLH, DR, SZ_GROW) X(TE_FF_ALLX, DR, SZ_GROW)                   \
     X(TE_FF_ALLH, DR, SZ_VDEL) X(TE_FF_ALLX, DR, SZ_VDEL) X(TE_FF_ALLH, DR, SZ_EFCS) X(TE_FF_ALLX, DR, SZ_EFCS)  \
     X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)                                                          \
@@ -3031,7 +3035,7 @@ extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small)
     const bool reads = (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     const int sz_ = wave_inst[k].sz;
     if ((sz_ == SZ_MTU || sz_ == SZ_FUZZ) && TE_WK_CUT_TILE_BYTES) return TE_WK_CUT_TILE_BYTES;
-    return reads ? (sz_ == SZ_NONE                                          ? TE_WK_READS_TILE_BYTES
+    return reads ? (sz_ == SZ_NONE ? ((wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_TILE_BYTES : TE_WK_READS_TILE_BYTES)
                     : sz_ == SZ_GROW || sz_ == SZ_VDEL || sz_ == SZ_EFCS ? TE_WK_SIZED_TILE_BYTES
                                                                          : TE_WK_TILE_BYTES)
            : wave_inst[k].sz == SZ_NONE && !(wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_BIG_TILE_BYTES

@@ -14,6 +14,10 @@ from tcpreplay_amd import synth as S  # noqa: E402
 CASES = {
     "c2": (lambda: S.pcap_fixed(1_000_000, 64, seed=1), ["--seed=42", "--fixcsum"]),
     "c2x10": (lambda: S.pcap_fixed(10_000_000, 64, seed=1), ["--seed=42", "--fixcsum"]),
+    # small records under a cfg-reading instance (address map + port map)
+    "c2pnat": (lambda: S.pcap_fixed(1_000_000, 64, seed=1),
+               ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]),
+    "hdr": (lambda: S.pcap_imix(1_000_000, seed=1), ["--ttl=+1", "--tos=7"]),
     "c3": (lambda: S.pcap_imix(1_000_000, seed=1),
            ["--pnat=10.0.0.0/8:192.168.0.0/16", "--portmap=53:5353,80:8080", "--fixcsum"]),
     "c5": (lambda: S.pcap_mixed_v4v6(250_000, 1514, seed=1), ["--fixcsum"]),
