@@ -181,3 +181,33 @@ def test_fuzz_options_reach_the_device_config(built):
     for bad in (["--fuzz-factor=2"], ["--fuzz-seed=1", "--fuzz-factor=0"]):
         with pytest.raises(ValueError):
             derive(bad)
+
+
+def test_wave_tile_budgets_per_config_and_batch(built):
+    """the wave lane's tile budget for a config and a batch (te_wave_tile_bytes: the instance
+    wave_pick takes): a seed-only config runs the lean SEED instance (--seed's rewrite_ip
+    without a map changes nothing, edit_packet.c:787-878); batches of small records (the
+    TE_FF_SMALL mode) keep 5 KiB tiles on the lean instances and 6 KiB on the cfg-reading
+    ones; the others cut 8 KiB (round 6).  Host logic only: no kernel runs."""
+    L = ctypes.CDLL(TA.LIB_PATH)
+    f = L.te_wave_tile_bytes
+    f.restype, f.argtypes = ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    NONE, GROW, VDEL, EFCS, MTU, FUZZ = 0, 1, 2, 3, 4, 5
+    pnat = "--pnat=10.0.0.0/8:192.168.0.0/16"
+    cases = [
+        (["--seed=42", "--fixcsum"], NONE, 1, 5120), (["--seed=42", "--fixcsum"], NONE, 0, 8192),
+        (["--seed=42"], NONE, 1, 5120), (["--fixcsum"], NONE, 1, 5120), (["--fixcsum"], NONE, 0, 8192),
+        ([pnat, "--fixcsum"], NONE, 0, 8192), ([pnat, "--fixcsum"], NONE, 1, 6144),
+        ([pnat, "--seed=7", "--fixcsum"], NONE, 1, 6144),
+        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 0, 8192),
+        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 1, 8192),
+        (["--enet-vlan=del", "--fixcsum"], VDEL, 1, 8192), (["--efcs", "--fixcsum"], EFCS, 0, 8192),
+        (["--mtu=1000", "--mtu-trunc", "--fixcsum"], MTU, 1, 8192),
+        (["--fuzz-seed=42", "--fuzz-factor=2"], FUZZ, 0, 8192),
+    ]
+    for args, sz, small, want in cases:
+        te, cfg, _ = derive(args)
+        try:
+            assert f(ctypes.addressof(cfg), sz, small) == want, (args, sz, small)
+        finally:
+            te.close()
