@@ -619,9 +619,10 @@ def main():
             # (after the host-side oracle check the device is idle for seconds: a warm-up of
             # the same runs before either timing, then the kernel-only and the pipeline
             # timings in the primary line's order)
-            b2.time(max(5, opt.steps // 50))
-            _, kms2 = b2.time_kernels(max(5, opt.steps // 50))
-            ms2 = b2.time(max(5, opt.steps // 50))
+            k2 = max(20, opt.steps // 50)
+            b2.time(k2)
+            _, kms2 = b2.time_kernels(k2)
+            ms2 = b2.time(k2)
             ab = r2.bytes_in + r2.bytes_out
             extra[wl] = {"workload": WORKLOADS[wl][3], "packets": n2, "pipeline_ms": round(ms2, 4),
                          "kernel_ms": round(kms2, 4), "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),
