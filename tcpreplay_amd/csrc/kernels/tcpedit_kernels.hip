@@ -1369,20 +1369,26 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_CUT_BLOCKS
 #define TE_WK_CUT_BLOCKS 3  // (0: as the other lean / cfg instances; --fuzz-seed: TE_WK_FUZZ_BLOCKS)
 #endif
+#ifndef TE_WK_SIZED_LEAN_TILE_BYTES
+#define TE_WK_SIZED_LEAN_TILE_BYTES TE_WK_SIZED_TILE_BYTES
+#endif
+#ifndef TE_WK_SIZED_LEAN_BLOCKS
+#define TE_WK_SIZED_LEAN_BLOCKS TE_WK_SIZED_BLOCKS
+#endif
 template <uint32_t F, int SZ = 0, bool WIN = false>
 struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupancy target and tile budget
     static constexpr bool reads = (F & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     static constexpr bool big = !reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
     static constexpr bool rbig = reads && SZ == 0 && !WIN && !(F & TE_FF_SMALL);
-    static constexpr bool sized = reads && (SZ == TE_SZ_GROW || SZ == TE_SZ_VDEL || SZ == TE_SZ_EFCS);
+    static constexpr bool sized = SZ == TE_SZ_GROW || SZ == TE_SZ_VDEL || SZ == TE_SZ_EFCS;
     static constexpr int blocks = rbig    ? TE_WK_READS_BLOCKS
-                                  : sized ? TE_WK_SIZED_BLOCKS
+                                  : sized ? (reads ? TE_WK_SIZED_BLOCKS : TE_WK_SIZED_LEAN_BLOCKS)
                                   : SZ == TE_SZ_MTU && TE_WK_CUT_BLOCKS ? TE_WK_CUT_BLOCKS
                                   : reads || big ? TE_WK_MIN_BLOCKS
                                   : (F & TE_FF_SMALL) && SZ == 0 && !WIN ? TE_WK_SMALL_BLOCKS : TE_WK_LEAN_BLOCKS;
     static constexpr bool cut = SZ == TE_SZ_MTU || SZ == TE_SZ_FUZZ;
     static constexpr int tile = rbig    ? TE_WK_READS_TILE_BYTES
-                                : sized ? TE_WK_SIZED_TILE_BYTES
+                                : sized ? (reads ? TE_WK_SIZED_TILE_BYTES : TE_WK_SIZED_LEAN_TILE_BYTES)
                                 : cut && TE_WK_CUT_TILE_BYTES ? TE_WK_CUT_TILE_BYTES
                                 : reads ? TE_WK_TILE_BYTES : big ? TE_WK_BIG_TILE_BYTES : TE_WK_LEAN_TILE_BYTES;
 };
@@ -2941,6 +2947,16 @@ extern "C" int te_fast_grid(void) {
 #endif
 #define TE_FF_ALLH (TE_FF_ALL | TE_FF_HDR)
 #define DR TE_WK_DEPTH_READS
+#ifndef TE_WK_SIZED_LEAN
+#define TE_WK_SIZED_LEAN 0
+#endif
+#if TE_WK_SIZED_LEAN
+// (the static +-4 changes without an edit that reads the cfg, and C4's MACs + endpoints)
+#define TE_WAVE_SIZED_LEAN(X)                                                                        \
+    X(0u, 1, SZ_GROW) X(0u, 1, SZ_VDEL) X(0u, 1, SZ_EFCS) X(TE_FF_MAC | TE_FF_RWIP, 1, SZ_GROW)
+#else
+#define TE_WAVE_SIZED_LEAN(X)
+#endif
 #define TE_WAVE_INSTANCES(X)                                                                         \
     X(0u, TE_WK_DEPTH_LEAN, SZ_NONE) X(TE_FF_SEED, TE_WK_DEPTH_LEAN, SZ_NONE)                          \
     X(TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE) X(TE_FF_SEED | TE_FF_SMALL, TE_WK_DEPTH_SMALL, SZ_NONE)  \
@@ -2951,6 +2967,7 @@ extern "C" int te_fast_grid(void) {
     X(TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_SMALL, 1, SZ_NONE) X(TE_FF_ALL | TE_FF_SMALL, 1, SZ_NONE)      \
     X(TE_FF_ALLH | TE_FF_SMALL, 1, SZ_NONE) X(TE_FF_HDR | TE_FF_INCR | TE_FF_SMALL, 1, SZ_NONE)         \
     X(TE_FF_ALLX | TE_FF_SMALL, 1, SZ_NONE)                                                           \
+    TE_WAVE_SIZED_LEAN(X)                                                                             \
     X(TE_FF_ALL, DR, SZ_GROW) X(TE_FF_ALLH, DR, SZ_GROW) X(TE_FF_ALLX, DR, SZ_GROW)                   \
     X(TE_FF_ALLH, DR, SZ_VDEL) X(TE_FF_ALLX, DR, SZ_VDEL) X(TE_FF_ALLH, DR, SZ_EFCS) X(TE_FF_ALLX, DR, SZ_EFCS)  \
     X(0u, 1, SZ_MTU) X(TE_FF_ALLH, 1, SZ_MTU)                                                          \
@@ -3035,9 +3052,9 @@ extern "C" uint32_t te_wave_tile_bytes(const te_dev_cfg_t *c, int sz, int small)
     const bool reads = (wave_inst[k].feat & (TE_FF_MAC | TE_FF_PORTMAP | TE_FF_RWIP | TE_FF_HDR)) != 0;
     const int sz_ = wave_inst[k].sz;
     if ((sz_ == SZ_MTU || sz_ == SZ_FUZZ) && TE_WK_CUT_TILE_BYTES) return TE_WK_CUT_TILE_BYTES;
+    if (sz_ == SZ_GROW || sz_ == SZ_VDEL || sz_ == SZ_EFCS) return reads ? TE_WK_SIZED_TILE_BYTES : TE_WK_SIZED_LEAN_TILE_BYTES;
     return reads ? (sz_ == SZ_NONE ? ((wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_TILE_BYTES : TE_WK_READS_TILE_BYTES)
-                    : sz_ == SZ_GROW || sz_ == SZ_VDEL || sz_ == SZ_EFCS ? TE_WK_SIZED_TILE_BYTES
-                                                                         : TE_WK_TILE_BYTES)
+                                   : TE_WK_TILE_BYTES)
            : wave_inst[k].sz == SZ_NONE && !(wave_inst[k].feat & TE_FF_SMALL) ? TE_WK_BIG_TILE_BYTES
                                                                             : TE_WK_LEAN_TILE_BYTES;
 }
