@@ -3533,6 +3533,9 @@ extern "C" int te_mtu_cuts(const uint8_t *in, const te_tile_t *tiles, const uint
 // output is the per-64-tile layout te_mtu_cut_scan reads).
 // ===========================================================================
 constexpr uint32_t FZ_REACH_TILES = 16;
+#ifndef FZ_REACH_U
+#define FZ_REACH_U 4
+#endif
 constexpr uint32_t FZD_VALID = 1u << 31, FZD_LT = 1u << 19, FZD_V6 = 1u << 20, FZD_TCP = 1u << 21,
                    FZD_UDP = 1u << 22;
 
@@ -3579,22 +3582,53 @@ __global__ void __launch_bounds__(256) te_fuzz_reach(const uint8_t *in, const te
     if (lane < 2) openb[w][lane] = 0;
     const uint32_t nt = fz_load_tiles<FZ_REACH_TILES>(tiles, n, t0, T, lane);
     const uint32_t r0 = T.fp[0], r1 = T.fp[nt];
-    for (uint32_t r = r0 + lane; r < r1; r += 64u) {
-        const uint32_t j = fz_tile_of(T, nt, r);
-        const uint8_t *rec = in + T.so[j] + pkt_rel[r];
-        const uint32_t cap = ld32(rec + 8), len = ld32(rec + 12);
-        const uint8_t *d = rec + 16;
-        const uint32_t et = cap >= 14 ? ((uint32_t)d[12] << 8) | d[13] : 0u;
-        const bool v4 = et == 0x0800u && cap >= 34 && d[14] == 0x45u;
-        const bool v6 = et == 0x86DDu && cap >= 54 && (d[20] == 6u || d[20] == 17u);
-        if (v4 || v6) {
-            const uint32_t pr = v6 ? d[20] : d[23];
-            status[r] = 1;
-            desc[r] = FZD_VALID | cap | (len < cap ? FZD_LT : 0u) | (v6 ? FZD_V6 : 0u) | (pr == 6u ? FZD_TCP : 0u) |
-                      (pr == 17u ? FZD_UDP : 0u);
-        } else {
-            desc[r] = 0u;
-            atomicOr(&openb[w][j >> 5], 1u << (j & 31u));
+    // FZ_REACH_U records a lane at once, each header read as three 16-byte loads from its
+    // dword below caplen's field (the record offsets first, then every header load in flight
+    // together: a record at a time waited out two dependent loads and 13 byte loads each)
+    for (uint32_t rb = r0; rb < r1; rb += 64u * FZ_REACH_U) {
+        uint32_t rr[FZ_REACH_U], rel[FZ_REACH_U];
+#pragma unroll
+        for (int k = 0; k < FZ_REACH_U; ++k) {
+            rr[k] = umin32(rb + (uint32_t)lane + 64u * k, r1 - 1u);  // (past the end: the last record again)
+            rel[k] = pkt_rel[rr[k]];
+        }
+        uint32_t q[FZ_REACH_U][12], sh[FZ_REACH_U], jt[FZ_REACH_U];
+#pragma unroll
+        for (int k = 0; k < FZ_REACH_U; ++k) {
+            jt[k] = fz_tile_of(T, nt, rr[k]);
+            const uint64_t a = T.so[jt[k]] + rel[k] + 8u;  // caplen's field
+            sh[k] = (uint32_t)(a & 3u);
+            const uint32_t *qa = (const uint32_t *)(in + (a & ~3ull));
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const uint4 v = *(const uint4 *)(qa + 4 * i);  // (the image has 64 bytes of slack past its end)
+                q[k][4 * i] = v.x, q[k][4 * i + 1] = v.y, q[k][4 * i + 2] = v.z, q[k][4 * i + 3] = v.w;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < FZ_REACH_U; ++k) {
+            const uint32_t r = rb + (uint32_t)lane + 64u * k;
+            if (r >= r1) continue;
+            // header bytes from caplen's field on: D[0] caplen, D[1] len, D[5] packet bytes 12..15,
+            // D[7] packet bytes 20..23
+            const uint32_t s8 = sh[k];
+            const uint32_t cap = __builtin_amdgcn_alignbyte(q[k][1], q[k][0], s8);
+            const uint32_t len = __builtin_amdgcn_alignbyte(q[k][2], q[k][1], s8);
+            const uint32_t d5 = __builtin_amdgcn_alignbyte(q[k][6], q[k][5], s8);
+            const uint32_t d7 = __builtin_amdgcn_alignbyte(q[k][8], q[k][7], s8);
+            const uint32_t et = cap >= 14 ? ((d5 & 0xffu) << 8) | ((d5 >> 8) & 0xffu) : 0u;
+            const uint32_t d14 = (d5 >> 16) & 0xffu, d20 = d7 & 0xffu, d23 = d7 >> 24;
+            const bool v4 = et == 0x0800u && cap >= 34 && d14 == 0x45u;
+            const bool v6 = et == 0x86DDu && cap >= 54 && (d20 == 6u || d20 == 17u);
+            if (v4 || v6) {
+                const uint32_t pr = v6 ? d20 : d23;
+                status[r] = 1;
+                desc[r] = FZD_VALID | cap | (len < cap ? FZD_LT : 0u) | (v6 ? FZD_V6 : 0u) | (pr == 6u ? FZD_TCP : 0u) |
+                          (pr == 17u ? FZD_UDP : 0u);
+            } else {
+                desc[r] = 0u;
+                atomicOr(&openb[w][jt[k] >> 5], 1u << (jt[k] & 31u));
+            }
         }
     }
     WK_LANES_SYNC();
