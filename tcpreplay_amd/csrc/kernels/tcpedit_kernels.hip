@@ -3655,12 +3655,25 @@ __global__ void __launch_bounds__(256) te_fuzz_tile_cut(const uint8_t *in, const
     const uint32_t nt = fz_load_tiles(tiles, n, t0, T, lane);
     const uint32_t factor = cfg->fuzz_factor;
     const uint32_t r0 = T.fp[0], r1 = T.fp[nt];
-    for (uint32_t r = r0 + lane; r < r1; r += 64u) {
-        if (!(status[r] & 1u)) continue;
-        uint32_t st = states[r];
+    // FZ_REACH_U records a lane at once, their flag, state and word loaded together (a record
+    // at a time waited for the flag, then for the state)
+    for (uint32_t rb = r0; rb < r1; rb += 64u * FZ_REACH_U) {
+    uint32_t fl_[FZ_REACH_U], st_[FZ_REACH_U], dw_[FZ_REACH_U];
+#pragma unroll
+    for (int k = 0; k < FZ_REACH_U; ++k) {
+        const uint32_t rk = umin32(rb + (uint32_t)lane + 64u * k, r1 - 1u);
+        fl_[k] = status[rk];
+        st_[k] = states[rk];
+        dw_[k] = desc[rk];
+    }
+#pragma unroll
+    for (int k = 0; k < FZ_REACH_U; ++k) {
+        const uint32_t r = rb + (uint32_t)lane + 64u * k;
+        if (r >= r1 || !(fl_[k] & 1u)) continue;
+        uint32_t st = st_[k];
         const uint32_t rnd = tcpr_random_dev(st);
         if (rnd % factor) continue;
-        const uint32_t dw = desc[r];
+        const uint32_t dw = dw_[k];
         FzPlan f;
         uint32_t cap;
         if (dw & FZD_VALID) {
@@ -3674,6 +3687,7 @@ __global__ void __launch_bounds__(256) te_fuzz_tile_cut(const uint8_t *in, const
             f = fuzz_plan(rec + 16, cap, ld32(rec + 12), cap, *cfg, rnd);
         }
         if (f.cut) atomicAdd(&cut[w][fz_tile_of(T, nt, r)], f.nl ? cap - f.nl : 16u + cap);
+    }
     }
     WK_LANES_SYNC();
     const long long v = lane < nt ? (long long)cut[w][lane] : 0ll;
