@@ -1337,6 +1337,9 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #ifndef TE_WK_BIG_TILE_BYTES
 #define TE_WK_BIG_TILE_BYTES 8192
 #endif
+#ifndef TE_WK_BIG_BLOCKS
+#define TE_WK_BIG_BLOCKS TE_WK_MIN_BLOCKS
+#endif
 // (TE_FF_SMALL instances keep TE_WK_LEAN_TILE_BYTES at 5 blocks/CU: a batch of C2's 80-byte
 // records fills 63 of them into 5 KiB, so the 8 KiB image buys nothing but a block per CU --
 // C2 0.626 -> 0.678 of peak, seed 0.685 -> 0.70, A/B on one box, round 6; the cfg-reading
@@ -1384,7 +1387,8 @@ struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupan
     static constexpr int blocks = rbig    ? TE_WK_READS_BLOCKS
                                   : sized ? (reads ? TE_WK_SIZED_BLOCKS : TE_WK_SIZED_LEAN_BLOCKS)
                                   : SZ == TE_SZ_MTU && TE_WK_CUT_BLOCKS ? TE_WK_CUT_BLOCKS
-                                  : reads || big ? TE_WK_MIN_BLOCKS
+                                  : big ? TE_WK_BIG_BLOCKS
+                                  : reads ? TE_WK_MIN_BLOCKS
                                   : (F & TE_FF_SMALL) && SZ == 0 && !WIN ? TE_WK_SMALL_BLOCKS : TE_WK_LEAN_BLOCKS;
     static constexpr bool cut = SZ == TE_SZ_MTU || SZ == TE_SZ_FUZZ;
     static constexpr int tile = rbig    ? TE_WK_READS_TILE_BYTES
@@ -1442,12 +1446,13 @@ constexpr uint32_t WIN_F_EDIT = 0x100u;
 static_assert((WIN_F_EDIT & (IDX_STOP | IDX_ERROR | IDX_END | IDX_TRIM)) == 0, "a flag bit of its own");
 static_assert(WIN_W + 48 + WIN_TAIL < 65536, "record offsets from a window's start fit 16 bits");
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
-static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 8, "whole chunks per lane, <= 8 registers");
+static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 16, "whole chunks per lane, <= 16 registers");
+static_assert(TE_WK_BIG_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_BIG_TILE_BYTES) <= 16, "big tile budget");
 // the sized stores (VLAN push / pop, --efcs: the instances that read the cfg) map a tile's
 // output chunks in 512 16-bit entries, laid out for 6 KiB tiles; 7 and 8 KiB builds wrote
 // wrong C4 bytes (A/B builds, round 5), so the budget is pinned
 static_assert(TE_WK_SIZED_TILE_BYTES <= 8192, "the sized stores' chunk map: at most 1,024 entries");
-static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 8, "lean tile budget");
+static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 16, "lean tile budget");
 static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
 
 // TE_WK_STAMPS builds (diagnostics only): s_memtime per phase, summed per wave,
@@ -1924,12 +1929,12 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
     // record offset and tcpprep cache byte
     struct Span {
         te_tile_t tl;
-        uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+        uint4 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v15;
         uint32_t rel, dirb;
         bool dirv;     // (the cache byte exists: idx < dirbits_len)
         uint32_t fzs;  // FUZZ: the record's RNG state
     };
-#define WK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define WK_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
     const uint32_t W = gridDim.x * WK_NW;
     const uint32_t w0 = blockIdx.x * WK_NW + wid;
     const uint32_t n_tiles = a.n_tiles;
@@ -2267,7 +2272,7 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 const uint8_t *src = S + LDS_FRONT + (uint32_t)(C0 - A0);
                 // named registers, all reads in flight before the first store (left to itself the
                 // scheduler reuses one register quad and waits out each read's LDS latency in turn)
-                uint4 w0, w1, w2, w3, w4, w5, w6, w7;
+                uint4 w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15;
 #define WK_RD(k) \
         if constexpr (k < WK_KL) w##k = *(const uint4 *)(src + (umin32((uint32_t)lane + 64u * k, nown - 1u) << 4));
 #define WK_WR(k)                                                                                       \
