@@ -1,0 +1,20 @@
+"""The bench's extra lines, one workload at a time (diagnostic): the first run's result
+(generic-lane tiles, lane kind) and the pipeline vs kernel-only times over the same runs,
+for the bench's own seed (11) and the primary line's (1)."""
+import os
+import sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402
+
+for wl in (sys.argv[1:] or ["vdel", "mtu", "c4", "c3"]):
+    for seed in (11, 1):
+        n = bench.DEFAULT_PACKETS[wl]
+        te, b, r, _, _ = bench.run_workload(wl, n, 0, 3, seed=seed, device=0, verify=False)
+        b.time(20)
+        pk, kk = b.time_kernels(20)
+        p = b.time(20)
+        r2 = b.result()
+        print(f"{wl} seed {seed}: generic_tiles {r.generic_tiles} fast_kind {r.fast_kind} listed_after {r2.generic_tiles} "
+              f"pipeline {p:.4f} ms, kernel {kk:.4f} ms (event-pair run {pk:.4f})", flush=True)
+        b.close()
+        te.close()
