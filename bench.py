@@ -372,6 +372,28 @@ def e2e_line(opt):
                            "pageable copies (median of 3)"))
 
 
+def extra_line(wl, steps, verify):
+    """one secondary config's line (BASELINE configs[2..4] and the common tcprewrite lines),
+    run by `bench.py --extra-child WL` in a process of its own (main() starts it): its first
+    run checked against the oracle, then warm-up, kernel-only and pipeline timings"""
+    n2 = DEFAULT_PACKETS[wl]
+    te2, b2, r2, _, chk2 = run_workload(wl, n2, 0, 3, seed=11, device=0, verify=verify)
+    k2 = max(20, steps // 50)
+    b2.time(k2)
+    _, kms2 = b2.time_kernels(k2)
+    ms2 = b2.time(k2)
+    ab = r2.bytes_in + r2.bytes_out
+    line = {"workload": WORKLOADS[wl][3], "packets": n2, "pipeline_ms": round(ms2, 4),
+            "kernel_ms": round(kms2, 4), "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),
+            "gbps_algorithmic": round(ab / (ms2 * 1e-3) / 1e9, 1),
+            "frac_hbm_peak": round(ab / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_frac_hbm_peak": round(ab / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "verified": chk2 == n2, "verified_records": chk2}
+    b2.close()
+    te2.close()
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -390,6 +412,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end rate")
     ap.add_argument("--e2e-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--extra-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of every workload's "
                     "first run (on by default: the bench line is parity evidence)")
     ap.add_argument("--no-strong-side", action="store_true", help="N > 1: skip the BASELINE configs[3] line "
@@ -402,6 +425,9 @@ def main():
     opt = ap.parse_args()
     if opt.e2e_child:  # (main() of the parent process starts this)
         print(json.dumps(e2e_line(opt)), flush=True)
+        return
+    if opt.extra_child:  # (likewise)
+        print(json.dumps(extra_line(opt.extra_child, opt.steps, not opt.no_verify)), flush=True)
         return
     if opt.strong:  # one big job: the per-config side lines measure other things
         opt.extra, opt.no_e2e, opt.no_cpu_baseline = "", True, True
@@ -614,24 +640,16 @@ def main():
                              "gbps_algorithmic": round(ent * 50.25 / (kms2 * 1e-3) / 1e9, 1),
                              "cpu_baseline": cpu_prep}
                 continue
-            n2 = DEFAULT_PACKETS[wl]
-            te2, b2, r2, _, chk2 = run_workload(wl, n2, 0, 3, seed=11, device=0, verify=not opt.no_verify)
-            # (after the host-side oracle check the device is idle for seconds: a warm-up of
-            # the same runs before either timing, then the kernel-only and the pipeline
-            # timings in the primary line's order)
-            k2 = max(20, opt.steps // 50)
-            b2.time(k2)
-            _, kms2 = b2.time_kernels(k2)
-            ms2 = b2.time(k2)
-            ab = r2.bytes_in + r2.bytes_out
-            extra[wl] = {"workload": WORKLOADS[wl][3], "packets": n2, "pipeline_ms": round(ms2, 4),
-                         "kernel_ms": round(kms2, 4), "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),
-                         "gbps_algorithmic": round(ab / (ms2 * 1e-3) / 1e9, 1),
-                         "frac_hbm_peak": round(ab / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "kernel_frac_hbm_peak": round(ab / (kms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "verified": chk2 == n2, "verified_records": chk2}
-            b2.close()
-            te2.close()
+            # each line in a child process of its own, as a tcprewrite run has the device (the
+            # same runs measured 3-8 % slower inside this process after its other lines, the
+            # pipeline column below the kernel-only one -- the cause was not isolated)
+            import subprocess
+            cmd = [sys.executable, os.path.abspath(__file__), "--extra-child", wl, "--steps", str(opt.steps)] + \
+                (["--no-verify"] if opt.no_verify else [])
+            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            if cp.returncode != 0:
+                raise RuntimeError(f"extra line {wl} failed: {cp.stderr[-2000:]}")
+            extra[wl] = json.loads(cp.stdout.strip().splitlines()[-1])
         if extra:
             result["extra_configs"] = extra
         if not opt.no_e2e:

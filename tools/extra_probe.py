@@ -6,6 +6,20 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import bench  # noqa: E402
 
+if os.environ.get("XP_TORCH"):  # (the bench process has torch's device context)
+    import torch
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
+
+keep = []
+if os.environ.get("XP_PRIMARY"):  # (the bench's primary line first, its batch left open)
+    te0, b0, _, _, _ = bench.run_workload("c2", 1_000_000, 0, 10, seed=1, device=0, verify=False)
+    b0.time_kernels(int(os.environ.get("XP_PRIMARY")))
+    b0.time(int(os.environ.get("XP_PRIMARY")))
+    keep.append((te0, b0))
+    if os.environ.get("XP_CLOSE"):
+        b0.close()
+        te0.close()
 for wl in (sys.argv[1:] or ["vdel", "mtu", "c4", "c3"]):
     for seed in (11, 1):
         n = bench.DEFAULT_PACKETS[wl]
