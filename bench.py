@@ -379,9 +379,14 @@ def extra_line(wl, steps, verify):
     n2 = DEFAULT_PACKETS[wl]
     te2, b2, r2, _, chk2 = run_workload(wl, n2, 0, 3, seed=11, device=0, verify=verify)
     k2 = max(20, steps // 50)
-    b2.time(k2)
-    _, kms2 = b2.time_kernels(k2)
-    ms2 = b2.time(k2)
+    b2.time(k2)  # (the first window after the oracle check runs up to 10 % slow: clocks/caches)
+    # three alternating pipeline / kernel-only windows, the median of each (tools/extra_probe.py
+    # XP_WINDOWS: one window in three still moved by 5-9 % on a box where the rest agreed)
+    ps, ks = [], []
+    for _ in range(3):
+        ps.append(b2.time(k2))
+        ks.append(b2.time_kernels(k2)[1])
+    ms2, kms2 = sorted(ps)[1], sorted(ks)[1]
     ab = r2.bytes_in + r2.bytes_out
     line = {"workload": WORKLOADS[wl][3], "packets": n2, "pipeline_ms": round(ms2, 4),
             "kernel_ms": round(kms2, 4), "mpkt_s": round(n2 / (ms2 * 1e-3) / 1e6, 1),

@@ -23,7 +23,12 @@ if os.environ.get("XP_PRIMARY"):  # (the bench's primary line first, its batch l
 for wl in (sys.argv[1:] or ["vdel", "mtu", "c4", "c3"]):
     for seed in (11, 1):
         n = bench.DEFAULT_PACKETS[wl]
-        te, b, r, _, _ = bench.run_workload(wl, n, 0, 3, seed=seed, device=0, verify=False)
+        te, b, r, _, _ = bench.run_workload(wl, n, 0, 3, seed=seed, device=0, verify=bool(os.environ.get("XP_VERIFY")))
+        if os.environ.get("XP_WINDOWS"):  # alternating pipeline / kernel-only windows after the first run
+            for i in range(int(os.environ.get("XP_WINDOWS"))):
+                p = b.time(20)
+                _, kk = b.time_kernels(20)
+                print(f"{wl} window {i}: pipeline {p:.4f} ms, kernel {kk:.4f} ms", flush=True)
         b.time(20)
         pk, kk = b.time_kernels(20)
         p = b.time(20)
