@@ -1355,9 +1355,11 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 #define TE_WK_READS_BLOCKS 3
 #endif
 // the static +-4 instances (VLAN push / pop, --efcs: wk_store_sized) likewise: C4 0.564 ->
-// 0.581, vdel 0.589 -> 0.595, efcs 0.591 -> 0.595 (their chunk map sized by the budget)
+// 0.581, vdel 0.589 -> 0.595, efcs 0.591 -> 0.595 (their chunk map sized by the budget);
+// 9 KiB (51,840 B of LDS a block, 3 blocks in 160 KiB): C4 0.584 -> 0.586-0.596, vdel +0.2 %
+// (10 KiB does not fit 3 blocks; 9 KiB for the size-preserving cfg instances: C3, hdr -1 %)
 #ifndef TE_WK_SIZED_TILE_BYTES
-#define TE_WK_SIZED_TILE_BYTES 8192
+#define TE_WK_SIZED_TILE_BYTES 9216
 #endif
 #ifndef TE_WK_SIZED_BLOCKS
 #define TE_WK_SIZED_BLOCKS 3
@@ -1448,10 +1450,11 @@ static_assert(WIN_W + 48 + WIN_TAIL < 65536, "record offsets from a window's sta
 static_assert(WIN_IMG % 16 == 0, "16-byte aligned window images");
 static_assert(TE_WK_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_TILE_BYTES) <= 16, "whole chunks per lane, <= 16 registers");
 static_assert(TE_WK_BIG_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_BIG_TILE_BYTES) <= 16, "big tile budget");
-// the sized stores (VLAN push / pop, --efcs: the instances that read the cfg) map a tile's
-// output chunks in 512 16-bit entries, laid out for 6 KiB tiles; 7 and 8 KiB builds wrote
-// wrong C4 bytes (A/B builds, round 5), so the budget is pinned
-static_assert(TE_WK_SIZED_TILE_BYTES <= 8192, "the sized stores' chunk map: at most 1,024 entries");
+// the sized stores (VLAN push / pop, --efcs) map a tile's output chunks 8 or 16 entries a
+// lane (wk_store_sized: round 6, after 7 and 8 KiB builds of the 512-entry map wrote wrong
+// C4 bytes in round 5): at most 1,024 chunks
+static_assert(TE_WK_SIZED_TILE_BYTES % 1024 == 0 && (TE_WK_SIZED_TILE_BYTES + 256) / 16 + 1 <= 1024,
+              "the sized stores' chunk map: at most 1,024 entries");
 static_assert(TE_WK_LEAN_TILE_BYTES % 1024 == 0 && wk_kl(TE_WK_LEAN_TILE_BYTES) <= 16, "lean tile budget");
 static_assert(wk_img(TE_WK_TILE_BYTES) % 16 == 0 && wk_img(TE_WK_LEAN_TILE_BYTES) % 16 == 0, "16-byte aligned images");
 

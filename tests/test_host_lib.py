@@ -199,9 +199,9 @@ def test_wave_tile_budgets_per_config_and_batch(built):
         (["--seed=42"], NONE, 1, 5120), (["--fixcsum"], NONE, 1, 5120), (["--fixcsum"], NONE, 0, 8192),
         ([pnat, "--fixcsum"], NONE, 0, 8192), ([pnat, "--fixcsum"], NONE, 1, 6144),
         ([pnat, "--seed=7", "--fixcsum"], NONE, 1, 6144),
-        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 0, 8192),
-        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 1, 8192),
-        (["--enet-vlan=del", "--fixcsum"], VDEL, 1, 8192), (["--efcs", "--fixcsum"], EFCS, 0, 8192),
+        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 0, 9216),
+        (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 1, 9216),
+        (["--enet-vlan=del", "--fixcsum"], VDEL, 1, 9216), (["--efcs", "--fixcsum"], EFCS, 0, 9216),
         (["--mtu=1000", "--mtu-trunc", "--fixcsum"], MTU, 1, 8192),
         (["--fuzz-seed=42", "--fuzz-factor=2"], FUZZ, 0, 8192),
     ]
