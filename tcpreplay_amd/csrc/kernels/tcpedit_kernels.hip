@@ -1406,6 +1406,11 @@ struct WkCfg {  // does instance F read te_dev_cfg_t (its LDS copy); its occupan
 #ifndef TE_WK_FILL_EARLY
 #define TE_WK_FILL_EARLY 1
 #endif
+// and for the per-record cut stores (wk_store_mtu: --mtu-trunc, --fuzz-seed; A/B: mtu 1.8 %
+// slower, fz even -- off)
+#ifndef TE_WK_CUT_FILL_EARLY
+#define TE_WK_CUT_FILL_EARLY 0
+#endif
 // the same for the static +4 store (wk_store_sized, VLAN push: C4 0.596 -> 0.600, A/B)
 #ifndef TE_WK_SIZED_FILL_EARLY
 #define TE_WK_SIZED_FILL_EARLY 1
@@ -1771,13 +1776,14 @@ __device__ __forceinline__ bool wk_store_sized(const uint8_t *S, uint32_t *P, g_
 // without it (SZ_MTU) the kept records are lanes [0, npkt) and each is >= 50 bytes.
 // (NE: map entries a lane -- 8, or 16 for tiles past 8 KiB of output chunks -- the record
 //  table T then starts at u32 32 NE: P holds >= 32 NE + 64 words, wk_mtu_nch)
-template <int NK, bool DROPS, int NE = 8>
-__device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
+// pre_store (TE_WK_CUT_FILL_EARLY): as wk_store_sized's
+template <int NK, bool DROPS, int NE, typename PRE>
+__device__ __forceinline__ bool wk_store_mtu(const uint8_t *S, uint32_t ib, uint32_t *P, g_u8 *gout, uint64_t OS,
                                              uint32_t out_len, uint32_t npkt, uint32_t my_rel, uint32_t my_op,
-                                             bool keep, int lane, bool stream) {
+                                             bool keep, int lane, bool stream, PRE &&pre_store) {
     static_assert(NE == 8 || NE == 16, "whole uint4s of entries a lane");
     static_assert(NK <= NE, "the map covers the full chunks");
-    if (DROPS && out_len == 0) return;  // (wave-uniform: every record dropped)
+    if (DROPS && out_len == 0) return false;  // (wave-uniform: every record dropped)
     uint32_t ci = (uint32_t)lane, nk = npkt;  // this record's kept number; the kept records
     if constexpr (DROPS) {
         const unsigned long long km = __ballot(keep);
@@ -1823,6 +1829,58 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
     const uint32_t x = (keep && ci > 0) ? my_op - o0 : 16u, c1 = x >> 4, t1 = x & 15u;
     if (t1 != 0 && c1 < nfull) K[c1] = (uint16_t)(ci | 0x8000);
     WK_LANES_SYNC();
+    if constexpr (TE_WK_CUT_FILL_EARLY) {
+        // every read of the image first (pass 1's, pass 2's, the trailing and leading bytes'),
+        // then the next span into LDS, then the stores
+        const bool p1 = !DROPS || nfull;  // (wave-uniform)
+        uint32_t kv[NK], w[NK][4];
+        if (p1) {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) kv[k] = K[umin32((uint32_t)lane + 64u * k, nfull - 1u)];
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const uint32_t cc = umin32((uint32_t)lane + 64u * k, nfull - 1u);
+                const uint32_t e = T[(kv[k] & 0x7fu) - 1u];
+                const uint4 v = read16(S, ib + (e & 0xffffu) + o0 + 16u * cc - (e >> 16));
+                w[k][0] = v.x;
+                w[k][1] = v.y;
+                w[k][2] = v.z;
+                w[k][3] = v.w;
+            }
+        }
+        const uint32_t ep = T[ci > 0 ? ci - 1 : 0], prel = ep & 0xffffu, pop = ep >> 16;
+        const uint32_t q = o0 + 16u * c1;
+        const bool p2 = t1 != 0 && c1 < nfull;
+        const uint4 va = read16(S, p2 ? ib + prel + (q - pop) : ib);
+        const uint4 vb = read16(S, p2 ? ib + my_rel - t1 : ib);
+        const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
+        uint32_t m[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t mk = fl::bmask(0, (int)t1 - 4 * i);
+            m[i] = (A[i] & mk) | (B[i] & ~mk);
+        }
+        const uint32_t q0t = o0 + 16u * nfull, ntr = out_len - q0t;
+        const uint32_t qb = q0t + umin32((uint32_t)lane, ntr ? ntr - 1u : 0u);
+        const uint32_t j = (K[nfull] & 0x7fu) - 1u;
+        const uint32_t e1 = T[umin32(j + 1u, nk - 1u)];
+        const uint32_t e = (j + 1u < nk && qb >= (e1 >> 16)) ? e1 : T[j];
+        const uint8_t tv = S[ib + (e & 0xffffu) + qb - (e >> 16)];
+        const uint32_t ll = (uint32_t)lane < o0 ? (uint32_t)lane : 0u;
+        const uint8_t lv = S[ib + (DROPS ? T[0] & 0xffffu : 0u) + ll];
+        WK_LANES_SYNC();
+        const bool filled = pre_store();
+        if (p1) {
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                if ((kv[k] >> 15) == 0u)
+                    wk_put16(gout, C0 + 16ull * umin32((uint32_t)lane + 64u * k, nfull - 1u), w[k], stream);
+        }
+        if (p2) wk_put16(gout, C0 + 16ull * c1, m, stream);
+        if ((uint32_t)lane < ntr) gout[OS + qb] = tv;
+        if ((uint32_t)lane < o0) gout[OS + (uint32_t)lane] = lv;
+        return filled;
+    }
     if (!DROPS || nfull) {  // (wave-uniform)
         uint32_t kv[NK], w[NK][4];
 #pragma unroll
@@ -1871,6 +1929,8 @@ __device__ __forceinline__ void wk_store_mtu(const uint8_t *S, uint32_t ib, uint
     }
     // the leading bytes: the first kept record's (op 0; MTU: record 0, rel 0)
     if ((uint32_t)lane < o0) gout[OS + (uint32_t)lane] = S[ib + (DROPS ? T[0] & 0xffffu : 0u) + (uint32_t)lane];
+    (void)pre_store;
+    return false;
 }
 
 // big-endian / nanosecond input: a record header in host order and microseconds
@@ -2305,8 +2365,9 @@ __global__ void __launch_bounds__(WKB, WIN              ? (WkCfg<F>::reads ? TE_
                 const uint32_t cut = tile.span_len - out_len;
                 if (lane == 0 && (long long)cut != k1 - k0) atomicOr(a.grow_bad, 1u);  // (a stale prediction)
                 c_cut += cut;
-                wk_store_mtu<WK_KL + 1, FUZZ, MTU_NE>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0), out_len,
-                                              npkt, my_rel, incl - osz, osz != 0u, lane, stream && WK_MTU_STREAM);
+                filled = wk_store_mtu<WK_KL + 1, FUZZ, MTU_NE>(S, LDS_FRONT + g0, P, gout, (uint64_t)((long long)G0 - k0),
+                                                           out_len, npkt, my_rel, incl - osz, osz != 0u, lane,
+                                                           stream && WK_MTU_STREAM, pre_store);
                 if constexpr (FUZZ) {
                     c_drop += (unsigned long long)__popcll(__ballot(on && fz_cut && fz_nl == 0u));
                     c_soft += (unsigned long long)__popcll(__ballot(on && fz_cut));
