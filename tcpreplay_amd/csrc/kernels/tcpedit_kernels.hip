@@ -3145,6 +3145,16 @@ static uint32_t fast_feat(const te_dev_cfg_t *c) {
            (c->fixcsum ? 0u : TE_FF_INCR);
 }
 
+// the wave lane's grid cut to the waves that give every wave the same number of tiles
+// (ceil(tiles / resident waves) rounds), instead of all resident waves with a last round
+// only some of them take: the same rounds, no lone tail (A/B: C5 0.631 -> 0.646, C2, C3,
+// seed within 0.3 %; TCPEDIT_HIP_WAVE_BALANCE=0 launches every resident wave)
+static bool wave_balance() {
+    static int v = -1;
+    if (v < 0) v = getenv("TCPEDIT_HIP_WAVE_BALANCE") ? atoi(getenv("TCPEDIT_HIP_WAVE_BALANCE")) != 0 : 1;
+    return v != 0;
+}
+
 static int wave_inst_grid(int k) {
     if (wave_inst[k].grid) return wave_inst[k].grid;
     int cus = cu_count(), per_cu = 0;
@@ -3987,6 +3997,11 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         if (fgrid < 1) return -1;
         const uint32_t need = wave ? (L->n_tiles + WK_NW - 1) / WK_NW : L->n_tiles;
         if ((uint32_t)fgrid > need) fgrid = (int)need;
+        if (wave && wave_balance()) {
+            const uint32_t wv = (uint32_t)fgrid * WK_NW, rounds = (L->n_tiles + wv - 1) / wv;
+            const uint32_t bal = ((L->n_tiles + rounds - 1) / rounds + WK_NW - 1) / WK_NW;
+            if (bal >= 1 && bal < (uint32_t)fgrid) fgrid = (int)bal;
+        }
         if (wave && (!L->slots || ((L->out_base - L->rec0) & 15)))
             return -1;  // the wave lane stores whole 16-byte chunks at input offsets + a multiple of 16
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
