@@ -1367,9 +1367,10 @@ __global__ void __launch_bounds__(FKB, TE_FK_MIN_BLOCKS) te_fast_tiles(FastArgs 
 // the per-record cut instances (--mtu-trunc, --fuzz-seed: wk_store_mtu): their tile budget
 // for the lean and the cfg-reading instances
 // (8 KiB at 3 blocks/CU, a map of 16 entries a lane: mtu 0.547 -> 0.587, fz 0.365 -> 0.412 of
-//  peak, A/B on one box, round 6; the lean 5 KiB / cfg 6 KiB budgets before -- 0 restores them)
+//  peak, A/B on one box, round 6; the lean 5 KiB / cfg 6 KiB budgets before -- 0 restores them;
+//  9 KiB, still 3 blocks in 160 KiB: mtu 0.585 -> 0.604, fz 0.431 -> 0.460)
 #ifndef TE_WK_CUT_TILE_BYTES
-#define TE_WK_CUT_TILE_BYTES 8192
+#define TE_WK_CUT_TILE_BYTES 9216
 #endif
 #ifndef TE_WK_CUT_BLOCKS
 #define TE_WK_CUT_BLOCKS 3  // (0: as the other lean / cfg instances; --fuzz-seed: TE_WK_FUZZ_BLOCKS)

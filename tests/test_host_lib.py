@@ -202,8 +202,8 @@ def test_wave_tile_budgets_per_config_and_batch(built):
         (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 0, 9216),
         (["--enet-vlan=add", "--enet-vlan-tag=5", "--fixcsum"], GROW, 1, 9216),
         (["--enet-vlan=del", "--fixcsum"], VDEL, 1, 9216), (["--efcs", "--fixcsum"], EFCS, 0, 9216),
-        (["--mtu=1000", "--mtu-trunc", "--fixcsum"], MTU, 1, 8192),
-        (["--fuzz-seed=42", "--fuzz-factor=2"], FUZZ, 0, 8192),
+        (["--mtu=1000", "--mtu-trunc", "--fixcsum"], MTU, 1, 9216),
+        (["--fuzz-seed=42", "--fuzz-factor=2"], FUZZ, 0, 9216),
     ]
     for args, sz, small, want in cases:
         te, cfg, _ = derive(args)
