@@ -4003,6 +4003,13 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             const uint32_t bal = ((L->n_tiles + rounds - 1) / rounds + WK_NW - 1) / WK_NW;
             if (bal >= 1 && bal < (uint32_t)fgrid) fgrid = (int)bal;
         }
+        if (wave) {  // (diagnostics: TCPEDIT_HIP_WAVE_GRID_SUB=k launches k blocks fewer)
+            static int sub = -1, rot = -1;
+            if (sub < 0) sub = getenv("TCPEDIT_HIP_WAVE_GRID_SUB") ? atoi(getenv("TCPEDIT_HIP_WAVE_GRID_SUB")) : 0;
+            if (sub > 0 && sub < fgrid) fgrid -= sub;
+            if (rot < 0) rot = getenv("TCPEDIT_HIP_WAVE_ROTATE") ? atoi(getenv("TCPEDIT_HIP_WAVE_ROTATE")) != 0 : 0;
+            if (rot && fgrid > 8 && fgrid % 8 == 0 && (uint32_t)fgrid * WK_NW < L->n_tiles) fgrid -= 1;
+        }
         if (wave && (!L->slots || ((L->out_base - L->rec0) & 15)))
             return -1;  // the wave lane stores whole 16-byte chunks at input offsets + a multiple of 16
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
