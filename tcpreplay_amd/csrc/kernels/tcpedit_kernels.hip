@@ -3914,6 +3914,15 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
         int grid = win_inst[wk].grid;
         const uint32_t need = (L->nwin + WK_NW - 1) / WK_NW;
         if ((uint32_t)grid > need) grid = (int)need;
+        {  // TCPEDIT_HIP_WIN_BALANCE=1: equal rounds of windows, as the wave lane's tiles
+            static int wb = -1;
+            if (wb < 0) wb = getenv("TCPEDIT_HIP_WIN_BALANCE") ? atoi(getenv("TCPEDIT_HIP_WIN_BALANCE")) != 0 : 0;
+            if (wb && grid > 0) {
+                const uint32_t wv = (uint32_t)grid * WK_NW, rounds = (L->nwin + wv - 1) / wv;
+                const uint32_t bal = ((L->nwin + rounds - 1) / rounds + WK_NW - 1) / WK_NW;
+                if (bal >= 1 && bal < (uint32_t)grid) grid = (int)bal;
+            }
+        }
         if (grid < 1 || ((L->out_base - L->rec0) & 15)) return -1;
         // (the verdict words: zeroed by the window kernel itself, which never writes them)
         if (L->ev_k0 && hipEventRecord((hipEvent_t)L->ev_k0, stream) != hipSuccess) return -1;
