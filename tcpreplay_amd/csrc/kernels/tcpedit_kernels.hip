@@ -4016,8 +4016,14 @@ extern "C" int te_launch_edit(te_launch_t *L, hipStream_t stream) {
             static int sub = -1, rot = -1;
             if (sub < 0) sub = getenv("TCPEDIT_HIP_WAVE_GRID_SUB") ? atoi(getenv("TCPEDIT_HIP_WAVE_GRID_SUB")) : 0;
             if (sub > 0 && sub < fgrid) fgrid -= sub;
-            if (rot < 0) rot = getenv("TCPEDIT_HIP_WAVE_ROTATE") ? atoi(getenv("TCPEDIT_HIP_WAVE_ROTATE")) != 0 : 0;
-            if (rot && fgrid > 8 && fgrid % 8 == 0 && (uint32_t)fgrid * WK_NW < L->n_tiles) fgrid -= 1;
+            // a grid that is a multiple of the 8 XCDs deals each XCD the same tile stripes every
+            // round: C5 at 1,024 blocks 0.630, at 1,023 0.645-0.667 (A/B); one block fewer there
+            // (C3, C4, hdr, vdel: no change either way; TCPEDIT_HIP_WAVE_ROTATE=0 keeps it)
+            if (rot < 0) rot = getenv("TCPEDIT_HIP_WAVE_ROTATE") ? atoi(getenv("TCPEDIT_HIP_WAVE_ROTATE")) != 0 : 1;
+            if (rot && fgrid > 8 && fgrid % 8 == 0) {  // (only where the rounds stay as many)
+                const uint32_t w1 = (uint32_t)fgrid * WK_NW, w2 = w1 - WK_NW;
+                if ((L->n_tiles + w1 - 1) / w1 == (L->n_tiles + w2 - 1) / w2) fgrid -= 1;
+            }
         }
         if (wave && (!L->slots || ((L->out_base - L->rec0) & 15)))
             return -1;  // the wave lane stores whole 16-byte chunks at input offsets + a multiple of 16
